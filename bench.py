@@ -1,0 +1,149 @@
+#!/usr/bin/env python3
+"""Headline benchmark: GCUPS of the NW-affine hot path on MI355X.
+
+Workload (BASELINE.json configs[1]): 100,000 independent 150 x 150 G-iid DNA
+pairs per GPU (seed 0x5EED0002 + rank), sequences resident in HBM.  One step
+= one pass of the hot path over the batch: NW-affine matrix fill with the
+1 B/cell parent mask (nw_fill) + the reference's first-printed traceback per
+pair -> score, panic status, CIGAR (nw_traceback); with N > 1 ranks also the
+RCCL gather of the 16-byte per-pair result records to rank 0 (db sharded,
+SURVEY.md §8(e)).  value = all ranks' cells / max-over-ranks wall time.
+
+    python bench.py --gpus N --steps K --warmup W
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "GCUPS (affine-gap NW) at 1/2/4/8 MI355X; % of HBM roofline"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+N_PAIRS, LQ, LD = 100_000, 150, 150
+SEED = 0x5EED0002
+
+
+def cpu_baseline(budget_s: float = 12.0) -> dict:
+    """Oracle (C port of the reference CPU path: full 3-matrix fill with
+    parent sets + the reference's exhaustive DFS traceback), single core, on
+    a bounded sample of the same workload."""
+    from oracle import refcpu  # cpu_baseline leg only
+    from sequencealigning_amd import synth
+    refcpu.build()
+    n = 20000
+    qs, qo, ds, do = synth.iid_pairs(n, LQ, LD, seed=SEED)
+    qb, db = qs.tobytes(), ds.tobytes()
+    done = cells = 0
+    t0 = time.perf_counter()
+    while done < n and time.perf_counter() - t0 < budget_s:
+        k = min(64, n - done)
+        cells += refcpu.run_pairs(qb[done * LQ:(done + k) * LQ], qo[:k + 1],
+                                  db[done * LD:(done + k) * LD], do[:k + 1], k, max_pops=100_000)
+        done += k
+    dt = time.perf_counter() - t0
+    return {"value": round(cells / dt / 1e9, 6), "unit": "GCUPS", "cores": 1, "kind": "port",
+            "sample": f"{done} of the 150x150 G-iid pairs (seed {SEED:#x}), oracle/refcpu.c "
+                      f"fill + literal DFS (<=1e5 pops/pair), 1 thread, {dt:.1f} s"}
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--pairs", type=int, default=N_PAIRS)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    import sequencealigning_amd as saln
+    from sequencealigning_amd import synth
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    n = args.pairs
+    qs, qo, ds, do = synth.iid_pairs(n, LQ, LD, seed=SEED + rank)
+    plan = saln.NwPlan(qo, do, pairs=np.stack([np.arange(n), np.arange(n)], 1), device=local)
+    dq = torch.from_numpy(qs).to(f"cuda:{local}")
+    dd = torch.from_numpy(ds).to(f"cuda:{local}")
+    res = torch.zeros(n * 4, dtype=torch.int32, device=f"cuda:{local}")
+    cig = torch.zeros(max(1, plan.cigar_words), dtype=torch.int32, device=f"cuda:{local}")
+    gathered = ([torch.empty_like(res) for _ in range(world)] if (world > 1 and rank == 0)
+                else None)
+
+    def step():
+        plan.execute(dq, dd, res, cig)
+        if world > 1:
+            dist.gather(res, gathered, dst=0)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    plan.set_timing(True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    fill_ms, fill_n = plan.kernel_time("nw_fill")
+    tb_ms, tb_n = plan.kernel_time("nw_traceback")
+    t = torch.tensor([dt], dtype=torch.float64, device=f"cuda:{local}")
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dt = float(t.item())
+    cells_rank = plan.cells
+    total_cells = cells_rank * world * args.steps
+    gcups = total_cells / dt / 1e9
+    fill_avg_s = fill_ms / max(1, fill_n) / 1e3
+    achieved = cells_rank * 1.0 / fill_avg_s / 1e9  # 1 B/cell parent mask, GB/s
+    if rank == 0:
+        hr = res.cpu().numpy()
+        statuses = np.bincount(hr[1::4] & 0xFF, minlength=3)
+        out = {
+            "metric": METRIC, "value": round(gcups, 3), "unit": "GCUPS", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(dt / args.steps * 1e3, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "int32",
+            "data": "synthetic (splitmix64 G-iid ACGT)",
+            "config": {"workload": "configs[1]: independent 150x150 NW-affine pairs per GPU "
+                                   "(fill + 1 B/cell parent mask + first-printed traceback/CIGAR)",
+                       "pairs_per_gpu": n, "len_q": LQ, "len_db": LD, "seed": hex(SEED),
+                       "parallelism": f"db-sharded x{world}" + (" + RCCL gather" if world > 1
+                                                               else "")},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "traffic": None, "kernel": "nw_fill",
+                         "kernel_avg_ms": round(fill_avg_s * 1e3, 4),
+                         "traceback_avg_ms": round(tb_ms / max(1, tb_n), 4)},
+            "status_counts": {"ok": int(statuses[0]), "ref_panic_boundary": int(statuses[2])},
+        }
+        if not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline()
+        print(json.dumps(out), flush=True)
+    plan.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,185 @@
+/*
+ * saln — MI355X-native drop-in engine for the NW-affine (and WFA) hot path of
+ * Qw11111111111/SequenceAligning.
+ *
+ * C ABI only: plain pointers, sizes and POD structs; no C++ or torch types.
+ * Every entry point names the reference interface it replaces.  The
+ * reference is Rust (src/main.rs dispatches to free functions), so the
+ * binding a maintainer adds is an `extern "C"` block in Rust — see
+ * INTEGRATION.md.
+ *
+ * Orientation (reference convention, needleman_wunsch_affine.rs:424-430):
+ *   seq1 = query  -> y, columns, inner loop
+ *   seq2 = db     -> x, rows,    outer loop
+ */
+#ifndef SALN_H
+#define SALN_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SALN_ABI_VERSION 1
+
+/* Mode — src/parse.rs:44-50 (declaration order Global, Local, SemiGlobal). */
+typedef enum {
+    SALN_MODE_GLOBAL = 0,
+    SALN_MODE_LOCAL = 1,
+    SALN_MODE_SEMI_GLOBAL = 2
+} saln_mode;
+
+/* Per-pair status and API return codes.  The reference returns
+ * AlignerError values (src/errors.rs:7-15) or panics (aborting the whole
+ * process, exit 101); this library never aborts and reports a status instead. */
+typedef enum {
+    SALN_OK = 0,
+    SALN_NOT_IMPLEMENTED = 1,    /* AlignmentError("not implemented"): NW :433-434, WFA :26 */
+    SALN_REF_PANIC_BOUNDARY = 2, /* NW traceback index panic, needleman_wunsch_affine.rs:299/:303 */
+    SALN_REF_PANIC_TRIM = 3,     /* WFA Ocean::trim rotate_left panic, wfa.rs:577/:603 */
+    SALN_REF_PANIC_SLICE = 4,    /* WFA rec_tr slice panic, wfa.rs:695-744 */
+    SALN_NONCONVERGED = 5,       /* WFA score loop hit the caller's step cap (wfa.rs:28) */
+    SALN_ENUM_CAP = 6,           /* NW co-optimal enumeration hit the caller's cap */
+
+    SALN_E_INVALID = -1,   /* bad argument */
+    SALN_E_HIP = -2,       /* HIP runtime error (message: saln_last_error) */
+    SALN_E_NO_DEVICE = -3, /* no gfx950 device / extension not usable */
+    SALN_E_CAPACITY = -4,  /* caller buffer too small */
+    SALN_E_IO = -5,        /* file could not be read */
+    SALN_E_FASTA = -6,     /* AlignerError::FastaError (bad extension), parse.rs:55-60 */
+    SALN_E_FASTA_CHARS = -7 /* AlignerError::CharError; records are still returned, parse.rs:92-97 */
+} saln_status;
+
+/* ScoringScheme, needleman_wunsch_affine.rs:15-20 / :382-388.
+ * NULL everywhere means the reference SCHEME {5, -4, -8, -6}. */
+typedef struct {
+    int32_t match;      /* +5 */
+    int32_t mismatch;   /* -4 */
+    int32_t gap_open;   /* -8 (added once when a gap opens from M) */
+    int32_t gap_extend; /* -6 (added for every gap column) */
+} saln_nw_scoring;
+
+/* Result of one NW pair (16 bytes). */
+typedef struct {
+    int32_t score;      /* max(M,I,D)[len_db][len_q], :247-250 (never printed by the reference) */
+    int32_t status;     /* SALN_OK | SALN_REF_PANIC_BOUNDARY | SALN_NOT_IMPLEMENTED */
+    uint32_t cigar_len; /* RLE ops written for the first printed alignment (0 if none) */
+    uint8_t end_states; /* bit0 M, bit1 I, bit2 D: end states equal to score (:251-280) */
+    uint8_t printed;    /* 1 if the reference prints at least one alignment block */
+    uint8_t flags;      /* internal diagnostics (0) */
+    uint8_t reserved;
+} saln_nw_result;
+
+/* CIGAR words: (run_length << 4) | op, BAM op codes, forward order, db as
+ * the reference sequence:  '=' 7 (M column, bases equal), 'X' 8 (M column,
+ * bases differ), 'I' 1 (query base vs '-', I state), 'D' 2 ('-' vs db base,
+ * D state).  A run never exceeds 2^28-1. */
+#define SALN_CIGAR_EQ 7u
+#define SALN_CIGAR_X 8u
+#define SALN_CIGAR_I 1u
+#define SALN_CIGAR_D 2u
+
+/* ---------------------------------------------------------------- context */
+typedef struct saln_context saln_context;
+
+/* Creates a context bound to HIP device `device` (one stream per context;
+ * reentrant per context, not shared across threads).  Fails with
+ * SALN_E_NO_DEVICE if no gfx950 device is present: there is no CPU path. */
+int saln_context_create(int device, saln_context **out);
+int saln_context_destroy(saln_context *ctx);
+const char *saln_last_error(void);     /* thread-local message for the last error */
+int saln_abi_version(void);
+
+/* ------------------------------------------------------- NW: per pair (drop-in)
+ * Replaces `pub fn n_w_align(seq1: &Record, seq2: &Record, _verbose: bool,
+ * mode: Mode) -> Result<()>` (needleman_wunsch_affine.rs:424-437).
+ * q = seq1.seq (query), d = seq2.seq (db).  `verbose` is ignored, as in the
+ * reference.  cigar (capacity cigar_cap words) may be NULL.
+ * Returns SALN_OK or SALN_NOT_IMPLEMENTED (mode != GLOBAL, like :433-434) or
+ * an SALN_E_* error; the per-pair outcome (incl. reference panics) is in
+ * out->status. */
+int saln_nw_align(saln_context *ctx, const uint8_t *q, uint64_t len_q, const uint8_t *d,
+                  uint64_t len_db, int verbose, int32_t mode, const saln_nw_scoring *scoring,
+                  saln_nw_result *out, uint32_t *cigar, uint64_t cigar_cap);
+
+/* Text the reference prints for this pair (needleman_wunsch_affine.rs:281-286
+ * with TraceBackInfo Display :390-411): every co-optimal alignment block in
+ * the reference's DFS order, up to the first panic.  The nondeterministic
+ * `{:#?}` timing line (:431) is not produced.  max_blocks = 0: unlimited.
+ * *status: SALN_OK, SALN_REF_PANIC_BOUNDARY (the reference would abort after
+ * the returned text) or SALN_ENUM_CAP.  out may be NULL to query *out_len. */
+int saln_nw_render(saln_context *ctx, const uint8_t *q, uint64_t len_q, const uint8_t *d,
+                   uint64_t len_db, int32_t mode, uint64_t max_blocks, char *out, uint64_t cap,
+                   uint64_t *out_len, uint64_t *n_blocks, int32_t *status);
+
+/* Dense parent mask for parity checks: (len_db+1) x (len_q+1) bytes,
+ * row-major over db.  Byte bits: 0-2 = {M,I,D} equal to max(M,I,D) at the
+ * cell (so the M parent set of (x,y) is the byte of (x-1,y-1)), 3-4 = I
+ * parents {extend I[x][y-1], open M[x][y-1]}, 5-6 = D parents {extend
+ * D[x-1][y], open M[x-1][y]} (needleman_wunsch_affine.rs:96-153, boundary
+ * parents :196,:208). */
+int saln_nw_dense_mask(saln_context *ctx, const uint8_t *q, uint64_t len_q, const uint8_t *d,
+                       uint64_t len_db, const saln_nw_scoring *scoring, uint8_t *out);
+
+/* --------------------------------------------------------- NW: batched (host)
+ * Replaces the pair loop `for d in db { for q in query { n_w_align(q, d) } }`
+ * (main.rs:61-67).  Sequences are CSR: q_seq bytes with q_off[n_q+1].  Pair p
+ * aligns query pair_q[p] against db pair_db[p]; if pair_q == pair_db == NULL,
+ * all-vs-all in the reference order (db outer, query inner:
+ * p = d * n_q + q).  cigar/cigar_off may be NULL; cigar_off[p] (words) must
+ * leave room for len_q + len_db words per pair (saln_nw_cigar_offsets). */
+int saln_nw_align_batch(saln_context *ctx, const uint8_t *q_seq, const uint64_t *q_off,
+                        uint64_t n_q, const uint8_t *db_seq, const uint64_t *db_off,
+                        uint64_t n_db, const uint32_t *pair_q, const uint32_t *pair_db,
+                        uint64_t n_pairs, int32_t mode, const saln_nw_scoring *scoring,
+                        saln_nw_result *results, uint32_t *cigar, const uint64_t *cigar_off);
+
+/* -------------------------------------------------- NW: batched (device, plan)
+ * For callers whose data is already resident in HBM (bench, multi-GPU
+ * driver).  The plan is built once from host-side lengths; execute then only
+ * launches kernels on `stream` (hipStream_t; NULL = the context's stream).
+ * Device buffers: q_seq/db_seq (same CSR byte layout as the host offsets
+ * given to the plan), results[n_pairs], cigar[plan cigar words] (may be
+ * NULL: traceback still runs, ops are not stored). */
+typedef struct saln_nw_plan saln_nw_plan;
+
+int saln_nw_plan_create(saln_context *ctx, const uint64_t *q_off, uint64_t n_q,
+                        const uint64_t *db_off, uint64_t n_db, const uint32_t *pair_q,
+                        const uint32_t *pair_db, uint64_t n_pairs, int32_t mode,
+                        const saln_nw_scoring *scoring, saln_nw_plan **out);
+/* mask_bytes: HBM parent-mask workspace (owned by the plan);
+ * cigar_words: required length of the device cigar buffer. */
+int saln_nw_plan_info(const saln_nw_plan *plan, uint64_t *mask_bytes, uint64_t *cigar_words,
+                      uint64_t *cells);
+int saln_nw_cigar_offsets(const saln_nw_plan *plan, uint64_t *cigar_off /* n_pairs+1 */);
+int saln_nw_execute(saln_nw_plan *plan, const uint8_t *d_q_seq, const uint8_t *d_db_seq,
+                    saln_nw_result *d_results, uint32_t *d_cigar, void *stream);
+/* Optional per-kernel timing (hipEvents recorded on the launch stream around
+ * each kernel of every execute while enabled).  Names: "nw_fill", "nw_traceback". */
+int saln_nw_plan_set_timing(saln_nw_plan *plan, int enable);
+int saln_nw_plan_kernel_time(const saln_nw_plan *plan, const char *kernel, double *total_ms,
+                             uint64_t *launches);
+int saln_nw_plan_destroy(saln_nw_plan *plan);
+
+/* --------------------------------------------------------------------- FASTA
+ * Replaces `pub fn parse_fasta(path: PathBuf) -> Result<Records>`
+ * (parse.rs:54-99): extension must be exactly fa|fasta|fna; '>' opens a record
+ * whose name includes the '>'; bytes outside {A,G,C,T,N} in sequence lines are
+ * dropped and reported (returns SALN_E_FASTA_CHARS with the records still
+ * valid, like CharError{res,chars}). */
+typedef struct saln_records saln_records;
+int saln_parse_fasta(const char *path, saln_records **out, uint8_t *bad_chars, uint64_t bad_cap,
+                     uint64_t *n_bad);
+int saln_parse_fasta_buffer(const uint8_t *buf, uint64_t len, saln_records **out,
+                            uint8_t *bad_chars, uint64_t bad_cap, uint64_t *n_bad);
+uint64_t saln_records_count(const saln_records *r);
+int saln_records_get(const saln_records *r, uint64_t i, const uint8_t **name, uint64_t *name_len,
+                     const uint8_t **seq, uint64_t *seq_len);
+void saln_records_free(saln_records *r);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SALN_H */

@@ -1,0 +1,154 @@
+"""ORACLE — test infrastructure only.
+
+ctypes front-end for the C restatement in ``oracle/refcpu.c`` (reference:
+``src/needleman_wunsch_affine.rs``, ``src/parse.rs``).  Only ``tests/``,
+``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline`` leg import
+this module, and only as the checker.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+from dataclasses import dataclass
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "_build", "librefcpu.so")
+_lib = None
+
+
+def build() -> str:
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+    return _LIB_PATH
+
+
+class _Mats(C.Structure):
+    _fields_ = [("lq", C.c_size_t), ("ld", C.c_size_t),
+                ("M", C.POINTER(C.c_int32)), ("I", C.POINTER(C.c_int32)),
+                ("D", C.POINTER(C.c_int32)),
+                ("pM", C.POINTER(C.c_uint8)), ("pI", C.POINTER(C.c_uint8)),
+                ("pD", C.POINTER(C.c_uint8))]
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            build()
+        L = C.CDLL(_LIB_PATH)
+        u8p = C.POINTER(C.c_uint8)
+        L.ref_nw_fill.argtypes = [u8p, C.c_size_t, u8p, C.c_size_t, C.POINTER(_Mats)]
+        L.ref_nw_free.argtypes = [C.POINTER(_Mats)]
+        L.ref_nw_dense_mask.argtypes = [C.POINTER(_Mats), u8p]
+        L.ref_nw_score.argtypes = [C.POINTER(_Mats), u8p]
+        L.ref_nw_score.restype = C.c_int32
+        L.ref_nw_traceback_dfs.argtypes = [u8p, u8p, C.POINTER(_Mats), C.c_char_p, C.c_size_t,
+                                           C.POINTER(C.c_size_t), C.c_uint64,
+                                           C.POINTER(C.c_uint64)]
+        L.ref_nw_dag_summary.argtypes = [u8p, u8p, C.POINTER(_Mats), C.POINTER(C.c_uint64),
+                                         C.POINTER(C.c_int), C.c_char_p, C.c_size_t,
+                                         C.POINTER(C.c_int64)]
+        L.ref_nw_run_pairs.argtypes = [u8p, C.POINTER(C.c_uint64), u8p, C.POINTER(C.c_uint64),
+                                       C.c_uint64, C.c_uint64]
+        L.ref_nw_run_pairs.restype = C.c_uint64
+        L.ref_parse_fasta.argtypes = [u8p, C.c_size_t, C.c_int, u8p, C.c_size_t,
+                                      C.POINTER(C.c_size_t), u8p, C.c_size_t,
+                                      C.POINTER(C.c_size_t)]
+        L.ref_parse_fasta.restype = C.c_int64
+        _lib = L
+    return _lib
+
+
+def _u8(b: bytes):
+    buf = (C.c_uint8 * max(1, len(b))).from_buffer_copy(b if b else b"\0")
+    return buf
+
+
+@dataclass
+class NwOracle:
+    score: int
+    end_states: int          # bit0 M, bit1 I, bit2 D
+    dense_mask: np.ndarray   # (ld+1, lq+1) uint8, same bit meaning as the product export
+    M: np.ndarray
+    I: np.ndarray
+    D: np.ndarray
+    stdout: str | None       # literal DFS output (None when not requested)
+    dfs_rc: int | None       # 0 finished, 1 panic, 2 pop cap
+    dfs_blocks: int | None
+    n_blocks: int            # memoised DFS: blocks printed before the first panic
+    panics: bool
+    first_ops: str | None    # first printed alignment ('=','X','I','D'), None if none printed
+
+
+def nw(query: bytes, db: bytes, *, literal_dfs: bool = True, max_pops: int = 2_000_000,
+       out_cap: int = 1 << 22) -> NwOracle:
+    L = lib()
+    q, d = _u8(query), _u8(db)
+    m = _Mats()
+    if L.ref_nw_fill(q, len(query), d, len(db), C.byref(m)) != 0:
+        raise MemoryError("oracle fill")
+    try:
+        H, W = len(db) + 1, len(query) + 1
+        dense = np.zeros((H, W), np.uint8)
+        L.ref_nw_dense_mask(C.byref(m), dense.ctypes.data_as(C.POINTER(C.c_uint8)))
+        es = C.c_uint8(0)
+        score = L.ref_nw_score(C.byref(m), C.byref(es))
+        Mv = np.ctypeslib.as_array(m.M, shape=(H * W,)).reshape(H, W).copy()
+        Iv = np.ctypeslib.as_array(m.I, shape=(H * W,)).reshape(H, W).copy()
+        Dv = np.ctypeslib.as_array(m.D, shape=(H * W,)).reshape(H, W).copy()
+        text = rc = blocks = None
+        if literal_dfs:
+            out = C.create_string_buffer(out_cap)
+            olen = C.c_size_t(0)
+            nb = C.c_uint64(0)
+            rc = L.ref_nw_traceback_dfs(q, d, C.byref(m), out, out_cap, C.byref(olen), max_pops,
+                                        C.byref(nb))
+            text = out.raw[:min(olen.value, out_cap)].decode("latin-1")
+            blocks = nb.value
+        nbk = C.c_uint64(0)
+        pan = C.c_int(0)
+        cap = len(query) + len(db) + 1
+        ops = C.create_string_buffer(cap)
+        olen2 = C.c_int64(0)
+        L.ref_nw_dag_summary(q, d, C.byref(m), C.byref(nbk), C.byref(pan), ops, cap,
+                             C.byref(olen2))
+        first = ops.raw[:olen2.value].decode() if olen2.value >= 0 else None
+        return NwOracle(score, es.value, dense, Mv, Iv, Dv, text, rc, blocks, nbk.value,
+                        bool(pan.value), first)
+    finally:
+        L.ref_nw_free(C.byref(m))
+
+
+def run_pairs(qs: bytes, q_off: np.ndarray, ds: bytes, d_off: np.ndarray, n_pairs: int,
+              max_pops: int = 100_000) -> int:
+    """Timed CPU baseline body: literal fill + DFS over n_pairs (CSR inputs)."""
+    L = lib()
+    qo = np.ascontiguousarray(q_off, np.uint64)
+    do = np.ascontiguousarray(d_off, np.uint64)
+    return L.ref_nw_run_pairs(_u8(qs), qo.ctypes.data_as(C.POINTER(C.c_uint64)), _u8(ds),
+                              do.ctypes.data_as(C.POINTER(C.c_uint64)), n_pairs, max_pops)
+
+
+def parse_fasta_bytes(data: bytes, valid_ext: bool = True):
+    """Returns (records [(name, seq)], bad_chars bytes) or None for FastaError."""
+    L = lib()
+    cap = len(data) * 2 + 64
+    out = (C.c_uint8 * cap)()
+    rl = C.c_size_t(0)
+    bad = (C.c_uint8 * (len(data) + 1))()
+    nb = C.c_size_t(0)
+    n = L.ref_parse_fasta(_u8(data), len(data), int(valid_ext), out, cap, C.byref(rl), bad,
+                          len(data) + 1, C.byref(nb))
+    if n < 0:
+        return None
+    raw = bytes(out)[:rl.value]
+    recs, o = [], 0
+    for _ in range(n):
+        nl = int.from_bytes(raw[o:o + 4], "little"); o += 4
+        name = raw[o:o + nl]; o += nl
+        sl = int.from_bytes(raw[o:o + 4], "little"); o += 4
+        seq = raw[o:o + sl]; o += sl
+        recs.append((name, seq))
+    return recs, bytes(bad)[:nb.value]

@@ -1,0 +1,168 @@
+"""ctypes binding of ``libsaln.so`` (the C ABI declared in ``include/saln.h``).
+
+The library is built in-tree by ``__graft_entry__.build()``.  There is no
+CPU fallback: if the shared object is missing, importing the compute entry
+points raises, and creating a context without a gfx950 device fails with
+``SALN_E_NO_DEVICE``.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libsaln.so")
+
+# saln_status (include/saln.h)
+OK = 0
+NOT_IMPLEMENTED = 1
+REF_PANIC_BOUNDARY = 2
+REF_PANIC_TRIM = 3
+REF_PANIC_SLICE = 4
+NONCONVERGED = 5
+ENUM_CAP = 6
+E_INVALID = -1
+E_HIP = -2
+E_NO_DEVICE = -3
+E_CAPACITY = -4
+E_IO = -5
+E_FASTA = -6
+E_FASTA_CHARS = -7
+
+STATUS_NAMES = {
+    OK: "OK", NOT_IMPLEMENTED: "NOT_IMPLEMENTED", REF_PANIC_BOUNDARY: "REF_PANIC_BOUNDARY",
+    REF_PANIC_TRIM: "REF_PANIC_TRIM", REF_PANIC_SLICE: "REF_PANIC_SLICE",
+    NONCONVERGED: "NONCONVERGED", ENUM_CAP: "ENUM_CAP", E_INVALID: "E_INVALID", E_HIP: "E_HIP",
+    E_NO_DEVICE: "E_NO_DEVICE", E_CAPACITY: "E_CAPACITY", E_IO: "E_IO", E_FASTA: "E_FASTA",
+    E_FASTA_CHARS: "E_FASTA_CHARS",
+}
+
+CIGAR_OPS = {7: "=", 8: "X", 1: "I", 2: "D"}
+
+
+class NwScoring(C.Structure):
+    _fields_ = [("match", C.c_int32), ("mismatch", C.c_int32), ("gap_open", C.c_int32),
+                ("gap_extend", C.c_int32)]
+
+
+class NwResult(C.Structure):
+    _fields_ = [("score", C.c_int32), ("status", C.c_int32), ("cigar_len", C.c_uint32),
+                ("end_states", C.c_uint8), ("printed", C.c_uint8), ("flags", C.c_uint8),
+                ("reserved", C.c_uint8)]
+
+
+# numpy view of saln_nw_result
+RESULT_DTYPE = [("score", "<i4"), ("status", "<i4"), ("cigar_len", "<u4"), ("end_states", "u1"),
+                ("printed", "u1"), ("flags", "u1"), ("reserved", "u1")]
+
+# symbols every build must export (tests check this list against include/saln.h)
+EXPORTS = [
+    "saln_context_create", "saln_context_destroy", "saln_last_error", "saln_abi_version",
+    "saln_nw_align", "saln_nw_render", "saln_nw_dense_mask", "saln_nw_align_batch",
+    "saln_nw_plan_create", "saln_nw_plan_info", "saln_nw_cigar_offsets", "saln_nw_execute",
+    "saln_nw_plan_set_timing", "saln_nw_plan_kernel_time", "saln_nw_plan_destroy",
+    "saln_parse_fasta", "saln_parse_fasta_buffer", "saln_records_count", "saln_records_get",
+    "saln_records_free",
+]
+
+_lib = None
+_lock = threading.Lock()
+
+
+class SalnError(RuntimeError):
+    def __init__(self, code: int, what: str):
+        self.code = code
+        msg = last_error() if _lib is not None else ""
+        super().__init__(f"{what}: {STATUS_NAMES.get(code, code)} {msg}".strip())
+
+
+def lib() -> C.CDLL:
+    """Load libsaln.so (raises if the in-tree build is missing)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        # torch-ROCm ships its own libamdhip64 (soname libamdhip64.so.7).  If
+        # torch is importable, load it first so libsaln binds to that same
+        # HIP runtime by soname; loading /opt/rocm's copy first would leave
+        # two HIP runtimes in the process and torch would see no GPU.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(
+                f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; "
+                f"g.build()'` (there is no CPU fallback)")
+        L = C.CDLL(LIB_PATH)
+        u8p, u32p, u64p, i32p = (C.POINTER(C.c_uint8), C.POINTER(C.c_uint32),
+                                 C.POINTER(C.c_uint64), C.POINTER(C.c_int32))
+        vp = C.c_void_p
+        L.saln_last_error.restype = C.c_char_p
+        L.saln_context_create.argtypes = [C.c_int, C.POINTER(vp)]
+        L.saln_context_destroy.argtypes = [vp]
+        L.saln_nw_align.argtypes = [vp, vp, C.c_uint64, vp, C.c_uint64, C.c_int, C.c_int32,
+                                    C.POINTER(NwScoring), C.POINTER(NwResult), u32p, C.c_uint64]
+        L.saln_nw_render.argtypes = [vp, vp, C.c_uint64, vp, C.c_uint64, C.c_int32, C.c_uint64,
+                                     C.c_char_p, C.c_uint64, u64p, u64p, i32p]
+        L.saln_nw_dense_mask.argtypes = [vp, vp, C.c_uint64, vp, C.c_uint64,
+                                         C.POINTER(NwScoring), vp]
+        L.saln_nw_align_batch.argtypes = [vp, vp, vp, C.c_uint64, vp, vp, C.c_uint64, vp, vp,
+                                          C.c_uint64, C.c_int32, C.POINTER(NwScoring), vp, vp,
+                                          vp]
+        L.saln_nw_plan_create.argtypes = [vp, vp, C.c_uint64, vp, C.c_uint64, vp, vp,
+                                          C.c_uint64, C.c_int32, C.POINTER(NwScoring),
+                                          C.POINTER(vp)]
+        L.saln_nw_plan_info.argtypes = [vp, u64p, u64p, u64p]
+        L.saln_nw_cigar_offsets.argtypes = [vp, vp]
+        L.saln_nw_execute.argtypes = [vp, vp, vp, vp, vp, vp]
+        L.saln_nw_plan_set_timing.argtypes = [vp, C.c_int]
+        L.saln_nw_plan_kernel_time.argtypes = [vp, C.c_char_p, C.POINTER(C.c_double), u64p]
+        L.saln_nw_plan_destroy.argtypes = [vp]
+        L.saln_parse_fasta.argtypes = [C.c_char_p, C.POINTER(vp), u8p, C.c_uint64, u64p]
+        L.saln_parse_fasta_buffer.argtypes = [vp, C.c_uint64, C.POINTER(vp), u8p, C.c_uint64,
+                                              u64p]
+        L.saln_records_count.argtypes = [vp]
+        L.saln_records_count.restype = C.c_uint64
+        L.saln_records_get.argtypes = [vp, C.c_uint64, C.POINTER(vp), u64p, C.POINTER(vp), u64p]
+        L.saln_records_free.argtypes = [vp]
+        L.saln_records_free.restype = None
+        _lib = L
+        return L
+
+
+def last_error() -> str:
+    msg = lib().saln_last_error()
+    return msg.decode(errors="replace") if msg else ""
+
+
+def check(rc: int, what: str, ok=(OK,)) -> int:
+    if rc not in ok:
+        raise SalnError(rc, what)
+    return rc
+
+
+_contexts: dict[int, C.c_void_p] = {}
+
+
+def context(device: int = 0) -> C.c_void_p:
+    """Per-process context for `device` (created on first use)."""
+    with _lock:
+        ctx = _contexts.get(device)
+        if ctx is None:
+            ctx = C.c_void_p()
+            check(lib().saln_context_create(device, C.byref(ctx)), "saln_context_create")
+            _contexts[device] = ctx
+        return ctx
+
+
+def scoring_arg(scoring) -> C.POINTER(NwScoring) | None:
+    if scoring is None:
+        return None
+    if isinstance(scoring, NwScoring):
+        return C.pointer(scoring)
+    m, x, o, e = scoring
+    return C.pointer(NwScoring(m, x, o, e))

@@ -1,0 +1,202 @@
+// Host-buffer entry points of the C ABI: per-pair n_w_align replacement,
+// host batch, reference-text rendering and dense-mask export.  Each one is a
+// thin wrapper: upload -> plan -> saln_nw_execute (GPU) -> download.
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "nw_host.hpp"
+
+using namespace saln;
+
+namespace {
+
+struct DevBuf {
+    void *p = nullptr;
+    ~DevBuf() {
+        if (p) (void)hipFree(p);
+    }
+    hipError_t alloc(size_t n) { return hipMalloc(&p, n ? n : 1); }
+};
+
+#define TRY_HIP(expr)                                                                      \
+    do {                                                                                   \
+        hipError_t e_ = (expr);                                                            \
+        if (e_ != hipSuccess) {                                                            \
+            set_error(std::string(#expr) + ": " + hipGetErrorString(e_));                  \
+            return SALN_E_HIP;                                                             \
+        }                                                                                  \
+    } while (0)
+
+struct PlanGuard {
+    saln_nw_plan *p = nullptr;
+    ~PlanGuard() { saln_nw_plan_destroy(p); }
+};
+
+}  // namespace
+
+static int run_batch(saln_context *ctx, const uint8_t *q_seq, const uint64_t *q_off, uint64_t n_q,
+                     const uint8_t *db_seq, const uint64_t *db_off, uint64_t n_db,
+                     const uint32_t *pair_q, const uint32_t *pair_db, uint64_t n_pairs,
+                     int32_t mode, const saln_nw_scoring *scoring, saln_nw_result *results,
+                     uint32_t *cigar, const uint64_t *cigar_off,
+                     std::vector<std::vector<uint8_t>> *masks_out) {
+    PlanGuard g;
+    int rc = saln_nw_plan_create(ctx, q_off, n_q, db_off, n_db, pair_q, pair_db, n_pairs, mode,
+                                 scoring, &g.p);
+    if (rc == SALN_NOT_IMPLEMENTED) {
+        for (uint64_t k = 0; k < n_pairs; ++k) {
+            std::memset(&results[k], 0, sizeof(saln_nw_result));
+            results[k].status = SALN_NOT_IMPLEMENTED;
+        }
+        return rc;
+    }
+    if (rc != SALN_OK) return rc;
+    std::vector<uint64_t> coff(n_pairs + 1);
+    saln_nw_cigar_offsets(g.p, coff.data());
+    uint64_t cig_words = coff[n_pairs];
+    DevBuf dq, dd, dr, dc;
+    const uint64_t qbytes = q_off[n_q], dbytes = db_off[n_db];
+    TRY_HIP(dq.alloc(qbytes));
+    TRY_HIP(dd.alloc(dbytes));
+    TRY_HIP(dr.alloc(n_pairs * sizeof(saln_nw_result)));
+    TRY_HIP(dc.alloc(cig_words * 4));
+    if (qbytes) TRY_HIP(hipMemcpy(dq.p, q_seq, qbytes, hipMemcpyHostToDevice));
+    if (dbytes) TRY_HIP(hipMemcpy(dd.p, db_seq, dbytes, hipMemcpyHostToDevice));
+    rc = saln_nw_execute(g.p, (const uint8_t *)dq.p, (const uint8_t *)dd.p,
+                         (saln_nw_result *)dr.p, (uint32_t *)dc.p, nullptr);
+    if (rc != SALN_OK) return rc;
+    TRY_HIP(hipDeviceSynchronize());
+    TRY_HIP(hipMemcpy(results, dr.p, n_pairs * sizeof(saln_nw_result), hipMemcpyDeviceToHost));
+    std::vector<uint32_t> hc(cig_words);
+    if (cig_words) TRY_HIP(hipMemcpy(hc.data(), dc.p, cig_words * 4, hipMemcpyDeviceToHost));
+    // per-pair masks are needed for host fix-ups (sentinel dead ends) and
+    // for the callers that render reference text.
+    std::vector<char> need(n_pairs, 0);
+    bool any = masks_out != nullptr;
+    for (uint64_t k = 0; k < n_pairs; ++k)
+        if (results[k].flags & 1) need[k] = 1, any = true;
+    if (any) {
+        if (masks_out) masks_out->resize(n_pairs);
+        for (uint64_t k = 0; k < n_pairs; ++k) {
+            if (!need[k] && !masks_out) continue;
+            std::vector<uint8_t> m;
+            Geom geo{16, 10};
+            rc = plan_pair_mask(g.p, k, &m, &geo);
+            if (rc != SALN_OK) return rc;
+            if (need[k]) {
+                const uint64_t qi = pair_q ? pair_q[k] : k % n_q;
+                const uint64_t di = pair_db ? pair_db[k] : k / n_q;
+                HostMask hm;
+                hm.m = m.data();
+                hm.g = geo;
+                hm.lq = (uint32_t)(q_off[qi + 1] - q_off[qi]);
+                hm.ld = (uint32_t)(db_off[di + 1] - db_off[di]);
+                hm.sc = scoring_or_default(scoring);
+                std::vector<uint32_t> c;
+                const bool printed = first_alignment(hm, q_seq + q_off[qi], db_seq + db_off[di], &c);
+                results[k].printed = printed ? 1 : 0;
+                results[k].cigar_len = printed ? (uint32_t)c.size() : 0;
+                std::copy(c.begin(), c.end(), hc.begin() + (long)coff[k]);
+                results[k].flags &= (uint8_t)~1u;
+            }
+            if (masks_out) (*masks_out)[k] = std::move(m);
+        }
+    }
+    if (cigar) {
+        for (uint64_t k = 0; k < n_pairs; ++k) {
+            const uint64_t dst = cigar_off ? cigar_off[k] : coff[k];
+            std::memcpy(cigar + dst, hc.data() + coff[k], results[k].cigar_len * 4);
+        }
+    }
+    return SALN_OK;
+}
+
+extern "C" {
+
+int saln_nw_align_batch(saln_context *ctx, const uint8_t *q_seq, const uint64_t *q_off,
+                        uint64_t n_q, const uint8_t *db_seq, const uint64_t *db_off,
+                        uint64_t n_db, const uint32_t *pair_q, const uint32_t *pair_db,
+                        uint64_t n_pairs, int32_t mode, const saln_nw_scoring *scoring,
+                        saln_nw_result *results, uint32_t *cigar, const uint64_t *cigar_off) {
+    if (!ctx || !q_off || !db_off || !results) return SALN_E_INVALID;
+    return run_batch(ctx, q_seq, q_off, n_q, db_seq, db_off, n_db, pair_q, pair_db, n_pairs, mode,
+                     scoring, results, cigar, cigar_off, nullptr);
+}
+
+int saln_nw_align(saln_context *ctx, const uint8_t *q, uint64_t len_q, const uint8_t *d,
+                  uint64_t len_db, int verbose, int32_t mode, const saln_nw_scoring *scoring,
+                  saln_nw_result *out, uint32_t *cigar, uint64_t cigar_cap) {
+    (void)verbose;  // `_verbose` is unused by the reference (:424)
+    if (!ctx || !out || (len_q && !q) || (len_db && !d)) return SALN_E_INVALID;
+    const uint64_t qo[2] = {0, len_q}, dof[2] = {0, len_db};
+    const uint32_t z = 0;
+    std::vector<uint32_t> c(len_q + len_db + 1);
+    const uint64_t co[1] = {0};
+    int rc = run_batch(ctx, q, qo, 1, d, dof, 1, &z, &z, 1, mode, scoring, out, c.data(), co,
+                       nullptr);
+    if (rc != SALN_OK) return rc;
+    if (cigar) {
+        if (out->cigar_len > cigar_cap) return SALN_E_CAPACITY;
+        std::memcpy(cigar, c.data(), out->cigar_len * 4);
+    }
+    return SALN_OK;
+}
+
+int saln_nw_render(saln_context *ctx, const uint8_t *q, uint64_t len_q, const uint8_t *d,
+                   uint64_t len_db, int32_t mode, uint64_t max_blocks, char *out, uint64_t cap,
+                   uint64_t *out_len, uint64_t *n_blocks, int32_t *status) {
+    if (!ctx || (len_q && !q) || (len_db && !d)) return SALN_E_INVALID;
+    const uint64_t qo[2] = {0, len_q}, dof[2] = {0, len_db};
+    const uint32_t z = 0;
+    saln_nw_result r;
+    std::vector<std::vector<uint8_t>> masks;
+    int rc = run_batch(ctx, q, qo, 1, d, dof, 1, &z, &z, 1, mode, nullptr, &r, nullptr, nullptr,
+                       &masks);
+    if (rc == SALN_NOT_IMPLEMENTED) {
+        if (status) *status = SALN_NOT_IMPLEMENTED;
+        if (out_len) *out_len = 0;
+        if (n_blocks) *n_blocks = 0;
+        return rc;
+    }
+    if (rc != SALN_OK) return rc;
+    HostMask hm;
+    hm.m = masks[0].data();
+    hm.g = variant_geom(choose_variant((uint32_t)len_q));
+    hm.lq = (uint32_t)len_q;
+    hm.ld = (uint32_t)len_db;
+    std::string text;
+    const DfsOutcome o = render_blocks(hm, q, d, max_blocks, &text);
+    if (out_len) *out_len = text.size();
+    if (n_blocks) *n_blocks = o.blocks;
+    if (status) *status = o.status;
+    if (out) {
+        std::memcpy(out, text.data(), text.size() < cap ? text.size() : cap);
+        if (text.size() > cap) return SALN_E_CAPACITY;
+    }
+    return SALN_OK;
+}
+
+int saln_nw_dense_mask(saln_context *ctx, const uint8_t *q, uint64_t len_q, const uint8_t *d,
+                       uint64_t len_db, const saln_nw_scoring *scoring, uint8_t *out) {
+    if (!ctx || !out || (len_q && !q) || (len_db && !d)) return SALN_E_INVALID;
+    const uint64_t qo[2] = {0, len_q}, dof[2] = {0, len_db};
+    const uint32_t z = 0;
+    saln_nw_result r;
+    std::vector<std::vector<uint8_t>> masks;
+    int rc = run_batch(ctx, q, qo, 1, d, dof, 1, &z, &z, 1, SALN_MODE_GLOBAL, scoring, &r,
+                       nullptr, nullptr, &masks);
+    if (rc != SALN_OK) return rc;
+    HostMask hm;
+    hm.m = masks[0].data();
+    hm.g = variant_geom(choose_variant((uint32_t)len_q));
+    hm.lq = (uint32_t)len_q;
+    hm.ld = (uint32_t)len_db;
+    hm.sc = scoring_or_default(scoring);
+    hm.to_dense(out);
+    return SALN_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,126 @@
+// Shared host/device definitions for the NW-affine engine.
+//
+// Scaled representation ("flag-in-LSB"): every score V of the reference
+// recurrence (needleman_wunsch_affine.rs:76-94) is carried as V' = 2V + p,
+// where p = 1 iff a reference boundary panic node (D[0][j>=1] :196, I[i>=1][0]
+// :208) is reachable from this (cell,state) through the reference's parent
+// pointers.  max() over scaled candidates returns the max score and ORs the
+// flags of the tied maxima, which is exactly the "panic reachable" closure of
+// the reference's DFS (:281-329).  Constants are added scaled by 2, which
+// keeps the flag.  Equality with the max is tested against H' & ~1.
+#pragma once
+#include <stdint.h>
+
+#ifndef SALN_HD
+#if defined(__HIPCC__)
+#define SALN_HD __host__ __device__ __forceinline__
+#else
+#define SALN_HD inline
+#endif
+#endif
+
+namespace saln {
+
+constexpr int32_t kSentinel = -32768;  // i16::MIN as i32, needleman_wunsch_affine.rs:174
+
+struct Scoring {
+    int32_t match, mismatch, gap_open, gap_extend;
+};
+
+// Cell-code bits (dense mask layout, include/saln.h saln_nw_dense_mask).
+enum : uint8_t {
+    kArgM = 1, kArgI = 2, kArgD = 4,
+    kIExt = 8, kIOpen = 16,
+    kDExt = 32, kDOpen = 64,
+};
+
+// One pair as the fill/traceback kernels see it (plan order).
+struct NwPairDesc {
+    uint64_t q_off, db_off;  // byte offsets into the query / db sequence buffers
+    uint64_t mask_off;       // byte offset of this pair's parent mask in the workspace
+    uint64_t cigar_off;      // word offset of this pair's cigar (in results order)
+    uint64_t scratch_off;    // int2 offset of the chunk-boundary column (multi-chunk pairs)
+    uint32_t len_q, len_db;
+    uint32_t pair_id;        // index into results
+    uint32_t variant;        // fill kernel variant (kernel geometry)
+};
+
+// Kernel geometry of one fill variant: G lanes per pair, K query columns per
+// lane, KD = ceil(K/4) mask dwords per lane per step.  A pair's query is cut
+// in chunks of W = G*K columns; chunk c's mask is laid out [step][lane][KD
+// dwords], step t holding row r = t - lane + 1 of lane `lane`.
+struct Geom {
+    uint32_t G, K;
+    SALN_HD uint32_t KD() const { return (K + 3) / 4; }
+    SALN_HD uint32_t W() const { return G * K; }
+    SALN_HD uint32_t step_bytes() const { return G * KD() * 4; }
+    SALN_HD uint32_t n_chunks(uint32_t len_q) const { return (len_q + W() - 1) / W(); }
+    SALN_HD uint64_t chunk_bytes(uint32_t len_db) const {
+        return (uint64_t)(len_db + G - 1) * step_bytes();
+    }
+    SALN_HD uint64_t mask_bytes(uint32_t len_q, uint32_t len_db) const {
+        return (uint64_t)n_chunks(len_q) * chunk_bytes(len_db);
+    }
+    // byte offset (within the pair's mask) of interior cell (i, j), 1-based.
+    SALN_HD uint64_t cell(uint32_t i, uint32_t j, uint32_t len_db) const {
+        const uint32_t jj0 = j - 1;
+        const uint32_t c = jj0 / W(), jj = jj0 % W();
+        const uint32_t lane = jj / K, k = jj % K;
+        const uint64_t t = (uint64_t)(i - 1) + lane;
+        return (uint64_t)c * chunk_bytes(len_db) + t * step_bytes() + (uint64_t)lane * KD() * 4 + k;
+    }
+};
+
+// ---------------------------------------------------------------- boundary
+// Reference boundary values (needleman_wunsch_affine.rs:172-216), true scores.
+SALN_HD int32_t d_row0(const Scoring &s, uint32_t j) {  // D[0][j], j >= 1
+    return ((int32_t)j + 1) * s.gap_extend + s.gap_open;
+}
+SALN_HD int32_t i_col0(const Scoring &s, uint32_t i) {  // I[i][0], i >= 1
+    return s.gap_open + ((int32_t)i + 1) * s.gap_extend;
+}
+SALN_HD int32_t imax(int32_t a, int32_t b) { return a > b ? a : b; }
+
+// Scaled H'(0, j) and H'(i, 0).
+SALN_HD int32_t hs_row0(const Scoring &s, uint32_t j) {
+    return j == 0 ? 0 : imax(2 * kSentinel, 2 * d_row0(s, j) + 1);
+}
+SALN_HD int32_t hs_col0(const Scoring &s, uint32_t i) {
+    return i == 0 ? 0 : imax(2 * kSentinel, 2 * i_col0(s, i) + 1);
+}
+// Scaled D'(1, j) (first-row D, from row 0) and I'(i, 1) (first-column I).
+SALN_HD int32_t ds_row1(const Scoring &s, uint32_t j) {
+    return imax(2 * kSentinel + 2 * s.gap_open, 2 * d_row0(s, j) + 1) + 2 * s.gap_extend;
+}
+SALN_HD int32_t is_col1(const Scoring &s, uint32_t i) {
+    return imax(2 * kSentinel + 2 * s.gap_open, 2 * i_col0(s, i) + 1) + 2 * s.gap_extend;
+}
+
+// argmax-set bits of boundary cells.
+SALN_HD uint8_t argmax_row0(const Scoring &s, uint32_t j) {
+    if (j == 0) return kArgM;
+    const int32_t dv = d_row0(s, j), h = imax(kSentinel, dv);
+    return (uint8_t)((kSentinel == h ? (kArgM | kArgI) : 0) | (dv == h ? kArgD : 0));
+}
+SALN_HD uint8_t argmax_col0(const Scoring &s, uint32_t i) {
+    if (i == 0) return kArgM;
+    const int32_t iv = i_col0(s, i), h = imax(kSentinel, iv);
+    return (uint8_t)((kSentinel == h ? (kArgM | kArgD) : 0) | (iv == h ? kArgI : 0));
+}
+// Parent bits of I(i,1) and D(1,j) (their producers are boundary cells).
+SALN_HD uint8_t ibits_col1(const Scoring &s, uint32_t i) {
+    const int32_t ext = i_col0(s, i), open = kSentinel + s.gap_open;
+    return (uint8_t)((ext >= open ? 1 : 0) | (open >= ext ? 2 : 0));
+}
+SALN_HD uint8_t dbits_row1(const Scoring &s, uint32_t j) {
+    const int32_t ext = d_row0(s, j), open = kSentinel + s.gap_open;
+    return (uint8_t)((ext >= open ? 1 : 0) | (open >= ext ? 2 : 0));
+}
+
+// Scaled end value H'(len_db, len_q) when a length is 0.
+SALN_HD int32_t hs_boundary_end(const Scoring &s, uint32_t len_q, uint32_t len_db) {
+    if (len_db == 0) return hs_row0(s, len_q);
+    return hs_col0(s, len_db);
+}
+
+}  // namespace saln

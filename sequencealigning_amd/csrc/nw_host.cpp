@@ -1,0 +1,520 @@
+// C ABI implementation for the NW-affine engine (include/saln.h).
+//
+// Replaces n_w_align (src/needleman_wunsch_affine.rs:424-437) and the
+// db x query pair loop that calls it (src/main.rs:61-67).  All arithmetic
+// runs in the HIP kernels of nw_kernels.hip; the host only plans batches,
+// moves buffers and, for the reference's text output, walks the parent codes
+// the GPU produced (the reference's exhaustive DFS, :281-329).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <array>
+#include <cstring>
+#include <map>
+#include <numeric>
+#include <string>
+#include <unordered_set>
+#include <vector>
+
+#include "nw_host.hpp"
+
+namespace saln {
+
+static thread_local std::string g_err;
+void set_error(const std::string &msg) { g_err = msg; }
+
+Scoring scoring_or_default(const saln_nw_scoring *s) {
+    if (!s) return Scoring{5, -4, -8, -6};  // SCHEME, needleman_wunsch_affine.rs:15-20
+    return Scoring{s->match, s->mismatch, s->gap_open, s->gap_extend};
+}
+
+#define HIP_TRY(expr)                                                                      \
+    do {                                                                                   \
+        hipError_t e_ = (expr);                                                            \
+        if (e_ != hipSuccess) {                                                            \
+            set_error(std::string(#expr) + ": " + hipGetErrorString(e_));                  \
+            return SALN_E_HIP;                                                             \
+        }                                                                                  \
+    } while (0)
+
+}  // namespace saln
+
+using namespace saln;
+
+struct saln_context {
+    int device = 0;
+    hipStream_t stream = nullptr;
+};
+
+struct saln_nw_plan {
+    saln_context *ctx = nullptr;
+    Scoring sc{};
+    uint64_t n_pairs = 0;
+    std::vector<NwPairDesc> h_pairs;  // plan order
+    std::vector<uint32_t> plan_index;  // results index -> plan order
+    NwPairDesc *d_pairs = nullptr;
+    uint32_t var_first[4] = {0, 0, 0, 0}, var_count[4] = {0, 0, 0, 0};
+    uint8_t *d_mask = nullptr;
+    uint64_t mask_bytes = 0;
+    int2 *d_scratch = nullptr;
+    uint64_t scratch_elems = 0;
+    int32_t *d_endh = nullptr;
+    std::vector<uint64_t> cigar_off;  // results order, n_pairs + 1
+    uint64_t cells = 0;
+    bool timing = false;
+    // hipEvents around the fill and traceback launches of each execute;
+    // resolved lazily (no host sync inside execute).
+    std::vector<std::array<hipEvent_t, 3>> ev_pool;
+    size_t ev_used = 0;
+    std::map<std::string, std::pair<double, uint64_t>> ktime;
+    int resolve_events();
+};
+
+extern "C" {
+
+const char *saln_last_error(void) { return g_err.c_str(); }
+int saln_abi_version(void) { return SALN_ABI_VERSION; }
+
+int saln_context_create(int device, saln_context **out) {
+    if (!out) return SALN_E_INVALID;
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= device || device < 0) {
+        set_error("no HIP device " + std::to_string(device) + " (saln has no CPU path)");
+        return SALN_E_NO_DEVICE;
+    }
+    hipDeviceProp_t prop;
+    HIP_TRY(hipGetDeviceProperties(&prop, device));
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+        set_error(std::string("device is ") + prop.gcnArchName + ", saln is built for gfx950");
+        return SALN_E_NO_DEVICE;
+    }
+    HIP_TRY(hipSetDevice(device));
+    auto *c = new saln_context;
+    c->device = device;
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        set_error("hipStreamCreate failed");
+        return SALN_E_HIP;
+    }
+    *out = c;
+    return SALN_OK;
+}
+
+int saln_context_destroy(saln_context *ctx) {
+    if (!ctx) return SALN_OK;
+    (void)hipSetDevice(ctx->device);
+    if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+    return SALN_OK;
+}
+
+int saln_nw_plan_destroy(saln_nw_plan *p) {
+    if (!p) return SALN_OK;
+    (void)hipSetDevice(p->ctx->device);
+    (void)hipFree(p->d_pairs);
+    (void)hipFree(p->d_mask);
+    (void)hipFree(p->d_scratch);
+    (void)hipFree(p->d_endh);
+    for (auto &t : p->ev_pool)
+        for (auto &e : t) (void)hipEventDestroy(e);
+    delete p;
+    return SALN_OK;
+}
+
+int saln_nw_plan_create(saln_context *ctx, const uint64_t *q_off, uint64_t n_q,
+                        const uint64_t *db_off, uint64_t n_db, const uint32_t *pair_q,
+                        const uint32_t *pair_db, uint64_t n_pairs, int32_t mode,
+                        const saln_nw_scoring *scoring, saln_nw_plan **out) {
+    if (!ctx || !q_off || !db_off || !out) return SALN_E_INVALID;
+    *out = nullptr;
+    if (mode != SALN_MODE_GLOBAL) {
+        set_error("not implemented");  // needleman_wunsch_affine.rs:433-434
+        return SALN_NOT_IMPLEMENTED;
+    }
+    if ((pair_q == nullptr) != (pair_db == nullptr)) return SALN_E_INVALID;
+    if (!pair_q && n_pairs != n_q * n_db) {
+        set_error("all-vs-all needs n_pairs == n_q * n_db");
+        return SALN_E_INVALID;
+    }
+    if (n_pairs > 0xFFFFFFFFull) return SALN_E_INVALID;
+    HIP_TRY(hipSetDevice(ctx->device));
+    auto *p = new saln_nw_plan;
+    p->ctx = ctx;
+    p->sc = scoring_or_default(scoring);
+    p->n_pairs = n_pairs;
+    p->cigar_off.resize(n_pairs + 1);
+    std::vector<NwPairDesc> descs(n_pairs);
+    uint64_t cig = 0;
+    for (uint64_t k = 0; k < n_pairs; ++k) {
+        const uint64_t qi = pair_q ? pair_q[k] : k % n_q;
+        const uint64_t di = pair_db ? pair_db[k] : k / n_q;
+        if (qi >= n_q || di >= n_db) {
+            delete p;
+            set_error("pair index out of range");
+            return SALN_E_INVALID;
+        }
+        NwPairDesc &d = descs[k];
+        std::memset(&d, 0, sizeof(d));
+        d.q_off = q_off[qi];
+        d.db_off = db_off[di];
+        const uint64_t lq = q_off[qi + 1] - q_off[qi], ld = db_off[di + 1] - db_off[di];
+        if (lq > 0x7FFFFFFFull || ld > 0x7FFFFFFFull) {
+            delete p;
+            set_error("sequence too long");
+            return SALN_E_INVALID;
+        }
+        d.len_q = (uint32_t)lq;
+        d.len_db = (uint32_t)ld;
+        d.pair_id = (uint32_t)k;
+        d.variant = (uint32_t)choose_variant(d.len_q);
+        d.cigar_off = cig;
+        p->cigar_off[k] = cig;
+        cig += lq + ld;
+        p->cells += lq * ld;
+    }
+    p->cigar_off[n_pairs] = cig;
+    // plan order: fill pairs grouped by variant, longest db first (balances
+    // the groups of a block); pairs with an empty side last (traceback only).
+    std::vector<uint32_t> order(n_pairs);
+    std::iota(order.begin(), order.end(), 0u);
+    auto key = [&](uint32_t k) {
+        const NwPairDesc &d = descs[k];
+        const bool empty = d.len_q == 0 || d.len_db == 0;
+        return std::make_tuple(empty ? 4u : d.variant, ~d.len_db, k);
+    };
+    std::sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return key(a) < key(b); });
+    p->h_pairs.resize(n_pairs);
+    uint64_t moff = 0, soff = 0;
+    for (uint64_t r = 0; r < n_pairs; ++r) {
+        NwPairDesc d = descs[order[r]];
+        const bool empty = d.len_q == 0 || d.len_db == 0;
+        if (!empty) {
+            const Geom g = variant_geom((int)d.variant);
+            d.mask_off = moff;
+            moff += (g.mask_bytes(d.len_q, d.len_db) + 255) & ~255ull;
+            if (g.n_chunks(d.len_q) > 1) {
+                d.scratch_off = soff;
+                soff += d.len_db + 2;
+            }
+            if (p->var_count[d.variant] == 0) p->var_first[d.variant] = (uint32_t)r;
+            p->var_count[d.variant]++;
+        }
+        p->h_pairs[r] = d;
+    }
+    p->plan_index.resize(n_pairs);
+    for (uint64_t r = 0; r < n_pairs; ++r) p->plan_index[p->h_pairs[r].pair_id] = (uint32_t)r;
+    p->mask_bytes = moff;
+    p->scratch_elems = soff;
+    auto fail = [&](hipError_t e, const char *what) {
+        set_error(std::string(what) + ": " + hipGetErrorString(e));
+        saln_nw_plan_destroy(p);
+        return SALN_E_HIP;
+    };
+    hipError_t e;
+    if (n_pairs) {
+        if ((e = hipMalloc(&p->d_pairs, n_pairs * sizeof(NwPairDesc))) != hipSuccess)
+            return fail(e, "hipMalloc(pairs)");
+        if ((e = hipMemcpy(p->d_pairs, p->h_pairs.data(), n_pairs * sizeof(NwPairDesc),
+                           hipMemcpyHostToDevice)) != hipSuccess)
+            return fail(e, "hipMemcpy(pairs)");
+        if ((e = hipMalloc(&p->d_endh, n_pairs * sizeof(int32_t))) != hipSuccess)
+            return fail(e, "hipMalloc(end)");
+    }
+    if (moff && (e = hipMalloc(&p->d_mask, moff)) != hipSuccess)
+        return fail(e, "hipMalloc(mask workspace)");
+    if (soff && (e = hipMalloc(&p->d_scratch, soff * sizeof(int2))) != hipSuccess)
+        return fail(e, "hipMalloc(scratch)");
+    *out = p;
+    return SALN_OK;
+}
+
+int saln_nw_plan_info(const saln_nw_plan *p, uint64_t *mask_bytes, uint64_t *cigar_words,
+                      uint64_t *cells) {
+    if (!p) return SALN_E_INVALID;
+    if (mask_bytes) *mask_bytes = p->mask_bytes;
+    if (cigar_words) *cigar_words = p->cigar_off.back();
+    if (cells) *cells = p->cells;
+    return SALN_OK;
+}
+
+int saln_nw_cigar_offsets(const saln_nw_plan *p, uint64_t *off) {
+    if (!p || !off) return SALN_E_INVALID;
+    std::memcpy(off, p->cigar_off.data(), p->cigar_off.size() * sizeof(uint64_t));
+    return SALN_OK;
+}
+
+int saln_nw_plan_set_timing(saln_nw_plan *p, int enable) {
+    if (!p) return SALN_E_INVALID;
+    HIP_TRY(hipSetDevice(p->ctx->device));
+    if (p->ev_used) {
+        const int rc = p->resolve_events();
+        if (rc != SALN_OK) return rc;
+    }
+    p->timing = enable != 0;
+    p->ktime.clear();
+    return SALN_OK;
+}
+
+int saln_nw_plan_kernel_time(const saln_nw_plan *p, const char *kernel, double *total_ms,
+                             uint64_t *launches) {
+    if (!p || !kernel) return SALN_E_INVALID;
+    const int rc = const_cast<saln_nw_plan *>(p)->resolve_events();
+    if (rc != SALN_OK) return rc;
+    auto it = p->ktime.find(kernel);
+    if (total_ms) *total_ms = it == p->ktime.end() ? 0.0 : it->second.first;
+    if (launches) *launches = it == p->ktime.end() ? 0 : it->second.second;
+    return SALN_OK;
+}
+
+int saln_nw_execute(saln_nw_plan *p, const uint8_t *d_q, const uint8_t *d_db,
+                    saln_nw_result *d_results, uint32_t *d_cigar, void *stream) {
+    if (!p || !d_results || (!d_q && p->n_pairs) || (!d_db && p->n_pairs)) return SALN_E_INVALID;
+    if (p->n_pairs == 0) return SALN_OK;
+    HIP_TRY(hipSetDevice(p->ctx->device));
+    hipStream_t s = stream ? (hipStream_t)stream : p->ctx->stream;
+    hipEvent_t *ev = nullptr;
+    if (p->timing) {
+        if (p->ev_used == p->ev_pool.size()) {
+            std::array<hipEvent_t, 3> t{};
+            for (auto &e : t) HIP_TRY(hipEventCreate(&e));
+            p->ev_pool.push_back(t);
+        }
+        ev = p->ev_pool[p->ev_used++].data();
+        HIP_TRY(hipEventRecord(ev[0], s));
+    }
+    for (int v = 0; v < 4; ++v)
+        HIP_TRY(launch_fill(v, p->d_pairs, p->var_first[v], p->var_count[v], d_q, d_db, p->d_mask,
+                            p->d_scratch, p->d_endh, p->sc, s));
+    if (ev) HIP_TRY(hipEventRecord(ev[1], s));
+    HIP_TRY(launch_traceback(p->d_pairs, (uint32_t)p->n_pairs, d_q, d_db, p->d_mask, p->d_endh,
+                             d_results, d_cigar, p->sc, s));
+    if (ev) HIP_TRY(hipEventRecord(ev[2], s));
+    return SALN_OK;
+}
+
+}  // extern "C"
+
+int saln_nw_plan::resolve_events() {
+    HIP_TRY(hipSetDevice(ctx->device));
+    for (size_t k = 0; k < ev_used; ++k) {
+        hipEvent_t *ev = ev_pool[k].data();
+        HIP_TRY(hipEventSynchronize(ev[2]));
+        float a = 0, b = 0;
+        HIP_TRY(hipEventElapsedTime(&a, ev[0], ev[1]));
+        HIP_TRY(hipEventElapsedTime(&b, ev[1], ev[2]));
+        auto &f = ktime["nw_fill"];
+        f.first += a;
+        f.second += 1;
+        auto &t = ktime["nw_traceback"];
+        t.first += b;
+        t.second += 1;
+    }
+    ev_used = 0;
+    return SALN_OK;
+}
+
+// ----------------------------------------------------------- host traceback
+namespace saln {
+
+int plan_pair_mask(const saln_nw_plan *p, uint64_t pair_id, std::vector<uint8_t> *mask,
+                   Geom *geo) {
+    if (!p || pair_id >= p->n_pairs) return SALN_E_INVALID;
+    const NwPairDesc &d = p->h_pairs[p->plan_index[pair_id]];
+    *geo = variant_geom((int)d.variant);
+    mask->clear();
+    if (d.len_q == 0 || d.len_db == 0) return SALN_OK;
+    const uint64_t n = geo->mask_bytes(d.len_q, d.len_db);
+    mask->resize(n);
+    HIP_TRY(hipSetDevice(p->ctx->device));
+    HIP_TRY(hipMemcpy(mask->data(), p->d_mask + d.mask_off, n, hipMemcpyDeviceToHost));
+    return SALN_OK;
+}
+
+void HostMask::to_dense(uint8_t *out) const {
+    const uint64_t W = (uint64_t)lq + 1;
+    for (uint32_t i = 0; i <= ld; ++i) {
+        for (uint32_t j = 0; j <= lq; ++j) {
+            uint8_t b = argmax(i, j);
+            if (i >= 1 && j >= 1) b |= (uint8_t)(ibits(i, j) << 3 | dbits(i, j) << 5);
+            if (i == 0 && j >= 1) b |= kDExt;  // D[0][j] <- D[0][j-1], :196
+            if (j == 0 && i >= 1) b |= kIExt;  // I[i][0] <- I[i-1][0], :208
+            out[(uint64_t)i * W + j] = b;
+        }
+    }
+}
+
+namespace {
+enum { ST_M = 0, ST_I = 1, ST_D = 2 };
+
+// Parents of a node in the reference's push order (DFS visits them reversed).
+int parents(const HostMask &hm, int st, uint32_t i, uint32_t j, int *ps, uint32_t *pi,
+            uint32_t *pj) {
+    int n = 0;
+    if (i == 0 || j == 0) {  // boundary nodes, :172-216
+        if (st == ST_D && i == 0 && j >= 1) { ps[0] = ST_D; pi[0] = 0; pj[0] = j - 1; return 1; }
+        if (st == ST_I && j == 0 && i >= 1) { ps[0] = ST_I; pi[0] = i - 1; pj[0] = 0; return 1; }
+        return 0;
+    }
+    if (st == ST_M) {
+        const uint8_t a = hm.argmax(i - 1, j - 1);
+        if (a & kArgM) { ps[n] = ST_M; pi[n] = i - 1; pj[n] = j - 1; ++n; }
+        if (a & kArgI) { ps[n] = ST_I; pi[n] = i - 1; pj[n] = j - 1; ++n; }
+        if (a & kArgD) { ps[n] = ST_D; pi[n] = i - 1; pj[n] = j - 1; ++n; }
+    } else if (st == ST_I) {
+        const uint8_t b = hm.ibits(i, j);
+        if (b & 1) { ps[n] = ST_I; pi[n] = i; pj[n] = j - 1; ++n; }
+        if (b & 2) { ps[n] = ST_M; pi[n] = i; pj[n] = j - 1; ++n; }
+    } else {
+        const uint8_t b = hm.dbits(i, j);
+        if (b & 1) { ps[n] = ST_D; pi[n] = i - 1; pj[n] = j; ++n; }
+        if (b & 2) { ps[n] = ST_M; pi[n] = i - 1; pj[n] = j; ++n; }
+    }
+    return n;
+}
+
+// Panics when a node with parents is expanded at x == 0 (M, D) or y == 0 (M, I).
+bool panics(int st, uint32_t i, uint32_t j, int np) {
+    if (np == 0) return false;
+    if (st == ST_M) return i == 0 || j == 0;
+    if (st == ST_D) return i == 0;
+    return j == 0;
+}
+
+struct Node {
+    int st;
+    uint32_t i, j;
+};
+
+// end states in DFS pop order: D, M, I (pushed I, M, D at :251-280)
+int end_nodes(const HostMask &hm, Node *out) {
+    const uint8_t a = hm.argmax(hm.ld, hm.lq);
+    int n = 0;
+    if (a & kArgD) out[n++] = {ST_D, hm.ld, hm.lq};
+    if (a & kArgM) out[n++] = {ST_M, hm.ld, hm.lq};
+    if (a & kArgI) out[n++] = {ST_I, hm.ld, hm.lq};
+    return n;
+}
+
+char col_q(int st, const uint8_t *q, uint32_t j) { return st == ST_D ? '-' : (char)q[j - 1]; }
+char col_d(int st, const uint8_t *d, uint32_t i) { return st == ST_I ? '-' : (char)d[i - 1]; }
+}  // namespace
+
+DfsOutcome render_blocks(const HostMask &hm, const uint8_t *q, const uint8_t *d,
+                         uint64_t max_blocks, std::string *out) {
+    DfsOutcome res;
+    struct Item {
+        Node n;
+        uint32_t depth;
+    };
+    std::vector<Item> stack;
+    std::vector<char> p1(hm.lq + hm.ld + 1), p2(hm.lq + hm.ld + 1);
+    Node ends[3];
+    const int ne = end_nodes(hm, ends);
+    for (int k = ne - 1; k >= 0; --k) stack.push_back({ends[k], 0});  // pop order D, M, I
+    while (!stack.empty()) {
+        const Item it = stack.back();
+        stack.pop_back();
+        const Node n = it.n;
+        if (n.i == 0 && n.j == 0) {  // :283-286
+            if (max_blocks && res.blocks >= max_blocks) {
+                res.status = SALN_ENUM_CAP;
+                return res;
+            }
+            if (out) {
+                out->append("alignment found\n\nseq1: ");
+                for (uint32_t k = it.depth; k-- > 0;) out->push_back(p1[k]);
+                out->append("\n      ");
+                for (uint32_t k = it.depth; k-- > 0;) out->push_back(p1[k] == p2[k] ? '|' : ' ');
+                out->append("\nseq2: ");
+                for (uint32_t k = it.depth; k-- > 0;) out->push_back(p2[k]);
+                out->push_back('\n');
+            }
+            ++res.blocks;
+        }
+        int ps[3];
+        uint32_t pi[3], pj[3];
+        const int np = parents(hm, n.st, n.i, n.j, ps, pi, pj);
+        if (panics(n.st, n.i, n.j, np)) {
+            res.status = SALN_REF_PANIC_BOUNDARY;
+            return res;
+        }
+        if (np) {
+            p1[it.depth] = col_q(n.st, q, n.j);
+            p2[it.depth] = col_d(n.st, d, n.i);
+        }
+        for (int k = 0; k < np; ++k) stack.push_back({{ps[k], pi[k], pj[k]}, it.depth + 1});
+    }
+    return res;
+}
+
+bool first_alignment(const HostMask &hm, const uint8_t *q, const uint8_t *d,
+                     std::vector<uint32_t> *cigar) {
+    // DFS in the reference order with "no event below" memoisation: the
+    // first event is the origin (printed) or a panic node (nothing printed).
+    auto key = [&](const Node &n) {
+        return ((uint64_t)n.i * ((uint64_t)hm.lq + 1) + n.j) * 3 + (uint64_t)n.st;
+    };
+    std::unordered_set<uint64_t> dead;
+    struct Frame {
+        Node n;
+        int np, next;  // next child index (counting down)
+        int ps[3];
+        uint32_t pi[3], pj[3];
+    };
+    std::vector<Frame> path;
+    Node ends[3];
+    const int ne = end_nodes(hm, ends);
+    for (int e = 0; e < ne; ++e) {
+        path.clear();
+        auto enter = [&](const Node &n) -> int {  // 1 origin, 2 panic, 0 continue
+            if (n.i == 0 && n.j == 0) return 1;
+            Frame f;
+            f.n = n;
+            f.np = parents(hm, n.st, n.i, n.j, f.ps, f.pi, f.pj);
+            if (panics(n.st, n.i, n.j, f.np)) return 2;
+            f.next = f.np - 1;
+            path.push_back(f);
+            return 0;
+        };
+        int ev = enter(ends[e]);
+        while (ev == 0 && !path.empty()) {
+            Frame &f = path.back();
+            bool descended = false;
+            while (f.next >= 0) {
+                const Node c{f.ps[f.next], f.pi[f.next], f.pj[f.next]};
+                --f.next;
+                if (dead.count(key(c))) continue;
+                ev = enter(c);
+                descended = true;
+                break;
+            }
+            if (ev) break;
+            if (!descended) {
+                dead.insert(key(path.back().n));
+                path.pop_back();
+            }
+        }
+        if (ev == 2) return false;
+        if (ev == 1) {
+            if (cigar) {
+                cigar->clear();
+                // path holds the expanded nodes from the end to the origin's child
+                for (size_t k = path.size(); k-- > 0;) {
+                    const Node &n = path[k].n;
+                    uint32_t op = n.st == ST_I ? SALN_CIGAR_I
+                                  : n.st == ST_D ? SALN_CIGAR_D
+                                  : (q[n.j - 1] == d[n.i - 1] ? SALN_CIGAR_EQ : SALN_CIGAR_X);
+                    if (!cigar->empty() && (cigar->back() & 15u) == op)
+                        cigar->back() += 16u;
+                    else
+                        cigar->push_back(16u | op);
+                }
+            }
+            return true;
+        }
+    }
+    return false;
+}
+
+}  // namespace saln

@@ -1,0 +1,68 @@
+// Host-side pieces shared by the C ABI and the CLI.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "nw_common.hpp"
+#include "saln.h"
+
+namespace saln {
+
+// kernels (nw_kernels.hip)
+hipError_t launch_fill(int variant, const NwPairDesc *pairs, uint32_t first, uint32_t count,
+                       const uint8_t *qs, const uint8_t *ds, uint8_t *mask, int2 *scratch,
+                       int32_t *end_h, Scoring sc, hipStream_t stream);
+hipError_t launch_traceback(const NwPairDesc *pairs, uint32_t n, const uint8_t *qs,
+                            const uint8_t *ds, const uint8_t *mask, const int32_t *end_h,
+                            saln_nw_result *results, uint32_t *cigar, Scoring sc,
+                            hipStream_t stream);
+Geom variant_geom(int v);
+int choose_variant(uint32_t len_q);
+
+void set_error(const std::string &msg);
+Scoring scoring_or_default(const saln_nw_scoring *s);
+
+// Random access to one pair's parent codes (kernel layout + boundary rules).
+struct HostMask {
+    const uint8_t *m = nullptr;  // pair's mask bytes (host copy)
+    Geom g{16, 10};
+    uint32_t lq = 0, ld = 0;
+    Scoring sc{5, -4, -8, -6};
+    uint8_t byte(uint32_t i, uint32_t j) const { return m[g.cell(i, j, ld)]; }
+    uint8_t argmax(uint32_t i, uint32_t j) const {
+        if (i == 0) return argmax_row0(sc, j);
+        if (j == 0) return argmax_col0(sc, i);
+        return byte(i, j) & 7;
+    }
+    uint8_t ibits(uint32_t i, uint32_t j) const {
+        return j == 1 ? ibits_col1(sc, i) : (byte(i, j - 1) >> 3) & 3;
+    }
+    uint8_t dbits(uint32_t i, uint32_t j) const {
+        return i == 1 ? dbits_row1(sc, j) : (byte(i - 1, j) >> 5) & 3;
+    }
+    // Dense export (include/saln.h saln_nw_dense_mask).
+    void to_dense(uint8_t *out) const;
+};
+
+// Copies one pair's parent codes (kernel layout) from a plan's workspace
+// after execute; pair_id is the results index.
+int plan_pair_mask(const saln_nw_plan *plan, uint64_t pair_id, std::vector<uint8_t> *mask,
+                   Geom *geo);
+
+// Reference DFS (needleman_wunsch_affine.rs:246-329) over the parent codes.
+struct DfsOutcome {
+    uint64_t blocks = 0;
+    int32_t status = SALN_OK;  // SALN_OK | SALN_REF_PANIC_BOUNDARY | SALN_ENUM_CAP
+};
+// Prints every block (reference text, no timing line) until panic / cap.
+DfsOutcome render_blocks(const HostMask &hm, const uint8_t *q, const uint8_t *d,
+                         uint64_t max_blocks, std::string *out);
+// First printed alignment with backtracking over sentinel dead ends.
+// Returns true if one is printed; cigar gets forward RLE words.
+bool first_alignment(const HostMask &hm, const uint8_t *q, const uint8_t *d,
+                     std::vector<uint32_t> *cigar);
+
+}  // namespace saln

@@ -1,0 +1,240 @@
+"""NW-affine engine, Python face of the C ABI.
+
+Mirrors ``pub fn n_w_align(seq1: &Record, seq2: &Record, _verbose: bool,
+mode: Mode) -> Result<()>`` (src/needleman_wunsch_affine.rs:424-437): seq1 is
+the query, seq2 the db record; non-global modes raise
+``AlignmentError("not implemented")`` like :433-434.  Where the reference
+only prints, this returns the score, the reference's would-be panic as a
+status, and the first printed alignment as a CIGAR; ``render`` produces the
+reference's exact text.  All compute runs in libsaln's HIP kernels.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _lib
+from .records import AlignmentError, Mode, Record
+
+DEFAULT_SCORING = (5, -4, -8, -6)  # SCHEME, needleman_wunsch_affine.rs:15-20
+
+
+@dataclass
+class NwAlignment:
+    score: int
+    status: int                     # _lib.OK / REF_PANIC_BOUNDARY
+    end_states: int                 # bit0 M, bit1 I, bit2 D
+    printed: bool                   # the reference prints >= 1 block
+    cigar: list[tuple[int, str]]    # first printed alignment, forward order
+
+    @property
+    def panics(self) -> bool:
+        return self.status == _lib.REF_PANIC_BOUNDARY
+
+    @property
+    def cigar_str(self) -> str:
+        return "".join(f"{n}{op}" for n, op in self.cigar)
+
+
+def _decode_cigar(words) -> list[tuple[int, str]]:
+    return [(int(w) >> 4, _lib.CIGAR_OPS[int(w) & 15]) for w in words]
+
+
+def cigar_ops_string(cigar: list[tuple[int, str]]) -> str:
+    """Expanded one-char-per-column op string ('=', 'X', 'I', 'D')."""
+    return "".join(op * n for n, op in cigar)
+
+
+def alignment_rows(query: bytes, db: bytes, cigar: list[tuple[int, str]]) -> tuple[str, str, str]:
+    """(seq1 line, bar line, seq2 line) of an alignment, TraceBackInfo Display :390-411."""
+    i = j = 0
+    s1, s2 = [], []
+    for n, op in cigar:
+        for _ in range(n):
+            if op in "=X":
+                s1.append(chr(query[j])); s2.append(chr(db[i])); i += 1; j += 1
+            elif op == "I":
+                s1.append(chr(query[j])); s2.append("-"); j += 1
+            else:
+                s1.append("-"); s2.append(chr(db[i])); i += 1
+    bars = "".join("|" if a == b else " " for a, b in zip(s1, s2))
+    return "".join(s1), bars, "".join(s2)
+
+
+def _bytes(x) -> bytes:
+    if isinstance(x, Record):
+        return x.seq
+    return bytes(x)
+
+
+def n_w_align(seq1, seq2, verbose: bool = False, mode: Mode = Mode.Global, *, scoring=None,
+              device: int = 0) -> NwAlignment:
+    """needleman_wunsch_affine.rs:424 — seq1 = query, seq2 = db (Record or bytes)."""
+    q, d = _bytes(seq1), _bytes(seq2)
+    L = _lib.lib()
+    ctx = _lib.context(device)
+    res = _lib.NwResult()
+    cap = len(q) + len(d) + 1
+    cig = (C.c_uint32 * cap)()
+    qb = C.create_string_buffer(q, len(q)) if q else None
+    db = C.create_string_buffer(d, len(d)) if d else None
+    rc = L.saln_nw_align(ctx, qb, len(q), db, len(d), int(verbose), int(mode),
+                         _lib.scoring_arg(scoring), C.byref(res), cig, cap)
+    if rc == _lib.NOT_IMPLEMENTED:
+        raise AlignmentError("not implemented")
+    _lib.check(rc, "saln_nw_align")
+    return NwAlignment(res.score, res.status, res.end_states, bool(res.printed),
+                       _decode_cigar(cig[:res.cigar_len]))
+
+
+def render(seq1, seq2, mode: Mode = Mode.Global, max_blocks: int = 0, *,
+           device: int = 0) -> tuple[str, int, int]:
+    """Reference stdout for one pair (timing line excluded): (text, blocks, status)."""
+    q, d = _bytes(seq1), _bytes(seq2)
+    L = _lib.lib()
+    ctx = _lib.context(device)
+    qb = C.create_string_buffer(q, len(q)) if q else None
+    db = C.create_string_buffer(d, len(d)) if d else None
+    n = C.c_uint64()
+    nb = C.c_uint64()
+    st = C.c_int32()
+    rc = L.saln_nw_render(ctx, qb, len(q), db, len(d), int(mode), max_blocks, None, 0,
+                          C.byref(n), C.byref(nb), C.byref(st))
+    if rc == _lib.NOT_IMPLEMENTED:
+        raise AlignmentError("not implemented")
+    _lib.check(rc, "saln_nw_render")
+    buf = C.create_string_buffer(n.value + 1)
+    rc = L.saln_nw_render(ctx, qb, len(q), db, len(d), int(mode), max_blocks, buf, n.value + 1,
+                          C.byref(n), C.byref(nb), C.byref(st))
+    _lib.check(rc, "saln_nw_render")
+    return buf.raw[:n.value].decode("latin-1"), nb.value, st.value
+
+
+def dense_mask(seq1, seq2, scoring=None, *, device: int = 0) -> np.ndarray:
+    """(len_db+1, len_q+1) uint8 parent codes (include/saln.h saln_nw_dense_mask)."""
+    q, d = _bytes(seq1), _bytes(seq2)
+    out = np.zeros((len(d) + 1, len(q) + 1), np.uint8)
+    qb = C.create_string_buffer(q, len(q)) if q else None
+    db = C.create_string_buffer(d, len(d)) if d else None
+    _lib.check(_lib.lib().saln_nw_dense_mask(_lib.context(device), qb, len(q), db, len(d),
+                                             _lib.scoring_arg(scoring),
+                                             out.ctypes.data_as(C.c_void_p)),
+               "saln_nw_dense_mask")
+    return out
+
+
+def pack_csr(seqs) -> tuple[np.ndarray, np.ndarray]:
+    """list of bytes -> (uint8 concatenation, uint64 offsets[n+1])."""
+    seqs = [_bytes(s) for s in seqs]
+    off = np.zeros(len(seqs) + 1, np.uint64)
+    if seqs:
+        off[1:] = np.cumsum([len(s) for s in seqs], dtype=np.uint64)
+    buf = np.frombuffer(b"".join(seqs), np.uint8) if off[-1] else np.zeros(1, np.uint8)
+    return np.ascontiguousarray(buf), off
+
+
+def nw_align_batch(queries, dbs, pairs=None, mode: Mode = Mode.Global, *, scoring=None,
+                   device: int = 0, with_cigar: bool = True):
+    """Batched n_w_align.  pairs: None (all-vs-all, db outer / query inner like
+    main.rs:61-62) or an (n, 2) array of (query index, db index).
+    Returns (results structured array, list of CIGARs or None)."""
+    qs, qo = pack_csr(queries)
+    ds, do = pack_csr(dbs)
+    if pairs is None:
+        n = len(qo) - 1
+        n_pairs = n * (len(do) - 1)
+        pq = pd = None
+    else:
+        pairs = np.asarray(pairs, np.uint32).reshape(-1, 2)
+        n_pairs = len(pairs)
+        pq = np.ascontiguousarray(pairs[:, 0])
+        pd = np.ascontiguousarray(pairs[:, 1])
+    res = np.zeros(n_pairs, dtype=_lib.RESULT_DTYPE)
+    if n_pairs == 0:
+        return res, ([] if with_cigar else None)
+    lq = np.diff(qo).astype(np.int64)
+    ld = np.diff(do).astype(np.int64)
+    if pairs is None:
+        per = np.add.outer(ld, lq).reshape(-1)
+    else:
+        per = lq[pq] + ld[pd]
+    coff = np.zeros(n_pairs + 1, np.uint64)
+    coff[1:] = np.cumsum(per, dtype=np.uint64)
+    cig = np.zeros(max(1, int(coff[-1])), np.uint32) if with_cigar else None
+    vp = lambda a: a.ctypes.data_as(C.c_void_p) if a is not None else None  # noqa: E731
+    rc = _lib.lib().saln_nw_align_batch(
+        _lib.context(device), vp(qs), vp(qo), len(qo) - 1, vp(ds), vp(do), len(do) - 1, vp(pq),
+        vp(pd), n_pairs, int(mode), _lib.scoring_arg(scoring), vp(res), vp(cig), vp(coff))
+    if rc == _lib.NOT_IMPLEMENTED:
+        raise AlignmentError("not implemented")
+    _lib.check(rc, "saln_nw_align_batch")
+    cigars = None
+    if with_cigar:
+        cigars = [_decode_cigar(cig[int(coff[k]):int(coff[k]) + int(res["cigar_len"][k])])
+                  for k in range(n_pairs)]
+    return res, cigars
+
+
+class NwPlan:
+    """Device-resident batch: plan once from host lengths, execute on torch
+    device tensors (inputs resident in HBM).  Used by bench.py and the
+    multi-GPU driver."""
+
+    def __init__(self, q_off: np.ndarray, db_off: np.ndarray, pairs=None, *, scoring=None,
+                 device: int = 0):
+        self._L = _lib.lib()
+        self.device = device
+        self.q_off = np.ascontiguousarray(q_off, np.uint64)
+        self.db_off = np.ascontiguousarray(db_off, np.uint64)
+        n_q, n_db = len(self.q_off) - 1, len(self.db_off) - 1
+        if pairs is None:
+            self.n_pairs = n_q * n_db
+            pq = pd = None
+        else:
+            pairs = np.asarray(pairs, np.uint32).reshape(-1, 2)
+            self.n_pairs = len(pairs)
+            pq = np.ascontiguousarray(pairs[:, 0])
+            pd = np.ascontiguousarray(pairs[:, 1])
+        self._h = C.c_void_p()
+        vp = lambda a: a.ctypes.data_as(C.c_void_p) if a is not None else None  # noqa: E731
+        _lib.check(self._L.saln_nw_plan_create(_lib.context(device), vp(self.q_off), n_q,
+                                               vp(self.db_off), n_db, vp(pq), vp(pd),
+                                               self.n_pairs, int(Mode.Global),
+                                               _lib.scoring_arg(scoring), C.byref(self._h)),
+                   "saln_nw_plan_create")
+        mb, cw, cells = C.c_uint64(), C.c_uint64(), C.c_uint64()
+        self._L.saln_nw_plan_info(self._h, C.byref(mb), C.byref(cw), C.byref(cells))
+        self.mask_bytes, self.cigar_words, self.cells = mb.value, cw.value, cells.value
+        self.cigar_off = np.zeros(self.n_pairs + 1, np.uint64)
+        self._L.saln_nw_cigar_offsets(self._h, self.cigar_off.ctypes.data_as(C.c_void_p))
+
+    def execute(self, q_seq, db_seq, results, cigar=None, stream=None) -> None:
+        """q_seq/db_seq/results/cigar: torch CUDA tensors (uint8 / uint8 /
+        int32[n_pairs*4] / int32[cigar_words]) or raw device pointers."""
+        ptr = lambda t: None if t is None else (t if isinstance(t, int) else t.data_ptr())  # noqa
+        if stream is None:
+            import torch
+            stream = torch.cuda.current_stream(self.device).cuda_stream
+        _lib.check(self._L.saln_nw_execute(self._h, ptr(q_seq), ptr(db_seq), ptr(results),
+                                           ptr(cigar), stream), "saln_nw_execute")
+
+    def set_timing(self, enable: bool) -> None:
+        _lib.check(self._L.saln_nw_plan_set_timing(self._h, int(enable)), "set_timing")
+
+    def kernel_time(self, name: str) -> tuple[float, int]:
+        ms, n = C.c_double(), C.c_uint64()
+        self._L.saln_nw_plan_kernel_time(self._h, name.encode(), C.byref(ms), C.byref(n))
+        return ms.value, n.value
+
+    def close(self) -> None:
+        if self._h:
+            self._L.saln_nw_plan_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -1,0 +1,162 @@
+"""GPU parity: libsaln's HIP NW-affine path vs the CPU oracle (oracle/refcpu.c,
+a restatement of src/needleman_wunsch_affine.rs).  Bit-exact on scores, end
+states, panic status, every parent code of every cell, the first printed
+alignment and the full reference text."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from nw_check import expand, path_score, rand_seq
+
+pytestmark = pytest.mark.gpu
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def _compare(saln, oracle, q: bytes, d: bytes, *, mask=True, text=True, max_pops=200_000):
+    o = oracle.nw(q, d, literal_dfs=text, max_pops=max_pops)
+    r = saln.n_w_align(saln.Record(q, b">q"), saln.Record(d, b">d"))
+    tag = f"q={q[:40]!r}.. ({len(q)}) d={d[:40]!r}.. ({len(d)})"
+    assert r.score == o.score, tag
+    assert r.end_states == o.end_states, tag
+    assert r.panics == o.panics, tag
+    assert r.printed == (o.first_ops is not None), tag
+    if o.first_ops is not None:
+        assert expand(r.cigar) == o.first_ops, tag
+    if mask:
+        dm = saln.dense_mask(q, d)
+        if not np.array_equal(dm, o.dense_mask):
+            bad = np.argwhere(dm != o.dense_mask)[:5]
+            raise AssertionError(f"{tag}: mask differs at {bad.tolist()} "
+                                 f"gpu={[int(dm[tuple(b)]) for b in bad]} "
+                                 f"ref={[int(o.dense_mask[tuple(b)]) for b in bad]}")
+    if text and o.dfs_rc != 2:
+        t, nb, st = saln.render(q, d)
+        assert t == o.stdout, tag
+        assert nb == o.dfs_blocks, tag
+        assert (st == 2) == (o.dfs_rc == 1), tag
+    return r, o
+
+
+def test_hand_kats(saln, oracle):
+    """SURVEY.md §8.4 N1-N6 (hand-traced from needleman_wunsch_affine.rs)."""
+    with open(os.path.join(GOLDEN, "nw_kats.json")) as f:
+        kats = json.load(f)["hand"]
+    for k in kats:
+        q, d = k["query"].encode(), k["db"].encode()
+        r = saln.n_w_align(q, d)
+        assert r.score == k["score"], k["id"]
+        t, nb, st = saln.render(q, d)
+        assert t == k["stdout"], k["id"]
+        assert (st == 2) == k["panics"], k["id"]
+
+
+def test_golden_vectors(saln):
+    """Committed oracle-generated vectors (tests/golden/make_golden.py)."""
+    with open(os.path.join(GOLDEN, "nw_random.json")) as f:
+        vecs = json.load(f)["pairs"]
+    res, cig = saln.nw_align_batch([v["query"].encode() for v in vecs],
+                                   [v["db"].encode() for v in vecs],
+                                   pairs=[(k, k) for k in range(len(vecs))])
+    for k, v in enumerate(vecs):
+        assert int(res["score"][k]) == v["score"], k
+        assert int(res["end_states"][k]) == v["end_states"], k
+        assert (int(res["status"][k]) == 2) == v["panics"], k
+        ops = expand(cig[k]) if res["printed"][k] else None
+        assert ops == v["first_ops"], k
+
+
+@pytest.mark.parametrize("lq,ld", [(1, 1), (2, 3), (7, 5), (16, 16), (31, 40), (150, 150),
+                                   (160, 150), (161, 20), (200, 180), (256, 100), (257, 64),
+                                   (300, 300), (512, 90), (513, 70), (1000, 1000),
+                                   (1024, 30), (1025, 40), (2100, 33), (40, 2000)])
+def test_random_shapes(saln, oracle, lq, ld):
+    rng = np.random.default_rng(lq * 7919 + ld)
+    for rep in range(3):
+        q = rand_seq(rng, lq)
+        d = rand_seq(rng, ld)
+        _compare(saln, oracle, q, d, text=lq * ld <= 40_000)
+
+
+def test_mutated_and_ties(saln, oracle):
+    from sequencealigning_amd import synth
+    rng = np.random.default_rng(5)
+    cases = [(b"A" * 30, b"A" * 25), (b"AC" * 20, b"CA" * 19), (b"ACGTN" * 10, b"NNNNN" * 8),
+             (b"GATTACA", b"GATTACA"), (b"TA", b"A"), (b"AAA", b"AA")]
+    for k in range(10):
+        q, d = synth.mut_pair(int(rng.integers(20, 400)), 0.05, 1000 + k)
+        cases.append((q, d))
+    for q, d in cases:
+        _compare(saln, oracle, q, d, text=len(q) * len(d) < 40_000, max_pops=100_000)
+
+
+def test_empty_and_N(saln, oracle):
+    for q, d in [(b"", b""), (b"", b"A"), (b"A", b""), (b"", b"ACGT" * 50), (b"N", b"N"),
+                 (b"NNNN", b"NANN")]:
+        _compare(saln, oracle, q, d, mask=len(q) > 0 and len(d) > 0)
+
+
+def test_not_implemented_modes(saln):
+    for m in (saln.Mode.Local, saln.Mode.SemiGlobal):
+        with pytest.raises(saln.AlignmentError, match="not implemented"):
+            saln.n_w_align(b"AC", b"AC", False, m)
+
+
+def test_batch_ragged_all_vs_all(saln, oracle):
+    rng = np.random.default_rng(11)
+    qs = [rand_seq(rng, int(n)) for n in [0, 1, 5, 150, 151, 300, 700, 1030]]
+    ds = [rand_seq(rng, int(n)) for n in [0, 3, 150, 222, 999]]
+    res, cig = saln.nw_align_batch(qs, ds)  # all-vs-all, db outer / query inner
+    assert len(res) == len(qs) * len(ds)
+    for di, d in enumerate(ds):
+        for qi, q in enumerate(qs):
+            k = di * len(qs) + qi
+            o = oracle.nw(q, d, literal_dfs=False)
+            assert int(res["score"][k]) == o.score, (qi, di)
+            assert int(res["end_states"][k]) == o.end_states
+            assert (int(res["status"][k]) == 2) == o.panics
+            assert (expand(cig[k]) if res["printed"][k] else None) == o.first_ops
+
+
+def test_c2_scale_properties(saln, oracle):
+    """configs[1]: 100k G-iid 150x150 pairs through the device plan; every
+    pair's CIGAR must re-score to its score under the reference recurrences,
+    and a seeded sample is checked bit-exact against the oracle."""
+    import torch
+    from sequencealigning_amd import synth
+    n, L = 100_000, 150
+    qs, qo, ds, do = synth.iid_pairs(n, L, L, seed=0x5EED0002)
+    plan = saln.NwPlan(qo, do, pairs=np.stack([np.arange(n), np.arange(n)], 1))
+    dq = torch.from_numpy(qs).cuda()
+    dd = torch.from_numpy(ds).cuda()
+    res_t = torch.zeros(n * 4, dtype=torch.int32, device="cuda")
+    cig_t = torch.zeros(max(1, plan.cigar_words), dtype=torch.int32, device="cuda")
+    plan.execute(dq, dd, res_t, cig_t)
+    torch.cuda.synchronize()
+    res = res_t.cpu().numpy().view(np.dtype([("score", "<i4"), ("status", "<i4"),
+                                             ("cigar_len", "<u4"), ("end_states", "u1"),
+                                             ("printed", "u1"), ("flags", "u1"),
+                                             ("reserved", "u1")]))
+    cig = cig_t.cpu().numpy().view(np.uint32)
+    assert (res["flags"] == 0).all()
+    ops = {7: "=", 8: "X", 1: "I", 2: "D"}
+    qb, db = qs.tobytes(), ds.tobytes()
+    for k in range(n):
+        q, d = qb[k * L:(k + 1) * L], db[k * L:(k + 1) * L]
+        if res["printed"][k]:
+            o0 = int(plan.cigar_off[k])
+            c = [(int(w) >> 4, ops[int(w) & 15]) for w in cig[o0:o0 + int(res["cigar_len"][k])]]
+            s, ok = path_score(q, d, c)
+            assert ok and s == int(res["score"][k]), k
+        else:
+            assert res["status"][k] == 2, k
+    rng = np.random.default_rng(2)
+    for k in rng.choice(n, 200, replace=False):
+        q, d = qb[k * L:(k + 1) * L], db[k * L:(k + 1) * L]
+        o = oracle.nw(q, d, literal_dfs=False)
+        assert int(res["score"][k]) == o.score
+        assert (res["status"][k] == 2) == o.panics
+        assert int(res["end_states"][k]) == o.end_states
+    plan.close()

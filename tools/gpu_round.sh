@@ -1,0 +1,25 @@
+#!/bin/bash
+# One GPU session: smoke, GPU parity tests, bench, rocprof kernel trace.
+# Every GPU step is time-limited and chained with &&.
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+STEP=${1:-all}
+if [[ $STEP == all || $STEP == smoke ]]; then
+  timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { echo "smoke failed rc=$?"; tail -30 gpurun_out/smoke.log; exit 1; }
+  tail -2 gpurun_out/smoke.log
+fi
+if [[ $STEP == all || $STEP == test ]]; then
+  timeout -k 10 900 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu.log 2>&1 || { echo "pytest gpu failed rc=$?"; tail -40 gpurun_out/pytest_gpu.log; exit 1; }
+  tail -3 gpurun_out/pytest_gpu.log
+fi
+if [[ $STEP == all || $STEP == bench ]]; then
+  timeout -k 10 600 python bench.py --steps 10 --warmup 3 > gpurun_out/bench.log 2>&1 || { echo "bench failed rc=$?"; tail -30 gpurun_out/bench.log; exit 1; }
+  tail -1 gpurun_out/bench.log
+fi
+if [[ $STEP == all || $STEP == prof ]]; then
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline > gpurun_out/prof.log 2>&1 || { echo "rocprof failed rc=$?"; tail -30 gpurun_out/prof.log; exit 1; }
+  find gpurun_out/prof -name "*kernel_stats.csv" | head -3
+  for f in $(find gpurun_out/prof -name "*kernel_stats.csv"); do head -5 "$f"; done
+fi
