@@ -123,7 +123,7 @@ def main() -> None:
             "metric": METRIC, "value": round(gcups, 3), "unit": "GCUPS", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(dt / args.steps * 1e3, 4), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "int32",
+            "scaling": "weak", "vs_baseline": None, "dtype": "int16x2",
             "data": "synthetic (splitmix64 G-iid ACGT)",
             "config": {"workload": "configs[1]: independent 150x150 NW-affine pairs per GPU "
                                    "(fill + 1 B/cell parent mask + first-printed traceback/CIGAR)",

@@ -164,7 +164,7 @@ int saln_nw_render(saln_context *ctx, const uint8_t *q, uint64_t len_q, const ui
     if (rc != SALN_OK) return rc;
     HostMask hm;
     hm.m = masks[0].data();
-    hm.g = variant_geom(choose_variant((uint32_t)len_q));
+    hm.g = variant_geom(choose_variant((uint32_t)len_q, (uint32_t)len_db, hm.sc));
     hm.lq = (uint32_t)len_q;
     hm.ld = (uint32_t)len_db;
     std::string text;
@@ -191,10 +191,10 @@ int saln_nw_dense_mask(saln_context *ctx, const uint8_t *q, uint64_t len_q, cons
     if (rc != SALN_OK) return rc;
     HostMask hm;
     hm.m = masks[0].data();
-    hm.g = variant_geom(choose_variant((uint32_t)len_q));
+    hm.sc = scoring_or_default(scoring);
+    hm.g = variant_geom(choose_variant((uint32_t)len_q, (uint32_t)len_db, hm.sc));
     hm.lq = (uint32_t)len_q;
     hm.ld = (uint32_t)len_db;
-    hm.sc = scoring_or_default(scoring);
     hm.to_dense(out);
     return SALN_OK;
 }

@@ -53,7 +53,7 @@ struct saln_nw_plan {
     std::vector<NwPairDesc> h_pairs;  // plan order
     std::vector<uint32_t> plan_index;  // results index -> plan order
     NwPairDesc *d_pairs = nullptr;
-    uint32_t var_first[4] = {0, 0, 0, 0}, var_count[4] = {0, 0, 0, 0};
+    uint32_t var_first[kNumVariants] = {}, var_count[kNumVariants] = {};
     uint8_t *d_mask = nullptr;
     uint64_t mask_bytes = 0;
     int2 *d_scratch = nullptr;
@@ -167,7 +167,7 @@ int saln_nw_plan_create(saln_context *ctx, const uint64_t *q_off, uint64_t n_q,
         d.len_q = (uint32_t)lq;
         d.len_db = (uint32_t)ld;
         d.pair_id = (uint32_t)k;
-        d.variant = (uint32_t)choose_variant(d.len_q);
+        d.variant = (uint32_t)choose_variant(d.len_q, d.len_db, p->sc);
         d.cigar_off = cig;
         p->cigar_off[k] = cig;
         cig += lq + ld;
@@ -181,7 +181,7 @@ int saln_nw_plan_create(saln_context *ctx, const uint64_t *q_off, uint64_t n_q,
     auto key = [&](uint32_t k) {
         const NwPairDesc &d = descs[k];
         const bool empty = d.len_q == 0 || d.len_db == 0;
-        return std::make_tuple(empty ? 4u : d.variant, ~d.len_db, k);
+        return std::make_tuple(empty ? (uint32_t)kNumVariants : d.variant, ~d.len_db, k);
     };
     std::sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return key(a) < key(b); });
     p->h_pairs.resize(n_pairs);
@@ -283,7 +283,7 @@ int saln_nw_execute(saln_nw_plan *p, const uint8_t *d_q, const uint8_t *d_db,
         ev = p->ev_pool[p->ev_used++].data();
         HIP_TRY(hipEventRecord(ev[0], s));
     }
-    for (int v = 0; v < 4; ++v)
+    for (int v = 0; v < kNumVariants; ++v)
         HIP_TRY(launch_fill(v, p->d_pairs, p->var_first[v], p->var_count[v], d_q, d_db, p->d_mask,
                             p->d_scratch, p->d_endh, p->sc, s));
     if (ev) HIP_TRY(hipEventRecord(ev[1], s));

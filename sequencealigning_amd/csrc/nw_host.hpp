@@ -20,7 +20,8 @@ hipError_t launch_traceback(const NwPairDesc *pairs, uint32_t n, const uint8_t *
                             saln_nw_result *results, uint32_t *cigar, Scoring sc,
                             hipStream_t stream);
 Geom variant_geom(int v);
-int choose_variant(uint32_t len_q);
+bool variant_packed(int v);
+int choose_variant(uint32_t len_q, uint32_t len_db, const Scoring &sc);
 
 void set_error(const std::string &msg);
 Scoring scoring_or_default(const saln_nw_scoring *s);
@@ -31,7 +32,8 @@ struct HostMask {
     Geom g{16, 10};
     uint32_t lq = 0, ld = 0;
     Scoring sc{5, -4, -8, -6};
-    uint8_t byte(uint32_t i, uint32_t j) const { return m[g.cell(i, j, ld)]; }
+    // codes are stored inverted (bit set = parent absent)
+    uint8_t byte(uint32_t i, uint32_t j) const { return m[g.cell(i, j, ld)] ^ 0x7F; }
     uint8_t argmax(uint32_t i, uint32_t j) const {
         if (i == 0) return argmax_row0(sc, j);
         if (j == 0) return argmax_col0(sc, i);

@@ -17,6 +17,9 @@
 // group.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <cstdlib>
+
 #include "nw_common.hpp"
 #include "saln.h"
 
@@ -122,6 +125,8 @@ __global__ __launch_bounds__(256) void nw_fill_kernel(const NwPairDesc *__restri
                 hd = inH;
                 pubF = F;
                 pubH = Hp[K - 1];
+#pragma unroll
+                for (int k = 0; k < KD; ++k) mw.w[k] ^= 0x7F7F7F7Fu;  // stored inverted
                 *reinterpret_cast<MaskWords<K> *>(mchunk + (uint64_t)t * geo.step_bytes() +
                                                   (uint32_t)lane * KD * 4) = mw;
                 if (lane == G - 1 && c + 1 < nch) scr[r] = make_int2(pubH, pubF);
@@ -138,9 +143,206 @@ __global__ __launch_bounds__(256) void nw_fill_kernel(const NwPairDesc *__restri
     }
 }
 
+// ------------------------------------------------------- packed-i16 fill
+// Two pairs per lane group: pair A in the low 16 bits of every register,
+// pair B in the high 16 bits, so every v_pk_* instruction advances two cells.
+//
+// Representation: X~(r,c) = X'(r,c) + alpha*r + beta*c, X' the flag-in-LSB
+// scaled score (nw_common.hpp).  With alpha + beta = -2*match the diagonal
+// step is M~ = H~(r-1,c-1) - pen*[q != d] (pen = 2*(match - mismatch)); with
+// beta = -2*gap_extend the I recurrence is a bare max: I~(r,c+1) =
+// max(M~ + 2*gap_open, I~); D~(r+1,c) = max(M~ + 2*gap_open, D~) + 2*ge + alpha.
+// All parent decisions compare values of the same cell, where the offsets
+// cancel.  Offsets are even, so the panic flag in the LSB survives.
+// Mismatch detection: chars are carried as c << 5, so (q ^ d) is 0 on a match
+// and >= 32 otherwise; pen = min_u16(q ^ d, pen_max).
+// Parent codes come from sign bits of same-cell differences (1 = parent
+// absent): v_perm's sign-replicating selectors (8..11) gather two signs per
+// pair into 0x00/0xFF bytes, v_and_or weights them into bit positions.
+typedef short s16x2 __attribute__((ext_vector_type(2)));
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ s16x2 as_s2(uint32_t x) { return __builtin_bit_cast(s16x2, x); }
+__device__ __forceinline__ uint32_t as_u(s16x2 x) { return __builtin_bit_cast(uint32_t, x); }
+__device__ __forceinline__ s16x2 spl(int32_t v) { return s16x2{(short)v, (short)v}; }
+__device__ __forceinline__ uint32_t pk2(int32_t lo, int32_t hi) {
+    return ((uint32_t)lo & 0xFFFFu) | ((uint32_t)hi << 16);
+}
+__device__ __forceinline__ s16x2 vmax(s16x2 a, s16x2 b) { return __builtin_elementwise_max(a, b); }
+
+// lane <- lane-1 of the same group; a group's first lane takes `bnd`.
+template <int G>
+__device__ __forceinline__ uint32_t gshift(uint32_t bnd, uint32_t v, bool group_start) {
+    uint32_t s;
+    if constexpr (G <= 16)
+        s = __builtin_amdgcn_update_dpp(bnd, v, 0x111 /*row_shr:1*/, 0xf, 0xf, false);
+    else
+        s = __builtin_amdgcn_update_dpp(bnd, v, 0x138 /*wave_shr:1*/, 0xf, 0xf, false);
+    if constexpr (G == 16 || G == 64) return s;
+    return group_start ? bnd : s;
+}
+
+// signs of (lo, hi) halves of s0 and s1 -> 0x00/0xFF bytes [A0, A1, B0, B1]
+__device__ __forceinline__ uint32_t sign_bytes(uint32_t s0, uint32_t s1) {
+    return __builtin_amdgcn_perm(s1, s0, 0x0B090A08u);
+}
+
+// 4 per-cell accumulators [A_even, A_odd, B_even, B_odd] -> (A codes, B codes)
+__device__ __forceinline__ void pack4(uint32_t a0, uint32_t a1, uint32_t a2, uint32_t a3,
+                                      uint32_t &ca, uint32_t &cb) {
+    const uint32_t x = __builtin_amdgcn_perm(a1, a0, 0x05040100u);  // [a0.b0 a0.b1 a1.b0 a1.b1]
+    const uint32_t y = __builtin_amdgcn_perm(a3, a2, 0x05040100u);
+    ca = __builtin_amdgcn_perm(y, x, 0x06040200u) | __builtin_amdgcn_perm(y, x, 0x07050301u);
+    const uint32_t xb = __builtin_amdgcn_perm(a1, a0, 0x07060302u);
+    const uint32_t yb = __builtin_amdgcn_perm(a3, a2, 0x07060302u);
+    cb = __builtin_amdgcn_perm(yb, xb, 0x06040200u) | __builtin_amdgcn_perm(yb, xb, 0x07050301u);
+}
+
+template <int K>
+struct PkMask {
+    uint32_t w[(K + 3) / 4];
+};
+
+template <int G, int K>
+__global__ __launch_bounds__(256) void nw_fill_pk_kernel(const NwPairDesc *__restrict__ pairs,
+                                                         uint32_t first, uint32_t count,
+                                                         const uint8_t *__restrict__ qs,
+                                                         const uint8_t *__restrict__ ds,
+                                                         uint8_t *__restrict__ mask,
+                                                         int32_t *__restrict__ end_h, Scoring sc) {
+    constexpr int GPB = 256 / G;
+    constexpr int KD = (K + 3) / 4;
+    constexpr Geom geo{G, K};
+    const int lane = threadIdx.x % G;
+    const uint32_t gi = blockIdx.x * GPB + threadIdx.x / G;
+    const uint32_t ia = 2 * gi, ib = 2 * gi + 1;
+    if (ia >= count) return;  // whole group
+    const bool hasB = ib < count;
+    const NwPairDesc pa = pairs[first + ia];
+    NwPairDesc pb = pa;
+    if (hasB) pb = pairs[first + ib];
+    const int ldA = (int)pa.len_db, ldB = hasB ? (int)pb.len_db : 0;
+    const int lqA = (int)pa.len_q, lqB = hasB ? (int)pb.len_q : 0;
+    const uint8_t *__restrict__ qA = qs + pa.q_off;
+    const uint8_t *__restrict__ qB = qs + pb.q_off;
+    const uint8_t *__restrict__ dA = ds + pa.db_off;
+    const uint8_t *__restrict__ dB = ds + pb.db_off;
+    const int ldM = ldA > ldB ? ldA : ldB;
+    const int T = ldM + G - 1;
+    const int32_t beta = -2 * sc.gap_extend;
+    const int32_t alpha = -2 * sc.match - beta;
+    const s16x2 kPen = spl(2 * (sc.match - sc.mismatch));
+    const s16x2 kOpen = spl(2 * sc.gap_open);
+    const s16x2 kDstep = spl(2 * sc.gap_extend + alpha);
+    const bool gstart = lane == 0;
+
+    const int col0 = lane * K;  // my columns: col0+1 .. col0+K
+    // loop-carried state is kept as plain dwords (2 x i16) so the compiler
+    // does not split it into halves
+    uint32_t qc[K], Hp[K], Dn[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const int j = col0 + k + 1;
+        const uint32_t ca = j <= lqA ? (uint32_t)qA[j - 1] << 5 : 0xE000u;
+        const uint32_t cb = j <= lqB ? (uint32_t)qB[j - 1] << 5 : 0xE000u;
+        qc[k] = ca | (cb << 16);
+        const int32_t h0 = hs_row0(sc, (uint32_t)j) + beta * j;           // H~(0, j)
+        const int32_t d1 = ds_row1(sc, (uint32_t)j) + alpha + beta * j;   // D~(1, j)
+        Hp[k] = pk2(h0, h0);
+        Dn[k] = pk2(d1, d1);
+    }
+    uint32_t hd = pk2(hs_row0(sc, (uint32_t)col0) + beta * col0,
+                      hs_row0(sc, (uint32_t)col0) + beta * col0);  // H~(r-1, col0)
+    uint32_t pubF = 0, pubH = 0;
+    // db chars of my next row, per half (row r+1 -> index r).  Loads are
+    // unconditional (clamped index) and consumed one step later, so their
+    // latency hides behind a whole step of arithmetic.
+    // Two-step pipeline: the chars of row r arrive two steps ahead.
+    const int ldA1 = ldA - 1, ldB1 = (hasB ? ldB : ldA) - 1;
+    uint32_t pa0 = dA[min(max(-lane, 0), ldA1)], pb0 = dB[min(max(-lane, 0), ldB1)];
+    uint32_t pa1 = dA[min(max(1 - lane, 0), ldA1)], pb1 = dB[min(max(1 - lane, 0), ldB1)];
+    // end-cell owners
+    const int lA = (lqA - 1) / K, kA = (lqA - 1) % K;
+    const int lB = hasB ? (lqB - 1) / K : -1, kB = hasB ? (lqB - 1) % K : 0;
+    uint8_t *__restrict__ mA = mask + pa.mask_off + (uint32_t)lane * KD * 4;
+    uint8_t *__restrict__ mB = mask + pb.mask_off + (uint32_t)lane * KD * 4;
+
+    for (int t = 0; t < T; ++t) {
+        const int r = t - lane + 1;
+        const uint32_t dch = (pa0 << 5) | (pb0 << 21);
+        pa0 = pa1;
+        pb0 = pb1;
+        pa1 = dA[min(max(r + 1, 0), ldA1)];
+        pb1 = dB[min(max(r + 1, 0), ldB1)];
+        // group-start inputs for row t+1: I~(r,1) and H~(r,0) (same for A and B)
+        const int32_t rb = t + 1;
+        const int32_t bF = is_col1(sc, (uint32_t)rb) + alpha * rb + beta;
+        const int32_t bH = hs_col0(sc, (uint32_t)rb) + alpha * rb;
+        const uint32_t inF = gshift<G>(pk2(bF, bF), pubF, gstart);
+        const uint32_t inH = gshift<G>(pk2(bH, bH), pubH, gstart);
+        if (r >= 1 && r <= ldM) {
+            uint32_t F = inF;
+            PkMask<K> wa, wb;
+            uint32_t acc[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                const u16x2 x = __builtin_bit_cast(u16x2, qc[k] ^ dch);
+                const s16x2 pen = __builtin_bit_cast(
+                    s16x2, __builtin_elementwise_min(x, __builtin_bit_cast(u16x2, kPen)));
+                const s16x2 M = as_s2(hd) - pen;
+                const s16x2 I = as_s2(F), D = as_s2(Dn[k]);
+                const s16x2 H = vmax(M, vmax(I, D));
+                const s16x2 Hc = as_s2(as_u(H) & 0xFFFEFFFEu);
+                const s16x2 tO = M + kOpen;
+                // sign set <=> parent absent.  Extend/open ties are decided on
+                // the flag-free order: ext <=> (X|1) >= tO, open <=> (tO|1) >= X.
+                const s16x2 tOr = as_s2(as_u(tO) | 0x00010001u);
+                const s16x2 Ir = as_s2(as_u(I) | 0x00010001u);
+                const s16x2 Dr = as_s2(as_u(D) | 0x00010001u);
+                const uint32_t s0 = as_u(M - Hc), s1 = as_u(I - Hc), s2 = as_u(D - Hc);
+                const uint32_t s3 = as_u(Ir - tO), s4 = as_u(tOr - I);
+                const uint32_t s5 = as_u(Dr - tO), s6 = as_u(tOr - D);
+                uint32_t a = sign_bytes(s0, s1) & 0x02010201u;
+                a = (sign_bytes(s2, s3) & 0x08040804u) | a;
+                a = (sign_bytes(s4, s5) & 0x20102010u) | a;
+                a = (sign_bytes(s6, s6) & 0x00400040u) | a;
+                acc[k % 4] = a;
+                if (k % 4 == 3 || k == K - 1) {
+                    pack4(acc[0], k % 4 >= 1 ? acc[1] : 0u, k % 4 >= 2 ? acc[2] : 0u,
+                          k % 4 >= 3 ? acc[3] : 0u, wa.w[k / 4], wb.w[k / 4]);
+                }
+                F = as_u(vmax(tO, I));
+                Dn[k] = as_u(vmax(tO, D) + kDstep);
+                hd = Hp[k];
+                Hp[k] = as_u(H);
+            }
+            hd = inH;
+            pubF = F;
+            pubH = Hp[K - 1];
+            const uint64_t so = (uint64_t)t * geo.step_bytes();
+            if (r <= ldA) *reinterpret_cast<PkMask<K> *>(mA + so) = wa;
+            if (r <= ldB) *reinterpret_cast<PkMask<K> *>(mB + so) = wb;
+            if (r == ldA && lane == lA) {
+                int32_t e = 0;
+#pragma unroll
+                for (int k = 0; k < K; ++k)
+                    if (k == kA) e = (int16_t)(Hp[k] & 0xFFFFu);
+                end_h[first + ia] = e - alpha * ldA - beta * lqA;
+            }
+            if (r == ldB && lane == lB) {
+                int32_t e = 0;
+#pragma unroll
+                for (int k = 0; k < K; ++k)
+                    if (k == kB) e = (int16_t)(Hp[k] >> 16);
+                end_h[first + ib] = e - alpha * ldB - beta * lqB;
+            }
+        }
+    }
+}
+
 // --------------------------------------------------------------- traceback
 struct GeomTable {
-    Geom g[4];
+    Geom g[kNumVariants];
 };
 
 struct MaskCell {
@@ -148,7 +350,8 @@ struct MaskCell {
     Geom g;
     uint32_t lq, ld;
     Scoring sc;
-    __device__ uint8_t byte(uint32_t i, uint32_t j) const { return m[g.cell(i, j, ld)]; }
+    // codes are stored inverted (bit set = parent absent)
+    __device__ uint8_t byte(uint32_t i, uint32_t j) const { return m[g.cell(i, j, ld)] ^ 0x7F; }
     __device__ uint8_t argmax(uint32_t i, uint32_t j) const {
         if (i == 0) return argmax_row0(sc, j);
         if (j == 0) return argmax_col0(sc, i);
@@ -183,7 +386,7 @@ __global__ __launch_bounds__(256) void nw_traceback_kernel(
     const uint32_t lq = p.len_q, ld = p.len_db;
     const uint8_t *q = qs + p.q_off;
     const uint8_t *d = ds + p.db_off;
-    const MaskCell mc{mask + p.mask_off, gt.g[p.variant & 3], lq, ld, sc};
+    const MaskCell mc{mask + p.mask_off, gt.g[p.variant], lq, ld, sc};
     const int32_t hend = (lq && ld) ? end_h[idx] : hs_boundary_end(sc, lq, ld);
     const uint8_t am_end = mc.argmax(ld, lq);
     int st = (am_end & kArgD) ? kStD : ((am_end & kArgM) ? kStM : kStI);
@@ -249,31 +452,42 @@ __global__ __launch_bounds__(256) void nw_traceback_kernel(
 }
 
 // ----------------------------------------------------------------- launchers
-constexpr Geom kVariants[4] = {{16, 10}, {16, 16}, {64, 8}, {64, 16}};
+// variants 0-3: i32 lanes; 4-6: packed i16 (two pairs per lane)
+constexpr Geom kVariants[kNumVariants] = {{16, 10}, {16, 16}, {64, 8}, {64, 16},
+                                          {8, 19},  {16, 16}, {32, 16}};
+constexpr bool kPacked[kNumVariants] = {false, false, false, false, true, true, true};
+
+template <int G, int K>
+static void fill_i32(dim3 grid, hipStream_t s, const NwPairDesc *pairs, uint32_t first,
+                     uint32_t count, const uint8_t *qs, const uint8_t *ds, uint8_t *mask,
+                     int2 *scratch, int32_t *end_h, Scoring sc) {
+    nw_fill_kernel<G, K><<<grid, dim3(256), 0, s>>>(pairs, first, count, qs, ds, mask, scratch,
+                                                     end_h, sc);
+}
+
+template <int G, int K>
+static void fill_pk(dim3 grid, hipStream_t s, const NwPairDesc *pairs, uint32_t first,
+                    uint32_t count, const uint8_t *qs, const uint8_t *ds, uint8_t *mask,
+                    int32_t *end_h, Scoring sc) {
+    nw_fill_pk_kernel<G, K><<<grid, dim3(256), 0, s>>>(pairs, first, count, qs, ds, mask, end_h,
+                                                        sc);
+}
 
 hipError_t launch_fill(int variant, const NwPairDesc *pairs, uint32_t first, uint32_t count,
                        const uint8_t *qs, const uint8_t *ds, uint8_t *mask, int2 *scratch,
                        int32_t *end_h, Scoring sc, hipStream_t stream) {
     if (count == 0) return hipSuccess;
-    const uint32_t gpb = 256 / kVariants[variant].G;
-    const dim3 grid((count + gpb - 1) / gpb), block(256);
+    const uint32_t gpb = 256 / kVariants[variant].G;  // lane groups per block
+    const uint32_t groups = kPacked[variant] ? (count + 1) / 2 : count;
+    const dim3 grid((groups + gpb - 1) / gpb);
     switch (variant) {
-        case 0:
-            nw_fill_kernel<16, 10><<<grid, block, 0, stream>>>(pairs, first, count, qs, ds, mask,
-                                                                scratch, end_h, sc);
-            break;
-        case 1:
-            nw_fill_kernel<16, 16><<<grid, block, 0, stream>>>(pairs, first, count, qs, ds, mask,
-                                                                scratch, end_h, sc);
-            break;
-        case 2:
-            nw_fill_kernel<64, 8><<<grid, block, 0, stream>>>(pairs, first, count, qs, ds, mask,
-                                                               scratch, end_h, sc);
-            break;
-        default:
-            nw_fill_kernel<64, 16><<<grid, block, 0, stream>>>(pairs, first, count, qs, ds, mask,
-                                                                scratch, end_h, sc);
-            break;
+        case 0: fill_i32<16, 10>(grid, stream, pairs, first, count, qs, ds, mask, scratch, end_h, sc); break;
+        case 1: fill_i32<16, 16>(grid, stream, pairs, first, count, qs, ds, mask, scratch, end_h, sc); break;
+        case 2: fill_i32<64, 8>(grid, stream, pairs, first, count, qs, ds, mask, scratch, end_h, sc); break;
+        case 3: fill_i32<64, 16>(grid, stream, pairs, first, count, qs, ds, mask, scratch, end_h, sc); break;
+        case 4: fill_pk<8, 19>(grid, stream, pairs, first, count, qs, ds, mask, end_h, sc); break;
+        case 5: fill_pk<16, 16>(grid, stream, pairs, first, count, qs, ds, mask, end_h, sc); break;
+        default: fill_pk<32, 16>(grid, stream, pairs, first, count, qs, ds, mask, end_h, sc); break;
     }
     return hipGetLastError();
 }
@@ -284,15 +498,32 @@ hipError_t launch_traceback(const NwPairDesc *pairs, uint32_t n, const uint8_t *
                             hipStream_t stream) {
     if (n == 0) return hipSuccess;
     GeomTable gt;
-    for (int v = 0; v < 4; ++v) gt.g[v] = kVariants[v];
+    for (int v = 0; v < kNumVariants; ++v) gt.g[v] = kVariants[v];
     nw_traceback_kernel<<<dim3((n + 255) / 256), dim3(256), 0, stream>>>(
         pairs, n, qs, ds, mask, end_h, results, cigar, sc, gt);
     return hipGetLastError();
 }
 
 Geom variant_geom(int v) { return kVariants[v]; }
+bool variant_packed(int v) { return kPacked[v]; }
 
-int choose_variant(uint32_t len_q) {
+// Packed i16 is exact while every value and every same-cell difference stays
+// inside int16 with the position offsets of nw_fill_pk_kernel (see there).
+static bool packed_ok(uint32_t lq, uint32_t ld, const Scoring &sc) {
+    const int64_t pen = 2ll * (sc.match - sc.mismatch);
+    if (pen < 0 || pen > 32 || sc.gap_extend > 0 || sc.gap_open > 0) return false;
+    const int64_t span = std::max<int64_t>(
+        {std::abs(sc.match), std::abs(sc.mismatch), std::abs(sc.gap_open) + std::abs(sc.gap_extend)});
+    const int64_t a = 2 * (std::abs(sc.match) + std::abs(sc.gap_extend)) + 2 * span;
+    return (int64_t)ld * a + (int64_t)lq * (2 * std::abs(sc.gap_extend) + 2 * span) + 256 < 30000;
+}
+
+int choose_variant(uint32_t len_q, uint32_t len_db, const Scoring &sc) {
+    if (packed_ok(len_q, len_db, sc)) {
+        if (len_q <= 152) return 4;
+        if (len_q <= 256) return 5;
+        if (len_q <= 512) return 6;
+    }
     if (len_q <= 160) return 0;
     if (len_q <= 256) return 1;
     if (len_q <= 512) return 2;
