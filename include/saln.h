@@ -161,6 +161,14 @@ int saln_nw_execute(saln_nw_plan *plan, const uint8_t *d_q_seq, const uint8_t *d
 int saln_nw_plan_set_timing(saln_nw_plan *plan, int enable);
 int saln_nw_plan_kernel_time(const saln_nw_plan *plan, const char *kernel, double *total_ms,
                              uint64_t *launches);
+/* Pipelined mode: execute returns with the traceback still running on the
+ * context's second stream, so the traceback of batch n overlaps the fill of
+ * batch n+1 (the plan double-buffers its mask workspace).  Results of an
+ * execute are complete only after saln_nw_plan_sync(plan, stream, ...) has
+ * made `stream` wait for them; keep_latest = 1 leaves the most recent execute
+ * pending (software pipelining). */
+int saln_nw_plan_set_async(saln_nw_plan *plan, int enable);
+int saln_nw_plan_sync(saln_nw_plan *plan, void *stream, int keep_latest);
 int saln_nw_plan_destroy(saln_nw_plan *plan);
 
 /* --------------------------------------------------------------------- FASTA

@@ -61,7 +61,8 @@ EXPORTS = [
     "saln_context_create", "saln_context_destroy", "saln_last_error", "saln_abi_version",
     "saln_nw_align", "saln_nw_render", "saln_nw_dense_mask", "saln_nw_align_batch",
     "saln_nw_plan_create", "saln_nw_plan_info", "saln_nw_cigar_offsets", "saln_nw_execute",
-    "saln_nw_plan_set_timing", "saln_nw_plan_kernel_time", "saln_nw_plan_destroy",
+    "saln_nw_plan_set_timing", "saln_nw_plan_kernel_time", "saln_nw_plan_set_async",
+    "saln_nw_plan_sync", "saln_nw_plan_destroy",
     "saln_parse_fasta", "saln_parse_fasta_buffer", "saln_records_count", "saln_records_get",
     "saln_records_free",
 ]
@@ -121,6 +122,8 @@ def lib() -> C.CDLL:
         L.saln_nw_execute.argtypes = [vp, vp, vp, vp, vp, vp]
         L.saln_nw_plan_set_timing.argtypes = [vp, C.c_int]
         L.saln_nw_plan_kernel_time.argtypes = [vp, C.c_char_p, C.POINTER(C.c_double), u64p]
+        L.saln_nw_plan_set_async.argtypes = [vp, C.c_int]
+        L.saln_nw_plan_sync.argtypes = [vp, vp, C.c_int]
         L.saln_nw_plan_destroy.argtypes = [vp]
         L.saln_parse_fasta.argtypes = [C.c_char_p, C.POINTER(vp), u8p, C.c_uint64, u64p]
         L.saln_parse_fasta_buffer.argtypes = [vp, C.c_uint64, C.POINTER(vp), u8p, C.c_uint64,

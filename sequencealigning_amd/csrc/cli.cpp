@@ -1,1 +1,309 @@
-int main(){return 0;}
+// saln — command-line drop-in for the reference binary (src/main.rs:19-80,
+// src/parse.rs:8-50): same short/long flags (-q -d -o -v -m -a), same value
+// names, same db-outer / query-inner pair order and the same stdout/stderr
+// text.  NW alignments are computed by libsaln on the GPU; the reference's
+// exhaustive block printing is replayed on the host from the GPU's parent
+// codes (saln_nw_render).  The `{:#?}` timing line after each NW pair
+// (needleman_wunsch_affine.rs:431) prints this engine's wall time.
+//
+// Differences by design: `-a a-star` (the reference default) is not part of
+// this engine and is rejected; a reference panic (boundary index panic of the
+// NW traceback) aborts with exit code 101 after the blocks printed before it,
+// like the reference, unless --no-abort is given.
+#include <chrono>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "saln.h"
+
+namespace {
+
+struct Args {
+    std::string query, db, out = "./results";
+    bool verbose = false;
+    int mode = SALN_MODE_GLOBAL;
+    int algo = 0;  // 0 a-star (reference default), 1 needleman-wunsch, 2 wfa
+    int device = 0;
+    bool timing = true, abort_on_panic = true;
+    uint64_t max_blocks = 0;
+};
+
+const char *kUsage =
+    "Usage: saln [OPTIONS] --query-file <QUERY_FILE> --db-file <DB_FILE>\n"
+    "\n"
+    "Options:\n"
+    "  -q, --query-file <QUERY_FILE>  Path to query sequence\n"
+    "  -d, --db-file <DB_FILE>        path to db sequence\n"
+    "  -o, --out-path <OUT_PATH>      out path [default: ./results]\n"
+    "  -v, --verbose                  verbose\n"
+    "  -m, --mode <MODE>              modus [default: global] [possible values: global, local, "
+    "semi-global]\n"
+    "  -a, --algo <ALGO>              algo [default: a-star] [possible values: a-star, "
+    "needleman-wunsch, wfa]\n"
+    "      --device <N>               HIP device [default: 0]\n"
+    "      --no-timing                omit the per-pair timing line\n"
+    "      --no-abort                 report reference panics and continue\n"
+    "      --max-blocks <N>           cap on printed alignments per pair [default: 0 = none]\n"
+    "  -h, --help                     Print help\n";
+
+[[noreturn]] void usage_error(const std::string &msg) {
+    std::fprintf(stderr, "error: %s\n\n%s", msg.c_str(), kUsage);
+    std::exit(2);
+}
+
+Args parse_args(int argc, char **argv) {
+    Args a;
+    bool have_q = false, have_d = false;
+    for (int k = 1; k < argc; ++k) {
+        std::string s = argv[k];
+        std::string val;
+        auto need = [&](const char *name) -> std::string {
+            const size_t eq = s.find('=');
+            if (s.rfind("--", 0) == 0 && eq != std::string::npos) return s.substr(eq + 1);
+            if (k + 1 >= argc) usage_error(std::string("a value is required for '") + name + "'");
+            return argv[++k];
+        };
+        auto is = [&](const char *sh, const char *lg) {
+            return s == sh || s == lg || (s.rfind(std::string(lg) + "=", 0) == 0);
+        };
+        if (s == "-h" || s == "--help") {
+            std::fputs(kUsage, stdout);
+            std::exit(0);
+        } else if (is("-q", "--query-file")) {
+            a.query = need("--query-file <QUERY_FILE>");
+            have_q = true;
+        } else if (is("-d", "--db-file")) {
+            a.db = need("--db-file <DB_FILE>");
+            have_d = true;
+        } else if (is("-o", "--out-path")) {
+            a.out = need("--out-path <OUT_PATH>");
+        } else if (s == "-v" || s == "--verbose") {
+            a.verbose = true;
+        } else if (is("-m", "--mode")) {
+            val = need("--mode <MODE>");
+            if (val == "global") a.mode = SALN_MODE_GLOBAL;
+            else if (val == "local") a.mode = SALN_MODE_LOCAL;
+            else if (val == "semi-global") a.mode = SALN_MODE_SEMI_GLOBAL;
+            else usage_error("invalid value '" + val + "' for '--mode <MODE>'");
+        } else if (is("-a", "--algo")) {
+            val = need("--algo <ALGO>");
+            if (val == "a-star") a.algo = 0;
+            else if (val == "needleman-wunsch") a.algo = 1;
+            else if (val == "wfa") a.algo = 2;
+            else usage_error("invalid value '" + val + "' for '--algo <ALGO>'");
+        } else if (is("--device", "--device")) {
+            a.device = std::atoi(need("--device <N>").c_str());
+        } else if (s == "--no-timing") {
+            a.timing = false;
+        } else if (s == "--no-abort") {
+            a.abort_on_panic = false;
+        } else if (is("--max-blocks", "--max-blocks")) {
+            a.max_blocks = std::strtoull(need("--max-blocks <N>").c_str(), nullptr, 10);
+        } else {
+            usage_error("unexpected argument '" + s + "' found");
+        }
+    }
+    if (!have_q || !have_d)
+        usage_error("the following required arguments were not provided:\n  --query-file "
+                    "<QUERY_FILE>\n  --db-file <DB_FILE>");
+    return a;
+}
+
+// Rust `{:?}` of a char (used for the CharError vector, main.rs:29-35).
+std::string rust_char_debug(uint8_t c) {
+    switch (c) {
+        case '\t': return "'\\t'";
+        case '\r': return "'\\r'";
+        case '\n': return "'\\n'";
+        case '\'': return "'\\''";
+        case '\\': return "'\\\\'";
+        case 0: return "'\\0'";
+        default: break;
+    }
+    char buf[16];
+    if (c < 0x20 || (c >= 0x7F && c < 0xA0) || c == 0xAD) {
+        std::snprintf(buf, sizeof(buf), "'\\u{%x}'", c);
+        return buf;
+    }
+    if (c < 0x80) {
+        std::snprintf(buf, sizeof(buf), "'%c'", c);
+        return buf;
+    }
+    // Latin-1 code point as UTF-8
+    buf[0] = '\'';
+    buf[1] = (char)(0xC0 | (c >> 6));
+    buf[2] = (char)(0x80 | (c & 0x3F));
+    buf[3] = '\'';
+    buf[4] = 0;
+    return buf;
+}
+
+// `{:#?}` of a Vec<char>
+std::string vec_char_pretty(const std::vector<uint8_t> &v) {
+    if (v.empty()) return "[]";
+    std::string s = "[\n";
+    for (uint8_t c : v) s += "    " + rust_char_debug(c) + ",\n";
+    return s + "]";
+}
+
+// `{:#?}` of a std::time::Duration (Debug: integer part + trimmed fraction)
+std::string duration_debug(uint64_t ns) {
+    const char *unit;
+    uint64_t integer, frac, frac_digits;
+    if (ns >= 1000000000ull) {
+        unit = "s";
+        integer = ns / 1000000000ull;
+        frac = ns % 1000000000ull;
+        frac_digits = 9;
+    } else if (ns >= 1000000ull) {
+        unit = "ms";
+        integer = ns / 1000000ull;
+        frac = ns % 1000000ull;
+        frac_digits = 6;
+    } else if (ns >= 1000ull) {
+        unit = "\xC2\xB5s";
+        integer = ns / 1000ull;
+        frac = ns % 1000ull;
+        frac_digits = 3;
+    } else {
+        return std::to_string(ns) + "ns";
+    }
+    std::string s = std::to_string(integer);
+    if (frac) {
+        std::string f = std::to_string(frac);
+        f = std::string(frac_digits - f.size(), '0') + f;
+        while (!f.empty() && f.back() == '0') f.pop_back();
+        s += "." + f;
+    }
+    return s + unit;
+}
+
+struct Rec {
+    std::vector<uint8_t> name, seq;
+};
+
+// parse_fasta + the match in main.rs:22-60.  Returns false to stop (`return`).
+bool load(const std::string &path, const char *which, std::vector<Rec> *out) {
+    saln_records *r = nullptr;
+    std::vector<uint8_t> bad(1 << 16);
+    uint64_t nbad = 0;
+    const int rc = saln_parse_fasta(path.c_str(), &r, bad.data(), bad.size(), &nbad);
+    if (rc == SALN_E_FASTA) {
+        std::string e = saln_last_error();
+        const std::string pre = "Fasta could not be opened with err: ";
+        if (e.rfind(pre, 0) == 0) e = e.substr(pre.size());
+        std::fprintf(stderr, "%s fasta could not be opened: %s\naborting\n", which, e.c_str());
+        return false;
+    }
+    if (rc != SALN_OK && rc != SALN_E_FASTA_CHARS) {
+        std::fprintf(stderr, "Unexpected error in %s fasta: %s\n", which, saln_last_error());
+        return false;
+    }
+    if (rc == SALN_E_FASTA_CHARS) {
+        if (nbad > bad.size()) {  // re-read with room for every dropped byte
+            saln_records_free(r);
+            bad.resize(nbad);
+            saln_parse_fasta(path.c_str(), &r, bad.data(), bad.size(), &nbad);
+        }
+        bad.resize(nbad);
+        std::fprintf(stderr, "Invalid character '%s' detected in %s fasta; continuing by ignoring it\n",
+                     vec_char_pretty(bad).c_str(), which[0] == 'D' ? "db" : "query");
+    }
+    const uint64_t n = saln_records_count(r);
+    out->resize(n);
+    for (uint64_t k = 0; k < n; ++k) {
+        const uint8_t *nm, *sq;
+        uint64_t nl, sl;
+        saln_records_get(r, k, &nm, &nl, &sq, &sl);
+        (*out)[k].name.assign(nm, nm + nl);
+        (*out)[k].seq.assign(sq, sq + sl);
+    }
+    saln_records_free(r);
+    return true;
+}
+
+std::string as_str(const std::vector<uint8_t> &v) { return std::string(v.begin(), v.end()); }
+
+}  // namespace
+
+int main(int argc, char **argv) {
+    const Args a = parse_args(argc, argv);
+    std::vector<Rec> db, query;
+    if (!load(a.db, "DB", &db)) return 0;
+    if (!load(a.query, "Query", &query)) return 0;
+    if (a.algo == 0) {
+        std::fprintf(stderr,
+                     "saln: -a a-star (the reference's A* aligner) is not part of this engine; "
+                     "use -a needleman-wunsch or -a wfa\n");
+        return 2;
+    }
+    if (a.algo == 2) {
+        std::fprintf(stderr, "saln: -a wfa is not available in this build\n");
+        return 2;
+    }
+    saln_context *ctx = nullptr;
+    if (saln_context_create(a.device, &ctx) != SALN_OK) {
+        std::fprintf(stderr, "saln: %s\n", saln_last_error());
+        return 1;
+    }
+    std::string text;
+    for (const Rec &d : db) {          // main.rs:61
+        for (const Rec &q : query) {   // main.rs:62
+            const auto t0 = std::chrono::steady_clock::now();
+            uint64_t len = 0, blocks = 0;
+            int32_t status = SALN_OK;
+            int rc = saln_nw_render(ctx, q.seq.data(), q.seq.size(), d.seq.data(), d.seq.size(),
+                                    a.mode, a.max_blocks, nullptr, 0, &len, &blocks, &status);
+            if (rc == SALN_NOT_IMPLEMENTED) {  // main.rs:68-74
+                std::fprintf(stderr,
+                             "An error occured during alignment of %s and %s\nError in alignment: "
+                             "not implemented\n",
+                             as_str(q.name).c_str(), as_str(d.name).c_str());
+                continue;
+            }
+            if (rc != SALN_OK) {
+                std::fprintf(stderr, "saln: %s\n", saln_last_error());
+                return 1;
+            }
+            text.assign(len, '\0');
+            rc = saln_nw_render(ctx, q.seq.data(), q.seq.size(), d.seq.data(), d.seq.size(),
+                                a.mode, a.max_blocks, text.data(), len, &len, &blocks, &status);
+            if (rc != SALN_OK) {
+                std::fprintf(stderr, "saln: %s\n", saln_last_error());
+                return 1;
+            }
+            std::fwrite(text.data(), 1, text.size(), stdout);
+            if (status == SALN_REF_PANIC_BOUNDARY) {
+                std::fflush(stdout);
+                if (a.abort_on_panic) {
+                    std::fprintf(stderr,
+                                 "thread 'main' panicked at src/needleman_wunsch_affine.rs: index "
+                                 "out of bounds (traceback reached a boundary cell other than the "
+                                 "origin)\nnote: run with `RUST_BACKTRACE=1` environment variable "
+                                 "to display a backtrace\n");
+                    saln_context_destroy(ctx);
+                    return 101;
+                }
+                std::fprintf(stderr, "saln: reference panic (REF_PANIC_BOUNDARY) for %s vs %s\n",
+                             as_str(q.name).c_str(), as_str(d.name).c_str());
+                continue;
+            }
+            if (status == SALN_ENUM_CAP)
+                std::fprintf(stderr, "saln: enumeration capped at %llu blocks for %s vs %s\n",
+                             (unsigned long long)a.max_blocks, as_str(q.name).c_str(),
+                             as_str(d.name).c_str());
+            if (a.timing) {
+                const auto ns = (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+                                    std::chrono::steady_clock::now() - t0)
+                                    .count();
+                std::printf("%s\n", duration_debug(ns).c_str());
+            }
+        }
+    }
+    saln_context_destroy(ctx);
+    return 0;
+}

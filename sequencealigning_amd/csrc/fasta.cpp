@@ -94,8 +94,11 @@ int saln_parse_fasta(const char *path, saln_records **out, uint8_t *bad_chars, u
         return SALN_E_FASTA;
     }
     FILE *f = std::fopen(path, "rb");
+    const int err_no = errno;
     if (!f) {
-        saln::set_error(std::string("Fasta could not be opened with err: ") + std::strerror(errno));
+        // io::Error Display: "<strerror> (os error N)"
+        saln::set_error(std::string("Fasta could not be opened with err: ") + std::strerror(err_no) +
+                        " (os error " + std::to_string(err_no) + ")");
         return SALN_E_FASTA;
     }
     std::vector<uint8_t> data;

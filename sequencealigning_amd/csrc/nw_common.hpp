@@ -22,7 +22,7 @@
 namespace saln {
 
 constexpr int32_t kSentinel = -32768;  // i16::MIN as i32, needleman_wunsch_affine.rs:174
-constexpr int kNumVariants = 7;        // fill kernel variants (nw_kernels.hip)
+constexpr int kNumVariants = 8;        // fill kernel variants (nw_kernels.hip)
 
 struct Scoring {
     int32_t match, mismatch, gap_open, gap_extend;
@@ -47,28 +47,41 @@ struct NwPairDesc {
 };
 
 // Kernel geometry of one fill variant: G lanes per pair, K query columns per
-// lane, KD = ceil(K/4) mask dwords per lane per step.  A pair's query is cut
-// in chunks of W = G*K columns; chunk c's mask is laid out [step][lane][KD
-// dwords], step t holding row r = t - lane + 1 of lane `lane`.
+// lane, KD = ceil(K/4) mask dwords per lane-row segment (LB = 4*KD bytes).
+// A pair's query is cut in chunks of W = G*K columns.  Within a chunk, lane
+// `lane` computes row r = t - lane + 1 at step t (t = 0 .. len_db+G-2).
+// Mask layout (step tiles): [chunk][t / R][lane][t % R][LB bytes].  Each lane
+// buffers R step-segments in registers and a group stores a whole tile
+// (G*R*LB contiguous bytes) at once; a lane block's consecutive rows are
+// adjacent inside a tile, so the traceback walk reuses each fetched line for
+// up to R rows.
+constexpr uint32_t kTileSteps = 4;  // R
+
 struct Geom {
     uint32_t G, K;
     SALN_HD uint32_t KD() const { return (K + 3) / 4; }
+    SALN_HD uint32_t LB() const { return KD() * 4; }
     SALN_HD uint32_t W() const { return G * K; }
-    SALN_HD uint32_t step_bytes() const { return G * KD() * 4; }
     SALN_HD uint32_t n_chunks(uint32_t len_q) const { return (len_q + W() - 1) / W(); }
-    SALN_HD uint64_t chunk_bytes(uint32_t len_db) const {
-        return (uint64_t)(len_db + G - 1) * step_bytes();
+    SALN_HD uint32_t steps(uint32_t len_db) const { return len_db + G - 1; }
+    SALN_HD uint32_t tiles(uint32_t len_db) const {
+        return (steps(len_db) + kTileSteps - 1) / kTileSteps;
     }
+    SALN_HD uint64_t tile_bytes() const { return (uint64_t)G * kTileSteps * LB(); }
+    SALN_HD uint64_t chunk_bytes(uint32_t len_db) const { return tiles(len_db) * tile_bytes(); }
     SALN_HD uint64_t mask_bytes(uint32_t len_q, uint32_t len_db) const {
         return (uint64_t)n_chunks(len_q) * chunk_bytes(len_db);
+    }
+    // segment of (chunk-local) lane `lane` at step t, relative to its chunk
+    SALN_HD uint64_t seg_step(uint32_t lane, uint32_t t) const {
+        return (uint64_t)(t / kTileSteps) * tile_bytes() + (uint64_t)lane * kTileSteps * LB() +
+               (uint64_t)(t % kTileSteps) * LB();
     }
     // byte offset (within the pair's mask) of interior cell (i, j), 1-based.
     SALN_HD uint64_t cell(uint32_t i, uint32_t j, uint32_t len_db) const {
         const uint32_t jj0 = j - 1;
-        const uint32_t c = jj0 / W(), jj = jj0 % W();
-        const uint32_t lane = jj / K, k = jj % K;
-        const uint64_t t = (uint64_t)(i - 1) + lane;
-        return (uint64_t)c * chunk_bytes(len_db) + t * step_bytes() + (uint64_t)lane * KD() * 4 + k;
+        const uint32_t c = jj0 / W(), lane = (jj0 % W()) / K, k = jj0 % K;
+        return (uint64_t)c * chunk_bytes(len_db) + seg_step(lane, i - 1 + lane) + k;
     }
 };
 

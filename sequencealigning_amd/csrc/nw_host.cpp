@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <array>
 #include <cstring>
 #include <map>
@@ -44,6 +45,7 @@ using namespace saln;
 struct saln_context {
     int device = 0;
     hipStream_t stream = nullptr;
+    hipStream_t tb_stream = nullptr;  // traceback stream, overlaps the next fill sub-batch
 };
 
 struct saln_nw_plan {
@@ -54,7 +56,14 @@ struct saln_nw_plan {
     std::vector<uint32_t> plan_index;  // results index -> plan order
     NwPairDesc *d_pairs = nullptr;
     uint32_t var_first[kNumVariants] = {}, var_count[kNumVariants] = {};
+    uint32_t n_fill = 0;  // plan order: [0, n_fill) filled pairs, then empty-side pairs
     uint8_t *d_mask = nullptr;
+    uint8_t *d_mask2 = nullptr;  // second workspace for the async (2-deep) pipeline
+    int32_t *d_endh2 = nullptr;
+    bool async_tb = false;
+    int buf = 0;                           // workspace of the next execute (async mode)
+    bool tb_pending[2] = {false, false};
+    int last_buf = 0;
     uint64_t mask_bytes = 0;
     int2 *d_scratch = nullptr;
     uint64_t scratch_elems = 0;
@@ -64,10 +73,16 @@ struct saln_nw_plan {
     bool timing = false;
     // hipEvents around the fill and traceback launches of each execute;
     // resolved lazily (no host sync inside execute).
-    std::vector<std::array<hipEvent_t, 3>> ev_pool;
+    std::vector<std::array<hipEvent_t, 4>> ev_pool;
     size_t ev_used = 0;
     std::map<std::string, std::pair<double, uint64_t>> ktime;
     int resolve_events();
+    // the two events after the sub-batch events mark "traceback of workspace b done"
+    hipEvent_t tb_done(int b) const { return sync_ev[sync_ev.size() - 2 + b]; }
+    // fill/traceback pipelining: plan-order boundaries of the sub-batches of
+    // [0, n_fill) and one sync event per sub-batch (+1 for the final join)
+    std::vector<uint32_t> sub;
+    std::vector<hipEvent_t> sync_ev;
 };
 
 extern "C" {
@@ -92,7 +107,8 @@ int saln_context_create(int device, saln_context **out) {
     HIP_TRY(hipSetDevice(device));
     auto *c = new saln_context;
     c->device = device;
-    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->tb_stream, hipStreamNonBlocking) != hipSuccess) {
         delete c;
         set_error("hipStreamCreate failed");
         return SALN_E_HIP;
@@ -105,6 +121,7 @@ int saln_context_destroy(saln_context *ctx) {
     if (!ctx) return SALN_OK;
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    if (ctx->tb_stream) (void)hipStreamDestroy(ctx->tb_stream);
     delete ctx;
     return SALN_OK;
 }
@@ -114,8 +131,11 @@ int saln_nw_plan_destroy(saln_nw_plan *p) {
     (void)hipSetDevice(p->ctx->device);
     (void)hipFree(p->d_pairs);
     (void)hipFree(p->d_mask);
+    (void)hipFree(p->d_mask2);
+    (void)hipFree(p->d_endh2);
     (void)hipFree(p->d_scratch);
     (void)hipFree(p->d_endh);
+    for (auto &e : p->sync_ev) (void)hipEventDestroy(e);
     for (auto &t : p->ev_pool)
         for (auto &e : t) (void)hipEventDestroy(e);
     delete p;
@@ -199,8 +219,29 @@ int saln_nw_plan_create(saln_context *ctx, const uint64_t *q_off, uint64_t n_q,
             }
             if (p->var_count[d.variant] == 0) p->var_first[d.variant] = (uint32_t)r;
             p->var_count[d.variant]++;
+            p->n_fill++;
         }
         p->h_pairs[r] = d;
+    }
+    {
+        // sub-batches for fill/traceback overlap inside one execute
+        // (SALN_TB_CHUNKS, default 1); boundaries kept even so packed groups
+        // stay paired
+        uint32_t nsub = 1;
+        if (const char *e = std::getenv("SALN_TB_CHUNKS")) nsub = std::max(1, std::atoi(e));
+        const uint32_t step = ((p->n_fill + nsub - 1) / nsub + 1) & ~1u;
+        p->sub.push_back(0);
+        for (uint32_t b = step; b < p->n_fill; b += step) p->sub.push_back(b);
+        p->sub.push_back(p->n_fill);
+        p->sync_ev.resize(p->sub.size() + 1);
+        for (auto &e : p->sync_ev) {
+            if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
+                e = nullptr;
+                set_error("hipEventCreate");
+                saln_nw_plan_destroy(p);
+                return SALN_E_HIP;
+            }
+        }
     }
     p->plan_index.resize(n_pairs);
     for (uint64_t r = 0; r < n_pairs; ++r) p->plan_index[p->h_pairs[r].pair_id] = (uint32_t)r;
@@ -221,7 +262,8 @@ int saln_nw_plan_create(saln_context *ctx, const uint64_t *q_off, uint64_t n_q,
         if ((e = hipMalloc(&p->d_endh, n_pairs * sizeof(int32_t))) != hipSuccess)
             return fail(e, "hipMalloc(end)");
     }
-    if (moff && (e = hipMalloc(&p->d_mask, moff)) != hipSuccess)
+    // +64 B: the traceback walker reads whole 5-dword segments
+    if (moff && (e = hipMalloc(&p->d_mask, moff + 64)) != hipSuccess)
         return fail(e, "hipMalloc(mask workspace)");
     if (soff && (e = hipMalloc(&p->d_scratch, soff * sizeof(int2))) != hipSuccess)
         return fail(e, "hipMalloc(scratch)");
@@ -273,23 +315,84 @@ int saln_nw_execute(saln_nw_plan *p, const uint8_t *d_q, const uint8_t *d_db,
     if (p->n_pairs == 0) return SALN_OK;
     HIP_TRY(hipSetDevice(p->ctx->device));
     hipStream_t s = stream ? (hipStream_t)stream : p->ctx->stream;
+    hipStream_t t = p->ctx->tb_stream;
+    const int cur = p->async_tb ? p->buf : 0;
+    uint8_t *mask = cur ? p->d_mask2 : p->d_mask;
+    int32_t *endh = cur ? p->d_endh2 : p->d_endh;
+    // this workspace may still be read by the traceback of execute n-2
+    if (p->tb_pending[cur]) HIP_TRY(hipStreamWaitEvent(s, p->tb_done(cur), 0));
     hipEvent_t *ev = nullptr;
     if (p->timing) {
         if (p->ev_used == p->ev_pool.size()) {
-            std::array<hipEvent_t, 3> t{};
-            for (auto &e : t) HIP_TRY(hipEventCreate(&e));
-            p->ev_pool.push_back(t);
+            std::array<hipEvent_t, 4> e4{};
+            for (auto &e : e4) HIP_TRY(hipEventCreate(&e));
+            p->ev_pool.push_back(e4);
         }
         ev = p->ev_pool[p->ev_used++].data();
         HIP_TRY(hipEventRecord(ev[0], s));
     }
-    for (int v = 0; v < kNumVariants; ++v)
-        HIP_TRY(launch_fill(v, p->d_pairs, p->var_first[v], p->var_count[v], d_q, d_db, p->d_mask,
-                            p->d_scratch, p->d_endh, p->sc, s));
-    if (ev) HIP_TRY(hipEventRecord(ev[1], s));
-    HIP_TRY(launch_traceback(p->d_pairs, (uint32_t)p->n_pairs, d_q, d_db, p->d_mask, p->d_endh,
-                             d_results, d_cigar, p->sc, s));
-    if (ev) HIP_TRY(hipEventRecord(ev[2], s));
+    // Sub-batch k: fill on `s`, then its traceback on the context's second
+    // stream; the (latency-bound) traceback overlaps the next fill.
+    const size_t nsub = p->sub.size() - 1;  // >= 1 (an empty sub-batch if n_fill == 0)
+    for (size_t k = 0; k < nsub; ++k) {
+        const uint32_t lo = p->sub[k], hi = p->sub[k + 1];
+        for (int v = 0; v < kNumVariants; ++v) {
+            const uint32_t a = std::max(lo, p->var_first[v]);
+            const uint32_t b = std::min(hi, p->var_first[v] + p->var_count[v]);
+            if (a < b)
+                HIP_TRY(launch_fill(v, p->d_pairs, a, b - a, d_q, d_db, mask, p->d_scratch, endh,
+                                    d_results, d_cigar, p->sc, s));
+        }
+        if (ev && k + 1 == nsub) HIP_TRY(hipEventRecord(ev[1], s));
+        HIP_TRY(hipEventRecord(p->sync_ev[k], s));
+        HIP_TRY(hipStreamWaitEvent(t, p->sync_ev[k], 0));
+        if (ev && k == 0) HIP_TRY(hipEventRecord(ev[2], t));
+        for (int v = 0; v < kNumVariants; ++v) {
+            const uint32_t a = std::max(lo, p->var_first[v]);
+            const uint32_t b = std::min(hi, p->var_first[v] + p->var_count[v]);
+            if (a < b)
+                HIP_TRY(launch_traceback(v, p->d_pairs, a, b - a, d_q, d_db, mask, endh,
+                                         d_results, d_cigar, p->sc, t));
+        }
+    }
+    // pairs with an empty side (boundary-only walk) ride on the traceback stream
+    if (p->n_pairs > p->n_fill)
+        HIP_TRY(launch_traceback(-1, p->d_pairs, p->n_fill, (uint32_t)(p->n_pairs - p->n_fill),
+                                 d_q, d_db, mask, endh, d_results, d_cigar, p->sc, t));
+    if (ev) HIP_TRY(hipEventRecord(ev[3], t));
+    HIP_TRY(hipEventRecord(p->tb_done(cur), t));
+    p->tb_pending[cur] = true;
+    p->last_buf = cur;
+    if (p->async_tb) {
+        p->buf ^= 1;  // results complete once saln_nw_plan_sync'ed
+    } else {
+        HIP_TRY(hipStreamWaitEvent(s, p->tb_done(cur), 0));
+        p->tb_pending[cur] = false;
+    }
+    return SALN_OK;
+}
+
+int saln_nw_plan_set_async(saln_nw_plan *p, int enable) {
+    if (!p) return SALN_E_INVALID;
+    HIP_TRY(hipSetDevice(p->ctx->device));
+    if (enable && !p->d_mask2 && p->mask_bytes) {
+        HIP_TRY(hipMalloc(&p->d_mask2, p->mask_bytes + 64));
+        HIP_TRY(hipMalloc(&p->d_endh2, p->n_pairs * sizeof(int32_t)));
+    }
+    p->async_tb = enable != 0;
+    p->buf = 0;
+    return SALN_OK;
+}
+
+int saln_nw_plan_sync(saln_nw_plan *p, void *stream, int keep_latest) {
+    if (!p) return SALN_E_INVALID;
+    HIP_TRY(hipSetDevice(p->ctx->device));
+    hipStream_t s = stream ? (hipStream_t)stream : p->ctx->stream;
+    for (int b = 0; b < 2; ++b) {
+        if (!p->tb_pending[b] || (keep_latest && b == p->last_buf)) continue;
+        HIP_TRY(hipStreamWaitEvent(s, p->tb_done(b), 0));
+        p->tb_pending[b] = false;
+    }
     return SALN_OK;
 }
 
@@ -299,16 +402,20 @@ int saln_nw_plan::resolve_events() {
     HIP_TRY(hipSetDevice(ctx->device));
     for (size_t k = 0; k < ev_used; ++k) {
         hipEvent_t *ev = ev_pool[k].data();
-        HIP_TRY(hipEventSynchronize(ev[2]));
-        float a = 0, b = 0;
-        HIP_TRY(hipEventElapsedTime(&a, ev[0], ev[1]));
-        HIP_TRY(hipEventElapsedTime(&b, ev[1], ev[2]));
+        HIP_TRY(hipEventSynchronize(ev[3]));
+        float a = 0, b = 0, c = 0;
+        HIP_TRY(hipEventElapsedTime(&a, ev[0], ev[1]));  // fill span on the caller's stream
+        HIP_TRY(hipEventElapsedTime(&b, ev[2], ev[3]));  // traceback span on its stream
+        HIP_TRY(hipEventElapsedTime(&c, ev[0], ev[3]));  // whole execute
         auto &f = ktime["nw_fill"];
         f.first += a;
         f.second += 1;
         auto &t = ktime["nw_traceback"];
         t.first += b;
         t.second += 1;
+        auto &x = ktime["nw_execute"];
+        x.first += c;
+        x.second += 1;
     }
     ev_used = 0;
     return SALN_OK;

@@ -14,8 +14,10 @@ namespace saln {
 // kernels (nw_kernels.hip)
 hipError_t launch_fill(int variant, const NwPairDesc *pairs, uint32_t first, uint32_t count,
                        const uint8_t *qs, const uint8_t *ds, uint8_t *mask, int2 *scratch,
-                       int32_t *end_h, Scoring sc, hipStream_t stream);
-hipError_t launch_traceback(const NwPairDesc *pairs, uint32_t n, const uint8_t *qs,
+                       int32_t *end_h, saln_nw_result *results, uint32_t *cigar, Scoring sc,
+                       hipStream_t stream);
+hipError_t launch_traceback(int variant, const NwPairDesc *pairs, uint32_t first, uint32_t n,
+                            const uint8_t *qs,
                             const uint8_t *ds, const uint8_t *mask, const int32_t *end_h,
                             saln_nw_result *results, uint32_t *cigar, Scoring sc,
                             hipStream_t stream);

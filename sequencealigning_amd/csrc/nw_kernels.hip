@@ -35,6 +35,524 @@ __device__ __forceinline__ int32_t shr1(int32_t old, int32_t v) {
         return __builtin_amdgcn_update_dpp(old, v, 0x138 /*wave_shr:1*/, 0xf, 0xf, false);
 }
 
+// --------------------------------------------------------------- traceback
+struct GeomTable {
+    Geom g[kNumVariants];
+};
+
+struct MaskCell {
+    const uint8_t *m;
+    Geom g;
+    uint32_t lq, ld;
+    Scoring sc;
+    // codes are stored inverted (bit set = parent absent)
+    __device__ uint8_t byte(uint32_t i, uint32_t j) const { return m[g.cell(i, j, ld)] ^ 0x7F; }
+    __device__ uint8_t argmax(uint32_t i, uint32_t j) const {
+        if (i == 0) return argmax_row0(sc, j);
+        if (j == 0) return argmax_col0(sc, i);
+        return byte(i, j) & 7;
+    }
+    __device__ uint8_t ibits(uint32_t i, uint32_t j) const {  // i, j >= 1
+        return j == 1 ? ibits_col1(sc, i) : (byte(i, j - 1) >> 3) & 3;
+    }
+    __device__ uint8_t dbits(uint32_t i, uint32_t j) const {  // i, j >= 1
+        return i == 1 ? dbits_row1(sc, j) : (byte(i - 1, j) >> 5) & 3;
+    }
+};
+
+enum { kStM = 0, kStI = 1, kStD = 2 };
+enum { kEvOrigin = 0, kEvPanic = 1, kEvDead = 2 };
+
+// Canonical (first printed) alignment: the reference DFS pops end states in
+// the order D, M, I (:251-280 push I, M, D) and parents in reverse push order
+// (M: D>I>M; I: open>extend; D: open>extend).  While no sentinel cell is
+// reachable every DFS path ends at the origin or at a boundary panic node,
+// so the first path is this greedy walk.  A sentinel dead end (only possible
+// once len_q+len_db >~ 5,450) sets flags bit0 and the host redoes the walk
+// with backtracking.
+__device__ __forceinline__ void walk_pair(const NwPairDesc &p, int32_t hend,
+                                       const uint8_t *__restrict__ qs,
+                                       const uint8_t *__restrict__ ds,
+                                       const uint8_t *__restrict__ mask, Geom geo,
+                                       saln_nw_result *__restrict__ results,
+                                       uint32_t *__restrict__ cigar, Scoring sc) {
+    const uint32_t lq = p.len_q, ld = p.len_db;
+    const uint8_t *q = qs + p.q_off;
+    const uint8_t *d = ds + p.db_off;
+    const MaskCell mc{mask + p.mask_off, geo, lq, ld, sc};
+    const uint8_t am_end = mc.argmax(ld, lq);
+    int st = (am_end & kArgD) ? kStD : ((am_end & kArgM) ? kStM : kStI);
+    uint32_t i = ld, j = lq;
+    uint32_t *out = cigar ? cigar + p.cigar_off : nullptr;
+    uint32_t nops = 0, run_op = 0, run_len = 0;
+    int ev;
+    for (;;) {
+        uint32_t op;
+        if (st == kStM) {
+            if (i == 0 && j == 0) { ev = kEvOrigin; break; }
+            if (i == 0 || j == 0) { ev = kEvDead; break; }
+            op = q[j - 1] == d[i - 1] ? SALN_CIGAR_EQ : SALN_CIGAR_X;
+            const uint8_t a = mc.argmax(i - 1, j - 1);
+            --i;
+            --j;
+            st = (a & kArgD) ? kStD : ((a & kArgI) ? kStI : kStM);
+        } else if (st == kStI) {
+            if (j == 0) { ev = i >= 1 ? kEvPanic : kEvDead; break; }
+            if (i == 0) { ev = kEvDead; break; }
+            op = SALN_CIGAR_I;
+            const uint8_t b = mc.ibits(i, j);
+            --j;
+            st = (b & 2) ? kStM : kStI;
+        } else {
+            if (i == 0) { ev = j >= 1 ? kEvPanic : kEvDead; break; }
+            if (j == 0) { ev = kEvDead; break; }
+            op = SALN_CIGAR_D;
+            const uint8_t b = mc.dbits(i, j);
+            --i;
+            st = (b & 2) ? kStM : kStD;
+        }
+        if (op == run_op && run_len) {
+            ++run_len;
+        } else {
+            if (run_len && out) out[nops] = (run_len << 4) | run_op;
+            nops += run_len ? 1 : 0;
+            run_op = op;
+            run_len = 1;
+        }
+    }
+    if (run_len) {
+        if (out) out[nops] = (run_len << 4) | run_op;
+        ++nops;
+    }
+    if (ev != kEvOrigin) nops = 0;
+    if (out) {  // ops were produced back to front
+        for (uint32_t a = 0, b = nops ? nops - 1 : 0; a < b; ++a, --b) {
+            const uint32_t tmp = out[a];
+            out[a] = out[b];
+            out[b] = tmp;
+        }
+    }
+    saln_nw_result r;
+    r.score = hend >> 1;
+    r.status = (hend & 1) ? SALN_REF_PANIC_BOUNDARY : SALN_OK;
+    r.cigar_len = nops;
+    r.end_states = am_end;
+    r.printed = ev == kEvOrigin ? 1 : 0;
+    r.flags = (ev == kEvDead ? 1 : 0) | ((ev == kEvPanic && !(hend & 1)) ? 2 : 0);
+    r.reserved = 0;
+    results[p.pair_id] = r;
+}
+
+// Streaming walker.  The mask of a pair is laid out [step][lane][KD dwords]
+// (nw_common.hpp Geom): the K columns of lane block L at row i are one
+// KD-dword segment at step i-1+L.  Walking back from the end cell the row
+// only decreases, so within a lane block the walker keeps a window of kWin
+// row segments in flight (slot s of a round holds row base-s) and refills a
+// slot as soon as the path leaves its row; a block change restarts the
+// window.  Every decision reads one byte of the cell the walk moves into:
+// bits 0-2 choose the state after a diagonal move (D > I > M), bits 3-4
+// (I parents) after a horizontal one, bits 5-6 (D parents) after a vertical
+// one, and bit 7 (query char == db char) names the M column '=' or 'X'.
+constexpr int kWin = 8;
+enum { kFromM = 0, kFromI = 1, kFromD = 2, kFromEnd = 3 };
+
+// named fields (not an array) so the dword select below stays in registers
+struct Seg {
+    uint32_t w0, w1, w2, w3, w4;
+};
+
+__device__ __forceinline__ Seg load_seg(const uint8_t *__restrict__ m, uint64_t off) {
+    const uint32_t *p = reinterpret_cast<const uint32_t *>(m + off);
+    return Seg{p[0], p[1], p[2], p[3], p[4]};
+}
+
+__device__ __forceinline__ uint32_t seg_byte(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3,
+                                             uint32_t w4, uint32_t k) {
+    const uint32_t d = k >> 2;
+    uint32_t w = d == 0 ? w0 : w1;
+    w = d >= 2 ? w2 : w;
+    w = d >= 3 ? w3 : w;
+    w = d >= 4 ? w4 : w;
+    return ((w >> (8 * (k & 3))) & 0xFFu) ^ 0x7Fu;  // decoded: bit set = parent present
+}
+
+__device__ __forceinline__ int next_state(int from, uint32_t b) {
+    switch (from) {
+        case kFromM: return (b & kArgD) ? kStD : ((b & kArgI) ? kStI : kStM);
+        case kFromI: return (b & kIOpen) ? kStM : kStI;
+        case kFromD: return (b & kDOpen) ? kStM : kStD;
+        default: return (b & kArgD) ? kStD : ((b & kArgM) ? kStM : kStI);
+    }
+}
+
+__device__ void walk_pair_stream(const NwPairDesc &p, int32_t hend,
+                                 const uint8_t *__restrict__ mask, Geom geo,
+                                 saln_nw_result *__restrict__ results,
+                                 uint32_t *__restrict__ cigar, Scoring sc) {
+    // Lock-step walker: every lane of the wave is in the same window phase S
+    // (0..kWin-1) with its target row == base - S; the phases are unrolled so
+    // each window slot is a fixed register set.  A lane whose walk changes
+    // column block re-bases its window (base = target row + S) to stay in
+    // phase.  Loads are unconditional (row clamped into the pair): a select on
+    // a loaded value would make the compiler wait for it on the spot.
+    const uint32_t K = geo.K, G = geo.G;
+    const uint64_t cb = geo.chunk_bytes(p.len_db);
+    const uint8_t *__restrict__ m = mask + p.mask_off;
+    uint32_t *out = cigar ? cigar + p.cigar_off : nullptr;
+    uint32_t nops = 0, run_op = 0, run_len = 0;
+    uint32_t ti = p.len_db, tj = p.len_q;  // target cell
+    int from = kFromEnd;                    // how the walk arrives at the target
+    uint8_t am_end = 0;
+    bool walking = true;
+    uint32_t B = (tj - 1) / K, L = B % G, base = ti;
+    const uint8_t *__restrict__ mc = m + (uint64_t)(B / G) * cb;
+    const int32_t ldi = (int32_t)p.len_db;
+    Seg w0, w1, w2, w3, w4, w5, w6, w7;
+#define SALN_ROW(S2, S) ((int32_t)((S2) >= (S) ? base - (S2) : base - (S2) - kWin))
+#define SALN_LOAD(W, ROW) \
+    W = load_seg(mc, geo.seg_step(L, (uint32_t)min(max((int32_t)(ROW), 1), ldi) - 1 + L))
+#define SALN_PHASE(W, S)                                                                    \
+    while (walking) {                                                                       \
+        if ((tj - 1) / K != B) { /* block change: re-base the window into phase S */        \
+            B = (tj - 1) / K;                                                               \
+            L = B % G;                                                                      \
+            mc = m + (uint64_t)(B / G) * cb;                                                \
+            base = ti + (S);                                                                \
+            SALN_LOAD(w0, SALN_ROW(0, S)); SALN_LOAD(w1, SALN_ROW(1, S));                   \
+            SALN_LOAD(w2, SALN_ROW(2, S)); SALN_LOAD(w3, SALN_ROW(3, S));                   \
+            SALN_LOAD(w4, SALN_ROW(4, S)); SALN_LOAD(w5, SALN_ROW(5, S));                   \
+            SALN_LOAD(w6, SALN_ROW(6, S)); SALN_LOAD(w7, SALN_ROW(7, S));                   \
+        }                                                                                   \
+        const uint32_t b = seg_byte(W.w0, W.w1, W.w2, W.w3, W.w4, tj - 1 - B * K);          \
+        if (from == kFromEnd) am_end = (uint8_t)(b & 7);                                    \
+        const int st = next_state(from, b);                                                 \
+        const uint32_t op = st == kStI   ? SALN_CIGAR_I                                     \
+                            : st == kStD ? SALN_CIGAR_D                                     \
+                                         : ((b & 0x80u) ? SALN_CIGAR_EQ : SALN_CIGAR_X);     \
+        const bool brk = run_len != 0 && op != run_op;                                      \
+        if (brk && out) out[nops] = (run_len << 4) | run_op;                                \
+        nops += brk ? 1u : 0u;                                                              \
+        run_len = brk || run_len == 0 ? 1u : run_len + 1u;                                  \
+        run_op = op;                                                                        \
+        const uint32_t i0 = ti;                                                             \
+        ti -= st != kStI ? 1u : 0u;                                                         \
+        tj -= st != kStD ? 1u : 0u;                                                         \
+        from = st; /* kFromM/I/D == kStM/I/D */                                             \
+        if (ti == 0 || tj == 0) walking = false;                                            \
+        else if (ti != i0 && (tj - 1) / K == B) break; /* up one row: next phase */         \
+    }                                                                                       \
+    if (walking) SALN_LOAD(W, base - (S) - kWin);
+    SALN_LOAD(w0, SALN_ROW(0, 0)); SALN_LOAD(w1, SALN_ROW(1, 0));
+    SALN_LOAD(w2, SALN_ROW(2, 0)); SALN_LOAD(w3, SALN_ROW(3, 0));
+    SALN_LOAD(w4, SALN_ROW(4, 0)); SALN_LOAD(w5, SALN_ROW(5, 0));
+    SALN_LOAD(w6, SALN_ROW(6, 0)); SALN_LOAD(w7, SALN_ROW(7, 0));
+    while (walking) {
+        SALN_PHASE(w0, 0)
+        SALN_PHASE(w1, 1)
+        SALN_PHASE(w2, 2)
+        SALN_PHASE(w3, 3)
+        SALN_PHASE(w4, 4)
+        SALN_PHASE(w5, 5)
+        SALN_PHASE(w6, 6)
+        SALN_PHASE(w7, 7)
+        base -= kWin;
+    }
+#undef SALN_PHASE
+#undef SALN_LOAD
+#undef SALN_ROW
+    // boundary arrival at (ti, tj) (row or column 0) from state `from`
+    int ev, bst;
+    if (from == kFromM && ti == 0 && tj == 0) {
+        ev = kEvOrigin;
+    } else {
+        if (from == kFromM) {
+            const uint8_t a = ti == 0 ? argmax_row0(sc, tj) : argmax_col0(sc, ti);
+            bst = (a & kArgD) ? kStD : ((a & kArgI) ? kStI : kStM);
+        } else if (from == kFromI) {  // (ti, 0), ti >= 1
+            bst = (ibits_col1(sc, ti) & 2) ? kStM : kStI;
+        } else {  // kFromD: (0, tj), tj >= 1
+            bst = (dbits_row1(sc, tj) & 2) ? kStM : kStD;
+        }
+        // expanding a boundary node: D[0][j>=1] / I[i>=1][0] panic; other
+        // non-origin boundary nodes are parentless sentinels (dead ends)
+        if (bst == kStD && ti == 0 && tj >= 1) ev = kEvPanic;
+        else if (bst == kStI && tj == 0 && ti >= 1) ev = kEvPanic;
+        else ev = kEvDead;
+    }
+    if (run_len) {
+        if (out) out[nops] = (run_len << 4) | run_op;
+        ++nops;
+    }
+    if (ev != kEvOrigin) nops = 0;
+    if (out) {
+        for (uint32_t a = 0, b = nops ? nops - 1 : 0; a < b; ++a, --b) {
+            const uint32_t tmp = out[a];
+            out[a] = out[b];
+            out[b] = tmp;
+        }
+    }
+    saln_nw_result r;
+    r.score = hend >> 1;
+    r.status = (hend & 1) ? SALN_REF_PANIC_BOUNDARY : SALN_OK;
+    r.cigar_len = nops;
+    r.end_states = am_end;
+    r.printed = ev == kEvOrigin ? 1 : 0;
+    r.flags = (ev == kEvDead ? 1 : 0) | ((ev == kEvPanic && !(hend & 1)) ? 2 : 0);
+    r.reserved = 0;
+    results[p.pair_id] = r;
+}
+
+// LDS-window walker (segments of <= 16 bytes, i.e. K <= 16).  Lock-step
+// phases as in walk_pair_stream (every lane in phase S, target row base-S),
+// but the windows live in LDS, filled by LDS-DMA (global_load_lds_dwordx4:
+// lane l's 16 bytes land at slot base + 16*l; the slot base is wave-uniform
+// because all lanes are in the same phase).  There are two windows, one for
+// even and one for odd column blocks; at the end of phase S every lane
+// refills slot S of both with row base-S-kWin of the blocks {B, B-1} (B = its
+// current block), so when the walk crosses into block B-1 the data is
+// already resident.  valid[] bits track which slots of each window hold the
+// block currently assigned to it; a crossing that comes back faster than the
+// refills falls back to a synchronous load.  Exactly two DMAs per phase keep
+// >= 2*kWin-2 younger VMEM operations behind any slot a phase reads, so the
+// read waits with vmcnt(14) in the same asm statement (the compiler cannot
+// hoist it or turn it into a conservative vmcnt(0)).
+constexpr uint32_t kSlotBytes = 64 * 16;                 // one slot of a wave
+constexpr uint32_t kWinBytes = kWin * kSlotBytes;        // one window of a wave
+constexpr uint32_t kWaveLds = 2 * kWinBytes;             // even + odd window: 16 KiB
+typedef __attribute__((address_space(3))) uint8_t lds_u8;
+
+__device__ __forceinline__ uint32_t lds_off(const lds_u8 *p) { return (uint32_t)(uintptr_t)p; }
+
+__device__ __forceinline__ uint32_t window_byte(uint32_t addr) {
+    uint32_t v;
+    asm volatile("s_waitcnt vmcnt(14)\n\tds_read_u8 %0, %1\n\ts_waitcnt lgkmcnt(0)"
+                 : "=v"(v) : "v"(addr) : "memory");
+    static_assert(kWin == 8, "vmcnt(14) above is 2*kWin - 2");
+    return v ^ 0x7Fu;  // decoded: bit set = parent present
+}
+
+__device__ __forceinline__ uint32_t window_byte_sync(uint32_t addr) {
+    uint32_t v;
+    asm volatile("s_waitcnt vmcnt(0)\n\tds_read_u8 %0, %1\n\ts_waitcnt lgkmcnt(0)"
+                 : "=v"(v) : "v"(addr) : "memory");
+    return v ^ 0x7Fu;
+}
+
+#ifdef SALN_WALK_CHECK
+// debug build: compare every window read with the byte in HBM
+#define SALN_WALK_CHECK_HOOK(S)                                                          \
+    {                                                                                    \
+        const uint32_t tru = (uint32_t)m[geo.cell(ti, tj, p.len_db)] ^ 0x7Fu;            \
+        if (tru != b) {                                                                  \
+            if (!dbg_n) dbg_info = (S) | (par << 3) | (((valid >> (par * 8u + (S))) & 1u) << 4) | \
+                                   ((ti & 0xFFFu) << 8) | ((tj & 0xFFFu) << 20);          \
+            ++dbg_n;                                                                     \
+            b = tru;                                                                     \
+        }                                                                                \
+    }
+#else
+#define SALN_WALK_CHECK_HOOK(S)
+#endif
+
+template <int G, int K>
+__device__ void walk_pair_lds(const NwPairDesc &p, int32_t hend, const uint8_t *__restrict__ mask,
+                              saln_nw_result *__restrict__ results,
+                              uint32_t *__restrict__ cigar, Scoring sc, lds_u8 *win) {
+    constexpr Geom geo{G, K};
+    constexpr uint32_t LB = (K + 3) / 4 * 4;
+    constexpr uint32_t TB = G * kTileSteps * LB;  // tile bytes
+    static_assert(LB <= 16, "LDS window slots hold 16 bytes per lane");
+    const uint64_t cb = geo.chunk_bytes(p.len_db);
+    const uint8_t *__restrict__ m = mask + p.mask_off;
+    uint32_t *out = cigar ? cigar + p.cigar_off : nullptr;
+    uint32_t nops = 0, run_op = 0, run_len = 0;
+    uint32_t ti = p.len_db, tj = p.len_q;
+    int from = kFromEnd;
+    uint8_t am_end = 0;
+    bool walking = true;
+    uint32_t B = (tj - 1) / K, base = ti;
+    uint32_t col = (tj - 1) % K;  // target column inside block B
+    uint32_t valid = 0xFFFFu;     // bits 0-7: even window slots, 8-15: odd window slots
+    const uint32_t lane16 = (threadIdx.x & 63u) * 16u;
+    const uint32_t wbase = lds_off(win);
+#ifdef SALN_WALK_CHECK
+    uint32_t dbg_n = 0, dbg_info = 0;
+#endif
+    // per-block segment base (chunk + lane offset) and lane index, for B and B-1
+    auto blk_base = [&](uint32_t blk) __attribute__((always_inline)) {
+        return m + (uint64_t)(blk / G) * cb + (blk % G) * (kTileSteps * LB);
+    };
+    const uint8_t *bp_cur = blk_base(B), *bp_prv = blk_base(B ? B - 1 : 0);
+    uint32_t L_cur = B % G, L_prv = (B ? B - 1 : 0) % G;
+    // global address of a segment at `row` (clamped to >= 1) given block base/lane
+    auto seg = [&](const uint8_t *bp, uint32_t L, int32_t row) __attribute__((always_inline)) {
+        const uint32_t t = (uint32_t)max(row, 1) - 1 + L;
+        return (const void *)(bp + (uint64_t)(t / kTileSteps) * TB + (t % kTileSteps) * LB);
+    };
+#define SALN_ROW(S2, S) ((int32_t)((S2) >= (S) ? base - (S2) : base - (S2) - kWin))
+#define SALN_DMA(WIN, SLOT, ADDR)                                                              \
+    __builtin_amdgcn_global_load_lds(                                                          \
+        ADDR, (__attribute__((address_space(3))) void *)(win + (WIN) * kWinBytes +             \
+                                                         (SLOT) * kSlotBytes),                 \
+        16, 0, 0)
+    // even / odd windows hold {B, B-1}
+#define SALN_REFILL(S, ROW)                                                                    \
+    {                                                                                          \
+        const void *ac = seg(bp_cur, L_cur, ROW), *ap = seg(bp_prv, L_prv, ROW);               \
+        const bool odd = (B & 1u) != 0;                                                        \
+        SALN_DMA(0, S, odd ? ap : ac);                                                         \
+        SALN_DMA(1, S, odd ? ac : ap);                                                         \
+    }
+#define SALN_PHASE(S)                                                                          \
+    while (walking) {                                                                          \
+        const uint32_t par = B & 1u;                                                           \
+        const uint32_t addr = wbase + par * kWinBytes + (S) * kSlotBytes + lane16 + col;       \
+        uint32_t b;                                                                            \
+        if (valid & (1u << (par * 8u + (S)))) {                                                \
+            b = window_byte(addr);                                                             \
+        } else { /* window not refreshed since the last crossing: load this slot now */        \
+            /* two independent ifs (not if/else): the compiler must not merge the   */         \
+            /* calls into one DMA with a per-lane (then readfirstlane'd) LDS base    */         \
+            const void *ac = seg(bp_cur, L_cur, (int32_t)(base - (S)));                        \
+            if (par == 0) { SALN_DMA(0, S, ac); }                                              \
+            __builtin_amdgcn_sched_barrier(0);                                                 \
+            if (par == 1) { SALN_DMA(1, S, ac); }                                              \
+            b = window_byte_sync(addr);                                                        \
+            valid |= 1u << (par * 8u + (S));                                                   \
+        }                                                                                      \
+        SALN_WALK_CHECK_HOOK(S)                                                                \
+        if (from == kFromEnd) am_end = (uint8_t)(b & 7);                                       \
+        const int st = next_state(from, b);                                                    \
+        const uint32_t op = st == kStI   ? SALN_CIGAR_I                                        \
+                            : st == kStD ? SALN_CIGAR_D                                        \
+                                         : ((b & 0x80u) ? SALN_CIGAR_EQ : SALN_CIGAR_X);        \
+        const bool brk = run_len != 0 && op != run_op;                                         \
+        if (brk && out) out[nops] = (run_len << 4) | run_op;                                   \
+        nops += brk ? 1u : 0u;                                                                 \
+        run_len = brk || run_len == 0 ? 1u : run_len + 1u;                                     \
+        run_op = op;                                                                           \
+        const bool up = st != kStI, left = st != kStD;                                         \
+        ti -= up ? 1u : 0u;                                                                    \
+        tj -= left ? 1u : 0u;                                                                  \
+        from = st;                                                                             \
+        if (ti == 0 || tj == 0) { walking = false; break; }                                    \
+        if (left) {                                                                            \
+            if (col == 0) { /* crossed into B-1: its window now gets B-2 */                    \
+                valid &= par ? 0x00FFu : 0xFF00u;                                              \
+                --B;                                                                           \
+                col = K - 1;                                                                   \
+                bp_cur = bp_prv;                                                               \
+                L_cur = L_prv;                                                                 \
+                bp_prv = blk_base(B ? B - 1 : 0);                                              \
+                L_prv = (B ? B - 1 : 0) % G;                                                   \
+            } else {                                                                           \
+                --col;                                                                         \
+            }                                                                                  \
+        }                                                                                      \
+        if (up) break; /* up one row: next phase */                                            \
+    }                                                                                          \
+    /* exactly two DMAs per phase for every lane of the wave */                                \
+    SALN_REFILL(S, (int32_t)(base - (S) - kWin))                                               \
+    valid |= 0x101u << (S);
+#define SALN_INIT(S2) SALN_REFILL(S2, SALN_ROW(S2, 0))
+    SALN_INIT(0) SALN_INIT(1) SALN_INIT(2) SALN_INIT(3)
+    SALN_INIT(4) SALN_INIT(5) SALN_INIT(6) SALN_INIT(7)
+    while (walking) {
+        SALN_PHASE(0)
+        SALN_PHASE(1)
+        SALN_PHASE(2)
+        SALN_PHASE(3)
+        SALN_PHASE(4)
+        SALN_PHASE(5)
+        SALN_PHASE(6)
+        SALN_PHASE(7)
+        base -= kWin;
+    }
+#undef SALN_INIT
+#undef SALN_PHASE
+#undef SALN_REFILL
+#undef SALN_DMA
+#undef SALN_ROW
+    int ev, bst;
+    if (from == kFromM && ti == 0 && tj == 0) {
+        ev = kEvOrigin;
+    } else {
+        if (from == kFromM) {
+            const uint8_t a = ti == 0 ? argmax_row0(sc, tj) : argmax_col0(sc, ti);
+            bst = (a & kArgD) ? kStD : ((a & kArgI) ? kStI : kStM);
+        } else if (from == kFromI) {
+            bst = (ibits_col1(sc, ti) & 2) ? kStM : kStI;
+        } else {
+            bst = (dbits_row1(sc, tj) & 2) ? kStM : kStD;
+        }
+        if (bst == kStD && ti == 0 && tj >= 1) ev = kEvPanic;
+        else if (bst == kStI && tj == 0 && ti >= 1) ev = kEvPanic;
+        else ev = kEvDead;
+    }
+    if (run_len) {
+        if (out) out[nops] = (run_len << 4) | run_op;
+        ++nops;
+    }
+    if (ev != kEvOrigin) nops = 0;
+    if (out) {
+        for (uint32_t a2 = 0, b2 = nops ? nops - 1 : 0; a2 < b2; ++a2, --b2) {
+            const uint32_t tmp = out[a2];
+            out[a2] = out[b2];
+            out[b2] = tmp;
+        }
+    }
+    saln_nw_result r;
+    r.score = hend >> 1;
+    r.status = (hend & 1) ? SALN_REF_PANIC_BOUNDARY : SALN_OK;
+    r.cigar_len = nops;
+    r.end_states = am_end;
+    r.printed = ev == kEvOrigin ? 1 : 0;
+    r.flags = (ev == kEvDead ? 1 : 0) | ((ev == kEvPanic && !(hend & 1)) ? 2 : 0);
+    r.reserved = 0;
+#ifdef SALN_WALK_CHECK
+    if (dbg_n) {
+        r.flags |= 4;
+        r.reserved = (uint8_t)(dbg_n > 255 ? 255 : dbg_n);
+        r.cigar_len = dbg_info;
+    }
+#endif
+    results[p.pair_id] = r;
+}
+
+// Per-variant traceback for filled pairs whose segments fit an LDS slot.
+template <int G, int K>
+__global__ __launch_bounds__(256) void nw_traceback_lds_kernel(
+    const NwPairDesc *__restrict__ pairs, uint32_t first, uint32_t n,
+    const uint8_t *__restrict__ mask, const int32_t *__restrict__ end_h,
+    saln_nw_result *__restrict__ results, uint32_t *__restrict__ cigar, Scoring sc) {
+    __shared__ __attribute__((aligned(16))) uint8_t win_all[4 * kWaveLds];
+    const uint32_t idx = first + blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= first + n) return;
+    const NwPairDesc p = pairs[idx];
+    walk_pair_lds<G, K>(p, end_h[idx], mask, results, cigar, sc,
+                        (lds_u8 *)(win_all + (threadIdx.x / 64u) * kWaveLds));
+}
+
+// One walker per pair.  Pairs with an empty side have no mask and take the
+// boundary-only walk.
+__global__ __launch_bounds__(256) void nw_traceback_kernel(
+    const NwPairDesc *__restrict__ pairs, uint32_t first, uint32_t n,
+    const uint8_t *__restrict__ qs, const uint8_t *__restrict__ ds,
+    const uint8_t *__restrict__ mask, const int32_t *__restrict__ end_h,
+    saln_nw_result *__restrict__ results, uint32_t *__restrict__ cigar, Scoring sc,
+    GeomTable gt) {
+    const uint32_t idx = first + blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= first + n) return;
+    const NwPairDesc p = pairs[idx];
+    const Geom geo = gt.g[p.variant];
+    if (p.len_q && p.len_db) {
+        walk_pair_stream(p, end_h[idx], mask, geo, results, cigar, sc);
+    } else {
+        walk_pair(p, hs_boundary_end(sc, p.len_q, p.len_db), qs, ds, mask, geo, results, cigar,
+                  sc);
+    }
+}
+
 template <int K>
 struct MaskWords {
     uint32_t w[(K + 3) / 4];
@@ -47,7 +565,9 @@ __global__ __launch_bounds__(256) void nw_fill_kernel(const NwPairDesc *__restri
                                                       const uint8_t *__restrict__ ds,
                                                       uint8_t *__restrict__ mask,
                                                       int2 *__restrict__ scratch,
-                                                      int32_t *__restrict__ end_h, Scoring sc) {
+                                                      int32_t *__restrict__ end_h,
+                                                      saln_nw_result *__restrict__ results,
+                                                      uint32_t *__restrict__ cigar, Scoring sc) {
     constexpr int GPB = 256 / G;
     constexpr int KD = (K + 3) / 4;
     constexpr Geom geo{G, K};
@@ -61,12 +581,12 @@ __global__ __launch_bounds__(256) void nw_fill_kernel(const NwPairDesc *__restri
     uint8_t *__restrict__ mk = mask + p.mask_off;
     int2 *__restrict__ scr = scratch + p.scratch_off;
     const uint32_t nch = geo.n_chunks(lq);
-    const int T = (int)ld + G - 1;
     const int32_t sM = 2 * sc.match, sX = 2 * sc.mismatch;
     const int32_t sO = 2 * sc.gap_open, sE = 2 * sc.gap_extend;
     // end cell owner
     const uint32_t jend = lq - 1;
     const uint32_t c_end = jend / geo.W(), l_end = (jend % geo.W()) / K, k_end = jend % K;
+    int32_t my_end = 0;
 
     for (uint32_t c = 0; c < nch; ++c) {
         const uint32_t col0 = c * geo.W() + (uint32_t)lane * K;  // my columns: col0+1 .. col0+K
@@ -83,9 +603,14 @@ __global__ __launch_bounds__(256) void nw_fill_kernel(const NwPairDesc *__restri
         int32_t dnext = (lane == 0) ? (int32_t)d[0] : 0;
         int2 bnext = make_int2(0, 0);
         if (c > 0 && lane == 0) bnext = scr[1];
-        uint8_t *mchunk = mk + (uint64_t)c * geo.chunk_bytes(ld);
+        uint8_t *mtile = mk + (uint64_t)c * geo.chunk_bytes(ld) + geo.seg_step((uint32_t)lane, 0);
+        const int Tt = (int)(geo.tiles(ld) * kTileSteps);
 
-        for (int t = 0; t < T; ++t) {
+        for (int t0 = 0; t0 < Tt; t0 += kTileSteps) {
+          MaskWords<K> tb[kTileSteps];  // this lane's segments of the current step tile
+#pragma unroll
+          for (int ts = 0; ts < (int)kTileSteps; ++ts) {
+            const int t = t0 + ts;
             const int r = t - lane + 1;
             const int32_t dch = dnext;
             if (r >= 0 && r < (int)ld) dnext = (int32_t)d[r];
@@ -107,7 +632,8 @@ __global__ __launch_bounds__(256) void nw_fill_kernel(const NwPairDesc *__restri
                 for (int k = 0; k < KD; ++k) mw.w[k] = 0;
 #pragma unroll
                 for (int k = 0; k < K; ++k) {
-                    const int32_t M = hd + (qc[k] == dch ? sM : sX);
+                    const bool eq = qc[k] == dch;
+                    const int32_t M = hd + (eq ? sM : sX);
                     const int32_t I = F, D = Dn[k];
                     const int32_t H = max(M, max(I, D));
                     const int32_t Hc = H & ~1;
@@ -116,6 +642,7 @@ __global__ __launch_bounds__(256) void nw_fill_kernel(const NwPairDesc *__restri
                                  (D >= Hc ? kArgD : 0u);
                     b |= ((I | 1) >= tO ? kIExt : 0u) | ((tO | 1) >= I ? kIOpen : 0u);
                     b |= ((D | 1) >= tO ? kDExt : 0u) | ((tO | 1) >= D ? kDOpen : 0u);
+                    b |= eq ? 0x80u : 0u;  // bit 7: q == d (not inverted)
                     mw.w[k / 4] |= b << (8 * (k % 4));
                     F = max(tO, I) + sE;
                     Dn[k] = max(tO, D) + sE;
@@ -127,20 +654,26 @@ __global__ __launch_bounds__(256) void nw_fill_kernel(const NwPairDesc *__restri
                 pubH = Hp[K - 1];
 #pragma unroll
                 for (int k = 0; k < KD; ++k) mw.w[k] ^= 0x7F7F7F7Fu;  // stored inverted
-                *reinterpret_cast<MaskWords<K> *>(mchunk + (uint64_t)t * geo.step_bytes() +
-                                                  (uint32_t)lane * KD * 4) = mw;
+                tb[ts] = mw;
                 if (lane == G - 1 && c + 1 < nch) scr[r] = make_int2(pubH, pubF);
                 if (c == c_end && (uint32_t)lane == l_end && r == (int)ld) {
-                    int32_t e = 0;
 #pragma unroll
                     for (int k = 0; k < K; ++k)
-                        if ((uint32_t)k == k_end) e = Hp[k];
-                    end_h[first + gi] = e;
+                        if ((uint32_t)k == k_end) my_end = Hp[k];
+                    end_h[first + gi] = my_end;
                 }
             }
+          }
+          // the whole group finishes tile t0 / R together: one contiguous store
+          struct Tile { MaskWords<K> s[kTileSteps]; };
+          *reinterpret_cast<Tile *>(mtile + (uint64_t)(t0 / (int)kTileSteps) * geo.tile_bytes()) =
+              *reinterpret_cast<const Tile *>(tb);
         }
         if (c + 1 < nch) __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
     }
+    (void)my_end;
+    (void)results;
+    (void)cigar;
 }
 
 // ------------------------------------------------------- packed-i16 fill
@@ -209,9 +742,10 @@ __global__ __launch_bounds__(256) void nw_fill_pk_kernel(const NwPairDesc *__res
                                                          const uint8_t *__restrict__ qs,
                                                          const uint8_t *__restrict__ ds,
                                                          uint8_t *__restrict__ mask,
-                                                         int32_t *__restrict__ end_h, Scoring sc) {
+                                                         int32_t *__restrict__ end_h,
+                                                         saln_nw_result *__restrict__ results,
+                                                         uint32_t *__restrict__ cigar, Scoring sc) {
     constexpr int GPB = 256 / G;
-    constexpr int KD = (K + 3) / 4;
     constexpr Geom geo{G, K};
     const int lane = threadIdx.x % G;
     const uint32_t gi = blockIdx.x * GPB + threadIdx.x / G;
@@ -228,7 +762,6 @@ __global__ __launch_bounds__(256) void nw_fill_pk_kernel(const NwPairDesc *__res
     const uint8_t *__restrict__ dA = ds + pa.db_off;
     const uint8_t *__restrict__ dB = ds + pb.db_off;
     const int ldM = ldA > ldB ? ldA : ldB;
-    const int T = ldM + G - 1;
     const int32_t beta = -2 * sc.gap_extend;
     const int32_t alpha = -2 * sc.match - beta;
     const s16x2 kPen = spl(2 * (sc.match - sc.mismatch));
@@ -264,10 +797,17 @@ __global__ __launch_bounds__(256) void nw_fill_pk_kernel(const NwPairDesc *__res
     // end-cell owners
     const int lA = (lqA - 1) / K, kA = (lqA - 1) % K;
     const int lB = hasB ? (lqB - 1) / K : -1, kB = hasB ? (lqB - 1) % K : 0;
-    uint8_t *__restrict__ mA = mask + pa.mask_off + (uint32_t)lane * KD * 4;
-    uint8_t *__restrict__ mB = mask + pb.mask_off + (uint32_t)lane * KD * 4;
+    int32_t endA = 0, endB = 0;
+    uint8_t *__restrict__ mA = mask + pa.mask_off + geo.seg_step((uint32_t)lane, 0);
+    uint8_t *__restrict__ mB = mask + pb.mask_off + geo.seg_step((uint32_t)lane, 0);
+    const int tilesA = (int)geo.tiles((uint32_t)ldA), tilesB = hasB ? (int)geo.tiles((uint32_t)ldB) : 0;
+    const int Tt = (tilesA > tilesB ? tilesA : tilesB) * (int)kTileSteps;
 
-    for (int t = 0; t < T; ++t) {
+    for (int t0 = 0; t0 < Tt; t0 += kTileSteps) {
+      PkMask<K> ta[kTileSteps], tbb[kTileSteps];
+#pragma unroll
+      for (int ts = 0; ts < (int)kTileSteps; ++ts) {
+        const int t = t0 + ts;
         const int r = t - lane + 1;
         const uint32_t dch = (pa0 << 5) | (pb0 << 21);
         pa0 = pa1;
@@ -305,7 +845,8 @@ __global__ __launch_bounds__(256) void nw_fill_pk_kernel(const NwPairDesc *__res
                 uint32_t a = sign_bytes(s0, s1) & 0x02010201u;
                 a = (sign_bytes(s2, s3) & 0x08040804u) | a;
                 a = (sign_bytes(s4, s5) & 0x20102010u) | a;
-                a = (sign_bytes(s6, s6) & 0x00400040u) | a;
+                const uint32_t s7 = as_u(pen - spl(1));  // sign <=> q == d (bit 7)
+                a = (sign_bytes(s6, s7) & 0x80408040u) | a;
                 acc[k % 4] = a;
                 if (k % 4 == 3 || k == K - 1) {
                     pack4(acc[0], k % 4 >= 1 ? acc[1] : 0u, k % 4 >= 2 ? acc[2] : 0u,
@@ -319,188 +860,113 @@ __global__ __launch_bounds__(256) void nw_fill_pk_kernel(const NwPairDesc *__res
             hd = inH;
             pubF = F;
             pubH = Hp[K - 1];
-            const uint64_t so = (uint64_t)t * geo.step_bytes();
-            if (r <= ldA) *reinterpret_cast<PkMask<K> *>(mA + so) = wa;
-            if (r <= ldB) *reinterpret_cast<PkMask<K> *>(mB + so) = wb;
+            ta[ts] = wa;
+            tbb[ts] = wb;
             if (r == ldA && lane == lA) {
                 int32_t e = 0;
 #pragma unroll
                 for (int k = 0; k < K; ++k)
                     if (k == kA) e = (int16_t)(Hp[k] & 0xFFFFu);
-                end_h[first + ia] = e - alpha * ldA - beta * lqA;
+                endA = e - alpha * ldA - beta * lqA;
+                end_h[first + ia] = endA;
             }
             if (r == ldB && lane == lB) {
                 int32_t e = 0;
 #pragma unroll
                 for (int k = 0; k < K; ++k)
                     if (k == kB) e = (int16_t)(Hp[k] >> 16);
-                end_h[first + ib] = e - alpha * ldB - beta * lqB;
+                endB = e - alpha * ldB - beta * lqB;
+                end_h[first + ib] = endB;
             }
         }
+      }
+      // the group finishes tile t0 / R together: contiguous stores
+      struct Tile { PkMask<K> s[kTileSteps]; };
+      const int tile = t0 / (int)kTileSteps;
+      const uint64_t to = (uint64_t)tile * geo.tile_bytes();
+      if (tile < tilesA) *reinterpret_cast<Tile *>(mA + to) = *reinterpret_cast<const Tile *>(ta);
+      if (tile < tilesB) *reinterpret_cast<Tile *>(mB + to) = *reinterpret_cast<const Tile *>(tbb);
     }
-}
-
-// --------------------------------------------------------------- traceback
-struct GeomTable {
-    Geom g[kNumVariants];
-};
-
-struct MaskCell {
-    const uint8_t *m;
-    Geom g;
-    uint32_t lq, ld;
-    Scoring sc;
-    // codes are stored inverted (bit set = parent absent)
-    __device__ uint8_t byte(uint32_t i, uint32_t j) const { return m[g.cell(i, j, ld)] ^ 0x7F; }
-    __device__ uint8_t argmax(uint32_t i, uint32_t j) const {
-        if (i == 0) return argmax_row0(sc, j);
-        if (j == 0) return argmax_col0(sc, i);
-        return byte(i, j) & 7;
-    }
-    __device__ uint8_t ibits(uint32_t i, uint32_t j) const {  // i, j >= 1
-        return j == 1 ? ibits_col1(sc, i) : (byte(i, j - 1) >> 3) & 3;
-    }
-    __device__ uint8_t dbits(uint32_t i, uint32_t j) const {  // i, j >= 1
-        return i == 1 ? dbits_row1(sc, j) : (byte(i - 1, j) >> 5) & 3;
-    }
-};
-
-enum { kStM = 0, kStI = 1, kStD = 2 };
-enum { kEvOrigin = 0, kEvPanic = 1, kEvDead = 2 };
-
-// Canonical (first printed) alignment: the reference DFS pops end states in
-// the order D, M, I (:251-280 push I, M, D) and parents in reverse push order
-// (M: D>I>M; I: open>extend; D: open>extend).  While no sentinel cell is
-// reachable every DFS path ends at the origin or at a boundary panic node,
-// so the first path is this greedy walk.  A sentinel dead end (only possible
-// once len_q+len_db >~ 5,450) sets flags bit0 and the host redoes the walk
-// with backtracking.
-__global__ __launch_bounds__(256) void nw_traceback_kernel(
-    const NwPairDesc *__restrict__ pairs, uint32_t n, const uint8_t *__restrict__ qs,
-    const uint8_t *__restrict__ ds, const uint8_t *__restrict__ mask,
-    const int32_t *__restrict__ end_h, saln_nw_result *__restrict__ results,
-    uint32_t *__restrict__ cigar, Scoring sc, GeomTable gt) {
-    const uint32_t idx = blockIdx.x * blockDim.x + threadIdx.x;
-    if (idx >= n) return;
-    const NwPairDesc p = pairs[idx];
-    const uint32_t lq = p.len_q, ld = p.len_db;
-    const uint8_t *q = qs + p.q_off;
-    const uint8_t *d = ds + p.db_off;
-    const MaskCell mc{mask + p.mask_off, gt.g[p.variant], lq, ld, sc};
-    const int32_t hend = (lq && ld) ? end_h[idx] : hs_boundary_end(sc, lq, ld);
-    const uint8_t am_end = mc.argmax(ld, lq);
-    int st = (am_end & kArgD) ? kStD : ((am_end & kArgM) ? kStM : kStI);
-    uint32_t i = ld, j = lq;
-    uint32_t *out = cigar ? cigar + p.cigar_off : nullptr;
-    uint32_t nops = 0, run_op = 0, run_len = 0;
-    int ev;
-    for (;;) {
-        uint32_t op;
-        if (st == kStM) {
-            if (i == 0 && j == 0) { ev = kEvOrigin; break; }
-            if (i == 0 || j == 0) { ev = kEvDead; break; }
-            op = q[j - 1] == d[i - 1] ? SALN_CIGAR_EQ : SALN_CIGAR_X;
-            const uint8_t a = mc.argmax(i - 1, j - 1);
-            --i;
-            --j;
-            st = (a & kArgD) ? kStD : ((a & kArgI) ? kStI : kStM);
-        } else if (st == kStI) {
-            if (j == 0) { ev = i >= 1 ? kEvPanic : kEvDead; break; }
-            if (i == 0) { ev = kEvDead; break; }
-            op = SALN_CIGAR_I;
-            const uint8_t b = mc.ibits(i, j);
-            --j;
-            st = (b & 2) ? kStM : kStI;
-        } else {
-            if (i == 0) { ev = j >= 1 ? kEvPanic : kEvDead; break; }
-            if (j == 0) { ev = kEvDead; break; }
-            op = SALN_CIGAR_D;
-            const uint8_t b = mc.dbits(i, j);
-            --i;
-            st = (b & 2) ? kStM : kStD;
-        }
-        if (op == run_op && run_len) {
-            ++run_len;
-        } else {
-            if (run_len && out) out[nops] = (run_len << 4) | run_op;
-            nops += run_len ? 1 : 0;
-            run_op = op;
-            run_len = 1;
-        }
-    }
-    if (run_len) {
-        if (out) out[nops] = (run_len << 4) | run_op;
-        ++nops;
-    }
-    if (ev != kEvOrigin) nops = 0;
-    if (out) {  // ops were produced back to front
-        for (uint32_t a = 0, b = nops ? nops - 1 : 0; a < b; ++a, --b) {
-            const uint32_t tmp = out[a];
-            out[a] = out[b];
-            out[b] = tmp;
-        }
-    }
-    saln_nw_result r;
-    r.score = hend >> 1;
-    r.status = (hend & 1) ? SALN_REF_PANIC_BOUNDARY : SALN_OK;
-    r.cigar_len = nops;
-    r.end_states = am_end;
-    r.printed = ev == kEvOrigin ? 1 : 0;
-    r.flags = (ev == kEvDead ? 1 : 0) | ((ev == kEvPanic && !(hend & 1)) ? 2 : 0);
-    r.reserved = 0;
-    results[p.pair_id] = r;
+    (void)results;
+    (void)cigar;
 }
 
 // ----------------------------------------------------------------- launchers
 // variants 0-3: i32 lanes; 4-6: packed i16 (two pairs per lane)
 constexpr Geom kVariants[kNumVariants] = {{16, 10}, {16, 16}, {64, 8}, {64, 16},
-                                          {8, 19},  {16, 16}, {32, 16}};
-constexpr bool kPacked[kNumVariants] = {false, false, false, false, true, true, true};
+                                          {8, 19},  {16, 16}, {32, 16}, {16, 10}};
+constexpr bool kPacked[kNumVariants] = {false, false, false, false, true, true, true, true};
 
 template <int G, int K>
 static void fill_i32(dim3 grid, hipStream_t s, const NwPairDesc *pairs, uint32_t first,
                      uint32_t count, const uint8_t *qs, const uint8_t *ds, uint8_t *mask,
-                     int2 *scratch, int32_t *end_h, Scoring sc) {
+                     int2 *scratch, int32_t *end_h, saln_nw_result *res, uint32_t *cig,
+                     Scoring sc) {
     nw_fill_kernel<G, K><<<grid, dim3(256), 0, s>>>(pairs, first, count, qs, ds, mask, scratch,
-                                                     end_h, sc);
+                                                     end_h, res, cig, sc);
 }
 
 template <int G, int K>
 static void fill_pk(dim3 grid, hipStream_t s, const NwPairDesc *pairs, uint32_t first,
                     uint32_t count, const uint8_t *qs, const uint8_t *ds, uint8_t *mask,
-                    int32_t *end_h, Scoring sc) {
+                    int32_t *end_h, saln_nw_result *res, uint32_t *cig, Scoring sc) {
     nw_fill_pk_kernel<G, K><<<grid, dim3(256), 0, s>>>(pairs, first, count, qs, ds, mask, end_h,
-                                                        sc);
+                                                        res, cig, sc);
 }
 
 hipError_t launch_fill(int variant, const NwPairDesc *pairs, uint32_t first, uint32_t count,
                        const uint8_t *qs, const uint8_t *ds, uint8_t *mask, int2 *scratch,
-                       int32_t *end_h, Scoring sc, hipStream_t stream) {
+                       int32_t *end_h, saln_nw_result *res, uint32_t *cig, Scoring sc,
+                       hipStream_t stream) {
     if (count == 0) return hipSuccess;
     const uint32_t gpb = 256 / kVariants[variant].G;  // lane groups per block
     const uint32_t groups = kPacked[variant] ? (count + 1) / 2 : count;
     const dim3 grid((groups + gpb - 1) / gpb);
     switch (variant) {
-        case 0: fill_i32<16, 10>(grid, stream, pairs, first, count, qs, ds, mask, scratch, end_h, sc); break;
-        case 1: fill_i32<16, 16>(grid, stream, pairs, first, count, qs, ds, mask, scratch, end_h, sc); break;
-        case 2: fill_i32<64, 8>(grid, stream, pairs, first, count, qs, ds, mask, scratch, end_h, sc); break;
-        case 3: fill_i32<64, 16>(grid, stream, pairs, first, count, qs, ds, mask, scratch, end_h, sc); break;
-        case 4: fill_pk<8, 19>(grid, stream, pairs, first, count, qs, ds, mask, end_h, sc); break;
-        case 5: fill_pk<16, 16>(grid, stream, pairs, first, count, qs, ds, mask, end_h, sc); break;
-        default: fill_pk<32, 16>(grid, stream, pairs, first, count, qs, ds, mask, end_h, sc); break;
+        case 0: fill_i32<16, 10>(grid, stream, pairs, first, count, qs, ds, mask, scratch, end_h, res, cig, sc); break;
+        case 1: fill_i32<16, 16>(grid, stream, pairs, first, count, qs, ds, mask, scratch, end_h, res, cig, sc); break;
+        case 2: fill_i32<64, 8>(grid, stream, pairs, first, count, qs, ds, mask, scratch, end_h, res, cig, sc); break;
+        case 3: fill_i32<64, 16>(grid, stream, pairs, first, count, qs, ds, mask, scratch, end_h, res, cig, sc); break;
+        case 4: fill_pk<8, 19>(grid, stream, pairs, first, count, qs, ds, mask, end_h, res, cig, sc); break;
+        case 5: fill_pk<16, 16>(grid, stream, pairs, first, count, qs, ds, mask, end_h, res, cig, sc); break;
+        case 7: fill_pk<16, 10>(grid, stream, pairs, first, count, qs, ds, mask, end_h, res, cig, sc); break;
+        default: fill_pk<32, 16>(grid, stream, pairs, first, count, qs, ds, mask, end_h, res, cig, sc); break;
     }
     return hipGetLastError();
 }
 
-hipError_t launch_traceback(const NwPairDesc *pairs, uint32_t n, const uint8_t *qs,
-                            const uint8_t *ds, const uint8_t *mask, const int32_t *end_h,
-                            saln_nw_result *results, uint32_t *cigar, Scoring sc,
-                            hipStream_t stream) {
+template <int G, int K>
+static void tb_lds(dim3 grid, hipStream_t s, const NwPairDesc *pairs, uint32_t first, uint32_t n,
+                   const uint8_t *mask, const int32_t *end_h, saln_nw_result *res, uint32_t *cig,
+                   Scoring sc) {
+    nw_traceback_lds_kernel<G, K><<<grid, dim3(256), 0, s>>>(pairs, first, n, mask, end_h, res,
+                                                              cig, sc);
+}
+
+// Traceback of plan range [first, first+n).  variant >= 0: all pairs of that
+// fill variant (LDS walker where the segments fit); variant < 0: generic
+// walker (pairs with an empty side, or any variant).
+hipError_t launch_traceback(int variant, const NwPairDesc *pairs, uint32_t first, uint32_t n,
+                            const uint8_t *qs, const uint8_t *ds, const uint8_t *mask,
+                            const int32_t *end_h, saln_nw_result *results, uint32_t *cigar,
+                            Scoring sc, hipStream_t stream) {
     if (n == 0) return hipSuccess;
-    GeomTable gt;
-    for (int v = 0; v < kNumVariants; ++v) gt.g[v] = kVariants[v];
-    nw_traceback_kernel<<<dim3((n + 255) / 256), dim3(256), 0, stream>>>(
-        pairs, n, qs, ds, mask, end_h, results, cigar, sc, gt);
+    const dim3 grid((n + 255) / 256);
+    switch (variant) {
+        case 0: tb_lds<16, 10>(grid, stream, pairs, first, n, mask, end_h, results, cigar, sc); break;
+        case 1: tb_lds<16, 16>(grid, stream, pairs, first, n, mask, end_h, results, cigar, sc); break;
+        case 2: tb_lds<64, 8>(grid, stream, pairs, first, n, mask, end_h, results, cigar, sc); break;
+        case 3: tb_lds<64, 16>(grid, stream, pairs, first, n, mask, end_h, results, cigar, sc); break;
+        case 5: tb_lds<16, 16>(grid, stream, pairs, first, n, mask, end_h, results, cigar, sc); break;
+        case 6: tb_lds<32, 16>(grid, stream, pairs, first, n, mask, end_h, results, cigar, sc); break;
+        case 7: tb_lds<16, 10>(grid, stream, pairs, first, n, mask, end_h, results, cigar, sc); break;
+        default: {  // variant 4 (20-byte segments) and empty-side pairs
+            GeomTable gt;
+            for (int v = 0; v < kNumVariants; ++v) gt.g[v] = kVariants[v];
+            nw_traceback_kernel<<<grid, dim3(256), 0, stream>>>(pairs, first, n, qs, ds, mask,
+                                                                end_h, results, cigar, sc, gt);
+        }
+    }
     return hipGetLastError();
 }
 
@@ -519,8 +985,13 @@ static bool packed_ok(uint32_t lq, uint32_t ld, const Scoring &sc) {
 }
 
 int choose_variant(uint32_t len_q, uint32_t len_db, const Scoring &sc) {
+    static const int narrow = [] {
+        const char *e = std::getenv("SALN_NARROW_GROUPS");  // experiment switch: 8-lane groups
+        return e && e[0] == '1' ? 1 : 0;
+    }();
     if (packed_ok(len_q, len_db, sc)) {
-        if (len_q <= 152) return 4;
+        if (len_q <= 152 && narrow) return 4;
+        if (len_q <= 160) return 7;
         if (len_q <= 256) return 5;
         if (len_q <= 512) return 6;
     }

@@ -220,6 +220,17 @@ class NwPlan:
         _lib.check(self._L.saln_nw_execute(self._h, ptr(q_seq), ptr(db_seq), ptr(results),
                                            ptr(cigar), stream), "saln_nw_execute")
 
+    def set_async(self, enable: bool) -> None:
+        """2-deep pipeline: traceback of execute n overlaps the fill of n+1."""
+        _lib.check(self._L.saln_nw_plan_set_async(self._h, int(enable)), "set_async")
+
+    def sync(self, stream=None, keep_latest: bool = False) -> None:
+        """Make `stream` wait for the pending tracebacks (all, or all but the latest)."""
+        if stream is None:
+            import torch
+            stream = torch.cuda.current_stream(self.device).cuda_stream
+        _lib.check(self._L.saln_nw_plan_sync(self._h, stream, int(keep_latest)), "sync")
+
     def set_timing(self, enable: bool) -> None:
         _lib.check(self._L.saln_nw_plan_set_timing(self._h, int(enable)), "set_timing")
 

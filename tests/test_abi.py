@@ -1,0 +1,60 @@
+"""CPU: the C-ABI library loads, exports every entry point include/saln.h
+declares, and refuses to compute without a gfx950 device (no CPU path)."""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _declared():
+    src = open(os.path.join(ROOT, "include", "saln.h")).read()
+    return sorted(set(re.findall(r"\b(saln_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_header_matches_exports(saln):
+    from sequencealigning_amd import _lib
+    names = _declared()
+    assert set(names) == set(_lib.EXPORTS)
+    L = ctypes.CDLL(_lib.LIB_PATH)
+    for n in names:
+        assert hasattr(L, n), n
+
+
+def test_nm_exports_are_extern_c(saln):
+    from sequencealigning_amd import _lib
+    out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True,
+                         text=True, check=True).stdout
+    syms = {l.split()[-1] for l in out.splitlines() if " T " in l}
+    for n in _declared():
+        assert n in syms, n
+
+
+def test_abi_version(saln):
+    from sequencealigning_amd import _lib
+    assert _lib.lib().saln_abi_version() == 1
+
+
+def test_no_cpu_fallback(saln):
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    from sequencealigning_amd import _lib
+    with pytest.raises(_lib.SalnError, match="E_NO_DEVICE"):
+        saln.n_w_align(b"AC", b"AC")
+
+
+def test_struct_sizes(saln):
+    from sequencealigning_amd import _lib
+    assert ctypes.sizeof(_lib.NwResult) == 16
+    assert ctypes.sizeof(_lib.NwScoring) == 16
+
+
+def test_cli_help():
+    cli = os.path.join(ROOT, "sequencealigning_amd", "saln")
+    r = subprocess.run([cli, "--help"], capture_output=True, text=True)
+    assert r.returncode == 0
+    assert "--query-file" in r.stdout and "--algo" in r.stdout

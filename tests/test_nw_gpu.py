@@ -160,3 +160,48 @@ def test_c2_scale_properties(saln, oracle):
         assert (res["status"][k] == 2) == o.panics
         assert int(res["end_states"][k]) == o.end_states
     plan.close()
+
+
+def test_pipelined_plan_matches_sync(saln):
+    """saln_nw_plan_set_async: tracebacks overlap the next fill through two
+    mask workspaces; five pipelined executes (ragged lengths, several
+    variants, different inputs per step) must equal the synchronous plan byte
+    for byte."""
+    import torch
+    from sequencealigning_amd import synth
+    rng = np.random.default_rng(5)
+    n = 3000
+    lq = rng.integers(0, 400, n)
+    ld = rng.integers(0, 400, n)
+    lq[:5] = 0
+    qo = np.zeros(n + 1, np.uint64); qo[1:] = np.cumsum(lq)
+    do = np.zeros(n + 1, np.uint64); do[1:] = np.cumsum(ld)
+    pairs = np.stack([np.arange(n), np.arange(n)], 1)
+    sync_plan = saln.NwPlan(qo, do, pairs=pairs)
+    pipe = saln.NwPlan(qo, do, pairs=pairs)
+    pipe.set_async(True)
+    steps = 5
+    ins, want = [], []
+    for s in range(steps):
+        qs = synth.random_bases(100 + s, int(qo[-1]))
+        ds = synth.random_bases(200 + s, int(do[-1]))
+        dq, dd = torch.from_numpy(qs).cuda(), torch.from_numpy(ds).cuda()
+        r = torch.zeros(n * 4, dtype=torch.int32, device="cuda")
+        c = torch.zeros(max(1, sync_plan.cigar_words), dtype=torch.int32, device="cuda")
+        sync_plan.execute(dq, dd, r, c)
+        ins.append((dq, dd))
+        want.append((r, c))
+    got = []
+    for s in range(steps):
+        r = torch.zeros(n * 4, dtype=torch.int32, device="cuda")
+        c = torch.zeros(max(1, pipe.cigar_words), dtype=torch.int32, device="cuda")
+        pipe.execute(*ins[s], r, c)
+        got.append((r, c))
+        pipe.sync(keep_latest=True)
+    pipe.sync()
+    torch.cuda.synchronize()
+    for s in range(steps):
+        assert torch.equal(got[s][0], want[s][0]), s
+        assert torch.equal(got[s][1], want[s][1]), s
+    sync_plan.close()
+    pipe.close()

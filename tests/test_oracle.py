@@ -1,0 +1,78 @@
+"""CPU: the oracle (oracle/refcpu.c) against the hand-derived KATs of
+SURVEY.md §8.4 and against itself (literal DFS vs memoised DFS).  These are
+the pins of NW parity: the reference's own NW tests are empty stubs
+(needleman_wunsch_affine.rs:458-470), so NW parity is pinned by hand KATs,
+not by reference-run fixtures."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from nw_check import path_score, rand_seq
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def test_hand_kats(oracle):
+    with open(os.path.join(GOLDEN, "nw_kats.json")) as f:
+        data = json.load(f)
+    for k in data["hand"]:
+        o = oracle.nw(k["query"].encode(), k["db"].encode())
+        assert o.score == k["score"], k["id"]
+        assert o.stdout == k["stdout"], k["id"]
+        assert (o.dfs_rc == 1) == k["panics"], k["id"]
+        assert o.panics == k["panics"], k["id"]
+    # N4 worked cells (interior, [x][y] 1-based)
+    o = oracle.nw(b"AAA", b"AA")
+    for st, arr in (("M", o.M), ("I", o.I), ("D", o.D)):
+        assert arr[1:, 1:].tolist() == data["n4_cells"][st], st
+
+
+def test_boundary_quirks(oracle):
+    """needleman_wunsch_affine.rs:183-216: D on row 0, I on column 0, one extra
+    extension, sentinel i16::MIN."""
+    o = oracle.nw(b"ACGT", b"AC", literal_dfs=False)
+    assert o.D[0, 1:].tolist() == [-8 - 6 * (j + 1) for j in range(1, 5)]
+    assert o.I[1:, 0].tolist() == [-8 - 6 * (i + 1) for i in range(1, 3)]
+    assert (o.M[0, 1:] == -32768).all() and (o.M[1:, 0] == -32768).all()
+    assert o.I[0, 0] == -32768 and o.D[0, 0] == -32768 and o.M[0, 0] == 0
+
+
+def test_literal_vs_memoised(oracle):
+    rng = np.random.default_rng(3)
+    for _ in range(300):
+        q = rand_seq(rng, int(rng.integers(0, 12)), b"ACGTN")
+        d = rand_seq(rng, int(rng.integers(0, 12)), b"ACGTN")
+        o = oracle.nw(q, d)
+        assert o.dfs_rc in (0, 1)
+        assert (o.dfs_rc == 1) == o.panics, (q, d)
+        assert o.dfs_blocks == o.n_blocks, (q, d)
+        if o.first_ops is not None:
+            first = o.stdout.split("alignment found\n")[1]
+            s1 = first.split("\n")[1][6:]
+            assert len(s1) == len(o.first_ops)
+
+
+def test_first_alignment_rescored(oracle):
+    rng = np.random.default_rng(4)
+    for _ in range(100):
+        q = rand_seq(rng, int(rng.integers(1, 60)))
+        d = rand_seq(rng, int(rng.integers(1, 60)))
+        o = oracle.nw(q, d, literal_dfs=False)
+        if o.first_ops is None:
+            assert o.panics
+            continue
+        cig = [(1, c) for c in o.first_ops]
+        s, ok = path_score(q, d, cig)
+        assert ok and s == o.score
+
+
+def test_golden_random_consistent(oracle):
+    with open(os.path.join(GOLDEN, "nw_random.json")) as f:
+        pairs = json.load(f)["pairs"]
+    for v in pairs[:64]:
+        o = oracle.nw(v["query"].encode(), v["db"].encode(), literal_dfs=False)
+        assert o.score == v["score"]
+        assert o.first_ops == v["first_ops"]
+        assert o.panics == v["panics"]
