@@ -54,6 +54,7 @@ static int run_batch(saln_context *ctx, const uint8_t *q_seq, const uint64_t *q_
         return rc;
     }
     if (rc != SALN_OK) return rc;
+    if (masks_out) plan_set_full_codes(g.p, true);
     std::vector<uint64_t> coff(n_pairs + 1);
     saln_nw_cigar_offsets(g.p, coff.data());
     uint64_t cig_words = coff[n_pairs];
@@ -79,12 +80,36 @@ static int run_batch(saln_context *ctx, const uint8_t *q_seq, const uint64_t *q_
     for (uint64_t k = 0; k < n_pairs; ++k)
         if (results[k].flags & 1) need[k] = 1, any = true;
     if (any) {
+        // Sentinel dead ends need the full parent sets: re-fill just those
+        // pairs with full codes unless the main plan already has them.
+        PlanGuard g2;
+        std::vector<uint32_t> pq2, pd2, idx2(n_pairs, 0);
+        const saln_nw_plan *src = g.p;
+        if (!masks_out) {
+            for (uint64_t k = 0; k < n_pairs; ++k) {
+                if (!need[k]) continue;
+                idx2[k] = (uint32_t)pq2.size();
+                pq2.push_back((uint32_t)(pair_q ? pair_q[k] : k % n_q));
+                pd2.push_back((uint32_t)(pair_db ? pair_db[k] : k / n_q));
+            }
+            rc = saln_nw_plan_create(ctx, q_off, n_q, db_off, n_db, pq2.data(), pd2.data(),
+                                     pq2.size(), mode, scoring, &g2.p);
+            if (rc != SALN_OK) return rc;
+            plan_set_full_codes(g2.p, true);
+            DevBuf dr2;
+            TRY_HIP(dr2.alloc(pq2.size() * sizeof(saln_nw_result)));
+            rc = saln_nw_execute(g2.p, (const uint8_t *)dq.p, (const uint8_t *)dd.p,
+                                 (saln_nw_result *)dr2.p, nullptr, nullptr);
+            if (rc != SALN_OK) return rc;
+            TRY_HIP(hipDeviceSynchronize());
+            src = g2.p;
+        }
         if (masks_out) masks_out->resize(n_pairs);
         for (uint64_t k = 0; k < n_pairs; ++k) {
             if (!need[k] && !masks_out) continue;
             std::vector<uint8_t> m;
             Geom geo{16, 10};
-            rc = plan_pair_mask(g.p, k, &m, &geo);
+            rc = plan_pair_mask(src, masks_out ? k : idx2[k], &m, &geo);
             if (rc != SALN_OK) return rc;
             if (need[k]) {
                 const uint64_t qi = pair_q ? pair_q[k] : k % n_q;

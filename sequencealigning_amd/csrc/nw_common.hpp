@@ -41,6 +41,7 @@ struct NwPairDesc {
     uint64_t mask_off;       // byte offset of this pair's parent mask in the workspace
     uint64_t cigar_off;      // word offset of this pair's cigar (in results order)
     uint64_t scratch_off;    // int2 offset of the chunk-boundary column (multi-chunk pairs)
+    uint64_t ops_off;        // word offset of the traceback's 2-bit op stream (walker scratch)
     uint32_t len_q, len_db;
     uint32_t pair_id;        // index into results
     uint32_t variant;        // fill kernel variant (kernel geometry)

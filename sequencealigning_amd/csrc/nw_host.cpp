@@ -61,11 +61,13 @@ struct saln_nw_plan {
     uint8_t *d_mask2 = nullptr;  // second workspace for the async (2-deep) pipeline
     int32_t *d_endh2 = nullptr;
     bool async_tb = false;
+    bool full_codes = false;  // walk codes (default) or every parent set
     int buf = 0;                           // workspace of the next execute (async mode)
     bool tb_pending[2] = {false, false};
     int last_buf = 0;
     uint64_t mask_bytes = 0;
     int2 *d_scratch = nullptr;
+    uint32_t *d_ops = nullptr;  // traceback op-stream scratch (one traceback at a time)
     uint64_t scratch_elems = 0;
     int32_t *d_endh = nullptr;
     std::vector<uint64_t> cigar_off;  // results order, n_pairs + 1
@@ -134,6 +136,7 @@ int saln_nw_plan_destroy(saln_nw_plan *p) {
     (void)hipFree(p->d_mask2);
     (void)hipFree(p->d_endh2);
     (void)hipFree(p->d_scratch);
+    (void)hipFree(p->d_ops);
     (void)hipFree(p->d_endh);
     for (auto &e : p->sync_ev) (void)hipEventDestroy(e);
     for (auto &t : p->ev_pool)
@@ -205,7 +208,7 @@ int saln_nw_plan_create(saln_context *ctx, const uint64_t *q_off, uint64_t n_q,
     };
     std::sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return key(a) < key(b); });
     p->h_pairs.resize(n_pairs);
-    uint64_t moff = 0, soff = 0;
+    uint64_t moff = 0, soff = 0, ooff = 0;
     for (uint64_t r = 0; r < n_pairs; ++r) {
         NwPairDesc d = descs[order[r]];
         const bool empty = d.len_q == 0 || d.len_db == 0;
@@ -213,6 +216,8 @@ int saln_nw_plan_create(saln_context *ctx, const uint64_t *q_off, uint64_t n_q,
             const Geom g = variant_geom((int)d.variant);
             d.mask_off = moff;
             moff += (g.mask_bytes(d.len_q, d.len_db) + 255) & ~255ull;
+            d.ops_off = ooff;
+            ooff += (d.len_q + d.len_db + 9) / 10 + 1;  // 3-bit ops, ten per word
             if (g.n_chunks(d.len_q) > 1) {
                 d.scratch_off = soff;
                 soff += d.len_db + 2;
@@ -267,6 +272,8 @@ int saln_nw_plan_create(saln_context *ctx, const uint64_t *q_off, uint64_t n_q,
         return fail(e, "hipMalloc(mask workspace)");
     if (soff && (e = hipMalloc(&p->d_scratch, soff * sizeof(int2))) != hipSuccess)
         return fail(e, "hipMalloc(scratch)");
+    if (ooff && (e = hipMalloc(&p->d_ops, ooff * sizeof(uint32_t))) != hipSuccess)
+        return fail(e, "hipMalloc(op stream)");
     *out = p;
     return SALN_OK;
 }
@@ -341,7 +348,7 @@ int saln_nw_execute(saln_nw_plan *p, const uint8_t *d_q, const uint8_t *d_db,
             const uint32_t b = std::min(hi, p->var_first[v] + p->var_count[v]);
             if (a < b)
                 HIP_TRY(launch_fill(v, p->d_pairs, a, b - a, d_q, d_db, mask, p->d_scratch, endh,
-                                    d_results, d_cigar, p->sc, s));
+                                    d_results, d_cigar, p->sc, p->full_codes, s));
         }
         if (ev && k + 1 == nsub) HIP_TRY(hipEventRecord(ev[1], s));
         HIP_TRY(hipEventRecord(p->sync_ev[k], s));
@@ -351,14 +358,14 @@ int saln_nw_execute(saln_nw_plan *p, const uint8_t *d_q, const uint8_t *d_db,
             const uint32_t a = std::max(lo, p->var_first[v]);
             const uint32_t b = std::min(hi, p->var_first[v] + p->var_count[v]);
             if (a < b)
-                HIP_TRY(launch_traceback(v, p->d_pairs, a, b - a, d_q, d_db, mask, endh,
+                HIP_TRY(launch_traceback(v, p->d_pairs, a, b - a, d_q, d_db, mask, endh, p->d_ops,
                                          d_results, d_cigar, p->sc, t));
         }
     }
     // pairs with an empty side (boundary-only walk) ride on the traceback stream
     if (p->n_pairs > p->n_fill)
         HIP_TRY(launch_traceback(-1, p->d_pairs, p->n_fill, (uint32_t)(p->n_pairs - p->n_fill),
-                                 d_q, d_db, mask, endh, d_results, d_cigar, p->sc, t));
+                                 d_q, d_db, mask, endh, p->d_ops, d_results, d_cigar, p->sc, t));
     if (ev) HIP_TRY(hipEventRecord(ev[3], t));
     HIP_TRY(hipEventRecord(p->tb_done(cur), t));
     p->tb_pending[cur] = true;
@@ -424,10 +431,20 @@ int saln_nw_plan::resolve_events() {
 // ----------------------------------------------------------- host traceback
 namespace saln {
 
+int plan_set_full_codes(saln_nw_plan *p, bool full) {
+    if (!p) return SALN_E_INVALID;
+    p->full_codes = full;
+    return SALN_OK;
+}
+
 int plan_pair_mask(const saln_nw_plan *p, uint64_t pair_id, std::vector<uint8_t> *mask,
                    Geom *geo) {
     if (!p || pair_id >= p->n_pairs) return SALN_E_INVALID;
     const NwPairDesc &d = p->h_pairs[p->plan_index[pair_id]];
+    if (!p->full_codes && variant_packed((int)d.variant)) {
+        set_error("plan_pair_mask: plan stores walk codes only");
+        return SALN_E_INVALID;
+    }
     *geo = variant_geom((int)d.variant);
     mask->clear();
     if (d.len_q == 0 || d.len_db == 0) return SALN_OK;

@@ -15,11 +15,11 @@ namespace saln {
 hipError_t launch_fill(int variant, const NwPairDesc *pairs, uint32_t first, uint32_t count,
                        const uint8_t *qs, const uint8_t *ds, uint8_t *mask, int2 *scratch,
                        int32_t *end_h, saln_nw_result *results, uint32_t *cigar, Scoring sc,
-                       hipStream_t stream);
+                       bool full_codes, hipStream_t stream);
 hipError_t launch_traceback(int variant, const NwPairDesc *pairs, uint32_t first, uint32_t n,
                             const uint8_t *qs,
                             const uint8_t *ds, const uint8_t *mask, const int32_t *end_h,
-                            saln_nw_result *results, uint32_t *cigar, Scoring sc,
+                            uint32_t *ops, saln_nw_result *results, uint32_t *cigar, Scoring sc,
                             hipStream_t stream);
 Geom variant_geom(int v);
 bool variant_packed(int v);
@@ -50,6 +50,10 @@ struct HostMask {
     // Dense export (include/saln.h saln_nw_dense_mask).
     void to_dense(uint8_t *out) const;
 };
+
+// Full parent codes (every parent set, needed by the host DFS and the dense
+// export) instead of the walk codes a plan stores by default.
+int plan_set_full_codes(saln_nw_plan *plan, bool full);
 
 // Copies one pair's parent codes (kernel layout) from a plan's workspace
 // after execute; pair_id is the results index.

@@ -304,50 +304,111 @@ __device__ void walk_pair_stream(const NwPairDesc &p, int32_t hend,
 
 // LDS-window walker (segments of <= 16 bytes, i.e. K <= 16).  Lock-step
 // phases as in walk_pair_stream (every lane in phase S, target row base-S),
-// but the windows live in LDS, filled by LDS-DMA (global_load_lds_dwordx4:
-// lane l's 16 bytes land at slot base + 16*l; the slot base is wave-uniform
-// because all lanes are in the same phase).  There are two windows, one for
-// even and one for odd column blocks; at the end of phase S every lane
-// refills slot S of both with row base-S-kWin of the blocks {B, B-1} (B = its
-// current block), so when the walk crosses into block B-1 the data is
-// already resident.  valid[] bits track which slots of each window hold the
-// block currently assigned to it; a crossing that comes back faster than the
-// refills falls back to a synchronous load.  Exactly two DMAs per phase keep
-// >= 2*kWin-2 younger VMEM operations behind any slot a phase reads, so the
-// read waits with vmcnt(14) in the same asm statement (the compiler cannot
-// hoist it or turn it into a conservative vmcnt(0)).
-constexpr uint32_t kSlotBytes = 64 * 16;                 // one slot of a wave
-constexpr uint32_t kWinBytes = kWin * kSlotBytes;        // one window of a wave
-constexpr uint32_t kWaveLds = 2 * kWinBytes;             // even + odd window: 16 KiB
+// but the windows live in LDS, filled by LDS-DMA (global_load_lds_dwordx{3,4}:
+// lane l's bytes land at slot base + 16*l; the slot base is wave-uniform
+// because all lanes are in the same phase).  Block b lives in window b % NW
+// (WalkGeo); at the end of phase S every lane refills slot S of every window
+// with row base-S-W of the blocks {B, .., B-NW+1} (B = its current block),
+// so when the walk crosses into block B-1 the data is already resident.
+// valid bits track which slots of each window hold the block currently
+// assigned to it; a crossing that comes back faster than the refills falls
+// back to a synchronous load.
+// Decisions are table lookups on the raw code byte: three bits at a
+// state-dependent offset index kNextLut (no branches on the state).  The
+// walk records 3-bit ops (state | eq << 2, ten per word) and stores a word
+// once it is complete, at a phase end, before the DMAs; the CIGAR (forward
+// order, run-length words) is produced from that stream after the walk.
+// Exactly NW DMAs per phase (the init issues the same group per slot) keep
+// >= NW*(W-1) younger VMEM operations behind any slot a phase reads, so the
+// read waits with that vmcnt in the same asm statement (the compiler cannot
+// hoist it or turn it into a conservative vmcnt(0)).  Extra VMEM operations
+// (op-stream stores, fallback loads) only make that wait more conservative.
+constexpr uint32_t kOpsPerWord = 10;                     // 3-bit ops per op-stream word
+
+// Window geometry of the walker for K columns per block: NW = 2 windows
+// (blocks B, B-1 resident) of W slots (rows).  A slot holds 16 bytes per lane
+// (the LDS-DMA lane stride, also for dwordx3).  Each phase end issues the NW
+// DMAs (always) after the op-stream store (only when a word is complete), so
+// a phase reads the slot its DMA filled W-1 phases earlier behind >= NW*(W-1)
+// younger VMEM operations.  The walk is bound by L2 request throughput (one
+// request per lane per DMA), so W is kept small: with 10-column blocks a
+// diagonal path crosses a block every ~10 rows and W = 4 lets the window of
+// B-2 refill before the next crossing.
+template <int K>
+struct WalkGeo {
+    static constexpr uint32_t LB = (K + 3) / 4 * 4;
+    static constexpr uint32_t NW = 2;
+    static constexpr uint32_t W = K < 16 ? 4 : 8;
+    static constexpr uint32_t SB = LB == 12 ? 12 : 16;        // DMA bytes per lane
+    static constexpr uint32_t kSlotBytes = 64 * 16;          // one slot of a wave
+    static constexpr uint32_t kWinBytes = W * kSlotBytes;    // one window of a wave
+    static constexpr uint32_t kWaveLds = NW * kWinBytes;
+    static constexpr uint32_t kVmcnt = NW * (W - 1);
+    static_assert(LB <= 16, "LDS window slots hold at most 16 bytes per lane");
+};
+
 typedef __attribute__((address_space(3))) uint8_t lds_u8;
 
 __device__ __forceinline__ uint32_t lds_off(const lds_u8 *p) { return (uint32_t)(uintptr_t)p; }
 
-__device__ __forceinline__ uint32_t window_byte(uint32_t addr) {
+// Raw code byte (bits 0-6 stored inverted: 1 = parent absent; bit 7 = eq),
+// once at most N younger VMEM operations are outstanding.
+template <uint32_t N>
+__device__ __forceinline__ uint32_t window_raw(uint32_t addr) {
+    static_assert(N == 6 || N == 14, "add the immediate below");
     uint32_t v;
-    asm volatile("s_waitcnt vmcnt(14)\n\tds_read_u8 %0, %1\n\ts_waitcnt lgkmcnt(0)"
-                 : "=v"(v) : "v"(addr) : "memory");
-    static_assert(kWin == 8, "vmcnt(14) above is 2*kWin - 2");
-    return v ^ 0x7Fu;  // decoded: bit set = parent present
+    if constexpr (N == 6)
+        asm volatile("s_waitcnt vmcnt(6)\n\tds_read_u8 %0, %1\n\ts_waitcnt lgkmcnt(0)"
+                     : "=v"(v) : "v"(addr) : "memory");
+    else
+        asm volatile("s_waitcnt vmcnt(14)\n\tds_read_u8 %0, %1\n\ts_waitcnt lgkmcnt(0)"
+                     : "=v"(v) : "v"(addr) : "memory");
+    return v;
 }
 
-__device__ __forceinline__ uint32_t window_byte_sync(uint32_t addr) {
-    uint32_t v;
-    asm volatile("s_waitcnt vmcnt(0)\n\tds_read_u8 %0, %1\n\ts_waitcnt lgkmcnt(0)"
-                 : "=v"(v) : "v"(addr) : "memory");
-    return v ^ 0x7Fu;
+// A store the compiler can neither merge nor drop: the walker's vmcnt
+// arithmetic counts every one of them.
+__device__ __forceinline__ void counted_store(uint32_t *ptr, uint32_t v) {
+    asm volatile("global_store_dword %0, %1, off" : : "v"(ptr), "v"(v) : "memory");
 }
+
+// Next state from the current state st (M, I, D, or 3 = at the end cell)
+// and the three raw code bits at offset kLutShift(st): M reads bits 1-3
+// (argI, argD; D > I > M), I bits 3-5 (I-open > extend), D bits 5-7 (D-open
+// > extend), the end cell bits 0-2 (argM, argI, argD; D > M > I).
+__host__ __device__ constexpr uint32_t next_state_raw(uint32_t st, uint32_t f) {
+    const uint32_t pr = f ^ 7u;  // present bits (bit 2 of the D view is eq: unused)
+    return st == 0 ? ((pr & 2) ? kStD : (pr & 1) ? kStI : kStM)
+         : st == 1 ? ((pr & 2) ? kStM : kStI)
+         : st == 2 ? ((pr & 2) ? kStM : kStD)
+                   : ((pr & 4) ? kStD : (pr & 1) ? kStM : kStI);
+}
+__host__ __device__ constexpr uint64_t make_next_lut() {
+    uint64_t l = 0;
+    for (uint32_t st = 0; st < 4; ++st)
+        for (uint32_t f = 0; f < 8; ++f) l |= (uint64_t)next_state_raw(st, f) << (16 * st + 2 * f);
+    return l;
+}
+constexpr uint64_t kNextLut = make_next_lut();
+
+#ifdef SALN_WALK_PROF
+// profiling build: shader-clock time in the window waits / sync loads
+#define SALN_PROF_T() __builtin_amdgcn_s_memtime()
+#else
+#define SALN_PROF_T() 0ull
+#endif
 
 #ifdef SALN_WALK_CHECK
 // debug build: compare every window read with the byte in HBM
 #define SALN_WALK_CHECK_HOOK(S)                                                          \
     {                                                                                    \
-        const uint32_t tru = (uint32_t)m[geo.cell(ti, tj, p.len_db)] ^ 0x7Fu;            \
-        if (tru != b) {                                                                  \
-            if (!dbg_n) dbg_info = (S) | (par << 3) | (((valid >> (par * 8u + (S))) & 1u) << 4) | \
+        const uint32_t tru = (uint32_t)m[geo.cell(ti, tj, p.len_db)];                   \
+        if (tru != raw) {                                                                \
+            const uint32_t par = wc;                                                     \
+            if (!dbg_n) dbg_info = (S) | (par << 3) | (((valid >> (par * 8u + (S))) & 1u) << 5) | \
                                    ((ti & 0xFFFu) << 8) | ((tj & 0xFFFu) << 20);          \
             ++dbg_n;                                                                     \
-            b = tru;                                                                     \
+            raw = tru;                                                                   \
         }                                                                                \
     }
 #else
@@ -356,131 +417,183 @@ __device__ __forceinline__ uint32_t window_byte_sync(uint32_t addr) {
 
 template <int G, int K>
 __device__ void walk_pair_lds(const NwPairDesc &p, int32_t hend, const uint8_t *__restrict__ mask,
-                              saln_nw_result *__restrict__ results,
+                              uint32_t *__restrict__ ops_all, saln_nw_result *__restrict__ results,
                               uint32_t *__restrict__ cigar, Scoring sc, lds_u8 *win) {
+    using WG = WalkGeo<K>;
     constexpr Geom geo{G, K};
-    constexpr uint32_t LB = (K + 3) / 4 * 4;
+    constexpr uint32_t LB = WG::LB, NW = WG::NW, kW = WG::W;
     constexpr uint32_t TB = G * kTileSteps * LB;  // tile bytes
-    static_assert(LB <= 16, "LDS window slots hold 16 bytes per lane");
+    constexpr uint32_t kAll = (1u << (8 * NW)) - 1u;
     const uint64_t cb = geo.chunk_bytes(p.len_db);
     const uint8_t *__restrict__ m = mask + p.mask_off;
     uint32_t *out = cigar ? cigar + p.cigar_off : nullptr;
-    uint32_t nops = 0, run_op = 0, run_len = 0;
+    uint32_t *const ops = ops_all + p.ops_off;
+    // op stream: `cur` = word wi (sh3/3 ops so far); `full` = word wi-1 while not yet stored
+    uint32_t wi = 0, sh3 = 0, cur = 0, full = 0, hf = 0;  // hf: `full` pending
     uint32_t ti = p.len_db, tj = p.len_q;
-    int from = kFromEnd;
-    uint8_t am_end = 0;
-    bool walking = true;
+    uint32_t st = 3, lsh = 0;  // state (3 = at the end cell) and its code-bit offset
+    uint32_t walking = 1;
     uint32_t B = (tj - 1) / K, base = ti;
     uint32_t col = (tj - 1) % K;  // target column inside block B
-    uint32_t valid = 0xFFFFu;     // bits 0-7: even window slots, 8-15: odd window slots
-    const uint32_t lane16 = (threadIdx.x & 63u) * 16u;
-    const uint32_t wbase = lds_off(win);
+    uint32_t wc = B % NW;         // window of block B (block b lives in window b % NW)
+    uint32_t valid = kAll;        // bit 8w+s: slot s of window w holds its block
+    const uint32_t wbase = lds_off(win) + (threadIdx.x & 63u) * 16u;
+    uint32_t wrow = 0;            // LDS address of (window wc, slot S, my lane)
+    uint64_t p_twait = 0, p_tsync = 0, p_t0 = SALN_PROF_T();
+    uint32_t p_iter = 0, p_sync = 0;
+    (void)p_twait, (void)p_tsync, (void)p_t0, (void)p_iter, (void)p_sync;
 #ifdef SALN_WALK_CHECK
     uint32_t dbg_n = 0, dbg_info = 0;
 #endif
-    // per-block segment base (chunk + lane offset) and lane index, for B and B-1
+    // per-block segment base (chunk + lane offset) and lane index, for B, B-1, B-2
     auto blk_base = [&](uint32_t blk) __attribute__((always_inline)) {
         return m + (uint64_t)(blk / G) * cb + (blk % G) * (kTileSteps * LB);
     };
-    const uint8_t *bp_cur = blk_base(B), *bp_prv = blk_base(B ? B - 1 : 0);
-    uint32_t L_cur = B % G, L_prv = (B ? B - 1 : 0) % G;
+    const uint8_t *bp0 = blk_base(B), *bp1 = blk_base(B >= 1 ? B - 1 : 0);
+    const uint8_t *bp2 = blk_base(B >= 2 ? B - 2 : 0);
+    uint32_t L0 = B % G, L1 = (B >= 1 ? B - 1 : 0) % G, L2 = (B >= 2 ? B - 2 : 0) % G;
+    (void)bp2;
+    (void)L2;
     // global address of a segment at `row` (clamped to >= 1) given block base/lane
     auto seg = [&](const uint8_t *bp, uint32_t L, int32_t row) __attribute__((always_inline)) {
         const uint32_t t = (uint32_t)max(row, 1) - 1 + L;
         return (const void *)(bp + (uint64_t)(t / kTileSteps) * TB + (t % kTileSteps) * LB);
     };
-#define SALN_ROW(S2, S) ((int32_t)((S2) >= (S) ? base - (S2) : base - (S2) - kWin))
+#define SALN_ROW(S2, S) ((int32_t)((S2) >= (S) ? base - (S2) : base - (S2) - kW))
 #define SALN_DMA(WIN, SLOT, ADDR)                                                              \
     __builtin_amdgcn_global_load_lds(                                                          \
-        ADDR, (__attribute__((address_space(3))) void *)(win + (WIN) * kWinBytes +             \
-                                                         (SLOT) * kSlotBytes),                 \
-        16, 0, 0)
-    // even / odd windows hold {B, B-1}
+        ADDR, (__attribute__((address_space(3))) void *)(win + (WIN) * WG::kWinBytes +         \
+                                                         (SLOT) * WG::kSlotBytes),             \
+        WalkGeo<K>::SB, 0, 0)
+    // window w holds the resident block congruent to w (mod NW)
 #define SALN_REFILL(S, ROW)                                                                    \
     {                                                                                          \
-        const void *ac = seg(bp_cur, L_cur, ROW), *ap = seg(bp_prv, L_prv, ROW);               \
-        const bool odd = (B & 1u) != 0;                                                        \
-        SALN_DMA(0, S, odd ? ap : ac);                                                         \
-        SALN_DMA(1, S, odd ? ac : ap);                                                         \
+        const void *a0 = seg(bp0, L0, ROW), *a1 = seg(bp1, L1, ROW);                           \
+        if constexpr (NW == 2) {                                                               \
+            SALN_DMA(0, S, wc ? a1 : a0);                                                      \
+            SALN_DMA(1, S, wc ? a0 : a1);                                                      \
+        } else {                                                                               \
+            const void *a2 = seg(bp2, L2, ROW);                                                \
+            /* window w gets block B - ((wc - w) mod 3) */                                     \
+            SALN_DMA(0, S, wc == 0 ? a0 : wc == 1 ? a1 : a2);                                  \
+            SALN_DMA(1, S, wc == 1 ? a0 : wc == 2 ? a1 : a2);                                  \
+            SALN_DMA(2, S, wc == 2 ? a0 : wc == 0 ? a1 : a2);                                  \
+        }                                                                                      \
+    }
+    // slot S of window wc not refreshed since a crossing: load it now.
+    // Independent ifs (not if/else): the compiler must not merge the calls
+    // into one DMA with a per-lane (then readfirstlane'd) LDS base.
+#define SALN_ENSURE(S)                                                                         \
+    if (!(valid & (1u << (wc * 8u + (S))))) {                                                  \
+        const uint64_t tq0 = SALN_PROF_T();                                                    \
+        ++p_sync;                                                                              \
+        const void *ac = seg(bp0, L0, (int32_t)(base - (S)));                                  \
+        if (wc == 0) { SALN_DMA(0, S, ac); }                                                   \
+        __builtin_amdgcn_sched_barrier(0);                                                     \
+        if (wc == 1) { SALN_DMA(1, S, ac); }                                                   \
+        if constexpr (NW == 3) {                                                               \
+            __builtin_amdgcn_sched_barrier(0);                                                 \
+            if (wc == 2) { SALN_DMA(2, S, ac); }                                               \
+        }                                                                                      \
+        asm volatile("s_waitcnt vmcnt(0)" : : : "memory");                                     \
+        valid |= 1u << (wc * 8u + (S));                                                        \
+        p_tsync += SALN_PROF_T() - tq0;                                                        \
     }
 #define SALN_PHASE(S)                                                                          \
-    while (walking) {                                                                          \
-        const uint32_t par = B & 1u;                                                           \
-        const uint32_t addr = wbase + par * kWinBytes + (S) * kSlotBytes + lane16 + col;       \
-        uint32_t b;                                                                            \
-        if (valid & (1u << (par * 8u + (S)))) {                                                \
-            b = window_byte(addr);                                                             \
-        } else { /* window not refreshed since the last crossing: load this slot now */        \
-            /* two independent ifs (not if/else): the compiler must not merge the   */         \
-            /* calls into one DMA with a per-lane (then readfirstlane'd) LDS base    */         \
-            const void *ac = seg(bp_cur, L_cur, (int32_t)(base - (S)));                        \
-            if (par == 0) { SALN_DMA(0, S, ac); }                                              \
-            __builtin_amdgcn_sched_barrier(0);                                                 \
-            if (par == 1) { SALN_DMA(1, S, ac); }                                              \
-            b = window_byte_sync(addr);                                                        \
-            valid |= 1u << (par * 8u + (S));                                                   \
-        }                                                                                      \
-        SALN_WALK_CHECK_HOOK(S)                                                                \
-        if (from == kFromEnd) am_end = (uint8_t)(b & 7);                                       \
-        const int st = next_state(from, b);                                                    \
-        const uint32_t op = st == kStI   ? SALN_CIGAR_I                                        \
-                            : st == kStD ? SALN_CIGAR_D                                        \
-                                         : ((b & 0x80u) ? SALN_CIGAR_EQ : SALN_CIGAR_X);        \
-        const bool brk = run_len != 0 && op != run_op;                                         \
-        if (brk && out) out[nops] = (run_len << 4) | run_op;                                   \
-        nops += brk ? 1u : 0u;                                                                 \
-        run_len = brk || run_len == 0 ? 1u : run_len + 1u;                                     \
-        run_op = op;                                                                           \
-        const bool up = st != kStI, left = st != kStD;                                         \
-        ti -= up ? 1u : 0u;                                                                    \
-        tj -= left ? 1u : 0u;                                                                  \
-        from = st;                                                                             \
-        if (ti == 0 || tj == 0) { walking = false; break; }                                    \
-        if (left) {                                                                            \
-            if (col == 0) { /* crossed into B-1: its window now gets B-2 */                    \
-                valid &= par ? 0x00FFu : 0xFF00u;                                              \
+    wrow = wbase + wc * WG::kWinBytes + (S) * WG::kSlotBytes;                                  \
+    if (walking) {                                                                             \
+        SALN_ENSURE(S)                                                                         \
+        for (;;) {                                                                             \
+            const uint64_t tw0 = SALN_PROF_T();                                                \
+            uint32_t raw = window_raw<WG::kVmcnt>(wrow + col);                                 \
+            p_twait += SALN_PROF_T() - tw0;                                                    \
+            ++p_iter;                                                                          \
+            SALN_WALK_CHECK_HOOK(S)                                                            \
+            const uint32_t f3 = __builtin_amdgcn_ubfe(raw, lsh, 3);                            \
+            const uint32_t nx = (uint32_t)(kNextLut >> (f3 * 2u + st * 16u)) & 3u;             \
+            cur |= (nx | ((raw >> 5) & 4u)) << sh3;                                            \
+            sh3 += 3;                                                                          \
+            const bool wrap = sh3 == 3 * kOpsPerWord;                                          \
+            if (wrap && hf) counted_store(ops + wi - 1, full); /* > 10 ops in one row */      \
+            full = wrap ? cur : full;                                                          \
+            cur = wrap ? 0u : cur;                                                             \
+            sh3 = wrap ? 0u : sh3;                                                             \
+            wi += wrap ? 1u : 0u;                                                              \
+            hf = wrap ? 1u : hf;                                                               \
+            st = nx;                                                                           \
+            lsh = 2u * nx + 1u;                                                                \
+            const bool up = nx != kStI, left = nx != kStD;                                     \
+            ti -= up ? 1u : 0u;                                                                \
+            tj -= left ? 1u : 0u;                                                              \
+            const bool done = ti == 0 || tj == 0;                                              \
+            walking = done ? 0u : 1u;                                                          \
+            if (left && col == 0 && !done) { /* crossed into B-1; B's window gets B-NW */     \
+                valid &= ~(0xFFu << (wc * 8u));                                                \
                 --B;                                                                           \
-                col = K - 1;                                                                   \
-                bp_cur = bp_prv;                                                               \
-                L_cur = L_prv;                                                                 \
-                bp_prv = blk_base(B ? B - 1 : 0);                                              \
-                L_prv = (B ? B - 1 : 0) % G;                                                   \
-            } else {                                                                           \
-                --col;                                                                         \
+                wc = wc ? wc - 1u : NW - 1u;                                                   \
+                wrow = wbase + wc * WG::kWinBytes + (S) * WG::kSlotBytes;                      \
+                bp0 = bp1;                                                                     \
+                L0 = L1;                                                                       \
+                if constexpr (NW == 2) {                                                       \
+                    bp1 = blk_base(B >= 1 ? B - 1 : 0);                                        \
+                    L1 = (B >= 1 ? B - 1 : 0) % G;                                             \
+                } else {                                                                       \
+                    bp1 = bp2;                                                                 \
+                    L1 = L2;                                                                   \
+                    bp2 = blk_base(B >= 2 ? B - 2 : 0);                                        \
+                    L2 = (B >= 2 ? B - 2 : 0) % G;                                             \
+                }                                                                              \
+                SALN_ENSURE(S)                                                                 \
             }                                                                                  \
+            col = left ? (col == 0 ? K - 1 : col - 1) : col;                                   \
+            if (up || done) break; /* up one row: next phase */                                \
         }                                                                                      \
-        if (up) break; /* up one row: next phase */                                            \
     }                                                                                          \
-    /* exactly two DMAs per phase for every lane of the wave */                                \
-    SALN_REFILL(S, (int32_t)(base - (S) - kWin))                                               \
-    valid |= 0x101u << (S);
+    /* the completed op word (if any), then exactly NW DMAs per phase */                       \
+    {                                                                                          \
+        const uint64_t te0 = SALN_PROF_T();                                                    \
+        SALN_FLUSH()                                                                           \
+        SALN_REFILL(S, (int32_t)(base - (S) - kW))                                             \
+        p_tsync += SALN_PROF_T() - te0;                                                        \
+    }                                                                                          \
+    valid |= (kAll / 0xFFu) << (S);
+#define SALN_FLUSH()                                                                           \
+    if (hf) {                                                                                  \
+        counted_store(ops + wi - 1, full);                                                     \
+        hf = 0;                                                                                \
+    }
 #define SALN_INIT(S2) SALN_REFILL(S2, SALN_ROW(S2, 0))
+    static_assert(kW == 4 || kW == 8, "phases are unrolled below");
     SALN_INIT(0) SALN_INIT(1) SALN_INIT(2) SALN_INIT(3)
-    SALN_INIT(4) SALN_INIT(5) SALN_INIT(6) SALN_INIT(7)
+    if constexpr (kW == 8) { SALN_INIT(4) SALN_INIT(5) SALN_INIT(6) SALN_INIT(7) }
     while (walking) {
         SALN_PHASE(0)
         SALN_PHASE(1)
         SALN_PHASE(2)
         SALN_PHASE(3)
-        SALN_PHASE(4)
-        SALN_PHASE(5)
-        SALN_PHASE(6)
-        SALN_PHASE(7)
-        base -= kWin;
+        if constexpr (kW == 8) {
+            SALN_PHASE(4)
+            SALN_PHASE(5)
+            SALN_PHASE(6)
+            SALN_PHASE(7)
+        }
+        base -= kW;
     }
 #undef SALN_INIT
+#undef SALN_FLUSH
 #undef SALN_PHASE
+#undef SALN_ENSURE
 #undef SALN_REFILL
 #undef SALN_DMA
 #undef SALN_ROW
     int ev, bst;
-    if (from == kFromM && ti == 0 && tj == 0) {
+    if (st == kStM && ti == 0 && tj == 0) {
         ev = kEvOrigin;
     } else {
-        if (from == kFromM) {
+        if (st == kStM) {
             const uint8_t a = ti == 0 ? argmax_row0(sc, tj) : argmax_col0(sc, ti);
             bst = (a & kArgD) ? kStD : ((a & kArgI) ? kStI : kStM);
-        } else if (from == kFromI) {
+        } else if (st == kStI) {
             bst = (ibits_col1(sc, ti) & 2) ? kStM : kStI;
         } else {
             bst = (dbits_row1(sc, tj) & 2) ? kStM : kStD;
@@ -489,26 +602,55 @@ __device__ void walk_pair_lds(const NwPairDesc &p, int32_t hend, const uint8_t *
         else if (bst == kStI && tj == 0 && ti >= 1) ev = kEvPanic;
         else ev = kEvDead;
     }
-    if (run_len) {
-        if (out) out[nops] = (run_len << 4) | run_op;
-        ++nops;
-    }
-    if (ev != kEvOrigin) nops = 0;
-    if (out) {
-        for (uint32_t a2 = 0, b2 = nops ? nops - 1 : 0; a2 < b2; ++a2, --b2) {
-            const uint32_t tmp = out[a2];
-            out[a2] = out[b2];
-            out[b2] = tmp;
+    // CIGAR: the op stream read back in forward order (last recorded op first)
+    uint32_t nops = 0;
+    if (ev == kEvOrigin) {
+        if (hf) counted_store(ops + wi - 1, full);
+        if (sh3) counted_store(ops + wi, cur);
+        asm volatile("s_waitcnt vmcnt(0)" : : : "memory");
+        const uint32_t nrec = wi * kOpsPerWord + sh3 / 3;
+        uint32_t run_op = 0, run_len = 0;
+        for (int32_t w = (int32_t)((nrec - 1u) / kOpsPerWord); w >= 0; --w) {
+            const uint32_t word = ops[w];
+            const uint32_t top = (uint32_t)w == (nrec - 1u) / kOpsPerWord
+                                     ? (nrec - 1u) % kOpsPerWord : kOpsPerWord - 1;
+            for (int32_t k = (int32_t)top; k >= 0; --k) {
+                const uint32_t c = (word >> (3 * k)) & 7u;
+                const uint32_t op = (c & 3u) == kStI   ? SALN_CIGAR_I
+                                    : (c & 3u) == kStD ? SALN_CIGAR_D
+                                    : (c & 4u)         ? SALN_CIGAR_EQ : SALN_CIGAR_X;
+                if (run_len && op != run_op) {
+                    if (out) out[nops] = (run_len << 4) | run_op;
+                    ++nops;
+                    run_len = 0;
+                }
+                run_op = op;
+                ++run_len;
+            }
+        }
+        if (run_len) {
+            if (out) out[nops] = (run_len << 4) | run_op;
+            ++nops;
         }
     }
     saln_nw_result r;
     r.score = hend >> 1;
     r.status = (hend & 1) ? SALN_REF_PANIC_BOUNDARY : SALN_OK;
     r.cigar_len = nops;
-    r.end_states = am_end;
+    r.end_states = (uint8_t)((m[geo.cell(p.len_db, p.len_q, p.len_db)] ^ 0x7Fu) & 7u);
     r.printed = ev == kEvOrigin ? 1 : 0;
     r.flags = (ev == kEvDead ? 1 : 0) | ((ev == kEvPanic && !(hend & 1)) ? 2 : 0);
     r.reserved = 0;
+#ifdef SALN_WALK_PROF
+    {
+        const uint64_t tt = SALN_PROF_T() - p_t0;
+        r.score = (int32_t)(tt >> 4);
+        r.status = (int32_t)(p_twait >> 4);
+        r.cigar_len = (uint32_t)(p_tsync >> 4);
+        r.flags = (uint8_t)min(p_sync, 255u);
+        r.reserved = (uint8_t)min(p_iter >> 2, 255u);
+    }
+#endif
 #ifdef SALN_WALK_CHECK
     if (dbg_n) {
         r.flags |= 4;
@@ -524,13 +666,15 @@ template <int G, int K>
 __global__ __launch_bounds__(256) void nw_traceback_lds_kernel(
     const NwPairDesc *__restrict__ pairs, uint32_t first, uint32_t n,
     const uint8_t *__restrict__ mask, const int32_t *__restrict__ end_h,
-    saln_nw_result *__restrict__ results, uint32_t *__restrict__ cigar, Scoring sc) {
-    __shared__ __attribute__((aligned(16))) uint8_t win_all[4 * kWaveLds];
+    uint32_t *__restrict__ ops, saln_nw_result *__restrict__ results,
+    uint32_t *__restrict__ cigar, Scoring sc) {
+    constexpr uint32_t kWave = WalkGeo<K>::kWaveLds;
+    __shared__ __attribute__((aligned(16))) uint8_t win_all[4 * kWave];
     const uint32_t idx = first + blockIdx.x * blockDim.x + threadIdx.x;
     if (idx >= first + n) return;
     const NwPairDesc p = pairs[idx];
-    walk_pair_lds<G, K>(p, end_h[idx], mask, results, cigar, sc,
-                        (lds_u8 *)(win_all + (threadIdx.x / 64u) * kWaveLds));
+    walk_pair_lds<G, K>(p, end_h[idx], mask, ops, results, cigar, sc,
+                        (lds_u8 *)(win_all + (threadIdx.x / 64u) * kWave));
 }
 
 // One walker per pair.  Pairs with an empty side have no mask and take the
@@ -736,7 +880,10 @@ struct PkMask {
     uint32_t w[(K + 3) / 4];
 };
 
-template <int G, int K>
+// kWalk: store walk codes only (argM/argI/argD, I-open, D-open, eq) - the
+// bits the device walker reads; the extend bits (3, 5) are left 0.  Full
+// codes (every parent set) are kept for the dense-mask / render paths.
+template <int G, int K, bool kWalk>
 __global__ __launch_bounds__(256) void nw_fill_pk_kernel(const NwPairDesc *__restrict__ pairs,
                                                          uint32_t first, uint32_t count,
                                                          const uint8_t *__restrict__ qs,
@@ -835,17 +982,21 @@ __global__ __launch_bounds__(256) void nw_fill_pk_kernel(const NwPairDesc *__res
                 const s16x2 Hc = as_s2(as_u(H) & 0xFFFEFFFEu);
                 const s16x2 tO = M + kOpen;
                 // sign set <=> parent absent.  Extend/open ties are decided on
-                // the flag-free order: ext <=> (X|1) >= tO, open <=> (tO|1) >= X.
+                // the flag-free order: with X = 2x+f, tO = 2o+g,
+                // ext <=> x >= o <=> X >= (tO & ~1),  open <=> o >= x <=> (tO | 1) >= X.
                 const s16x2 tOr = as_s2(as_u(tO) | 0x00010001u);
-                const s16x2 Ir = as_s2(as_u(I) | 0x00010001u);
-                const s16x2 Dr = as_s2(as_u(D) | 0x00010001u);
                 const uint32_t s0 = as_u(M - Hc), s1 = as_u(I - Hc), s2 = as_u(D - Hc);
-                const uint32_t s3 = as_u(Ir - tO), s4 = as_u(tOr - I);
-                const uint32_t s5 = as_u(Dr - tO), s6 = as_u(tOr - D);
-                uint32_t a = sign_bytes(s0, s1) & 0x02010201u;
-                a = (sign_bytes(s2, s3) & 0x08040804u) | a;
-                a = (sign_bytes(s4, s5) & 0x20102010u) | a;
+                const uint32_t s4 = as_u(tOr - I), s6 = as_u(tOr - D);
                 const uint32_t s7 = as_u(pen - spl(1));  // sign <=> q == d (bit 7)
+                uint32_t a = sign_bytes(s0, s1) & 0x02010201u;
+                if constexpr (kWalk) {
+                    a = (sign_bytes(s2, s4) & 0x10041004u) | a;
+                } else {
+                    const s16x2 tOc = as_s2(as_u(tO) & 0xFFFEFFFEu);
+                    const uint32_t s3 = as_u(I - tOc), s5 = as_u(D - tOc);
+                    a = (sign_bytes(s2, s3) & 0x08040804u) | a;
+                    a = (sign_bytes(s4, s5) & 0x20102010u) | a;
+                }
                 a = (sign_bytes(s6, s7) & 0x80408040u) | a;
                 acc[k % 4] = a;
                 if (k % 4 == 3 || k == K - 1) {
@@ -909,15 +1060,19 @@ static void fill_i32(dim3 grid, hipStream_t s, const NwPairDesc *pairs, uint32_t
 template <int G, int K>
 static void fill_pk(dim3 grid, hipStream_t s, const NwPairDesc *pairs, uint32_t first,
                     uint32_t count, const uint8_t *qs, const uint8_t *ds, uint8_t *mask,
-                    int32_t *end_h, saln_nw_result *res, uint32_t *cig, Scoring sc) {
-    nw_fill_pk_kernel<G, K><<<grid, dim3(256), 0, s>>>(pairs, first, count, qs, ds, mask, end_h,
-                                                        res, cig, sc);
+                    int32_t *end_h, saln_nw_result *res, uint32_t *cig, Scoring sc, bool full) {
+    if (full)
+        nw_fill_pk_kernel<G, K, false><<<grid, dim3(256), 0, s>>>(pairs, first, count, qs, ds,
+                                                                   mask, end_h, res, cig, sc);
+    else
+        nw_fill_pk_kernel<G, K, true><<<grid, dim3(256), 0, s>>>(pairs, first, count, qs, ds,
+                                                                  mask, end_h, res, cig, sc);
 }
 
 hipError_t launch_fill(int variant, const NwPairDesc *pairs, uint32_t first, uint32_t count,
                        const uint8_t *qs, const uint8_t *ds, uint8_t *mask, int2 *scratch,
                        int32_t *end_h, saln_nw_result *res, uint32_t *cig, Scoring sc,
-                       hipStream_t stream) {
+                       bool full_codes, hipStream_t stream) {
     if (count == 0) return hipSuccess;
     const uint32_t gpb = 256 / kVariants[variant].G;  // lane groups per block
     const uint32_t groups = kPacked[variant] ? (count + 1) / 2 : count;
@@ -927,20 +1082,20 @@ hipError_t launch_fill(int variant, const NwPairDesc *pairs, uint32_t first, uin
         case 1: fill_i32<16, 16>(grid, stream, pairs, first, count, qs, ds, mask, scratch, end_h, res, cig, sc); break;
         case 2: fill_i32<64, 8>(grid, stream, pairs, first, count, qs, ds, mask, scratch, end_h, res, cig, sc); break;
         case 3: fill_i32<64, 16>(grid, stream, pairs, first, count, qs, ds, mask, scratch, end_h, res, cig, sc); break;
-        case 4: fill_pk<8, 19>(grid, stream, pairs, first, count, qs, ds, mask, end_h, res, cig, sc); break;
-        case 5: fill_pk<16, 16>(grid, stream, pairs, first, count, qs, ds, mask, end_h, res, cig, sc); break;
-        case 7: fill_pk<16, 10>(grid, stream, pairs, first, count, qs, ds, mask, end_h, res, cig, sc); break;
-        default: fill_pk<32, 16>(grid, stream, pairs, first, count, qs, ds, mask, end_h, res, cig, sc); break;
+        case 4: fill_pk<8, 19>(grid, stream, pairs, first, count, qs, ds, mask, end_h, res, cig, sc, full_codes); break;
+        case 5: fill_pk<16, 16>(grid, stream, pairs, first, count, qs, ds, mask, end_h, res, cig, sc, full_codes); break;
+        case 7: fill_pk<16, 10>(grid, stream, pairs, first, count, qs, ds, mask, end_h, res, cig, sc, full_codes); break;
+        default: fill_pk<32, 16>(grid, stream, pairs, first, count, qs, ds, mask, end_h, res, cig, sc, full_codes); break;
     }
     return hipGetLastError();
 }
 
 template <int G, int K>
 static void tb_lds(dim3 grid, hipStream_t s, const NwPairDesc *pairs, uint32_t first, uint32_t n,
-                   const uint8_t *mask, const int32_t *end_h, saln_nw_result *res, uint32_t *cig,
-                   Scoring sc) {
-    nw_traceback_lds_kernel<G, K><<<grid, dim3(256), 0, s>>>(pairs, first, n, mask, end_h, res,
-                                                              cig, sc);
+                   const uint8_t *mask, const int32_t *end_h, uint32_t *ops, saln_nw_result *res,
+                   uint32_t *cig, Scoring sc) {
+    nw_traceback_lds_kernel<G, K><<<grid, dim3(256), 0, s>>>(pairs, first, n, mask, end_h, ops,
+                                                              res, cig, sc);
 }
 
 // Traceback of plan range [first, first+n).  variant >= 0: all pairs of that
@@ -948,18 +1103,18 @@ static void tb_lds(dim3 grid, hipStream_t s, const NwPairDesc *pairs, uint32_t f
 // walker (pairs with an empty side, or any variant).
 hipError_t launch_traceback(int variant, const NwPairDesc *pairs, uint32_t first, uint32_t n,
                             const uint8_t *qs, const uint8_t *ds, const uint8_t *mask,
-                            const int32_t *end_h, saln_nw_result *results, uint32_t *cigar,
-                            Scoring sc, hipStream_t stream) {
+                            const int32_t *end_h, uint32_t *ops, saln_nw_result *results,
+                            uint32_t *cigar, Scoring sc, hipStream_t stream) {
     if (n == 0) return hipSuccess;
     const dim3 grid((n + 255) / 256);
     switch (variant) {
-        case 0: tb_lds<16, 10>(grid, stream, pairs, first, n, mask, end_h, results, cigar, sc); break;
-        case 1: tb_lds<16, 16>(grid, stream, pairs, first, n, mask, end_h, results, cigar, sc); break;
-        case 2: tb_lds<64, 8>(grid, stream, pairs, first, n, mask, end_h, results, cigar, sc); break;
-        case 3: tb_lds<64, 16>(grid, stream, pairs, first, n, mask, end_h, results, cigar, sc); break;
-        case 5: tb_lds<16, 16>(grid, stream, pairs, first, n, mask, end_h, results, cigar, sc); break;
-        case 6: tb_lds<32, 16>(grid, stream, pairs, first, n, mask, end_h, results, cigar, sc); break;
-        case 7: tb_lds<16, 10>(grid, stream, pairs, first, n, mask, end_h, results, cigar, sc); break;
+        case 0: tb_lds<16, 10>(grid, stream, pairs, first, n, mask, end_h, ops, results, cigar, sc); break;
+        case 1: tb_lds<16, 16>(grid, stream, pairs, first, n, mask, end_h, ops, results, cigar, sc); break;
+        case 2: tb_lds<64, 8>(grid, stream, pairs, first, n, mask, end_h, ops, results, cigar, sc); break;
+        case 3: tb_lds<64, 16>(grid, stream, pairs, first, n, mask, end_h, ops, results, cigar, sc); break;
+        case 5: tb_lds<16, 16>(grid, stream, pairs, first, n, mask, end_h, ops, results, cigar, sc); break;
+        case 6: tb_lds<32, 16>(grid, stream, pairs, first, n, mask, end_h, ops, results, cigar, sc); break;
+        case 7: tb_lds<16, 10>(grid, stream, pairs, first, n, mask, end_h, ops, results, cigar, sc); break;
         default: {  // variant 4 (20-byte segments) and empty-side pairs
             GeomTable gt;
             for (int v = 0; v < kNumVariants; ++v) gt.g[v] = kVariants[v];
