@@ -42,7 +42,7 @@ static int run_batch(saln_context *ctx, const uint8_t *q_seq, const uint64_t *q_
                      const uint32_t *pair_q, const uint32_t *pair_db, uint64_t n_pairs,
                      int32_t mode, const saln_nw_scoring *scoring, saln_nw_result *results,
                      uint32_t *cigar, const uint64_t *cigar_off,
-                     std::vector<std::vector<uint8_t>> *masks_out) {
+                     std::vector<PairMask> *masks_out) {
     PlanGuard g;
     int rc = saln_nw_plan_create(ctx, q_off, n_q, db_off, n_db, pair_q, pair_db, n_pairs, mode,
                                  scoring, &g.p);
@@ -107,19 +107,15 @@ static int run_batch(saln_context *ctx, const uint8_t *q_seq, const uint64_t *q_
         if (masks_out) masks_out->resize(n_pairs);
         for (uint64_t k = 0; k < n_pairs; ++k) {
             if (!need[k] && !masks_out) continue;
-            std::vector<uint8_t> m;
-            Geom geo{16, 10};
-            rc = plan_pair_mask(src, masks_out ? k : idx2[k], &m, &geo);
+            PairMask m;
+            rc = plan_pair_mask(src, masks_out ? k : idx2[k], &m);
             if (rc != SALN_OK) return rc;
             if (need[k]) {
                 const uint64_t qi = pair_q ? pair_q[k] : k % n_q;
                 const uint64_t di = pair_db ? pair_db[k] : k / n_q;
-                HostMask hm;
-                hm.m = m.data();
-                hm.g = geo;
-                hm.lq = (uint32_t)(q_off[qi + 1] - q_off[qi]);
-                hm.ld = (uint32_t)(db_off[di + 1] - db_off[di]);
-                hm.sc = scoring_or_default(scoring);
+                const HostMask hm(m, (uint32_t)(q_off[qi + 1] - q_off[qi]),
+                                  (uint32_t)(db_off[di + 1] - db_off[di]),
+                                  scoring_or_default(scoring));
                 std::vector<uint32_t> c;
                 const bool printed = first_alignment(hm, q_seq + q_off[qi], db_seq + db_off[di], &c);
                 results[k].printed = printed ? 1 : 0;
@@ -177,7 +173,7 @@ int saln_nw_render(saln_context *ctx, const uint8_t *q, uint64_t len_q, const ui
     const uint64_t qo[2] = {0, len_q}, dof[2] = {0, len_db};
     const uint32_t z = 0;
     saln_nw_result r;
-    std::vector<std::vector<uint8_t>> masks;
+    std::vector<PairMask> masks;
     int rc = run_batch(ctx, q, qo, 1, d, dof, 1, &z, &z, 1, mode, nullptr, &r, nullptr, nullptr,
                        &masks);
     if (rc == SALN_NOT_IMPLEMENTED) {
@@ -187,11 +183,7 @@ int saln_nw_render(saln_context *ctx, const uint8_t *q, uint64_t len_q, const ui
         return rc;
     }
     if (rc != SALN_OK) return rc;
-    HostMask hm;
-    hm.m = masks[0].data();
-    hm.g = variant_geom(choose_variant((uint32_t)len_q, (uint32_t)len_db, hm.sc));
-    hm.lq = (uint32_t)len_q;
-    hm.ld = (uint32_t)len_db;
+    const HostMask hm(masks[0], (uint32_t)len_q, (uint32_t)len_db, scoring_or_default(nullptr));
     std::string text;
     const DfsOutcome o = render_blocks(hm, q, d, max_blocks, &text);
     if (out_len) *out_len = text.size();
@@ -210,16 +202,11 @@ int saln_nw_dense_mask(saln_context *ctx, const uint8_t *q, uint64_t len_q, cons
     const uint64_t qo[2] = {0, len_q}, dof[2] = {0, len_db};
     const uint32_t z = 0;
     saln_nw_result r;
-    std::vector<std::vector<uint8_t>> masks;
+    std::vector<PairMask> masks;
     int rc = run_batch(ctx, q, qo, 1, d, dof, 1, &z, &z, 1, SALN_MODE_GLOBAL, scoring, &r,
                        nullptr, nullptr, &masks);
     if (rc != SALN_OK) return rc;
-    HostMask hm;
-    hm.m = masks[0].data();
-    hm.sc = scoring_or_default(scoring);
-    hm.g = variant_geom(choose_variant((uint32_t)len_q, (uint32_t)len_db, hm.sc));
-    hm.lq = (uint32_t)len_q;
-    hm.ld = (uint32_t)len_db;
+    const HostMask hm(masks[0], (uint32_t)len_q, (uint32_t)len_db, scoring_or_default(scoring));
     hm.to_dense(out);
     return SALN_OK;
 }

@@ -38,51 +38,42 @@ enum : uint8_t {
 // One pair as the fill/traceback kernels see it (plan order).
 struct NwPairDesc {
     uint64_t q_off, db_off;  // byte offsets into the query / db sequence buffers
-    uint64_t mask_off;       // byte offset of this pair's parent mask in the workspace
+    uint64_t mask_off;       // byte offset of this pair's segment (row 1, block 0) in the workspace
+    uint64_t mask_rs;        // bytes from row i to row i+1 of the pair's mask
     uint64_t cigar_off;      // word offset of this pair's cigar (in results order)
     uint64_t scratch_off;    // int2 offset of the chunk-boundary column (multi-chunk pairs)
-    uint64_t ops_off;        // word offset of the traceback's 2-bit op stream (walker scratch)
+    uint64_t ops_off;        // word offset of the traceback's op stream (walker scratch)
+    uint32_t mask_bs;        // bytes from column block b to b+1
     uint32_t len_q, len_db;
     uint32_t pair_id;        // index into results
     uint32_t variant;        // fill kernel variant (kernel geometry)
+    uint32_t reserved;
 };
 
 // Kernel geometry of one fill variant: G lanes per pair, K query columns per
 // lane, KD = ceil(K/4) mask dwords per lane-row segment (LB = 4*KD bytes).
-// A pair's query is cut in chunks of W = G*K columns.  Within a chunk, lane
-// `lane` computes row r = t - lane + 1 at step t (t = 0 .. len_db+G-2).
-// Mask layout (step tiles): [chunk][t / R][lane][t % R][LB bytes].  Each lane
-// buffers R step-segments in registers and a group stores a whole tile
-// (G*R*LB contiguous bytes) at once; a lane block's consecutive rows are
-// adjacent inside a tile, so the traceback walk reuses each fetched line for
-// up to R rows.
-constexpr uint32_t kTileSteps = 4;  // R
-
+// A pair's query is cut in chunks of W = G*K columns; column block
+// b = (j-1)/K (chunk b/G, lane b%G).  Within a chunk, lane `lane` computes
+// row r = t - lane + 1 at step t (t = 0 .. len_db+G-2).
+// Mask layout (row-major, block-interleaved): the K codes of block b at row i
+// are one LB-byte segment at mask_off + (i-1)*rs + b*bs.  A plan interleaves
+// the segments of up to 64 consecutive pairs of a variant (one traceback
+// wave): bs = n*LB and pair slot s sits at +s*LB, so the walker's per-lane
+// loads of one (row, block) touch adjacent bytes and the fill's stores of a
+// row are contiguous across the pairs of a wave.  A pair outside such a pack
+// has bs = LB and rs = (blocks)*LB.
 struct Geom {
     uint32_t G, K;
     SALN_HD uint32_t KD() const { return (K + 3) / 4; }
     SALN_HD uint32_t LB() const { return KD() * 4; }
     SALN_HD uint32_t W() const { return G * K; }
     SALN_HD uint32_t n_chunks(uint32_t len_q) const { return (len_q + W() - 1) / W(); }
+    SALN_HD uint32_t n_blocks(uint32_t len_q) const { return n_chunks(len_q) * G; }
     SALN_HD uint32_t steps(uint32_t len_db) const { return len_db + G - 1; }
-    SALN_HD uint32_t tiles(uint32_t len_db) const {
-        return (steps(len_db) + kTileSteps - 1) / kTileSteps;
-    }
-    SALN_HD uint64_t tile_bytes() const { return (uint64_t)G * kTileSteps * LB(); }
-    SALN_HD uint64_t chunk_bytes(uint32_t len_db) const { return tiles(len_db) * tile_bytes(); }
-    SALN_HD uint64_t mask_bytes(uint32_t len_q, uint32_t len_db) const {
-        return (uint64_t)n_chunks(len_q) * chunk_bytes(len_db);
-    }
-    // segment of (chunk-local) lane `lane` at step t, relative to its chunk
-    SALN_HD uint64_t seg_step(uint32_t lane, uint32_t t) const {
-        return (uint64_t)(t / kTileSteps) * tile_bytes() + (uint64_t)lane * kTileSteps * LB() +
-               (uint64_t)(t % kTileSteps) * LB();
-    }
-    // byte offset (within the pair's mask) of interior cell (i, j), 1-based.
-    SALN_HD uint64_t cell(uint32_t i, uint32_t j, uint32_t len_db) const {
+    // byte offset (from mask_off) of interior cell (i, j), 1-based
+    SALN_HD uint64_t cell(uint32_t i, uint32_t j, uint64_t rs, uint32_t bs) const {
         const uint32_t jj0 = j - 1;
-        const uint32_t c = jj0 / W(), lane = (jj0 % W()) / K, k = jj0 % K;
-        return (uint64_t)c * chunk_bytes(len_db) + seg_step(lane, i - 1 + lane) + k;
+        return (uint64_t)(i - 1) * rs + (uint64_t)(jj0 / K) * bs + jj0 % K;
     }
 };
 

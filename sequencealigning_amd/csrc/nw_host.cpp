@@ -56,6 +56,7 @@ struct saln_nw_plan {
     std::vector<uint32_t> plan_index;  // results index -> plan order
     NwPairDesc *d_pairs = nullptr;
     uint32_t var_first[kNumVariants] = {}, var_count[kNumVariants] = {};
+    uint32_t var_maxld[kNumVariants] = {};  // longest db of each variant's pairs
     uint32_t n_fill = 0;  // plan order: [0, n_fill) filled pairs, then empty-side pairs
     uint8_t *d_mask = nullptr;
     uint8_t *d_mask2 = nullptr;  // second workspace for the async (2-deep) pipeline
@@ -197,25 +198,25 @@ int saln_nw_plan_create(saln_context *ctx, const uint64_t *q_off, uint64_t n_q,
         p->cells += lq * ld;
     }
     p->cigar_off[n_pairs] = cig;
-    // plan order: fill pairs grouped by variant, longest db first (balances
-    // the groups of a block); pairs with an empty side last (traceback only).
+    // plan order: fill pairs grouped by variant, then by query chunk count,
+    // longest db first (balances the groups of a block and keeps the pairs of
+    // a mask pack alike); pairs with an empty side last (traceback only).
     std::vector<uint32_t> order(n_pairs);
     std::iota(order.begin(), order.end(), 0u);
     auto key = [&](uint32_t k) {
         const NwPairDesc &d = descs[k];
         const bool empty = d.len_q == 0 || d.len_db == 0;
-        return std::make_tuple(empty ? (uint32_t)kNumVariants : d.variant, ~d.len_db, k);
+        const uint32_t nch = empty ? 0 : variant_geom((int)d.variant).n_chunks(d.len_q);
+        return std::make_tuple(empty ? (uint32_t)kNumVariants : d.variant, ~nch, ~d.len_db, k);
     };
     std::sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return key(a) < key(b); });
     p->h_pairs.resize(n_pairs);
-    uint64_t moff = 0, soff = 0, ooff = 0;
+    uint64_t soff = 0, ooff = 0;
     for (uint64_t r = 0; r < n_pairs; ++r) {
         NwPairDesc d = descs[order[r]];
         const bool empty = d.len_q == 0 || d.len_db == 0;
         if (!empty) {
             const Geom g = variant_geom((int)d.variant);
-            d.mask_off = moff;
-            moff += (g.mask_bytes(d.len_q, d.len_db) + 255) & ~255ull;
             d.ops_off = ooff;
             ooff += (d.len_q + d.len_db + 9) / 10 + 1;  // 3-bit ops, ten per word
             if (g.n_chunks(d.len_q) > 1) {
@@ -224,9 +225,47 @@ int saln_nw_plan_create(saln_context *ctx, const uint64_t *q_off, uint64_t n_q,
             }
             if (p->var_count[d.variant] == 0) p->var_first[d.variant] = (uint32_t)r;
             p->var_count[d.variant]++;
+            p->var_maxld[d.variant] = std::max(p->var_maxld[d.variant], d.len_db);
             p->n_fill++;
         }
         p->h_pairs[r] = d;
+    }
+    // Mask packs: up to 64 consecutive pairs of a variant (one traceback
+    // wave) with interleaved segments (nw_common.hpp Geom), unless padding
+    // them to the pack's longest db / widest query would cost over 25 % more
+    // than storing them apart.
+    uint64_t moff = 0;
+    for (int v = 0; v < kNumVariants; ++v) {
+        const Geom g = variant_geom(v);
+        const uint64_t lb = g.LB();
+        for (uint32_t a = p->var_first[v], e = a + p->var_count[v]; a < e; a += 64) {
+            const uint32_t np = std::min<uint32_t>(64, e - a);
+            uint64_t rows = 0, nbm = 0, own = 0;
+            for (uint32_t s = 0; s < np; ++s) {
+                const NwPairDesc &d = p->h_pairs[a + s];
+                rows = std::max<uint64_t>(rows, d.len_db);
+                nbm = std::max<uint64_t>(nbm, g.n_blocks(d.len_q));
+                own += (uint64_t)d.len_db * g.n_blocks(d.len_q) * lb;
+            }
+            const uint64_t packed = rows * nbm * np * lb;
+            if (4 * packed <= 5 * own + 4096) {
+                for (uint32_t s = 0; s < np; ++s) {
+                    NwPairDesc &d = p->h_pairs[a + s];
+                    d.mask_off = moff + s * lb;
+                    d.mask_bs = (uint32_t)(np * lb);
+                    d.mask_rs = nbm * np * lb;
+                }
+                moff += (packed + 255) & ~255ull;
+            } else {
+                for (uint32_t s = 0; s < np; ++s) {
+                    NwPairDesc &d = p->h_pairs[a + s];
+                    d.mask_off = moff;
+                    d.mask_bs = (uint32_t)lb;
+                    d.mask_rs = g.n_blocks(d.len_q) * lb;
+                    moff += ((uint64_t)d.len_db * d.mask_rs + 255) & ~255ull;
+                }
+            }
+        }
     }
     {
         // sub-batches for fill/traceback overlap inside one execute
@@ -348,7 +387,7 @@ int saln_nw_execute(saln_nw_plan *p, const uint8_t *d_q, const uint8_t *d_db,
             const uint32_t b = std::min(hi, p->var_first[v] + p->var_count[v]);
             if (a < b)
                 HIP_TRY(launch_fill(v, p->d_pairs, a, b - a, d_q, d_db, mask, p->d_scratch, endh,
-                                    d_results, d_cigar, p->sc, p->full_codes, s));
+                                    d_results, d_cigar, p->sc, p->full_codes, p->var_maxld[v], s));
         }
         if (ev && k + 1 == nsub) HIP_TRY(hipEventRecord(ev[1], s));
         HIP_TRY(hipEventRecord(p->sync_ev[k], s));
@@ -437,21 +476,27 @@ int plan_set_full_codes(saln_nw_plan *p, bool full) {
     return SALN_OK;
 }
 
-int plan_pair_mask(const saln_nw_plan *p, uint64_t pair_id, std::vector<uint8_t> *mask,
-                   Geom *geo) {
+int plan_pair_mask(const saln_nw_plan *p, uint64_t pair_id, PairMask *pm) {
     if (!p || pair_id >= p->n_pairs) return SALN_E_INVALID;
     const NwPairDesc &d = p->h_pairs[p->plan_index[pair_id]];
     if (!p->full_codes && variant_packed((int)d.variant)) {
         set_error("plan_pair_mask: plan stores walk codes only");
         return SALN_E_INVALID;
     }
-    *geo = variant_geom((int)d.variant);
-    mask->clear();
+    pm->g = variant_geom((int)d.variant);
+    pm->m.clear();
+    pm->rs = 0;
+    pm->bs = pm->g.LB();
     if (d.len_q == 0 || d.len_db == 0) return SALN_OK;
-    const uint64_t n = geo->mask_bytes(d.len_q, d.len_db);
-    mask->resize(n);
+    // every row holds rs / bs blocks (the pack's width); copy them all as
+    // LB-byte rows of one bs-pitched 2-D region
+    const uint64_t nb = d.mask_rs / d.mask_bs;
+    const uint64_t lb = pm->g.LB();
+    pm->rs = nb * lb;
+    pm->m.resize((uint64_t)d.len_db * nb * lb);
     HIP_TRY(hipSetDevice(p->ctx->device));
-    HIP_TRY(hipMemcpy(mask->data(), p->d_mask + d.mask_off, n, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy2D(pm->m.data(), lb, p->d_mask + d.mask_off, d.mask_bs, lb,
+                        (uint64_t)d.len_db * nb, hipMemcpyDeviceToHost));
     return SALN_OK;
 }
 

@@ -15,7 +15,7 @@ namespace saln {
 hipError_t launch_fill(int variant, const NwPairDesc *pairs, uint32_t first, uint32_t count,
                        const uint8_t *qs, const uint8_t *ds, uint8_t *mask, int2 *scratch,
                        int32_t *end_h, saln_nw_result *results, uint32_t *cigar, Scoring sc,
-                       bool full_codes, hipStream_t stream);
+                       bool full_codes, uint32_t ld_max, hipStream_t stream);
 hipError_t launch_traceback(int variant, const NwPairDesc *pairs, uint32_t first, uint32_t n,
                             const uint8_t *qs,
                             const uint8_t *ds, const uint8_t *mask, const int32_t *end_h,
@@ -28,14 +28,28 @@ int choose_variant(uint32_t len_q, uint32_t len_db, const Scoring &sc);
 void set_error(const std::string &msg);
 Scoring scoring_or_default(const saln_nw_scoring *s);
 
+// Host copy of one pair's parent codes: LB-byte segments, row-major, with
+// row stride rs and block stride bs (nw_common.hpp Geom).
+struct PairMask {
+    std::vector<uint8_t> m;
+    Geom g{16, 10};
+    uint64_t rs = 0;
+    uint32_t bs = 0;
+};
+
 // Random access to one pair's parent codes (kernel layout + boundary rules).
 struct HostMask {
     const uint8_t *m = nullptr;  // pair's mask bytes (host copy)
     Geom g{16, 10};
+    uint64_t rs = 0;
+    uint32_t bs = 0;
     uint32_t lq = 0, ld = 0;
     Scoring sc{5, -4, -8, -6};
+    HostMask() = default;
+    HostMask(const PairMask &pm, uint32_t lq_, uint32_t ld_, const Scoring &sc_)
+        : m(pm.m.data()), g(pm.g), rs(pm.rs), bs(pm.bs), lq(lq_), ld(ld_), sc(sc_) {}
     // codes are stored inverted (bit set = parent absent)
-    uint8_t byte(uint32_t i, uint32_t j) const { return m[g.cell(i, j, ld)] ^ 0x7F; }
+    uint8_t byte(uint32_t i, uint32_t j) const { return m[g.cell(i, j, rs, bs)] ^ 0x7F; }
     uint8_t argmax(uint32_t i, uint32_t j) const {
         if (i == 0) return argmax_row0(sc, j);
         if (j == 0) return argmax_col0(sc, i);
@@ -55,10 +69,9 @@ struct HostMask {
 // export) instead of the walk codes a plan stores by default.
 int plan_set_full_codes(saln_nw_plan *plan, bool full);
 
-// Copies one pair's parent codes (kernel layout) from a plan's workspace
-// after execute; pair_id is the results index.
-int plan_pair_mask(const saln_nw_plan *plan, uint64_t pair_id, std::vector<uint8_t> *mask,
-                   Geom *geo);
+// Copies one pair's parent codes from a plan's workspace after execute
+// (compact: bs = LB); pair_id is the results index.
+int plan_pair_mask(const saln_nw_plan *plan, uint64_t pair_id, PairMask *mask);
 
 // Reference DFS (needleman_wunsch_affine.rs:246-329) over the parent codes.
 struct DfsOutcome {

@@ -12,9 +12,10 @@
 // (the row's I candidate leaving the lane's last column and the last
 // column's H), fused as update_dpp moves.  Each lane keeps its previous-row
 // H and next-row D for its K columns in registers; nothing else of the matrix
-// is stored except the 7-bit parent code per cell (1 B/cell), written
-// [step][lane][ceil(K/4) dwords] so every step is one contiguous store per
-// group.
+// is stored except the parent code per cell (1 B/cell), one ceil(K/4)-dword
+// segment per lane and step, in the block-interleaved row-major layout of
+// nw_common.hpp (Geom): the segments of one row and block of the pairs of a
+// pack (64 consecutive pairs of a variant) are adjacent.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -35,6 +36,19 @@ __device__ __forceinline__ int32_t shr1(int32_t old, int32_t v) {
         return __builtin_amdgcn_update_dpp(old, v, 0x138 /*wave_shr:1*/, 0xf, 0xf, false);
 }
 
+// Workgroups are dispatched round-robin over the 8 XCDs (block i -> XCD
+// i % 8).  The bpp workgroups that fill one pack (64 consecutive pairs whose
+// mask rows are interleaved) are remapped onto one XCD, so the partial lines
+// they write meet in one L2.  The grid is a multiple of 8*bpp.
+__device__ __forceinline__ uint32_t pack_block(uint32_t bpp) {
+    const uint32_t i = blockIdx.x, sup = 8u * bpp;
+    const uint32_t r = i % sup;
+    return i - r + (r % 8u) * bpp + r / 8u;
+}
+constexpr uint32_t blocks_per_pack(uint32_t pairs_per_block) {
+    return pairs_per_block >= 64 ? 1u : 64u / pairs_per_block;
+}
+
 // --------------------------------------------------------------- traceback
 struct GeomTable {
     Geom g[kNumVariants];
@@ -43,10 +57,11 @@ struct GeomTable {
 struct MaskCell {
     const uint8_t *m;
     Geom g;
-    uint32_t lq, ld;
+    uint64_t rs;
+    uint32_t bs;
     Scoring sc;
     // codes are stored inverted (bit set = parent absent)
-    __device__ uint8_t byte(uint32_t i, uint32_t j) const { return m[g.cell(i, j, ld)] ^ 0x7F; }
+    __device__ uint8_t byte(uint32_t i, uint32_t j) const { return m[g.cell(i, j, rs, bs)] ^ 0x7F; }
     __device__ uint8_t argmax(uint32_t i, uint32_t j) const {
         if (i == 0) return argmax_row0(sc, j);
         if (j == 0) return argmax_col0(sc, i);
@@ -79,7 +94,7 @@ __device__ __forceinline__ void walk_pair(const NwPairDesc &p, int32_t hend,
     const uint32_t lq = p.len_q, ld = p.len_db;
     const uint8_t *q = qs + p.q_off;
     const uint8_t *d = ds + p.db_off;
-    const MaskCell mc{mask + p.mask_off, geo, lq, ld, sc};
+    const MaskCell mc{mask + p.mask_off, geo, p.mask_rs, p.mask_bs, sc};
     const uint8_t am_end = mc.argmax(ld, lq);
     int st = (am_end & kArgD) ? kStD : ((am_end & kArgM) ? kStM : kStI);
     uint32_t i = ld, j = lq;
@@ -143,168 +158,9 @@ __device__ __forceinline__ void walk_pair(const NwPairDesc &p, int32_t hend,
     results[p.pair_id] = r;
 }
 
-// Streaming walker.  The mask of a pair is laid out [step][lane][KD dwords]
-// (nw_common.hpp Geom): the K columns of lane block L at row i are one
-// KD-dword segment at step i-1+L.  Walking back from the end cell the row
-// only decreases, so within a lane block the walker keeps a window of kWin
-// row segments in flight (slot s of a round holds row base-s) and refills a
-// slot as soon as the path leaves its row; a block change restarts the
-// window.  Every decision reads one byte of the cell the walk moves into:
-// bits 0-2 choose the state after a diagonal move (D > I > M), bits 3-4
-// (I parents) after a horizontal one, bits 5-6 (D parents) after a vertical
-// one, and bit 7 (query char == db char) names the M column '=' or 'X'.
-constexpr int kWin = 8;
-enum { kFromM = 0, kFromI = 1, kFromD = 2, kFromEnd = 3 };
-
-// named fields (not an array) so the dword select below stays in registers
-struct Seg {
-    uint32_t w0, w1, w2, w3, w4;
-};
-
-__device__ __forceinline__ Seg load_seg(const uint8_t *__restrict__ m, uint64_t off) {
-    const uint32_t *p = reinterpret_cast<const uint32_t *>(m + off);
-    return Seg{p[0], p[1], p[2], p[3], p[4]};
-}
-
-__device__ __forceinline__ uint32_t seg_byte(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3,
-                                             uint32_t w4, uint32_t k) {
-    const uint32_t d = k >> 2;
-    uint32_t w = d == 0 ? w0 : w1;
-    w = d >= 2 ? w2 : w;
-    w = d >= 3 ? w3 : w;
-    w = d >= 4 ? w4 : w;
-    return ((w >> (8 * (k & 3))) & 0xFFu) ^ 0x7Fu;  // decoded: bit set = parent present
-}
-
-__device__ __forceinline__ int next_state(int from, uint32_t b) {
-    switch (from) {
-        case kFromM: return (b & kArgD) ? kStD : ((b & kArgI) ? kStI : kStM);
-        case kFromI: return (b & kIOpen) ? kStM : kStI;
-        case kFromD: return (b & kDOpen) ? kStM : kStD;
-        default: return (b & kArgD) ? kStD : ((b & kArgM) ? kStM : kStI);
-    }
-}
-
-__device__ void walk_pair_stream(const NwPairDesc &p, int32_t hend,
-                                 const uint8_t *__restrict__ mask, Geom geo,
-                                 saln_nw_result *__restrict__ results,
-                                 uint32_t *__restrict__ cigar, Scoring sc) {
-    // Lock-step walker: every lane of the wave is in the same window phase S
-    // (0..kWin-1) with its target row == base - S; the phases are unrolled so
-    // each window slot is a fixed register set.  A lane whose walk changes
-    // column block re-bases its window (base = target row + S) to stay in
-    // phase.  Loads are unconditional (row clamped into the pair): a select on
-    // a loaded value would make the compiler wait for it on the spot.
-    const uint32_t K = geo.K, G = geo.G;
-    const uint64_t cb = geo.chunk_bytes(p.len_db);
-    const uint8_t *__restrict__ m = mask + p.mask_off;
-    uint32_t *out = cigar ? cigar + p.cigar_off : nullptr;
-    uint32_t nops = 0, run_op = 0, run_len = 0;
-    uint32_t ti = p.len_db, tj = p.len_q;  // target cell
-    int from = kFromEnd;                    // how the walk arrives at the target
-    uint8_t am_end = 0;
-    bool walking = true;
-    uint32_t B = (tj - 1) / K, L = B % G, base = ti;
-    const uint8_t *__restrict__ mc = m + (uint64_t)(B / G) * cb;
-    const int32_t ldi = (int32_t)p.len_db;
-    Seg w0, w1, w2, w3, w4, w5, w6, w7;
-#define SALN_ROW(S2, S) ((int32_t)((S2) >= (S) ? base - (S2) : base - (S2) - kWin))
-#define SALN_LOAD(W, ROW) \
-    W = load_seg(mc, geo.seg_step(L, (uint32_t)min(max((int32_t)(ROW), 1), ldi) - 1 + L))
-#define SALN_PHASE(W, S)                                                                    \
-    while (walking) {                                                                       \
-        if ((tj - 1) / K != B) { /* block change: re-base the window into phase S */        \
-            B = (tj - 1) / K;                                                               \
-            L = B % G;                                                                      \
-            mc = m + (uint64_t)(B / G) * cb;                                                \
-            base = ti + (S);                                                                \
-            SALN_LOAD(w0, SALN_ROW(0, S)); SALN_LOAD(w1, SALN_ROW(1, S));                   \
-            SALN_LOAD(w2, SALN_ROW(2, S)); SALN_LOAD(w3, SALN_ROW(3, S));                   \
-            SALN_LOAD(w4, SALN_ROW(4, S)); SALN_LOAD(w5, SALN_ROW(5, S));                   \
-            SALN_LOAD(w6, SALN_ROW(6, S)); SALN_LOAD(w7, SALN_ROW(7, S));                   \
-        }                                                                                   \
-        const uint32_t b = seg_byte(W.w0, W.w1, W.w2, W.w3, W.w4, tj - 1 - B * K);          \
-        if (from == kFromEnd) am_end = (uint8_t)(b & 7);                                    \
-        const int st = next_state(from, b);                                                 \
-        const uint32_t op = st == kStI   ? SALN_CIGAR_I                                     \
-                            : st == kStD ? SALN_CIGAR_D                                     \
-                                         : ((b & 0x80u) ? SALN_CIGAR_EQ : SALN_CIGAR_X);     \
-        const bool brk = run_len != 0 && op != run_op;                                      \
-        if (brk && out) out[nops] = (run_len << 4) | run_op;                                \
-        nops += brk ? 1u : 0u;                                                              \
-        run_len = brk || run_len == 0 ? 1u : run_len + 1u;                                  \
-        run_op = op;                                                                        \
-        const uint32_t i0 = ti;                                                             \
-        ti -= st != kStI ? 1u : 0u;                                                         \
-        tj -= st != kStD ? 1u : 0u;                                                         \
-        from = st; /* kFromM/I/D == kStM/I/D */                                             \
-        if (ti == 0 || tj == 0) walking = false;                                            \
-        else if (ti != i0 && (tj - 1) / K == B) break; /* up one row: next phase */         \
-    }                                                                                       \
-    if (walking) SALN_LOAD(W, base - (S) - kWin);
-    SALN_LOAD(w0, SALN_ROW(0, 0)); SALN_LOAD(w1, SALN_ROW(1, 0));
-    SALN_LOAD(w2, SALN_ROW(2, 0)); SALN_LOAD(w3, SALN_ROW(3, 0));
-    SALN_LOAD(w4, SALN_ROW(4, 0)); SALN_LOAD(w5, SALN_ROW(5, 0));
-    SALN_LOAD(w6, SALN_ROW(6, 0)); SALN_LOAD(w7, SALN_ROW(7, 0));
-    while (walking) {
-        SALN_PHASE(w0, 0)
-        SALN_PHASE(w1, 1)
-        SALN_PHASE(w2, 2)
-        SALN_PHASE(w3, 3)
-        SALN_PHASE(w4, 4)
-        SALN_PHASE(w5, 5)
-        SALN_PHASE(w6, 6)
-        SALN_PHASE(w7, 7)
-        base -= kWin;
-    }
-#undef SALN_PHASE
-#undef SALN_LOAD
-#undef SALN_ROW
-    // boundary arrival at (ti, tj) (row or column 0) from state `from`
-    int ev, bst;
-    if (from == kFromM && ti == 0 && tj == 0) {
-        ev = kEvOrigin;
-    } else {
-        if (from == kFromM) {
-            const uint8_t a = ti == 0 ? argmax_row0(sc, tj) : argmax_col0(sc, ti);
-            bst = (a & kArgD) ? kStD : ((a & kArgI) ? kStI : kStM);
-        } else if (from == kFromI) {  // (ti, 0), ti >= 1
-            bst = (ibits_col1(sc, ti) & 2) ? kStM : kStI;
-        } else {  // kFromD: (0, tj), tj >= 1
-            bst = (dbits_row1(sc, tj) & 2) ? kStM : kStD;
-        }
-        // expanding a boundary node: D[0][j>=1] / I[i>=1][0] panic; other
-        // non-origin boundary nodes are parentless sentinels (dead ends)
-        if (bst == kStD && ti == 0 && tj >= 1) ev = kEvPanic;
-        else if (bst == kStI && tj == 0 && ti >= 1) ev = kEvPanic;
-        else ev = kEvDead;
-    }
-    if (run_len) {
-        if (out) out[nops] = (run_len << 4) | run_op;
-        ++nops;
-    }
-    if (ev != kEvOrigin) nops = 0;
-    if (out) {
-        for (uint32_t a = 0, b = nops ? nops - 1 : 0; a < b; ++a, --b) {
-            const uint32_t tmp = out[a];
-            out[a] = out[b];
-            out[b] = tmp;
-        }
-    }
-    saln_nw_result r;
-    r.score = hend >> 1;
-    r.status = (hend & 1) ? SALN_REF_PANIC_BOUNDARY : SALN_OK;
-    r.cigar_len = nops;
-    r.end_states = am_end;
-    r.printed = ev == kEvOrigin ? 1 : 0;
-    r.flags = (ev == kEvDead ? 1 : 0) | ((ev == kEvPanic && !(hend & 1)) ? 2 : 0);
-    r.reserved = 0;
-    results[p.pair_id] = r;
-}
-
 // LDS-window walker (segments of <= 16 bytes, i.e. K <= 16).  Lock-step
-// phases as in walk_pair_stream (every lane in phase S, target row base-S),
-// but the windows live in LDS, filled by LDS-DMA (global_load_lds_dwordx{3,4}:
+// phases: every lane of the wave is in the same window phase S (0..W-1) with
+// its target row == base - S (phases unrolled).  The windows live in LDS, filled by LDS-DMA (global_load_lds_dwordx{3,4}:
 // lane l's bytes land at slot base + 16*l; the slot base is wave-uniform
 // because all lanes are in the same phase).  Block b lives in window b % NW
 // (WalkGeo); at the end of phase S every lane refills slot S of every window
@@ -402,7 +258,7 @@ constexpr uint64_t kNextLut = make_next_lut();
 // debug build: compare every window read with the byte in HBM
 #define SALN_WALK_CHECK_HOOK(S)                                                          \
     {                                                                                    \
-        const uint32_t tru = (uint32_t)m[geo.cell(ti, tj, p.len_db)];                   \
+        const uint32_t tru = (uint32_t)m[geo.cell(ti, tj, rs, bs)];                     \
         if (tru != raw) {                                                                \
             const uint32_t par = wc;                                                     \
             if (!dbg_n) dbg_info = (S) | (par << 3) | (((valid >> (par * 8u + (S))) & 1u) << 5) | \
@@ -421,10 +277,10 @@ __device__ void walk_pair_lds(const NwPairDesc &p, int32_t hend, const uint8_t *
                               uint32_t *__restrict__ cigar, Scoring sc, lds_u8 *win) {
     using WG = WalkGeo<K>;
     constexpr Geom geo{G, K};
-    constexpr uint32_t LB = WG::LB, NW = WG::NW, kW = WG::W;
-    constexpr uint32_t TB = G * kTileSteps * LB;  // tile bytes
+    constexpr uint32_t NW = WG::NW, kW = WG::W;
     constexpr uint32_t kAll = (1u << (8 * NW)) - 1u;
-    const uint64_t cb = geo.chunk_bytes(p.len_db);
+    const uint64_t rs = p.mask_rs;
+    const uint32_t bs = p.mask_bs;
     const uint8_t *__restrict__ m = mask + p.mask_off;
     uint32_t *out = cigar ? cigar + p.cigar_off : nullptr;
     uint32_t *const ops = ops_all + p.ops_off;
@@ -445,19 +301,16 @@ __device__ void walk_pair_lds(const NwPairDesc &p, int32_t hend, const uint8_t *
 #ifdef SALN_WALK_CHECK
     uint32_t dbg_n = 0, dbg_info = 0;
 #endif
-    // per-block segment base (chunk + lane offset) and lane index, for B, B-1, B-2
+    // per-block segment bases for B, B-1, B-2
     auto blk_base = [&](uint32_t blk) __attribute__((always_inline)) {
-        return m + (uint64_t)(blk / G) * cb + (blk % G) * (kTileSteps * LB);
+        return m + (uint64_t)blk * bs;
     };
     const uint8_t *bp0 = blk_base(B), *bp1 = blk_base(B >= 1 ? B - 1 : 0);
     const uint8_t *bp2 = blk_base(B >= 2 ? B - 2 : 0);
-    uint32_t L0 = B % G, L1 = (B >= 1 ? B - 1 : 0) % G, L2 = (B >= 2 ? B - 2 : 0) % G;
     (void)bp2;
-    (void)L2;
-    // global address of a segment at `row` (clamped to >= 1) given block base/lane
-    auto seg = [&](const uint8_t *bp, uint32_t L, int32_t row) __attribute__((always_inline)) {
-        const uint32_t t = (uint32_t)max(row, 1) - 1 + L;
-        return (const void *)(bp + (uint64_t)(t / kTileSteps) * TB + (t % kTileSteps) * LB);
+    // global address of a block's segment at `row` (clamped to >= 1)
+    auto seg = [&](const uint8_t *bp, int32_t row) __attribute__((always_inline)) {
+        return (const void *)(bp + (uint64_t)((uint32_t)max(row, 1) - 1) * rs);
     };
 #define SALN_ROW(S2, S) ((int32_t)((S2) >= (S) ? base - (S2) : base - (S2) - kW))
 #define SALN_DMA(WIN, SLOT, ADDR)                                                              \
@@ -468,12 +321,12 @@ __device__ void walk_pair_lds(const NwPairDesc &p, int32_t hend, const uint8_t *
     // window w holds the resident block congruent to w (mod NW)
 #define SALN_REFILL(S, ROW)                                                                    \
     {                                                                                          \
-        const void *a0 = seg(bp0, L0, ROW), *a1 = seg(bp1, L1, ROW);                           \
+        const void *a0 = seg(bp0, ROW), *a1 = seg(bp1, ROW);                                   \
         if constexpr (NW == 2) {                                                               \
             SALN_DMA(0, S, wc ? a1 : a0);                                                      \
             SALN_DMA(1, S, wc ? a0 : a1);                                                      \
         } else {                                                                               \
-            const void *a2 = seg(bp2, L2, ROW);                                                \
+            const void *a2 = seg(bp2, ROW);                                                    \
             /* window w gets block B - ((wc - w) mod 3) */                                     \
             SALN_DMA(0, S, wc == 0 ? a0 : wc == 1 ? a1 : a2);                                  \
             SALN_DMA(1, S, wc == 1 ? a0 : wc == 2 ? a1 : a2);                                  \
@@ -487,7 +340,7 @@ __device__ void walk_pair_lds(const NwPairDesc &p, int32_t hend, const uint8_t *
     if (!(valid & (1u << (wc * 8u + (S))))) {                                                  \
         const uint64_t tq0 = SALN_PROF_T();                                                    \
         ++p_sync;                                                                              \
-        const void *ac = seg(bp0, L0, (int32_t)(base - (S)));                                  \
+        const void *ac = seg(bp0, (int32_t)(base - (S)));                                      \
         if (wc == 0) { SALN_DMA(0, S, ac); }                                                   \
         __builtin_amdgcn_sched_barrier(0);                                                     \
         if (wc == 1) { SALN_DMA(1, S, ac); }                                                   \
@@ -533,15 +386,11 @@ __device__ void walk_pair_lds(const NwPairDesc &p, int32_t hend, const uint8_t *
                 wc = wc ? wc - 1u : NW - 1u;                                                   \
                 wrow = wbase + wc * WG::kWinBytes + (S) * WG::kSlotBytes;                      \
                 bp0 = bp1;                                                                     \
-                L0 = L1;                                                                       \
                 if constexpr (NW == 2) {                                                       \
                     bp1 = blk_base(B >= 1 ? B - 1 : 0);                                        \
-                    L1 = (B >= 1 ? B - 1 : 0) % G;                                             \
                 } else {                                                                       \
                     bp1 = bp2;                                                                 \
-                    L1 = L2;                                                                   \
                     bp2 = blk_base(B >= 2 ? B - 2 : 0);                                        \
-                    L2 = (B >= 2 ? B - 2 : 0) % G;                                             \
                 }                                                                              \
                 SALN_ENSURE(S)                                                                 \
             }                                                                                  \
@@ -637,7 +486,7 @@ __device__ void walk_pair_lds(const NwPairDesc &p, int32_t hend, const uint8_t *
     r.score = hend >> 1;
     r.status = (hend & 1) ? SALN_REF_PANIC_BOUNDARY : SALN_OK;
     r.cigar_len = nops;
-    r.end_states = (uint8_t)((m[geo.cell(p.len_db, p.len_q, p.len_db)] ^ 0x7Fu) & 7u);
+    r.end_states = (uint8_t)((m[geo.cell(p.len_db, p.len_q, rs, bs)] ^ 0x7Fu) & 7u);
     r.printed = ev == kEvOrigin ? 1 : 0;
     r.flags = (ev == kEvDead ? 1 : 0) | ((ev == kEvPanic && !(hend & 1)) ? 2 : 0);
     r.reserved = 0;
@@ -689,12 +538,8 @@ __global__ __launch_bounds__(256) void nw_traceback_kernel(
     if (idx >= first + n) return;
     const NwPairDesc p = pairs[idx];
     const Geom geo = gt.g[p.variant];
-    if (p.len_q && p.len_db) {
-        walk_pair_stream(p, end_h[idx], mask, geo, results, cigar, sc);
-    } else {
-        walk_pair(p, hs_boundary_end(sc, p.len_q, p.len_db), qs, ds, mask, geo, results, cigar,
-                  sc);
-    }
+    walk_pair(p, p.len_q && p.len_db ? end_h[idx] : hs_boundary_end(sc, p.len_q, p.len_db), qs,
+              ds, mask, geo, results, cigar, sc);
 }
 
 template <int K>
@@ -716,7 +561,7 @@ __global__ __launch_bounds__(256) void nw_fill_kernel(const NwPairDesc *__restri
     constexpr int KD = (K + 3) / 4;
     constexpr Geom geo{G, K};
     const int lane = threadIdx.x % G;
-    const uint32_t gi = blockIdx.x * GPB + threadIdx.x / G;
+    const uint32_t gi = pack_block(blocks_per_pack(GPB)) * GPB + threadIdx.x / G;
     if (gi >= count) return;  // whole group (DPP never crosses groups)
     const NwPairDesc p = pairs[first + gi];
     const uint32_t lq = p.len_q, ld = p.len_db;
@@ -747,14 +592,11 @@ __global__ __launch_bounds__(256) void nw_fill_kernel(const NwPairDesc *__restri
         int32_t dnext = (lane == 0) ? (int32_t)d[0] : 0;
         int2 bnext = make_int2(0, 0);
         if (c > 0 && lane == 0) bnext = scr[1];
-        uint8_t *mtile = mk + (uint64_t)c * geo.chunk_bytes(ld) + geo.seg_step((uint32_t)lane, 0);
-        const int Tt = (int)(geo.tiles(ld) * kTileSteps);
+        // this lane's segment of row 1 in block c*G + lane
+        uint8_t *mseg = mk + (uint64_t)(c * G + (uint32_t)lane) * p.mask_bs;
+        const int T = (int)geo.steps(ld);
 
-        for (int t0 = 0; t0 < Tt; t0 += kTileSteps) {
-          MaskWords<K> tb[kTileSteps];  // this lane's segments of the current step tile
-#pragma unroll
-          for (int ts = 0; ts < (int)kTileSteps; ++ts) {
-            const int t = t0 + ts;
+        for (int t = 0; t < T; ++t) {
             const int r = t - lane + 1;
             const int32_t dch = dnext;
             if (r >= 0 && r < (int)ld) dnext = (int32_t)d[r];
@@ -798,7 +640,7 @@ __global__ __launch_bounds__(256) void nw_fill_kernel(const NwPairDesc *__restri
                 pubH = Hp[K - 1];
 #pragma unroll
                 for (int k = 0; k < KD; ++k) mw.w[k] ^= 0x7F7F7F7Fu;  // stored inverted
-                tb[ts] = mw;
+                *reinterpret_cast<MaskWords<K> *>(mseg + (uint64_t)(r - 1) * p.mask_rs) = mw;
                 if (lane == G - 1 && c + 1 < nch) scr[r] = make_int2(pubH, pubF);
                 if (c == c_end && (uint32_t)lane == l_end && r == (int)ld) {
 #pragma unroll
@@ -807,11 +649,6 @@ __global__ __launch_bounds__(256) void nw_fill_kernel(const NwPairDesc *__restri
                     end_h[first + gi] = my_end;
                 }
             }
-          }
-          // the whole group finishes tile t0 / R together: one contiguous store
-          struct Tile { MaskWords<K> s[kTileSteps]; };
-          *reinterpret_cast<Tile *>(mtile + (uint64_t)(t0 / (int)kTileSteps) * geo.tile_bytes()) =
-              *reinterpret_cast<const Tile *>(tb);
         }
         if (c + 1 < nch) __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
     }
@@ -891,11 +728,13 @@ __global__ __launch_bounds__(256) void nw_fill_pk_kernel(const NwPairDesc *__res
                                                          uint8_t *__restrict__ mask,
                                                          int32_t *__restrict__ end_h,
                                                          saln_nw_result *__restrict__ results,
-                                                         uint32_t *__restrict__ cigar, Scoring sc) {
+                                                         uint32_t *__restrict__ cigar, Scoring sc,
+                                                         uint32_t ld_max) {
     constexpr int GPB = 256 / G;
     constexpr Geom geo{G, K};
+    extern __shared__ uint32_t drow[];  // [GPB][ld_max] packed db chars (dch) per row
     const int lane = threadIdx.x % G;
-    const uint32_t gi = blockIdx.x * GPB + threadIdx.x / G;
+    const uint32_t gi = pack_block(blocks_per_pack(2 * GPB)) * GPB + threadIdx.x / G;
     const uint32_t ia = 2 * gi, ib = 2 * gi + 1;
     if (ia >= count) return;  // whole group
     const bool hasB = ib < count;
@@ -934,33 +773,30 @@ __global__ __launch_bounds__(256) void nw_fill_pk_kernel(const NwPairDesc *__res
     uint32_t hd = pk2(hs_row0(sc, (uint32_t)col0) + beta * col0,
                       hs_row0(sc, (uint32_t)col0) + beta * col0);  // H~(r-1, col0)
     uint32_t pubF = 0, pubH = 0;
-    // db chars of my next row, per half (row r+1 -> index r).  Loads are
-    // unconditional (clamped index) and consumed one step later, so their
-    // latency hides behind a whole step of arithmetic.
-    // Two-step pipeline: the chars of row r arrive two steps ahead.
-    const int ldA1 = ldA - 1, ldB1 = (hasB ? ldB : ldA) - 1;
-    uint32_t pa0 = dA[min(max(-lane, 0), ldA1)], pb0 = dB[min(max(-lane, 0), ldB1)];
-    uint32_t pa1 = dA[min(max(1 - lane, 0), ldA1)], pb1 = dB[min(max(1 - lane, 0), ldB1)];
+    // db chars of both pairs, staged once per group in LDS as the packed
+    // (A << 5 | B << 21) word of each row; a step reads its row's word from
+    // LDS (lgkmcnt), so no global load sits in the step loop next to the
+    // mask stores (vmcnt).
+    uint32_t *__restrict__ myrow = drow + (threadIdx.x / G) * ld_max;
+    for (int i = lane; i < ldM; i += G) {
+        const uint32_t ca = i < ldA ? (uint32_t)dA[i] : 0u;
+        const uint32_t cb = i < ldB ? (uint32_t)dB[i] : 0u;
+        myrow[i] = (ca << 5) | (cb << 21);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" : : : "memory");
+    __builtin_amdgcn_wave_barrier();
     // end-cell owners
     const int lA = (lqA - 1) / K, kA = (lqA - 1) % K;
     const int lB = hasB ? (lqB - 1) / K : -1, kB = hasB ? (lqB - 1) % K : 0;
     int32_t endA = 0, endB = 0;
-    uint8_t *__restrict__ mA = mask + pa.mask_off + geo.seg_step((uint32_t)lane, 0);
-    uint8_t *__restrict__ mB = mask + pb.mask_off + geo.seg_step((uint32_t)lane, 0);
-    const int tilesA = (int)geo.tiles((uint32_t)ldA), tilesB = hasB ? (int)geo.tiles((uint32_t)ldB) : 0;
-    const int Tt = (tilesA > tilesB ? tilesA : tilesB) * (int)kTileSteps;
+    // this lane's segments of row 1 (block = lane)
+    uint8_t *__restrict__ mA = mask + pa.mask_off + (uint64_t)lane * pa.mask_bs;
+    uint8_t *__restrict__ mB = mask + pb.mask_off + (uint64_t)lane * pb.mask_bs;
+    const int T = (int)geo.steps((uint32_t)ldM);
 
-    for (int t0 = 0; t0 < Tt; t0 += kTileSteps) {
-      PkMask<K> ta[kTileSteps], tbb[kTileSteps];
-#pragma unroll
-      for (int ts = 0; ts < (int)kTileSteps; ++ts) {
-        const int t = t0 + ts;
+    for (int t = 0; t < T; ++t) {
         const int r = t - lane + 1;
-        const uint32_t dch = (pa0 << 5) | (pb0 << 21);
-        pa0 = pa1;
-        pb0 = pb1;
-        pa1 = dA[min(max(r + 1, 0), ldA1)];
-        pb1 = dB[min(max(r + 1, 0), ldB1)];
+        const uint32_t dch = myrow[min(max(r - 1, 0), ldM - 1)];
         // group-start inputs for row t+1: I~(r,1) and H~(r,0) (same for A and B)
         const int32_t rb = t + 1;
         const int32_t bF = is_col1(sc, (uint32_t)rb) + alpha * rb + beta;
@@ -1011,8 +847,8 @@ __global__ __launch_bounds__(256) void nw_fill_pk_kernel(const NwPairDesc *__res
             hd = inH;
             pubF = F;
             pubH = Hp[K - 1];
-            ta[ts] = wa;
-            tbb[ts] = wb;
+            if (r <= ldA) *reinterpret_cast<PkMask<K> *>(mA + (uint64_t)(r - 1) * pa.mask_rs) = wa;
+            if (r <= ldB) *reinterpret_cast<PkMask<K> *>(mB + (uint64_t)(r - 1) * pb.mask_rs) = wb;
             if (r == ldA && lane == lA) {
                 int32_t e = 0;
 #pragma unroll
@@ -1030,13 +866,6 @@ __global__ __launch_bounds__(256) void nw_fill_pk_kernel(const NwPairDesc *__res
                 end_h[first + ib] = endB;
             }
         }
-      }
-      // the group finishes tile t0 / R together: contiguous stores
-      struct Tile { PkMask<K> s[kTileSteps]; };
-      const int tile = t0 / (int)kTileSteps;
-      const uint64_t to = (uint64_t)tile * geo.tile_bytes();
-      if (tile < tilesA) *reinterpret_cast<Tile *>(mA + to) = *reinterpret_cast<const Tile *>(ta);
-      if (tile < tilesB) *reinterpret_cast<Tile *>(mB + to) = *reinterpret_cast<const Tile *>(tbb);
     }
     (void)results;
     (void)cigar;
@@ -1060,32 +889,35 @@ static void fill_i32(dim3 grid, hipStream_t s, const NwPairDesc *pairs, uint32_t
 template <int G, int K>
 static void fill_pk(dim3 grid, hipStream_t s, const NwPairDesc *pairs, uint32_t first,
                     uint32_t count, const uint8_t *qs, const uint8_t *ds, uint8_t *mask,
-                    int32_t *end_h, saln_nw_result *res, uint32_t *cig, Scoring sc, bool full) {
+                    int32_t *end_h, saln_nw_result *res, uint32_t *cig, Scoring sc, bool full,
+                    uint32_t ld_max) {
+    const size_t lds = (size_t)(256 / G) * ld_max * sizeof(uint32_t);
     if (full)
-        nw_fill_pk_kernel<G, K, false><<<grid, dim3(256), 0, s>>>(pairs, first, count, qs, ds,
-                                                                   mask, end_h, res, cig, sc);
+        nw_fill_pk_kernel<G, K, false><<<grid, dim3(256), lds, s>>>(
+            pairs, first, count, qs, ds, mask, end_h, res, cig, sc, ld_max);
     else
-        nw_fill_pk_kernel<G, K, true><<<grid, dim3(256), 0, s>>>(pairs, first, count, qs, ds,
-                                                                  mask, end_h, res, cig, sc);
+        nw_fill_pk_kernel<G, K, true><<<grid, dim3(256), lds, s>>>(
+            pairs, first, count, qs, ds, mask, end_h, res, cig, sc, ld_max);
 }
 
 hipError_t launch_fill(int variant, const NwPairDesc *pairs, uint32_t first, uint32_t count,
                        const uint8_t *qs, const uint8_t *ds, uint8_t *mask, int2 *scratch,
                        int32_t *end_h, saln_nw_result *res, uint32_t *cig, Scoring sc,
-                       bool full_codes, hipStream_t stream) {
+                       bool full_codes, uint32_t ld_max, hipStream_t stream) {
     if (count == 0) return hipSuccess;
     const uint32_t gpb = 256 / kVariants[variant].G;  // lane groups per block
     const uint32_t groups = kPacked[variant] ? (count + 1) / 2 : count;
-    const dim3 grid((groups + gpb - 1) / gpb);
+    const uint32_t sup = 8 * blocks_per_pack(kPacked[variant] ? 2 * gpb : gpb);
+    const dim3 grid(((groups + gpb - 1) / gpb + sup - 1) / sup * sup);
     switch (variant) {
         case 0: fill_i32<16, 10>(grid, stream, pairs, first, count, qs, ds, mask, scratch, end_h, res, cig, sc); break;
         case 1: fill_i32<16, 16>(grid, stream, pairs, first, count, qs, ds, mask, scratch, end_h, res, cig, sc); break;
         case 2: fill_i32<64, 8>(grid, stream, pairs, first, count, qs, ds, mask, scratch, end_h, res, cig, sc); break;
         case 3: fill_i32<64, 16>(grid, stream, pairs, first, count, qs, ds, mask, scratch, end_h, res, cig, sc); break;
-        case 4: fill_pk<8, 19>(grid, stream, pairs, first, count, qs, ds, mask, end_h, res, cig, sc, full_codes); break;
-        case 5: fill_pk<16, 16>(grid, stream, pairs, first, count, qs, ds, mask, end_h, res, cig, sc, full_codes); break;
-        case 7: fill_pk<16, 10>(grid, stream, pairs, first, count, qs, ds, mask, end_h, res, cig, sc, full_codes); break;
-        default: fill_pk<32, 16>(grid, stream, pairs, first, count, qs, ds, mask, end_h, res, cig, sc, full_codes); break;
+        case 4: fill_pk<8, 19>(grid, stream, pairs, first, count, qs, ds, mask, end_h, res, cig, sc, full_codes, ld_max); break;
+        case 5: fill_pk<16, 16>(grid, stream, pairs, first, count, qs, ds, mask, end_h, res, cig, sc, full_codes, ld_max); break;
+        case 7: fill_pk<16, 10>(grid, stream, pairs, first, count, qs, ds, mask, end_h, res, cig, sc, full_codes, ld_max); break;
+        default: fill_pk<32, 16>(grid, stream, pairs, first, count, qs, ds, mask, end_h, res, cig, sc, full_codes, ld_max); break;
     }
     return hipGetLastError();
 }
