@@ -54,6 +54,21 @@ def cpu_baseline(budget_s: float = 12.0) -> dict:
                       f"fill + literal DFS (<=1e5 pops/pair), 1 thread, {dt:.1f} s"}
 
 
+def pmc_traffic(kernel: str):
+    """HBM bytes per launch of `kernel` from the committed PMC summary
+    (profiles/pmc_traffic.json, written by tools/pmc_traffic.py from the
+    rocprofv3 --pmc passes of tools/pmc.sh on this workload), or None."""
+    try:
+        with open(os.path.join(ROOT, "profiles", "pmc_traffic.json")) as fh:
+            doc = json.load(fh)
+    except (OSError, ValueError):
+        return None
+    for name, v in doc.get("kernels", {}).items():
+        if kernel in name:
+            return v.get("hbm_bytes")
+    return None
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -163,7 +178,9 @@ def main() -> None:
                                                                else "")},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": None, "kernel": "nw_fill",
+                         "traffic": pmc_traffic("nw_fill_pk_kernel<16, 10, true>"),
+                         "traffic_unit": "bytes/launch (PMC FETCH_SIZE*2 + WRITE_SIZE)",
+                         "algorithmic_bytes": cells_rank, "kernel": "nw_fill",
                          "kernel_avg_ms": round(fill_avg_s * 1e3, 4),
                          "traceback_avg_ms": round(tb_ms / max(1, tb_n), 4),
                          "execute_avg_ms": round(ex_ms / max(1, ex_n), 4),

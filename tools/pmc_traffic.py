@@ -1,0 +1,40 @@
+"""HBM traffic per launch from the rocprofv3 --pmc passes of tools/pmc.sh.
+
+FETCH_SIZE / WRITE_SIZE are in KiB per dispatch.  On gfx950 FETCH_SIZE counts
+half the bytes of wide streaming reads (MI355X_MICROARCH.md, HBM section), so
+reads are doubled; WRITE_SIZE is taken as is (the fill's dwordx3 stores were
+checked against the plan's exact mask byte count).  Writes the per-kernel mean
+to profiles/pmc_traffic.json, which bench.py reports as roofline.traffic."""
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+
+def main(d="gpurun_out/pmc", out="profiles/pmc_traffic.json", tag=""):
+    acc = defaultdict(lambda: defaultdict(list))
+    for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+        with open(f) as fh:
+            for row in csv.DictReader(fh):
+                name = row.get("Kernel_Name", "?").split("(")[0].replace("void ", "")
+                acc[name][row["Counter_Name"]].append(float(row["Counter_Value"]))
+    res = {}
+    for k, cs in acc.items():
+        if "FETCH_SIZE" not in cs or "WRITE_SIZE" not in cs:
+            continue
+        fetch = sum(cs["FETCH_SIZE"]) / len(cs["FETCH_SIZE"]) * 1024 * 2
+        write = sum(cs["WRITE_SIZE"]) / len(cs["WRITE_SIZE"]) * 1024
+        res[k] = {"read_bytes": round(fetch), "write_bytes": round(write),
+                  "hbm_bytes": round(fetch + write), "dispatches": len(cs["FETCH_SIZE"])}
+    doc = {"source": "tools/pmc.sh (rocprofv3 --pmc, one counter group per pass) on "
+                     "tools/prof_nw.py: 100000 x 150x150 G-iid pairs, seed 0x5EED0002",
+           "round": tag, "kernels": res}
+    with open(out, "w") as fh:
+        json.dump(doc, fh, indent=1)
+    print(json.dumps(doc, indent=1))
+
+
+if __name__ == "__main__":
+    main(*sys.argv[1:])
