@@ -93,6 +93,34 @@ int64_t ref_parse_fasta(const uint8_t *buf, size_t len, int has_valid_ext, uint8
 /* splitmix64 synthetic generator. */
 uint64_t ref_splitmix64(uint64_t *state);
 
+/* ---------------------------------------------------------------- WFA
+ * ref_wfa_align: wfa_align(seq1 = q, seq2 = d, mode) (wfa.rs:23-42) with
+ * release semantics.  out gets everything the reference prints to stdout
+ * for the pair (the `lo/hi` lines, the convergence and traceback debug
+ * lines, the alignment and its Debug dump).  max_steps caps the expand loop
+ * (0 = unlimited; the reference can loop forever).  Returns res->status. */
+enum {
+    REF_WFA_OK = 0,
+    REF_WFA_NOT_IMPLEMENTED = 1, /* non-global mode :26 */
+    REF_WFA_PANIC_TRIM = 3,      /* Ocean::trim rotate_left / expect / unwrap :524-603 */
+    REF_WFA_PANIC_SLICE = 4,     /* rec_tr slice indexing :695-844 */
+    REF_WFA_NONCONVERGED = 5     /* max_steps reached */
+};
+typedef struct {
+    int32_t status;
+    uint64_t steps;    /* expand calls */
+    int64_t score;     /* printed score wfs.len() */
+    uint64_t aln_len1, aln_len2;
+} ref_wfa_result;
+int ref_wfa_align(const uint8_t *q, size_t lq, const uint8_t *d, size_t ld, int mode,
+                  uint64_t max_steps, ref_wfa_result *res, char *out, size_t out_cap,
+                  size_t *out_len);
+/* WaveFrontTensor::new on flat-encoded tensors (refwfa.c) for the
+ * reference's tensor tests; NULL = None.  Returns the encoded length. */
+int64_t ref_wfa_tensor_new(const int32_t *o, const int32_t *e, const int32_t *x, int32_t *out,
+                           char *txt_out, size_t txt_cap);
+int ref_wfa_initial_converged(const uint8_t *q, size_t lq, const uint8_t *d, size_t ld);
+
 #ifdef __cplusplus
 }
 #endif

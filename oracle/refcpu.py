@@ -57,6 +57,12 @@ def lib():
                                       C.POINTER(C.c_size_t), u8p, C.c_size_t,
                                       C.POINTER(C.c_size_t)]
         L.ref_parse_fasta.restype = C.c_int64
+        i32p = C.POINTER(C.c_int32)
+        L.ref_wfa_align.argtypes = [u8p, C.c_size_t, u8p, C.c_size_t, C.c_int, C.c_uint64,
+                                    C.c_void_p, C.c_char_p, C.c_size_t, C.POINTER(C.c_size_t)]
+        L.ref_wfa_tensor_new.argtypes = [i32p, i32p, i32p, i32p, C.c_char_p, C.c_size_t]
+        L.ref_wfa_tensor_new.restype = C.c_int64
+        L.ref_wfa_initial_converged.argtypes = [u8p, C.c_size_t, u8p, C.c_size_t]
         _lib = L
     return _lib
 
@@ -152,3 +158,91 @@ def parse_fasta_bytes(data: bytes, valid_ext: bool = True):
         seq = raw[o:o + sl]; o += sl
         recs.append((name, seq))
     return recs, bytes(bad)[:nb.value]
+
+
+# ----------------------------------------------------------------------- WFA
+class _WfaRes(C.Structure):
+    _fields_ = [("status", C.c_int32), ("steps", C.c_uint64), ("score", C.c_int64),
+                ("aln_len1", C.c_uint64), ("aln_len2", C.c_uint64)]
+
+
+WFA_OK, WFA_NOT_IMPLEMENTED, WFA_PANIC_TRIM, WFA_PANIC_SLICE, WFA_NONCONVERGED = 0, 1, 3, 4, 5
+_STATES = "MDI"  # enum State { M, D, I } (wfa.rs:44-50)
+
+
+@dataclass
+class WfaOracle:
+    status: int
+    steps: int
+    score: int            # printed score: wfs.len()
+    stdout: str
+    aln_len1: int
+    aln_len2: int
+
+
+def wfa(query: bytes, db: bytes, *, mode: int = 0, max_steps: int = 0) -> WfaOracle:
+    """wfa_align(seq1=query, seq2=db, mode) (wfa.rs:23-42), release semantics."""
+    L = lib()
+    res = _WfaRes()
+    n = C.c_size_t()
+    L.ref_wfa_align(_u8(query), len(query), _u8(db), len(db), mode, max_steps, C.byref(res),
+                    None, 0, C.byref(n))
+    buf = C.create_string_buffer(n.value + 1)
+    L.ref_wfa_align(_u8(query), len(query), _u8(db), len(db), mode, max_steps, C.byref(res),
+                    buf, n.value + 1, C.byref(n))
+    return WfaOracle(res.status, res.steps, res.score, buf.raw[:n.value].decode("latin-1"),
+                     res.aln_len1, res.aln_len2)
+
+
+def _enc_front(f):
+    if f is None:
+        return [0, 0, 0, 0]
+    out = [1, f["lo"], f["hi"], len(f["elements"])]
+    for e in f["elements"]:
+        if e is None:
+            out += [0] * 7
+        else:
+            off, st, par = e
+            p = [_STATES.index(x) for x in par] + [0, 0, 0]
+            out += [1, off, _STATES.index(st), len(par)] + p[:3]
+    return out
+
+
+def _enc_tensor(t):
+    if t is None:
+        return None
+    arr = [1] + _enc_front(t.get("i")) + _enc_front(t.get("d")) + _enc_front(t.get("m"))
+    return (C.c_int32 * len(arr))(*arr)
+
+
+def _dec_front(a, k):
+    some, lo, hi, n = a[k:k + 4]
+    k += 4
+    els = []
+    for _ in range(n):
+        s, off, st, np_, p0, p1, p2 = a[k:k + 7]
+        k += 7
+        els.append((off, _STATES[st], [_STATES[x] for x in (p0, p1, p2)[:np_]]) if s else None)
+    return ({"lo": lo, "hi": hi, "elements": els} if some else None), k
+
+
+def wfa_tensor_new(o=None, e=None, x=None):
+    """WaveFrontTensor::new(o, e, x) (wfa.rs:225-420) on tensors given as
+    {'i'|'d'|'m': None | {'lo', 'hi', 'elements': [None | (offset, state,
+    [parents])]}} -> (tensor or None, printed text)."""
+    L = lib()
+    out = (C.c_int32 * 65536)()
+    txt = C.create_string_buffer(256)
+    L.ref_wfa_tensor_new(_enc_tensor(o), _enc_tensor(e), _enc_tensor(x), out, txt, 256)
+    a = list(out)
+    if not a[0]:
+        return None, txt.value.decode()
+    i, k = _dec_front(a, 1)
+    d, k = _dec_front(a, k)
+    m, k = _dec_front(a, k)
+    return {"i": i, "d": d, "m": m}, txt.value.decode()
+
+
+def wfa_initial_converged(query: bytes, db: bytes) -> bool:
+    """Ocean::global().is_converged(query, db) (test_converge, wfa.rs:1289-1294)."""
+    return bool(lib().ref_wfa_initial_converged(_u8(query), len(query), _u8(db), len(db)))
