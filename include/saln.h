@@ -171,6 +171,49 @@ int saln_nw_plan_set_async(saln_nw_plan *plan, int enable);
 int saln_nw_plan_sync(saln_nw_plan *plan, void *stream, int keep_latest);
 int saln_nw_plan_destroy(saln_nw_plan *plan);
 
+/* ----------------------------------------------------------------------- WFA
+ * Replaces `pub fn wfa_align(seq1: &Record, seq2: &Record, mode: Mode)`
+ * (wfa.rs:23-42) with the reference's exact (quirky) semantics: wavefront
+ * tensors built by WaveFrontTensor::new (:225-420), extension of the newest
+ * M front only (:127-139, :467-488), Ocean::trim (:490-623), convergence on
+ * the newest tensor at (len_db-1, len_q-1) (:180-191), and the greedy rec_tr
+ * traceback (:654-853).  seq1 = query, seq2 = db.  The reference loops
+ * forever when it never converges; max_steps bounds the expand loop
+ * (status SALN_NONCONVERGED), and max_width bounds a wavefront's width
+ * (also SALN_NONCONVERGED).  Rust panics are statuses:
+ * SALN_REF_PANIC_TRIM (rotate_left / expect / unwrap in trim),
+ * SALN_REF_PANIC_SLICE (slice indexing in rec_tr). */
+typedef struct {
+    int32_t score;        /* printed score: wfs.len() at convergence (:33-38) */
+    int32_t status;       /* SALN_OK | SALN_NOT_IMPLEMENTED | SALN_REF_PANIC_* | SALN_NONCONVERGED */
+    uint32_t steps;       /* Ocean::expand calls */
+    uint32_t aln_len1;    /* bytes of Alignment.seq1 / seq2 (traceback output) */
+    uint32_t aln_len2;
+    int32_t conv_offset;  /* converged element (:640): offset, state (0 M, 1 D, 2 I), */
+    uint8_t conv_state;   /*   parents (np entries, same codes)                      */
+    uint8_t conv_np;
+    uint8_t conv_parents[3];
+    uint8_t reserved[3];
+} saln_wfa_result;        /* 32 bytes */
+
+/* Batched wfa_align over pairs (same pair conventions as
+ * saln_nw_align_batch).  aln (optional): per pair 2*aln_cap bytes at
+ * aln_off[p] (seq1 then seq2, in the reference's push order, i.e. reversed).
+ * max_steps = 0 selects 64; max_width = 0 selects 64. */
+int saln_wfa_align_batch(saln_context *ctx, const uint8_t *q_seq, const uint64_t *q_off,
+                         uint64_t n_q, const uint8_t *db_seq, const uint64_t *db_off,
+                         uint64_t n_db, const uint32_t *pair_q, const uint32_t *pair_db,
+                         uint64_t n_pairs, int32_t mode, uint32_t max_steps, uint32_t max_width,
+                         saln_wfa_result *results, uint8_t *aln, const uint64_t *aln_off,
+                         uint32_t aln_cap);
+
+/* Everything the reference prints to stdout for one wfa_align call (the
+ * `lo/hi` lines, `converged with score`, the traceback's debug lines, the
+ * alignment and its Debug dump), up to the point where it would panic. */
+int saln_wfa_render(saln_context *ctx, const uint8_t *q, uint64_t len_q, const uint8_t *d,
+                    uint64_t len_db, int32_t mode, uint32_t max_steps, uint32_t max_width,
+                    char *out, uint64_t cap, uint64_t *out_len, saln_wfa_result *result);
+
 /* --------------------------------------------------------------------- FASTA
  * Replaces `pub fn parse_fasta(path: PathBuf) -> Result<Records>`
  * (parse.rs:54-99): extension must be exactly fa|fasta|fna; '>' opens a record

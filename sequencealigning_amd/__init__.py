@@ -1,18 +1,22 @@
 """sequencealigning_amd — MI355X-native drop-in engine for the NW-affine hot
-path of Qw11111111111/SequenceAligning (src/needleman_wunsch_affine.rs).
+and WFA paths of Qw11111111111/SequenceAligning (src/needleman_wunsch_affine.rs,
+src/wfa.rs).
 
 Compute lives in ``libsaln.so`` (HIP kernels for gfx950 behind the C ABI in
 ``include/saln.h``); this package is the host-side mirror of the reference's
 interface: ``parse_fasta``/``Record``/``Mode`` (src/parse.rs), the
-``AlignerError`` family (src/errors.rs) and ``n_w_align``.
+``AlignerError`` family (src/errors.rs), ``n_w_align`` and ``wfa_align``.
 """
 from .records import (AlignerError, AlignmentError, Algo, CharError, FastaError, Mode, Record,
                       Records, parse_fasta, parse_fasta_bytes)
 from .nw import (NwAlignment, NwPlan, alignment_rows, cigar_ops_string, dense_mask, n_w_align,
                  nw_align_batch, pack_csr, render)
+from . import wfa
+from .wfa import WfaAlignment, wfa_align, wfa_align_batch
 
 __all__ = [
     "AlignerError", "AlignmentError", "Algo", "CharError", "FastaError", "Mode", "Record",
     "Records", "parse_fasta", "parse_fasta_bytes", "NwAlignment", "NwPlan", "alignment_rows",
     "cigar_ops_string", "dense_mask", "n_w_align", "nw_align_batch", "pack_csr", "render",
+    "wfa", "WfaAlignment", "wfa_align", "wfa_align_batch",
 ]

@@ -56,13 +56,24 @@ class NwResult(C.Structure):
 RESULT_DTYPE = [("score", "<i4"), ("status", "<i4"), ("cigar_len", "<u4"), ("end_states", "u1"),
                 ("printed", "u1"), ("flags", "u1"), ("reserved", "u1")]
 
+class WfaResult(C.Structure):
+    _fields_ = [("score", C.c_int32), ("status", C.c_int32), ("steps", C.c_uint32),
+                ("aln_len1", C.c_uint32), ("aln_len2", C.c_uint32), ("conv_offset", C.c_int32),
+                ("conv_state", C.c_uint8), ("conv_np", C.c_uint8),
+                ("conv_parents", C.c_uint8 * 3), ("reserved", C.c_uint8 * 3)]
+
+
+WFA_RESULT_DTYPE = [("score", "<i4"), ("status", "<i4"), ("steps", "<u4"), ("aln_len1", "<u4"),
+                    ("aln_len2", "<u4"), ("conv_offset", "<i4"), ("conv_state", "u1"),
+                    ("conv_np", "u1"), ("conv_parents", "u1", (3,)), ("reserved", "u1", (3,))]
+
 # symbols every build must export (tests check this list against include/saln.h)
 EXPORTS = [
     "saln_context_create", "saln_context_destroy", "saln_last_error", "saln_abi_version",
     "saln_nw_align", "saln_nw_render", "saln_nw_dense_mask", "saln_nw_align_batch",
     "saln_nw_plan_create", "saln_nw_plan_info", "saln_nw_cigar_offsets", "saln_nw_execute",
     "saln_nw_plan_set_timing", "saln_nw_plan_kernel_time", "saln_nw_plan_set_async",
-    "saln_nw_plan_sync", "saln_nw_plan_destroy",
+    "saln_nw_plan_sync", "saln_nw_plan_destroy", "saln_wfa_align_batch", "saln_wfa_render",
     "saln_parse_fasta", "saln_parse_fasta_buffer", "saln_records_count", "saln_records_get",
     "saln_records_free",
 ]
@@ -125,6 +136,12 @@ def lib() -> C.CDLL:
         L.saln_nw_plan_set_async.argtypes = [vp, C.c_int]
         L.saln_nw_plan_sync.argtypes = [vp, vp, C.c_int]
         L.saln_nw_plan_destroy.argtypes = [vp]
+        L.saln_wfa_align_batch.argtypes = [vp, vp, vp, C.c_uint64, vp, vp, C.c_uint64, vp, vp,
+                                           C.c_uint64, C.c_int32, C.c_uint32, C.c_uint32, vp,
+                                           vp, vp, C.c_uint32]
+        L.saln_wfa_render.argtypes = [vp, vp, C.c_uint64, vp, C.c_uint64, C.c_int32, C.c_uint32,
+                                      C.c_uint32, C.c_char_p, C.c_uint64, u64p,
+                                      C.POINTER(WfaResult)]
         L.saln_parse_fasta.argtypes = [C.c_char_p, C.POINTER(vp), u8p, C.c_uint64, u64p]
         L.saln_parse_fasta_buffer.argtypes = [vp, C.c_uint64, C.POINTER(vp), u8p, C.c_uint64,
                                               u64p]

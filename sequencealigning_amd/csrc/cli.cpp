@@ -7,7 +7,8 @@
 // (needleman_wunsch_affine.rs:431) prints this engine's wall time.
 //
 // Differences by design: `-a a-star` (the reference default) is not part of
-// this engine and is rejected; a reference panic (boundary index panic of the
+// this engine and is rejected; `-a wfa` caps the score loop (--wfa-steps),
+// where the reference would not terminate; a reference panic (boundary index panic of the
 // NW traceback) aborts with exit code 101 after the blocks printed before it,
 // like the reference, unless --no-abort is given.
 #include <chrono>
@@ -29,6 +30,7 @@ struct Args {
     int algo = 0;  // 0 a-star (reference default), 1 needleman-wunsch, 2 wfa
     int device = 0;
     bool timing = true, abort_on_panic = true;
+    uint32_t wfa_steps = 64;  // cap on WFA score steps (the reference loops without one)
     uint64_t max_blocks = 0;
 };
 
@@ -47,6 +49,7 @@ const char *kUsage =
     "      --device <N>               HIP device [default: 0]\n"
     "      --no-timing                omit the per-pair timing line\n"
     "      --no-abort                 report reference panics and continue\n"
+    "      --wfa-steps <N>            cap on WFA score steps [default: 64]\n"
     "      --max-blocks <N>           cap on printed alignments per pair [default: 0 = none]\n"
     "  -h, --help                     Print help\n";
 
@@ -101,6 +104,8 @@ Args parse_args(int argc, char **argv) {
             a.timing = false;
         } else if (s == "--no-abort") {
             a.abort_on_panic = false;
+        } else if (is("--wfa-steps", "--wfa-steps")) {
+            a.wfa_steps = (uint32_t)std::strtoul(need("--wfa-steps <N>").c_str(), nullptr, 10);
         } else if (is("--max-blocks", "--max-blocks")) {
             a.max_blocks = std::strtoull(need("--max-blocks <N>").c_str(), nullptr, 10);
         } else {
@@ -241,16 +246,68 @@ int main(int argc, char **argv) {
                      "use -a needleman-wunsch or -a wfa\n");
         return 2;
     }
-    if (a.algo == 2) {
-        std::fprintf(stderr, "saln: -a wfa is not available in this build\n");
-        return 2;
-    }
     saln_context *ctx = nullptr;
     if (saln_context_create(a.device, &ctx) != SALN_OK) {
         std::fprintf(stderr, "saln: %s\n", saln_last_error());
         return 1;
     }
     std::string text;
+    if (a.algo == 2) {  // Algo::Wfa => wfa_align(q, d, mode)  (main.rs:66)
+        for (const Rec &d : db) {
+            for (const Rec &q : query) {
+                uint64_t len = 0;
+                saln_wfa_result r;
+                int rc = saln_wfa_render(ctx, q.seq.data(), q.seq.size(), d.seq.data(),
+                                         d.seq.size(), a.mode, a.wfa_steps, 0, nullptr, 0, &len, &r);
+                if (rc == SALN_OK && r.status == SALN_NOT_IMPLEMENTED) {
+                    std::fprintf(stderr,
+                                 "An error occured during alignment of %s and %s\nError in "
+                                 "alignment: not implemented\n",
+                                 as_str(q.name).c_str(), as_str(d.name).c_str());
+                    continue;
+                }
+                if (rc == SALN_OK) {
+                    text.assign(len, '\0');
+                    rc = saln_wfa_render(ctx, q.seq.data(), q.seq.size(), d.seq.data(),
+                                         d.seq.size(), a.mode, a.wfa_steps, 0, text.data(), len,
+                                         &len, &r);
+                }
+                if (rc != SALN_OK) {
+                    std::fprintf(stderr, "saln: %s\n", saln_last_error());
+                    saln_context_destroy(ctx);
+                    return 1;
+                }
+                std::fwrite(text.data(), 1, text.size(), stdout);
+                if (r.status == SALN_REF_PANIC_TRIM || r.status == SALN_REF_PANIC_SLICE) {
+                    std::fflush(stdout);
+                    const char *where = r.status == SALN_REF_PANIC_TRIM
+                                            ? "src/wfa.rs: mid > len (Ocean::trim rotate_left)"
+                                            : "src/wfa.rs: slice index out of range (rec_tr)";
+                    if (a.abort_on_panic) {
+                        std::fprintf(stderr,
+                                     "thread 'main' panicked at %s\nnote: run with "
+                                     "`RUST_BACKTRACE=1` environment variable to display a "
+                                     "backtrace\n",
+                                     where);
+                        saln_context_destroy(ctx);
+                        return 101;
+                    }
+                    std::fprintf(stderr, "saln: reference panic (%s) for %s vs %s\n",
+                                 r.status == SALN_REF_PANIC_TRIM ? "REF_PANIC_TRIM"
+                                                                 : "REF_PANIC_SLICE",
+                                 as_str(q.name).c_str(), as_str(d.name).c_str());
+                    continue;
+                }
+                if (r.status == SALN_NONCONVERGED)
+                    std::fprintf(stderr,
+                                 "saln: %s vs %s did not converge within %u score steps (the "
+                                 "reference would not terminate)\n",
+                                 as_str(q.name).c_str(), as_str(d.name).c_str(), a.wfa_steps);
+            }
+        }
+        saln_context_destroy(ctx);
+        return 0;
+    }
     for (const Rec &d : db) {          // main.rs:61
         for (const Rec &q : query) {   // main.rs:62
             const auto t0 = std::chrono::steady_clock::now();

@@ -42,11 +42,7 @@ Scoring scoring_or_default(const saln_nw_scoring *s) {
 
 using namespace saln;
 
-struct saln_context {
-    int device = 0;
-    hipStream_t stream = nullptr;
-    hipStream_t tb_stream = nullptr;  // traceback stream, overlaps the next fill sub-batch
-};
+
 
 struct saln_nw_plan {
     saln_context *ctx = nullptr;

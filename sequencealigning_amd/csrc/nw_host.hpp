@@ -9,6 +9,12 @@
 #include "nw_common.hpp"
 #include "saln.h"
 
+struct saln_context {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    hipStream_t tb_stream = nullptr;  // traceback stream (pipelined NW plans)
+};
+
 namespace saln {
 
 // kernels (nw_kernels.hip)

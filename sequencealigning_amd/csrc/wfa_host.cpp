@@ -1,0 +1,271 @@
+// C ABI of the WFA engine (include/saln.h): replaces wfa_align
+// (src/wfa.rs:23-42) and, batched, the pair loop of src/main.rs:61-67 for
+// `-a wfa`.  The score loop, trim and traceback run in wfa_kernels.hip; the
+// host uploads, launches in chunks that bound the tensor-history arena, and
+// formats the reference's stdout from the per-step and traceback logs the
+// kernel writes.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <climits>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "nw_host.hpp"
+#include "wfa_host.hpp"
+
+using namespace saln;
+
+namespace {
+
+#define TRY_HIP(expr)                                                                      \
+    do {                                                                                   \
+        hipError_t e_ = (expr);                                                            \
+        if (e_ != hipSuccess) {                                                            \
+            set_error(std::string(#expr) + ": " + hipGetErrorString(e_));                  \
+            return SALN_E_HIP;                                                             \
+        }                                                                                  \
+    } while (0)
+
+struct DevBuf {
+    void *p = nullptr;
+    ~DevBuf() {
+        if (p) (void)hipFree(p);
+    }
+    hipError_t alloc(size_t n) { return hipMalloc(&p, n ? n : 1); }
+};
+
+constexpr uint32_t kDefaultSteps = 64, kDefaultWidth = 64;
+constexpr uint64_t kArenaBudget = 8ull << 30;  // bytes of tensor history per launch
+
+uint32_t ev_cap_for(uint32_t max_steps) { return 7 * (max_steps / 4 + 2) + 8; }
+
+struct Logs {
+    std::vector<int32_t> lohi;  // 2 per pair-step
+    std::vector<uint8_t> ev;    // ev_cap per pair
+    uint32_t ev_cap = 0;
+};
+
+// Runs the pairs; logs (optional) receive the per-step lo/hi and the rec_tr
+// events of every pair (used for rendering).
+int run_wfa(saln_context *ctx, const uint8_t *q_seq, const uint64_t *q_off, uint64_t n_q,
+            const uint8_t *db_seq, const uint64_t *db_off, uint64_t n_db, const uint32_t *pair_q,
+            const uint32_t *pair_db, uint64_t n_pairs, int32_t mode, uint32_t max_steps,
+            uint32_t max_width, saln_wfa_result *results, uint8_t *aln, const uint64_t *aln_off,
+            uint32_t aln_cap, Logs *logs) {
+    if (!ctx || !q_off || !db_off || !results) return SALN_E_INVALID;
+    if (!max_steps) max_steps = kDefaultSteps;
+    if (!max_width) max_width = kDefaultWidth;
+    if (n_pairs == 0) return SALN_OK;
+    if (n_pairs > 0xFFFFFFFFull) return SALN_E_INVALID;
+    TRY_HIP(hipSetDevice(ctx->device));
+    std::vector<WfaPairDesc> descs(n_pairs);
+    uint64_t aln_bytes = 0;
+    for (uint64_t k = 0; k < n_pairs; ++k) {
+        const uint64_t qi = pair_q ? pair_q[k] : k % n_q;
+        const uint64_t di = pair_db ? pair_db[k] : k / n_q;
+        if (qi >= n_q || di >= n_db) {
+            set_error("pair index out of range");
+            return SALN_E_INVALID;
+        }
+        WfaPairDesc &d = descs[k];
+        std::memset(&d, 0, sizeof d);
+        d.q_off = q_off[qi];
+        d.db_off = db_off[di];
+        const uint64_t lq = q_off[qi + 1] - q_off[qi], ld = db_off[di + 1] - db_off[di];
+        if (lq > 0x7FFFFFFFull || ld > 0x7FFFFFFFull) {
+            set_error("sequence too long");
+            return SALN_E_INVALID;
+        }
+        d.len_q = (uint32_t)lq;
+        d.len_db = (uint32_t)ld;
+        d.pair_id = (uint32_t)k;
+        d.mode = mode;
+        d.aln_cap = aln ? aln_cap : 0;
+        d.aln_off = aln && aln_off ? aln_off[k] : 0;
+        if (aln) aln_bytes = std::max<uint64_t>(aln_bytes, d.aln_off + 2ull * aln_cap);
+    }
+    const uint64_t qbytes = q_off[n_q], dbytes = db_off[n_db];
+    DevBuf dq, dd, dp, dr, da, dl, de, ah, ao, am, at;
+    TRY_HIP(dq.alloc(qbytes));
+    TRY_HIP(dd.alloc(dbytes));
+    TRY_HIP(dp.alloc(n_pairs * sizeof(WfaPairDesc)));
+    TRY_HIP(dr.alloc(n_pairs * sizeof(saln_wfa_result)));
+    if (qbytes) TRY_HIP(hipMemcpy(dq.p, q_seq, qbytes, hipMemcpyHostToDevice));
+    if (dbytes) TRY_HIP(hipMemcpy(dd.p, db_seq, dbytes, hipMemcpyHostToDevice));
+    TRY_HIP(hipMemcpy(dp.p, descs.data(), n_pairs * sizeof(WfaPairDesc), hipMemcpyHostToDevice));
+    if (aln) TRY_HIP(da.alloc(aln_bytes));
+    const uint32_t ev_cap = ev_cap_for(max_steps);
+    if (logs) {
+        TRY_HIP(dl.alloc(n_pairs * 2ull * max_steps * sizeof(int32_t)));
+        TRY_HIP(de.alloc(n_pairs * (uint64_t)ev_cap));
+    }
+    // arena chunking
+    const uint64_t S = max_steps / 2 + 1, W = max_width;
+    const uint64_t per_lane = S * 3 * 4 * 4 + S * 3 * W * 8 + S;
+    uint64_t nl = std::max<uint64_t>(256, std::min<uint64_t>(n_pairs, kArenaBudget / per_lane));
+    nl = std::min<uint64_t>(nl, n_pairs);
+    TRY_HIP(ah.alloc(S * 3 * 4 * nl * sizeof(int32_t)));
+    TRY_HIP(ao.alloc(S * 3 * W * nl * sizeof(int32_t)));
+    TRY_HIP(am.alloc(S * 3 * W * nl * sizeof(uint32_t)));
+    TRY_HIP(at.alloc(S * nl));
+    WfaArena arena{(int32_t *)ah.p, (int32_t *)ao.p, (uint32_t *)am.p, (uint8_t *)at.p,
+                   (uint32_t)nl, (uint32_t)S, (uint32_t)W};
+    for (uint64_t first = 0; first < n_pairs; first += nl) {
+        const uint32_t cnt = (uint32_t)std::min<uint64_t>(nl, n_pairs - first);
+        TRY_HIP(launch_wfa((const WfaPairDesc *)dp.p, (uint32_t)first, cnt,
+                           (const uint8_t *)dq.p, (const uint8_t *)dd.p, arena, max_steps,
+                           (saln_wfa_result *)dr.p, (uint8_t *)da.p, (int32_t *)dl.p,
+                           (uint8_t *)de.p, ev_cap, ctx->stream));
+    }
+    TRY_HIP(hipStreamSynchronize(ctx->stream));
+    TRY_HIP(hipMemcpy(results, dr.p, n_pairs * sizeof(saln_wfa_result), hipMemcpyDeviceToHost));
+    if (aln) TRY_HIP(hipMemcpy(aln, da.p, aln_bytes, hipMemcpyDeviceToHost));
+    if (logs) {
+        logs->lohi.resize(n_pairs * 2ull * max_steps);
+        logs->ev.resize(n_pairs * (uint64_t)ev_cap);
+        logs->ev_cap = ev_cap;
+        TRY_HIP(hipMemcpy(logs->lohi.data(), dl.p, logs->lohi.size() * sizeof(int32_t),
+                          hipMemcpyDeviceToHost));
+        TRY_HIP(hipMemcpy(logs->ev.data(), de.p, logs->ev.size(), hipMemcpyDeviceToHost));
+    }
+    return SALN_OK;
+}
+
+const char *state_name(int s) { return s == 0 ? "M" : s == 1 ? "D" : "I"; }
+
+void appendf(std::string *s, const char *fmt, long long v) {
+    char b[64];
+    std::snprintf(b, sizeof b, fmt, v);
+    *s += b;
+}
+
+}  // namespace
+
+extern "C" {
+
+int saln_wfa_align_batch(saln_context *ctx, const uint8_t *q_seq, const uint64_t *q_off,
+                         uint64_t n_q, const uint8_t *db_seq, const uint64_t *db_off,
+                         uint64_t n_db, const uint32_t *pair_q, const uint32_t *pair_db,
+                         uint64_t n_pairs, int32_t mode, uint32_t max_steps, uint32_t max_width,
+                         saln_wfa_result *results, uint8_t *aln, const uint64_t *aln_off,
+                         uint32_t aln_cap) {
+    return run_wfa(ctx, q_seq, q_off, n_q, db_seq, db_off, n_db, pair_q, pair_db, n_pairs, mode,
+                   max_steps, max_width, results, aln, aln_off, aln_cap, nullptr);
+}
+
+int saln_wfa_render(saln_context *ctx, const uint8_t *q, uint64_t len_q, const uint8_t *d,
+                    uint64_t len_db, int32_t mode, uint32_t max_steps, uint32_t max_width,
+                    char *out, uint64_t cap, uint64_t *out_len, saln_wfa_result *result) {
+    if (!ctx || (len_q && !q) || (len_db && !d)) return SALN_E_INVALID;
+    if (!max_steps) max_steps = kDefaultSteps;
+    const uint64_t qo[2] = {0, len_q}, dof[2] = {0, len_db};
+    const uint32_t z = 0;
+    const uint32_t acap = (uint32_t)std::min<uint64_t>(0x7FFFFFFF, 2 * (len_q + len_db) + 64);
+    std::vector<uint8_t> aln(2ull * acap);
+    const uint64_t aoff = 0;
+    saln_wfa_result r;
+    Logs logs;
+    int rc = run_wfa(ctx, q, qo, 1, d, dof, 1, &z, &z, 1, mode, max_steps, max_width, &r,
+                     aln.data(), &aoff, acap, &logs);
+    if (rc != SALN_OK) return rc;
+    if (result) *result = r;
+    std::string t;
+    if (r.status != SALN_NOT_IMPLEMENTED) {
+        // `lo: {}, hi: {}` of every WaveFrontTensor::new that had sources (:251)
+        for (uint32_t s = 0; s < r.steps; ++s) {
+            const int32_t lo = logs.lohi[2 * s], hi = logs.lohi[2 * s + 1];
+            if (lo == INT32_MIN) continue;
+            appendf(&t, "lo: %lld, ", lo);
+            appendf(&t, "hi: %lld\n", hi);
+        }
+    }
+    if (r.status == SALN_OK || r.status == SALN_REF_PANIC_SLICE) {
+        appendf(&t, "converged with score %lld: \n", r.score);       // :38
+        appendf(&t, "huhu, diag: %lld\n", (long long)len_q - (long long)len_db);  // :650
+        t += "Element {\n";                                            // Debug :103-116
+        t += std::string("\tstate: ") + state_name(r.conv_state) + "\n";
+        appendf(&t, "\toffset: %lld\n", r.conv_offset);
+        if (!r.conv_np) {
+            t += "\tparents: []\n";
+        } else {
+            t += "\tparents: [\n";
+            for (int k = 0; k < r.conv_np; ++k)
+                t += std::string("    ") + state_name(r.conv_parents[k]) + ",\n";
+            t += "]\n";
+        }
+        t += "}\n";
+        appendf(&t, "\nscore: %lld\n", r.score);
+        // rec_tr events (:654-853): every attempt prints `well shit` or
+        // `yeah, score: N`; an attempt that moves prints its action and the
+        // walk restarts at the lower score; `open` without a move is the
+        // last attempt, so `huh` follows it.
+        enum { WELL = 0, YEAH = 1, MISMATCH = 2, EXTEND = 3, OPEN = 4, RET = 5, HUH = 6 };
+        static const uint64_t nds[3] = {4, 6, 8};
+        const uint8_t *ev = logs.ev.data();
+        const uint32_t nev = logs.ev_cap;
+        uint64_t score = (uint64_t)r.score;
+        int attempt = 0;
+        for (uint32_t k = 0; k < nev;) {
+            const uint8_t e = ev[k++];
+            if (e == RET) { t += "ret\n"; break; }
+            if (e == HUH) { t += "huh\n"; break; }
+            if (e == WELL) { t += "well shit\n"; ++attempt; continue; }
+            if (e != YEAH || attempt >= 3) break;
+            const uint64_t ns = score - nds[attempt];
+            appendf(&t, "yeah, score: %lld\n", (long long)ns);
+            const uint8_t nx = k < nev ? ev[k] : (uint8_t)HUH;
+            if (nx == MISMATCH || nx == EXTEND) {
+                t += nx == MISMATCH ? "mismatch\n" : "extend\n";
+                ++k;
+                score = ns;
+                attempt = 0;
+            } else if (nx == OPEN) {
+                t += "open\n";
+                ++k;
+                if (k < nev && ev[k] == HUH) {
+                    ++attempt;
+                } else {
+                    score = ns;
+                    attempt = 0;
+                }
+            } else {
+                ++attempt;
+            }
+        }
+        if (r.status == SALN_OK) {
+            // Display (:950-980) + println, then Debug (`{:#?}`)
+            const uint8_t *a1 = aln.data(), *a2 = aln.data() + acap;
+            const uint32_t n1 = std::min(r.aln_len1, acap), n2 = std::min(r.aln_len2, acap);
+            for (uint32_t k = n1; k > 0; --k) t += (char)a1[k - 1];
+            t += "\n";
+            for (uint32_t k = std::min(n1, n2); k > 0; --k) t += a1[k - 1] != a2[k - 1] ? " " : "|";
+            for (uint32_t k = n2; k > 0; --k) t += (char)a2[k - 1];
+            t += "\n\n";
+            t += "Alignment {\n";
+            const uint8_t *rows[2] = {a1, a2};
+            const uint32_t lens[2] = {n1, n2};
+            const char *names[2] = {"seq1", "seq2"};
+            for (int w = 0; w < 2; ++w) {
+                if (!lens[w]) {
+                    t += std::string("    ") + names[w] + ": [],\n";
+                    continue;
+                }
+                t += std::string("    ") + names[w] + ": [\n";
+                for (uint32_t k = 0; k < lens[w]; ++k) appendf(&t, "        %lld,\n", rows[w][k]);
+                t += "    ],\n";
+            }
+            t += "}\n";
+        }
+    }
+    if (out_len) *out_len = t.size();
+    if (out) {
+        std::memcpy(out, t.data(), std::min<uint64_t>(t.size(), cap));
+        if (t.size() > cap) return SALN_E_CAPACITY;
+    }
+    return SALN_OK;
+}
+
+}  // extern "C"

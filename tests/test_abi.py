@@ -51,6 +51,7 @@ def test_struct_sizes(saln):
     from sequencealigning_amd import _lib
     assert ctypes.sizeof(_lib.NwResult) == 16
     assert ctypes.sizeof(_lib.NwScoring) == 16
+    assert ctypes.sizeof(_lib.WfaResult) == 32
 
 
 def test_cli_help():
