@@ -76,6 +76,8 @@ def main() -> None:
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--pairs", type=int, default=N_PAIRS)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--score-only", action="store_true",
+                    help="score + panic status only (no parent codes / traceback; the C5 mode)")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="run each step's traceback to completion before the next fill")
     args = ap.parse_args()
@@ -101,7 +103,8 @@ def main() -> None:
     # Pipelined steps (default): the traceback of step k runs on the engine's
     # second stream while step k+1 fills; results/cigar/mask are double-buffered
     # and every step's results are complete (and gathered) inside the timed region.
-    pipelined = not args.no_pipeline
+    pipelined = not args.no_pipeline and not args.score_only
+    plan.set_score_only(args.score_only)
     plan.set_async(pipelined)
     nbuf = 2 if pipelined else 1
     res = [torch.zeros(n * 4, dtype=torch.int32, device=f"cuda:{local}") for _ in range(nbuf)]
@@ -171,14 +174,17 @@ def main() -> None:
             "ms_per_step": round(dt / args.steps * 1e3, 4), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "int16x2",
             "data": "synthetic (splitmix64 G-iid ACGT)",
-            "config": {"workload": "configs[1]: independent 150x150 NW-affine pairs per GPU "
-                                   "(fill + 1 B/cell parent mask + first-printed traceback/CIGAR)",
+            "config": {"workload": ("configs[1]: independent 150x150 NW-affine pairs per GPU "
+                                    "(fill + 1 B/cell parent mask + first-printed traceback/CIGAR)")
+                       if not args.score_only else
+                       ("score-only 150x150 NW-affine pairs per GPU (the configs[4] per-pair "
+                        "mode: score + panic status, no mask)"),
                        "pairs_per_gpu": n, "len_q": LQ, "len_db": LD, "seed": hex(SEED),
                        "parallelism": f"db-sharded x{world}" + (" + RCCL gather" if world > 1
                                                                else "")},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": pmc_traffic("nw_fill_pk_kernel<16, 10, true>"),
+                         "traffic": pmc_traffic("nw_fill_pk_kernel<16, 10,") if not args.score_only else None,
                          "traffic_unit": "bytes/launch (PMC FETCH_SIZE*2 + WRITE_SIZE)",
                          "algorithmic_bytes": cells_rank, "kernel": "nw_fill",
                          "kernel_avg_ms": round(fill_avg_s * 1e3, 4),

@@ -168,6 +168,10 @@ int saln_nw_plan_kernel_time(const saln_nw_plan *plan, const char *kernel, doubl
  * made `stream` wait for them; keep_latest = 1 leaves the most recent execute
  * pending (software pipelining). */
 int saln_nw_plan_set_async(saln_nw_plan *plan, int enable);
+/* Score-only mode (the all-vs-all C5 workload): no parent codes, no
+ * traceback; results carry score and the reference's panic status
+ * (end_states = printed = cigar_len = 0, flags bit 3 set). */
+int saln_nw_plan_set_score_only(saln_nw_plan *plan, int enable);
 int saln_nw_plan_sync(saln_nw_plan *plan, void *stream, int keep_latest);
 int saln_nw_plan_destroy(saln_nw_plan *plan);
 

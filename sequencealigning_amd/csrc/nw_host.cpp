@@ -59,6 +59,7 @@ struct saln_nw_plan {
     int32_t *d_endh2 = nullptr;
     bool async_tb = false;
     bool full_codes = false;  // walk codes (default) or every parent set
+    bool score_only = false;  // no parent codes / traceback (saln_nw_plan_set_score_only)
     int buf = 0;                           // workspace of the next execute (async mode)
     bool tb_pending[2] = {false, false};
     int last_buf = 0;
@@ -383,7 +384,9 @@ int saln_nw_execute(saln_nw_plan *p, const uint8_t *d_q, const uint8_t *d_db,
             const uint32_t b = std::min(hi, p->var_first[v] + p->var_count[v]);
             if (a < b)
                 HIP_TRY(launch_fill(v, p->d_pairs, a, b - a, d_q, d_db, mask, p->d_scratch, endh,
-                                    d_results, d_cigar, p->sc, p->full_codes, p->var_maxld[v], s));
+                                    d_results, d_cigar, p->sc,
+                                    p->score_only ? 2 : p->full_codes ? 1 : 0, p->var_maxld[v],
+                                    s));
         }
         if (ev && k + 1 == nsub) HIP_TRY(hipEventRecord(ev[1], s));
         HIP_TRY(hipEventRecord(p->sync_ev[k], s));
@@ -392,13 +395,18 @@ int saln_nw_execute(saln_nw_plan *p, const uint8_t *d_q, const uint8_t *d_db,
         for (int v = 0; v < kNumVariants; ++v) {
             const uint32_t a = std::max(lo, p->var_first[v]);
             const uint32_t b = std::min(hi, p->var_first[v] + p->var_count[v]);
-            if (a < b)
+            if (a < b && p->score_only)
+                HIP_TRY(launch_score_results(p->d_pairs, a, b - a, endh, d_results, p->sc, t));
+            else if (a < b)
                 HIP_TRY(launch_traceback(v, p->d_pairs, a, b - a, d_q, d_db, mask, endh, p->d_ops,
                                          d_results, d_cigar, p->sc, t));
         }
     }
     // pairs with an empty side (boundary-only walk) ride on the traceback stream
-    if (p->n_pairs > p->n_fill)
+    if (p->n_pairs > p->n_fill && p->score_only)
+        HIP_TRY(launch_score_results(p->d_pairs, p->n_fill, (uint32_t)(p->n_pairs - p->n_fill),
+                                     endh, d_results, p->sc, t));
+    else if (p->n_pairs > p->n_fill)
         HIP_TRY(launch_traceback(-1, p->d_pairs, p->n_fill, (uint32_t)(p->n_pairs - p->n_fill),
                                  d_q, d_db, mask, endh, p->d_ops, d_results, d_cigar, p->sc, t));
     if (ev) HIP_TRY(hipEventRecord(ev[3], t));
@@ -411,6 +419,12 @@ int saln_nw_execute(saln_nw_plan *p, const uint8_t *d_q, const uint8_t *d_db,
         HIP_TRY(hipStreamWaitEvent(s, p->tb_done(cur), 0));
         p->tb_pending[cur] = false;
     }
+    return SALN_OK;
+}
+
+int saln_nw_plan_set_score_only(saln_nw_plan *p, int enable) {
+    if (!p) return SALN_E_INVALID;
+    p->score_only = enable != 0;
     return SALN_OK;
 }
 

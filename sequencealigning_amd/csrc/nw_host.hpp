@@ -21,7 +21,11 @@ namespace saln {
 hipError_t launch_fill(int variant, const NwPairDesc *pairs, uint32_t first, uint32_t count,
                        const uint8_t *qs, const uint8_t *ds, uint8_t *mask, int2 *scratch,
                        int32_t *end_h, saln_nw_result *results, uint32_t *cigar, Scoring sc,
-                       bool full_codes, uint32_t ld_max, hipStream_t stream);
+                       int codes /* 0 walk, 1 full, 2 none */, uint32_t ld_max,
+                       hipStream_t stream);
+hipError_t launch_score_results(const NwPairDesc *pairs, uint32_t first, uint32_t n,
+                                const int32_t *end_h, saln_nw_result *results, Scoring sc,
+                                hipStream_t stream);
 hipError_t launch_traceback(int variant, const NwPairDesc *pairs, uint32_t first, uint32_t n,
                             const uint8_t *qs,
                             const uint8_t *ds, const uint8_t *mask, const int32_t *end_h,

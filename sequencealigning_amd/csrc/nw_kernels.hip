@@ -717,10 +717,12 @@ struct PkMask {
     uint32_t w[(K + 3) / 4];
 };
 
-// kWalk: store walk codes only (argM/argI/argD, I-open, D-open, eq) - the
+// kCodes: kCodesWalk stores walk codes only (argM/argI/argD, I-open, D-open,
+// eq) - the
 // bits the device walker reads; the extend bits (3, 5) are left 0.  Full
 // codes (every parent set) are kept for the dense-mask / render paths.
-template <int G, int K, bool kWalk>
+enum { kCodesWalk = 0, kCodesFull = 1, kCodesNone = 2 };
+template <int G, int K, int kCodes>
 __global__ __launch_bounds__(256) void nw_fill_pk_kernel(const NwPairDesc *__restrict__ pairs,
                                                          uint32_t first, uint32_t count,
                                                          const uint8_t *__restrict__ qs,
@@ -817,6 +819,7 @@ __global__ __launch_bounds__(256) void nw_fill_pk_kernel(const NwPairDesc *__res
                 const s16x2 H = vmax(M, vmax(I, D));
                 const s16x2 Hc = as_s2(as_u(H) & 0xFFFEFFFEu);
                 const s16x2 tO = M + kOpen;
+                if constexpr (kCodes != kCodesNone) {
                 // sign set <=> parent absent.  Extend/open ties are decided on
                 // the flag-free order: with X = 2x+f, tO = 2o+g,
                 // ext <=> x >= o <=> X >= (tO & ~1),  open <=> o >= x <=> (tO | 1) >= X.
@@ -825,7 +828,7 @@ __global__ __launch_bounds__(256) void nw_fill_pk_kernel(const NwPairDesc *__res
                 const uint32_t s4 = as_u(tOr - I), s6 = as_u(tOr - D);
                 const uint32_t s7 = as_u(pen - spl(1));  // sign <=> q == d (bit 7)
                 uint32_t a = sign_bytes(s0, s1) & 0x02010201u;
-                if constexpr (kWalk) {
+                if constexpr (kCodes == kCodesWalk) {
                     a = (sign_bytes(s2, s4) & 0x10041004u) | a;
                 } else {
                     const s16x2 tOc = as_s2(as_u(tO) & 0xFFFEFFFEu);
@@ -839,6 +842,7 @@ __global__ __launch_bounds__(256) void nw_fill_pk_kernel(const NwPairDesc *__res
                     pack4(acc[0], k % 4 >= 1 ? acc[1] : 0u, k % 4 >= 2 ? acc[2] : 0u,
                           k % 4 >= 3 ? acc[3] : 0u, wa.w[k / 4], wb.w[k / 4]);
                 }
+                }
                 F = as_u(vmax(tO, I));
                 Dn[k] = as_u(vmax(tO, D) + kDstep);
                 hd = Hp[k];
@@ -847,8 +851,10 @@ __global__ __launch_bounds__(256) void nw_fill_pk_kernel(const NwPairDesc *__res
             hd = inH;
             pubF = F;
             pubH = Hp[K - 1];
-            if (r <= ldA) *reinterpret_cast<PkMask<K> *>(mA + (uint64_t)(r - 1) * pa.mask_rs) = wa;
-            if (r <= ldB) *reinterpret_cast<PkMask<K> *>(mB + (uint64_t)(r - 1) * pb.mask_rs) = wb;
+            if constexpr (kCodes != kCodesNone) {
+                if (r <= ldA) *reinterpret_cast<PkMask<K> *>(mA + (uint64_t)(r - 1) * pa.mask_rs) = wa;
+                if (r <= ldB) *reinterpret_cast<PkMask<K> *>(mB + (uint64_t)(r - 1) * pb.mask_rs) = wb;
+            }
             if (r == ldA && lane == lA) {
                 int32_t e = 0;
 #pragma unroll
@@ -871,6 +877,37 @@ __global__ __launch_bounds__(256) void nw_fill_pk_kernel(const NwPairDesc *__res
     (void)cigar;
 }
 
+// Score-only results (saln_nw_plan_set_score_only): score and panic status
+// from the end value; no traceback fields (flags bit 3).
+__global__ __launch_bounds__(256) void nw_score_results_kernel(const NwPairDesc *__restrict__ pairs,
+                                                               uint32_t first, uint32_t n,
+                                                               const int32_t *__restrict__ end_h,
+                                                               saln_nw_result *__restrict__ results,
+                                                               Scoring sc) {
+    const uint32_t idx = first + blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= first + n) return;
+    const NwPairDesc p = pairs[idx];
+    const int32_t h = p.len_q && p.len_db ? end_h[idx] : hs_boundary_end(sc, p.len_q, p.len_db);
+    saln_nw_result r;
+    r.score = h >> 1;
+    r.status = (h & 1) ? SALN_REF_PANIC_BOUNDARY : SALN_OK;
+    r.cigar_len = 0;
+    r.end_states = 0;
+    r.printed = 0;
+    r.flags = 8;
+    r.reserved = 0;
+    results[p.pair_id] = r;
+}
+
+hipError_t launch_score_results(const NwPairDesc *pairs, uint32_t first, uint32_t n,
+                                const int32_t *end_h, saln_nw_result *results, Scoring sc,
+                                hipStream_t stream) {
+    if (!n) return hipSuccess;
+    nw_score_results_kernel<<<dim3((n + 255) / 256), dim3(256), 0, stream>>>(pairs, first, n, end_h,
+                                                                            results, sc);
+    return hipGetLastError();
+}
+
 // ----------------------------------------------------------------- launchers
 // variants 0-3: i32 lanes; 4-6: packed i16 (two pairs per lane)
 constexpr Geom kVariants[kNumVariants] = {{16, 10}, {16, 16}, {64, 8}, {64, 16},
@@ -889,21 +926,24 @@ static void fill_i32(dim3 grid, hipStream_t s, const NwPairDesc *pairs, uint32_t
 template <int G, int K>
 static void fill_pk(dim3 grid, hipStream_t s, const NwPairDesc *pairs, uint32_t first,
                     uint32_t count, const uint8_t *qs, const uint8_t *ds, uint8_t *mask,
-                    int32_t *end_h, saln_nw_result *res, uint32_t *cig, Scoring sc, bool full,
+                    int32_t *end_h, saln_nw_result *res, uint32_t *cig, Scoring sc, int codes,
                     uint32_t ld_max) {
     const size_t lds = (size_t)(256 / G) * ld_max * sizeof(uint32_t);
-    if (full)
-        nw_fill_pk_kernel<G, K, false><<<grid, dim3(256), lds, s>>>(
+    if (codes == kCodesFull)
+        nw_fill_pk_kernel<G, K, kCodesFull><<<grid, dim3(256), lds, s>>>(
+            pairs, first, count, qs, ds, mask, end_h, res, cig, sc, ld_max);
+    else if (codes == kCodesNone)
+        nw_fill_pk_kernel<G, K, kCodesNone><<<grid, dim3(256), lds, s>>>(
             pairs, first, count, qs, ds, mask, end_h, res, cig, sc, ld_max);
     else
-        nw_fill_pk_kernel<G, K, true><<<grid, dim3(256), lds, s>>>(
+        nw_fill_pk_kernel<G, K, kCodesWalk><<<grid, dim3(256), lds, s>>>(
             pairs, first, count, qs, ds, mask, end_h, res, cig, sc, ld_max);
 }
 
 hipError_t launch_fill(int variant, const NwPairDesc *pairs, uint32_t first, uint32_t count,
                        const uint8_t *qs, const uint8_t *ds, uint8_t *mask, int2 *scratch,
                        int32_t *end_h, saln_nw_result *res, uint32_t *cig, Scoring sc,
-                       bool full_codes, uint32_t ld_max, hipStream_t stream) {
+                       int codes, uint32_t ld_max, hipStream_t stream) {
     if (count == 0) return hipSuccess;
     const uint32_t gpb = 256 / kVariants[variant].G;  // lane groups per block
     const uint32_t groups = kPacked[variant] ? (count + 1) / 2 : count;
@@ -914,10 +954,10 @@ hipError_t launch_fill(int variant, const NwPairDesc *pairs, uint32_t first, uin
         case 1: fill_i32<16, 16>(grid, stream, pairs, first, count, qs, ds, mask, scratch, end_h, res, cig, sc); break;
         case 2: fill_i32<64, 8>(grid, stream, pairs, first, count, qs, ds, mask, scratch, end_h, res, cig, sc); break;
         case 3: fill_i32<64, 16>(grid, stream, pairs, first, count, qs, ds, mask, scratch, end_h, res, cig, sc); break;
-        case 4: fill_pk<8, 19>(grid, stream, pairs, first, count, qs, ds, mask, end_h, res, cig, sc, full_codes, ld_max); break;
-        case 5: fill_pk<16, 16>(grid, stream, pairs, first, count, qs, ds, mask, end_h, res, cig, sc, full_codes, ld_max); break;
-        case 7: fill_pk<16, 10>(grid, stream, pairs, first, count, qs, ds, mask, end_h, res, cig, sc, full_codes, ld_max); break;
-        default: fill_pk<32, 16>(grid, stream, pairs, first, count, qs, ds, mask, end_h, res, cig, sc, full_codes, ld_max); break;
+        case 4: fill_pk<8, 19>(grid, stream, pairs, first, count, qs, ds, mask, end_h, res, cig, sc, codes, ld_max); break;
+        case 5: fill_pk<16, 16>(grid, stream, pairs, first, count, qs, ds, mask, end_h, res, cig, sc, codes, ld_max); break;
+        case 7: fill_pk<16, 10>(grid, stream, pairs, first, count, qs, ds, mask, end_h, res, cig, sc, codes, ld_max); break;
+        default: fill_pk<32, 16>(grid, stream, pairs, first, count, qs, ds, mask, end_h, res, cig, sc, codes, ld_max); break;
     }
     return hipGetLastError();
 }

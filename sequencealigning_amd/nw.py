@@ -231,6 +231,10 @@ class NwPlan:
             stream = torch.cuda.current_stream(self.device).cuda_stream
         _lib.check(self._L.saln_nw_plan_sync(self._h, stream, int(keep_latest)), "sync")
 
+    def set_score_only(self, enable: bool) -> None:
+        """Score + panic status only: no parent codes, no traceback (C5)."""
+        _lib.check(self._L.saln_nw_plan_set_score_only(self._h, int(enable)), "set_score_only")
+
     def set_timing(self, enable: bool) -> None:
         _lib.check(self._L.saln_nw_plan_set_timing(self._h, int(enable)), "set_timing")
 

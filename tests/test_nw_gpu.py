@@ -205,3 +205,34 @@ def test_pipelined_plan_matches_sync(saln):
         assert torch.equal(got[s][1], want[s][1]), s
     sync_plan.close()
     pipe.close()
+
+
+def test_score_only_plan_matches_full(saln):
+    """saln_nw_plan_set_score_only (C5 mode): same scores and panic statuses
+    as the full fill + traceback, over packed and i32 variants and empty sides."""
+    import torch
+    from sequencealigning_amd import synth
+    rng = np.random.default_rng(8)
+    n = 2000
+    lq = rng.integers(0, 700, n)
+    ld = rng.integers(0, 700, n)
+    qo = np.zeros(n + 1, np.uint64); qo[1:] = np.cumsum(lq)
+    do = np.zeros(n + 1, np.uint64); do[1:] = np.cumsum(ld)
+    qs = torch.from_numpy(synth.random_bases(41, int(qo[-1]))).cuda()
+    ds = torch.from_numpy(synth.random_bases(42, int(do[-1]))).cuda()
+    pairs = np.stack([np.arange(n), np.arange(n)], 1)
+    full = saln.NwPlan(qo, do, pairs=pairs)
+    fast = saln.NwPlan(qo, do, pairs=pairs)
+    fast.set_score_only(True)
+    r1 = torch.zeros(n * 4, dtype=torch.int32, device="cuda")
+    r2 = torch.zeros(n * 4, dtype=torch.int32, device="cuda")
+    full.execute(qs, ds, r1, None)
+    fast.execute(qs, ds, r2, None)
+    torch.cuda.synchronize()
+    a = r1.cpu().numpy().reshape(n, 4)
+    b = r2.cpu().numpy().reshape(n, 4)
+    assert np.array_equal(a[:, 0], b[:, 0])          # score
+    assert np.array_equal(a[:, 1], b[:, 1])          # status
+    assert ((b[:, 3] >> 16) & 0xFF == 8).all()       # flags: score-only
+    full.close()
+    fast.close()
