@@ -70,6 +70,7 @@ static int run_batch(saln_context *ctx, const uint8_t *q_seq, const uint64_t *q_
                          (saln_nw_result *)dr.p, (uint32_t *)dc.p, nullptr);
     if (rc != SALN_OK) return rc;
     TRY_HIP(hipDeviceSynchronize());
+    if ((rc = plan_check_error(g.p)) != SALN_OK) return rc;
     TRY_HIP(hipMemcpy(results, dr.p, n_pairs * sizeof(saln_nw_result), hipMemcpyDeviceToHost));
     std::vector<uint32_t> hc(cig_words);
     if (cig_words) TRY_HIP(hipMemcpy(hc.data(), dc.p, cig_words * 4, hipMemcpyDeviceToHost));

@@ -65,6 +65,12 @@ struct saln_nw_plan {
     int last_buf = 0;
     uint64_t mask_bytes = 0;
     int2 *d_scratch = nullptr;
+    // column-stripe pairs (kStripeVariant): work items (plan index, chunk),
+    // per-pair first work item (plan order, n_pairs+1), progress counters
+    uint2 *d_work = nullptr;
+    std::vector<uint32_t> work_first;
+    uint32_t *d_prog = nullptr, *d_err = nullptr;
+    uint64_t n_prog = 0;
     uint32_t *d_ops = nullptr;  // traceback op-stream scratch (one traceback at a time)
     uint64_t scratch_elems = 0;
     int32_t *d_endh = nullptr;
@@ -134,6 +140,9 @@ int saln_nw_plan_destroy(saln_nw_plan *p) {
     (void)hipFree(p->d_mask2);
     (void)hipFree(p->d_endh2);
     (void)hipFree(p->d_scratch);
+    (void)hipFree(p->d_work);
+    (void)hipFree(p->d_prog);
+    (void)hipFree(p->d_err);
     (void)hipFree(p->d_ops);
     (void)hipFree(p->d_endh);
     for (auto &e : p->sync_ev) (void)hipEventDestroy(e);
@@ -218,7 +227,9 @@ int saln_nw_plan_create(saln_context *ctx, const uint64_t *q_off, uint64_t n_q,
             ooff += (d.len_q + d.len_db + 9) / 10 + 1;  // 3-bit ops, ten per word
             if (g.n_chunks(d.len_q) > 1) {
                 d.scratch_off = soff;
-                soff += d.len_db + 2;
+                // stripes run concurrently: one boundary column per chunk boundary
+                soff += (uint64_t)(d.variant == kStripeVariant ? g.n_chunks(d.len_q) : 1) *
+                        (d.len_db + 2);
             }
             if (p->var_count[d.variant] == 0) p->var_first[d.variant] = (uint32_t)r;
             p->var_count[d.variant]++;
@@ -306,6 +317,34 @@ int saln_nw_plan_create(saln_context *ctx, const uint64_t *q_off, uint64_t n_q,
     // +64 B: the traceback walker reads whole 5-dword segments
     if (moff && (e = hipMalloc(&p->d_mask, moff + 64)) != hipSuccess)
         return fail(e, "hipMalloc(mask workspace)");
+    {
+        // stripe work list (pair-major, chunk-ascending: a stripe's predecessor
+        // always has a lower workgroup id) and progress counters
+        std::vector<uint2> work;
+        p->work_first.assign(n_pairs + 1, 0);
+        for (uint64_t r = 0; r < n_pairs; ++r) {
+            NwPairDesc &d = p->h_pairs[r];
+            p->work_first[r] = (uint32_t)work.size();
+            if (d.variant != (uint32_t)kStripeVariant || !d.len_q || !d.len_db) continue;
+            const uint32_t nch = variant_geom(kStripeVariant).n_chunks(d.len_q);
+            d.reserved = (uint32_t)p->n_prog;
+            p->n_prog += nch;
+            for (uint32_t ch = 0; ch < nch; ++ch) work.push_back(make_uint2((uint32_t)r, ch));
+        }
+        p->work_first[n_pairs] = (uint32_t)work.size();
+        if (!work.empty()) {
+            if ((e = hipMalloc(&p->d_work, work.size() * sizeof(uint2))) != hipSuccess ||
+                (e = hipMemcpy(p->d_work, work.data(), work.size() * sizeof(uint2),
+                               hipMemcpyHostToDevice)) != hipSuccess ||
+                (e = hipMalloc(&p->d_prog, p->n_prog * sizeof(uint32_t))) != hipSuccess ||
+                (e = hipMalloc(&p->d_err, sizeof(uint32_t))) != hipSuccess ||
+                (e = hipMemset(p->d_err, 0, sizeof(uint32_t))) != hipSuccess)
+                return fail(e, "stripe work list");
+            if ((e = hipMemcpy(p->d_pairs, p->h_pairs.data(), n_pairs * sizeof(NwPairDesc),
+                               hipMemcpyHostToDevice)) != hipSuccess)
+                return fail(e, "hipMemcpy(pairs)");
+        }
+    }
     if (soff && (e = hipMalloc(&p->d_scratch, soff * sizeof(int2))) != hipSuccess)
         return fail(e, "hipMalloc(scratch)");
     if (ooff && (e = hipMalloc(&p->d_ops, ooff * sizeof(uint32_t))) != hipSuccess)
@@ -382,7 +421,18 @@ int saln_nw_execute(saln_nw_plan *p, const uint8_t *d_q, const uint8_t *d_db,
         for (int v = 0; v < kNumVariants; ++v) {
             const uint32_t a = std::max(lo, p->var_first[v]);
             const uint32_t b = std::min(hi, p->var_first[v] + p->var_count[v]);
-            if (a < b)
+            if (a < b && v == kStripeVariant) {
+                const uint32_t w0 = p->work_first[a], w1 = p->work_first[b];
+                if (w1 > w0) {
+                    const uint32_t g0 = p->h_pairs[a].reserved;
+                    const uint32_t g1 = p->h_pairs[b - 1].reserved +
+                                        variant_geom(v).n_chunks(p->h_pairs[b - 1].len_q);
+                    HIP_TRY(hipMemsetAsync(p->d_prog + g0, 0, (g1 - g0) * sizeof(uint32_t), s));
+                    HIP_TRY(launch_fill_stripes(p->d_pairs, p->d_work + w0, w1 - w0, d_q, d_db,
+                                                mask, p->d_scratch, p->d_prog, p->d_err, endh,
+                                                p->sc, s));
+                }
+            } else if (a < b)
                 HIP_TRY(launch_fill(v, p->d_pairs, a, b - a, d_q, d_db, mask, p->d_scratch, endh,
                                     d_results, d_cigar, p->sc,
                                     p->score_only ? 2 : p->full_codes ? 1 : 0, p->var_maxld[v],
@@ -696,4 +746,17 @@ bool first_alignment(const HostMask &hm, const uint8_t *q, const uint8_t *d,
     return false;
 }
 
+}  // namespace saln
+
+namespace saln {
+int plan_check_error(const saln_nw_plan *p) {
+    if (!p || !p->d_err) return SALN_OK;
+    uint32_t v = 0;
+    HIP_TRY(hipMemcpy(&v, p->d_err, sizeof v, hipMemcpyDeviceToHost));
+    if (v) {
+        set_error("column-stripe dependency wait timed out");
+        return SALN_E_HIP;
+    }
+    return SALN_OK;
+}
 }  // namespace saln

@@ -23,6 +23,11 @@ hipError_t launch_fill(int variant, const NwPairDesc *pairs, uint32_t first, uin
                        int32_t *end_h, saln_nw_result *results, uint32_t *cigar, Scoring sc,
                        int codes /* 0 walk, 1 full, 2 none */, uint32_t ld_max,
                        hipStream_t stream);
+hipError_t launch_fill_stripes(const NwPairDesc *pairs, const uint2 *work, uint32_t n_work,
+                               const uint8_t *qs, const uint8_t *ds, uint8_t *mask,
+                               int2 *scratch, uint32_t *prog, uint32_t *err, int32_t *end_h,
+                               Scoring sc, hipStream_t stream);
+constexpr int kStripeVariant = 3;
 hipError_t launch_score_results(const NwPairDesc *pairs, uint32_t first, uint32_t n,
                                 const int32_t *end_h, saln_nw_result *results, Scoring sc,
                                 hipStream_t stream);
@@ -74,6 +79,9 @@ struct HostMask {
     // Dense export (include/saln.h saln_nw_dense_mask).
     void to_dense(uint8_t *out) const;
 };
+
+// SALN_E_HIP if a column-stripe fill hit its dependency-wait bound.
+int plan_check_error(const saln_nw_plan *plan);
 
 // Full parent codes (every parent set, needed by the host DFS and the dense
 // export) instead of the walk codes a plan stores by default.

@@ -657,6 +657,145 @@ __global__ __launch_bounds__(256) void nw_fill_kernel(const NwPairDesc *__restri
     (void)cigar;
 }
 
+// ----------------------------------------------------- long pairs: stripes
+// One wave per column stripe of G*K = 64*K columns; all stripes of a pair run
+// concurrently as a pipeline down the rows (the "anti-diagonal tiling across
+// CUs" of configs[3]).  Stripe c's last lane publishes, per row, the H and
+// I-candidate leaving its last column (scratch column c) and, every kPub
+// rows, its progress counter with an agent-scope release; stripe c+1 reads
+// 32-row blocks of that column after an acquire of the counter.  Work items
+// are ordered pair-major, chunk-ascending, so a stripe's predecessor always
+// has a lower workgroup id and has been dispatched before it (no deadlock);
+// a bounded spin turns a lost dependency into an error flag instead of a hang.
+constexpr uint32_t kPub = 32;
+constexpr uint32_t kSpinCap = 1u << 24;
+
+template <int K>
+__global__ __launch_bounds__(64) void nw_fill_stripe_kernel(
+    const NwPairDesc *__restrict__ pairs, const uint2 *__restrict__ work,
+    const uint8_t *__restrict__ qs, const uint8_t *__restrict__ ds, uint8_t *__restrict__ mask,
+    int2 *__restrict__ scratch, uint32_t *__restrict__ prog, uint32_t *__restrict__ err,
+    int32_t *__restrict__ end_h, Scoring sc) {
+    constexpr int G = 64;
+    constexpr int KD = (K + 3) / 4;
+    constexpr Geom geo{G, K};
+    const int lane = threadIdx.x;
+    const uint2 wk = work[blockIdx.x];
+    const NwPairDesc p = pairs[wk.x];
+    const uint32_t c = wk.y;
+    const uint32_t lq = p.len_q, ld = p.len_db;
+    const uint8_t *__restrict__ q = qs + p.q_off;
+    const uint8_t *__restrict__ d = ds + p.db_off;
+    const uint32_t nch = geo.n_chunks(lq);
+    const int2 *__restrict__ scr_in = c > 0 ? scratch + p.scratch_off + (uint64_t)(c - 1) * (ld + 2) : nullptr;
+    int2 *__restrict__ scr_out = c + 1 < nch ? scratch + p.scratch_off + (uint64_t)c * (ld + 2) : nullptr;
+    uint32_t *prog_in = c > 0 ? prog + p.reserved + c - 1 : nullptr;
+    uint32_t *prog_out = prog + p.reserved + c;
+    const int32_t sM = 2 * sc.match, sX = 2 * sc.mismatch;
+    const int32_t sO = 2 * sc.gap_open, sE = 2 * sc.gap_extend;
+    const uint32_t jend = lq - 1;
+    const bool end_lane = jend / geo.W() == c && (uint32_t)lane == (jend % geo.W()) / K;
+    const uint32_t k_end = jend % K;
+
+    const uint32_t col0 = c * geo.W() + (uint32_t)lane * K;  // my columns: col0+1 .. col0+K
+    int32_t qc[K], Hp[K], Dn[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const uint32_t j = col0 + k + 1;
+        qc[k] = j <= lq ? (int32_t)q[j - 1] : -1;
+        Hp[k] = hs_row0(sc, j);
+        Dn[k] = ds_row1(sc, j);
+    }
+    int32_t hd = hs_row0(sc, col0);
+    int32_t pubF = 0, pubH = 0;
+    int32_t dnext = (lane == 0) ? (int32_t)d[0] : 0;
+    int32_t blkH = 0, blkF = 0;  // lanes 0..31: the left column of the current 32-row block
+    uint32_t avail = 0;          // rows of the left column known to be published
+    bool failed = false;
+    uint8_t *mseg = mask + p.mask_off + (uint64_t)(c * G + (uint32_t)lane) * p.mask_bs;
+    const int T = (int)geo.steps(ld);
+    for (int t = 0; t < T; ++t) {
+        const int r = t - lane + 1;
+        const int32_t dch = dnext;
+        if (r >= 0 && r < (int)ld) dnext = (int32_t)d[r];
+        int32_t bF, bH;
+        const uint32_t rr = (uint32_t)t + 1;  // lane 0's row
+        if (c == 0) {
+            bF = is_col1(sc, rr);
+            bH = hs_col0(sc, rr);
+        } else {
+            if ((rr - 1) % kPub == 0 && rr <= ld) {  // new 32-row block of the left column
+                const uint32_t need = min(rr - 1 + kPub, ld);
+                uint32_t spins = 0;
+                while (avail < need && !failed) {
+                    avail = __hip_atomic_load(prog_in, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+                    avail = __builtin_amdgcn_readfirstlane(avail);
+                    if (avail < need) {
+                        __builtin_amdgcn_s_sleep(2);
+                        if (++spins > kSpinCap) failed = true;
+                    }
+                }
+                const uint32_t row = rr + (uint32_t)lane;
+                if (lane < (int)kPub && row <= ld) {
+                    const int2 v = scr_in[row];
+                    blkH = v.x;
+                    blkF = v.y;
+                }
+            }
+            const uint32_t sl = (rr - 1) % kPub;
+            bH = __builtin_amdgcn_readlane(blkH, sl);
+            bF = __builtin_amdgcn_readlane(blkF, sl);
+        }
+        const int32_t inF = shr1<G>(bF, pubF);
+        const int32_t inH = shr1<G>(bH, pubH);
+        if (r >= 1 && r <= (int)ld) {
+            int32_t F = inF;
+            MaskWords<K> mw;
+#pragma unroll
+            for (int k = 0; k < KD; ++k) mw.w[k] = 0;
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                const bool eq = qc[k] == dch;
+                const int32_t M = hd + (eq ? sM : sX);
+                const int32_t I = F, D = Dn[k];
+                const int32_t H = max(M, max(I, D));
+                const int32_t Hc = H & ~1;
+                const int32_t tO = M + sO;
+                uint32_t b = (M >= Hc ? kArgM : 0u) | (I >= Hc ? kArgI : 0u) |
+                             (D >= Hc ? kArgD : 0u);
+                b |= ((I | 1) >= tO ? kIExt : 0u) | ((tO | 1) >= I ? kIOpen : 0u);
+                b |= ((D | 1) >= tO ? kDExt : 0u) | ((tO | 1) >= D ? kDOpen : 0u);
+                b |= eq ? 0x80u : 0u;
+                mw.w[k / 4] |= b << (8 * (k % 4));
+                F = max(tO, I) + sE;
+                Dn[k] = max(tO, D) + sE;
+                hd = Hp[k];
+                Hp[k] = H;
+            }
+            hd = inH;
+            pubF = F;
+            pubH = Hp[K - 1];
+#pragma unroll
+            for (int k = 0; k < KD; ++k) mw.w[k] ^= 0x7F7F7F7Fu;
+            *reinterpret_cast<MaskWords<K> *>(mseg + (uint64_t)(r - 1) * p.mask_rs) = mw;
+            if (lane == G - 1 && scr_out) {
+                scr_out[r] = make_int2(pubH, pubF);
+                if ((uint32_t)r % kPub == 0 || (uint32_t)r == ld)
+                    __hip_atomic_store(prog_out, (uint32_t)r, __ATOMIC_RELEASE,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+            }
+            if (end_lane && r == (int)ld) {
+                int32_t e = 0;
+#pragma unroll
+                for (int k = 0; k < K; ++k)
+                    if ((uint32_t)k == k_end) e = Hp[k];
+                end_h[wk.x] = e;
+            }
+        }
+    }
+    if (failed && lane == 0) atomicOr(err, 1u);
+}
+
 // ------------------------------------------------------- packed-i16 fill
 // Two pairs per lane group: pair A in the low 16 bits of every register,
 // pair B in the high 16 bits, so every v_pk_* instruction advances two cells.
@@ -910,7 +1049,7 @@ hipError_t launch_score_results(const NwPairDesc *pairs, uint32_t first, uint32_
 
 // ----------------------------------------------------------------- launchers
 // variants 0-3: i32 lanes; 4-6: packed i16 (two pairs per lane)
-constexpr Geom kVariants[kNumVariants] = {{16, 10}, {16, 16}, {64, 8}, {64, 16},
+constexpr Geom kVariants[kNumVariants] = {{16, 10}, {16, 16}, {64, 8}, {64, 4},
                                           {8, 19},  {16, 16}, {32, 16}, {16, 10}};
 constexpr bool kPacked[kNumVariants] = {false, false, false, false, true, true, true, true};
 
@@ -953,7 +1092,7 @@ hipError_t launch_fill(int variant, const NwPairDesc *pairs, uint32_t first, uin
         case 0: fill_i32<16, 10>(grid, stream, pairs, first, count, qs, ds, mask, scratch, end_h, res, cig, sc); break;
         case 1: fill_i32<16, 16>(grid, stream, pairs, first, count, qs, ds, mask, scratch, end_h, res, cig, sc); break;
         case 2: fill_i32<64, 8>(grid, stream, pairs, first, count, qs, ds, mask, scratch, end_h, res, cig, sc); break;
-        case 3: fill_i32<64, 16>(grid, stream, pairs, first, count, qs, ds, mask, scratch, end_h, res, cig, sc); break;
+        case 3: return hipErrorInvalidValue;  // stripes: launch_fill_stripes
         case 4: fill_pk<8, 19>(grid, stream, pairs, first, count, qs, ds, mask, end_h, res, cig, sc, codes, ld_max); break;
         case 5: fill_pk<16, 16>(grid, stream, pairs, first, count, qs, ds, mask, end_h, res, cig, sc, codes, ld_max); break;
         case 7: fill_pk<16, 10>(grid, stream, pairs, first, count, qs, ds, mask, end_h, res, cig, sc, codes, ld_max); break;
@@ -983,7 +1122,7 @@ hipError_t launch_traceback(int variant, const NwPairDesc *pairs, uint32_t first
         case 0: tb_lds<16, 10>(grid, stream, pairs, first, n, mask, end_h, ops, results, cigar, sc); break;
         case 1: tb_lds<16, 16>(grid, stream, pairs, first, n, mask, end_h, ops, results, cigar, sc); break;
         case 2: tb_lds<64, 8>(grid, stream, pairs, first, n, mask, end_h, ops, results, cigar, sc); break;
-        case 3: tb_lds<64, 16>(grid, stream, pairs, first, n, mask, end_h, ops, results, cigar, sc); break;
+        case 3: tb_lds<64, 4>(grid, stream, pairs, first, n, mask, end_h, ops, results, cigar, sc); break;
         case 5: tb_lds<16, 16>(grid, stream, pairs, first, n, mask, end_h, ops, results, cigar, sc); break;
         case 6: tb_lds<32, 16>(grid, stream, pairs, first, n, mask, end_h, ops, results, cigar, sc); break;
         case 7: tb_lds<16, 10>(grid, stream, pairs, first, n, mask, end_h, ops, results, cigar, sc); break;
@@ -994,6 +1133,16 @@ hipError_t launch_traceback(int variant, const NwPairDesc *pairs, uint32_t first
                                                                 end_h, results, cigar, sc, gt);
         }
     }
+    return hipGetLastError();
+}
+
+hipError_t launch_fill_stripes(const NwPairDesc *pairs, const uint2 *work, uint32_t n_work,
+                               const uint8_t *qs, const uint8_t *ds, uint8_t *mask,
+                               int2 *scratch, uint32_t *prog, uint32_t *err, int32_t *end_h,
+                               Scoring sc, hipStream_t stream) {
+    if (!n_work) return hipSuccess;
+    nw_fill_stripe_kernel<4><<<dim3(n_work), dim3(64), 0, stream>>>(pairs, work, qs, ds, mask,
+                                                                     scratch, prog, err, end_h, sc);
     return hipGetLastError();
 }
 
@@ -1025,7 +1174,7 @@ int choose_variant(uint32_t len_q, uint32_t len_db, const Scoring &sc) {
     if (len_q <= 160) return 0;
     if (len_q <= 256) return 1;
     if (len_q <= 512) return 2;
-    return 3;
+    return 3;  // column stripes, one wave each (nw_fill_stripe_kernel)
 }
 
 }  // namespace saln
