@@ -661,9 +661,11 @@ __global__ __launch_bounds__(256) void nw_fill_kernel(const NwPairDesc *__restri
 // One wave per column stripe of G*K = 64*K columns; all stripes of a pair run
 // concurrently as a pipeline down the rows (the "anti-diagonal tiling across
 // CUs" of configs[3]).  Stripe c's last lane publishes, per row, the H and
-// I-candidate leaving its last column (scratch column c) and, every kPub
-// rows, its progress counter with an agent-scope release; stripe c+1 reads
-// 32-row blocks of that column after an acquire of the counter.  Work items
+// I-candidate leaving its last column (scratch column c, agent-coherent
+// stores) and, every kPub rows once those stores are complete, its progress
+// counter; stripe c+1 polls the counter and then reads 32-row blocks of that
+// column with agent-coherent loads.  (A release/acquire pair would write
+// back and invalidate the whole L2 at every publication.)  Work items
 // are ordered pair-major, chunk-ascending, so a stripe's predecessor always
 // has a lower workgroup id and has been dispatched before it (no deadlock);
 // a bounded spin turns a lost dependency into an error flag instead of a hang.
@@ -708,16 +710,29 @@ __global__ __launch_bounds__(64) void nw_fill_stripe_kernel(
     }
     int32_t hd = hs_row0(sc, col0);
     int32_t pubF = 0, pubH = 0;
-    int32_t dnext = (lane == 0) ? (int32_t)d[0] : 0;
+    // db chars: lane 0 needs d[t] at step t; it is wave-uniform, so it comes
+    // through a scalar load (lgkmcnt: no wait on the mask stores' vmcnt), and
+    // the other lanes take their row's char from their left neighbour's
+    // previous step (DPP).
+    typedef const __attribute__((address_space(4))) uint32_t cu32;  // constant: scalar loads
+    cu32 *dw = (cu32 *)((uintptr_t)d & ~(uintptr_t)3);
+    const uint32_t dsh = (uint32_t)((uintptr_t)d & 3);
+    int32_t dch = 0;
     int32_t blkH = 0, blkF = 0;  // lanes 0..31: the left column of the current 32-row block
     uint32_t avail = 0;          // rows of the left column known to be published
     bool failed = false;
     uint8_t *mseg = mask + p.mask_off + (uint64_t)(c * G + (uint32_t)lane) * p.mask_bs;
     const int T = (int)geo.steps(ld);
+    // the query chars above arrive here: otherwise the wait for them lands
+    // inside the loop, where it would also wait for every mask store
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
     for (int t = 0; t < T; ++t) {
         const int r = t - lane + 1;
-        const int32_t dch = dnext;
-        if (r >= 0 && r < (int)ld) dnext = (int32_t)d[r];
+        {
+            const uint32_t j = (uint32_t)min(t, (int)ld - 1) + dsh;
+            const uint32_t w = __builtin_amdgcn_readfirstlane(dw[j >> 2]);
+            dch = shr1<G>((int32_t)((w >> (8 * (j & 3))) & 0xFFu), dch);  // d[r-1]
+        }
         int32_t bF, bH;
         const uint32_t rr = (uint32_t)t + 1;  // lane 0's row
         if (c == 0) {
@@ -728,7 +743,7 @@ __global__ __launch_bounds__(64) void nw_fill_stripe_kernel(
                 const uint32_t need = min(rr - 1 + kPub, ld);
                 uint32_t spins = 0;
                 while (avail < need && !failed) {
-                    avail = __hip_atomic_load(prog_in, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+                    avail = __hip_atomic_load(prog_in, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     avail = __builtin_amdgcn_readfirstlane(avail);
                     if (avail < need) {
                         __builtin_amdgcn_s_sleep(2);
@@ -737,9 +752,10 @@ __global__ __launch_bounds__(64) void nw_fill_stripe_kernel(
                 }
                 const uint32_t row = rr + (uint32_t)lane;
                 if (lane < (int)kPub && row <= ld) {
-                    const int2 v = scr_in[row];
-                    blkH = v.x;
-                    blkF = v.y;
+                    const uint64_t v = __hip_atomic_load((const uint64_t *)(scr_in + row),
+                                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    blkH = (int32_t)(uint32_t)v;
+                    blkF = (int32_t)(uint32_t)(v >> 32);
                 }
             }
             const uint32_t sl = (rr - 1) % kPub;
@@ -779,10 +795,16 @@ __global__ __launch_bounds__(64) void nw_fill_stripe_kernel(
             for (int k = 0; k < KD; ++k) mw.w[k] ^= 0x7F7F7F7Fu;
             *reinterpret_cast<MaskWords<K> *>(mseg + (uint64_t)(r - 1) * p.mask_rs) = mw;
             if (lane == G - 1 && scr_out) {
-                scr_out[r] = make_int2(pubH, pubF);
-                if ((uint32_t)r % kPub == 0 || (uint32_t)r == ld)
-                    __hip_atomic_store(prog_out, (uint32_t)r, __ATOMIC_RELEASE,
+                // agent-coherent (write-through) stores: the publication below
+                // needs only these to be complete, not an L2 write-back
+                __hip_atomic_store((uint64_t *)(scr_out + r),
+                                   (uint64_t)(uint32_t)pubH | ((uint64_t)(uint32_t)pubF << 32),
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if ((uint32_t)r % kPub == 0 || (uint32_t)r == ld) {
+                    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): column stores done
+                    __hip_atomic_store(prog_out, (uint32_t)r, __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_AGENT);
+                }
             }
             if (end_lane && r == (int)ld) {
                 int32_t e = 0;

@@ -236,3 +236,18 @@ def test_score_only_plan_matches_full(saln):
     assert ((b[:, 3] >> 16) & 0xFF == 8).all()       # flags: score-only
     full.close()
     fast.close()
+
+
+@pytest.mark.parametrize("L", [3000])
+def test_long_pair_stripes(saln, oracle, L):
+    """A single long mutated pair through the column-stripe fill (12 stripes of
+    256 columns, pipelined): score, end states, status and the first printed
+    alignment equal the oracle's."""
+    from sequencealigning_amd import synth
+    q = synth.random_bases(77, L).tobytes()
+    d = synth.mutate(q, 0.05, seed=78)
+    r = saln.n_w_align(q, d)
+    o = oracle.nw(q, d, literal_dfs=False)
+    assert r.score == o.score and r.end_states == o.end_states and r.panics == o.panics
+    if o.first_ops is not None:
+        assert expand(r.cigar) == o.first_ops

@@ -1,0 +1,60 @@
+"""Single-pair NW timing on the GPU: configs[0] (1 kbp x 1 kbp) and
+configs[3] (100 kbp x 100 kbp), G-mut(5%), through a device-resident plan.
+Reports fill / traceback / execute times and GCUPS (cells / execute time).
+
+    python tools/bench_long.py [--len 100000] [--reps 3] [--score-only]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--len", type=int, default=1000)
+    ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--score-only", action="store_true")
+    a = ap.parse_args()
+    import torch
+    import sequencealigning_amd as saln
+    from sequencealigning_amd import synth
+    L = a.len
+    q = synth.random_bases(0x5EED0000 + (3 if L > 10_000 else 0), L).tobytes()
+    d = synth.mutate(q, 0.05, seed=L)
+    qo = np.array([0, len(q)], np.uint64)
+    do = np.array([0, len(d)], np.uint64)
+    plan = saln.NwPlan(qo, do, pairs=[(0, 0)])
+    plan.set_score_only(a.score_only)
+    dq = torch.frombuffer(bytearray(q), dtype=torch.uint8).cuda()
+    dd = torch.frombuffer(bytearray(d), dtype=torch.uint8).cuda()
+    res = torch.zeros(4, dtype=torch.int32, device="cuda")
+    cig = torch.zeros(max(1, plan.cigar_words), dtype=torch.int32, device="cuda")
+    plan.execute(dq, dd, res, cig)
+    torch.cuda.synchronize()
+    plan.set_timing(True)
+    t0 = time.perf_counter()
+    for _ in range(a.reps):
+        plan.execute(dq, dd, res, cig)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / a.reps
+    f, _ = plan.kernel_time("nw_fill")
+    tb, _ = plan.kernel_time("nw_traceback")
+    r = res.cpu().numpy()
+    print(json.dumps({"len_q": len(q), "len_db": len(d), "cells": plan.cells,
+                      "score": int(r[0]), "status": int(r[1] & 0xFF),
+                      "mask_bytes": plan.mask_bytes, "score_only": a.score_only,
+                      "execute_ms": round(dt * 1e3, 3), "fill_ms": round(f / a.reps, 3),
+                      "traceback_ms": round(tb / a.reps, 3),
+                      "gcups": round(plan.cells / dt / 1e9, 2),
+                      "fill_gcups": round(plan.cells / (f / a.reps / 1e3) / 1e9, 2)}))
+    plan.close()
+
+
+if __name__ == "__main__":
+    main()
