@@ -672,7 +672,7 @@ __global__ __launch_bounds__(256) void nw_fill_kernel(const NwPairDesc *__restri
 constexpr uint32_t kPub = 32;
 constexpr uint32_t kSpinCap = 1u << 24;
 
-template <int K>
+template <int K, bool kCodes>
 __global__ __launch_bounds__(64) void nw_fill_stripe_kernel(
     const NwPairDesc *__restrict__ pairs, const uint2 *__restrict__ work,
     const uint8_t *__restrict__ qs, const uint8_t *__restrict__ ds, uint8_t *__restrict__ mask,
@@ -777,12 +777,15 @@ __global__ __launch_bounds__(64) void nw_fill_stripe_kernel(
                 const int32_t H = max(M, max(I, D));
                 const int32_t Hc = H & ~1;
                 const int32_t tO = M + sO;
-                uint32_t b = (M >= Hc ? kArgM : 0u) | (I >= Hc ? kArgI : 0u) |
-                             (D >= Hc ? kArgD : 0u);
-                b |= ((I | 1) >= tO ? kIExt : 0u) | ((tO | 1) >= I ? kIOpen : 0u);
-                b |= ((D | 1) >= tO ? kDExt : 0u) | ((tO | 1) >= D ? kDOpen : 0u);
-                b |= eq ? 0x80u : 0u;
-                mw.w[k / 4] |= b << (8 * (k % 4));
+                if constexpr (kCodes) {
+                    uint32_t b = (M >= Hc ? kArgM : 0u) | (I >= Hc ? kArgI : 0u) |
+                                 (D >= Hc ? kArgD : 0u);
+                    b |= ((I | 1) >= tO ? kIExt : 0u) | ((tO | 1) >= I ? kIOpen : 0u);
+                    b |= ((D | 1) >= tO ? kDExt : 0u) | ((tO | 1) >= D ? kDOpen : 0u);
+                    b |= eq ? 0x80u : 0u;
+                    mw.w[k / 4] |= b << (8 * (k % 4));
+                }
+                (void)Hc;
                 F = max(tO, I) + sE;
                 Dn[k] = max(tO, D) + sE;
                 hd = Hp[k];
@@ -791,9 +794,11 @@ __global__ __launch_bounds__(64) void nw_fill_stripe_kernel(
             hd = inH;
             pubF = F;
             pubH = Hp[K - 1];
+            if constexpr (kCodes) {
 #pragma unroll
-            for (int k = 0; k < KD; ++k) mw.w[k] ^= 0x7F7F7F7Fu;
-            *reinterpret_cast<MaskWords<K> *>(mseg + (uint64_t)(r - 1) * p.mask_rs) = mw;
+                for (int k = 0; k < KD; ++k) mw.w[k] ^= 0x7F7F7F7Fu;
+                *reinterpret_cast<MaskWords<K> *>(mseg + (uint64_t)(r - 1) * p.mask_rs) = mw;
+            }
             if (lane == G - 1 && scr_out) {
                 // agent-coherent (write-through) stores: the publication below
                 // needs only these to be complete, not an L2 write-back
@@ -1161,10 +1166,14 @@ hipError_t launch_traceback(int variant, const NwPairDesc *pairs, uint32_t first
 hipError_t launch_fill_stripes(const NwPairDesc *pairs, const uint2 *work, uint32_t n_work,
                                const uint8_t *qs, const uint8_t *ds, uint8_t *mask,
                                int2 *scratch, uint32_t *prog, uint32_t *err, int32_t *end_h,
-                               Scoring sc, hipStream_t stream) {
+                               Scoring sc, bool codes, hipStream_t stream) {
     if (!n_work) return hipSuccess;
-    nw_fill_stripe_kernel<4><<<dim3(n_work), dim3(64), 0, stream>>>(pairs, work, qs, ds, mask,
-                                                                     scratch, prog, err, end_h, sc);
+    if (codes)
+        nw_fill_stripe_kernel<4, true><<<dim3(n_work), dim3(64), 0, stream>>>(
+            pairs, work, qs, ds, mask, scratch, prog, err, end_h, sc);
+    else
+        nw_fill_stripe_kernel<4, false><<<dim3(n_work), dim3(64), 0, stream>>>(
+            pairs, work, qs, ds, mask, scratch, prog, err, end_h, sc);
     return hipGetLastError();
 }
 
