@@ -175,6 +175,26 @@ int saln_nw_plan_set_score_only(saln_nw_plan *plan, int enable);
 int saln_nw_plan_sync(saln_nw_plan *plan, void *stream, int keep_latest);
 int saln_nw_plan_destroy(saln_nw_plan *plan);
 
+/* ------------------------------------ NW: score-only all-vs-all (device, C5)
+ * The pair loop `for d in db { for q in query { n_w_align(q, d) } }`
+ * (main.rs:61-67) reduced to what a score-only caller keeps: for every pair
+ * p = d * n_q + q (reference order) out[2p] = score, out[2p+1] = status
+ * (SALN_OK | SALN_REF_PANIC_BOUNDARY).  No per-pair descriptors: short
+ * queries (packed-i16 region) are grouped into length classes and every
+ * class runs as one index space over (query, db record); other queries go
+ * through an internal score-only plan.  q_off/db_off are host offsets; the
+ * sequences and `out` (int32[2 * n_q * n_db]) live on the device. */
+typedef struct saln_nw_avsa saln_nw_avsa;
+int saln_nw_avsa_create(saln_context *ctx, const uint64_t *q_off, uint64_t n_q,
+                        const uint64_t *db_off, uint64_t n_db, int32_t mode,
+                        const saln_nw_scoring *scoring, saln_nw_avsa **out);
+int saln_nw_avsa_execute(saln_nw_avsa *a, const uint8_t *d_q_seq, const uint8_t *d_db_seq,
+                         int32_t *d_out, void *stream);
+/* cells = sum over all pairs of len_q * len_db; fallback_pairs = pairs that
+ * take the plan path. */
+int saln_nw_avsa_info(const saln_nw_avsa *a, uint64_t *cells, uint64_t *fallback_pairs);
+int saln_nw_avsa_destroy(saln_nw_avsa *a);
+
 /* ----------------------------------------------------------------------- WFA
  * Replaces `pub fn wfa_align(seq1: &Record, seq2: &Record, mode: Mode)`
  * (wfa.rs:23-42) with the reference's exact (quirky) semantics: wavefront
@@ -217,6 +237,20 @@ int saln_wfa_align_batch(saln_context *ctx, const uint8_t *q_seq, const uint64_t
 int saln_wfa_render(saln_context *ctx, const uint8_t *q, uint64_t len_q, const uint8_t *d,
                     uint64_t len_db, int32_t mode, uint32_t max_steps, uint32_t max_width,
                     char *out, uint64_t cap, uint64_t *out_len, saln_wfa_result *result);
+
+/* Device-resident WFA batch (configs[2] / C3 measurement): plan once from host
+ * offsets and a pair list (NULL = all-vs-all, reference order), then execute
+ * on device sequences (same CSR layout) into device results[n_pairs].  No
+ * alignment rows.  Pairs that reach a 64-step first pass are re-run with
+ * max_steps; the results equal a single pass at max_steps. */
+typedef struct saln_wfa_plan saln_wfa_plan;
+int saln_wfa_plan_create(saln_context *ctx, const uint64_t *q_off, uint64_t n_q,
+                         const uint64_t *db_off, uint64_t n_db, const uint32_t *pair_q,
+                         const uint32_t *pair_db, uint64_t n_pairs, int32_t mode,
+                         uint32_t max_steps, uint32_t max_width, saln_wfa_plan **out);
+int saln_wfa_execute(saln_wfa_plan *plan, const uint8_t *d_q_seq, const uint8_t *d_db_seq,
+                     saln_wfa_result *d_results, void *stream);
+int saln_wfa_plan_destroy(saln_wfa_plan *plan);
 
 /* --------------------------------------------------------------------- FASTA
  * Replaces `pub fn parse_fasta(path: PathBuf) -> Result<Records>`

@@ -80,6 +80,12 @@ int ref_nw_dag_summary(const uint8_t *q, const uint8_t *d, const ref_nw_mats *m,
 uint64_t ref_nw_run_pairs(const uint8_t *qs, const uint64_t *q_off, const uint8_t *ds,
                           const uint64_t *d_off, uint64_t n_pairs, uint64_t max_pops);
 
+/* Linear-memory score + end states + panic status of one pair with the
+ * reference semantics (reflinear.c), on `threads` column stripes.  For
+ * pairs too large for ref_nw_fill (C4).  Returns 0 on success. */
+int ref_nw_score_linear(const uint8_t *q, size_t lq, const uint8_t *d, size_t ld, int threads,
+                        int32_t *score, uint8_t *end_states, int *panics);
+
 /* FASTA parser restatement (parse.rs:54-99) on an in-memory buffer.
  * has_valid_ext: result of the extension check (:55-60) done by the caller.
  * Records are returned as a flat byte stream: for each record

@@ -53,6 +53,8 @@ def lib():
         L.ref_nw_run_pairs.argtypes = [u8p, C.POINTER(C.c_uint64), u8p, C.POINTER(C.c_uint64),
                                        C.c_uint64, C.c_uint64]
         L.ref_nw_run_pairs.restype = C.c_uint64
+        L.ref_nw_score_linear.argtypes = [u8p, C.c_size_t, u8p, C.c_size_t, C.c_int,
+                                          C.POINTER(C.c_int32), u8p, C.POINTER(C.c_int)]
         L.ref_parse_fasta.argtypes = [u8p, C.c_size_t, C.c_int, u8p, C.c_size_t,
                                       C.POINTER(C.c_size_t), u8p, C.c_size_t,
                                       C.POINTER(C.c_size_t)]
@@ -125,6 +127,18 @@ def nw(query: bytes, db: bytes, *, literal_dfs: bool = True, max_pops: int = 2_0
                         bool(pan.value), first)
     finally:
         L.ref_nw_free(C.byref(m))
+
+
+def nw_score_linear(query: bytes, db: bytes, threads: int = 0) -> tuple[int, int, bool]:
+    """(score, end_states, panics) of one pair in linear memory (reflinear.c),
+    for pairs too large for the full-matrix oracle (configs[3])."""
+    if threads <= 0:
+        threads = min(16, os.cpu_count() or 1)
+    sc, es, pan = C.c_int32(0), C.c_uint8(0), C.c_int(0)
+    if lib().ref_nw_score_linear(_u8(query), len(query), _u8(db), len(db), threads,
+                                 C.byref(sc), C.byref(es), C.byref(pan)) != 0:
+        raise MemoryError("oracle linear fill")
+    return sc.value, es.value, bool(pan.value)
 
 
 def run_pairs(qs: bytes, q_off: np.ndarray, ds: bytes, d_off: np.ndarray, n_pairs: int,

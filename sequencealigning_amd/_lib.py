@@ -73,7 +73,10 @@ EXPORTS = [
     "saln_nw_align", "saln_nw_render", "saln_nw_dense_mask", "saln_nw_align_batch",
     "saln_nw_plan_create", "saln_nw_plan_info", "saln_nw_cigar_offsets", "saln_nw_execute",
     "saln_nw_plan_set_timing", "saln_nw_plan_kernel_time", "saln_nw_plan_set_async",
-    "saln_nw_plan_set_score_only", "saln_nw_plan_sync", "saln_nw_plan_destroy", "saln_wfa_align_batch", "saln_wfa_render",
+    "saln_nw_plan_set_score_only", "saln_nw_plan_sync", "saln_nw_plan_destroy",
+    "saln_nw_avsa_create", "saln_nw_avsa_execute", "saln_nw_avsa_info", "saln_nw_avsa_destroy",
+    "saln_wfa_align_batch", "saln_wfa_render", "saln_wfa_plan_create", "saln_wfa_execute",
+    "saln_wfa_plan_destroy",
     "saln_parse_fasta", "saln_parse_fasta_buffer", "saln_records_count", "saln_records_get",
     "saln_records_free",
 ]
@@ -137,6 +140,16 @@ def lib() -> C.CDLL:
         L.saln_nw_plan_sync.argtypes = [vp, vp, C.c_int]
         L.saln_nw_plan_set_score_only.argtypes = [vp, C.c_int]
         L.saln_nw_plan_destroy.argtypes = [vp]
+        L.saln_nw_avsa_create.argtypes = [vp, vp, C.c_uint64, vp, C.c_uint64, C.c_int32,
+                                          C.POINTER(NwScoring), C.POINTER(vp)]
+        L.saln_nw_avsa_execute.argtypes = [vp, vp, vp, vp, vp]
+        L.saln_nw_avsa_info.argtypes = [vp, u64p, u64p]
+        L.saln_nw_avsa_destroy.argtypes = [vp]
+        L.saln_wfa_plan_create.argtypes = [vp, vp, C.c_uint64, vp, C.c_uint64, vp, vp,
+                                           C.c_uint64, C.c_int32, C.c_uint32, C.c_uint32,
+                                           C.POINTER(vp)]
+        L.saln_wfa_execute.argtypes = [vp, vp, vp, vp, vp]
+        L.saln_wfa_plan_destroy.argtypes = [vp]
         L.saln_wfa_align_batch.argtypes = [vp, vp, vp, C.c_uint64, vp, vp, C.c_uint64, vp, vp,
                                            C.c_uint64, C.c_int32, C.c_uint32, C.c_uint32, vp,
                                            vp, vp, C.c_uint32]

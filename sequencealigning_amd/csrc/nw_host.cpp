@@ -29,15 +29,6 @@ Scoring scoring_or_default(const saln_nw_scoring *s) {
     return Scoring{s->match, s->mismatch, s->gap_open, s->gap_extend};
 }
 
-#define HIP_TRY(expr)                                                                      \
-    do {                                                                                   \
-        hipError_t e_ = (expr);                                                            \
-        if (e_ != hipSuccess) {                                                            \
-            set_error(std::string(#expr) + ": " + hipGetErrorString(e_));                  \
-            return SALN_E_HIP;                                                             \
-        }                                                                                  \
-    } while (0)
-
 }  // namespace saln
 
 using namespace saln;

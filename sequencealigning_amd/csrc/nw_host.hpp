@@ -36,12 +36,34 @@ hipError_t launch_traceback(int variant, const NwPairDesc *pairs, uint32_t first
                             const uint8_t *ds, const uint8_t *mask, const int32_t *end_h,
                             uint32_t *ops, saln_nw_result *results, uint32_t *cigar, Scoring sc,
                             hipStream_t stream);
+// score-only all-vs-all (nw_avsa.cpp)
+hipError_t launch_avsa(int variant, const uint64_t *q_off, const uint64_t *d_off,
+                       const uint32_t *q_ids, uint32_t nq, const uint32_t *d_ids,
+                       uint32_t nq_total, uint64_t base, uint32_t count, const uint8_t *qs,
+                       const uint8_t *ds, int2 *out, Scoring sc, uint32_t ld_max,
+                       hipStream_t stream);
+hipError_t launch_avsa_boundary(const uint64_t *q_off, const uint64_t *d_off,
+                                const uint32_t *q_ids, uint32_t nq, const uint32_t *d_ids,
+                                uint64_t n, uint32_t nq_total, int2 *out, Scoring sc,
+                                hipStream_t stream);
+hipError_t launch_avsa_scatter(const saln_nw_result *res, const uint32_t *q_ids, uint32_t nq,
+                               const uint32_t *d_ids, uint64_t n, uint32_t nq_total, int2 *out,
+                               hipStream_t stream);
 Geom variant_geom(int v);
 bool variant_packed(int v);
 int choose_variant(uint32_t len_q, uint32_t len_db, const Scoring &sc);
 
 void set_error(const std::string &msg);
 Scoring scoring_or_default(const saln_nw_scoring *s);
+
+#define HIP_TRY(expr)                                                                      \
+    do {                                                                                   \
+        hipError_t e_ = (expr);                                                            \
+        if (e_ != hipSuccess) {                                                            \
+            ::saln::set_error(std::string(#expr) + ": " + hipGetErrorString(e_));          \
+            return SALN_E_HIP;                                                             \
+        }                                                                                  \
+    } while (0)
 
 // Host copy of one pair's parent codes: LB-byte segments, row-major, with
 // row stride rs and block stride bs (nw_common.hpp Geom).

@@ -888,15 +888,53 @@ struct PkMask {
 // bits the device walker reads; the extend bits (3, 5) are left 0.  Full
 // codes (every parent set) are kept for the dense-mask / render paths.
 enum { kCodesWalk = 0, kCodesFull = 1, kCodesNone = 2 };
-template <int G, int K, int kCodes>
-__global__ __launch_bounds__(256) void nw_fill_pk_kernel(const NwPairDesc *__restrict__ pairs,
-                                                         uint32_t first, uint32_t count,
+
+// Where the packed fill gets its pairs and puts the end values.
+// PlanSrc: the plan's sorted descriptor table; the scaled end value goes to
+// end_h for the traceback / score-results kernels.
+struct PlanSrc {
+    const NwPairDesc *pairs;
+    uint32_t first;
+    int32_t *end_h;
+    __device__ __forceinline__ NwPairDesc pair(uint32_t i) const { return pairs[first + i]; }
+    __device__ __forceinline__ void end(uint32_t i, const NwPairDesc &, int32_t h) const {
+        end_h[first + i] = h;
+    }
+};
+
+// AvsaSrc: score-only all-vs-all (configs[4]) without descriptors.  Pair
+// k = base + i of a query class is (class query k % nq, db record k / nq) -
+// both pairs of a lane group usually share the db record; the result
+// {score, status} goes straight to out[d * nq_total + q], the reference's
+// db-outer / query-inner order (main.rs:61-62).
+struct AvsaSrc {
+    const uint64_t *q_off, *d_off;  // full CSR offsets (n+1)
+    const uint32_t *q_ids, *d_ids;  // the class's queries, the non-empty db records
+    uint32_t nq;                    // queries in the class
+    uint32_t nq_total;
+    uint64_t base;
+    int2 *out;
+    __device__ __forceinline__ NwPairDesc pair(uint32_t i) const {
+        const uint64_t k = base + i;
+        const uint32_t qi = q_ids[k % nq], di = d_ids[k / nq];
+        NwPairDesc p{};
+        p.q_off = q_off[qi];
+        p.db_off = d_off[di];
+        p.len_q = (uint32_t)(q_off[qi + 1] - p.q_off);
+        p.len_db = (uint32_t)(d_off[di + 1] - p.db_off);
+        p.mask_off = (uint64_t)di * nq_total + qi;  // result slot (no mask in this mode)
+        return p;
+    }
+    __device__ __forceinline__ void end(uint32_t, const NwPairDesc &p, int32_t h) const {
+        out[p.mask_off] = make_int2(h >> 1, (h & 1) ? SALN_REF_PANIC_BOUNDARY : SALN_OK);
+    }
+};
+
+template <int G, int K, int kCodes, typename Src>
+__global__ __launch_bounds__(256) void nw_fill_pk_kernel(Src src, uint32_t count,
                                                          const uint8_t *__restrict__ qs,
                                                          const uint8_t *__restrict__ ds,
-                                                         uint8_t *__restrict__ mask,
-                                                         int32_t *__restrict__ end_h,
-                                                         saln_nw_result *__restrict__ results,
-                                                         uint32_t *__restrict__ cigar, Scoring sc,
+                                                         uint8_t *__restrict__ mask, Scoring sc,
                                                          uint32_t ld_max) {
     constexpr int GPB = 256 / G;
     constexpr Geom geo{G, K};
@@ -906,9 +944,9 @@ __global__ __launch_bounds__(256) void nw_fill_pk_kernel(const NwPairDesc *__res
     const uint32_t ia = 2 * gi, ib = 2 * gi + 1;
     if (ia >= count) return;  // whole group
     const bool hasB = ib < count;
-    const NwPairDesc pa = pairs[first + ia];
+    const NwPairDesc pa = src.pair(ia);
     NwPairDesc pb = pa;
-    if (hasB) pb = pairs[first + ib];
+    if (hasB) pb = src.pair(ib);
     const int ldA = (int)pa.len_db, ldB = hasB ? (int)pb.len_db : 0;
     const int lqA = (int)pa.len_q, lqB = hasB ? (int)pb.len_q : 0;
     const uint8_t *__restrict__ qA = qs + pa.q_off;
@@ -956,7 +994,6 @@ __global__ __launch_bounds__(256) void nw_fill_pk_kernel(const NwPairDesc *__res
     // end-cell owners
     const int lA = (lqA - 1) / K, kA = (lqA - 1) % K;
     const int lB = hasB ? (lqB - 1) / K : -1, kB = hasB ? (lqB - 1) % K : 0;
-    int32_t endA = 0, endB = 0;
     // this lane's segments of row 1 (block = lane)
     uint8_t *__restrict__ mA = mask + pa.mask_off + (uint64_t)lane * pa.mask_bs;
     uint8_t *__restrict__ mB = mask + pb.mask_off + (uint64_t)lane * pb.mask_bs;
@@ -1026,21 +1063,17 @@ __global__ __launch_bounds__(256) void nw_fill_pk_kernel(const NwPairDesc *__res
 #pragma unroll
                 for (int k = 0; k < K; ++k)
                     if (k == kA) e = (int16_t)(Hp[k] & 0xFFFFu);
-                endA = e - alpha * ldA - beta * lqA;
-                end_h[first + ia] = endA;
+                src.end(ia, pa, e - alpha * ldA - beta * lqA);
             }
             if (r == ldB && lane == lB) {
                 int32_t e = 0;
 #pragma unroll
                 for (int k = 0; k < K; ++k)
                     if (k == kB) e = (int16_t)(Hp[k] >> 16);
-                endB = e - alpha * ldB - beta * lqB;
-                end_h[first + ib] = endB;
+                src.end(ib, pb, e - alpha * ldB - beta * lqB);
             }
         }
     }
-    (void)results;
-    (void)cigar;
 }
 
 // Score-only results (saln_nw_plan_set_score_only): score and panic status
@@ -1092,18 +1125,95 @@ static void fill_i32(dim3 grid, hipStream_t s, const NwPairDesc *pairs, uint32_t
 template <int G, int K>
 static void fill_pk(dim3 grid, hipStream_t s, const NwPairDesc *pairs, uint32_t first,
                     uint32_t count, const uint8_t *qs, const uint8_t *ds, uint8_t *mask,
-                    int32_t *end_h, saln_nw_result *res, uint32_t *cig, Scoring sc, int codes,
+                    int32_t *end_h, saln_nw_result *, uint32_t *, Scoring sc, int codes,
                     uint32_t ld_max) {
     const size_t lds = (size_t)(256 / G) * ld_max * sizeof(uint32_t);
+    const PlanSrc src{pairs, first, end_h};
     if (codes == kCodesFull)
-        nw_fill_pk_kernel<G, K, kCodesFull><<<grid, dim3(256), lds, s>>>(
-            pairs, first, count, qs, ds, mask, end_h, res, cig, sc, ld_max);
+        nw_fill_pk_kernel<G, K, kCodesFull><<<grid, dim3(256), lds, s>>>(src, count, qs, ds, mask,
+                                                                           sc, ld_max);
     else if (codes == kCodesNone)
-        nw_fill_pk_kernel<G, K, kCodesNone><<<grid, dim3(256), lds, s>>>(
-            pairs, first, count, qs, ds, mask, end_h, res, cig, sc, ld_max);
+        nw_fill_pk_kernel<G, K, kCodesNone><<<grid, dim3(256), lds, s>>>(src, count, qs, ds, mask,
+                                                                           sc, ld_max);
     else
-        nw_fill_pk_kernel<G, K, kCodesWalk><<<grid, dim3(256), lds, s>>>(
-            pairs, first, count, qs, ds, mask, end_h, res, cig, sc, ld_max);
+        nw_fill_pk_kernel<G, K, kCodesWalk><<<grid, dim3(256), lds, s>>>(src, count, qs, ds, mask,
+                                                                           sc, ld_max);
+}
+
+template <int G, int K>
+static void avsa_pk(const AvsaSrc &src, uint32_t count, const uint8_t *qs, const uint8_t *ds,
+                    Scoring sc, uint32_t ld_max, hipStream_t s) {
+    constexpr uint32_t gpb = 256 / G;
+    const uint32_t sup = 8 * blocks_per_pack(2 * gpb);
+    const uint32_t groups = (count + 1) / 2;
+    const dim3 grid(((groups + gpb - 1) / gpb + sup - 1) / sup * sup);
+    const size_t lds = (size_t)gpb * ld_max * sizeof(uint32_t);
+    nw_fill_pk_kernel<G, K, kCodesNone><<<grid, dim3(256), lds, s>>>(src, count, qs, ds, nullptr,
+                                                                       sc, ld_max);
+}
+
+// Score-only all-vs-all over one packed query class (variant 4-7): pairs
+// [base, base + count) of the class's (query, db) index space.
+hipError_t launch_avsa(int variant, const uint64_t *q_off, const uint64_t *d_off,
+                       const uint32_t *q_ids, uint32_t nq, const uint32_t *d_ids,
+                       uint32_t nq_total, uint64_t base, uint32_t count, const uint8_t *qs,
+                       const uint8_t *ds, int2 *out, Scoring sc, uint32_t ld_max,
+                       hipStream_t stream) {
+    if (!count) return hipSuccess;
+    const AvsaSrc src{q_off, d_off, q_ids, d_ids, nq, nq_total, base, out};
+    switch (variant) {
+        case 4: avsa_pk<8, 19>(src, count, qs, ds, sc, ld_max, stream); break;
+        case 5: avsa_pk<16, 16>(src, count, qs, ds, sc, ld_max, stream); break;
+        case 6: avsa_pk<32, 16>(src, count, qs, ds, sc, ld_max, stream); break;
+        case 7: avsa_pk<16, 10>(src, count, qs, ds, sc, ld_max, stream); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+// Pairs with an empty side (no fill): out[d * nq_total + q] from the
+// boundary formulas.  Index space: (q_ids[i % nq], d_ids[i / nq]).
+__global__ __launch_bounds__(256) void nw_avsa_boundary_kernel(
+    const uint64_t *__restrict__ q_off, const uint64_t *__restrict__ d_off,
+    const uint32_t *__restrict__ q_ids, uint32_t nq, const uint32_t *__restrict__ d_ids,
+    uint64_t n, uint32_t nq_total, int2 *__restrict__ out, Scoring sc) {
+    const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n) return;
+    const uint32_t qi = q_ids ? q_ids[k % nq] : (uint32_t)(k % nq);
+    const uint32_t di = d_ids ? d_ids[k / nq] : (uint32_t)(k / nq);
+    const int32_t h = hs_boundary_end(sc, (uint32_t)(q_off[qi + 1] - q_off[qi]),
+                                      (uint32_t)(d_off[di + 1] - d_off[di]));
+    out[(uint64_t)di * nq_total + qi] = make_int2(h >> 1, (h & 1) ? SALN_REF_PANIC_BOUNDARY : SALN_OK);
+}
+
+hipError_t launch_avsa_boundary(const uint64_t *q_off, const uint64_t *d_off,
+                                const uint32_t *q_ids, uint32_t nq, const uint32_t *d_ids,
+                                uint64_t n, uint32_t nq_total, int2 *out, Scoring sc,
+                                hipStream_t stream) {
+    if (!n) return hipSuccess;
+    nw_avsa_boundary_kernel<<<dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, stream>>>(
+        q_off, d_off, q_ids, nq, d_ids, n, nq_total, out, sc);
+    return hipGetLastError();
+}
+
+// Fallback queries run through an ordinary score-only plan whose pair k is
+// (q_ids[k % nq], d_ids[k / nq]); scatter its 16-byte results into out.
+__global__ __launch_bounds__(256) void nw_avsa_scatter_kernel(
+    const saln_nw_result *__restrict__ res, const uint32_t *__restrict__ q_ids, uint32_t nq,
+    const uint32_t *__restrict__ d_ids, uint64_t n, uint32_t nq_total, int2 *__restrict__ out) {
+    const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n) return;
+    const saln_nw_result r = res[k];
+    out[(uint64_t)d_ids[k / nq] * nq_total + q_ids[k % nq]] = make_int2(r.score, r.status);
+}
+
+hipError_t launch_avsa_scatter(const saln_nw_result *res, const uint32_t *q_ids, uint32_t nq,
+                               const uint32_t *d_ids, uint64_t n, uint32_t nq_total, int2 *out,
+                               hipStream_t stream) {
+    if (!n) return hipSuccess;
+    nw_avsa_scatter_kernel<<<dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, stream>>>(
+        res, q_ids, nq, d_ids, n, nq_total, out);
+    return hipGetLastError();
 }
 
 hipError_t launch_fill(int variant, const NwPairDesc *pairs, uint32_t first, uint32_t count,

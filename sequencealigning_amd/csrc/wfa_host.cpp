@@ -10,6 +10,7 @@
 #include <climits>
 #include <cstdio>
 #include <cstring>
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -39,6 +40,11 @@ struct DevBuf {
 
 constexpr uint32_t kDefaultSteps = 64, kDefaultWidth = 64;
 constexpr uint64_t kArenaBudget = 8ull << 30;  // bytes of tensor history per launch
+// Batch runs start every pair with this step cap (a small arena, many lanes
+// per launch); the pairs that reach it are re-run with the caller's cap.
+// Essentially every realistic pair ends far earlier (REF_PANIC_TRIM at s = 20,
+// SURVEY.md §8.5), so the big arena is only paid for the few that need it.
+constexpr uint32_t kFirstPassSteps = 64;
 
 uint32_t ev_cap_for(uint32_t max_steps) { return 7 * (max_steps / 4 + 2) + 8; }
 
@@ -47,6 +53,116 @@ struct Logs {
     std::vector<uint8_t> ev;    // ev_cap per pair
     uint32_t ev_cap = 0;
 };
+
+// Device scratch reused across launches / executes.
+struct WfaScratch {
+    DevBuf hdr, off, meta, tsome;
+    uint64_t S = 0, W = 0, nl = 0;
+    DevBuf rerun, cnt;
+    uint64_t rerun_n = 0;
+
+    hipError_t arena(uint64_t S_, uint64_t W_, uint64_t n_pairs, WfaArena *out) {
+        const uint64_t per_lane = S_ * 3 * 4 * 4 + S_ * 3 * W_ * 8 + S_;
+        uint64_t nl_ = std::max<uint64_t>(256, std::min<uint64_t>(n_pairs, kArenaBudget / per_lane));
+        nl_ = std::min<uint64_t>(nl_, n_pairs);
+        if (S_ * nl_ > S * nl || S_ * W_ * nl_ > S * W * nl) {
+            for (DevBuf *b : {&hdr, &off, &meta, &tsome}) {
+                if (b->p) (void)hipFree(b->p);
+                b->p = nullptr;
+            }
+            hipError_t e;
+            if ((e = hdr.alloc(S_ * 3 * 4 * nl_ * sizeof(int32_t))) != hipSuccess) return e;
+            if ((e = off.alloc(S_ * 3 * W_ * nl_ * sizeof(int32_t))) != hipSuccess) return e;
+            if ((e = meta.alloc(S_ * 3 * W_ * nl_ * sizeof(uint32_t))) != hipSuccess) return e;
+            if ((e = tsome.alloc(S_ * nl_)) != hipSuccess) return e;
+            S = S_;
+            W = W_;
+            nl = nl_;
+        }
+        // the kernel indexes with the launch's own (S, W, nl) inside the buffers
+        *out = WfaArena{(int32_t *)hdr.p, (int32_t *)off.p, (uint32_t *)meta.p,
+                        (uint8_t *)tsome.p, (uint32_t)nl_, (uint32_t)S_, (uint32_t)W_};
+        return hipSuccess;
+    }
+};
+
+// One pass over n pairs with step cap `steps`, chunked by the arena budget.
+int wfa_pass(WfaScratch &ws, const WfaPairDesc *d_pairs, uint32_t n, const uint8_t *dq,
+             const uint8_t *dd, uint32_t steps, uint32_t width, saln_wfa_result *d_res,
+             uint8_t *d_aln, int32_t *d_lohi, uint8_t *d_ev, uint32_t ev_cap, WfaPairDesc *rerun,
+             uint32_t *rerun_cnt, hipStream_t s) {
+    WfaArena arena;
+    TRY_HIP(ws.arena(steps / 2 + 1, width, n, &arena));
+    for (uint64_t first = 0; first < n; first += arena.nl) {
+        const uint32_t cnt = (uint32_t)std::min<uint64_t>(arena.nl, n - first);
+        TRY_HIP(launch_wfa(d_pairs, (uint32_t)first, cnt, dq, dd, arena, steps, d_res, d_aln,
+                           d_lohi, d_ev, ev_cap, rerun, rerun_cnt, s));
+    }
+    return SALN_OK;
+}
+
+// All pairs of d_pairs[0, n): with per-step logs (render) one pass at the
+// caller's cap; otherwise a short first pass and a full-cap pass over the
+// pairs that reached the short cap.  Results are identical either way: a
+// pair's run does not depend on the cap until it reaches it.
+int wfa_device(WfaScratch &ws, const WfaPairDesc *d_pairs, uint32_t n, const uint8_t *dq,
+               const uint8_t *dd, uint32_t max_steps, uint32_t width, saln_wfa_result *d_res,
+               uint8_t *d_aln, int32_t *d_lohi, uint8_t *d_ev, uint32_t ev_cap, hipStream_t s) {
+    if (!n) return SALN_OK;
+    if (d_lohi || max_steps <= kFirstPassSteps)
+        return wfa_pass(ws, d_pairs, n, dq, dd, max_steps, width, d_res, d_aln, d_lohi, d_ev,
+                        ev_cap, nullptr, nullptr, s);
+    if (ws.rerun_n < n) {
+        if (ws.rerun.p) (void)hipFree(ws.rerun.p);
+        ws.rerun.p = nullptr;
+        TRY_HIP(ws.rerun.alloc((uint64_t)n * sizeof(WfaPairDesc)));
+        ws.rerun_n = n;
+    }
+    if (!ws.cnt.p) TRY_HIP(ws.cnt.alloc(sizeof(uint32_t)));
+    TRY_HIP(hipMemsetAsync(ws.cnt.p, 0, sizeof(uint32_t), s));
+    int rc = wfa_pass(ws, d_pairs, n, dq, dd, kFirstPassSteps, width, d_res, d_aln, nullptr,
+                      nullptr, 0, (WfaPairDesc *)ws.rerun.p, (uint32_t *)ws.cnt.p, s);
+    if (rc != SALN_OK) return rc;
+    uint32_t again = 0;
+    TRY_HIP(hipMemcpyAsync(&again, ws.cnt.p, sizeof again, hipMemcpyDeviceToHost, s));
+    TRY_HIP(hipStreamSynchronize(s));
+    if (!again) return SALN_OK;
+    return wfa_pass(ws, (const WfaPairDesc *)ws.rerun.p, again, dq, dd, max_steps, width, d_res,
+                    d_aln, nullptr, nullptr, 0, nullptr, nullptr, s);
+}
+
+int build_descs(const uint64_t *q_off, uint64_t n_q, const uint64_t *db_off, uint64_t n_db,
+                const uint32_t *pair_q, const uint32_t *pair_db, uint64_t n_pairs, int32_t mode,
+                const uint64_t *aln_off, uint32_t aln_cap, std::vector<WfaPairDesc> *out,
+                uint64_t *aln_bytes) {
+    out->resize(n_pairs);
+    *aln_bytes = 0;
+    for (uint64_t k = 0; k < n_pairs; ++k) {
+        const uint64_t qi = pair_q ? pair_q[k] : k % n_q;
+        const uint64_t di = pair_db ? pair_db[k] : k / n_q;
+        if (qi >= n_q || di >= n_db) {
+            set_error("pair index out of range");
+            return SALN_E_INVALID;
+        }
+        WfaPairDesc &d = (*out)[k];
+        std::memset(&d, 0, sizeof d);
+        d.q_off = q_off[qi];
+        d.db_off = db_off[di];
+        const uint64_t lq = q_off[qi + 1] - q_off[qi], ld = db_off[di + 1] - db_off[di];
+        if (lq > 0x7FFFFFFFull || ld > 0x7FFFFFFFull) {
+            set_error("sequence too long");
+            return SALN_E_INVALID;
+        }
+        d.len_q = (uint32_t)lq;
+        d.len_db = (uint32_t)ld;
+        d.pair_id = (uint32_t)k;
+        d.mode = mode;
+        d.aln_cap = aln_cap;
+        d.aln_off = aln_cap && aln_off ? aln_off[k] : 0;
+        if (aln_cap) *aln_bytes = std::max<uint64_t>(*aln_bytes, d.aln_off + 2ull * aln_cap);
+    }
+    return SALN_OK;
+}
 
 // Runs the pairs; logs (optional) receive the per-step lo/hi and the rec_tr
 // events of every pair (used for rendering).
@@ -61,34 +177,13 @@ int run_wfa(saln_context *ctx, const uint8_t *q_seq, const uint64_t *q_off, uint
     if (n_pairs == 0) return SALN_OK;
     if (n_pairs > 0xFFFFFFFFull) return SALN_E_INVALID;
     TRY_HIP(hipSetDevice(ctx->device));
-    std::vector<WfaPairDesc> descs(n_pairs);
+    std::vector<WfaPairDesc> descs;
     uint64_t aln_bytes = 0;
-    for (uint64_t k = 0; k < n_pairs; ++k) {
-        const uint64_t qi = pair_q ? pair_q[k] : k % n_q;
-        const uint64_t di = pair_db ? pair_db[k] : k / n_q;
-        if (qi >= n_q || di >= n_db) {
-            set_error("pair index out of range");
-            return SALN_E_INVALID;
-        }
-        WfaPairDesc &d = descs[k];
-        std::memset(&d, 0, sizeof d);
-        d.q_off = q_off[qi];
-        d.db_off = db_off[di];
-        const uint64_t lq = q_off[qi + 1] - q_off[qi], ld = db_off[di + 1] - db_off[di];
-        if (lq > 0x7FFFFFFFull || ld > 0x7FFFFFFFull) {
-            set_error("sequence too long");
-            return SALN_E_INVALID;
-        }
-        d.len_q = (uint32_t)lq;
-        d.len_db = (uint32_t)ld;
-        d.pair_id = (uint32_t)k;
-        d.mode = mode;
-        d.aln_cap = aln ? aln_cap : 0;
-        d.aln_off = aln && aln_off ? aln_off[k] : 0;
-        if (aln) aln_bytes = std::max<uint64_t>(aln_bytes, d.aln_off + 2ull * aln_cap);
-    }
+    int rc = build_descs(q_off, n_q, db_off, n_db, pair_q, pair_db, n_pairs, mode, aln_off,
+                         aln ? aln_cap : 0, &descs, &aln_bytes);
+    if (rc != SALN_OK) return rc;
     const uint64_t qbytes = q_off[n_q], dbytes = db_off[n_db];
-    DevBuf dq, dd, dp, dr, da, dl, de, ah, ao, am, at;
+    DevBuf dq, dd, dp, dr, da, dl, de;
     TRY_HIP(dq.alloc(qbytes));
     TRY_HIP(dd.alloc(dbytes));
     TRY_HIP(dp.alloc(n_pairs * sizeof(WfaPairDesc)));
@@ -102,24 +197,11 @@ int run_wfa(saln_context *ctx, const uint8_t *q_seq, const uint64_t *q_off, uint
         TRY_HIP(dl.alloc(n_pairs * 2ull * max_steps * sizeof(int32_t)));
         TRY_HIP(de.alloc(n_pairs * (uint64_t)ev_cap));
     }
-    // arena chunking
-    const uint64_t S = max_steps / 2 + 1, W = max_width;
-    const uint64_t per_lane = S * 3 * 4 * 4 + S * 3 * W * 8 + S;
-    uint64_t nl = std::max<uint64_t>(256, std::min<uint64_t>(n_pairs, kArenaBudget / per_lane));
-    nl = std::min<uint64_t>(nl, n_pairs);
-    TRY_HIP(ah.alloc(S * 3 * 4 * nl * sizeof(int32_t)));
-    TRY_HIP(ao.alloc(S * 3 * W * nl * sizeof(int32_t)));
-    TRY_HIP(am.alloc(S * 3 * W * nl * sizeof(uint32_t)));
-    TRY_HIP(at.alloc(S * nl));
-    WfaArena arena{(int32_t *)ah.p, (int32_t *)ao.p, (uint32_t *)am.p, (uint8_t *)at.p,
-                   (uint32_t)nl, (uint32_t)S, (uint32_t)W};
-    for (uint64_t first = 0; first < n_pairs; first += nl) {
-        const uint32_t cnt = (uint32_t)std::min<uint64_t>(nl, n_pairs - first);
-        TRY_HIP(launch_wfa((const WfaPairDesc *)dp.p, (uint32_t)first, cnt,
-                           (const uint8_t *)dq.p, (const uint8_t *)dd.p, arena, max_steps,
-                           (saln_wfa_result *)dr.p, (uint8_t *)da.p, (int32_t *)dl.p,
-                           (uint8_t *)de.p, ev_cap, ctx->stream));
-    }
+    WfaScratch ws;
+    rc = wfa_device(ws, (const WfaPairDesc *)dp.p, (uint32_t)n_pairs, (const uint8_t *)dq.p,
+                    (const uint8_t *)dd.p, max_steps, max_width, (saln_wfa_result *)dr.p,
+                    (uint8_t *)da.p, (int32_t *)dl.p, (uint8_t *)de.p, ev_cap, ctx->stream);
+    if (rc != SALN_OK) return rc;
     TRY_HIP(hipStreamSynchronize(ctx->stream));
     TRY_HIP(hipMemcpy(results, dr.p, n_pairs * sizeof(saln_wfa_result), hipMemcpyDeviceToHost));
     if (aln) TRY_HIP(hipMemcpy(aln, da.p, aln_bytes, hipMemcpyDeviceToHost));
@@ -143,6 +225,13 @@ void appendf(std::string *s, const char *fmt, long long v) {
 }
 
 }  // namespace
+
+struct saln_wfa_plan {
+    saln_context *ctx = nullptr;
+    uint32_t n_pairs = 0, max_steps = 0, max_width = 0;
+    DevBuf pairs;
+    WfaScratch ws;
+};
 
 extern "C" {
 
@@ -265,6 +354,49 @@ int saln_wfa_render(saln_context *ctx, const uint8_t *q, uint64_t len_q, const u
         std::memcpy(out, t.data(), std::min<uint64_t>(t.size(), cap));
         if (t.size() > cap) return SALN_E_CAPACITY;
     }
+    return SALN_OK;
+}
+
+int saln_wfa_plan_create(saln_context *ctx, const uint64_t *q_off, uint64_t n_q,
+                         const uint64_t *db_off, uint64_t n_db, const uint32_t *pair_q,
+                         const uint32_t *pair_db, uint64_t n_pairs, int32_t mode,
+                         uint32_t max_steps, uint32_t max_width, saln_wfa_plan **out) {
+    if (!ctx || !q_off || !db_off || !out) return SALN_E_INVALID;
+    *out = nullptr;
+    if (n_pairs > 0xFFFFFFFFull) return SALN_E_INVALID;
+    TRY_HIP(hipSetDevice(ctx->device));
+    auto p = std::make_unique<saln_wfa_plan>();
+    p->ctx = ctx;
+    p->n_pairs = (uint32_t)n_pairs;
+    p->max_steps = max_steps ? max_steps : kDefaultSteps;
+    p->max_width = max_width ? max_width : kDefaultWidth;
+    std::vector<WfaPairDesc> descs;
+    uint64_t ab = 0;
+    int rc = build_descs(q_off, n_q, db_off, n_db, pair_q, pair_db, n_pairs, mode, nullptr, 0,
+                         &descs, &ab);
+    if (rc != SALN_OK) return rc;
+    if (n_pairs) {
+        TRY_HIP(p->pairs.alloc(n_pairs * sizeof(WfaPairDesc)));
+        TRY_HIP(hipMemcpy(p->pairs.p, descs.data(), n_pairs * sizeof(WfaPairDesc),
+                          hipMemcpyHostToDevice));
+    }
+    *out = p.release();
+    return SALN_OK;
+}
+
+int saln_wfa_execute(saln_wfa_plan *p, const uint8_t *d_q_seq, const uint8_t *d_db_seq,
+                     saln_wfa_result *d_results, void *stream) {
+    if (!p || (p->n_pairs && (!d_q_seq || !d_db_seq || !d_results))) return SALN_E_INVALID;
+    TRY_HIP(hipSetDevice(p->ctx->device));
+    hipStream_t s = stream ? (hipStream_t)stream : p->ctx->stream;
+    return wfa_device(p->ws, (const WfaPairDesc *)p->pairs.p, p->n_pairs, d_q_seq, d_db_seq,
+                      p->max_steps, p->max_width, d_results, nullptr, nullptr, nullptr, 0, s);
+}
+
+int saln_wfa_plan_destroy(saln_wfa_plan *p) {
+    if (!p) return SALN_OK;
+    (void)hipSetDevice(p->ctx->device);
+    delete p;
     return SALN_OK;
 }
 

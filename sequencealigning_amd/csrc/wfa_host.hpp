@@ -31,6 +31,7 @@ struct WfaArena {
 hipError_t launch_wfa(const WfaPairDesc *pairs, uint32_t first, uint32_t n, const uint8_t *qs,
                       const uint8_t *ds, const WfaArena &arena, uint32_t max_steps,
                       saln_wfa_result *results, uint8_t *aln, int32_t *lohi_log, uint8_t *ev_log,
-                      uint32_t ev_cap, hipStream_t stream);
+                      uint32_t ev_cap, WfaPairDesc *rerun, uint32_t *rerun_cnt,
+                      hipStream_t stream);
 
 }  // namespace saln

@@ -390,7 +390,8 @@ __global__ __launch_bounds__(256) void wfa_kernel(const WfaPairDesc *__restrict_
                                                   const uint8_t *__restrict__ ds, WfaArena arena,
                                                   uint32_t max_steps, saln_wfa_result *results,
                                                   uint8_t *aln, int32_t *lohi_log, uint8_t *ev_log,
-                                                  uint32_t ev_cap) {
+                                                  uint32_t ev_cap, WfaPairDesc *rerun,
+                                                  uint32_t *rerun_cnt) {
     const uint32_t l = blockIdx.x * blockDim.x + threadIdx.x;
     if (l >= n) return;
     const WfaPairDesc p = pairs[first + l];
@@ -422,6 +423,10 @@ __global__ __launch_bounds__(256) void wfa_kernel(const WfaPairDesc *__restrict_
         const bool newest_even = !((len - 1) & 1);
         if (newest_even && converged(L, (uint32_t)((len - 1) / 2), l1, l2, conv)) break;
         if (steps >= max_steps) {
+            if (rerun) {  // short first pass: hand the pair to the full-cap pass
+                rerun[atomicAdd(rerun_cnt, 1u)] = p;
+                return;
+            }
             status = SALN_NONCONVERGED;
             break;
         }
@@ -562,10 +567,12 @@ __global__ __launch_bounds__(256) void wfa_kernel(const WfaPairDesc *__restrict_
 hipError_t launch_wfa(const WfaPairDesc *pairs, uint32_t first, uint32_t n, const uint8_t *qs,
                       const uint8_t *ds, const WfaArena &arena, uint32_t max_steps,
                       saln_wfa_result *results, uint8_t *aln, int32_t *lohi_log, uint8_t *ev_log,
-                      uint32_t ev_cap, hipStream_t stream) {
+                      uint32_t ev_cap, WfaPairDesc *rerun, uint32_t *rerun_cnt,
+                      hipStream_t stream) {
     if (!n) return hipSuccess;
     wfa_kernel<<<dim3((n + 255) / 256), dim3(256), 0, stream>>>(
-        pairs, first, n, qs, ds, arena, max_steps, results, aln, lohi_log, ev_log, ev_cap);
+        pairs, first, n, qs, ds, arena, max_steps, results, aln, lohi_log, ev_log, ev_cap, rerun,
+        rerun_cnt);
     return hipGetLastError();
 }
 

@@ -35,22 +35,26 @@ def iid_pairs(n_pairs: int, len_q: int, len_db: int, seed: int):
 def mutate(seq: bytes | np.ndarray, delta: float, seed: int) -> bytes:
     s = np.frombuffer(bytes(seq), np.uint8)
     n = len(s)
+    if n == 0:
+        return b""
     r = splitmix64(seed, 3 * n)
     u = (r[:n] >> np.uint64(11)).astype(np.float64) / float(1 << 53)
     ev = (r[n:2 * n] >> np.uint64(62)).astype(np.int64)      # 0,1 sub; 2 ins; 3 del
     rb = (r[2 * n:] >> np.uint64(60)).astype(np.int64)
-    code = np.searchsorted(BASES, s) if n else s.astype(np.int64)
-    out = []
-    for k in range(n):
-        if u[k] >= delta:
-            out.append(int(s[k]))
-        elif ev[k] <= 1:                        # substitution to a different base
-            out.append(int(BASES[(code[k] + 1 + (rb[k] % 3)) % 4]))
-        elif ev[k] == 2:                        # insertion after the base
-            out.append(int(s[k]))
-            out.append(int(BASES[rb[k] & 3]))
-        # deletion: drop
-    return bytes(out)
+    code = np.searchsorted(BASES, s)
+    hit = u < delta
+    sub = hit & (ev <= 1)                                   # substitution to a different base
+    ins = hit & (ev == 2)                                   # insertion after the base
+    dele = hit & (ev == 3)                                  # deletion
+    base = s.copy()
+    base[sub] = BASES[(code[sub] + 1 + (rb[sub] % 3)) % 4]
+    cnt = np.ones(n, np.int64)
+    cnt[ins] = 2
+    cnt[dele] = 0
+    out = np.repeat(base, cnt)
+    start = np.cumsum(cnt) - cnt
+    out[start[ins] + 1] = BASES[rb[ins] & 3]
+    return out.tobytes()
 
 
 def mut_pair(length: int, delta: float, seed: int) -> tuple[bytes, bytes]:

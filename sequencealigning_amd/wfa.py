@@ -94,3 +94,51 @@ def wfa_align_batch(queries, dbs, pairs=None, mode: Mode = Mode.Global, *, max_s
             rows.append((aln[base:base + n1].tobytes()[::-1],
                          aln[base + cap:base + cap + n2].tobytes()[::-1]))
     return res, rows
+
+
+class WfaPlan:
+    """Device-resident WFA batch (include/saln.h saln_wfa_plan_*): plan once
+    from host offsets and a pair list, execute on device sequences into a
+    device results buffer (uint8[n_pairs * 32] or int32[n_pairs * 8]).  Used
+    for the configs[2] (C3) measurement."""
+
+    def __init__(self, q_off, db_off, pairs=None, mode: Mode = Mode.Global, *,
+                 max_steps: int = 64, max_width: int = 64, device: int = 0):
+        self._L = _lib.lib()
+        self.device = device
+        qo = np.ascontiguousarray(q_off, np.uint64)
+        do = np.ascontiguousarray(db_off, np.uint64)
+        n_q, n_db = len(qo) - 1, len(do) - 1
+        if pairs is None:
+            self.n_pairs = n_q * n_db
+            pq = pd = None
+        else:
+            pairs = np.asarray(pairs, np.uint32).reshape(-1, 2)
+            self.n_pairs = len(pairs)
+            pq = np.ascontiguousarray(pairs[:, 0])
+            pd = np.ascontiguousarray(pairs[:, 1])
+        vp = lambda a: a.ctypes.data_as(C.c_void_p) if a is not None else None  # noqa: E731
+        self._h = C.c_void_p()
+        _lib.check(self._L.saln_wfa_plan_create(_lib.context(device), vp(qo), n_q, vp(do), n_db,
+                                                vp(pq), vp(pd), self.n_pairs, int(mode),
+                                                max_steps, max_width, C.byref(self._h)),
+                   "saln_wfa_plan_create")
+
+    def execute(self, q_seq, db_seq, results, stream=None) -> None:
+        ptr = lambda t: t if isinstance(t, int) else t.data_ptr()  # noqa: E731
+        if stream is None:
+            import torch
+            stream = torch.cuda.current_stream(self.device).cuda_stream
+        _lib.check(self._L.saln_wfa_execute(self._h, ptr(q_seq), ptr(db_seq), ptr(results),
+                                            stream), "saln_wfa_execute")
+
+    def close(self) -> None:
+        if self._h:
+            self._L.saln_wfa_plan_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

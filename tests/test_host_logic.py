@@ -38,3 +38,32 @@ def test_pack_csr():
 
 def test_alignment_rows():
     assert alignment_rows(b"AAA", b"AA", [(1, "="), (1, "I"), (1, "=")]) == ("AAA", "| |", "A-A")
+
+
+def test_mutate_matches_per_base_definition():
+    """synth.mutate (vectorised) == the per-base G-mut(delta) definition of
+    SURVEY.md §8(d)."""
+    from sequencealigning_amd import synth
+
+    def slow(seq, delta, seed):
+        s = np.frombuffer(bytes(seq), np.uint8)
+        n = len(s)
+        r = synth.splitmix64(seed, 3 * n)
+        u = (r[:n] >> np.uint64(11)).astype(np.float64) / float(1 << 53)
+        ev = (r[n:2 * n] >> np.uint64(62)).astype(np.int64)
+        rb = (r[2 * n:] >> np.uint64(60)).astype(np.int64)
+        out = []
+        for k in range(n):
+            c = int(np.searchsorted(synth.BASES, s[k]))
+            if u[k] >= delta:
+                out.append(int(s[k]))
+            elif ev[k] <= 1:
+                out.append(int(synth.BASES[(c + 1 + (rb[k] % 3)) % 4]))
+            elif ev[k] == 2:
+                out.append(int(s[k]))
+                out.append(int(synth.BASES[rb[k] & 3]))
+        return bytes(out)
+
+    for seed, n, delta in [(1, 0, 0.1), (2, 1, 0.9), (3, 2000, 0.05), (4, 3000, 0.5)]:
+        q = synth.random_bases(seed, n).tobytes()
+        assert synth.mutate(q, delta, seed) == slow(q, delta, seed)

@@ -76,3 +76,25 @@ def test_golden_random_consistent(oracle):
         assert o.score == v["score"]
         assert o.first_ops == v["first_ops"]
         assert o.panics == v["panics"]
+
+
+def test_linear_oracle_matches_full(oracle):
+    """reflinear.c (linear memory, column stripes on threads) against the full
+    matrices + memoised DFS: score, end states and panic status, on small,
+    empty, tie-heavy and multi-stripe (lq > 256) pairs, and past the x+y
+    ~ 5,450 line where sentinel cells start to tie."""
+    from sequencealigning_amd import synth
+    rng = np.random.default_rng(11)
+    cases = [(b"", b""), (b"A", b""), (b"", b"ACG"), (b"ACGT", b"ACGT"), (b"AAAA", b"A")]
+    for _ in range(120):
+        cases.append((rand_seq(rng, int(rng.integers(0, 40)), b"ACGTN"),
+                      rand_seq(rng, int(rng.integers(0, 40)), b"AC")))
+    for lq, ld in [(700, 300), (300, 700), (1100, 40), (3100, 2600)]:
+        cases.append((rand_seq(rng, lq, b"ACGT"), rand_seq(rng, ld, b"ACGT")))
+    q, d = synth.mut_pair(900, 0.05, 7)
+    cases.append((q, d))
+    for q, d in cases:
+        o = oracle.nw(q, d, literal_dfs=False)
+        for threads in (1, 4):
+            got = oracle.nw_score_linear(q, d, threads)
+            assert got == (o.score, o.end_states, o.panics), (len(q), len(d), threads)

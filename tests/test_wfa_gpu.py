@@ -68,3 +68,47 @@ def test_modes(saln):
     for mode in (saln.Mode.Local, saln.Mode.SemiGlobal):
         with pytest.raises(saln.AlignmentError):
             saln.wfa_align(b"ACGT", b"ACGT", mode)
+
+
+def test_two_pass_cap_matches_oracle(saln, oracle):
+    """max_steps above the 64-step first pass: pairs that reach it are re-run
+    at the full cap; statuses / steps / scores equal one oracle run at the
+    full cap (incl. the never-converging pairs, NONCONVERGED at 400)."""
+    rng = np.random.default_rng(13)
+    qs, ds = [], []
+    for _ in range(400):
+        lq, ld = int(rng.integers(1, 120)), int(rng.integers(1, 120))
+        q = rand_seq(rng, lq)
+        d = (rand_seq(rng, ld) if rng.random() < 0.5
+             else (synth.mutate(q, 0.15, seed=int(rng.integers(1 << 30))) or b"A"))
+        qs.append(q)
+        ds.append(d)
+    n = len(qs)
+    res, _ = saln.wfa_align_batch(qs, ds, pairs=[(k, k) for k in range(n)], max_steps=400)
+    long_runs = 0
+    for k in range(n):
+        o = oracle.wfa(qs[k], ds[k], max_steps=400)
+        assert (int(res["status"][k]), int(res["steps"][k]), int(res["score"][k])) == \
+            (o.status, o.steps, o.score), k
+        long_runs += o.steps > 64
+    assert long_runs > 0
+
+
+def test_device_plan_matches_batch(saln):
+    """saln_wfa_plan_* on device buffers == the host batch API."""
+    import torch
+    rng = np.random.default_rng(14)
+    qs = [rand_seq(rng, int(rng.integers(1, 90))) for _ in range(300)]
+    ds = [synth.mutate(q, 0.1, seed=k) or b"G" for k, q in enumerate(qs)]
+    pairs = [(k, k) for k in range(len(qs))] + [(k, (k * 7) % len(ds)) for k in range(len(qs))]
+    ref, _ = saln.wfa_align_batch(qs, ds, pairs=pairs, max_steps=300)
+    q_seq, q_off = saln.pack_csr(qs)
+    d_seq, d_off = saln.pack_csr(ds)
+    plan = saln.WfaPlan(q_off, d_off, pairs=pairs, max_steps=300)
+    out = torch.zeros(len(pairs) * 8, dtype=torch.int32, device="cuda")
+    plan.execute(torch.from_numpy(q_seq.copy()).cuda(), torch.from_numpy(d_seq.copy()).cuda(), out)
+    torch.cuda.synchronize()
+    got = out.cpu().numpy().view(saln._lib.WFA_RESULT_DTYPE)
+    plan.close()
+    for f in ("score", "status", "steps", "conv_offset", "conv_state", "conv_np"):
+        assert np.array_equal(got[f], ref[f]), f
