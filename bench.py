@@ -78,8 +78,9 @@ def main() -> None:
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--score-only", action="store_true",
                     help="score + panic status only (no parent codes / traceback; the C5 mode)")
-    ap.add_argument("--no-pipeline", action="store_true",
-                    help="run each step's traceback to completion before the next fill")
+    ap.add_argument("--pipeline", action="store_true",
+                    help="overlap step k's traceback with step k+1's fill on a second stream "
+                         "(measured slower on MI355X: the walk slows the VALU-bound fill)")
     args = ap.parse_args()
 
     import torch
@@ -100,10 +101,10 @@ def main() -> None:
     plan = saln.NwPlan(qo, do, pairs=np.stack([np.arange(n), np.arange(n)], 1), device=local)
     dq = torch.from_numpy(qs).to(f"cuda:{local}")
     dd = torch.from_numpy(ds).to(f"cuda:{local}")
-    # Pipelined steps (default): the traceback of step k runs on the engine's
-    # second stream while step k+1 fills; results/cigar/mask are double-buffered
-    # and every step's results are complete (and gathered) inside the timed region.
-    pipelined = not args.no_pipeline and not args.score_only
+    # --pipeline: the traceback of step k runs on the engine's second stream
+    # while step k+1 fills; results/cigar/mask are double-buffered and every
+    # step's results are complete (and gathered) inside the timed region.
+    pipelined = args.pipeline and not args.score_only
     plan.set_score_only(args.score_only)
     plan.set_async(pipelined)
     nbuf = 2 if pipelined else 1

@@ -20,6 +20,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <type_traits>
 
 #include "nw_common.hpp"
 #include "saln.h"
@@ -521,6 +522,10 @@ __global__ __launch_bounds__(256) void nw_traceback_lds_kernel(
     __shared__ __attribute__((aligned(16))) uint8_t win_all[4 * kWave];
     const uint32_t idx = first + blockIdx.x * blockDim.x + threadIdx.x;
     if (idx >= first + n) return;
+    // The walk is a latency-bound chain; when it shares a SIMD with the
+    // VALU-bound fill of the next batch (pipelined plans) it must not queue
+    // behind the fill's instructions.
+    __builtin_amdgcn_s_setprio(3);
     const NwPairDesc p = pairs[idx];
     walk_pair_lds<G, K>(p, end_h[idx], mask, ops, results, cigar, sc,
                         (lds_u8 *)(win_all + (threadIdx.x / 64u) * kWave));
@@ -862,20 +867,43 @@ __device__ __forceinline__ uint32_t gshift(uint32_t bnd, uint32_t v, bool group_
     return group_start ? bnd : s;
 }
 
-// signs of (lo, hi) halves of s0 and s1 -> 0x00/0xFF bytes [A0, A1, B0, B1]
-__device__ __forceinline__ uint32_t sign_bytes(uint32_t s0, uint32_t s1) {
-    return __builtin_amdgcn_perm(s1, s0, 0x0B090A08u);
+// Sign bytes of one code source t over two columns: the (A, B) halves of
+// s_t at columns k-1 (lo) and k (hi) -> 0x00/0xFF bytes [A_k-1, B_k-1, A_k, B_k].
+__device__ __forceinline__ uint32_t col_pair_signs(uint32_t hi, uint32_t lo) {
+    return __builtin_amdgcn_perm(hi, lo, 0x0B0A0908u);
 }
 
-// 4 per-cell accumulators [A_even, A_odd, B_even, B_odd] -> (A codes, B codes)
-__device__ __forceinline__ void pack4(uint32_t a0, uint32_t a1, uint32_t a2, uint32_t a3,
-                                      uint32_t &ca, uint32_t &cb) {
-    const uint32_t x = __builtin_amdgcn_perm(a1, a0, 0x05040100u);  // [a0.b0 a0.b1 a1.b0 a1.b1]
-    const uint32_t y = __builtin_amdgcn_perm(a3, a2, 0x05040100u);
-    ca = __builtin_amdgcn_perm(y, x, 0x06040200u) | __builtin_amdgcn_perm(y, x, 0x07050301u);
-    const uint32_t xb = __builtin_amdgcn_perm(a1, a0, 0x07060302u);
-    const uint32_t yb = __builtin_amdgcn_perm(a3, a2, 0x07060302u);
-    cb = __builtin_amdgcn_perm(yb, xb, 0x06040200u) | __builtin_amdgcn_perm(yb, xb, 0x07050301u);
+// (m & a) | (~m & b) as one v_bfi_b32 (written out, the compiler turns a
+// chain of these into an and per source plus or3s).  m: a loop-invariant
+// constant, kept in an SGPR.
+__device__ __forceinline__ uint32_t bfi(uint32_t m, uint32_t a, uint32_t b) {
+    uint32_t r;
+    asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "s"(m), "v"(a), "v"(b));
+    return r;
+}
+
+// Merge the sign-byte words of the code sources (bit t of every cell byte
+// from source t) with a v_bfi chain: each step keeps the bits below the next
+// source and takes the rest from it.  Walk codes have no sources for bits 3
+// and 5; those bits then hold a copy of the next source (the walker never
+// reads them in walk mode).  argM (bit 0) is only read at the end cell; rows
+// that hold no end cell get a copy of bit 1 there.
+template <bool kArgMBit>
+__device__ __forceinline__ uint32_t merge_walk(const uint32_t (&p)[8]) {
+    uint32_t r = kArgMBit ? bfi(0x01010101u, p[0], p[1]) : p[1];
+    r = bfi(0x03030303u, r, p[2]);
+    r = bfi(0x07070707u, r, p[4]);
+    r = bfi(0x1F1F1F1Fu, r, p[6]);
+    return bfi(0x7F7F7F7Fu, r, p[7]);
+}
+__device__ __forceinline__ uint32_t merge_full(const uint32_t (&p)[8]) {
+    uint32_t r = bfi(0x01010101u, p[0], p[1]);
+    r = bfi(0x03030303u, r, p[2]);
+    r = bfi(0x07070707u, r, p[3]);
+    r = bfi(0x0F0F0F0Fu, r, p[4]);
+    r = bfi(0x1F1F1F1Fu, r, p[5]);
+    r = bfi(0x3F3F3F3Fu, r, p[6]);
+    return bfi(0x7F7F7F7Fu, r, p[7]);
 }
 
 template <int K>
@@ -1011,7 +1039,13 @@ __global__ __launch_bounds__(256) void nw_fill_pk_kernel(Src src, uint32_t count
         if (r >= 1 && r <= ldM) {
             uint32_t F = inF;
             PkMask<K> wa, wb;
-            uint32_t acc[4] = {0u, 0u, 0u, 0u};
+            // code words of column pairs: bytes [A_2c, B_2c, A_2c+1, B_2c+1]
+            uint32_t cw[(K + 1) / 2];
+            uint32_t prv[8];  // sign sources of the previous (even) column
+            // argM (bit 0) is only ever read at a pair's end cell: the wave
+            // computes it on the steps where one of its lanes holds one.
+            auto columns = [&](auto with_argm) __attribute__((always_inline)) {
+            constexpr bool kM = decltype(with_argm)::value;
 #pragma unroll
             for (int k = 0; k < K; ++k) {
                 const u16x2 x = __builtin_bit_cast(u16x2, qc[k] ^ dch);
@@ -1020,30 +1054,36 @@ __global__ __launch_bounds__(256) void nw_fill_pk_kernel(Src src, uint32_t count
                 const s16x2 M = as_s2(hd) - pen;
                 const s16x2 I = as_s2(F), D = as_s2(Dn[k]);
                 const s16x2 H = vmax(M, vmax(I, D));
-                const s16x2 Hc = as_s2(as_u(H) & 0xFFFEFFFEu);
                 const s16x2 tO = M + kOpen;
                 if constexpr (kCodes != kCodesNone) {
                 // sign set <=> parent absent.  Extend/open ties are decided on
                 // the flag-free order: with X = 2x+f, tO = 2o+g,
                 // ext <=> x >= o <=> X >= (tO & ~1),  open <=> o >= x <=> (tO | 1) >= X.
+                const s16x2 Hc = as_s2(as_u(H) & 0xFFFEFFFEu);
                 const s16x2 tOr = as_s2(as_u(tO) | 0x00010001u);
-                const uint32_t s0 = as_u(M - Hc), s1 = as_u(I - Hc), s2 = as_u(D - Hc);
-                const uint32_t s4 = as_u(tOr - I), s6 = as_u(tOr - D);
-                const uint32_t s7 = as_u(pen - spl(1));  // sign <=> q == d (bit 7)
-                uint32_t a = sign_bytes(s0, s1) & 0x02010201u;
-                if constexpr (kCodes == kCodesWalk) {
-                    a = (sign_bytes(s2, s4) & 0x10041004u) | a;
-                } else {
+                uint32_t sg[8];
+                sg[0] = kM ? as_u(M - Hc) : 0u;
+                sg[1] = as_u(I - Hc);
+                sg[2] = as_u(D - Hc);
+                sg[4] = as_u(tOr - I);
+                sg[6] = as_u(tOr - D);
+                sg[7] = as_u(pen - spl(1));  // sign <=> q == d (bit 7)
+                if constexpr (kCodes == kCodesFull) {
                     const s16x2 tOc = as_s2(as_u(tO) & 0xFFFEFFFEu);
-                    const uint32_t s3 = as_u(I - tOc), s5 = as_u(D - tOc);
-                    a = (sign_bytes(s2, s3) & 0x08040804u) | a;
-                    a = (sign_bytes(s4, s5) & 0x20102010u) | a;
+                    sg[3] = as_u(I - tOc);
+                    sg[5] = as_u(D - tOc);
+                } else {
+                    sg[3] = sg[5] = 0u;
                 }
-                a = (sign_bytes(s6, s7) & 0x80408040u) | a;
-                acc[k % 4] = a;
-                if (k % 4 == 3 || k == K - 1) {
-                    pack4(acc[0], k % 4 >= 1 ? acc[1] : 0u, k % 4 >= 2 ? acc[2] : 0u,
-                          k % 4 >= 3 ? acc[3] : 0u, wa.w[k / 4], wb.w[k / 4]);
+                if (k % 2 == 0 && k < K - 1) {
+#pragma unroll
+                    for (int t = 0; t < 8; ++t) prv[t] = sg[t];
+                } else {
+                    uint32_t pw[8];
+#pragma unroll
+                    for (int t = 0; t < 8; ++t)
+                        pw[t] = k % 2 ? col_pair_signs(sg[t], prv[t]) : col_pair_signs(0u, sg[t]);
+                    cw[k / 2] = kCodes == kCodesFull ? merge_full(pw) : merge_walk<kM>(pw);
                 }
                 }
                 F = as_u(vmax(tO, I));
@@ -1051,10 +1091,28 @@ __global__ __launch_bounds__(256) void nw_fill_pk_kernel(Src src, uint32_t count
                 hd = Hp[k];
                 Hp[k] = as_u(H);
             }
+            };
+            if constexpr (kCodes == kCodesWalk) {
+                const bool endcell = (r == ldA && lane == lA) || (r == ldB && lane == lB);
+                if (__builtin_amdgcn_ballot_w64(endcell))
+                    columns(std::true_type{});
+                else
+                    columns(std::false_type{});
+            } else {
+                columns(std::true_type{});
+            }
             hd = inH;
             pubF = F;
             pubH = Hp[K - 1];
             if constexpr (kCodes != kCodesNone) {
+                // column-pair words [A A' ..] -> per-pair words of 4 columns
+#pragma unroll
+                for (int w = 0; w < (K + 3) / 4; ++w) {
+                    const uint32_t lo = cw[2 * w];
+                    const uint32_t hi = 2 * w + 1 < (K + 1) / 2 ? cw[2 * w + 1] : 0u;
+                    wa.w[w] = __builtin_amdgcn_perm(hi, lo, 0x06040200u);
+                    wb.w[w] = __builtin_amdgcn_perm(hi, lo, 0x07050301u);
+                }
                 if (r <= ldA) *reinterpret_cast<PkMask<K> *>(mA + (uint64_t)(r - 1) * pa.mask_rs) = wa;
                 if (r <= ldB) *reinterpret_cast<PkMask<K> *>(mB + (uint64_t)(r - 1) * pb.mask_rs) = wb;
             }
@@ -1127,7 +1185,11 @@ static void fill_pk(dim3 grid, hipStream_t s, const NwPairDesc *pairs, uint32_t 
                     uint32_t count, const uint8_t *qs, const uint8_t *ds, uint8_t *mask,
                     int32_t *end_h, saln_nw_result *, uint32_t *, Scoring sc, int codes,
                     uint32_t ld_max) {
-    const size_t lds = (size_t)(256 / G) * ld_max * sizeof(uint32_t);
+    static const size_t pad = [] {  // experiment switch: LDS floor per workgroup (occupancy)
+        const char *e = std::getenv("SALN_FILL_LDS_MIN");
+        return e ? (size_t)std::atol(e) : (size_t)0;
+    }();
+    const size_t lds = std::max((size_t)(256 / G) * ld_max * sizeof(uint32_t), pad);
     const PlanSrc src{pairs, first, end_h};
     if (codes == kCodesFull)
         nw_fill_pk_kernel<G, K, kCodesFull><<<grid, dim3(256), lds, s>>>(src, count, qs, ds, mask,
