@@ -12,7 +12,8 @@ import os
 import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libsaln.so")
+# SALN_LIB: an instrumented / experimental in-tree build (tools/) instead of libsaln.so
+LIB_PATH = os.environ.get("SALN_LIB") or os.path.join(_HERE, "libsaln.so")
 
 # saln_status (include/saln.h)
 OK = 0

@@ -191,11 +191,15 @@ constexpr uint32_t kOpsPerWord = 10;                     // 3-bit ops per op-str
 // request per lane per DMA), so W is kept small: with 10-column blocks a
 // diagonal path crosses a block every ~10 rows and W = 4 lets the window of
 // B-2 refill before the next crossing.
+#ifndef SALN_WALK_W
+#define SALN_WALK_W 0  // experiment switch: force the window depth
+#endif
+constexpr uint32_t kWalkW = SALN_WALK_W;
 template <int K>
 struct WalkGeo {
     static constexpr uint32_t LB = (K + 3) / 4 * 4;
     static constexpr uint32_t NW = 2;
-    static constexpr uint32_t W = K < 16 ? 4 : 8;
+    static constexpr uint32_t W = kWalkW ? kWalkW : (K < 16 ? 4 : 8);
     static constexpr uint32_t SB = LB == 12 ? 12 : 16;        // DMA bytes per lane
     static constexpr uint32_t kSlotBytes = 64 * 16;          // one slot of a wave
     static constexpr uint32_t kWinBytes = W * kSlotBytes;    // one window of a wave
