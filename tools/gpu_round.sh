@@ -11,7 +11,7 @@ if [[ $STEP == all || $STEP == smoke ]]; then
   tail -2 gpurun_out/smoke.log
 fi
 if [[ $STEP == all || $STEP == test ]]; then
-  timeout -k 10 900 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu.log 2>&1 || { echo "pytest gpu failed rc=$?"; tail -40 gpurun_out/pytest_gpu.log; exit 1; }
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1 || { echo "pytest gpu failed rc=$?"; tail -40 gpurun_out/pytest_gpu.log; exit 1; }
   tail -3 gpurun_out/pytest_gpu.log
 fi
 if [[ $STEP == all || $STEP == bench ]]; then
