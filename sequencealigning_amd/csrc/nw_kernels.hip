@@ -25,6 +25,16 @@
 #include "nw_common.hpp"
 #include "saln.h"
 
+#ifndef SALN_PINGPONG
+#define SALN_PINGPONG 0
+#endif
+#ifndef SALN_PAIRMAP
+#define SALN_PAIRMAP 0
+#endif
+#ifndef SALN_EXP_NOSTORE
+#define SALN_EXP_NOSTORE 0  // experiment builds only: fill without mask stores
+#endif
+
 namespace saln {
 
 // lane i <- lane i-1 within the group; the group's lane 0 keeps `old`.
@@ -858,6 +868,27 @@ __device__ __forceinline__ uint32_t pk2(int32_t lo, int32_t hi) {
     return ((uint32_t)lo & 0xFFFFu) | ((uint32_t)hi << 16);
 }
 __device__ __forceinline__ s16x2 vmax(s16x2 a, s16x2 b) { return __builtin_elementwise_max(a, b); }
+// Biased pair word: each half holds v + 32768 (an unsigned 16-bit number
+// ordered like v).  Inside the packed region every value stays in
+// [-30000, 30000], so 32-bit adds / subtracts of these words never carry or
+// borrow across the halves (SWAR: one full-rate v_add/v_sub_u32 per two
+// cells), and a half's bit 15 of a 32-bit difference is the sign of that
+// half's difference; the low half's borrow only lowers the high half by 1,
+// which the comparisons below tolerate by never letting a high half be 0.
+__device__ __forceinline__ uint32_t pkb(int32_t lo, int32_t hi) {
+    return ((uint32_t)(lo + 32768) & 0xFFFFu) | ((uint32_t)(hi + 32768) << 16);
+}
+__device__ __forceinline__ uint32_t umax2(uint32_t a, uint32_t b) {
+    return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(u16x2, a),
+                                                                  __builtin_bit_cast(u16x2, b)));
+}
+__device__ __forceinline__ uint32_t umin2(uint32_t a, uint32_t b) {
+    return __builtin_bit_cast(uint32_t, __builtin_elementwise_min(__builtin_bit_cast(u16x2, a),
+                                                                  __builtin_bit_cast(u16x2, b)));
+}
+// constant c in both halves, as the 32-bit addend that adds c to each half
+// of a biased word (for c < 0 it is the two's complement of |c| * 0x10001)
+__device__ __forceinline__ uint32_t cst2(int32_t c) { return (uint32_t)c * 0x10001u; }
 
 // lane <- lane-1 of the same group; a group's first lane takes `bnd`.
 template <int G>
@@ -970,10 +1001,17 @@ __global__ __launch_bounds__(256) void nw_fill_pk_kernel(Src src, uint32_t count
                                                          uint32_t ld_max) {
     constexpr int GPB = 256 / G;
     constexpr Geom geo{G, K};
-    extern __shared__ uint32_t drow[];  // [GPB][ld_max] packed db chars (dch) per row
+    extern __shared__ uint32_t drow[];  // [GPB][G + ld_max + G] packed db chars (dch) per row
     const int lane = threadIdx.x % G;
     const uint32_t gi = pack_block(blocks_per_pack(2 * GPB)) * GPB + threadIdx.x / G;
+#if SALN_PAIRMAP
+    // the GW groups of a wave hold pairs w*2GW + g (A) and + GW (B): each
+    // mask store instruction writes GW adjacent segments per (row, block)
+    constexpr uint32_t GW = 64 / G;
+    const uint32_t ia = (gi / GW) * 2 * GW + gi % GW, ib = ia + GW;
+#else
     const uint32_t ia = 2 * gi, ib = 2 * gi + 1;
+#endif
     if (ia >= count) return;  // whole group
     const bool hasB = ib < count;
     const NwPairDesc pa = src.pair(ia);
@@ -988,9 +1026,10 @@ __global__ __launch_bounds__(256) void nw_fill_pk_kernel(Src src, uint32_t count
     const int ldM = ldA > ldB ? ldA : ldB;
     const int32_t beta = -2 * sc.gap_extend;
     const int32_t alpha = -2 * sc.match - beta;
-    const s16x2 kPen = spl(2 * (sc.match - sc.mismatch));
-    const s16x2 kOpen = spl(2 * sc.gap_open);
-    const s16x2 kDstep = spl(2 * sc.gap_extend + alpha);
+    const uint32_t kPen = cst2(2 * (sc.match - sc.mismatch));  // 0 < pen <= 32
+    const uint32_t kOpen = cst2(2 * sc.gap_open);
+    const uint32_t kOpen1 = cst2(2 * sc.gap_open + 1);
+    const uint32_t kDstep = cst2(2 * sc.gap_extend + alpha);
     const bool gstart = lane == 0;
 
     const int col0 = lane * K;  // my columns: col0+1 .. col0+K
@@ -1005,17 +1044,19 @@ __global__ __launch_bounds__(256) void nw_fill_pk_kernel(Src src, uint32_t count
         qc[k] = ca | (cb << 16);
         const int32_t h0 = hs_row0(sc, (uint32_t)j) + beta * j;           // H~(0, j)
         const int32_t d1 = ds_row1(sc, (uint32_t)j) + alpha + beta * j;   // D~(1, j)
-        Hp[k] = pk2(h0, h0);
-        Dn[k] = pk2(d1, d1);
+        Hp[k] = pkb(h0, h0);
+        Dn[k] = pkb(d1, d1);
     }
-    uint32_t hd = pk2(hs_row0(sc, (uint32_t)col0) + beta * col0,
+    uint32_t hd = pkb(hs_row0(sc, (uint32_t)col0) + beta * col0,
                       hs_row0(sc, (uint32_t)col0) + beta * col0);  // H~(r-1, col0)
     uint32_t pubF = 0, pubH = 0;
     // db chars of both pairs, staged once per group in LDS as the packed
     // (A << 5 | B << 21) word of each row; a step reads its row's word from
     // LDS (lgkmcnt), so no global load sits in the step loop next to the
-    // mask stores (vmcnt).
-    uint32_t *__restrict__ myrow = drow + (threadIdx.x / G) * ld_max;
+    // mask stores (vmcnt).  Rows are padded by G words on both sides, so the
+    // skewed row index r-1 of any lane at any step addresses the row without
+    // a clamp (the pad words are only read by steps whose body is skipped).
+    uint32_t *__restrict__ myrow = drow + (threadIdx.x / G) * (ld_max + 2 * G) + G;
     for (int i = lane; i < ldM; i += G) {
         const uint32_t ca = i < ldA ? (uint32_t)dA[i] : 0u;
         const uint32_t cb = i < ldB ? (uint32_t)dB[i] : 0u;
@@ -1026,20 +1067,28 @@ __global__ __launch_bounds__(256) void nw_fill_pk_kernel(Src src, uint32_t count
     // end-cell owners
     const int lA = (lqA - 1) / K, kA = (lqA - 1) % K;
     const int lB = hasB ? (lqB - 1) / K : -1, kB = hasB ? (lqB - 1) % K : 0;
-    // this lane's segments of row 1 (block = lane)
-    uint8_t *__restrict__ mA = mask + pa.mask_off + (uint64_t)lane * pa.mask_bs;
-    uint8_t *__restrict__ mB = mask + pb.mask_off + (uint64_t)lane * pb.mask_bs;
+    // this lane's segment of row r = t - lane + 1 (block = lane), advanced
+    // by one row per step (64-bit adds instead of a row multiply per store)
+    uint8_t *__restrict__ mA = mask + pa.mask_off + (uint64_t)lane * pa.mask_bs -
+                               (int64_t)lane * (int64_t)pa.mask_rs;
+    uint8_t *__restrict__ mB = mask + pb.mask_off + (uint64_t)lane * pb.mask_bs -
+                               (int64_t)lane * (int64_t)pb.mask_rs;
+    const uint32_t *__restrict__ rowp = myrow - lane;  // word of row r-1 at step 0
     const int T = (int)geo.steps((uint32_t)ldM);
+    // Previous-row H: step t reads Hin (row r-1) and writes Hout (row r).
+    // SALN_PINGPONG: a two-step unroll swaps two arrays (no register
+    // rotation, more live registers); otherwise in place.
+    uint32_t HpB[K];
 
-    for (int t = 0; t < T; ++t) {
+    auto step = [&](int t, uint32_t(&Hin)[K], uint32_t(&Hout)[K]) __attribute__((always_inline)) {
         const int r = t - lane + 1;
-        const uint32_t dch = myrow[min(max(r - 1, 0), ldM - 1)];
+        const uint32_t dch = rowp[t];
         // group-start inputs for row t+1: I~(r,1) and H~(r,0) (same for A and B)
         const int32_t rb = t + 1;
         const int32_t bF = is_col1(sc, (uint32_t)rb) + alpha * rb + beta;
         const int32_t bH = hs_col0(sc, (uint32_t)rb) + alpha * rb;
-        const uint32_t inF = gshift<G>(pk2(bF, bF), pubF, gstart);
-        const uint32_t inH = gshift<G>(pk2(bH, bH), pubH, gstart);
+        const uint32_t inF = gshift<G>(pkb(bF, bF), pubF, gstart);
+        const uint32_t inH = gshift<G>(pkb(bH, bH), pubH, gstart);
         if (r >= 1 && r <= ldM) {
             uint32_t F = inF;
             PkMask<K> wa, wb;
@@ -1050,32 +1099,41 @@ __global__ __launch_bounds__(256) void nw_fill_pk_kernel(Src src, uint32_t count
             // computes it on the steps where one of its lanes holds one.
             auto columns = [&](auto with_argm) __attribute__((always_inline)) {
             constexpr bool kM = decltype(with_argm)::value;
+            uint32_t diag = hd;  // H~(r-1, c-1) of column k
 #pragma unroll
             for (int k = 0; k < K; ++k) {
-                const u16x2 x = __builtin_bit_cast(u16x2, qc[k] ^ dch);
-                const s16x2 pen = __builtin_bit_cast(
-                    s16x2, __builtin_elementwise_min(x, __builtin_bit_cast(u16x2, kPen)));
-                const s16x2 M = as_s2(hd) - pen;
-                const s16x2 I = as_s2(F), D = as_s2(Dn[k]);
-                const s16x2 H = vmax(M, vmax(I, D));
-                const s16x2 tO = M + kOpen;
+                const uint32_t hdk = diag;
+                diag = Hin[k];
+                const uint32_t pen = umin2(qc[k] ^ dch, kPen);
+                const uint32_t M = hdk - pen;
+                const uint32_t I = F, D = Dn[k];
+                const uint32_t H = umax2(M, umax2(I, D));
+                const uint32_t tO = M + kOpen;
                 if constexpr (kCodes != kCodesNone) {
-                // sign set <=> parent absent.  Extend/open ties are decided on
-                // the flag-free order: with X = 2x+f, tO = 2o+g,
-                // ext <=> x >= o <=> X >= (tO & ~1),  open <=> o >= x <=> (tO | 1) >= X.
-                const s16x2 Hc = as_s2(as_u(H) & 0xFFFEFFFEu);
-                const s16x2 tOr = as_s2(as_u(tO) | 0x00010001u);
+                // Sign set <=> parent absent.  With X = 2x+f (flag f in the
+                // LSB) and tO = 2o+g, every test is a difference whose high
+                // half is never 0: present -> >= 1, absent -> <= -1.
+                //   arg X   (x == h):  (X | 1) - (H & ~1)
+                //   open    (o >= x):  ((tO & ~1) + 2) - (X | 1)
+                //   extend  (x >= o):  (X | 1) - (tO & ~1)
+                const uint32_t Hc = H & 0xFFFEFFFEu;
+                const uint32_t M1 = M | 0x00010001u;
+                const uint32_t I1 = I | 0x00010001u, D1 = D | 0x00010001u;
+                const uint32_t tOr1 = M1 + kOpen1;  // (tO & ~1) + 2
                 uint32_t sg[8];
-                sg[0] = kM ? as_u(M - Hc) : 0u;
-                sg[1] = as_u(I - Hc);
-                sg[2] = as_u(D - Hc);
-                sg[4] = as_u(tOr - I);
-                sg[6] = as_u(tOr - D);
-                sg[7] = as_u(pen - spl(1));  // sign <=> q == d (bit 7)
+                sg[0] = kM ? M1 - Hc : 0u;
+                sg[1] = I1 - Hc;
+                sg[2] = D1 - Hc;
+                sg[4] = tOr1 - I1;
+                sg[6] = tOr1 - D1;
+                // sign <=> q == d (bit 7): pen is 0 or pen_max >= 2 in both
+                // halves (the low half's borrow moves the high half from
+                // pen_max - 1 to pen_max - 2 or from -1 to -2)
+                sg[7] = pen - 0x00010001u;
                 if constexpr (kCodes == kCodesFull) {
-                    const s16x2 tOc = as_s2(as_u(tO) & 0xFFFEFFFEu);
-                    sg[3] = as_u(I - tOc);
-                    sg[5] = as_u(D - tOc);
+                    const uint32_t tOc = tO & 0xFFFEFFFEu;
+                    sg[3] = I1 - tOc;
+                    sg[5] = D1 - tOc;
                 } else {
                     sg[3] = sg[5] = 0u;
                 }
@@ -1090,10 +1148,9 @@ __global__ __launch_bounds__(256) void nw_fill_pk_kernel(Src src, uint32_t count
                     cw[k / 2] = kCodes == kCodesFull ? merge_full(pw) : merge_walk<kM>(pw);
                 }
                 }
-                F = as_u(vmax(tO, I));
-                Dn[k] = as_u(vmax(tO, D) + kDstep);
-                hd = Hp[k];
-                Hp[k] = as_u(H);
+                F = umax2(tO, I);
+                Dn[k] = umax2(tO, D) + kDstep;
+                Hout[k] = H;
             }
             };
             if constexpr (kCodes == kCodesWalk) {
@@ -1107,7 +1164,7 @@ __global__ __launch_bounds__(256) void nw_fill_pk_kernel(Src src, uint32_t count
             }
             hd = inH;
             pubF = F;
-            pubH = Hp[K - 1];
+            pubH = Hout[K - 1];
             if constexpr (kCodes != kCodesNone) {
                 // column-pair words [A A' ..] -> per-pair words of 4 columns
 #pragma unroll
@@ -1117,25 +1174,46 @@ __global__ __launch_bounds__(256) void nw_fill_pk_kernel(Src src, uint32_t count
                     wa.w[w] = __builtin_amdgcn_perm(hi, lo, 0x06040200u);
                     wb.w[w] = __builtin_amdgcn_perm(hi, lo, 0x07050301u);
                 }
-                if (r <= ldA) *reinterpret_cast<PkMask<K> *>(mA + (uint64_t)(r - 1) * pa.mask_rs) = wa;
-                if (r <= ldB) *reinterpret_cast<PkMask<K> *>(mB + (uint64_t)(r - 1) * pb.mask_rs) = wb;
+#if SALN_EXP_NOSTORE
+#pragma unroll
+                for (int w = 0; w < (K + 3) / 4; ++w) asm volatile("" : : "v"(wa.w[w]), "v"(wb.w[w]));
+#else
+                if (r <= ldA) *reinterpret_cast<PkMask<K> *>(mA) = wa;
+                if (r <= ldB) *reinterpret_cast<PkMask<K> *>(mB) = wb;
+#endif
             }
             if (r == ldA && lane == lA) {
                 int32_t e = 0;
 #pragma unroll
                 for (int k = 0; k < K; ++k)
-                    if (k == kA) e = (int16_t)(Hp[k] & 0xFFFFu);
+                    if (k == kA) e = (int32_t)(Hout[k] & 0xFFFFu) - 32768;
                 src.end(ia, pa, e - alpha * ldA - beta * lqA);
             }
             if (r == ldB && lane == lB) {
                 int32_t e = 0;
 #pragma unroll
                 for (int k = 0; k < K; ++k)
-                    if (k == kB) e = (int16_t)(Hp[k] >> 16);
+                    if (k == kB) e = (int32_t)(Hout[k] >> 16) - 32768;
                 src.end(ib, pb, e - alpha * ldB - beta * lqB);
             }
+        } else if (&Hout != &Hin) {
+#pragma unroll
+            for (int k = 0; k < K; ++k) Hout[k] = Hin[k];  // lane idle: keep row r-1
         }
+        mA += pa.mask_rs;
+        mB += pb.mask_rs;
+    };
+#if SALN_PINGPONG
+    int t = 0;
+    for (; t + 1 < T; t += 2) {
+        step(t, Hp, HpB);
+        step(t + 1, HpB, Hp);
     }
+    if (t < T) step(t, Hp, HpB);
+#else
+    (void)HpB;
+    for (int t = 0; t < T; ++t) step(t, Hp, Hp);
+#endif
 }
 
 // Score-only results (saln_nw_plan_set_score_only): score and panic status
@@ -1193,7 +1271,7 @@ static void fill_pk(dim3 grid, hipStream_t s, const NwPairDesc *pairs, uint32_t 
         const char *e = std::getenv("SALN_FILL_LDS_MIN");
         return e ? (size_t)std::atol(e) : (size_t)0;
     }();
-    const size_t lds = std::max((size_t)(256 / G) * ld_max * sizeof(uint32_t), pad);
+    const size_t lds = std::max((size_t)(256 / G) * (ld_max + 2 * G) * sizeof(uint32_t), pad);
     const PlanSrc src{pairs, first, end_h};
     if (codes == kCodesFull)
         nw_fill_pk_kernel<G, K, kCodesFull><<<grid, dim3(256), lds, s>>>(src, count, qs, ds, mask,
@@ -1213,7 +1291,7 @@ static void avsa_pk(const AvsaSrc &src, uint32_t count, const uint8_t *qs, const
     const uint32_t sup = 8 * blocks_per_pack(2 * gpb);
     const uint32_t groups = (count + 1) / 2;
     const dim3 grid(((groups + gpb - 1) / gpb + sup - 1) / sup * sup);
-    const size_t lds = (size_t)gpb * ld_max * sizeof(uint32_t);
+    const size_t lds = (size_t)gpb * (ld_max + 2 * G) * sizeof(uint32_t);
     nw_fill_pk_kernel<G, K, kCodesNone><<<grid, dim3(256), lds, s>>>(src, count, qs, ds, nullptr,
                                                                        sc, ld_max);
 }
@@ -1360,7 +1438,8 @@ bool variant_packed(int v) { return kPacked[v]; }
 // inside int16 with the position offsets of nw_fill_pk_kernel (see there).
 static bool packed_ok(uint32_t lq, uint32_t ld, const Scoring &sc) {
     const int64_t pen = 2ll * (sc.match - sc.mismatch);
-    if (pen < 0 || pen > 32 || sc.gap_extend > 0 || sc.gap_open > 0) return false;
+    // pen >= 2: the q==d bit comes from the penalty (0 or pen in each half)
+    if (pen < 2 || pen > 32 || sc.gap_extend > 0 || sc.gap_open > 0) return false;
     const int64_t span = std::max<int64_t>(
         {std::abs(sc.match), std::abs(sc.mismatch), std::abs(sc.gap_open) + std::abs(sc.gap_extend)});
     const int64_t a = 2 * (std::abs(sc.match) + std::abs(sc.gap_extend)) + 2 * span;

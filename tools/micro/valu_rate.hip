@@ -25,6 +25,35 @@
     };
 
 OP2(PkMaxI16, "v_pk_max_i16")
+OP2(PkAddU16, "v_pk_add_u16")
+OP2(SubU32, "v_sub_u32")
+OP2(AndB32, "v_and_b32")
+OP2(LshlB32, "v_lshlrev_b32")
+OP2(MinU32, "v_min_u32")
+OP2(MaxI16, "v_max_i16")
+OP2(SubU16, "v_sub_u16")
+OP2(MaxU32, "v_max_u32")
+OP3(LshlOr, "v_lshl_or_b32")
+OP3(Or3, "v_or3_b32")
+OP3(Xad, "v_xad_u32")
+struct MadU64 {
+    static constexpr const char *s = "v_mad_u64_u32";
+    __device__ static void run(uint32_t (&a)[8], uint32_t b) {
+        _Pragma("unroll") for (int i = 0; i < 4; ++i) {
+            uint64_t acc = ((uint64_t)a[2 * i + 1] << 32) | a[2 * i];
+            asm volatile("v_mad_u64_u32 %0, vcc, %1, %2, %0" : "+v"(acc) : "v"(b), "v"(b));
+            asm volatile("v_mad_u64_u32 %0, vcc, %1, %2, %0" : "+v"(acc) : "v"(b), "v"(b));
+            a[2 * i] = (uint32_t)acc; a[2 * i + 1] = (uint32_t)(acc >> 32);
+        }
+    }
+};
+struct MovDpp {
+    static constexpr const char *s = "v_mov_b32_dpp row_shr:1";
+    __device__ static void run(uint32_t (&a)[8], uint32_t b) {
+        _Pragma("unroll") for (int i = 0; i < 8; ++i)
+            asm volatile("v_mov_b32_dpp %0, %1 row_shr:1 row_mask:0xf bank_mask:0xf" : "+v"(a[i]) : "v"(a[(i + 1) % 8]));
+    }
+};
 OP2(PkSubI16, "v_pk_sub_i16")
 OP2(PkMinU16, "v_pk_min_u16")
 OP2(MaxI32, "v_max_i32")
@@ -86,6 +115,19 @@ int main() {
     hipEventCreate(&e0);
     hipEventCreate(&e1);
     bench<PkMaxI16>(out, e0, e1, cus);
+    bench<PkAddU16>(out, e0, e1, cus);
+    bench<SubU32>(out, e0, e1, cus);
+    bench<AndB32>(out, e0, e1, cus);
+    bench<LshlB32>(out, e0, e1, cus);
+    bench<MinU32>(out, e0, e1, cus);
+    bench<MaxU32>(out, e0, e1, cus);
+    bench<MaxI16>(out, e0, e1, cus);
+    bench<SubU16>(out, e0, e1, cus);
+    bench<LshlOr>(out, e0, e1, cus);
+    bench<Or3>(out, e0, e1, cus);
+    bench<Xad>(out, e0, e1, cus);
+    bench<MadU64>(out, e0, e1, cus);
+    bench<MovDpp>(out, e0, e1, cus);
     bench<PkSubI16>(out, e0, e1, cus);
     bench<PkMinU16>(out, e0, e1, cus);
     bench<MaxI32>(out, e0, e1, cus);
