@@ -421,7 +421,8 @@ int saln_nw_execute(saln_nw_plan *p, const uint8_t *d_q, const uint8_t *d_db,
                     HIP_TRY(hipMemsetAsync(p->d_prog + g0, 0, (g1 - g0) * sizeof(uint32_t), s));
                     HIP_TRY(launch_fill_stripes(p->d_pairs, p->d_work + w0, w1 - w0, d_q, d_db,
                                                 mask, p->d_scratch, p->d_prog, p->d_err, endh,
-                                                p->sc, !p->score_only, s));
+                                                p->sc,
+                                                p->score_only ? 2 : p->full_codes ? 1 : 0, s));
                 }
             } else if (a < b)
                 HIP_TRY(launch_fill(v, p->d_pairs, a, b - a, d_q, d_db, mask, p->d_scratch, endh,

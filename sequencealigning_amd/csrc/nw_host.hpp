@@ -26,7 +26,8 @@ hipError_t launch_fill(int variant, const NwPairDesc *pairs, uint32_t first, uin
 hipError_t launch_fill_stripes(const NwPairDesc *pairs, const uint2 *work, uint32_t n_work,
                                const uint8_t *qs, const uint8_t *ds, uint8_t *mask,
                                int2 *scratch, uint32_t *prog, uint32_t *err, int32_t *end_h,
-                               Scoring sc, bool codes, hipStream_t stream);
+                               Scoring sc, int codes /* 0 walk, 1 full, 2 none */,
+                               hipStream_t stream);
 constexpr int kStripeVariant = 3;
 hipError_t launch_score_results(const NwPairDesc *pairs, uint32_t first, uint32_t n,
                                 const int32_t *end_h, saln_nw_result *results, Scoring sc,

@@ -561,6 +561,184 @@ __global__ __launch_bounds__(256) void nw_traceback_kernel(
               ds, mask, geo, results, cigar, sc);
 }
 
+// ------------------------------------------- long pairs: cooperative walker
+// One wave per pair (column-stripe pairs, K = 4).  The same greedy walk as
+// walk_pair, but a step run is resolved by the whole wave at once: in state
+// M lane l looks at the l-th diagonal step (eq bit of cell (i-l, j-l), next
+// state from the argmax bits of (i-l-1, j-l-1)); in I / D lane l looks at the
+// l-th extend step.  A ballot of "the run ends after my step" gives the run
+// length, so a 64-step stretch of the path costs one round of LDS reads
+// instead of 64 dependent ones.  The codes come from an LDS window of
+// kCoopRows rows x kCoopBlk blocks of the mask, anchored at the current cell
+// and reloaded (LDS-DMA) when a run would leave it.  CIGAR words are emitted
+// back to front (uniform scalar run-length state) and reversed at the end.
+constexpr int32_t kCoopRows = 256, kCoopBlk = 64;
+
+__global__ __launch_bounds__(64) void nw_traceback_coop_kernel(
+    const NwPairDesc *__restrict__ pairs, uint32_t first, const uint8_t *__restrict__ mask,
+    const int32_t *__restrict__ end_h, saln_nw_result *__restrict__ results,
+    uint32_t *__restrict__ cigar, Scoring sc) {
+    constexpr int32_t kRowB = kCoopBlk * 4;  // LDS bytes per window row
+    __shared__ __attribute__((aligned(16))) uint8_t win[kCoopRows * kRowB];
+    const int32_t lane = (int32_t)threadIdx.x;
+    const uint32_t idx = first + blockIdx.x;
+    const NwPairDesc p = pairs[idx];
+    const int32_t hend = end_h[idx];
+    const int32_t lq = (int32_t)p.len_q, ld = (int32_t)p.len_db;
+    const uint8_t *__restrict__ m = mask + p.mask_off;
+    const uint64_t rs = p.mask_rs;
+    const uint32_t bs = p.mask_bs;
+    int32_t r_lo = 1, c_lo = 1;  // window: rows [r_lo, r_lo+255], columns [c_lo, c_lo+255]
+    // Rows [max(1, i-255), i] and the 64 blocks ending at the block of column
+    // j (a stripe pair's mask rows hold whole 256-column stripes, so all 64
+    // exist).  Rows past i repeat row i (never read).
+    auto load = [&](int32_t i, int32_t j) __attribute__((always_inline)) {
+        r_lo = max(1, i - kCoopRows + 1);
+        const int32_t bj = (j - 1) / 4;
+        const int32_t b_lo = max(0, bj - kCoopBlk + 1);
+        c_lo = 4 * b_lo + 1;
+        const int32_t nrows = i - r_lo + 1;
+        const uint8_t *mb = m + (uint64_t)b_lo * bs;
+        typedef __attribute__((address_space(3))) void lds_v;
+        if (bs == 4) {  // rows contiguous: 16 bytes (4 blocks) per lane, 4 rows per DMA
+            const int32_t sub = lane / 16, ch = lane % 16;
+            for (int32_t mm = 0; mm < (nrows + 3) / 4; ++mm) {
+                const int32_t rr = min(4 * mm + sub, nrows - 1);
+                __builtin_amdgcn_global_load_lds(mb + (uint64_t)(r_lo + rr - 1) * rs + 16 * ch,
+                                                 (lds_v *)(win + 4 * mm * kRowB), 16, 0, 0);
+            }
+        } else {  // one block per lane, one row per DMA
+            for (int32_t mm = 0; mm < nrows; ++mm)
+                __builtin_amdgcn_global_load_lds(mb + (uint64_t)(r_lo + mm - 1) * rs + (uint64_t)lane * bs,
+                                                 (lds_v *)(win + mm * kRowB), 4, 0, 0);
+        }
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the window has landed
+        __builtin_amdgcn_wave_barrier();
+    };
+    // code byte of interior cell (r, c) inside the window, bits 0-6 present-sets
+    auto code = [&](int32_t r, int32_t c) __attribute__((always_inline)) {
+        return (uint32_t)win[(r - r_lo) * kRowB + (c - c_lo)] ^ 0x7Fu;
+    };
+    int32_t i = ld, j = lq;
+    load(i, j);
+    const uint32_t am_end = code(i, j) & 7u;
+    int32_t st = (am_end & kArgD) ? kStD : ((am_end & kArgM) ? kStM : kStI);
+    uint32_t *out = cigar ? cigar + p.cigar_off : nullptr;
+    uint32_t nops = 0, run_op = 0, run_len = 0;
+    auto push = [&](uint32_t op, uint32_t len) __attribute__((always_inline)) {
+        if (run_len && run_op == op) {
+            run_len += len;
+        } else {
+            if (run_len) {
+                if (lane == 0 && out) out[nops] = (run_len << 4) | run_op;
+                ++nops;
+            }
+            run_op = op;
+            run_len = len;
+        }
+    };
+    int ev;
+    for (;;) {
+        if (st == kStM) {
+            if (i == 0 && j == 0) { ev = kEvOrigin; break; }
+            if (i == 0 || j == 0) { ev = kEvDead; break; }
+        } else if (st == kStI) {
+            if (j == 0) { ev = i >= 1 ? kEvPanic : kEvDead; break; }
+            if (i == 0) { ev = kEvDead; break; }
+        } else {
+            if (i == 0) { ev = j >= 1 ? kEvPanic : kEvDead; break; }
+            if (j == 0) { ev = kEvDead; break; }
+        }
+        // steps l whose reads stay in the window (row / column 0 come from
+        // the boundary formulas)
+        const int32_t lim_i = r_lo == 1 ? i - 1 : i - 1 - r_lo;
+        const int32_t lim_j = c_lo == 1 ? j - 1 : j - 1 - c_lo;
+        int32_t lmax = st == kStM ? min(lim_i, lim_j) : st == kStI ? lim_j : lim_i;
+        if (i < r_lo || j < c_lo || lmax < 0) {
+            load(i, j);
+            continue;
+        }
+        lmax = min(lmax, 63);
+        bool stop = true;
+        int32_t nxt = st;
+        uint32_t eq = 0;
+        if (lane <= lmax) {
+            if (st == kStM) {
+                const int32_t ni = i - lane - 1, nj = j - lane - 1;
+                eq = code(i - lane, j - lane) >> 7;
+                const uint32_t a = ni == 0 ? argmax_row0(sc, (uint32_t)nj)
+                                 : nj == 0 ? argmax_col0(sc, (uint32_t)ni)
+                                           : code(ni, nj) & 7u;
+                nxt = (a & kArgD) ? kStD : ((a & kArgI) ? kStI : kStM);
+                stop = nxt != kStM || ni == 0 || nj == 0;
+            } else if (st == kStI) {
+                const int32_t cj = j - lane;
+                const uint32_t b = cj == 1 ? ibits_col1(sc, (uint32_t)i) : (code(i, cj - 1) >> 3) & 3u;
+                nxt = (b & 2) ? kStM : kStI;
+                stop = nxt != kStI || cj == 1;
+            } else {
+                const int32_t ci = i - lane;
+                const uint32_t b = ci == 1 ? dbits_row1(sc, (uint32_t)j) : (code(ci - 1, j) >> 5) & 3u;
+                nxt = (b & 2) ? kStM : kStD;
+                stop = nxt != kStD || ci == 1;
+            }
+            stop = stop || lane == lmax;
+        }
+        const uint64_t sb = __builtin_amdgcn_ballot_w64(stop);
+        const int32_t L = __builtin_ctzll(sb);  // last step of this run (lane lmax always stops)
+        const uint32_t n = (uint32_t)L + 1;
+        if (st == kStM) {
+            const uint64_t lm = n >= 64 ? ~0ull : ((1ull << n) - 1);
+            const uint64_t e = __builtin_amdgcn_ballot_w64(eq != 0) & lm;
+            uint64_t bnd = (e ^ (e << 1)) & lm & ~1ull;  // lanes whose op differs from the previous
+            uint32_t cur = (e & 1) ? SALN_CIGAR_EQ : SALN_CIGAR_X;
+            int32_t s0 = 0;
+            while (bnd) {
+                const int32_t b = __builtin_ctzll(bnd);
+                push(cur, (uint32_t)(b - s0));
+                cur = cur == SALN_CIGAR_EQ ? SALN_CIGAR_X : SALN_CIGAR_EQ;
+                s0 = b;
+                bnd &= bnd - 1;
+            }
+            push(cur, n - (uint32_t)s0);
+            i -= (int32_t)n;
+            j -= (int32_t)n;
+        } else if (st == kStI) {
+            push(SALN_CIGAR_I, n);
+            j -= (int32_t)n;
+        } else {
+            push(SALN_CIGAR_D, n);
+            i -= (int32_t)n;
+        }
+        st = __builtin_amdgcn_readlane(nxt, L);
+    }
+    if (run_len) {
+        if (lane == 0 && out) out[nops] = (run_len << 4) | run_op;
+        ++nops;
+    }
+    if (ev != kEvOrigin) nops = 0;
+    if (out && nops > 1) {  // words were produced back to front
+        __builtin_amdgcn_s_waitcnt(0x0F70);
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+        for (uint32_t a = (uint32_t)lane; a < nops / 2; a += 64) {
+            const uint32_t x = out[a], y = out[nops - 1 - a];
+            out[a] = y;
+            out[nops - 1 - a] = x;
+        }
+    }
+    if (lane == 0) {
+        saln_nw_result r;
+        r.score = hend >> 1;
+        r.status = (hend & 1) ? SALN_REF_PANIC_BOUNDARY : SALN_OK;
+        r.cigar_len = nops;
+        r.end_states = (uint8_t)am_end;
+        r.printed = ev == kEvOrigin ? 1 : 0;
+        r.flags = (ev == kEvDead ? 1 : 0) | ((ev == kEvPanic && !(hend & 1)) ? 2 : 0);
+        r.reserved = 0;
+        results[p.pair_id] = r;
+    }
+}
+
 template <int K>
 struct MaskWords {
     uint32_t w[(K + 3) / 4];
@@ -690,157 +868,6 @@ __global__ __launch_bounds__(256) void nw_fill_kernel(const NwPairDesc *__restri
 // a bounded spin turns a lost dependency into an error flag instead of a hang.
 constexpr uint32_t kPub = 32;
 constexpr uint32_t kSpinCap = 1u << 24;
-
-template <int K, bool kCodes>
-__global__ __launch_bounds__(64) void nw_fill_stripe_kernel(
-    const NwPairDesc *__restrict__ pairs, const uint2 *__restrict__ work,
-    const uint8_t *__restrict__ qs, const uint8_t *__restrict__ ds, uint8_t *__restrict__ mask,
-    int2 *__restrict__ scratch, uint32_t *__restrict__ prog, uint32_t *__restrict__ err,
-    int32_t *__restrict__ end_h, Scoring sc) {
-    constexpr int G = 64;
-    constexpr int KD = (K + 3) / 4;
-    constexpr Geom geo{G, K};
-    const int lane = threadIdx.x;
-    const uint2 wk = work[blockIdx.x];
-    const NwPairDesc p = pairs[wk.x];
-    const uint32_t c = wk.y;
-    const uint32_t lq = p.len_q, ld = p.len_db;
-    const uint8_t *__restrict__ q = qs + p.q_off;
-    const uint8_t *__restrict__ d = ds + p.db_off;
-    const uint32_t nch = geo.n_chunks(lq);
-    const int2 *__restrict__ scr_in = c > 0 ? scratch + p.scratch_off + (uint64_t)(c - 1) * (ld + 2) : nullptr;
-    int2 *__restrict__ scr_out = c + 1 < nch ? scratch + p.scratch_off + (uint64_t)c * (ld + 2) : nullptr;
-    uint32_t *prog_in = c > 0 ? prog + p.reserved + c - 1 : nullptr;
-    uint32_t *prog_out = prog + p.reserved + c;
-    const int32_t sM = 2 * sc.match, sX = 2 * sc.mismatch;
-    const int32_t sO = 2 * sc.gap_open, sE = 2 * sc.gap_extend;
-    const uint32_t jend = lq - 1;
-    const bool end_lane = jend / geo.W() == c && (uint32_t)lane == (jend % geo.W()) / K;
-    const uint32_t k_end = jend % K;
-
-    const uint32_t col0 = c * geo.W() + (uint32_t)lane * K;  // my columns: col0+1 .. col0+K
-    int32_t qc[K], Hp[K], Dn[K];
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-        const uint32_t j = col0 + k + 1;
-        qc[k] = j <= lq ? (int32_t)q[j - 1] : -1;
-        Hp[k] = hs_row0(sc, j);
-        Dn[k] = ds_row1(sc, j);
-    }
-    int32_t hd = hs_row0(sc, col0);
-    int32_t pubF = 0, pubH = 0;
-    // db chars: lane 0 needs d[t] at step t; it is wave-uniform, so it comes
-    // through a scalar load (lgkmcnt: no wait on the mask stores' vmcnt), and
-    // the other lanes take their row's char from their left neighbour's
-    // previous step (DPP).
-    typedef const __attribute__((address_space(4))) uint32_t cu32;  // constant: scalar loads
-    cu32 *dw = (cu32 *)((uintptr_t)d & ~(uintptr_t)3);
-    const uint32_t dsh = (uint32_t)((uintptr_t)d & 3);
-    int32_t dch = 0;
-    int32_t blkH = 0, blkF = 0;  // lanes 0..31: the left column of the current 32-row block
-    uint32_t avail = 0;          // rows of the left column known to be published
-    bool failed = false;
-    uint8_t *mseg = mask + p.mask_off + (uint64_t)(c * G + (uint32_t)lane) * p.mask_bs;
-    const int T = (int)geo.steps(ld);
-    // the query chars above arrive here: otherwise the wait for them lands
-    // inside the loop, where it would also wait for every mask store
-    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
-    for (int t = 0; t < T; ++t) {
-        const int r = t - lane + 1;
-        {
-            const uint32_t j = (uint32_t)min(t, (int)ld - 1) + dsh;
-            const uint32_t w = __builtin_amdgcn_readfirstlane(dw[j >> 2]);
-            dch = shr1<G>((int32_t)((w >> (8 * (j & 3))) & 0xFFu), dch);  // d[r-1]
-        }
-        int32_t bF, bH;
-        const uint32_t rr = (uint32_t)t + 1;  // lane 0's row
-        if (c == 0) {
-            bF = is_col1(sc, rr);
-            bH = hs_col0(sc, rr);
-        } else {
-            if ((rr - 1) % kPub == 0 && rr <= ld) {  // new 32-row block of the left column
-                const uint32_t need = min(rr - 1 + kPub, ld);
-                uint32_t spins = 0;
-                while (avail < need && !failed) {
-                    avail = __hip_atomic_load(prog_in, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    avail = __builtin_amdgcn_readfirstlane(avail);
-                    if (avail < need) {
-                        __builtin_amdgcn_s_sleep(2);
-                        if (++spins > kSpinCap) failed = true;
-                    }
-                }
-                const uint32_t row = rr + (uint32_t)lane;
-                if (lane < (int)kPub && row <= ld) {
-                    const uint64_t v = __hip_atomic_load((const uint64_t *)(scr_in + row),
-                                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    blkH = (int32_t)(uint32_t)v;
-                    blkF = (int32_t)(uint32_t)(v >> 32);
-                }
-            }
-            const uint32_t sl = (rr - 1) % kPub;
-            bH = __builtin_amdgcn_readlane(blkH, sl);
-            bF = __builtin_amdgcn_readlane(blkF, sl);
-        }
-        const int32_t inF = shr1<G>(bF, pubF);
-        const int32_t inH = shr1<G>(bH, pubH);
-        if (r >= 1 && r <= (int)ld) {
-            int32_t F = inF;
-            MaskWords<K> mw;
-#pragma unroll
-            for (int k = 0; k < KD; ++k) mw.w[k] = 0;
-#pragma unroll
-            for (int k = 0; k < K; ++k) {
-                const bool eq = qc[k] == dch;
-                const int32_t M = hd + (eq ? sM : sX);
-                const int32_t I = F, D = Dn[k];
-                const int32_t H = max(M, max(I, D));
-                const int32_t Hc = H & ~1;
-                const int32_t tO = M + sO;
-                if constexpr (kCodes) {
-                    uint32_t b = (M >= Hc ? kArgM : 0u) | (I >= Hc ? kArgI : 0u) |
-                                 (D >= Hc ? kArgD : 0u);
-                    b |= ((I | 1) >= tO ? kIExt : 0u) | ((tO | 1) >= I ? kIOpen : 0u);
-                    b |= ((D | 1) >= tO ? kDExt : 0u) | ((tO | 1) >= D ? kDOpen : 0u);
-                    b |= eq ? 0x80u : 0u;
-                    mw.w[k / 4] |= b << (8 * (k % 4));
-                }
-                (void)Hc;
-                F = max(tO, I) + sE;
-                Dn[k] = max(tO, D) + sE;
-                hd = Hp[k];
-                Hp[k] = H;
-            }
-            hd = inH;
-            pubF = F;
-            pubH = Hp[K - 1];
-            if constexpr (kCodes) {
-#pragma unroll
-                for (int k = 0; k < KD; ++k) mw.w[k] ^= 0x7F7F7F7Fu;
-                *reinterpret_cast<MaskWords<K> *>(mseg + (uint64_t)(r - 1) * p.mask_rs) = mw;
-            }
-            if (lane == G - 1 && scr_out) {
-                // agent-coherent (write-through) stores: the publication below
-                // needs only these to be complete, not an L2 write-back
-                __hip_atomic_store((uint64_t *)(scr_out + r),
-                                   (uint64_t)(uint32_t)pubH | ((uint64_t)(uint32_t)pubF << 32),
-                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if ((uint32_t)r % kPub == 0 || (uint32_t)r == ld) {
-                    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): column stores done
-                    __hip_atomic_store(prog_out, (uint32_t)r, __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_AGENT);
-                }
-            }
-            if (end_lane && r == (int)ld) {
-                int32_t e = 0;
-#pragma unroll
-                for (int k = 0; k < K; ++k)
-                    if ((uint32_t)k == k_end) e = Hp[k];
-                end_h[wk.x] = e;
-            }
-        }
-    }
-    if (failed && lane == 0) atomicOr(err, 1u);
-}
 
 // ------------------------------------------------------- packed-i16 fill
 // Two pairs per lane group: pair A in the low 16 bits of every register,
@@ -1216,6 +1243,203 @@ __global__ __launch_bounds__(256) void nw_fill_pk_kernel(Src src, uint32_t count
 #endif
 }
 
+// Column-stripe fill (declared with the stripe protocol above), i32 lanes.
+// Representation: X~(r,c) = X'(r,c) + alpha*r + beta*c as in the packed
+// fill (beta = -2*gap_extend, alpha = -2*match - beta): M~ = H~(r-1,c-1) -
+// pen*[q != d], I~(r,c+1) = max(M~ + 2*gap_open, I~), D~(r+1,c) = max(M~ +
+// 2*gap_open, D~) + 2*gap_extend + alpha.  i32 carries the reference's
+// literal -32768 sentinel exactly (the boundary functions apply it; the
+// offsets are linear, so no value is clamped anywhere).
+// Parent codes from sign bits of same-cell differences (sign set <=> parent
+// absent, flag-free comparisons as in the packed fill); per source, two
+// v_perm gather the bit-31 signs of the four columns into 0x00/0xFF bytes and
+// a v_bfi chain merges the sources.
+template <int kCodes>
+__device__ __forceinline__ uint32_t stripe_code_word(const uint32_t (&s)[8][4]) {
+    uint32_t w[8];
+#pragma unroll
+    for (int t = 0; t < 8; ++t)
+        w[t] = __builtin_amdgcn_perm(s[t][1], s[t][0], 0x0C0C0B09u) |
+               __builtin_amdgcn_perm(s[t][3], s[t][2], 0x0B090C0Cu);
+    if constexpr (kCodes == kCodesFull) return merge_full(w);
+    return merge_walk<true>(w);
+}
+
+template <int K, int kCodes, bool kMinPen>
+__global__ __launch_bounds__(64) void nw_fill_stripe_kernel(
+    const NwPairDesc *__restrict__ pairs, const uint2 *__restrict__ work,
+    const uint8_t *__restrict__ qs, const uint8_t *__restrict__ ds, uint8_t *__restrict__ mask,
+    int2 *__restrict__ scratch, uint32_t *__restrict__ prog, uint32_t *__restrict__ err,
+    int32_t *__restrict__ end_h, Scoring sc) {
+    static_assert(K == 4, "one code dword per lane and row");
+    constexpr int G = 64;
+    constexpr Geom geo{G, K};
+    const int lane = threadIdx.x;
+    const uint2 wk = work[blockIdx.x];
+    const NwPairDesc p = pairs[wk.x];
+    const uint32_t c = wk.y;
+    const uint32_t lq = p.len_q, ld = p.len_db;
+    const uint8_t *__restrict__ q = qs + p.q_off;
+    const uint8_t *__restrict__ d = ds + p.db_off;
+    const uint32_t nch = geo.n_chunks(lq);
+    const int2 *__restrict__ scr_in = c > 0 ? scratch + p.scratch_off + (uint64_t)(c - 1) * (ld + 2) : nullptr;
+    int2 *__restrict__ scr_out = c + 1 < nch ? scratch + p.scratch_off + (uint64_t)c * (ld + 2) : nullptr;
+    uint32_t *prog_in = c > 0 ? prog + p.reserved + c - 1 : nullptr;
+    uint32_t *prog_out = prog + p.reserved + c;
+    const int32_t beta = -2 * sc.gap_extend;
+    const int32_t alpha = -2 * sc.match - beta;
+    const int32_t pen_max = 2 * (sc.match - sc.mismatch);
+    // chars carried as c << 8: q ^ d is 0 or >= 256, so min() is the penalty
+    // whenever 0 <= pen_max <= 256 (kMinPen); otherwise a select
+    const int32_t kOpen = 2 * sc.gap_open;
+    const int32_t kDstep = 2 * sc.gap_extend + alpha;
+    const uint32_t jend = lq - 1;
+    const bool end_lane = jend / geo.W() == c && (uint32_t)lane == (jend % geo.W()) / K;
+    const uint32_t k_end = jend % K;
+
+    const uint32_t col0 = c * geo.W() + (uint32_t)lane * K;  // my columns: col0+1 .. col0+K
+    uint32_t qc[K];
+    int32_t Hp[K], Dn[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const uint32_t j = col0 + k + 1;
+        qc[k] = j <= lq ? (uint32_t)q[j - 1] << 8 : 0xFFFFFF00u;
+        Hp[k] = hs_row0(sc, j) + beta * (int32_t)j;
+        Dn[k] = ds_row1(sc, j) + alpha + beta * (int32_t)j;
+    }
+    int32_t hd = hs_row0(sc, col0) + beta * (int32_t)col0;
+    int32_t pubF = 0, pubH = 0;
+    // db chars: lane 0 needs d[t] at step t (wave-uniform): 16-byte scalar
+    // loads, prefetched one block ahead so their wait never stalls a step;
+    // the other lanes take their row's char from the left neighbour's
+    // previous step (DPP).
+    typedef const __attribute__((address_space(4))) uint32_t cu32;  // constant: scalar loads
+    auto ld16 = [](uintptr_t a) {
+        const cu32 *w = (const cu32 *)a;
+        return make_uint4(w[0], w[1], w[2], w[3]);
+    };
+    const uintptr_t dbase = (uintptr_t)d & ~(uintptr_t)15;
+    const uint32_t dsh = (uint32_t)((uintptr_t)d & 15);
+    const uint32_t nblk = (ld + dsh + 15) / 16;  // 16-byte blocks holding d[0 .. ld)
+    uint4 dcur = ld16(dbase), dnxt = dcur;
+    if (nblk > 1) dnxt = ld16(dbase + 16);
+    uint32_t dch = 0;
+    int32_t blkH = 0, blkF = 0;  // lanes 0..31: the left column of the current 32-row block
+    uint32_t avail = 0;          // rows of the left column known to be published
+    bool failed = false;
+    uint8_t *mseg = mask + p.mask_off + (uint64_t)(c * G + (uint32_t)lane) * p.mask_bs -
+                    (int64_t)lane * (int64_t)p.mask_rs;  // row r-1 = t - lane at step 0
+    const int T = (int)geo.steps(ld);
+    // the query chars above arrive here: otherwise the wait for them lands
+    // inside the loop, where it would also wait for every mask store
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+    for (int t = 0; t < T; ++t) {
+        const int r = t - lane + 1;
+        {
+            const uint32_t j = (uint32_t)min(t, (int)ld - 1) + dsh;  // byte of d[t] from dbase
+            if ((j & 15) == 0 && j > 0 && t < (int)ld) {  // next 16-byte block
+                dcur = dnxt;
+                const uint32_t nb = (j >> 4) + 1;
+                if (nb < nblk) dnxt = ld16(dbase + 16 * nb);
+            }
+            const uint32_t wsel = (j >> 2) & 3;
+            const uint32_t w = wsel == 0 ? dcur.x : wsel == 1 ? dcur.y : wsel == 2 ? dcur.z : dcur.w;
+            dch = (uint32_t)shr1<G>((int32_t)(((w >> (8 * (j & 3))) & 0xFFu) << 8), (int32_t)dch);
+        }
+        int32_t bF, bH;
+        const uint32_t rr = (uint32_t)t + 1;  // lane 0's row
+        if (c == 0) {
+            bF = is_col1(sc, rr) + alpha * (int32_t)rr + beta;
+            bH = hs_col0(sc, rr) + alpha * (int32_t)rr;
+        } else {
+            if ((rr - 1) % kPub == 0 && rr <= ld) {  // new 32-row block of the left column
+                const uint32_t need = min(rr - 1 + kPub, ld);
+                uint32_t spins = 0;
+                while (avail < need && !failed) {
+                    avail = __hip_atomic_load(prog_in, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    avail = __builtin_amdgcn_readfirstlane(avail);
+                    if (avail < need) {
+                        __builtin_amdgcn_s_sleep(2);
+                        if (++spins > kSpinCap) failed = true;
+                    }
+                }
+                const uint32_t row = rr + (uint32_t)lane;
+                if (lane < (int)kPub && row <= ld) {
+                    const uint64_t v = __hip_atomic_load((const uint64_t *)(scr_in + row),
+                                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    blkH = (int32_t)(uint32_t)v;
+                    blkF = (int32_t)(uint32_t)(v >> 32);
+                }
+            }
+            const uint32_t sl = (rr - 1) % kPub;
+            bH = __builtin_amdgcn_readlane(blkH, sl);
+            bF = __builtin_amdgcn_readlane(blkF, sl);
+        }
+        const int32_t inF = shr1<G>(bF, pubF);
+        const int32_t inH = shr1<G>(bH, pubH);
+        if (r >= 1 && r <= (int)ld) {
+            int32_t F = inF;
+            uint32_t sg[8][4];
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                const uint32_t x = qc[k] ^ dch;
+                const int32_t pen = kMinPen ? (int32_t)min(x, (uint32_t)pen_max) : (x ? pen_max : 0);
+                const int32_t M = hd - pen;
+                const int32_t I = F, D = Dn[k];
+                const int32_t H = max(M, max(I, D));
+                const int32_t tO = M + kOpen;
+                if constexpr (kCodes != kCodesNone) {
+                    const int32_t Hc = H & ~1;
+                    const int32_t tOr = tO | 1;
+                    sg[0][k] = (uint32_t)(M - Hc);
+                    sg[1][k] = (uint32_t)(I - Hc);
+                    sg[2][k] = (uint32_t)(D - Hc);
+                    sg[4][k] = (uint32_t)(tOr - I);
+                    sg[6][k] = (uint32_t)(tOr - D);
+                    sg[7][k] = x - 1u;  // sign <=> q == d
+                    if constexpr (kCodes == kCodesFull) {
+                        const int32_t tOc = tO & ~1;
+                        sg[3][k] = (uint32_t)(I - tOc);
+                        sg[5][k] = (uint32_t)(D - tOc);
+                    } else {
+                        sg[3][k] = sg[5][k] = 0u;
+                    }
+                }
+                F = max(tO, I);
+                Dn[k] = max(tO, D) + kDstep;
+                hd = Hp[k];
+                Hp[k] = H;
+            }
+            hd = inH;
+            pubF = F;
+            pubH = Hp[K - 1];
+            if constexpr (kCodes != kCodesNone)
+                *reinterpret_cast<uint32_t *>(mseg) = stripe_code_word<kCodes>(sg);
+            if (lane == G - 1 && scr_out) {
+                // agent-coherent (write-through) stores: the publication below
+                // needs only these to be complete, not an L2 write-back
+                __hip_atomic_store((uint64_t *)(scr_out + r),
+                                   (uint64_t)(uint32_t)pubH | ((uint64_t)(uint32_t)pubF << 32),
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if ((uint32_t)r % kPub == 0 || (uint32_t)r == ld) {
+                    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): column stores done
+                    __hip_atomic_store(prog_out, (uint32_t)r, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+                }
+            }
+            if (end_lane && r == (int)ld) {
+                int32_t e = 0;
+#pragma unroll
+                for (int k = 0; k < K; ++k)
+                    if ((uint32_t)k == k_end) e = Hp[k];
+                end_h[wk.x] = e - alpha * (int32_t)ld - beta * (int32_t)lq;
+            }
+        }
+        mseg += p.mask_rs;
+    }
+    if (failed && lane == 0) atomicOr(err, 1u);
+}
+
 // Score-only results (saln_nw_plan_set_score_only): score and panic status
 // from the end value; no traceback fields (flags bit 3).
 __global__ __launch_bounds__(256) void nw_score_results_kernel(const NwPairDesc *__restrict__ pairs,
@@ -1403,7 +1627,10 @@ hipError_t launch_traceback(int variant, const NwPairDesc *pairs, uint32_t first
         case 0: tb_lds<16, 10>(grid, stream, pairs, first, n, mask, end_h, ops, results, cigar, sc); break;
         case 1: tb_lds<16, 16>(grid, stream, pairs, first, n, mask, end_h, ops, results, cigar, sc); break;
         case 2: tb_lds<64, 8>(grid, stream, pairs, first, n, mask, end_h, ops, results, cigar, sc); break;
-        case 3: tb_lds<64, 4>(grid, stream, pairs, first, n, mask, end_h, ops, results, cigar, sc); break;
+        case 3:  // column-stripe pairs: one cooperative wave per pair
+            nw_traceback_coop_kernel<<<dim3(n), dim3(64), 0, stream>>>(pairs, first, mask, end_h,
+                                                                      results, cigar, sc);
+            break;
         case 5: tb_lds<16, 16>(grid, stream, pairs, first, n, mask, end_h, ops, results, cigar, sc); break;
         case 6: tb_lds<32, 16>(grid, stream, pairs, first, n, mask, end_h, ops, results, cigar, sc); break;
         case 7: tb_lds<16, 10>(grid, stream, pairs, first, n, mask, end_h, ops, results, cigar, sc); break;
@@ -1420,14 +1647,21 @@ hipError_t launch_traceback(int variant, const NwPairDesc *pairs, uint32_t first
 hipError_t launch_fill_stripes(const NwPairDesc *pairs, const uint2 *work, uint32_t n_work,
                                const uint8_t *qs, const uint8_t *ds, uint8_t *mask,
                                int2 *scratch, uint32_t *prog, uint32_t *err, int32_t *end_h,
-                               Scoring sc, bool codes, hipStream_t stream) {
+                               Scoring sc, int codes, hipStream_t stream) {
     if (!n_work) return hipSuccess;
-    if (codes)
-        nw_fill_stripe_kernel<4, true><<<dim3(n_work), dim3(64), 0, stream>>>(
-            pairs, work, qs, ds, mask, scratch, prog, err, end_h, sc);
-    else
-        nw_fill_stripe_kernel<4, false><<<dim3(n_work), dim3(64), 0, stream>>>(
-            pairs, work, qs, ds, mask, scratch, prog, err, end_h, sc);
+    const dim3 grid(n_work), block(64);
+    const int32_t pen_max = 2 * (sc.match - sc.mismatch);
+    auto go = [&](auto codes_c, auto minpen_c) {
+        nw_fill_stripe_kernel<4, decltype(codes_c)::value, decltype(minpen_c)::value>
+            <<<grid, block, 0, stream>>>(pairs, work, qs, ds, mask, scratch, prog, err, end_h, sc);
+    };
+    auto by_codes = [&](auto minpen_c) {
+        if (codes == kCodesFull) go(std::integral_constant<int, kCodesFull>{}, minpen_c);
+        else if (codes == kCodesNone) go(std::integral_constant<int, kCodesNone>{}, minpen_c);
+        else go(std::integral_constant<int, kCodesWalk>{}, minpen_c);
+    };
+    if (pen_max >= 0 && pen_max <= 256) by_codes(std::true_type{});
+    else by_codes(std::false_type{});
     return hipGetLastError();
 }
 

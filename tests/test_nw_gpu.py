@@ -279,3 +279,41 @@ def test_very_long_pair_linear_oracle(saln, oracle, shape):
     if r.printed and not r.panics:
         s, ok = path_score(q, d, r.cigar)
         assert ok and s == r.score
+
+
+@pytest.mark.parametrize("packed", [False, True])
+def test_long_pairs_cooperative_walker(saln, oracle, packed):
+    """Column-stripe pairs (> 512 query columns) take the cooperative
+    traceback (one wave per pair, run-skipping over an LDS window of the
+    mask): a batch of mutated, i.i.d. and tie-heavy long pairs, alone or
+    sharing an interleaved mask pack, gives the oracle's score, end states,
+    status and first printed alignment."""
+    from sequencealigning_amd import synth
+    rng = np.random.default_rng(4242)
+    qs, ds = [], []
+    shapes = [(600, 590), (1300, 1280), (800, 1100), (1500, 700), (520, 530), (2000, 1900)]
+    for k, (lq, ld) in enumerate(shapes):
+        if k % 3 == 0:
+            q = synth.random_bases(100 + k, lq).tobytes()
+            d = synth.mutate(q, 0.05, seed=200 + k)[:ld]
+        elif k % 3 == 1:
+            q = synth.random_bases(100 + k, lq).tobytes()
+            d = synth.random_bases(300 + k, ld).tobytes()
+        else:  # two-letter alphabet: many co-optimal parents
+            q = bytes(rng.choice([65, 67], lq).astype(np.uint8))
+            d = bytes(rng.choice([65, 67], ld).astype(np.uint8))
+        qs.append(q)
+        ds.append(d)
+    if packed:
+        res, cig = saln.nw_align_batch(qs, ds, pairs=[(k, k) for k in range(len(qs))])
+        got = [(int(res["score"][k]), int(res["end_states"][k]), int(res["status"][k]) == 2,
+                saln.cigar_ops_string(cig[k]) if res["printed"][k] else None) for k in range(len(qs))]
+    else:
+        got = []
+        for q, d in zip(qs, ds):
+            r = saln.n_w_align(q, d)
+            got.append((r.score, r.end_states, r.panics, expand(r.cigar) if r.printed else None))
+    for k, (q, d) in enumerate(zip(qs, ds)):
+        o = oracle.nw(q, d, literal_dfs=False)
+        assert got[k][:3] == (o.score, o.end_states, o.panics), k
+        assert got[k][3] == o.first_ops, k
