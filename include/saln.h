@@ -252,6 +252,41 @@ int saln_wfa_execute(saln_wfa_plan *plan, const uint8_t *d_q_seq, const uint8_t 
                      saln_wfa_result *d_results, void *stream);
 int saln_wfa_plan_destroy(saln_wfa_plan *plan);
 
+/* ------------------------------------------- corrected gap-affine WFA (new)
+ * NOT a reference-parity path.  The reference's
+ * wfa_align (src/wfa.rs:23-42, above) defines no output for realistic inputs
+ * (Ocean::trim panics at s = 20).  These entry points compute
+ * what a gap-affine WFA is meant to: the minimum penalty of a global
+ * alignment, mismatch * #mismatches + sum(gap_open + gap_extend * len) over
+ * gaps, with the reference's penalties (wfa.rs:14-21) by default.  The
+ * checker is the Gotoh DP (oracle/refaffine.c).
+ * scores[p] >= 0: the penalty; -1: above max_score (max_score <= 0: no cap);
+ * -2: the wavefront grew past 2,048 diagonals (i16 offsets; 1,024 for a
+ * sequence longer than 32,000 bases). */
+typedef struct {
+    int32_t mismatch;   /* x = 4 */
+    int32_t gap_open;   /* o = 2 */
+    int32_t gap_extend; /* e = 6 */
+} saln_wfa_penalties;   /* NULL = the reference's {4, 2, 6} */
+
+int saln_wfa_affine_batch(saln_context *ctx, const uint8_t *q_seq, const uint64_t *q_off,
+                          uint64_t n_q, const uint8_t *db_seq, const uint64_t *db_off,
+                          uint64_t n_db, const uint32_t *pair_q, const uint32_t *pair_db,
+                          uint64_t n_pairs, const saln_wfa_penalties *pen, int32_t max_score,
+                          int32_t *scores);
+/* Device-resident form (configs[2] measurement with the corrected engine):
+ * plan from host offsets and a pair list (NULL = all-vs-all, reference
+ * order), execute on device sequences into device scores[n_pairs]. */
+typedef struct saln_wfa_affine_plan saln_wfa_affine_plan;
+int saln_wfa_affine_plan_create(saln_context *ctx, const uint64_t *q_off, uint64_t n_q,
+                                const uint64_t *db_off, uint64_t n_db, const uint32_t *pair_q,
+                                const uint32_t *pair_db, uint64_t n_pairs,
+                                const saln_wfa_penalties *pen, int32_t max_score,
+                                saln_wfa_affine_plan **out);
+int saln_wfa_affine_execute(saln_wfa_affine_plan *plan, const uint8_t *d_q_seq,
+                            const uint8_t *d_db_seq, int32_t *d_scores, void *stream);
+int saln_wfa_affine_plan_destroy(saln_wfa_affine_plan *plan);
+
 /* --------------------------------------------------------------------- FASTA
  * Replaces `pub fn parse_fasta(path: PathBuf) -> Result<Records>`
  * (parse.rs:54-99): extension must be exactly fa|fasta|fna; '>' opens a record

@@ -60,6 +60,13 @@ def lib():
                                       C.POINTER(C.c_size_t)]
         L.ref_parse_fasta.restype = C.c_int64
         i32p = C.POINTER(C.c_int32)
+        L.ref_affine_penalty.argtypes = [u8p, C.c_size_t, u8p, C.c_size_t, C.c_int32, C.c_int32,
+                                         C.c_int32]
+        L.ref_affine_penalty.restype = C.c_int64
+        L.ref_affine_run_pairs.argtypes = [u8p, C.POINTER(C.c_uint64), u8p, C.POINTER(C.c_uint64),
+                                           C.POINTER(C.c_uint32), C.POINTER(C.c_uint32),
+                                           C.c_uint64, C.c_int32, C.c_int32, C.c_int32, C.c_int,
+                                           C.POINTER(C.c_int64)]
         L.ref_wfa_align.argtypes = [u8p, C.c_size_t, u8p, C.c_size_t, C.c_int, C.c_uint64,
                                     C.c_void_p, C.c_char_p, C.c_size_t, C.POINTER(C.c_size_t)]
         L.ref_wfa_tensor_new.argtypes = [i32p, i32p, i32p, i32p, C.c_char_p, C.c_size_t]
@@ -260,3 +267,27 @@ def wfa_tensor_new(o=None, e=None, x=None):
 def wfa_initial_converged(query: bytes, db: bytes) -> bool:
     """Ocean::global().is_converged(query, db) (test_converge, wfa.rs:1289-1294)."""
     return bool(lib().ref_wfa_initial_converged(_u8(query), len(query), _u8(db), len(db)))
+
+
+def affine_penalty(query: bytes, db: bytes, x: int = 4, o: int = 2, e: int = 6) -> int:
+    """Minimum gap-affine penalty of a global alignment (oracle/refaffine.c):
+    the value the corrected gap-affine WFA computes."""
+    return int(lib().ref_affine_penalty(_u8(query), len(query), _u8(db), len(db), x, o, e))
+
+
+def affine_run_pairs(qs: np.ndarray, q_off: np.ndarray, ds: np.ndarray, d_off: np.ndarray,
+                     pair_q: np.ndarray, pair_d: np.ndarray, x: int = 4, o: int = 2, e: int = 6,
+                     threads: int = 1) -> np.ndarray:
+    """affine_penalty over (query, db) index pairs on `threads` threads."""
+    qs = np.ascontiguousarray(qs, np.uint8)
+    ds = np.ascontiguousarray(ds, np.uint8)
+    qo = np.ascontiguousarray(q_off, np.uint64)
+    do = np.ascontiguousarray(d_off, np.uint64)
+    pq = np.ascontiguousarray(pair_q, np.uint32)
+    pd = np.ascontiguousarray(pair_d, np.uint32)
+    out = np.zeros(len(pq), np.int64)
+    P = lambda a, t: a.ctypes.data_as(C.POINTER(t))  # noqa: E731
+    lib().ref_affine_run_pairs(P(qs, C.c_uint8), P(qo, C.c_uint64), P(ds, C.c_uint8),
+                               P(do, C.c_uint64), P(pq, C.c_uint32), P(pd, C.c_uint32), len(pq),
+                               x, o, e, threads, P(out, C.c_int64))
+    return out

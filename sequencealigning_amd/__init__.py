@@ -13,10 +13,11 @@ from .nw import (NwAlignment, NwAllVsAll, NwPlan, alignment_rows, cigar_ops_stri
                  nw_align_batch, nw_score_all_vs_all, pack_csr, render)
 from . import wfa
 from .wfa import WfaAlignment, WfaPlan, wfa_align, wfa_align_batch
+from . import wfa_affine
 
 __all__ = [
     "AlignerError", "AlignmentError", "Algo", "CharError", "FastaError", "Mode", "Record",
     "Records", "parse_fasta", "parse_fasta_bytes", "NwAlignment", "NwPlan", "alignment_rows",
     "cigar_ops_string", "dense_mask", "n_w_align", "NwAllVsAll", "nw_score_all_vs_all", "nw_align_batch", "pack_csr", "render",
-    "wfa", "WfaAlignment", "WfaPlan", "wfa_align", "wfa_align_batch",
+    "wfa", "WfaAlignment", "WfaPlan", "wfa_align", "wfa_align_batch", "wfa_affine",
 ]

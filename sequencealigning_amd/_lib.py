@@ -78,6 +78,8 @@ EXPORTS = [
     "saln_nw_avsa_create", "saln_nw_avsa_execute", "saln_nw_avsa_info", "saln_nw_avsa_destroy",
     "saln_wfa_align_batch", "saln_wfa_render", "saln_wfa_plan_create", "saln_wfa_execute",
     "saln_wfa_plan_destroy",
+    "saln_wfa_affine_batch", "saln_wfa_affine_plan_create", "saln_wfa_affine_execute",
+    "saln_wfa_affine_plan_destroy",
     "saln_parse_fasta", "saln_parse_fasta_buffer", "saln_records_count", "saln_records_get",
     "saln_records_free",
 ]
@@ -91,6 +93,11 @@ class SalnError(RuntimeError):
         self.code = code
         msg = last_error() if _lib is not None else ""
         super().__init__(f"{what}: {STATUS_NAMES.get(code, code)} {msg}".strip())
+
+
+class WfaPenalties(C.Structure):
+    """saln_wfa_penalties: corrected gap-affine WFA (x, o, e); wfa.rs:14-21 defaults."""
+    _fields_ = [("mismatch", C.c_int32), ("gap_open", C.c_int32), ("gap_extend", C.c_int32)]
 
 
 def lib() -> C.CDLL:
@@ -157,6 +164,13 @@ def lib() -> C.CDLL:
         L.saln_wfa_render.argtypes = [vp, vp, C.c_uint64, vp, C.c_uint64, C.c_int32, C.c_uint32,
                                       C.c_uint32, C.c_char_p, C.c_uint64, u64p,
                                       C.POINTER(WfaResult)]
+        L.saln_wfa_affine_batch.argtypes = [vp, vp, vp, C.c_uint64, vp, vp, C.c_uint64, vp, vp,
+                                            C.c_uint64, C.POINTER(WfaPenalties), C.c_int32, vp]
+        L.saln_wfa_affine_plan_create.argtypes = [vp, vp, C.c_uint64, vp, C.c_uint64, vp, vp,
+                                                  C.c_uint64, C.POINTER(WfaPenalties),
+                                                  C.c_int32, C.POINTER(vp)]
+        L.saln_wfa_affine_execute.argtypes = [vp, vp, vp, vp, vp]
+        L.saln_wfa_affine_plan_destroy.argtypes = [vp]
         L.saln_parse_fasta.argtypes = [C.c_char_p, C.POINTER(vp), u8p, C.c_uint64, u64p]
         L.saln_parse_fasta_buffer.argtypes = [vp, C.c_uint64, C.POINTER(vp), u8p, C.c_uint64,
                                               u64p]

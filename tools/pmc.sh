@@ -14,7 +14,7 @@ i=0
 IFS=';' read -ra PASSES <<< "$SETS"
 for ctrs in "${PASSES[@]}"; do
   i=$((i+1))
-  timeout -k 10 300 rocprofv3 --pmc $ctrs --output-format csv -d $OUT/p$i -o run -- python3 tools/prof_nw.py "$@" > $OUT/p$i.log 2>&1
+  timeout -k 10 300 rocprofv3 --pmc $ctrs --output-format csv -d $OUT/p$i -o run -- python3 ${PMC_SCRIPT:-tools/prof_nw.py} "$@" > $OUT/p$i.log 2>&1
   rc=$?
   if [[ $rc -eq 124 || $rc -eq 134 || $rc -eq 137 || $rc -eq 139 ]]; then echo "pass $i ($ctrs) rc=$rc: stopping"; tail -20 $OUT/p$i.log; exit 1; fi
   if [[ $rc -ne 0 ]]; then echo "pass $i ($ctrs) failed rc=$rc (skipped)"; tail -5 $OUT/p$i.log; fi
