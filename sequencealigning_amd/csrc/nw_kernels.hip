@@ -1055,7 +1055,6 @@ __global__ __launch_bounds__(256) void nw_fill_pk_kernel(Src src, uint32_t count
     const int32_t alpha = -2 * sc.match - beta;
     const uint32_t kPen = cst2(2 * (sc.match - sc.mismatch));  // 0 < pen <= 32
     const uint32_t kOpen = cst2(2 * sc.gap_open);
-    const uint32_t kOpen1 = cst2(2 * sc.gap_open + 1);
     const uint32_t kDstep = cst2(2 * sc.gap_extend + alpha);
     const bool gstart = lane == 0;
 
@@ -1137,30 +1136,28 @@ __global__ __launch_bounds__(256) void nw_fill_pk_kernel(Src src, uint32_t count
                 const uint32_t H = umax2(M, umax2(I, D));
                 const uint32_t tO = M + kOpen;
                 if constexpr (kCodes != kCodesNone) {
-                // Sign set <=> parent absent.  With X = 2x+f (flag f in the
-                // LSB) and tO = 2o+g, every test is a difference whose high
-                // half is never 0: present -> >= 1, absent -> <= -1.
-                //   arg X   (x == h):  (X | 1) - (H & ~1)
-                //   open    (o >= x):  ((tO & ~1) + 2) - (X | 1)
-                //   extend  (x >= o):  (X | 1) - (tO & ~1)
+                // Sign set <=> parent absent.  Same-cell differences of biased
+                // halves are the unbiased differences, taken with v_pk_sub
+                // (no borrow between halves); extend/open ties are decided on
+                // the flag-free order: with X = 2x+f, tO = 2o+g,
+                // ext <=> x >= o <=> X >= (tO & ~1),  open <=> o >= x <=> (tO | 1) >= X.
                 const uint32_t Hc = H & 0xFFFEFFFEu;
-                const uint32_t M1 = M | 0x00010001u;
-                const uint32_t I1 = I | 0x00010001u, D1 = D | 0x00010001u;
-                const uint32_t tOr1 = M1 + kOpen1;  // (tO & ~1) + 2
+                const uint32_t tOr = tO | 0x00010001u;
+                auto psub = [](uint32_t a, uint32_t b) { return as_u(as_s2(a) - as_s2(b)); };
                 uint32_t sg[8];
-                sg[0] = kM ? M1 - Hc : 0u;
-                sg[1] = I1 - Hc;
-                sg[2] = D1 - Hc;
-                sg[4] = tOr1 - I1;
-                sg[6] = tOr1 - D1;
+                sg[0] = kM ? psub(M, Hc) : 0u;
+                sg[1] = psub(I, Hc);
+                sg[2] = psub(D, Hc);
+                sg[4] = psub(tOr, I);
+                sg[6] = psub(tOr, D);
                 // sign <=> q == d (bit 7): pen is 0 or pen_max >= 2 in both
                 // halves (the low half's borrow moves the high half from
                 // pen_max - 1 to pen_max - 2 or from -1 to -2)
                 sg[7] = pen - 0x00010001u;
                 if constexpr (kCodes == kCodesFull) {
                     const uint32_t tOc = tO & 0xFFFEFFFEu;
-                    sg[3] = I1 - tOc;
-                    sg[5] = D1 - tOc;
+                    sg[3] = psub(I, tOc);
+                    sg[5] = psub(D, tOc);
                 } else {
                     sg[3] = sg[5] = 0u;
                 }
