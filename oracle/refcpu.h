@@ -79,6 +79,10 @@ int ref_nw_dag_summary(const uint8_t *q, const uint8_t *d, const ref_nw_mats *m,
  * Sequences are CSR (seq + offsets, n+1).  Returns cells processed. */
 uint64_t ref_nw_run_pairs(const uint8_t *qs, const uint64_t *q_off, const uint8_t *ds,
                           const uint64_t *d_off, uint64_t n_pairs, uint64_t max_pops);
+/* refmt.c: ref_nw_run_pairs over contiguous slices of the pairs on threads */
+uint64_t ref_nw_run_pairs_mt(const uint8_t *qs, const uint64_t *q_off, const uint8_t *ds,
+                             const uint64_t *d_off, uint64_t n_pairs, uint64_t max_pops,
+                             int threads);
 
 /* Linear-memory score + end states + panic status of one pair with the
  * reference semantics (reflinear.c), on `threads` column stripes.  For

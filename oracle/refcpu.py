@@ -53,6 +53,9 @@ def lib():
         L.ref_nw_run_pairs.argtypes = [u8p, C.POINTER(C.c_uint64), u8p, C.POINTER(C.c_uint64),
                                        C.c_uint64, C.c_uint64]
         L.ref_nw_run_pairs.restype = C.c_uint64
+        L.ref_nw_run_pairs_mt.argtypes = [u8p, C.POINTER(C.c_uint64), u8p, C.POINTER(C.c_uint64),
+                                          C.c_uint64, C.c_uint64, C.c_int]
+        L.ref_nw_run_pairs_mt.restype = C.c_uint64
         L.ref_nw_score_linear.argtypes = [u8p, C.c_size_t, u8p, C.c_size_t, C.c_int,
                                           C.POINTER(C.c_int32), u8p, C.POINTER(C.c_int)]
         L.ref_parse_fasta.argtypes = [u8p, C.c_size_t, C.c_int, u8p, C.c_size_t,
@@ -156,6 +159,17 @@ def run_pairs(qs: bytes, q_off: np.ndarray, ds: bytes, d_off: np.ndarray, n_pair
     do = np.ascontiguousarray(d_off, np.uint64)
     return L.ref_nw_run_pairs(_u8(qs), qo.ctypes.data_as(C.POINTER(C.c_uint64)), _u8(ds),
                               do.ctypes.data_as(C.POINTER(C.c_uint64)), n_pairs, max_pops)
+
+
+def run_pairs_mt(qs: bytes, q_off: np.ndarray, ds: bytes, d_off: np.ndarray, n_pairs: int,
+                 max_pops: int = 100_000, threads: int = 1) -> int:
+    """run_pairs over contiguous slices of the pairs on `threads` threads."""
+    L = lib()
+    qo = np.ascontiguousarray(q_off, np.uint64)
+    do = np.ascontiguousarray(d_off, np.uint64)
+    return L.ref_nw_run_pairs_mt(_u8(qs), qo.ctypes.data_as(C.POINTER(C.c_uint64)), _u8(ds),
+                                 do.ctypes.data_as(C.POINTER(C.c_uint64)), n_pairs, max_pops,
+                                 threads)
 
 
 def parse_fasta_bytes(data: bytes, valid_ext: bool = True):
