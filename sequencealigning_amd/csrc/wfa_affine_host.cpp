@@ -152,6 +152,10 @@ int saln_wfa_affine_plan_create(saln_context *ctx, const uint64_t *q_off, uint64
         const char *e = std::getenv("SALN_WFA2_W1");
         return e ? (int32_t)std::atoi(e) : 0;
     }();
+    static const int32_t w2 = [] {  // experiment switch: second-pass ring width
+        const char *e = std::getenv("SALN_WFA2_W2");
+        return e ? (int32_t)std::atoi(e) : 0;
+    }();
     auto pass = [&](int32_t W) {
         WfaAffParams q = p->prm;
         q.W = W;
@@ -162,7 +166,7 @@ int saln_wfa_affine_plan_create(saln_context *ctx, const uint64_t *q_off, uint64
         return q;
     };
     p->p1 = pass(w1 ? w1 : p->wide ? kW1Wide : kW1);
-    p->p2 = pass(p->wide ? kW2Wide : kW2);
+    p->p2 = pass(w2 ? w2 : p->wide ? kW2Wide : kW2);
     p->grid1 = grid_for(p->p1, p->wide, n_pairs, ctx->device);
     p->grid2 = grid_for(p->p2, p->wide, n_pairs, ctx->device);
     *out = p;

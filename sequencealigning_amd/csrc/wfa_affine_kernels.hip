@@ -178,11 +178,27 @@ __device__ __forceinline__ int32_t wfa_pair(P q, int32_t lq, P d, int32_t ld, co
             continue;
         }
         if (mHi - mLo + 1 > W) return -2;  // the ring is too narrow: re-run with a wider one
-        // LDS reads are always in bounds (k & wm), so the range test is a select
+        // LDS reads are always in bounds (k & wm), so a range test is a select.
+        // Predicates are arithmetic (one unsigned compare, or one max3 and a
+        // compare) so they cost VALU only, no SALU mask combining.  An empty
+        // source gets lo = 2^30, span 0: k - lo never passes.
+        auto span_of = [](int32_t &lo, int32_t hi) {
+            if (lo > hi) {
+                lo = 1 << 30;
+                return 0u;
+            }
+            return (uint32_t)(hi - lo);
+        };
+        const uint32_t spMo = span_of(loMo, hiMo), spMx = span_of(loMx, hiMx);
+        const uint32_t spI = span_of(loI, hiI), spD = span_of(loD, hiD);
         auto rd = [&](const OffT *ring, int32_t slot, int32_t k, int32_t lo,
-                      int32_t hi) __attribute__((always_inline)) {
+                      uint32_t sp) __attribute__((always_inline)) {
             const int32_t v = (int32_t)ring[slot * W + (k & wm)];
-            return (k >= lo && k <= hi) ? v : kNeg;
+            return (uint32_t)(k - lo) <= sp ? v : kNeg;
+        };
+        // an offset h on diagonal k is a cell iff 0 <= h <= ld and h - k <= lq
+        auto cell = [&](int32_t h, int32_t k) __attribute__((always_inline)) {
+            return max(max(-h, h - ld), h - k - lq) <= 0;
         };
         // Target slots (t % RM, t % RI) differ from every source slot
         // (RM > max(toe, tx), RI > te), so chunks read and write freely.
@@ -192,6 +208,7 @@ __device__ __forceinline__ int32_t wfa_pair(P q, int32_t lq, P d, int32_t ld, co
         // longer extensions and the writes.  Lanes past mHi compute -inf and
         // write it: entries outside a slot's stored range are never read, and
         // a group never spans more than W diagonals, so nothing valid is hit.
+        // (I and D outside their own ranges read -inf from both sources.)
         const int32_t span = mHi - mLo;
 #pragma unroll
         for (int g = 0; g < CM / 4; ++g) {
@@ -201,17 +218,16 @@ __device__ __forceinline__ int32_t wfa_pair(P q, int32_t lq, P d, int32_t ld, co
 #pragma unroll
             for (int c = 0; c < 4; ++c) {
                 const int32_t k = mLo + 64 * (4 * g + c) + lane;
-                int32_t I = max(rd(Mr, soe, k - 1, loMo, hiMo), rd(Ir, sie, k - 1, loI, hiI)) + 1;
-                if (k < iLo || k > iHi || I > ld || I - k > lq || I < 0) I = kNeg;
-                int32_t D = max(rd(Mr, soe, k + 1, loMo, hiMo), rd(Dr, sde, k + 1, loD, hiD));
-                if (k < dLo || k > dHi || D > ld || D - k > lq || D < 0) D = kNeg;
-                int32_t X = rd(Mr, sx, k, loMx, hiMx) + 1;
-                if (X > ld || X - k > lq) X = kNeg;
-                int32_t M = max(X, max(I, D));
-                if (k > mHi || M < 0) M = kNeg;
+                int32_t I = max(rd(Mr, soe, k - 1, loMo, spMo), rd(Ir, sie, k - 1, loI, spI)) + 1;
+                I = cell(I, k) ? I : kNeg;
+                int32_t D = max(rd(Mr, soe, k + 1, loMo, spMo), rd(Dr, sde, k + 1, loD, spD));
+                D = cell(D, k) ? D : kNeg;
+                int32_t X = rd(Mr, sx, k, loMx, spMx) + 1;
+                X = cell(X, k) ? X : kNeg;
+                const int32_t M = max(X, max(I, D));
                 Iv[c] = I;
                 Dv[c] = D;
-                Mv[c] = M;
+                Mv[c] = (uint32_t)(k - mLo) <= (uint32_t)span ? M : kNeg;
             }
             uint32_t more = 0;  // bit c: chunk c's lane matched 4 bases, keep extending
 #pragma unroll
@@ -219,18 +235,13 @@ __device__ __forceinline__ int32_t wfa_pair(P q, int32_t lq, P d, int32_t ld, co
                 const int32_t k = mLo + 64 * (4 * g + c) + lane;
                 const int32_t M = Mv[c];
                 const int32_t v = M - k;
-                const bool fast = kSafe0 && M >= 0 && v + 5 <= lq && M + 5 <= ld;
+                const bool fast = kSafe0 && max(max(-M, v + 5 - lq), M + 5 - ld) <= 0;
                 slow[c] = M >= 0 && !fast;
                 if constexpr (kSafe0) {  // loads at a safe address when not fast
                     const uint32_t x = load4(q + (fast ? v : 0)) ^ load4(d + (fast ? M : 0));
-                    if (fast) {
-                        if (x) {
-                            Mv[c] = M + (int32_t)(__builtin_ctz(x) >> 3);
-                        } else {
-                            Mv[c] = M + 4;
-                            more |= 1u << c;
-                        }
-                    }
+                    const int32_t adv = x ? (int32_t)(__builtin_ctz(x) >> 3) : 4;
+                    Mv[c] = fast ? M + adv : M;
+                    more |= (fast && !x) ? 1u << c : 0u;
                 }
             }
 #pragma unroll
