@@ -1391,6 +1391,10 @@ __global__ __launch_bounds__(64) void nw_fill_stripe_kernel(
                     blkH = (int32_t)(uint32_t)v;
                     blkF = (int32_t)(uint32_t)(v >> 32);
                 }
+                // wait here, on the block step only: otherwise the compiler
+                // puts a vmcnt(0) (every outstanding mask store) on the join
+                // path of every step, before the readlanes below
+                __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
             }
             const uint32_t sl = (rr - 1) % kPub;
             bH = __builtin_amdgcn_readlane(blkH, sl);
