@@ -1330,20 +1330,16 @@ __global__ __launch_bounds__(64) void nw_fill_stripe_kernel(
     }
     int32_t hd = hs_row0(sc, col0) + beta * (int32_t)col0;
     int32_t pubF = 0, pubH = 0;
-    // db chars: lane 0 needs d[t] at step t (wave-uniform): 16-byte scalar
-    // loads, prefetched one block ahead so their wait never stalls a step;
-    // the other lanes take their row's char from the left neighbour's
-    // previous step (DPP).
+    // db chars: lane 0 needs d[t] at step t (wave-uniform): a rolling pair of
+    // scalar dwords (the next one loaded four steps before it is used), so a
+    // step spends a shift and a mask on it; the other lanes take their row's
+    // char from the left neighbour's previous step (DPP).
     typedef const __attribute__((address_space(4))) uint32_t cu32;  // constant: scalar loads
-    auto ld16 = [](uintptr_t a) {
-        const cu32 *w = (const cu32 *)a;
-        return make_uint4(w[0], w[1], w[2], w[3]);
-    };
-    const uintptr_t dbase = (uintptr_t)d & ~(uintptr_t)15;
-    const uint32_t dsh = (uint32_t)((uintptr_t)d & 15);
-    const uint32_t nblk = (ld + dsh + 15) / 16;  // 16-byte blocks holding d[0 .. ld)
-    uint4 dcur = ld16(dbase), dnxt = dcur;
-    if (nblk > 1) dnxt = ld16(dbase + 16);
+    cu32 *dw = (cu32 *)((uintptr_t)d & ~(uintptr_t)3);
+    const uint32_t last_dw = ((uint32_t)ld - 1 + (uint32_t)((uintptr_t)d & 3)) >> 2;
+    uint32_t dpos = (uint32_t)((uintptr_t)d & 3);  // byte of d[t] in dcur
+    uint32_t dnidx = min(1u, last_dw);             // dword index of dnxt
+    uint32_t dcur = dw[0], dnxt = dw[dnidx];
     uint32_t dch = 0;
     int32_t blkH = 0, blkF = 0;  // lanes 0..31: the left column of the current 32-row block
     uint32_t avail = 0;          // rows of the left column known to be published
@@ -1356,16 +1352,12 @@ __global__ __launch_bounds__(64) void nw_fill_stripe_kernel(
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
     for (int t = 0; t < T; ++t) {
         const int r = t - lane + 1;
-        {
-            const uint32_t j = (uint32_t)min(t, (int)ld - 1) + dsh;  // byte of d[t] from dbase
-            if ((j & 15) == 0 && j > 0 && t < (int)ld) {  // next 16-byte block
-                dcur = dnxt;
-                const uint32_t nb = (j >> 4) + 1;
-                if (nb < nblk) dnxt = ld16(dbase + 16 * nb);
-            }
-            const uint32_t wsel = (j >> 2) & 3;
-            const uint32_t w = wsel == 0 ? dcur.x : wsel == 1 ? dcur.y : wsel == 2 ? dcur.z : dcur.w;
-            dch = (uint32_t)shr1<G>((int32_t)(((w >> (8 * (j & 3))) & 0xFFu) << 8), (int32_t)dch);
+        dch = (uint32_t)shr1<G>((int32_t)(((dcur >> (8 * dpos)) & 0xFFu) << 8), (int32_t)dch);  // d[r-1]
+        if (++dpos == 4) {  // past the stripe's last char the bytes are unused
+            dpos = 0;
+            dcur = dnxt;
+            dnidx = min(dnidx + 1, last_dw);
+            dnxt = dw[dnidx];
         }
         int32_t bF, bH;
         const uint32_t rr = (uint32_t)t + 1;  // lane 0's row
