@@ -48,6 +48,7 @@ struct NwPairDesc {
     uint32_t pair_id;        // index into results
     uint32_t variant;        // fill kernel variant (kernel geometry)
     uint32_t reserved;
+    uint64_t mask_cs;        // bytes from query chunk c to c+1 (G*bs unless skewed)
 };
 
 // Kernel geometry of one fill variant: G lanes per pair, K query columns per
@@ -61,7 +62,12 @@ struct NwPairDesc {
 // wave): bs = n*LB and pair slot s sits at +s*LB, so the walker's per-lane
 // loads of one (row, block) touch adjacent bytes and the fill's stores of a
 // row are contiguous across the pairs of a wave.  A pair outside such a pack
-// has bs = LB and rs = (blocks)*LB.
+// has bs = LB and rs = (blocks)*LB; in both, chunk stride cs = G*bs.
+// Column-stripe pairs (G = 64, K = 4) are stored skewed instead, in the order
+// the stripe wave writes them: the 64 lanes' code dwords of fill step t
+// (lane l at row t-l+1) are the 256 contiguous bytes of line t of the
+// stripe's region, so rs = 256, bs = 260 (next block: one row later, 4 bytes
+// on) and cs = (len_db + 63) * 256.
 struct Geom {
     uint32_t G, K;
     SALN_HD uint32_t KD() const { return (K + 3) / 4; }
@@ -71,9 +77,9 @@ struct Geom {
     SALN_HD uint32_t n_blocks(uint32_t len_q) const { return n_chunks(len_q) * G; }
     SALN_HD uint32_t steps(uint32_t len_db) const { return len_db + G - 1; }
     // byte offset (from mask_off) of interior cell (i, j), 1-based
-    SALN_HD uint64_t cell(uint32_t i, uint32_t j, uint64_t rs, uint32_t bs) const {
-        const uint32_t jj0 = j - 1;
-        return (uint64_t)(i - 1) * rs + (uint64_t)(jj0 / K) * bs + jj0 % K;
+    SALN_HD uint64_t cell(uint32_t i, uint32_t j, uint64_t rs, uint32_t bs, uint64_t cs) const {
+        const uint32_t jj0 = j - 1, b = jj0 / K;
+        return (uint64_t)(i - 1) * rs + (uint64_t)(b / G) * cs + (uint64_t)(b % G) * bs + jj0 % K;
     }
 };
 

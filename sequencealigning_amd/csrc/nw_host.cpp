@@ -247,12 +247,24 @@ int saln_nw_plan_create(saln_context *ctx, const uint64_t *q_off, uint64_t n_q,
                 own += (uint64_t)d.len_db * g.n_blocks(d.len_q) * lb;
             }
             const uint64_t packed = rows * nbm * np * lb;
-            if (4 * packed <= 5 * own + 4096) {
+            if (v == kStripeVariant) {
+                // skewed, one region per stripe (nw_common.hpp): every fill
+                // step of a stripe wave writes one whole 256-byte line
+                for (uint32_t s = 0; s < np; ++s) {
+                    NwPairDesc &d = p->h_pairs[a + s];
+                    d.mask_off = moff;
+                    d.mask_rs = g.W();
+                    d.mask_bs = (uint32_t)(g.W() + lb);
+                    d.mask_cs = ((uint64_t)d.len_db + g.G - 1) * g.W();
+                    moff += g.n_chunks(d.len_q) * d.mask_cs;
+                }
+            } else if (4 * packed <= 5 * own + 4096) {
                 for (uint32_t s = 0; s < np; ++s) {
                     NwPairDesc &d = p->h_pairs[a + s];
                     d.mask_off = moff + s * lb;
                     d.mask_bs = (uint32_t)(np * lb);
                     d.mask_rs = nbm * np * lb;
+                    d.mask_cs = (uint64_t)g.G * d.mask_bs;
                 }
                 moff += (packed + 255) & ~255ull;
             } else {
@@ -261,6 +273,7 @@ int saln_nw_plan_create(saln_context *ctx, const uint64_t *q_off, uint64_t n_q,
                     d.mask_off = moff;
                     d.mask_bs = (uint32_t)lb;
                     d.mask_rs = g.n_blocks(d.len_q) * lb;
+                    d.mask_cs = (uint64_t)g.G * lb;
                     moff += ((uint64_t)d.len_db * d.mask_rs + 255) & ~255ull;
                 }
             }
@@ -531,7 +544,7 @@ int plan_set_full_codes(saln_nw_plan *p, bool full) {
 int plan_pair_mask(const saln_nw_plan *p, uint64_t pair_id, PairMask *pm) {
     if (!p || pair_id >= p->n_pairs) return SALN_E_INVALID;
     const NwPairDesc &d = p->h_pairs[p->plan_index[pair_id]];
-    if (!p->full_codes && variant_packed((int)d.variant)) {
+    if (!p->full_codes && (variant_packed((int)d.variant) || d.variant == (uint32_t)kStripeVariant)) {
         set_error("plan_pair_mask: plan stores walk codes only");
         return SALN_E_INVALID;
     }
@@ -540,11 +553,21 @@ int plan_pair_mask(const saln_nw_plan *p, uint64_t pair_id, PairMask *pm) {
     pm->rs = 0;
     pm->bs = pm->g.LB();
     if (d.len_q == 0 || d.len_db == 0) return SALN_OK;
+    if (d.variant == (uint32_t)kStripeVariant) {  // skewed stripe regions: copied whole
+        pm->rs = d.mask_rs;
+        pm->bs = d.mask_bs;
+        pm->cs = d.mask_cs;
+        pm->m.resize(pm->g.n_chunks(d.len_q) * d.mask_cs);
+        HIP_TRY(hipSetDevice(p->ctx->device));
+        HIP_TRY(hipMemcpy(pm->m.data(), p->d_mask + d.mask_off, pm->m.size(), hipMemcpyDeviceToHost));
+        return SALN_OK;
+    }
     // every row holds rs / bs blocks (the pack's width); copy them all as
     // LB-byte rows of one bs-pitched 2-D region
     const uint64_t nb = d.mask_rs / d.mask_bs;
     const uint64_t lb = pm->g.LB();
     pm->rs = nb * lb;
+    pm->cs = (uint64_t)pm->g.G * lb;
     pm->m.resize((uint64_t)d.len_db * nb * lb);
     HIP_TRY(hipSetDevice(p->ctx->device));
     HIP_TRY(hipMemcpy2D(pm->m.data(), lb, p->d_mask + d.mask_off, d.mask_bs, lb,

@@ -73,6 +73,7 @@ struct PairMask {
     Geom g{16, 10};
     uint64_t rs = 0;
     uint32_t bs = 0;
+    uint64_t cs = 0;
 };
 
 // Random access to one pair's parent codes (kernel layout + boundary rules).
@@ -81,13 +82,14 @@ struct HostMask {
     Geom g{16, 10};
     uint64_t rs = 0;
     uint32_t bs = 0;
+    uint64_t cs = 0;
     uint32_t lq = 0, ld = 0;
     Scoring sc{5, -4, -8, -6};
     HostMask() = default;
     HostMask(const PairMask &pm, uint32_t lq_, uint32_t ld_, const Scoring &sc_)
-        : m(pm.m.data()), g(pm.g), rs(pm.rs), bs(pm.bs), lq(lq_), ld(ld_), sc(sc_) {}
+        : m(pm.m.data()), g(pm.g), rs(pm.rs), bs(pm.bs), cs(pm.cs), lq(lq_), ld(ld_), sc(sc_) {}
     // codes are stored inverted (bit set = parent absent)
-    uint8_t byte(uint32_t i, uint32_t j) const { return m[g.cell(i, j, rs, bs)] ^ 0x7F; }
+    uint8_t byte(uint32_t i, uint32_t j) const { return m[g.cell(i, j, rs, bs, cs)] ^ 0x7F; }
     uint8_t argmax(uint32_t i, uint32_t j) const {
         if (i == 0) return argmax_row0(sc, j);
         if (j == 0) return argmax_col0(sc, i);

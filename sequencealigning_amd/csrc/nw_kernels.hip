@@ -70,9 +70,10 @@ struct MaskCell {
     Geom g;
     uint64_t rs;
     uint32_t bs;
+    uint64_t cs;
     Scoring sc;
     // codes are stored inverted (bit set = parent absent)
-    __device__ uint8_t byte(uint32_t i, uint32_t j) const { return m[g.cell(i, j, rs, bs)] ^ 0x7F; }
+    __device__ uint8_t byte(uint32_t i, uint32_t j) const { return m[g.cell(i, j, rs, bs, cs)] ^ 0x7F; }
     __device__ uint8_t argmax(uint32_t i, uint32_t j) const {
         if (i == 0) return argmax_row0(sc, j);
         if (j == 0) return argmax_col0(sc, i);
@@ -105,7 +106,7 @@ __device__ __forceinline__ void walk_pair(const NwPairDesc &p, int32_t hend,
     const uint32_t lq = p.len_q, ld = p.len_db;
     const uint8_t *q = qs + p.q_off;
     const uint8_t *d = ds + p.db_off;
-    const MaskCell mc{mask + p.mask_off, geo, p.mask_rs, p.mask_bs, sc};
+    const MaskCell mc{mask + p.mask_off, geo, p.mask_rs, p.mask_bs, p.mask_cs, sc};
     const uint8_t am_end = mc.argmax(ld, lq);
     int st = (am_end & kArgD) ? kStD : ((am_end & kArgM) ? kStM : kStI);
     uint32_t i = ld, j = lq;
@@ -273,7 +274,7 @@ constexpr uint64_t kNextLut = make_next_lut();
 // debug build: compare every window read with the byte in HBM
 #define SALN_WALK_CHECK_HOOK(S)                                                          \
     {                                                                                    \
-        const uint32_t tru = (uint32_t)m[geo.cell(ti, tj, rs, bs)];                     \
+        const uint32_t tru = (uint32_t)m[geo.cell(ti, tj, rs, bs, p.mask_cs)];                     \
         if (tru != raw) {                                                                \
             const uint32_t par = wc;                                                     \
             if (!dbg_n) dbg_info = (S) | (par << 3) | (((valid >> (par * 8u + (S))) & 1u) << 5) | \
@@ -318,7 +319,7 @@ __device__ void walk_pair_lds(const NwPairDesc &p, int32_t hend, const uint8_t *
 #endif
     // per-block segment bases for B, B-1, B-2
     auto blk_base = [&](uint32_t blk) __attribute__((always_inline)) {
-        return m + (uint64_t)blk * bs;
+        return m + (uint64_t)(blk / G) * p.mask_cs + (uint64_t)(blk % G) * bs;
     };
     const uint8_t *bp0 = blk_base(B), *bp1 = blk_base(B >= 1 ? B - 1 : 0);
     const uint8_t *bp2 = blk_base(B >= 2 ? B - 2 : 0);
@@ -501,7 +502,7 @@ __device__ void walk_pair_lds(const NwPairDesc &p, int32_t hend, const uint8_t *
     r.score = hend >> 1;
     r.status = (hend & 1) ? SALN_REF_PANIC_BOUNDARY : SALN_OK;
     r.cigar_len = nops;
-    r.end_states = (uint8_t)((m[geo.cell(p.len_db, p.len_q, rs, bs)] ^ 0x7Fu) & 7u);
+    r.end_states = (uint8_t)((m[geo.cell(p.len_db, p.len_q, rs, bs, p.mask_cs)] ^ 0x7Fu) & 7u);
     r.printed = ev == kEvOrigin ? 1 : 0;
     r.flags = (ev == kEvDead ? 1 : 0) | ((ev == kEvPanic && !(hend & 1)) ? 2 : 0);
     r.reserved = 0;
@@ -568,56 +569,53 @@ __global__ __launch_bounds__(256) void nw_traceback_kernel(
 // state from the argmax bits of (i-l-1, j-l-1)); in I / D lane l looks at the
 // l-th extend step.  A ballot of "the run ends after my step" gives the run
 // length, so a 64-step stretch of the path costs one round of LDS reads
-// instead of 64 dependent ones.  The codes come from an LDS window of
-// kCoopRows rows x kCoopBlk blocks of the mask, anchored at the current cell
-// and reloaded (LDS-DMA) when a run would leave it.  CIGAR words are emitted
-// back to front (uniform scalar run-length state) and reversed at the end.
-constexpr int32_t kCoopRows = 256, kCoopBlk = 64;
+// instead of 64 dependent ones.  The codes come from an LDS window over the
+// stripe holding the current cell, rows [i-rows+1, i]: in the skewed stripe
+// layout (nw_common.hpp) that is one contiguous run of lines, copied by
+// LDS-DMA (1 KB per instruction) when a run would leave it.  A step into the
+// previous stripe takes the current cell's eq bit from the old window and the
+// rest from the new one.  CIGAR words are emitted back to front (uniform
+// scalar run-length state) and reversed at the end.  The window height is the
+// launch's choice (dynamic LDS of (rows + 64) lines): tall for a few long
+// pairs (fewer reloads), short for batches (more waves per CU).
+constexpr int32_t kCoopLine = 256;  // bytes per line (one stripe step)
+constexpr int32_t kCoopSlack = 64;  // rows loaded beyond a diagonal crossing of the stripe
 
 __global__ __launch_bounds__(64) void nw_traceback_coop_kernel(
     const NwPairDesc *__restrict__ pairs, uint32_t first, const uint8_t *__restrict__ mask,
     const int32_t *__restrict__ end_h, saln_nw_result *__restrict__ results,
-    uint32_t *__restrict__ cigar, Scoring sc) {
-    constexpr int32_t kRowB = kCoopBlk * 4;  // LDS bytes per window row
-    __shared__ __attribute__((aligned(16))) uint8_t win[kCoopRows * kRowB];
+    uint32_t *__restrict__ cigar, Scoring sc, int32_t kCoopRows) {
+    // kCoopRows + 63 lines, rounded up to whole 4-line DMAs
+    extern __shared__ __attribute__((aligned(16))) uint8_t win[];
     const int32_t lane = (int32_t)threadIdx.x;
     const uint32_t idx = first + blockIdx.x;
     const NwPairDesc p = pairs[idx];
     const int32_t hend = end_h[idx];
     const int32_t lq = (int32_t)p.len_q, ld = (int32_t)p.len_db;
     const uint8_t *__restrict__ m = mask + p.mask_off;
-    const uint64_t rs = p.mask_rs;
-    const uint32_t bs = p.mask_bs;
-    int32_t r_lo = 1, c_lo = 1;  // window: rows [r_lo, r_lo+255], columns [c_lo, c_lo+255]
-    // Rows [max(1, i-255), i] and the 64 blocks ending at the block of column
-    // j (a stripe pair's mask rows hold whole 256-column stripes, so all 64
-    // exist).  Rows past i repeat row i (never read).
+    int32_t r_lo = 1, c_lo = 1;  // window: rows [r_lo, i], the stripe's columns [c_lo, c_lo+255]
     auto load = [&](int32_t i, int32_t j) __attribute__((always_inline)) {
-        r_lo = max(1, i - kCoopRows + 1);
-        const int32_t bj = (j - 1) / 4;
-        const int32_t b_lo = max(0, bj - kCoopBlk + 1);
-        c_lo = 4 * b_lo + 1;
-        const int32_t nrows = i - r_lo + 1;
-        const uint8_t *mb = m + (uint64_t)b_lo * bs;
+        const int32_t s = (j - 1) / kCoopLine;
+        c_lo = s * kCoopLine + 1;
+        // a near-diagonal path leaves the stripe after j - c_lo + 1 rows:
+        // load those plus some slack for gaps, not the whole window height
+        r_lo = max(1, i - min(kCoopRows, j - c_lo + 1 + kCoopSlack) + 1);
+        // lines r_lo-1 .. i+62 of stripe s (row r of lane l is line r-1+l)
+        const int32_t t_lo = r_lo - 1, t_hi = i + 62;
+        const uint8_t *reg = m + (uint64_t)s * p.mask_cs;
         typedef __attribute__((address_space(3))) void lds_v;
-        if (bs == 4) {  // rows contiguous: 16 bytes (4 blocks) per lane, 4 rows per DMA
-            const int32_t sub = lane / 16, ch = lane % 16;
-            for (int32_t mm = 0; mm < (nrows + 3) / 4; ++mm) {
-                const int32_t rr = min(4 * mm + sub, nrows - 1);
-                __builtin_amdgcn_global_load_lds(mb + (uint64_t)(r_lo + rr - 1) * rs + 16 * ch,
-                                                 (lds_v *)(win + 4 * mm * kRowB), 16, 0, 0);
-            }
-        } else {  // one block per lane, one row per DMA
-            for (int32_t mm = 0; mm < nrows; ++mm)
-                __builtin_amdgcn_global_load_lds(mb + (uint64_t)(r_lo + mm - 1) * rs + (uint64_t)lane * bs,
-                                                 (lds_v *)(win + mm * kRowB), 4, 0, 0);
+        for (int32_t mm = 0; 4 * mm <= t_hi - t_lo; ++mm) {
+            const int32_t t = min(t_lo + 4 * mm + lane / 16, t_hi);  // clamped: stay in the region
+            __builtin_amdgcn_global_load_lds(reg + (uint64_t)t * kCoopLine + 16 * (lane % 16),
+                                             (lds_v *)(win + 4 * mm * kCoopLine), 16, 0, 0);
         }
         __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the window has landed
         __builtin_amdgcn_wave_barrier();
     };
     // code byte of interior cell (r, c) inside the window, bits 0-6 present-sets
     auto code = [&](int32_t r, int32_t c) __attribute__((always_inline)) {
-        return (uint32_t)win[(r - r_lo) * kRowB + (c - c_lo)] ^ 0x7Fu;
+        const int32_t o = c - c_lo;
+        return (uint32_t)win[(r - r_lo + (o >> 2)) * kCoopLine + o] ^ 0x7Fu;
     };
     int32_t i = ld, j = lq;
     load(i, j);
@@ -653,11 +651,19 @@ __global__ __launch_bounds__(64) void nw_traceback_coop_kernel(
         // the boundary formulas)
         const int32_t lim_i = r_lo == 1 ? i - 1 : i - 1 - r_lo;
         const int32_t lim_j = c_lo == 1 ? j - 1 : j - 1 - c_lo;
-        int32_t lmax = st == kStM ? min(lim_i, lim_j) : st == kStI ? lim_j : lim_i;
-        if (i < r_lo || j < c_lo || lmax < 0) {
-            load(i, j);
+        if (i < r_lo || j < c_lo || (st != kStI && lim_i < 0)) {
+            load(i, j);  // anchored at row i: lim_i >= 0 afterwards
             continue;
         }
+        // j == c_lo > 1 and the step reads column j-1: one step, lane 0,
+        // that column from global memory
+        const bool edge = st != kStD && lim_j < 0;
+        uint32_t eq0 = 0;
+        if (edge) {  // j == c_lo > 1: this step reads column j-1 of the previous stripe
+            if (st == kStM) eq0 = code(i, j) >> 7;  // (i, j) leaves the window now
+            load(i, j - 1);
+        }
+        int32_t lmax = edge ? 0 : st == kStM ? min(lim_i, lim_j) : st == kStI ? lim_j : lim_i;
         lmax = min(lmax, 63);
         bool stop = true;
         int32_t nxt = st;
@@ -665,7 +671,7 @@ __global__ __launch_bounds__(64) void nw_traceback_coop_kernel(
         if (lane <= lmax) {
             if (st == kStM) {
                 const int32_t ni = i - lane - 1, nj = j - lane - 1;
-                eq = code(i - lane, j - lane) >> 7;
+                eq = edge ? eq0 : code(i - lane, j - lane) >> 7;
                 const uint32_t a = ni == 0 ? argmax_row0(sc, (uint32_t)nj)
                                  : nj == 0 ? argmax_col0(sc, (uint32_t)ni)
                                            : code(ni, nj) & 7u;
@@ -1344,8 +1350,10 @@ __global__ __launch_bounds__(64) void nw_fill_stripe_kernel(
     int32_t blkH = 0, blkF = 0;  // lanes 0..31: the left column of the current 32-row block
     uint32_t avail = 0;          // rows of the left column known to be published
     bool failed = false;
-    uint8_t *mseg = mask + p.mask_off + (uint64_t)(c * G + (uint32_t)lane) * p.mask_bs -
-                    (int64_t)lane * (int64_t)p.mask_rs;  // row r-1 = t - lane at step 0
+    // lane l's row t-l+1 at step t: mask_off + c*cs + l*bs + (t-l)*rs; in the
+    // skewed stripe layout (nw_common.hpp) step t's dwords are line t
+    uint8_t *mseg = mask + p.mask_off + (uint64_t)c * p.mask_cs + (uint64_t)lane * p.mask_bs -
+                    (int64_t)lane * (int64_t)p.mask_rs;
     const int T = (int)geo.steps(ld);
     // the query chars above arrive here: otherwise the wait for them lands
     // inside the loop, where it would also wait for every mask store
@@ -1661,10 +1669,18 @@ hipError_t launch_traceback(int variant, const NwPairDesc *pairs, uint32_t first
         case 0: tb_lds<16, 10>(grid, stream, pairs, first, n, mask, end_h, ops, results, cigar, sc); break;
         case 1: tb_lds<16, 16>(grid, stream, pairs, first, n, mask, end_h, ops, results, cigar, sc); break;
         case 2: tb_lds<64, 8>(grid, stream, pairs, first, n, mask, end_h, ops, results, cigar, sc); break;
-        case 3:  // column-stripe pairs: one cooperative wave per pair
-            nw_traceback_coop_kernel<<<dim3(n), dim3(64), 0, stream>>>(pairs, first, mask, end_h,
-                                                                      results, cigar, sc);
+        case 3: {  // column-stripe pairs: one cooperative wave per pair
+            // a few pairs: the whole 160 KB (fewer window reloads); batches:
+            // 48 KB windows, three waves per CU
+            static const hipError_t attr = hipFuncSetAttribute(
+                (const void *)nw_traceback_coop_kernel,
+                hipFuncAttributeMaxDynamicSharedMemorySize, (576 + 64) * kCoopLine);
+            if (attr != hipSuccess) return attr;
+            const int32_t rows = n <= 256 ? 576 : 128;
+            nw_traceback_coop_kernel<<<dim3(n), dim3(64), (size_t)(rows + 64) * kCoopLine, stream>>>(
+                pairs, first, mask, end_h, results, cigar, sc, rows);
             break;
+        }
         case 5: tb_lds<16, 16>(grid, stream, pairs, first, n, mask, end_h, ops, results, cigar, sc); break;
         case 6: tb_lds<32, 16>(grid, stream, pairs, first, n, mask, end_h, ops, results, cigar, sc); break;
         case 7: tb_lds<16, 10>(grid, stream, pairs, first, n, mask, end_h, ops, results, cigar, sc); break;
