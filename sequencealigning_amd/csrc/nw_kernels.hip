@@ -1030,7 +1030,18 @@ struct AvsaSrc {
 // columns are stored as K/KS segments of KS codes.  KS < K lets a narrower
 // lane group (G*K = the same width, fewer lanes: less pipeline skew, per-step
 // overhead spread over more columns) write the layout of the wider one.
-template <int G, int K, int kCodes, typename Src, int KS>
+//
+// kRebase: pairs whose db is too long for one int16 frame (packed_ok_rebase).
+// Every kRebaseSteps steps all carried values drop by the column-0 drift of
+// that many rows, (2*gap_extend + alpha) * kRebaseSteps (even: flags
+// survive), so a value at step t is X~ - (2*ge + alpha) * r0(t), r0(t) = t
+// rounded down to the period; a lane's rows are then within period + G of
+// r0 and the values within the bound of a (period + G)-row pair.  Parent
+// codes compare values of one cell (frame-free); group-start inputs and end
+// values convert with r0(t).
+constexpr int kRebaseSteps = 64;
+
+template <int G, int K, int kCodes, typename Src, int KS, bool kRebase = false>
 __global__ __launch_bounds__(256) void nw_fill_pk_kernel(Src src, uint32_t count,
                                                          const uint8_t *__restrict__ qs,
                                                          const uint8_t *__restrict__ ds,
@@ -1066,6 +1077,8 @@ __global__ __launch_bounds__(256) void nw_fill_pk_kernel(Src src, uint32_t count
     const uint32_t kPen = cst2(2 * (sc.match - sc.mismatch));  // 0 < pen <= 32
     const uint32_t kOpen = cst2(2 * sc.gap_open);
     const uint32_t kDstep = cst2(2 * sc.gap_extend + alpha);
+    const int32_t drift = 2 * sc.gap_extend + alpha;  // column-0 X~ per row (kRebase)
+    const uint32_t kRebaseAdd = cst2(-drift * kRebaseSteps);
     const bool gstart = lane == 0;
 
     const int col0 = lane * K;  // my columns: col0+1 .. col0+K
@@ -1124,10 +1137,24 @@ __global__ __launch_bounds__(256) void nw_fill_pk_kernel(Src src, uint32_t count
     auto step = [&](int t, uint32_t(&Hin)[K], uint32_t(&Hout)[K]) __attribute__((always_inline)) {
         const int r = t - lane + 1;
         const uint32_t dch = rowp[t];
+        int32_t base = 0;  // frame of step t (kRebase)
+        if constexpr (kRebase) {
+            base = drift * (t & -kRebaseSteps);
+            if ((t & (kRebaseSteps - 1)) == 0 && t > 0) {  // wave-uniform
+#pragma unroll
+                for (int k = 0; k < K; ++k) {
+                    Hin[k] += kRebaseAdd;
+                    Dn[k] += kRebaseAdd;
+                }
+                hd += kRebaseAdd;
+                pubF += kRebaseAdd;
+                pubH += kRebaseAdd;
+            }
+        }
         // group-start inputs for row t+1: I~(r,1) and H~(r,0) (same for A and B)
         const int32_t rb = t + 1;
-        const int32_t bF = is_col1(sc, (uint32_t)rb) + alpha * rb + beta;
-        const int32_t bH = hs_col0(sc, (uint32_t)rb) + alpha * rb;
+        const int32_t bF = is_col1(sc, (uint32_t)rb) + alpha * rb + beta - base;
+        const int32_t bH = hs_col0(sc, (uint32_t)rb) + alpha * rb - base;
         const uint32_t inF = gshift<G>(pkb(bF, bF), pubF, gstart);
         const uint32_t inH = gshift<G>(pkb(bH, bH), pubH, gstart);
         if (r >= 1 && r <= ldM) {
@@ -1241,14 +1268,14 @@ __global__ __launch_bounds__(256) void nw_fill_pk_kernel(Src src, uint32_t count
 #pragma unroll
                 for (int k = 0; k < K; ++k)
                     if (k == kA) e = (int32_t)(Hout[k] & 0xFFFFu) - 32768;
-                src.end(ia, pa, e - alpha * ldA - beta * lqA);
+                src.end(ia, pa, e + base - alpha * ldA - beta * lqA);
             }
             if (t == tEB) {
                 int32_t e = 0;
 #pragma unroll
                 for (int k = 0; k < K; ++k)
                     if (k == kB) e = (int32_t)(Hout[k] >> 16) - 32768;
-                src.end(ib, pb, e - alpha * ldB - beta * lqB);
+                src.end(ib, pb, e + base - alpha * ldB - beta * lqB);
             }
         } else if (&Hout != &Hin) {
 #pragma unroll
@@ -1511,6 +1538,10 @@ constexpr bool kPacked[kNumVariants] = {false, false, false, false, true, true, 
 #endif
 constexpr uint32_t kFillG[kNumVariants] = {16, 16, 64, 64, 8, 16, 32, SALN_V7_NARROW ? 8u : 16u};
 
+// Dynamic LDS cap of the packed fill's staged db rows: two workgroups per CU.
+constexpr size_t kPackedLdsMax = 80 * 1024;
+static bool packed_ok(uint32_t lq, uint32_t ld, const Scoring &sc);
+
 template <int G, int K>
 static void fill_i32(dim3 grid, hipStream_t s, const NwPairDesc *pairs, uint32_t first,
                      uint32_t count, const uint8_t *qs, const uint8_t *ds, uint8_t *mask,
@@ -1521,37 +1552,58 @@ static void fill_i32(dim3 grid, hipStream_t s, const NwPairDesc *pairs, uint32_t
 }
 
 template <int G, int K, int KS = K>
-static void fill_pk(dim3 grid, hipStream_t s, const NwPairDesc *pairs, uint32_t first,
-                    uint32_t count, const uint8_t *qs, const uint8_t *ds, uint8_t *mask,
-                    int32_t *end_h, saln_nw_result *, uint32_t *, Scoring sc, int codes,
-                    uint32_t ld_max) {
+static hipError_t fill_pk(dim3 grid, hipStream_t s, const NwPairDesc *pairs, uint32_t first,
+                          uint32_t count, const uint8_t *qs, const uint8_t *ds, uint8_t *mask,
+                          int32_t *end_h, saln_nw_result *, uint32_t *, Scoring sc, int codes,
+                          uint32_t ld_max, bool rebase) {
     static const size_t pad = [] {  // experiment switch: LDS floor per workgroup (occupancy)
         const char *e = std::getenv("SALN_FILL_LDS_MIN");
         return e ? (size_t)std::atol(e) : (size_t)0;
     }();
     const size_t lds = std::max((size_t)(256 / G) * (ld_max + 2 * G) * sizeof(uint32_t), pad);
+    if (lds > kPackedLdsMax) return hipErrorInvalidValue;  // choose_variant keeps ld below this
     const PlanSrc src{pairs, first, end_h};
-    if (codes == kCodesFull)
-        nw_fill_pk_kernel<G, K, kCodesFull, PlanSrc, KS><<<grid, dim3(256), lds, s>>>(src, count, qs, ds, mask,
-                                                                           sc, ld_max);
-    else if (codes == kCodesNone)
-        nw_fill_pk_kernel<G, K, kCodesNone, PlanSrc, KS><<<grid, dim3(256), lds, s>>>(src, count, qs, ds, mask,
-                                                                           sc, ld_max);
-    else
-        nw_fill_pk_kernel<G, K, kCodesWalk, PlanSrc, KS><<<grid, dim3(256), lds, s>>>(src, count, qs, ds, mask,
-                                                                           sc, ld_max);
+    auto go = [&](auto codes_c, auto rebase_c) -> hipError_t {
+        const auto kern = nw_fill_pk_kernel<G, K, decltype(codes_c)::value, PlanSrc, KS,
+                                            decltype(rebase_c)::value>;
+        if (lds > 65536) {
+            const hipError_t e = hipFuncSetAttribute((const void *)kern,
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                     (int)kPackedLdsMax);
+            if (e != hipSuccess) return e;
+        }
+        kern<<<grid, dim3(256), lds, s>>>(src, count, qs, ds, mask, sc, ld_max);
+        return hipSuccess;
+    };
+    auto by_codes = [&](auto rebase_c) {
+        if (codes == kCodesFull) return go(std::integral_constant<int, kCodesFull>{}, rebase_c);
+        if (codes == kCodesNone) return go(std::integral_constant<int, kCodesNone>{}, rebase_c);
+        return go(std::integral_constant<int, kCodesWalk>{}, rebase_c);
+    };
+    return rebase ? by_codes(std::true_type{}) : by_codes(std::false_type{});
 }
 
 template <int G, int K>
-static void avsa_pk(const AvsaSrc &src, uint32_t count, const uint8_t *qs, const uint8_t *ds,
-                    Scoring sc, uint32_t ld_max, hipStream_t s) {
+static hipError_t avsa_pk(const AvsaSrc &src, uint32_t count, const uint8_t *qs, const uint8_t *ds,
+                          Scoring sc, uint32_t ld_max, hipStream_t s) {
     constexpr uint32_t gpb = 256 / G;
     const uint32_t sup = 8 * blocks_per_pack(2 * gpb);
     const uint32_t groups = (count + 1) / 2;
     const dim3 grid(((groups + gpb - 1) / gpb + sup - 1) / sup * sup);
     const size_t lds = (size_t)gpb * (ld_max + 2 * G) * sizeof(uint32_t);
-    nw_fill_pk_kernel<G, K, kCodesNone, AvsaSrc, K><<<grid, dim3(256), lds, s>>>(
-        src, count, qs, ds, nullptr, sc, ld_max);
+    if (lds > kPackedLdsMax) return hipErrorInvalidValue;
+    auto go = [&](auto rebase_c) -> hipError_t {
+        const auto kern = nw_fill_pk_kernel<G, K, kCodesNone, AvsaSrc, K, decltype(rebase_c)::value>;
+        if (lds > 65536) {
+            const hipError_t e = hipFuncSetAttribute((const void *)kern,
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                     (int)kPackedLdsMax);
+            if (e != hipSuccess) return e;
+        }
+        kern<<<grid, dim3(256), lds, s>>>(src, count, qs, ds, nullptr, sc, ld_max);
+        return hipSuccess;
+    };
+    return packed_ok(G * K, ld_max, sc) ? go(std::false_type{}) : go(std::true_type{});
 }
 
 // Score-only all-vs-all over one packed query class (variant 4-7): pairs
@@ -1563,17 +1615,19 @@ hipError_t launch_avsa(int variant, const uint64_t *q_off, const uint64_t *d_off
                        hipStream_t stream) {
     if (!count) return hipSuccess;
     const AvsaSrc src{q_off, d_off, q_ids, d_ids, nq, nq_total, base, out};
+    hipError_t e;
     switch (variant) {
-        case 4: avsa_pk<8, 19>(src, count, qs, ds, sc, ld_max, stream); break;
-        case 5: avsa_pk<16, 16>(src, count, qs, ds, sc, ld_max, stream); break;
-        case 6: avsa_pk<32, 16>(src, count, qs, ds, sc, ld_max, stream); break;
+        case 4: e = avsa_pk<8, 19>(src, count, qs, ds, sc, ld_max, stream); break;
+        case 5: e = avsa_pk<16, 16>(src, count, qs, ds, sc, ld_max, stream); break;
+        case 6: e = avsa_pk<32, 16>(src, count, qs, ds, sc, ld_max, stream); break;
 #if SALN_V7_NARROW
-        case 7: avsa_pk<8, 20>(src, count, qs, ds, sc, ld_max, stream); break;
+        case 7: e = avsa_pk<8, 20>(src, count, qs, ds, sc, ld_max, stream); break;
 #else
-        case 7: avsa_pk<16, 10>(src, count, qs, ds, sc, ld_max, stream); break;
+        case 7: e = avsa_pk<16, 10>(src, count, qs, ds, sc, ld_max, stream); break;
 #endif
         default: return hipErrorInvalidValue;
     }
+    if (e != hipSuccess) return e;
     return hipGetLastError();
 }
 
@@ -1631,20 +1685,24 @@ hipError_t launch_fill(int variant, const NwPairDesc *pairs, uint32_t first, uin
     const uint32_t groups = kPacked[variant] ? (count + 1) / 2 : count;
     const uint32_t sup = 8 * blocks_per_pack(kPacked[variant] ? 2 * gpb : gpb);
     const dim3 grid(((groups + gpb - 1) / gpb + sup - 1) / sup * sup);
+    // packed pairs beyond one int16 frame (packed_ok_rebase) take the rebasing fill
+    const bool rebase = kPacked[variant] && !packed_ok(kVariants[variant].W(), ld_max, sc);
+    hipError_t e = hipSuccess;
     switch (variant) {
         case 0: fill_i32<16, 10>(grid, stream, pairs, first, count, qs, ds, mask, scratch, end_h, res, cig, sc); break;
         case 1: fill_i32<16, 16>(grid, stream, pairs, first, count, qs, ds, mask, scratch, end_h, res, cig, sc); break;
         case 2: fill_i32<64, 8>(grid, stream, pairs, first, count, qs, ds, mask, scratch, end_h, res, cig, sc); break;
         case 3: return hipErrorInvalidValue;  // stripes: launch_fill_stripes
-        case 4: fill_pk<8, 19>(grid, stream, pairs, first, count, qs, ds, mask, end_h, res, cig, sc, codes, ld_max); break;
-        case 5: fill_pk<16, 16>(grid, stream, pairs, first, count, qs, ds, mask, end_h, res, cig, sc, codes, ld_max); break;
+        case 4: e = fill_pk<8, 19>(grid, stream, pairs, first, count, qs, ds, mask, end_h, res, cig, sc, codes, ld_max, rebase); break;
+        case 5: e = fill_pk<16, 16>(grid, stream, pairs, first, count, qs, ds, mask, end_h, res, cig, sc, codes, ld_max, rebase); break;
 #if SALN_V7_NARROW
-        case 7: fill_pk<8, 20, 10>(grid, stream, pairs, first, count, qs, ds, mask, end_h, res, cig, sc, codes, ld_max); break;
+        case 7: e = fill_pk<8, 20, 10>(grid, stream, pairs, first, count, qs, ds, mask, end_h, res, cig, sc, codes, ld_max, rebase); break;
 #else
-        case 7: fill_pk<16, 10>(grid, stream, pairs, first, count, qs, ds, mask, end_h, res, cig, sc, codes, ld_max); break;
+        case 7: e = fill_pk<16, 10>(grid, stream, pairs, first, count, qs, ds, mask, end_h, res, cig, sc, codes, ld_max, rebase); break;
 #endif
-        default: fill_pk<32, 16>(grid, stream, pairs, first, count, qs, ds, mask, end_h, res, cig, sc, codes, ld_max); break;
+        default: e = fill_pk<32, 16>(grid, stream, pairs, first, count, qs, ds, mask, end_h, res, cig, sc, codes, ld_max, rebase); break;
     }
+    if (e != hipSuccess) return e;
     return hipGetLastError();
 }
 
@@ -1719,15 +1777,42 @@ Geom variant_geom(int v) { return kVariants[v]; }
 bool variant_packed(int v) { return kPacked[v]; }
 
 // Packed i16 is exact while every value and every same-cell difference stays
-// inside int16 with the position offsets of nw_fill_pk_kernel (see there).
-static bool packed_ok(uint32_t lq, uint32_t ld, const Scoring &sc) {
+// inside int16 with the position offsets of nw_fill_pk_kernel (see there):
+// `rows` rows of growth a and lq columns of growth b from the frame's origin.
+static bool packed_range_ok(uint32_t lq, uint32_t rows, const Scoring &sc) {
     const int64_t pen = 2ll * (sc.match - sc.mismatch);
     // pen >= 2: the q==d bit comes from the penalty (0 or pen in each half)
     if (pen < 2 || pen > 32 || sc.gap_extend > 0 || sc.gap_open > 0) return false;
     const int64_t span = std::max<int64_t>(
         {std::abs(sc.match), std::abs(sc.mismatch), std::abs(sc.gap_open) + std::abs(sc.gap_extend)});
     const int64_t a = 2 * (std::abs(sc.match) + std::abs(sc.gap_extend)) + 2 * span;
-    return (int64_t)ld * a + (int64_t)lq * (2 * std::abs(sc.gap_extend) + 2 * span) + 256 < 30000;
+    return (int64_t)rows * a + (int64_t)lq * (2 * std::abs(sc.gap_extend) + 2 * span) + 256 < 30000;
+}
+static bool packed_ok(uint32_t lq, uint32_t ld, const Scoring &sc) {
+    return packed_range_ok(lq, ld, sc);
+}
+// The rebasing fill (kRebase).  At step t a lane's value is
+// X~(r,c) - drift * r0 with r in [r0 - G, r0 + kRebaseSteps) and
+//   X~(r,c) - drift*r0 = [X~(r,c) - X~(r,0)] + [X~(r,0) - drift*r] + drift*(r - r0):
+// the first term lies in [2*go, c*(2|m| + 4|ge|)] (a row's H exceeds its
+// column-0 value by at most c*(m - ge), the c columns' diagonal gain over the
+// gap it replaces, and falls below it by at most a gap; beta*c on top), the
+// second is the constant 2*(go + ge) + 1 while hs_col0 is linear (ld <= 4096
+// and |go| + 4097*|ge| < 2^15: the sentinel floor is not reached), the third
+// is at most |drift| * (period + G).  M / I / D sit within an open + extend +
+// penalty of H.  The db length is also bounded by the staged rows
+// (kPackedLdsMax).
+static bool packed_ok_rebase(uint32_t lq, uint32_t ld, const Scoring &sc, uint32_t G, uint32_t W) {
+    const int64_t pen = 2ll * (sc.match - sc.mismatch);
+    if (pen < 2 || pen > 32 || sc.gap_extend > 0 || sc.gap_open > 0 || lq > W) return false;
+    const uint32_t gpb = 256 / G;
+    if ((size_t)gpb * (ld + 2 * G) * sizeof(uint32_t) > kPackedLdsMax || ld > 4096) return false;
+    const int64_t m = std::abs(sc.match), ge = std::abs(sc.gap_extend), go = std::abs(sc.gap_open);
+    if (go + 4097 * ge >= 32768) return false;
+    const int64_t drift = std::abs(2 * sc.gap_extend - 2 * sc.match + 2 * sc.gap_extend);
+    const int64_t bound = (kRebaseSteps + (int64_t)G) * drift + (int64_t)W * (2 * m + 4 * ge) +
+                          4 * (go + ge) + 2 * pen + 512;
+    return bound < 30000;
 }
 
 int choose_variant(uint32_t len_q, uint32_t len_db, const Scoring &sc) {
@@ -1740,6 +1825,11 @@ int choose_variant(uint32_t len_q, uint32_t len_db, const Scoring &sc) {
         if (len_q <= 160) return 7;
         if (len_q <= 256) return 5;
         if (len_q <= 512) return 6;
+    }
+    // longer db: the same packed variants with a rebasing int16 frame
+    for (const int v : {7, 5, 6}) {
+        const Geom g = kVariants[v];
+        if (len_q <= g.W() && packed_ok_rebase(len_q, len_db, sc, g.G, g.W())) return v;
     }
     if (len_q <= 160) return 0;
     if (len_q <= 256) return 1;

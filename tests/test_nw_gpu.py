@@ -238,6 +238,38 @@ def test_score_only_plan_matches_full(saln):
     fast.close()
 
 
+def test_packed_rebase_shapes(saln, oracle):
+    """Pairs past one int16 frame (db up to 1,248 rows for <= 256 query
+    columns, 2,496 for <= 512) run through the packed fill with its rebasing
+    frame: identical and embedded pairs (the largest in-frame excursions:
+    the diagonal gains while column 0 drifts), random and two-letter pairs;
+    scores, end states, panics, first alignment and the full parent mask
+    equal the oracle's, alone and in one batch."""
+    from sequencealigning_amd import synth
+    rng = np.random.default_rng(777)
+    cases = []
+    base = synth.random_bases(900, 2500).tobytes()
+    cases.append((base[:512], base[:512]))                      # identical 512 x 512
+    cases.append((base[700:1212], base[:2000]))                 # embedded 512 in 2,000
+    cases.append((base[300:450], base[:1248]))                  # embedded 150 in 1,248
+    cases.append((rand_seq(rng, 256), rand_seq(rng, 1200)))     # random 256 x 1,200
+    cases.append((bytes(rng.choice([65, 67], 160).astype(np.uint8)),
+                  bytes(rng.choice([65, 67], 1000).astype(np.uint8))))  # two-letter
+    q, d = synth.mut_pair(600, 0.05, 4242)
+    cases.append((q[:300], d[:650]))                            # mutated prefix pair
+    for q, d in cases:
+        _compare(saln, oracle, q, d, text=False)
+    res, cig = saln.nw_align_batch([q for q, _ in cases] + [b"ACGT" * 30],
+                                   [d for _, d in cases] + [b"ACGA" * 30],
+                                   pairs=[(k, k) for k in range(len(cases) + 1)])
+    for k, (q, d) in enumerate(cases + [(b"ACGT" * 30, b"ACGA" * 30)]):
+        o = oracle.nw(q, d, literal_dfs=False)
+        assert int(res["score"][k]) == o.score, k
+        assert int(res["end_states"][k]) == o.end_states, k
+        assert (int(res["status"][k]) == 2) == o.panics, k
+        assert (saln.cigar_ops_string(cig[k]) if res["printed"][k] else None) == o.first_ops, k
+
+
 @pytest.mark.parametrize("L", [3000])
 def test_long_pair_stripes(saln, oracle, L):
     """A single long mutated pair through the column-stripe fill (12 stripes of
