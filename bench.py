@@ -27,6 +27,7 @@ sys.path.insert(0, ROOT)
 
 METRIC = "GCUPS (affine-gap NW) at 1/2/4/8 MI355X; % of HBM roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+VALU_PEAK_TOPS = 1024 * 16 * 2.4e9 / 1e12  # 39.3: 256 CUs x 4 SIMDs x 16 lanes x 2.4 GHz
 N_PAIRS, LQ, LD = 100_000, 150, 150
 SEED = 0x5EED0002
 
@@ -76,8 +77,9 @@ def cpu_baseline(budget_s: float = 12.0) -> dict:
                       f"fill + literal DFS (<=1e5 pops/pair)"}
 
 
-def pmc_traffic(kernel: str):
-    """HBM bytes per launch of `kernel` from the committed PMC summary
+def pmc_traffic(kernel: str, field: str = "hbm_bytes"):
+    """A per-launch PMC figure of `kernel` (HBM bytes, or VALU wave-instructions
+    with field="valu_wave_insts") from the committed PMC summary
     (profiles/pmc_traffic.json, written by tools/pmc_traffic.py from the
     rocprofv3 --pmc passes of tools/pmc.sh on this workload), or None."""
     try:
@@ -87,8 +89,22 @@ def pmc_traffic(kernel: str):
         return None
     for name, v in doc.get("kernels", {}).items():
         if kernel in name:
-            return v.get("hbm_bytes")
+            return v.get(field)
     return None
+
+
+def valu_roof(kernel: str, avg_s: float):
+    """SURVEY.md 8(d) asks for the VALU fraction beside the HBM one: the fill's
+    VALU wave-instructions per launch (PMC SQ_INSTS_VALU) x 64 lanes over its
+    measured duration, against 1,024 SIMDs x 16 lanes x 2.4 GHz (one wave64
+    instruction per 4 cycles per SIMD; the 2-cycle ops the kernel favours can
+    exceed that rate, so frac may approach or pass 1 when issue-bound)."""
+    n = pmc_traffic(kernel, "valu_wave_insts")
+    if not n:
+        return None
+    achieved = n * 64 / avg_s / 1e12
+    return {"wave_insts_per_launch": n, "achieved": round(achieved, 2),
+            "peak": VALU_PEAK_TOPS, "unit": "T int lane-ops/s", "frac": round(achieved / VALU_PEAK_TOPS, 4)}
 
 
 def main() -> None:
@@ -213,7 +229,9 @@ def main() -> None:
                          "kernel_avg_ms": round(fill_avg_s * 1e3, 4),
                          "traceback_avg_ms": round(tb_ms / max(1, tb_n), 4),
                          "execute_avg_ms": round(ex_ms / max(1, ex_n), 4),
-                         "pipelined": pipelined},
+                         "pipelined": pipelined,
+                         "valu": valu_roof("nw_fill_pk_kernel<16, 10,", fill_avg_s)
+                         if not args.score_only else None},
             "status_counts": {"ok": int(statuses[0]), "ref_panic_boundary": int(statuses[2])},
         }
         if not args.no_cpu_baseline:

@@ -22,7 +22,7 @@
 namespace saln {
 
 constexpr int32_t kSentinel = -32768;  // i16::MIN as i32, needleman_wunsch_affine.rs:174
-constexpr int kNumVariants = 8;        // fill kernel variants (nw_kernels.hip)
+constexpr int kNumVariants = 9;        // fill kernel variants (nw_kernels.hip)
 
 struct Scoring {
     int32_t match, mismatch, gap_open, gap_extend;

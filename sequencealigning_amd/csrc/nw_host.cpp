@@ -195,6 +195,23 @@ int saln_nw_plan_create(saln_context *ctx, const uint64_t *q_off, uint64_t n_q,
         p->cells += lq * ld;
     }
     p->cigar_off[n_pairs] = cig;
+    {
+        // Queries of 513-1,024 columns: the 64-lane packed variant is the
+        // throughput choice (two pairs per wave), the column stripes the
+        // latency choice (four waves per pair, pipelined): a plan with few
+        // such pairs keeps them on stripes.
+        static const uint64_t v8_min = [] {
+            const char *e = std::getenv("SALN_V8_MIN_PAIRS");  // experiment switch
+            return e ? (uint64_t)std::atoll(e) : (uint64_t)kWidePackedMinPairs;
+        }();
+        uint64_t wide = 0;
+        for (const NwPairDesc &d : descs)
+            wide += d.variant == (uint32_t)kWidePackedVariant && d.len_q > 512;
+        if (wide && wide < v8_min)
+            for (NwPairDesc &d : descs)
+                if (d.variant == (uint32_t)kWidePackedVariant && d.len_q > 512)
+                    d.variant = (uint32_t)kStripeVariant;
+    }
     // plan order: fill pairs grouped by variant, then by query chunk count,
     // longest db first (balances the groups of a block and keeps the pairs of
     // a mask pack alike); pairs with an empty side last (traceback only).

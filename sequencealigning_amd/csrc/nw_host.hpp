@@ -29,6 +29,8 @@ hipError_t launch_fill_stripes(const NwPairDesc *pairs, const uint2 *work, uint3
                                Scoring sc, int codes /* 0 walk, 1 full, 2 none */,
                                hipStream_t stream);
 constexpr int kStripeVariant = 3;
+constexpr int kWidePackedVariant = 8;        // packed, 64-lane groups, up to 1,024 columns
+constexpr uint64_t kWidePackedMinPairs = 1536;  // fewer such pairs: column stripes (measured crossover 1,024-2,048)
 hipError_t launch_score_results(const NwPairDesc *pairs, uint32_t first, uint32_t n,
                                 const int32_t *end_h, saln_nw_result *results, Scoring sc,
                                 hipStream_t stream);

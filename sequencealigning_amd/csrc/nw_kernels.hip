@@ -1040,6 +1040,14 @@ struct AvsaSrc {
 // codes compare values of one cell (frame-free); group-start inputs and end
 // values convert with r0(t).
 constexpr int kRebaseSteps = 64;
+// The column term of the frame bound is one-sided (a row's values exceed its
+// column-0 value by up to c*(2|m| + 4|ge|) and fall below it by at most a
+// small constant): the frame is centred on half the widest chunk's term.
+__host__ __device__ inline int32_t rebase_center(const Scoring &sc, int32_t W) {
+    const int32_t m = sc.match < 0 ? -sc.match : sc.match;
+    const int32_t ge = sc.gap_extend < 0 ? -sc.gap_extend : sc.gap_extend;
+    return (W * (2 * m + 4 * ge) / 2) & ~1;
+}
 
 template <int G, int K, int kCodes, typename Src, int KS, bool kRebase = false>
 __global__ __launch_bounds__(256) void nw_fill_pk_kernel(Src src, uint32_t count,
@@ -1079,6 +1087,7 @@ __global__ __launch_bounds__(256) void nw_fill_pk_kernel(Src src, uint32_t count
     const uint32_t kDstep = cst2(2 * sc.gap_extend + alpha);
     const int32_t drift = 2 * sc.gap_extend + alpha;  // column-0 X~ per row (kRebase)
     const uint32_t kRebaseAdd = cst2(-drift * kRebaseSteps);
+    const int32_t ctr = kRebase ? rebase_center(sc, G * K) : 0;  // frame centring (kRebase)
     const bool gstart = lane == 0;
 
     const int col0 = lane * K;  // my columns: col0+1 .. col0+K
@@ -1091,13 +1100,13 @@ __global__ __launch_bounds__(256) void nw_fill_pk_kernel(Src src, uint32_t count
         const uint32_t ca = j <= lqA ? (uint32_t)qA[j - 1] << 5 : 0xE000u;
         const uint32_t cb = j <= lqB ? (uint32_t)qB[j - 1] << 5 : 0xE000u;
         qc[k] = ca | (cb << 16);
-        const int32_t h0 = hs_row0(sc, (uint32_t)j) + beta * j;           // H~(0, j)
-        const int32_t d1 = ds_row1(sc, (uint32_t)j) + alpha + beta * j;   // D~(1, j)
+        const int32_t h0 = hs_row0(sc, (uint32_t)j) + beta * j - ctr;     // H~(0, j)
+        const int32_t d1 = ds_row1(sc, (uint32_t)j) + alpha + beta * j - ctr;  // D~(1, j)
         Hp[k] = pkb(h0, h0);
         Dn[k] = pkb(d1, d1);
     }
-    uint32_t hd = pkb(hs_row0(sc, (uint32_t)col0) + beta * col0,
-                      hs_row0(sc, (uint32_t)col0) + beta * col0);  // H~(r-1, col0)
+    uint32_t hd = pkb(hs_row0(sc, (uint32_t)col0) + beta * col0 - ctr,
+                      hs_row0(sc, (uint32_t)col0) + beta * col0 - ctr);  // H~(r-1, col0)
     uint32_t pubF = 0, pubH = 0;
     // db chars of both pairs, staged once per group in LDS as the packed
     // (A << 5 | B << 21) word of each row; a step reads its row's word from
@@ -1139,7 +1148,7 @@ __global__ __launch_bounds__(256) void nw_fill_pk_kernel(Src src, uint32_t count
         const uint32_t dch = rowp[t];
         int32_t base = 0;  // frame of step t (kRebase)
         if constexpr (kRebase) {
-            base = drift * (t & -kRebaseSteps);
+            base = drift * (t & -kRebaseSteps) + ctr;
             if ((t & (kRebaseSteps - 1)) == 0 && t > 0) {  // wave-uniform
 #pragma unroll
                 for (int k = 0; k < K; ++k) {
@@ -1526,8 +1535,8 @@ hipError_t launch_score_results(const NwPairDesc *pairs, uint32_t first, uint32_
 // ----------------------------------------------------------------- launchers
 // variants 0-3: i32 lanes; 4-6: packed i16 (two pairs per lane)
 constexpr Geom kVariants[kNumVariants] = {{16, 10}, {16, 16}, {64, 8}, {64, 4},
-                                          {8, 19},  {16, 16}, {32, 16}, {16, 10}};
-constexpr bool kPacked[kNumVariants] = {false, false, false, false, true, true, true, true};
+                                          {8, 19},  {16, 16}, {32, 16}, {16, 10}, {64, 16}};
+constexpr bool kPacked[kNumVariants] = {false, false, false, false, true, true, true, true, true};
 // Lanes per pair of each variant's fill kernel.  SALN_V7_NARROW fills
 // variant 7 (<= 160 columns, layout 16 lanes x 10 columns) with 8-lane groups
 // of 20 columns: half the pipeline skew and the per-step overhead over twice
@@ -1536,7 +1545,7 @@ constexpr bool kPacked[kNumVariants] = {false, false, false, false, true, true, 
 #ifndef SALN_V7_NARROW
 #define SALN_V7_NARROW 0
 #endif
-constexpr uint32_t kFillG[kNumVariants] = {16, 16, 64, 64, 8, 16, 32, SALN_V7_NARROW ? 8u : 16u};
+constexpr uint32_t kFillG[kNumVariants] = {16, 16, 64, 64, 8, 16, 32, SALN_V7_NARROW ? 8u : 16u, 64};
 
 // Dynamic LDS cap of the packed fill's staged db rows: two workgroups per CU.
 constexpr size_t kPackedLdsMax = 80 * 1024;
@@ -1625,6 +1634,7 @@ hipError_t launch_avsa(int variant, const uint64_t *q_off, const uint64_t *d_off
 #else
         case 7: e = avsa_pk<16, 10>(src, count, qs, ds, sc, ld_max, stream); break;
 #endif
+        case 8: e = avsa_pk<64, 16>(src, count, qs, ds, sc, ld_max, stream); break;
         default: return hipErrorInvalidValue;
     }
     if (e != hipSuccess) return e;
@@ -1700,6 +1710,7 @@ hipError_t launch_fill(int variant, const NwPairDesc *pairs, uint32_t first, uin
 #else
         case 7: e = fill_pk<16, 10>(grid, stream, pairs, first, count, qs, ds, mask, end_h, res, cig, sc, codes, ld_max, rebase); break;
 #endif
+        case 8: e = fill_pk<64, 16>(grid, stream, pairs, first, count, qs, ds, mask, end_h, res, cig, sc, codes, ld_max, rebase); break;
         default: e = fill_pk<32, 16>(grid, stream, pairs, first, count, qs, ds, mask, end_h, res, cig, sc, codes, ld_max, rebase); break;
     }
     if (e != hipSuccess) return e;
@@ -1742,6 +1753,7 @@ hipError_t launch_traceback(int variant, const NwPairDesc *pairs, uint32_t first
         case 5: tb_lds<16, 16>(grid, stream, pairs, first, n, mask, end_h, ops, results, cigar, sc); break;
         case 6: tb_lds<32, 16>(grid, stream, pairs, first, n, mask, end_h, ops, results, cigar, sc); break;
         case 7: tb_lds<16, 10>(grid, stream, pairs, first, n, mask, end_h, ops, results, cigar, sc); break;
+        case 8: tb_lds<64, 16>(grid, stream, pairs, first, n, mask, end_h, ops, results, cigar, sc); break;
         default: {  // variant 4 (20-byte segments) and empty-side pairs
             GeomTable gt;
             for (int v = 0; v < kNumVariants; ++v) gt.g[v] = kVariants[v];
@@ -1810,8 +1822,10 @@ static bool packed_ok_rebase(uint32_t lq, uint32_t ld, const Scoring &sc, uint32
     const int64_t m = std::abs(sc.match), ge = std::abs(sc.gap_extend), go = std::abs(sc.gap_open);
     if (go + 4097 * ge >= 32768) return false;
     const int64_t drift = std::abs(2 * sc.gap_extend - 2 * sc.match + 2 * sc.gap_extend);
-    const int64_t bound = (kRebaseSteps + (int64_t)G) * drift + (int64_t)W * (2 * m + 4 * ge) +
-                          4 * (go + ge) + 2 * pen + 512;
+    // column term [-(2go + 1), W*(2m + 4ge) + 2(go + ge)] centred by rebase_center
+    const int64_t col = (int64_t)W * (2 * m + 4 * ge);
+    const int64_t half = std::max<int64_t>(col - rebase_center(sc, (int32_t)W), rebase_center(sc, (int32_t)W));
+    const int64_t bound = half + (kRebaseSteps + (int64_t)G) * drift + 4 * (go + ge) + 2 * pen + 512;
     return bound < 30000;
 }
 
@@ -1826,11 +1840,14 @@ int choose_variant(uint32_t len_q, uint32_t len_db, const Scoring &sc) {
         if (len_q <= 256) return 5;
         if (len_q <= 512) return 6;
     }
-    // longer db: the same packed variants with a rebasing int16 frame
+    // longer db: the same packed variants with a rebasing int16 frame; 513 to
+    // 1,024 query columns in 64-lane groups (narrower queries would leave
+    // most of those lanes idle: the i32 lanes are faster for them)
     for (const int v : {7, 5, 6}) {
         const Geom g = kVariants[v];
         if (len_q <= g.W() && packed_ok_rebase(len_q, len_db, sc, g.G, g.W())) return v;
     }
+    if (len_q > 512 && packed_ok_rebase(len_q, len_db, sc, 64, 1024)) return 8;
     if (len_q <= 160) return 0;
     if (len_q <= 256) return 1;
     if (len_q <= 512) return 2;

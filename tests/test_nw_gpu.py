@@ -270,6 +270,40 @@ def test_packed_rebase_shapes(saln, oracle):
         assert (saln.cigar_ops_string(cig[k]) if res["printed"][k] else None) == o.first_ops, k
 
 
+def test_wide_packed_variant(saln, oracle):
+    """Queries of 513-1,024 columns in 64-lane packed groups with the centred
+    rebasing frame when a plan holds many of them, through the column stripes
+    when it holds few (a short query against a db past the narrow variants'
+    staged rows rides along on the i32 lanes).  All give the oracle's score,
+    end states, panics and first alignment."""
+    from sequencealigning_amd import synth
+    rng = np.random.default_rng(888)
+    base = synth.random_bases(901, 4200).tobytes()
+    cases = [(base[:1024], base[:1024]),                                  # identical 1,024
+             (base[1000:1800], base[:3000]),                              # embedded 800 in 3,000
+             (rand_seq(rng, 700), rand_seq(rng, 650)),
+             (bytes(rng.choice([65, 67], 600).astype(np.uint8)),
+              bytes(rng.choice([65, 67], 620).astype(np.uint8))),
+             (rand_seq(rng, 150), rand_seq(rng, 3000))]                   # long db, short query
+    q, d = synth.mut_pair(1000, 0.05, 4343)
+    cases.append((q, d))
+    want = [oracle.nw(q, d, literal_dfs=False) for q, d in cases]
+    for q, d in cases[2:4]:
+        _compare(saln, oracle, q, d, text=False)                          # full parent mask
+    reps = 1600 // 5 + 1   # five wide queries per round: > kWidePackedMinPairs, the packed variant
+    for n in (1, reps):
+        qs = [q for q, _ in cases] * n
+        ds = [d for _, d in cases] * n
+        res, cig = saln.nw_align_batch(qs, ds, pairs=[(k, k) for k in range(len(qs))])
+        for k in range(len(qs)):
+            o = want[k % len(cases)]
+            assert int(res["score"][k]) == o.score, (n, k)
+            assert int(res["end_states"][k]) == o.end_states, (n, k)
+            assert (int(res["status"][k]) == 2) == o.panics, (n, k)
+            if k < 2 * len(cases):
+                assert (saln.cigar_ops_string(cig[k]) if res["printed"][k] else None) == o.first_ops, (n, k)
+
+
 @pytest.mark.parametrize("L", [3000])
 def test_long_pair_stripes(saln, oracle, L):
     """A single long mutated pair through the column-stripe fill (12 stripes of
@@ -323,7 +357,7 @@ def test_long_pairs_cooperative_walker(saln, oracle, packed):
     from sequencealigning_amd import synth
     rng = np.random.default_rng(4242)
     qs, ds = [], []
-    shapes = [(600, 590), (1300, 1280), (800, 1100), (1500, 700), (520, 530), (2000, 1900)]
+    shapes = [(1100, 1090), (1300, 1280), (1030, 1500), (1500, 700), (1025, 1030), (2000, 1900)]
     for k, (lq, ld) in enumerate(shapes):
         if k % 3 == 0:
             q = synth.random_bases(100 + k, lq).tobytes()

@@ -14,7 +14,7 @@ timeout -k 10 600 python bench.py --steps 20 --warmup 3 > $O/bench.log 2>&1 || {
 tail -1 $O/bench.log
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $O/prof -o run --output-format csv -- python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline > $O/prof.log 2>&1 || { tail -20 $O/prof.log; exit 1; }
 tail -1 $O/prof.log
-PMC_SETS="FETCH_SIZE;WRITE_SIZE" bash tools/pmc.sh > $O/pmc.log 2>&1 || { tail -20 $O/pmc.log; exit 1; }
+PMC_SETS="FETCH_SIZE;WRITE_SIZE;SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU" bash tools/pmc.sh > $O/pmc.log 2>&1 || { tail -20 $O/pmc.log; exit 1; }
 python3 tools/pmc_traffic.py gpurun_out/pmc $O/pmc_traffic.json > /dev/null || exit 1
 cat $O/pmc_traffic.json
 timeout -k 10 300 python tools/bench_long.py --len 1000 --reps 5 > $O/long1k.log 2>&1 || exit 1

@@ -1,4 +1,5 @@
-"""HBM traffic per launch from the rocprofv3 --pmc passes of tools/pmc.sh.
+"""HBM traffic (and, when that pass ran, VALU / SALU instruction counts) per
+launch from the rocprofv3 --pmc passes of tools/pmc.sh.
 
 FETCH_SIZE / WRITE_SIZE are in KiB per dispatch.  On gfx950 FETCH_SIZE counts
 half the bytes of wide streaming reads (MI355X_MICROARCH.md, HBM section), so
@@ -28,6 +29,10 @@ def main(d="gpurun_out/pmc", out="profiles/pmc_traffic.json", tag=""):
         write = sum(cs["WRITE_SIZE"]) / len(cs["WRITE_SIZE"]) * 1024
         res[k] = {"read_bytes": round(fetch), "write_bytes": round(write),
                   "hbm_bytes": round(fetch + write), "dispatches": len(cs["FETCH_SIZE"])}
+        for c, key in (("SQ_INSTS_VALU", "valu_wave_insts"), ("SQ_INSTS_SALU", "salu_wave_insts"),
+                       ("SQ_WAVES", "waves")):
+            if c in cs:  # per-launch means of the instruction-count pass
+                res[k][key] = round(sum(cs[c]) / len(cs[c]))
     doc = {"source": "tools/pmc.sh (rocprofv3 --pmc, one counter group per pass) on "
                      "tools/prof_nw.py: 100000 x 150x150 G-iid pairs, seed 0x5EED0002",
            "round": tag, "kernels": res}
