@@ -1114,11 +1114,18 @@ __global__ __launch_bounds__(256) void nw_fill_pk_kernel(Src src, uint32_t count
     // mask stores (vmcnt).  Rows are padded by G words on both sides, so the
     // skewed row index r-1 of any lane at any step addresses the row without
     // a clamp (the pad words are only read by steps whose body is skipped).
+    // kRebase (long db): the row's two chars as a 16-bit (A | B << 8) word,
+    // half the LDS, widened in the step (one v_perm and a shift)
     uint32_t *__restrict__ myrow = drow + (threadIdx.x / G) * (ld_max + 2 * G) + G;
+    uint16_t *__restrict__ myrow16 = reinterpret_cast<uint16_t *>(drow) +
+                                     (threadIdx.x / G) * (ld_max + 2 * G) + G;
     for (int i = lane; i < ldM; i += G) {
         const uint32_t ca = i < ldA ? (uint32_t)dA[i] : 0u;
         const uint32_t cb = i < ldB ? (uint32_t)dB[i] : 0u;
-        myrow[i] = (ca << 5) | (cb << 21);
+        if constexpr (kRebase)
+            myrow16[i] = (uint16_t)(ca | (cb << 8));
+        else
+            myrow[i] = (ca << 5) | (cb << 21);
     }
     asm volatile("s_waitcnt lgkmcnt(0)" : : : "memory");
     __builtin_amdgcn_wave_barrier();
@@ -1137,6 +1144,7 @@ __global__ __launch_bounds__(256) void nw_fill_pk_kernel(Src src, uint32_t count
     uint8_t *__restrict__ mB = mask + pb.mask_off + (uint64_t)(lane * NS) * pb.mask_bs -
                                (int64_t)lane * (int64_t)pb.mask_rs;
     const uint32_t *__restrict__ rowp = myrow - lane;  // word of row r-1 at step 0
+    const uint16_t *__restrict__ rowp16 = myrow16 - lane;
     const int T = (int)geo.steps((uint32_t)ldM);
     // Previous-row H: step t reads Hin (row r-1) and writes Hout (row r).
     // SALN_PINGPONG: a two-step unroll swaps two arrays (no register
@@ -1145,7 +1153,11 @@ __global__ __launch_bounds__(256) void nw_fill_pk_kernel(Src src, uint32_t count
 
     auto step = [&](int t, uint32_t(&Hin)[K], uint32_t(&Hout)[K]) __attribute__((always_inline)) {
         const int r = t - lane + 1;
-        const uint32_t dch = rowp[t];
+        uint32_t dch;
+        if constexpr (kRebase)  // [A, 0, B, 0] << 5
+            dch = __builtin_amdgcn_perm(0u, (uint32_t)rowp16[t], 0x0C010C00u) << 5;
+        else
+            dch = rowp[t];
         int32_t base = 0;  // frame of step t (kRebase)
         if constexpr (kRebase) {
             base = drift * (t & -kRebaseSteps) + ctr;
@@ -1569,7 +1581,7 @@ static hipError_t fill_pk(dim3 grid, hipStream_t s, const NwPairDesc *pairs, uin
         const char *e = std::getenv("SALN_FILL_LDS_MIN");
         return e ? (size_t)std::atol(e) : (size_t)0;
     }();
-    const size_t lds = std::max((size_t)(256 / G) * (ld_max + 2 * G) * sizeof(uint32_t), pad);
+    const size_t lds = std::max((size_t)(256 / G) * (ld_max + 2 * G) * (rebase ? 2 : 4), pad);
     if (lds > kPackedLdsMax) return hipErrorInvalidValue;  // choose_variant keeps ld below this
     const PlanSrc src{pairs, first, end_h};
     auto go = [&](auto codes_c, auto rebase_c) -> hipError_t {
@@ -1599,7 +1611,8 @@ static hipError_t avsa_pk(const AvsaSrc &src, uint32_t count, const uint8_t *qs,
     const uint32_t sup = 8 * blocks_per_pack(2 * gpb);
     const uint32_t groups = (count + 1) / 2;
     const dim3 grid(((groups + gpb - 1) / gpb + sup - 1) / sup * sup);
-    const size_t lds = (size_t)gpb * (ld_max + 2 * G) * sizeof(uint32_t);
+    const bool rebase = !packed_ok(G * K, ld_max, sc);
+    const size_t lds = (size_t)gpb * (ld_max + 2 * G) * (rebase ? 2 : 4);
     if (lds > kPackedLdsMax) return hipErrorInvalidValue;
     auto go = [&](auto rebase_c) -> hipError_t {
         const auto kern = nw_fill_pk_kernel<G, K, kCodesNone, AvsaSrc, K, decltype(rebase_c)::value>;
@@ -1612,7 +1625,7 @@ static hipError_t avsa_pk(const AvsaSrc &src, uint32_t count, const uint8_t *qs,
         kern<<<grid, dim3(256), lds, s>>>(src, count, qs, ds, nullptr, sc, ld_max);
         return hipSuccess;
     };
-    return packed_ok(G * K, ld_max, sc) ? go(std::false_type{}) : go(std::true_type{});
+    return rebase ? go(std::true_type{}) : go(std::false_type{});
 }
 
 // Score-only all-vs-all over one packed query class (variant 4-7): pairs
@@ -1818,7 +1831,7 @@ static bool packed_ok_rebase(uint32_t lq, uint32_t ld, const Scoring &sc, uint32
     const int64_t pen = 2ll * (sc.match - sc.mismatch);
     if (pen < 2 || pen > 32 || sc.gap_extend > 0 || sc.gap_open > 0 || lq > W) return false;
     const uint32_t gpb = 256 / G;
-    if ((size_t)gpb * (ld + 2 * G) * sizeof(uint32_t) > kPackedLdsMax || ld > 4096) return false;
+    if ((size_t)gpb * (ld + 2 * G) * 2 > kPackedLdsMax || ld > 4096) return false;  // 16-bit rows
     const int64_t m = std::abs(sc.match), ge = std::abs(sc.gap_extend), go = std::abs(sc.gap_open);
     if (go + 4097 * ge >= 32768) return false;
     const int64_t drift = std::abs(2 * sc.gap_extend - 2 * sc.match + 2 * sc.gap_extend);

@@ -239,8 +239,8 @@ def test_score_only_plan_matches_full(saln):
 
 
 def test_packed_rebase_shapes(saln, oracle):
-    """Pairs past one int16 frame (db up to 1,248 rows for <= 256 query
-    columns, 2,496 for <= 512) run through the packed fill with its rebasing
+    """Pairs past one int16 frame (db up to 2,528 rows for <= 256 query
+    columns, 4,096 for <= 512) run through the packed fill with its rebasing
     frame: identical and embedded pairs (the largest in-frame excursions:
     the diagonal gains while column 0 drifts), random and two-letter pairs;
     scores, end states, panics, first alignment and the full parent mask
@@ -248,10 +248,12 @@ def test_packed_rebase_shapes(saln, oracle):
     from sequencealigning_amd import synth
     rng = np.random.default_rng(777)
     cases = []
-    base = synth.random_bases(900, 2500).tobytes()
+    base = synth.random_bases(900, 2600).tobytes()
     cases.append((base[:512], base[:512]))                      # identical 512 x 512
     cases.append((base[700:1212], base[:2000]))                 # embedded 512 in 2,000
     cases.append((base[300:450], base[:1248]))                  # embedded 150 in 1,248
+    cases.append((base[1000:1150], base[:2528]))                # embedded 150 in 2,528
+    cases.append((rand_seq(rng, 400), rand_seq(rng, 4000)))     # random 400 x 4,000
     cases.append((rand_seq(rng, 256), rand_seq(rng, 1200)))     # random 256 x 1,200
     cases.append((bytes(rng.choice([65, 67], 160).astype(np.uint8)),
                   bytes(rng.choice([65, 67], 1000).astype(np.uint8))))  # two-letter
