@@ -3,6 +3,9 @@
 // thin wrapper: upload -> plan -> saln_nw_execute (GPU) -> download.
 #include <hip/hip_runtime.h>
 
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -13,12 +16,18 @@ using namespace saln;
 
 namespace {
 
+// a context-cached device block (saln::dev_alloc), released on scope exit
 struct DevBuf {
+    saln_context *ctx;
     void *p = nullptr;
+    explicit DevBuf(saln_context *c) : ctx(c) {}
     ~DevBuf() {
-        if (p) (void)hipFree(p);
+        if (p) {
+            (void)hipDeviceSynchronize();
+            dev_free(ctx, p);
+        }
     }
-    hipError_t alloc(size_t n) { return hipMalloc(&p, n ? n : 1); }
+    hipError_t alloc(size_t n) { return dev_alloc(ctx, &p, n); }
 };
 
 #define TRY_HIP(expr)                                                                      \
@@ -43,6 +52,7 @@ static int run_batch(saln_context *ctx, const uint8_t *q_seq, const uint64_t *q_
                      int32_t mode, const saln_nw_scoring *scoring, saln_nw_result *results,
                      uint32_t *cigar, const uint64_t *cigar_off,
                      std::vector<PairMask> *masks_out) {
+    StageClock clk;
     PlanGuard g;
     int rc = saln_nw_plan_create(ctx, q_off, n_q, db_off, n_db, pair_q, pair_db, n_pairs, mode,
                                  scoring, &g.p);
@@ -55,10 +65,11 @@ static int run_batch(saln_context *ctx, const uint8_t *q_seq, const uint64_t *q_
     }
     if (rc != SALN_OK) return rc;
     if (masks_out) plan_set_full_codes(g.p, true);
+    clk.mark("plan");
     std::vector<uint64_t> coff(n_pairs + 1);
     saln_nw_cigar_offsets(g.p, coff.data());
     uint64_t cig_words = coff[n_pairs];
-    DevBuf dq, dd, dr, dc;
+    DevBuf dq(ctx), dd(ctx), dr(ctx), dc(ctx);
     const uint64_t qbytes = q_off[n_q], dbytes = db_off[n_db];
     TRY_HIP(dq.alloc(qbytes));
     TRY_HIP(dd.alloc(dbytes));
@@ -66,14 +77,43 @@ static int run_batch(saln_context *ctx, const uint8_t *q_seq, const uint64_t *q_
     TRY_HIP(dc.alloc(cig_words * 4));
     if (qbytes) TRY_HIP(hipMemcpy(dq.p, q_seq, qbytes, hipMemcpyHostToDevice));
     if (dbytes) TRY_HIP(hipMemcpy(dd.p, db_seq, dbytes, hipMemcpyHostToDevice));
+    clk.mark("alloc+h2d");
     rc = saln_nw_execute(g.p, (const uint8_t *)dq.p, (const uint8_t *)dd.p,
                          (saln_nw_result *)dr.p, (uint32_t *)dc.p, nullptr);
     if (rc != SALN_OK) return rc;
     TRY_HIP(hipDeviceSynchronize());
     if ((rc = plan_check_error(g.p)) != SALN_OK) return rc;
+    clk.mark("execute");
     TRY_HIP(hipMemcpy(results, dr.p, n_pairs * sizeof(saln_nw_result), hipMemcpyDeviceToHost));
-    std::vector<uint32_t> hc(cig_words);
-    if (cig_words) TRY_HIP(hipMemcpy(hc.data(), dc.p, cig_words * 4, hipMemcpyDeviceToHost));
+    // CIGARs: packed densely on the device, one download of the used words
+    // into pinned staging, scattered to the caller's offsets
+    std::vector<uint64_t> doff(n_pairs + 1, 0);
+    for (uint64_t k = 0; k < n_pairs; ++k) doff[k + 1] = doff[k] + results[k].cigar_len;
+    const uint32_t *hc = nullptr;
+    DevBuf dso(ctx), ddo(ctx), dcd(ctx);
+    if (cigar && doff[n_pairs]) {
+        TRY_HIP(dso.alloc((n_pairs + 1) * 8));
+        TRY_HIP(ddo.alloc((n_pairs + 1) * 8));
+        TRY_HIP(dcd.alloc(doff[n_pairs] * 4));
+        TRY_HIP(hipMemcpy(dso.p, coff.data(), (n_pairs + 1) * 8, hipMemcpyHostToDevice));
+        TRY_HIP(hipMemcpy(ddo.p, doff.data(), (n_pairs + 1) * 8, hipMemcpyHostToDevice));
+        TRY_HIP(launch_cigar_compact((const saln_nw_result *)dr.p, (const uint64_t *)dso.p,
+                                     (const uint64_t *)ddo.p, (const uint32_t *)dc.p,
+                                     (uint32_t *)dcd.p, n_pairs, ctx->stream));
+        void *st = nullptr;
+        TRY_HIP(pinned_staging(ctx, doff[n_pairs] * 4, &st));
+        TRY_HIP(hipMemcpyAsync(st, dcd.p, doff[n_pairs] * 4, hipMemcpyDeviceToHost, ctx->stream));
+        TRY_HIP(hipStreamSynchronize(ctx->stream));
+        hc = (const uint32_t *)st;
+    }
+    clk.mark("d2h");
+    if (cigar && hc) {
+        for (uint64_t k = 0; k < n_pairs; ++k) {
+            const uint64_t dst = cigar_off ? cigar_off[k] : coff[k];
+            std::memcpy(cigar + dst, hc + doff[k], results[k].cigar_len * 4);
+        }
+    }
+    clk.mark("scatter");
     // per-pair masks are needed for host fix-ups (sentinel dead ends) and
     // for the callers that render reference text.
     std::vector<char> need(n_pairs, 0);
@@ -97,7 +137,7 @@ static int run_batch(saln_context *ctx, const uint8_t *q_seq, const uint64_t *q_
                                      pq2.size(), mode, scoring, &g2.p);
             if (rc != SALN_OK) return rc;
             plan_set_full_codes(g2.p, true);
-            DevBuf dr2;
+            DevBuf dr2(ctx);
             TRY_HIP(dr2.alloc(pq2.size() * sizeof(saln_nw_result)));
             rc = saln_nw_execute(g2.p, (const uint8_t *)dq.p, (const uint8_t *)dd.p,
                                  (saln_nw_result *)dr2.p, nullptr, nullptr);
@@ -121,18 +161,14 @@ static int run_batch(saln_context *ctx, const uint8_t *q_seq, const uint64_t *q_
                 const bool printed = first_alignment(hm, q_seq + q_off[qi], db_seq + db_off[di], &c);
                 results[k].printed = printed ? 1 : 0;
                 results[k].cigar_len = printed ? (uint32_t)c.size() : 0;
-                std::copy(c.begin(), c.end(), hc.begin() + (long)coff[k]);
+                if (cigar)
+                    std::copy(c.begin(), c.end(), cigar + (cigar_off ? cigar_off[k] : coff[k]));
                 results[k].flags &= (uint8_t)~1u;
             }
             if (masks_out) (*masks_out)[k] = std::move(m);
         }
     }
-    if (cigar) {
-        for (uint64_t k = 0; k < n_pairs; ++k) {
-            const uint64_t dst = cigar_off ? cigar_off[k] : coff[k];
-            std::memcpy(cigar + dst, hc.data() + coff[k], results[k].cigar_len * 4);
-        }
-    }
+    clk.mark("fixups");
     return SALN_OK;
 }
 

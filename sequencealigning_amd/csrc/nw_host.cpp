@@ -117,6 +117,9 @@ int saln_context_create(int device, saln_context **out) {
 int saln_context_destroy(saln_context *ctx) {
     if (!ctx) return SALN_OK;
     (void)hipSetDevice(ctx->device);
+    (void)hipDeviceSynchronize();
+    dev_cache_clear(ctx);
+    if (ctx->pinned) (void)hipHostFree(ctx->pinned);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     if (ctx->tb_stream) (void)hipStreamDestroy(ctx->tb_stream);
     delete ctx;
@@ -126,16 +129,11 @@ int saln_context_destroy(saln_context *ctx) {
 int saln_nw_plan_destroy(saln_nw_plan *p) {
     if (!p) return SALN_OK;
     (void)hipSetDevice(p->ctx->device);
-    (void)hipFree(p->d_pairs);
-    (void)hipFree(p->d_mask);
-    (void)hipFree(p->d_mask2);
-    (void)hipFree(p->d_endh2);
-    (void)hipFree(p->d_scratch);
-    (void)hipFree(p->d_work);
-    (void)hipFree(p->d_prog);
-    (void)hipFree(p->d_err);
-    (void)hipFree(p->d_ops);
-    (void)hipFree(p->d_endh);
+    (void)hipDeviceSynchronize();  // the blocks go back to the context cache
+    for (void *b : {(void *)p->d_pairs, (void *)p->d_mask, (void *)p->d_mask2, (void *)p->d_endh2,
+                    (void *)p->d_scratch, (void *)p->d_work, (void *)p->d_prog, (void *)p->d_err,
+                    (void *)p->d_ops, (void *)p->d_endh})
+        dev_free(p->ctx, b);
     for (auto &e : p->sync_ev) (void)hipEventDestroy(e);
     for (auto &t : p->ev_pool)
         for (auto &e : t) (void)hipEventDestroy(e);
@@ -160,6 +158,7 @@ int saln_nw_plan_create(saln_context *ctx, const uint64_t *q_off, uint64_t n_q,
     }
     if (n_pairs > 0xFFFFFFFFull) return SALN_E_INVALID;
     HIP_TRY(hipSetDevice(ctx->device));
+    StageClock clk;
     auto *p = new saln_nw_plan;
     p->ctx = ctx;
     p->sc = scoring_or_default(scoring);
@@ -195,6 +194,7 @@ int saln_nw_plan_create(saln_context *ctx, const uint64_t *q_off, uint64_t n_q,
         p->cells += lq * ld;
     }
     p->cigar_off[n_pairs] = cig;
+    clk.mark("plan: descs");
     {
         // Queries of 513-1,024 columns: the 64-lane packed variant is the
         // throughput choice (two pairs per wave), the column stripes the
@@ -215,15 +215,23 @@ int saln_nw_plan_create(saln_context *ctx, const uint64_t *q_off, uint64_t n_q,
     // plan order: fill pairs grouped by variant, then by query chunk count,
     // longest db first (balances the groups of a block and keeps the pairs of
     // a mask pack alike); pairs with an empty side last (traceback only).
-    std::vector<uint32_t> order(n_pairs);
-    std::iota(order.begin(), order.end(), 0u);
-    auto key = [&](uint32_t k) {
+    // (variant, ~chunks, ~len_db) packed in one word, ties by results index;
+    // a batch of alike pairs is usually in order already
+    std::vector<uint64_t> skey(n_pairs);
+    for (uint64_t k = 0; k < n_pairs; ++k) {
         const NwPairDesc &d = descs[k];
         const bool empty = d.len_q == 0 || d.len_db == 0;
-        const uint32_t nch = empty ? 0 : variant_geom((int)d.variant).n_chunks(d.len_q);
-        return std::make_tuple(empty ? (uint32_t)kNumVariants : d.variant, ~nch, ~d.len_db, k);
-    };
-    std::sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return key(a) < key(b); });
+        const uint64_t nch = empty ? 0 : variant_geom((int)d.variant).n_chunks(d.len_q);
+        skey[k] = (uint64_t)(empty ? (uint32_t)kNumVariants : d.variant) << 56 |
+                  ((~nch) & 0xFFFFFFull) << 32 | (uint32_t)~d.len_db;
+    }
+    std::vector<uint32_t> order(n_pairs);
+    std::iota(order.begin(), order.end(), 0u);
+    if (!std::is_sorted(skey.begin(), skey.end()))
+        std::sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) {
+            return skey[a] != skey[b] ? skey[a] < skey[b] : a < b;
+        });
+    clk.mark("plan: sort");
     p->h_pairs.resize(n_pairs);
     uint64_t soff = 0, ooff = 0;
     for (uint64_t r = 0; r < n_pairs; ++r) {
@@ -316,6 +324,7 @@ int saln_nw_plan_create(saln_context *ctx, const uint64_t *q_off, uint64_t n_q,
             }
         }
     }
+    clk.mark("plan: layout");
     p->plan_index.resize(n_pairs);
     for (uint64_t r = 0; r < n_pairs; ++r) p->plan_index[p->h_pairs[r].pair_id] = (uint32_t)r;
     p->mask_bytes = moff;
@@ -327,16 +336,17 @@ int saln_nw_plan_create(saln_context *ctx, const uint64_t *q_off, uint64_t n_q,
     };
     hipError_t e;
     if (n_pairs) {
-        if ((e = hipMalloc(&p->d_pairs, n_pairs * sizeof(NwPairDesc))) != hipSuccess)
+        if ((e = dev_alloc(p->ctx, (void **)&p->d_pairs, n_pairs * sizeof(NwPairDesc))) != hipSuccess)
             return fail(e, "hipMalloc(pairs)");
         if ((e = hipMemcpy(p->d_pairs, p->h_pairs.data(), n_pairs * sizeof(NwPairDesc),
                            hipMemcpyHostToDevice)) != hipSuccess)
             return fail(e, "hipMemcpy(pairs)");
-        if ((e = hipMalloc(&p->d_endh, n_pairs * sizeof(int32_t))) != hipSuccess)
+        if ((e = dev_alloc(p->ctx, (void **)&p->d_endh, n_pairs * sizeof(int32_t))) != hipSuccess)
             return fail(e, "hipMalloc(end)");
     }
+    clk.mark("plan: pairs h2d");
     // +64 B: the traceback walker reads whole 5-dword segments
-    if (moff && (e = hipMalloc(&p->d_mask, moff + 64)) != hipSuccess)
+    if (moff && (e = dev_alloc(p->ctx, (void **)&p->d_mask, moff + 64)) != hipSuccess)
         return fail(e, "hipMalloc(mask workspace)");
     {
         // stripe work list (pair-major, chunk-ascending: a stripe's predecessor
@@ -354,11 +364,11 @@ int saln_nw_plan_create(saln_context *ctx, const uint64_t *q_off, uint64_t n_q,
         }
         p->work_first[n_pairs] = (uint32_t)work.size();
         if (!work.empty()) {
-            if ((e = hipMalloc(&p->d_work, work.size() * sizeof(uint2))) != hipSuccess ||
+            if ((e = dev_alloc(p->ctx, (void **)&p->d_work, work.size() * sizeof(uint2))) != hipSuccess ||
                 (e = hipMemcpy(p->d_work, work.data(), work.size() * sizeof(uint2),
                                hipMemcpyHostToDevice)) != hipSuccess ||
-                (e = hipMalloc(&p->d_prog, p->n_prog * sizeof(uint32_t))) != hipSuccess ||
-                (e = hipMalloc(&p->d_err, sizeof(uint32_t))) != hipSuccess ||
+                (e = dev_alloc(p->ctx, (void **)&p->d_prog, p->n_prog * sizeof(uint32_t))) != hipSuccess ||
+                (e = dev_alloc(p->ctx, (void **)&p->d_err, sizeof(uint32_t))) != hipSuccess ||
                 (e = hipMemset(p->d_err, 0, sizeof(uint32_t))) != hipSuccess)
                 return fail(e, "stripe work list");
             if ((e = hipMemcpy(p->d_pairs, p->h_pairs.data(), n_pairs * sizeof(NwPairDesc),
@@ -366,9 +376,10 @@ int saln_nw_plan_create(saln_context *ctx, const uint64_t *q_off, uint64_t n_q,
                 return fail(e, "hipMemcpy(pairs)");
         }
     }
-    if (soff && (e = hipMalloc(&p->d_scratch, soff * sizeof(int2))) != hipSuccess)
+    clk.mark("plan: mask+work");
+    if (soff && (e = dev_alloc(p->ctx, (void **)&p->d_scratch, soff * sizeof(int2))) != hipSuccess)
         return fail(e, "hipMalloc(scratch)");
-    if (ooff && (e = hipMalloc(&p->d_ops, ooff * sizeof(uint32_t))) != hipSuccess)
+    if (ooff && (e = dev_alloc(p->ctx, (void **)&p->d_ops, ooff * sizeof(uint32_t))) != hipSuccess)
         return fail(e, "hipMalloc(op stream)");
     *out = p;
     return SALN_OK;
@@ -504,8 +515,8 @@ int saln_nw_plan_set_async(saln_nw_plan *p, int enable) {
     if (!p) return SALN_E_INVALID;
     HIP_TRY(hipSetDevice(p->ctx->device));
     if (enable && !p->d_mask2 && p->mask_bytes) {
-        HIP_TRY(hipMalloc(&p->d_mask2, p->mask_bytes + 64));
-        HIP_TRY(hipMalloc(&p->d_endh2, p->n_pairs * sizeof(int32_t)));
+        HIP_TRY(dev_alloc(p->ctx, (void **)&p->d_mask2, p->mask_bytes + 64));
+        HIP_TRY(dev_alloc(p->ctx, (void **)&p->d_endh2, p->n_pairs * sizeof(int32_t)));
     }
     p->async_tb = enable != 0;
     p->buf = 0;
@@ -791,4 +802,72 @@ int plan_check_error(const saln_nw_plan *p) {
     }
     return SALN_OK;
 }
+}  // namespace saln
+
+namespace saln {
+
+hipError_t dev_alloc(saln_context *ctx, void **p, size_t n) {
+    n = n ? (n + 255) & ~size_t(255) : 256;
+    {
+        std::lock_guard<std::mutex> lk(ctx->mu);
+        auto it = ctx->cache.lower_bound(n);
+        if (it != ctx->cache.end() && it->first <= 2 * n) {
+            *p = it->second;
+            ctx->live[it->second] = it->first;
+            ctx->cached -= it->first;
+            ctx->cache.erase(it);
+            return hipSuccess;
+        }
+    }
+    hipError_t e = hipMalloc(p, n);
+    if (e == hipErrorOutOfMemory) {  // give the cached blocks back and retry once
+        (void)hipGetLastError();
+        dev_cache_clear(ctx);
+        e = hipMalloc(p, n);
+    }
+    if (e != hipSuccess) return e;
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    ctx->live[*p] = n;
+    return hipSuccess;
+}
+
+void dev_free(saln_context *ctx, void *p) {
+    if (!p) return;
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    auto it = ctx->live.find(p);
+    if (it == ctx->live.end()) {
+        (void)hipFree(p);
+        return;
+    }
+    const size_t n = it->second;
+    ctx->live.erase(it);
+    if (ctx->cached + n > kDevCacheMax) {
+        (void)hipFree(p);
+        return;
+    }
+    ctx->cache.emplace(n, p);
+    ctx->cached += n;
+}
+
+void dev_cache_clear(saln_context *ctx) {
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    for (auto &kv : ctx->cache) (void)hipFree(kv.second);
+    ctx->cache.clear();
+    ctx->cached = 0;
+}
+
+hipError_t pinned_staging(saln_context *ctx, size_t n, void **p) {
+    if (n > ctx->pinned_bytes) {
+        const size_t want = std::max(n, ctx->pinned_bytes * 2);
+        if (ctx->pinned) (void)hipHostFree(ctx->pinned);
+        ctx->pinned = nullptr;
+        ctx->pinned_bytes = 0;
+        hipError_t e = hipHostMalloc(&ctx->pinned, want, hipHostMallocDefault);
+        if (e != hipSuccess) return e;
+        ctx->pinned_bytes = want;
+    }
+    *p = ctx->pinned;
+    return hipSuccess;
+}
+
 }  // namespace saln

@@ -2,8 +2,14 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <chrono>
 #include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <map>
+#include <mutex>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "nw_common.hpp"
@@ -13,9 +19,45 @@ struct saln_context {
     int device = 0;
     hipStream_t stream = nullptr;
     hipStream_t tb_stream = nullptr;  // traceback stream (pipelined NW plans)
+    // Device blocks released by plans / host-path calls, kept for reuse
+    // (hipMalloc + hipFree of a 3 GB mask workspace cost more than the C2
+    // kernels): size -> block; `live` maps handed-out blocks to their size.
+    std::mutex mu;
+    std::multimap<size_t, void *> cache;
+    std::unordered_map<void *, size_t> live;
+    size_t cached = 0;
+    // pinned host staging for the host-path downloads (grow-only)
+    void *pinned = nullptr;
+    size_t pinned_bytes = 0;
 };
 
 namespace saln {
+
+// SALN_HOST_TIMING=1: stage times of the host-side paths on stderr
+struct StageClock {
+    bool on = [] {
+        const char *e = std::getenv("SALN_HOST_TIMING");
+        return e && e[0] == '1';
+    }();
+    std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+    void mark(const char *what) {
+        if (!on) return;
+        (void)hipDeviceSynchronize();
+        const auto n = std::chrono::steady_clock::now();
+        std::fprintf(stderr, "[saln host] %-16s %8.3f ms\n", what,
+                     std::chrono::duration<double, std::milli>(n - t).count());
+        t = n;
+    }
+};
+
+// Context-cached device memory: a released block is reused by a later request
+// of at most twice its size; at most kDevCacheMax bytes stay cached.  A block
+// must not be released while kernels may still use it (plan destroy syncs).
+constexpr size_t kDevCacheMax = size_t(32) << 30;
+hipError_t dev_alloc(saln_context *ctx, void **p, size_t n);
+void dev_free(saln_context *ctx, void *p);
+void dev_cache_clear(saln_context *ctx);
+hipError_t pinned_staging(saln_context *ctx, size_t n, void **p);
 
 // kernels (nw_kernels.hip)
 hipError_t launch_fill(int variant, const NwPairDesc *pairs, uint32_t first, uint32_t count,
@@ -28,6 +70,9 @@ hipError_t launch_fill_stripes(const NwPairDesc *pairs, const uint2 *work, uint3
                                int2 *scratch, uint32_t *prog, uint32_t *err, int32_t *end_h,
                                Scoring sc, int codes /* 0 walk, 1 full, 2 none */,
                                hipStream_t stream);
+hipError_t launch_cigar_compact(const saln_nw_result *res, const uint64_t *src_off,
+                                const uint64_t *dst_off, const uint32_t *src, uint32_t *dst,
+                                uint64_t n, hipStream_t stream);
 constexpr int kStripeVariant = 3;
 constexpr int kWidePackedVariant = 8;        // packed, 64-lane groups, up to 1,024 columns
 constexpr uint64_t kWidePackedMinPairs = 1536;  // fewer such pairs: column stripes (measured crossover 1,024-2,048)

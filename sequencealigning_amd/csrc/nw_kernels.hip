@@ -1798,6 +1798,29 @@ hipError_t launch_fill_stripes(const NwPairDesc *pairs, const uint2 *work, uint3
     return hipGetLastError();
 }
 
+// Host path: pack each pair's CIGAR words (capacity-spaced at src_off) densely
+// at dst_off, so only the used words cross PCIe.  One wave per pair.
+__global__ __launch_bounds__(256) void nw_cigar_compact_kernel(
+    const saln_nw_result *__restrict__ res, const uint64_t *__restrict__ src_off,
+    const uint64_t *__restrict__ dst_off, const uint32_t *__restrict__ src,
+    uint32_t *__restrict__ dst, uint64_t n) {
+    const uint64_t k = (uint64_t)blockIdx.x * 4 + threadIdx.x / 64;
+    if (k >= n) return;
+    const uint32_t len = res[k].cigar_len;
+    const uint32_t *s = src + src_off[k];
+    uint32_t *d = dst + dst_off[k];
+    for (uint32_t i = threadIdx.x % 64; i < len; i += 64) d[i] = s[i];
+}
+
+hipError_t launch_cigar_compact(const saln_nw_result *res, const uint64_t *src_off,
+                                const uint64_t *dst_off, const uint32_t *src, uint32_t *dst,
+                                uint64_t n, hipStream_t stream) {
+    if (!n) return hipSuccess;
+    nw_cigar_compact_kernel<<<dim3((uint32_t)((n + 3) / 4)), dim3(256), 0, stream>>>(
+        res, src_off, dst_off, src, dst, n);
+    return hipGetLastError();
+}
+
 Geom variant_geom(int v) { return kVariants[v]; }
 bool variant_packed(int v) { return kPacked[v]; }
 
