@@ -581,20 +581,22 @@ __global__ __launch_bounds__(256) void nw_traceback_kernel(
 constexpr int32_t kCoopLine = 256;  // bytes per line (one stripe step)
 constexpr int32_t kCoopSlack = 64;  // rows loaded beyond a diagonal crossing of the stripe
 
-__global__ __launch_bounds__(64) void nw_traceback_coop_kernel(
+template <int NWV>
+__global__ __launch_bounds__(64 * NWV) void nw_traceback_coop_kernel(
     const NwPairDesc *__restrict__ pairs, uint32_t first, const uint8_t *__restrict__ mask,
     const int32_t *__restrict__ end_h, saln_nw_result *__restrict__ results,
     uint32_t *__restrict__ cigar, Scoring sc, int32_t kCoopRows) {
-    // kCoopRows + 63 lines, rounded up to whole 4-line DMAs
+    // kCoopRows + 63 lines, rounded up to whole 4-line DMAs; then the request
+    // words wave 0 posts to the loader waves
     extern __shared__ __attribute__((aligned(16))) uint8_t win[];
-    const int32_t lane = (int32_t)threadIdx.x;
+    int32_t *req = reinterpret_cast<int32_t *>(win + (kCoopRows + 64) * kCoopLine);
+    const int32_t lane = (int32_t)threadIdx.x % 64, wv = (int32_t)threadIdx.x / 64;
     const uint32_t idx = first + blockIdx.x;
     const NwPairDesc p = pairs[idx];
-    const int32_t hend = end_h[idx];
-    const int32_t lq = (int32_t)p.len_q, ld = (int32_t)p.len_db;
     const uint8_t *__restrict__ m = mask + p.mask_off;
     int32_t r_lo = 1, c_lo = 1;  // window: rows [r_lo, i], the stripe's columns [c_lo, c_lo+255]
-    auto load = [&](int32_t i, int32_t j) __attribute__((always_inline)) {
+    // Wave w's share of the window for cell (i, j): every NWV-th 4-line DMA.
+    auto dma = [&](int32_t i, int32_t j, int32_t w) __attribute__((always_inline)) {
         const int32_t s = (j - 1) / kCoopLine;
         c_lo = s * kCoopLine + 1;
         // a near-diagonal path leaves the stripe after j - c_lo + 1 rows:
@@ -604,13 +606,38 @@ __global__ __launch_bounds__(64) void nw_traceback_coop_kernel(
         const int32_t t_lo = r_lo - 1, t_hi = i + 62;
         const uint8_t *reg = m + (uint64_t)s * p.mask_cs;
         typedef __attribute__((address_space(3))) void lds_v;
-        for (int32_t mm = 0; 4 * mm <= t_hi - t_lo; ++mm) {
+        for (int32_t mm = w; 4 * mm <= t_hi - t_lo; mm += NWV) {
             const int32_t t = min(t_lo + 4 * mm + lane / 16, t_hi);  // clamped: stay in the region
             __builtin_amdgcn_global_load_lds(reg + (uint64_t)t * kCoopLine + 16 * (lane % 16),
                                              (lds_v *)(win + 4 * mm * kCoopLine), 16, 0, 0);
         }
-        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the window has landed
-        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): my share has landed
+    };
+    // Waves 1.. only load windows: wait for a request (i, j), or i < 0 = done.
+    if (wv > 0) {
+        for (;;) {
+            __syncthreads();
+            const int32_t qi = req[0], qj = req[1];
+            if (qi < 0) return;
+            dma(qi, qj, wv);
+            __syncthreads();
+        }
+    }
+    const int32_t hend = end_h[idx];
+    const int32_t lq = (int32_t)p.len_q, ld = (int32_t)p.len_db;
+    auto load = [&](int32_t i, int32_t j) __attribute__((always_inline)) {
+        if (NWV > 1) {
+            if (lane == 0) {
+                req[0] = i;
+                req[1] = j;
+            }
+            __syncthreads();
+        }
+        dma(i, j, 0);
+        if (NWV > 1)
+            __syncthreads();  // every share has landed
+        else
+            __builtin_amdgcn_wave_barrier();
     };
     // code byte of interior cell (r, c) inside the window, bits 0-6 present-sets
     auto code = [&](int32_t r, int32_t c) __attribute__((always_inline)) {
@@ -717,6 +744,10 @@ __global__ __launch_bounds__(64) void nw_traceback_coop_kernel(
             i -= (int32_t)n;
         }
         st = __builtin_amdgcn_readlane(nxt, L);
+    }
+    if (NWV > 1) {  // release the loader waves
+        if (lane == 0) req[0] = -1;
+        __syncthreads();
     }
     if (run_len) {
         if (lane == 0 && out) out[nops] = (run_len << 4) | run_op;
@@ -1754,13 +1785,15 @@ hipError_t launch_traceback(int variant, const NwPairDesc *pairs, uint32_t first
         case 3: {  // column-stripe pairs: one cooperative wave per pair
             // a few pairs: the whole 160 KB (fewer window reloads); batches:
             // 48 KB windows, three waves per CU
+            constexpr int kLoaders = 4;  // waves per pair: one walks, all load its windows
             static const hipError_t attr = hipFuncSetAttribute(
-                (const void *)nw_traceback_coop_kernel,
-                hipFuncAttributeMaxDynamicSharedMemorySize, (576 + 64) * kCoopLine);
+                (const void *)nw_traceback_coop_kernel<kLoaders>,
+                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
             if (attr != hipSuccess) return attr;
-            const int32_t rows = n <= 256 ? 576 : 128;
-            nw_traceback_coop_kernel<<<dim3(n), dim3(64), (size_t)(rows + 64) * kCoopLine, stream>>>(
-                pairs, first, mask, end_h, results, cigar, sc, rows);
+            const int32_t rows = n <= 256 ? 568 : 128;
+            nw_traceback_coop_kernel<kLoaders>
+                <<<dim3(n), dim3(64 * kLoaders), (size_t)(rows + 64) * kCoopLine + 16, stream>>>(
+                    pairs, first, mask, end_h, results, cigar, sc, rows);
             break;
         }
         case 5: tb_lds<16, 16>(grid, stream, pairs, first, n, mask, end_h, ops, results, cigar, sc); break;
