@@ -1437,7 +1437,10 @@ __global__ __launch_bounds__(64) void nw_fill_stripe_kernel(
     // the query chars above arrive here: otherwise the wait for them lands
     // inside the loop, where it would also wait for every mask store
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
-    for (int t = 0; t < T; ++t) {
+    // Previous-row H: step t reads Hin (row r-1) and writes Hout (row r); a
+    // two-step unroll swaps the arrays instead of rotating registers.
+    int32_t HpB[K];
+    auto step = [&](int t, int32_t(&Hin)[K], int32_t(&Hout)[K]) __attribute__((always_inline)) {
         const int r = t - lane + 1;
         dch = (uint32_t)shr1<G>((int32_t)(((dcur >> (8 * dpos)) & 0xFFu) << 8), (int32_t)dch);  // d[r-1]
         if (++dpos == 4) {  // past the stripe's last char the bytes are unused
@@ -1484,11 +1487,14 @@ __global__ __launch_bounds__(64) void nw_fill_stripe_kernel(
         if (r >= 1 && r <= (int)ld) {
             int32_t F = inF;
             uint32_t sg[8][4];
+            int32_t diag = hd;  // H~(r-1, c-1) of column k
 #pragma unroll
             for (int k = 0; k < K; ++k) {
+                const int32_t hdk = diag;
+                diag = Hin[k];
                 const uint32_t x = qc[k] ^ dch;
                 const int32_t pen = kMinPen ? (int32_t)min(x, (uint32_t)pen_max) : (x ? pen_max : 0);
-                const int32_t M = hd - pen;
+                const int32_t M = hdk - pen;
                 const int32_t I = F, D = Dn[k];
                 const int32_t H = max(M, max(I, D));
                 const int32_t tO = M + kOpen;
@@ -1511,12 +1517,11 @@ __global__ __launch_bounds__(64) void nw_fill_stripe_kernel(
                 }
                 F = max(tO, I);
                 Dn[k] = max(tO, D) + kDstep;
-                hd = Hp[k];
-                Hp[k] = H;
+                Hout[k] = H;
             }
             hd = inH;
             pubF = F;
-            pubH = Hp[K - 1];
+            pubH = Hout[K - 1];
             if constexpr (kCodes != kCodesNone)
                 *reinterpret_cast<uint32_t *>(mseg) = stripe_code_word<kCodes>(sg);
             if (lane == G - 1 && scr_out) {
@@ -1535,12 +1540,21 @@ __global__ __launch_bounds__(64) void nw_fill_stripe_kernel(
                 int32_t e = 0;
 #pragma unroll
                 for (int k = 0; k < K; ++k)
-                    if ((uint32_t)k == k_end) e = Hp[k];
+                    if ((uint32_t)k == k_end) e = Hout[k];
                 end_h[wk.x] = e - alpha * (int32_t)ld - beta * (int32_t)lq;
             }
+        } else {
+#pragma unroll
+            for (int k = 0; k < K; ++k) Hout[k] = Hin[k];  // lane idle: keep row r-1
         }
         mseg += p.mask_rs;
+    };
+    int t = 0;
+    for (; t + 1 < T; t += 2) {
+        step(t, Hp, HpB);
+        step(t + 1, HpB, Hp);
     }
+    if (t < T) step(t, Hp, HpB);
     if (failed && lane == 0) atomicOr(err, 1u);
 }
 
