@@ -1415,16 +1415,25 @@ __global__ __launch_bounds__(64) void nw_fill_stripe_kernel(
     }
     int32_t hd = hs_row0(sc, col0) + beta * (int32_t)col0;
     int32_t pubF = 0, pubH = 0;
-    // db chars: lane 0 needs d[t] at step t (wave-uniform): a rolling pair of
-    // scalar dwords (the next one loaded four steps before it is used), so a
-    // step spends a shift and a mask on it; the other lanes take their row's
-    // char from the left neighbour's previous step (DPP).
+    // db chars: lane 0 needs d[t] at step t (wave-uniform).  Steps run in
+    // groups of four; a group's four chars d[t..t+3] are one scalar word
+    // funnel-shifted from a rolling pair of aligned dwords (the next loaded a
+    // group ahead), so a step spends one constant-shift extract on its char;
+    // the other lanes take their row's char from the left neighbour's
+    // previous step (DPP).
     typedef const __attribute__((address_space(4))) uint32_t cu32;  // constant: scalar loads
     cu32 *dw = (cu32 *)((uintptr_t)d & ~(uintptr_t)3);
+    const uint32_t doff = 8u * (uint32_t)((uintptr_t)d & 3);  // bit offset of d[0] in dw[0]
     const uint32_t last_dw = ((uint32_t)ld - 1 + (uint32_t)((uintptr_t)d & 3)) >> 2;
-    uint32_t dpos = (uint32_t)((uintptr_t)d & 3);  // byte of d[t] in dcur
-    uint32_t dnidx = min(1u, last_dw);             // dword index of dnxt
+    uint32_t dnidx = min(1u, last_dw);  // dword index of dnxt
     uint32_t dcur = dw[0], dnxt = dw[dnidx];
+    auto group_chars = [&]() __attribute__((always_inline)) {
+        const uint32_t w = doff ? (dcur >> doff) | (dnxt << (32u - doff)) : dcur;
+        dcur = dnxt;  // past the db's last dword the bytes are unused
+        dnidx = min(dnidx + 1, last_dw);
+        dnxt = dw[dnidx];
+        return w;
+    };
     uint32_t dch = 0;
     int32_t blkH = 0, blkF = 0;  // lanes 0..31: the left column of the current 32-row block
     uint32_t avail = 0;          // rows of the left column known to be published
@@ -1440,22 +1449,19 @@ __global__ __launch_bounds__(64) void nw_fill_stripe_kernel(
     // Previous-row H: step t reads Hin (row r-1) and writes Hout (row r); a
     // two-step unroll swaps the arrays instead of rotating registers.
     int32_t HpB[K];
-    auto step = [&](int t, int32_t(&Hin)[K], int32_t(&Hout)[K]) __attribute__((always_inline)) {
+    // kGroupStart: t % 4 == 0 (only such a step can open a 32-row block)
+    auto step = [&](int t, int32_t(&Hin)[K], int32_t(&Hout)[K], uint32_t dt,
+                    auto group_start) __attribute__((always_inline)) {
+        constexpr bool kGroupStart = decltype(group_start)::value;
         const int r = t - lane + 1;
-        dch = (uint32_t)shr1<G>((int32_t)(((dcur >> (8 * dpos)) & 0xFFu) << 8), (int32_t)dch);  // d[r-1]
-        if (++dpos == 4) {  // past the stripe's last char the bytes are unused
-            dpos = 0;
-            dcur = dnxt;
-            dnidx = min(dnidx + 1, last_dw);
-            dnxt = dw[dnidx];
-        }
+        dch = (uint32_t)shr1<G>((int32_t)(dt << 8), (int32_t)dch);  // d[r-1]
         int32_t bF, bH;
         const uint32_t rr = (uint32_t)t + 1;  // lane 0's row
         if (c == 0) {
             bF = is_col1(sc, rr) + alpha * (int32_t)rr + beta;
             bH = hs_col0(sc, rr) + alpha * (int32_t)rr;
         } else {
-            if ((rr - 1) % kPub == 0 && rr <= ld) {  // new 32-row block of the left column
+            if (kGroupStart && (rr - 1) % kPub == 0 && rr <= ld) {  // new 32-row block of the left column
                 const uint32_t need = min(rr - 1 + kPub, ld);
                 uint32_t spins = 0;
                 while (avail < need && !failed) {
@@ -1549,12 +1555,23 @@ __global__ __launch_bounds__(64) void nw_fill_stripe_kernel(
         }
         mseg += p.mask_rs;
     };
+    static_assert(kPub % 4 == 0, "block starts fall on group starts");
+    const std::true_type gs;
+    const std::false_type nogs;
     int t = 0;
-    for (; t + 1 < T; t += 2) {
-        step(t, Hp, HpB);
-        step(t + 1, HpB, Hp);
+    for (; t + 3 < T; t += 4) {
+        const uint32_t w = group_chars();
+        step(t, Hp, HpB, w & 0xFFu, gs);
+        step(t + 1, HpB, Hp, (w >> 8) & 0xFFu, nogs);
+        step(t + 2, Hp, HpB, (w >> 16) & 0xFFu, nogs);
+        step(t + 3, HpB, Hp, w >> 24, nogs);
     }
-    if (t < T) step(t, Hp, HpB);
+    if (t < T) {
+        const uint32_t w = group_chars();
+        step(t, Hp, HpB, w & 0xFFu, gs);
+        if (t + 1 < T) step(t + 1, HpB, Hp, (w >> 8) & 0xFFu, nogs);
+        if (t + 2 < T) step(t + 2, Hp, HpB, (w >> 16) & 0xFFu, nogs);
+    }
     if (failed && lane == 0) atomicOr(err, 1u);
 }
 
