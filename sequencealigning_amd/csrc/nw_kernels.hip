@@ -1449,10 +1449,14 @@ __global__ __launch_bounds__(64) void nw_fill_stripe_kernel(
     // Previous-row H: step t reads Hin (row r-1) and writes Hout (row r); a
     // two-step unroll swaps the arrays instead of rotating registers.
     int32_t HpB[K];
-    // kGroupStart: t % 4 == 0 (only such a step can open a 32-row block)
+    // the last lane's outputs of a group's four steps, published per group
+    // (named registers, not an array: the compiler put an array in scratch)
+    int32_t gH0 = 0, gH1 = 0, gH2 = 0, gH3 = 0, gF0 = 0, gF1 = 0, gF2 = 0, gF3 = 0;
+    // pos = t % 4; only a group start can open a 32-row block
     auto step = [&](int t, int32_t(&Hin)[K], int32_t(&Hout)[K], uint32_t dt,
-                    auto group_start) __attribute__((always_inline)) {
-        constexpr bool kGroupStart = decltype(group_start)::value;
+                    auto pos_c) __attribute__((always_inline)) {
+        constexpr int kPos = decltype(pos_c)::value;
+        constexpr bool kGroupStart = kPos == 0;
         const int r = t - lane + 1;
         dch = (uint32_t)shr1<G>((int32_t)(dt << 8), (int32_t)dch);  // d[r-1]
         int32_t bF, bH;
@@ -1528,49 +1532,73 @@ __global__ __launch_bounds__(64) void nw_fill_stripe_kernel(
             hd = inH;
             pubF = F;
             pubH = Hout[K - 1];
+            if constexpr (kPos == 0) gH0 = pubH, gF0 = pubF;
+            if constexpr (kPos == 1) gH1 = pubH, gF1 = pubF;
+            if constexpr (kPos == 2) gH2 = pubH, gF2 = pubF;
+            if constexpr (kPos == 3) gH3 = pubH, gF3 = pubF;
             if constexpr (kCodes != kCodesNone)
                 *reinterpret_cast<uint32_t *>(mseg) = stripe_code_word<kCodes>(sg);
-            if (lane == G - 1 && scr_out) {
-                // agent-coherent (write-through) stores: the publication below
-                // needs only these to be complete, not an L2 write-back
-                __hip_atomic_store((uint64_t *)(scr_out + r),
-                                   (uint64_t)(uint32_t)pubH | ((uint64_t)(uint32_t)pubF << 32),
-                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if ((uint32_t)r % kPub == 0 || (uint32_t)r == ld) {
-                    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): column stores done
-                    __hip_atomic_store(prog_out, (uint32_t)r, __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_AGENT);
-                }
-            }
-            if (end_lane && r == (int)ld) {
-                int32_t e = 0;
-#pragma unroll
-                for (int k = 0; k < K; ++k)
-                    if ((uint32_t)k == k_end) e = Hout[k];
-                end_h[wk.x] = e - alpha * (int32_t)ld - beta * (int32_t)lq;
-            }
         } else {
 #pragma unroll
             for (int k = 0; k < K; ++k) Hout[k] = Hin[k];  // lane idle: keep row r-1
         }
         mseg += p.mask_rs;
     };
+    // The last lane's rows of steps t0 .. t0+n-1 (rows t0-62 ..) to the
+    // boundary column, with agent-coherent (write-through) stores: the
+    // progress publication needs only these complete, not an L2 write-back.
+    // Progress goes out when the rows reach a 32-row block end or the db end.
+    auto publish = [&](int t0, int n) __attribute__((always_inline)) {
+        if (lane == G - 1 && scr_out) {
+            const int lo = max(t0 - (G - 2), 1), hi = min(t0 + n - 1 - (G - 2), (int)ld);
+            if (hi >= lo) {
+                auto put = [&](int q, int32_t h, int32_t f) __attribute__((always_inline)) {
+                    const int r = t0 + q - (G - 2);
+                    if (q < n && r >= lo && r <= hi)
+                        __hip_atomic_store((uint64_t *)(scr_out + r),
+                                           (uint64_t)(uint32_t)h | ((uint64_t)(uint32_t)f << 32),
+                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                };
+                put(0, gH0, gF0);
+                put(1, gH1, gF1);
+                put(2, gH2, gF2);
+                put(3, gH3, gF3);
+                if (hi / (int)kPub != (lo - 1) / (int)kPub || hi == (int)ld) {
+                    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): column stores done
+                    __hip_atomic_store(prog_out, (uint32_t)hi, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+                }
+            }
+        }
+    };
     static_assert(kPub % 4 == 0, "block starts fall on group starts");
-    const std::true_type gs;
-    const std::false_type nogs;
+    const std::integral_constant<int, 0> p0;
+    const std::integral_constant<int, 1> p1;
+    const std::integral_constant<int, 2> p2;
+    const std::integral_constant<int, 3> p3;
     int t = 0;
     for (; t + 3 < T; t += 4) {
         const uint32_t w = group_chars();
-        step(t, Hp, HpB, w & 0xFFu, gs);
-        step(t + 1, HpB, Hp, (w >> 8) & 0xFFu, nogs);
-        step(t + 2, Hp, HpB, (w >> 16) & 0xFFu, nogs);
-        step(t + 3, HpB, Hp, w >> 24, nogs);
+        step(t, Hp, HpB, w & 0xFFu, p0);
+        step(t + 1, HpB, Hp, (w >> 8) & 0xFFu, p1);
+        step(t + 2, Hp, HpB, (w >> 16) & 0xFFu, p2);
+        step(t + 3, HpB, Hp, w >> 24, p3);
+        publish(t, 4);
     }
-    if (t < T) {
+    const int ntail = T - t;
+    if (ntail > 0) {
         const uint32_t w = group_chars();
-        step(t, Hp, HpB, w & 0xFFu, gs);
-        if (t + 1 < T) step(t + 1, HpB, Hp, (w >> 8) & 0xFFu, nogs);
-        if (t + 2 < T) step(t + 2, Hp, HpB, (w >> 16) & 0xFFu, nogs);
+        step(t, Hp, HpB, w & 0xFFu, p0);
+        if (ntail > 1) step(t + 1, HpB, Hp, (w >> 8) & 0xFFu, p1);
+        if (ntail > 2) step(t + 2, Hp, HpB, (w >> 16) & 0xFFu, p2);
+        publish(t, ntail);
+    }
+    if (end_lane) {  // every lane ends on row ld, in the array the last step wrote
+        int32_t e = 0;
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+            if ((uint32_t)k == k_end) e = (ntail & 1) ? HpB[k] : Hp[k];
+        end_h[wk.x] = e - alpha * (int32_t)ld - beta * (int32_t)lq;
     }
     if (failed && lane == 0) atomicOr(err, 1u);
 }
