@@ -67,7 +67,10 @@ struct NwPairDesc {
 // the stripe wave writes them: the 64 lanes' code dwords of fill step t
 // (lane l at row t-l+1) are the 256 contiguous bytes of line t of the
 // stripe's region, so rs = 256, bs = 260 (next block: one row later, 4 bytes
-// on) and cs = (len_db + 63) * 256.
+// on) and cs = (len_db + 63) * 256.  The packed stripe fill (two int16
+// halves per lane: 128 virtual lanes of 2 columns, virtual lane v = l + 64h
+// at row t - v + 1 in step t) marks its layout with bs = 0: byte
+// 4l + 2(col % 2) + h of line t, cs = (len_db + 127) * 256.
 struct Geom {
     uint32_t G, K;
     SALN_HD uint32_t KD() const { return (K + 3) / 4; }
@@ -78,6 +81,11 @@ struct Geom {
     SALN_HD uint32_t steps(uint32_t len_db) const { return len_db + G - 1; }
     // byte offset (from mask_off) of interior cell (i, j), 1-based
     SALN_HD uint64_t cell(uint32_t i, uint32_t j, uint64_t rs, uint32_t bs, uint64_t cs) const {
+        if (bs == 0) {  // packed column stripes (nw_fill_stripe_pk_kernel): 256-byte lines
+            const uint32_t jj = j - 1, o = jj % 256, v = o / 2;
+            return (uint64_t)(jj / 256) * cs + (uint64_t)(i - 1 + v) * 256 + 4 * (v % 64) +
+                   2 * (o % 2) + v / 64;
+        }
         const uint32_t jj0 = j - 1, b = jj0 / K;
         return (uint64_t)(i - 1) * rs + (uint64_t)(b / G) * cs + (uint64_t)(b % G) * bs + jj0 % K;
     }

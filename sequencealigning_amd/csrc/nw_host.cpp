@@ -275,12 +275,13 @@ int saln_nw_plan_create(saln_context *ctx, const uint64_t *q_off, uint64_t n_q,
             if (v == kStripeVariant) {
                 // skewed, one region per stripe (nw_common.hpp): every fill
                 // step of a stripe wave writes one whole 256-byte line
+                const bool pk = stripe_packed(p->sc);
                 for (uint32_t s = 0; s < np; ++s) {
                     NwPairDesc &d = p->h_pairs[a + s];
                     d.mask_off = moff;
                     d.mask_rs = g.W();
-                    d.mask_bs = (uint32_t)(g.W() + lb);
-                    d.mask_cs = ((uint64_t)d.len_db + g.G - 1) * g.W();
+                    d.mask_bs = pk ? 0u : (uint32_t)(g.W() + lb);
+                    d.mask_cs = ((uint64_t)d.len_db + (pk ? 2 * g.G : g.G) - 1) * g.W();
                     moff += g.n_chunks(d.len_q) * d.mask_cs;
                 }
             } else if (4 * packed <= 5 * own + 4096) {

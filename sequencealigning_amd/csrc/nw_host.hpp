@@ -74,6 +74,8 @@ hipError_t launch_cigar_compact(const saln_nw_result *res, const uint64_t *src_o
                                 const uint64_t *dst_off, const uint32_t *src, uint32_t *dst,
                                 uint64_t n, hipStream_t stream);
 constexpr int kStripeVariant = 3;
+// column stripes run the packed (int16 halves) fill for this scoring
+bool stripe_packed(const Scoring &sc);
 constexpr int kWidePackedVariant = 8;        // packed, 64-lane groups, up to 1,024 columns
 constexpr uint64_t kWidePackedMinPairs = 1536;  // fewer such pairs: column stripes (measured crossover 1,024-2,048)
 hipError_t launch_score_results(const NwPairDesc *pairs, uint32_t first, uint32_t n,

@@ -25,6 +25,10 @@
 #include "nw_common.hpp"
 #include "saln.h"
 
+namespace saln {
+bool stripe_packed(const Scoring &sc);
+}
+
 #ifndef SALN_PINGPONG
 #define SALN_PINGPONG 1
 #endif
@@ -581,15 +585,18 @@ __global__ __launch_bounds__(256) void nw_traceback_kernel(
 constexpr int32_t kCoopLine = 256;  // bytes per line (one stripe step)
 constexpr int32_t kCoopSlack = 64;  // rows loaded beyond a diagonal crossing of the stripe
 
-template <int NWV>
+// kPk: the packed stripe layout (bs == 0): virtual lane v = (c - c0) / 2 of
+// row r sits on line r - 1 + v (127 lines of skew instead of 63).
+template <int NWV, bool kPk>
 __global__ __launch_bounds__(64 * NWV) void nw_traceback_coop_kernel(
     const NwPairDesc *__restrict__ pairs, uint32_t first, const uint8_t *__restrict__ mask,
     const int32_t *__restrict__ end_h, saln_nw_result *__restrict__ results,
     uint32_t *__restrict__ cigar, Scoring sc, int32_t kCoopRows) {
-    // kCoopRows + 63 lines, rounded up to whole 4-line DMAs; then the request
-    // words wave 0 posts to the loader waves
+    constexpr int32_t kSkew = kPk ? 127 : 63;  // lines from a row's first to its last block
+    // kCoopRows + kSkew lines, rounded up to whole 4-line DMAs; then the
+    // request words wave 0 posts to the loader waves
     extern __shared__ __attribute__((aligned(16))) uint8_t win[];
-    int32_t *req = reinterpret_cast<int32_t *>(win + (kCoopRows + 64) * kCoopLine);
+    int32_t *req = reinterpret_cast<int32_t *>(win + (kCoopRows + kSkew + 1) * kCoopLine);
     const int32_t lane = (int32_t)threadIdx.x % 64, wv = (int32_t)threadIdx.x / 64;
     const uint32_t idx = first + blockIdx.x;
     const NwPairDesc p = pairs[idx];
@@ -602,8 +609,8 @@ __global__ __launch_bounds__(64 * NWV) void nw_traceback_coop_kernel(
         // a near-diagonal path leaves the stripe after j - c_lo + 1 rows:
         // load those plus some slack for gaps, not the whole window height
         r_lo = max(1, i - min(kCoopRows, j - c_lo + 1 + kCoopSlack) + 1);
-        // lines r_lo-1 .. i+62 of stripe s (row r of lane l is line r-1+l)
-        const int32_t t_lo = r_lo - 1, t_hi = i + 62;
+        // lines r_lo-1 .. i-1+kSkew of stripe s (row r of lane l is line r-1+l)
+        const int32_t t_lo = r_lo - 1, t_hi = i - 1 + kSkew;
         const uint8_t *reg = m + (uint64_t)s * p.mask_cs;
         typedef __attribute__((address_space(3))) void lds_v;
         for (int32_t mm = w; 4 * mm <= t_hi - t_lo; mm += NWV) {
@@ -642,6 +649,11 @@ __global__ __launch_bounds__(64 * NWV) void nw_traceback_coop_kernel(
     // code byte of interior cell (r, c) inside the window, bits 0-6 present-sets
     auto code = [&](int32_t r, int32_t c) __attribute__((always_inline)) {
         const int32_t o = c - c_lo;
+        if constexpr (kPk) {
+            const int32_t v = o >> 1;
+            return (uint32_t)win[(r - r_lo + v) * kCoopLine + 4 * (v & 63) + 2 * (o & 1) + (v >> 6)] ^
+                   0x7Fu;
+        }
         return (uint32_t)win[(r - r_lo + (o >> 2)) * kCoopLine + o] ^ 0x7Fu;
     };
     int32_t i = ld, j = lq;
@@ -1603,6 +1615,299 @@ __global__ __launch_bounds__(64) void nw_fill_stripe_kernel(
     if (failed && lane == 0) atomicOr(err, 1u);
 }
 
+// ------------------------------------------- long pairs: packed stripe fill
+// The column-stripe protocol of nw_fill_stripe_kernel with int16 pairs.  A
+// stripe's 256 columns are 128 virtual lanes of 2 columns: lane l holds
+// virtual lane l in its low halves and virtual lane 64 + l in its high
+// halves.  A row's chain runs lanes 0..63 in the low halves and then, one
+// step later, lanes 0..63 in the high halves (wave_ror: lane 0's high half
+// takes lane 63's low half), so at step t lane l works on row t - l + 1 low
+// and row t - l - 63 high.  Every value of row r is held relative to the
+// row's frame B(r) = H~(r, c0) & ~1 (even: the panic flags survive), the
+// stripe's left input: a row's values lie within 256 * (2|m| + 4|ge|) of it
+// whatever the pair's length (packed_stripe_ok).  The frame step
+// dB(r) = B(r) - B(r-1) travels down the chain with the row (0 for rows
+// outside the db), and a lane moves its carried state (previous-row H, D,
+// the diagonal) into the new frame with one v_pk_sub each.  Halves outside
+// the db keep their state (bit selects, first 128 and last steps only).
+// The last lane tracks B of its high-half row to publish absolute values.
+// Mask layout (nw_common.hpp, bs == 0): line t of a stripe's region holds
+// the lanes' code dwords of step t, lane l's dword [lo k0, hi k0, lo k1, hi k1].
+template <int kCodes>
+__global__ __launch_bounds__(64) void nw_fill_stripe_pk_kernel(
+    const NwPairDesc *__restrict__ pairs, const uint2 *__restrict__ work,
+    const uint8_t *__restrict__ qs, const uint8_t *__restrict__ ds, uint8_t *__restrict__ mask,
+    int2 *__restrict__ scratch, uint32_t *__restrict__ prog, uint32_t *__restrict__ err,
+    int32_t *__restrict__ end_h, Scoring sc) {
+    constexpr int G = 64, K = 2, W = 256;
+    const int lane = threadIdx.x;
+    const uint2 wk = work[blockIdx.x];
+    const NwPairDesc p = pairs[wk.x];
+    const uint32_t c = wk.y;
+    const uint32_t lq = p.len_q, ld = p.len_db;
+    const uint8_t *__restrict__ q = qs + p.q_off;
+    const uint8_t *__restrict__ d = ds + p.db_off;
+    const uint32_t nch = (lq + W - 1) / W;
+    const int2 *__restrict__ scr_in = c > 0 ? scratch + p.scratch_off + (uint64_t)(c - 1) * (ld + 2) : nullptr;
+    int2 *__restrict__ scr_out = c + 1 < nch ? scratch + p.scratch_off + (uint64_t)c * (ld + 2) : nullptr;
+    uint32_t *prog_in = c > 0 ? prog + p.reserved + c - 1 : nullptr;
+    uint32_t *prog_out = prog + p.reserved + c;
+    const int32_t beta = -2 * sc.gap_extend;
+    const int32_t alpha = -2 * sc.match - beta;
+    const uint32_t kPen = cst2(2 * (sc.match - sc.mismatch));  // 2 <= pen <= 32
+    const uint32_t kOpen = cst2(2 * sc.gap_open);
+    const uint32_t kDstep = cst2(2 * sc.gap_extend + alpha);
+    auto psub = [](uint32_t a, uint32_t b) { return as_u(as_s2(a) - as_s2(b)); };
+
+    const int c0 = (int)(c * W);
+    const int col_lo = c0 + 2 * lane, col_hi = c0 + 128 + 2 * lane;  // my columns: +1, +2
+    const int32_t B0 = c == 0 ? 0 : ((hs_row0(sc, (uint32_t)c0) + beta * c0) & ~1);
+    uint32_t qc[K], Hp[K], HpB[K], Dn[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const int jl = col_lo + k + 1, jh = col_hi + k + 1;
+        const uint32_t ca = jl <= (int)lq ? (uint32_t)q[jl - 1] << 5 : 0xE000u;
+        const uint32_t cb = jh <= (int)lq ? (uint32_t)q[jh - 1] << 5 : 0xE000u;
+        qc[k] = ca | (cb << 16);
+        Hp[k] = pkb(hs_row0(sc, (uint32_t)jl) + beta * jl - B0, hs_row0(sc, (uint32_t)jh) + beta * jh - B0);
+        Dn[k] = pkb(ds_row1(sc, (uint32_t)jl) + alpha + beta * jl - B0,
+                    ds_row1(sc, (uint32_t)jh) + alpha + beta * jh - B0);
+    }
+    uint32_t hd = pkb(hs_row0(sc, (uint32_t)col_lo) + beta * col_lo - B0,
+                      hs_row0(sc, (uint32_t)col_hi) + beta * col_hi - B0);
+    uint32_t pubH = Hp[K - 1], pubF = 0x80008000u, dch = 0, dBc = 0;
+    int32_t Bprev = B0;   // lane 0's frame of the previous row (wave-uniform)
+    int32_t B63 = B0;     // frame of my high-half row (read in the last lane)
+    typedef const __attribute__((address_space(4))) uint32_t cu32;  // constant: scalar loads
+    cu32 *dw = (cu32 *)((uintptr_t)d & ~(uintptr_t)3);
+    const uint32_t doff = 8u * (uint32_t)((uintptr_t)d & 3);
+    const uint32_t last_dw = ((uint32_t)ld - 1 + (uint32_t)((uintptr_t)d & 3)) >> 2;
+    uint32_t dnidx = min(1u, last_dw);
+    uint32_t dcur = dw[0], dnxt = dw[dnidx];
+    auto group_chars = [&]() __attribute__((always_inline)) {
+        const uint32_t w = doff ? (dcur >> doff) | (dnxt << (32u - doff)) : dcur;
+        dcur = dnxt;
+        dnidx = min(dnidx + 1, last_dw);
+        dnxt = dw[dnidx];
+        return w;
+    };
+    int32_t blkH = 0, blkF = 0;
+    uint32_t avail = 0;
+    bool failed = false;
+    uint8_t *mseg = mask + p.mask_off + (uint64_t)c * p.mask_cs + (uint32_t)lane * 4u;
+    const int T = (int)ld + 2 * G - 1;
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the query chars
+    // lane 0 <- boundary (low half); others <- lane-1 of the previous step;
+    // lane 0's high half <- lane 63's low half (the row continues)
+    auto chain = [&](uint32_t v, uint32_t bnd16) __attribute__((always_inline)) {
+        const uint32_t rot = __builtin_amdgcn_update_dpp(0u, v, 0x13C /*wave_ror:1*/, 0xf, 0xf, false);
+        const uint32_t fix = __builtin_amdgcn_perm(rot, bnd16, 0x05040100u);
+        return lane == 0 ? fix : rot;
+    };
+    int32_t gH0 = 0, gH1 = 0, gH2 = 0, gH3 = 0, gF0 = 0, gF1 = 0, gF2 = 0, gF3 = 0;
+    auto step = [&](int t, uint32_t(&Hin)[K], uint32_t(&Hout)[K], uint32_t dt, auto pos_c,
+                    auto sel_c) __attribute__((always_inline)) {
+        constexpr int kPos = decltype(pos_c)::value;
+        constexpr bool kSel = decltype(sel_c)::value;  // some half outside the db
+        const uint32_t rr = (uint32_t)t + 1;  // lane 0's low-half row
+        int32_t inH0 = 0, inF0 = 0, dB0 = 0;
+        if (rr <= ld) {
+            int32_t bF, bH;
+            if (c == 0) {
+                bF = is_col1(sc, rr) + alpha * (int32_t)rr + beta;
+                bH = hs_col0(sc, rr) + alpha * (int32_t)rr;
+            } else {
+                if (kPos == 0 && (rr - 1) % kPub == 0) {  // new 32-row block of the left column
+                    const uint32_t need = min(rr - 1 + kPub, ld);
+                    uint32_t spins = 0;
+                    while (avail < need && !failed) {
+                        avail = __hip_atomic_load(prog_in, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        avail = __builtin_amdgcn_readfirstlane(avail);
+                        if (avail < need) {
+                            __builtin_amdgcn_s_sleep(2);
+                            if (++spins > kSpinCap) failed = true;
+                        }
+                    }
+                    const uint32_t row = rr + (uint32_t)lane;
+                    if (lane < (int)kPub && row <= ld) {
+                        const uint64_t v = __hip_atomic_load((const uint64_t *)(scr_in + row),
+                                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        blkH = (int32_t)(uint32_t)v;
+                        blkF = (int32_t)(uint32_t)(v >> 32);
+                    }
+                    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0), on the block step only
+                }
+                const uint32_t sl = (rr - 1) % kPub;
+                bH = __builtin_amdgcn_readlane(blkH, sl);
+                bF = __builtin_amdgcn_readlane(blkF, sl);
+            }
+            const int32_t Bn = bH & ~1;
+            dB0 = Bn - Bprev;
+            Bprev = Bn;
+            inH0 = bH - Bn;
+            inF0 = bF - Bn;
+        }
+        dch = chain(dch, dt << 5);
+        const uint32_t dB = chain(dBc, (uint32_t)dB0 & 0xFFFFu);
+        const uint32_t inF = chain(pubF, (uint32_t)(inF0 + 32768) & 0xFFFFu);
+        const uint32_t inH = chain(pubH, (uint32_t)(inH0 + 32768) & 0xFFFFu);
+        dBc = dB;
+        B63 += (int32_t)dB >> 16;  // the high half's frame step
+        // carried state into this row's frame (dB is 0 for a half outside the db)
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            Hin[k] = psub(Hin[k], dB);
+            Dn[k] = psub(Dn[k], dB);
+        }
+        hd = psub(hd, dB);
+        uint32_t F = inF;
+        uint32_t diag = hd;
+        uint32_t prv[8];
+        uint32_t cw = 0;
+        uint32_t Dnew[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const uint32_t hdk = diag;
+            diag = Hin[k];
+            const uint32_t pen = umin2(qc[k] ^ dch, kPen);
+            const uint32_t M = hdk - pen;
+            const uint32_t I = F, D = Dn[k];
+            const uint32_t H = umax2(M, umax2(I, D));
+            const uint32_t tO = M + kOpen;
+            if constexpr (kCodes != kCodesNone) {
+                const uint32_t Hc = H & 0xFFFEFFFEu;
+                const uint32_t tOr = tO | 0x00010001u;
+                uint32_t sg[8];
+                sg[0] = psub(M, Hc);
+                sg[1] = psub(I, Hc);
+                sg[2] = psub(D, Hc);
+                sg[4] = psub(tOr, I);
+                sg[6] = psub(tOr, D);
+                sg[7] = pen - 0x00010001u;
+                if constexpr (kCodes == kCodesFull) {
+                    const uint32_t tOc = tO & 0xFFFEFFFEu;
+                    sg[3] = psub(I, tOc);
+                    sg[5] = psub(D, tOc);
+                } else {
+                    sg[3] = sg[5] = 0u;
+                }
+                if (k == 0) {
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) prv[u] = sg[u];
+                } else {
+                    uint32_t pw[8];
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) pw[u] = col_pair_signs(sg[u], prv[u]);
+                    cw = kCodes == kCodesFull ? merge_full(pw) : merge_walk<true>(pw);
+                }
+            }
+            F = umax2(tO, I);
+            Dnew[k] = umax2(tO, D) + kDstep;
+            Hout[k] = H;
+        }
+        if constexpr (kSel) {  // keep the state of a half outside the db
+            const int rlo = t - lane + 1, rhi = rlo - G;
+            const uint32_t vm = ((rlo >= 1 && rlo <= (int)ld) ? 0x0000FFFFu : 0u) |
+                                ((rhi >= 1 && rhi <= (int)ld) ? 0xFFFF0000u : 0u);
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                Hout[k] = bfi(vm, Hout[k], Hin[k]);
+                Dn[k] = bfi(vm, Dnew[k], Dn[k]);
+            }
+            hd = bfi(vm, inH, hd);
+            pubF = bfi(vm, F, pubF);
+            pubH = bfi(vm, Hout[K - 1], pubH);
+        } else {
+#pragma unroll
+            for (int k = 0; k < K; ++k) Dn[k] = Dnew[k];
+            hd = inH;
+            pubF = F;
+            pubH = Hout[K - 1];
+        }
+        if constexpr (kCodes != kCodesNone) *reinterpret_cast<uint32_t *>(mseg) = cw;
+        mseg += kCoopLine;
+        // the last lane's high-half row t - 126 as absolute values
+        const int32_t aH = (int32_t)(pubH >> 16) - 32768 + B63;
+        const int32_t aF = (int32_t)(pubF >> 16) - 32768 + B63;
+        if constexpr (kPos == 0) gH0 = aH, gF0 = aF;
+        if constexpr (kPos == 1) gH1 = aH, gF1 = aF;
+        if constexpr (kPos == 2) gH2 = aH, gF2 = aF;
+        if constexpr (kPos == 3) gH3 = aH, gF3 = aF;
+    };
+    auto publish = [&](int t0, int n) __attribute__((always_inline)) {
+        if (lane == G - 1 && scr_out) {
+            const int lo = max(t0 - (2 * G - 2), 1), hi = min(t0 + n - 1 - (2 * G - 2), (int)ld);
+            if (hi >= lo) {
+                auto put = [&](int qq, int32_t h, int32_t f) __attribute__((always_inline)) {
+                    const int r = t0 + qq - (2 * G - 2);
+                    if (qq < n && r >= lo && r <= hi)
+                        __hip_atomic_store((uint64_t *)(scr_out + r),
+                                           (uint64_t)(uint32_t)h | ((uint64_t)(uint32_t)f << 32),
+                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                };
+                put(0, gH0, gF0);
+                put(1, gH1, gF1);
+                put(2, gH2, gF2);
+                put(3, gH3, gF3);
+                if (hi / (int)kPub != (lo - 1) / (int)kPub || hi == (int)ld) {
+                    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): column stores done
+                    __hip_atomic_store(prog_out, (uint32_t)hi, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+                }
+            }
+        }
+    };
+    const std::integral_constant<int, 0> p0;
+    const std::integral_constant<int, 1> p1;
+    const std::integral_constant<int, 2> p2;
+    const std::integral_constant<int, 3> p3;
+    const std::true_type slow;
+    const std::false_type fast;
+    int t = 0;
+    for (; t + 3 < T; t += 4) {
+        const uint32_t w = group_chars();
+        if (t >= 2 * G && t + 3 <= (int)ld - 1) {  // every half of every lane inside the db
+            step(t, Hp, HpB, w & 0xFFu, p0, fast);
+            step(t + 1, HpB, Hp, (w >> 8) & 0xFFu, p1, fast);
+            step(t + 2, Hp, HpB, (w >> 16) & 0xFFu, p2, fast);
+            step(t + 3, HpB, Hp, w >> 24, p3, fast);
+        } else {
+            step(t, Hp, HpB, w & 0xFFu, p0, slow);
+            step(t + 1, HpB, Hp, (w >> 8) & 0xFFu, p1, slow);
+            step(t + 2, Hp, HpB, (w >> 16) & 0xFFu, p2, slow);
+            step(t + 3, HpB, Hp, w >> 24, p3, slow);
+        }
+        publish(t, 4);
+    }
+    const int ntail = T - t;
+    if (ntail > 0) {
+        const uint32_t w = group_chars();
+        step(t, Hp, HpB, w & 0xFFu, p0, slow);
+        if (ntail > 1) step(t + 1, HpB, Hp, (w >> 8) & 0xFFu, p1, slow);
+        if (ntail > 2) step(t + 2, Hp, HpB, (w >> 16) & 0xFFu, p2, slow);
+        publish(t, ntail);
+    }
+    // end cell: every half ends on row ld in the array the last step wrote
+    const uint32_t jend = lq - 1;
+    if (jend / W == c) {
+        const uint32_t o = jend % W, v = o / 2;
+        if ((uint32_t)lane == v % 64) {
+            const uint32_t hv = v / 64, ke = o % 2;
+            uint32_t wv = 0;
+#pragma unroll
+            for (int k = 0; k < K; ++k)
+                if ((uint32_t)k == ke) wv = (ntail & 1) ? HpB[k] : Hp[k];
+            const int32_t rel = (int32_t)(hv ? wv >> 16 : wv & 0xFFFFu) - 32768;
+            const int32_t Bld = c == 0 ? (hs_col0(sc, ld) + alpha * (int32_t)ld) & ~1
+                                       : (int32_t)(uint32_t)__hip_atomic_load(
+                                             (const uint64_t *)(scr_in + ld), __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT) & ~1;
+            end_h[wk.x] = rel + Bld - alpha * (int32_t)ld - beta * (int32_t)lq;
+        }
+    }
+    if (failed && lane == 0) atomicOr(err, 1u);
+}
+
 // Score-only results (saln_nw_plan_set_score_only): score and panic status
 // from the end value; no traceback fields (flags bit 3).
 __global__ __launch_bounds__(256) void nw_score_results_kernel(const NwPairDesc *__restrict__ pairs,
@@ -1845,14 +2150,21 @@ hipError_t launch_traceback(int variant, const NwPairDesc *pairs, uint32_t first
             // a few pairs: the whole 160 KB (fewer window reloads); batches:
             // 48 KB windows, three waves per CU
             constexpr int kLoaders = 4;  // waves per pair: one walks, all load its windows
-            static const hipError_t attr = hipFuncSetAttribute(
-                (const void *)nw_traceback_coop_kernel<kLoaders>,
-                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-            if (attr != hipSuccess) return attr;
-            const int32_t rows = n <= 256 ? 568 : 128;
-            nw_traceback_coop_kernel<kLoaders>
-                <<<dim3(n), dim3(64 * kLoaders), (size_t)(rows + 64) * kCoopLine + 16, stream>>>(
-                    pairs, first, mask, end_h, results, cigar, sc, rows);
+            auto go = [&](auto pk_c) -> hipError_t {
+                constexpr bool kPk = decltype(pk_c)::value;
+                constexpr int32_t kSkew = kPk ? 127 : 63;
+                static const hipError_t attr = hipFuncSetAttribute(
+                    (const void *)nw_traceback_coop_kernel<kLoaders, kPk>,
+                    hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+                if (attr != hipSuccess) return attr;
+                const int32_t rows = n <= 256 ? 632 - (kSkew + 1) : 128;
+                nw_traceback_coop_kernel<kLoaders, kPk>
+                    <<<dim3(n), dim3(64 * kLoaders), (size_t)(rows + kSkew + 1) * kCoopLine + 16,
+                       stream>>>(pairs, first, mask, end_h, results, cigar, sc, rows);
+                return hipSuccess;
+            };
+            const hipError_t e = stripe_packed(sc) ? go(std::true_type{}) : go(std::false_type{});
+            if (e != hipSuccess) return e;
             break;
         }
         case 5: tb_lds<16, 16>(grid, stream, pairs, first, n, mask, end_h, ops, results, cigar, sc); break;
@@ -1876,9 +2188,14 @@ hipError_t launch_fill_stripes(const NwPairDesc *pairs, const uint2 *work, uint3
     if (!n_work) return hipSuccess;
     const dim3 grid(n_work), block(64);
     const int32_t pen_max = 2 * (sc.match - sc.mismatch);
+    const bool pk = stripe_packed(sc);
     auto go = [&](auto codes_c, auto minpen_c) {
-        nw_fill_stripe_kernel<4, decltype(codes_c)::value, decltype(minpen_c)::value>
-            <<<grid, block, 0, stream>>>(pairs, work, qs, ds, mask, scratch, prog, err, end_h, sc);
+        if (pk)
+            nw_fill_stripe_pk_kernel<decltype(codes_c)::value>
+                <<<grid, block, 0, stream>>>(pairs, work, qs, ds, mask, scratch, prog, err, end_h, sc);
+        else
+            nw_fill_stripe_kernel<4, decltype(codes_c)::value, decltype(minpen_c)::value>
+                <<<grid, block, 0, stream>>>(pairs, work, qs, ds, mask, scratch, prog, err, end_h, sc);
     };
     auto by_codes = [&](auto minpen_c) {
         if (codes == kCodesFull) go(std::integral_constant<int, kCodesFull>{}, minpen_c);
@@ -1914,6 +2231,22 @@ hipError_t launch_cigar_compact(const saln_nw_result *res, const uint64_t *src_o
 }
 
 Geom variant_geom(int v) { return kVariants[v]; }
+
+// The packed stripe fill holds a row relative to the stripe's left input:
+// within 256 columns of it values span 256 * (2|m| + 4|ge|) plus the gap
+// and penalty offsets of M / I / D (see nw_fill_stripe_pk_kernel).
+// Opt-in (SALN_STRIPE_PK=1, read per plan): the 128-virtual-lane chain
+// doubles a stripe's skew, so one long pair (C4) fills slower (49.7 vs
+// 44.9 ms) although the step is cheaper; batches of 2-5 kbp pairs fill
+// 8-16 % faster but walk slower (+63 lines per window).
+bool stripe_packed(const Scoring &sc) {
+    const char *e = std::getenv("SALN_STRIPE_PK");
+    if (!(e && e[0] == '1')) return false;
+    const int64_t pen = 2ll * (sc.match - sc.mismatch);
+    if (pen < 2 || pen > 32 || sc.gap_extend > 0 || sc.gap_open > 0) return false;
+    const int64_t m = std::abs(sc.match), ge = std::abs(sc.gap_extend), go = std::abs(sc.gap_open);
+    return 256 * (2 * m + 4 * ge) + 4 * (go + ge) + 2 * pen + 512 < 30000;
+}
 bool variant_packed(int v) { return kPacked[v]; }
 
 // Packed i16 is exact while every value and every same-cell difference stays

@@ -306,6 +306,29 @@ def test_wide_packed_variant(saln, oracle):
                 assert (saln.cigar_ops_string(cig[k]) if res["printed"][k] else None) == o.first_ops, (n, k)
 
 
+def test_packed_stripe_fill(saln, oracle, monkeypatch):
+    """The opt-in packed column-stripe fill (SALN_STRIPE_PK=1: int16 halves,
+    128 virtual lanes, per-row frames) and its mask layout: stripe pairs alone
+    (full parent mask, first alignment) and in a batch through the cooperative
+    walker equal the oracle."""
+    from sequencealigning_amd import synth
+    monkeypatch.setenv("SALN_STRIPE_PK", "1")
+    rng = np.random.default_rng(999)
+    for lq, ld in [(513, 70), (1025, 40), (700, 900), (1300, 1280)]:
+        _compare(saln, oracle, rand_seq(rng, lq), rand_seq(rng, ld), text=False)
+    q, d = synth.mut_pair(2500, 0.05, 4545)
+    cases = [(q, d), (rand_seq(rng, 1100), rand_seq(rng, 1000)),
+             (bytes(rng.choice([65, 67], 1200).astype(np.uint8)),
+              bytes(rng.choice([65, 67], 1150).astype(np.uint8)))]
+    res, cig = saln.nw_align_batch([a for a, _ in cases], [b for _, b in cases],
+                                   pairs=[(k, k) for k in range(len(cases))])
+    for k, (a, b) in enumerate(cases):
+        o = oracle.nw(a, b, literal_dfs=False)
+        assert (int(res["score"][k]), int(res["end_states"][k]), int(res["status"][k]) == 2) == \
+            (o.score, o.end_states, o.panics), k
+        assert (saln.cigar_ops_string(cig[k]) if res["printed"][k] else None) == o.first_ops, k
+
+
 @pytest.mark.parametrize("L", [3000])
 def test_long_pair_stripes(saln, oracle, L):
     """A single long mutated pair through the column-stripe fill (12 stripes of
