@@ -329,6 +329,30 @@ def test_packed_stripe_fill(saln, oracle, monkeypatch):
         assert (saln.cigar_ops_string(cig[k]) if res["printed"][k] else None) == o.first_ops, k
 
 
+def test_context_block_cache_reuse(saln, oracle):
+    """Plans of different sizes created and destroyed in turn on one context
+    reuse its cached device blocks (dirty from the previous plan): results
+    stay equal to the first run's and to the oracle's."""
+    rng = np.random.default_rng(1212)
+    batches = []
+    for lq, ld, n in [(150, 150, 300), (1100, 900, 3), (40, 2000, 20), (700, 650, 4), (150, 150, 300)]:
+        qs = [rand_seq(rng, lq) for _ in range(n)]
+        ds = [rand_seq(rng, ld) for _ in range(n)]
+        batches.append((qs, ds))
+    first = []
+    for qs, ds in batches:
+        res, cig = saln.nw_align_batch(qs, ds, pairs=[(k, k) for k in range(len(qs))])
+        first.append((res.copy(), cig))
+    for rep in range(2):
+        for (qs, ds), (r0, c0) in zip(batches[::-1], first[::-1]):
+            res, cig = saln.nw_align_batch(qs, ds, pairs=[(k, k) for k in range(len(qs))])
+            assert np.array_equal(res, r0) and cig == c0, rep
+    for (qs, ds), (r0, c0) in zip(batches[1:4], first[1:4]):
+        for k in range(min(3, len(qs))):
+            o = oracle.nw(qs[k], ds[k], literal_dfs=False)
+            assert (int(r0["score"][k]), int(r0["end_states"][k])) == (o.score, o.end_states)
+
+
 @pytest.mark.parametrize("L", [3000])
 def test_long_pair_stripes(saln, oracle, L):
     """A single long mutated pair through the column-stripe fill (12 stripes of
