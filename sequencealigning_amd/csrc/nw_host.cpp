@@ -573,7 +573,7 @@ int plan_set_full_codes(saln_nw_plan *p, bool full) {
 int plan_pair_mask(const saln_nw_plan *p, uint64_t pair_id, PairMask *pm) {
     if (!p || pair_id >= p->n_pairs) return SALN_E_INVALID;
     const NwPairDesc &d = p->h_pairs[p->plan_index[pair_id]];
-    if (!p->full_codes && (variant_packed((int)d.variant) || d.variant == (uint32_t)kStripeVariant)) {
+    if (!p->full_codes) {  // every fill stores walk codes unless the plan asks for all parents
         set_error("plan_pair_mask: plan stores walk codes only");
         return SALN_E_INVALID;
     }

@@ -793,115 +793,6 @@ struct MaskWords {
     uint32_t w[(K + 3) / 4];
 };
 
-template <int G, int K>
-__global__ __launch_bounds__(256) void nw_fill_kernel(const NwPairDesc *__restrict__ pairs,
-                                                      uint32_t first, uint32_t count,
-                                                      const uint8_t *__restrict__ qs,
-                                                      const uint8_t *__restrict__ ds,
-                                                      uint8_t *__restrict__ mask,
-                                                      int2 *__restrict__ scratch,
-                                                      int32_t *__restrict__ end_h,
-                                                      saln_nw_result *__restrict__ results,
-                                                      uint32_t *__restrict__ cigar, Scoring sc) {
-    constexpr int GPB = 256 / G;
-    constexpr int KD = (K + 3) / 4;
-    constexpr Geom geo{G, K};
-    const int lane = threadIdx.x % G;
-    const uint32_t gi = pack_block(blocks_per_pack(GPB)) * GPB + threadIdx.x / G;
-    if (gi >= count) return;  // whole group (DPP never crosses groups)
-    const NwPairDesc p = pairs[first + gi];
-    const uint32_t lq = p.len_q, ld = p.len_db;
-    const uint8_t *__restrict__ q = qs + p.q_off;
-    const uint8_t *__restrict__ d = ds + p.db_off;
-    uint8_t *__restrict__ mk = mask + p.mask_off;
-    int2 *__restrict__ scr = scratch + p.scratch_off;
-    const uint32_t nch = geo.n_chunks(lq);
-    const int32_t sM = 2 * sc.match, sX = 2 * sc.mismatch;
-    const int32_t sO = 2 * sc.gap_open, sE = 2 * sc.gap_extend;
-    // end cell owner
-    const uint32_t jend = lq - 1;
-    const uint32_t c_end = jend / geo.W(), l_end = (jend % geo.W()) / K, k_end = jend % K;
-    int32_t my_end = 0;
-
-    for (uint32_t c = 0; c < nch; ++c) {
-        const uint32_t col0 = c * geo.W() + (uint32_t)lane * K;  // my columns: col0+1 .. col0+K
-        int32_t qc[K], Hp[K], Dn[K];
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-            const uint32_t j = col0 + k + 1;
-            qc[k] = j <= lq ? (int32_t)q[j - 1] : -1;
-            Hp[k] = hs_row0(sc, j);  // H'(0, j)
-            Dn[k] = ds_row1(sc, j);  // D'(1, j)
-        }
-        int32_t hd = hs_row0(sc, col0);  // H'(r-1, col0): diagonal of my first column
-        int32_t pubF = 0, pubH = 0;
-        int32_t dnext = (lane == 0) ? (int32_t)d[0] : 0;
-        int2 bnext = make_int2(0, 0);
-        if (c > 0 && lane == 0) bnext = scr[1];
-        // this lane's segment of row 1 in block c*G + lane
-        uint8_t *mseg = mk + (uint64_t)(c * G + (uint32_t)lane) * p.mask_bs;
-        const int T = (int)geo.steps(ld);
-
-        for (int t = 0; t < T; ++t) {
-            const int r = t - lane + 1;
-            const int32_t dch = dnext;
-            if (r >= 0 && r < (int)ld) dnext = (int32_t)d[r];
-            int32_t bF, bH;
-            if (c == 0) {
-                bF = is_col1(sc, (uint32_t)(t + 1));
-                bH = hs_col0(sc, (uint32_t)(t + 1));
-            } else {
-                bH = bnext.x;
-                bF = bnext.y;
-                if (lane == 0 && t + 2 <= (int)ld) bnext = scr[t + 2];
-            }
-            const int32_t inF = shr1<G>(bF, pubF);  // I'(r, col0+1)
-            const int32_t inH = shr1<G>(bH, pubH);  // H'(r, col0)
-            if (r >= 1 && r <= (int)ld) {
-                int32_t F = inF;
-                MaskWords<K> mw;
-#pragma unroll
-                for (int k = 0; k < KD; ++k) mw.w[k] = 0;
-#pragma unroll
-                for (int k = 0; k < K; ++k) {
-                    const bool eq = qc[k] == dch;
-                    const int32_t M = hd + (eq ? sM : sX);
-                    const int32_t I = F, D = Dn[k];
-                    const int32_t H = max(M, max(I, D));
-                    const int32_t Hc = H & ~1;
-                    const int32_t tO = M + sO;
-                    uint32_t b = (M >= Hc ? kArgM : 0u) | (I >= Hc ? kArgI : 0u) |
-                                 (D >= Hc ? kArgD : 0u);
-                    b |= ((I | 1) >= tO ? kIExt : 0u) | ((tO | 1) >= I ? kIOpen : 0u);
-                    b |= ((D | 1) >= tO ? kDExt : 0u) | ((tO | 1) >= D ? kDOpen : 0u);
-                    b |= eq ? 0x80u : 0u;  // bit 7: q == d (not inverted)
-                    mw.w[k / 4] |= b << (8 * (k % 4));
-                    F = max(tO, I) + sE;
-                    Dn[k] = max(tO, D) + sE;
-                    hd = Hp[k];
-                    Hp[k] = H;
-                }
-                hd = inH;
-                pubF = F;
-                pubH = Hp[K - 1];
-#pragma unroll
-                for (int k = 0; k < KD; ++k) mw.w[k] ^= 0x7F7F7F7Fu;  // stored inverted
-                *reinterpret_cast<MaskWords<K> *>(mseg + (uint64_t)(r - 1) * p.mask_rs) = mw;
-                if (lane == G - 1 && c + 1 < nch) scr[r] = make_int2(pubH, pubF);
-                if (c == c_end && (uint32_t)lane == l_end && r == (int)ld) {
-#pragma unroll
-                    for (int k = 0; k < K; ++k)
-                        if ((uint32_t)k == k_end) my_end = Hp[k];
-                    end_h[first + gi] = my_end;
-                }
-            }
-        }
-        if (c + 1 < nch) __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-    }
-    (void)my_end;
-    (void)results;
-    (void)cigar;
-}
 
 // ----------------------------------------------------- long pairs: stripes
 // One wave per column stripe of G*K = 64*K columns; all stripes of a pair run
@@ -1615,6 +1506,175 @@ __global__ __launch_bounds__(64) void nw_fill_stripe_kernel(
     if (failed && lane == 0) atomicOr(err, 1u);
 }
 
+// ------------------------------------------------------------ i32 lanes
+// Pairs the packed fills cannot hold (long dbs, wide penalties): one pair per
+// group of G lanes, K columns per lane, i32 with the transformed recurrence
+// and sign-bit parent codes of the stripe fill (X~ = X' + alpha*r + beta*c;
+// the literal -32768 sentinel stays exact since the offsets are linear).
+// kStaged: the group's db row is staged in LDS (bytes, padded by G on both
+// sides) and a previous chunk's boundary column is read in G-row blocks with
+// the wait on the block step only: otherwise every step waits (vmcnt) for its
+// own char / boundary load and with it for every mask store.
+template <int G, int K, int kCodes, bool kMinPen, bool kStaged>
+__global__ __launch_bounds__(256) void nw_fill_lanes_kernel(
+    const NwPairDesc *__restrict__ pairs, uint32_t first, uint32_t count,
+    const uint8_t *__restrict__ qs, const uint8_t *__restrict__ ds, uint8_t *__restrict__ mask,
+    int2 *__restrict__ scratch, int32_t *__restrict__ end_h, Scoring sc, uint32_t ld_max) {
+    constexpr int GPB = 256 / G;
+    constexpr int KD = (K + 3) / 4;
+    constexpr Geom geo{G, K};
+    const int lane = threadIdx.x % G;
+    const uint32_t gi = pack_block(blocks_per_pack(GPB)) * GPB + threadIdx.x / G;
+    if (gi >= count) return;  // whole group (DPP never crosses groups)
+    const NwPairDesc p = pairs[first + gi];
+    const uint32_t lq = p.len_q, ld = p.len_db;
+    const uint8_t *__restrict__ q = qs + p.q_off;
+    const uint8_t *__restrict__ d = ds + p.db_off;
+    uint8_t *__restrict__ mk = mask + p.mask_off;
+    int2 *__restrict__ scr = scratch + p.scratch_off;
+    const uint32_t nch = geo.n_chunks(lq);
+    const int32_t beta = -2 * sc.gap_extend;
+    const int32_t alpha = -2 * sc.match - beta;
+    const int32_t pen_max = 2 * (sc.match - sc.mismatch);
+    const int32_t kOpen = 2 * sc.gap_open;
+    const int32_t kDstep = 2 * sc.gap_extend + alpha;
+    const uint32_t jend = lq - 1;
+    const uint32_t c_end = jend / geo.W(), l_end = (jend % geo.W()) / K, k_end = jend % K;
+    extern __shared__ uint8_t drow8[];  // kStaged: [GPB][G + ld_max + G] db chars
+    const uint8_t *myrow = drow8 + (threadIdx.x / G) * (ld_max + 2 * G) + G;
+    if constexpr (kStaged) {
+        uint8_t *row = drow8 + (threadIdx.x / G) * (ld_max + 2 * G) + G;
+        for (int i = lane; i < (int)ld; i += G) row[i] = d[i];
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+        __builtin_amdgcn_wave_barrier();
+    }
+    const int bsrc = (int)((threadIdx.x & 63u) & ~(uint32_t)(G - 1));  // my group's lane 0 in the wave
+
+    for (uint32_t c = 0; c < nch; ++c) {
+        const uint32_t col0 = c * geo.W() + (uint32_t)lane * K;  // my columns: col0+1 .. col0+K
+        uint32_t qc[K];
+        int32_t Hp[K], Dn[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const uint32_t j = col0 + k + 1;
+            qc[k] = j <= lq ? (uint32_t)q[j - 1] << 8 : 0xFFFFFF00u;
+            Hp[k] = hs_row0(sc, j) + beta * (int32_t)j;
+            Dn[k] = ds_row1(sc, j) + alpha + beta * (int32_t)j;
+        }
+        int32_t hd = hs_row0(sc, col0) + beta * (int32_t)col0;
+        int32_t pubF = 0, pubH = 0;
+        int32_t dnext = (!kStaged && lane == 0) ? (int32_t)d[0] : 0;
+        int2 bnext = make_int2(0, 0);
+        if (!kStaged && c > 0 && lane == 0) bnext = scr[1];
+        int32_t blkH = 0, blkF = 0;  // kStaged: lane i holds boundary row (block start + i)
+        uint8_t *mseg = mk + (uint64_t)(c * G + (uint32_t)lane) * p.mask_bs;
+        const int T = (int)geo.steps(ld);
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the query chars
+        for (int t = 0; t < T; ++t) {
+            const int r = t - lane + 1;
+            uint32_t dch;
+            if constexpr (kStaged) {
+                dch = (uint32_t)myrow[t - lane] << 8;  // d[r-1]; the pads cover r outside the db
+            } else {
+                dch = (uint32_t)dnext << 8;
+                if (r >= 0 && r < (int)ld) dnext = (int32_t)d[r];
+            }
+            int32_t bF, bH;
+            const int32_t rr = t + 1;  // lane 0's row
+            if (c == 0) {
+                bF = is_col1(sc, (uint32_t)rr) + alpha * rr + beta;
+                bH = hs_col0(sc, (uint32_t)rr) + alpha * rr;
+            } else if constexpr (kStaged) {
+                if (t % G == 0 && rr <= (int)ld) {  // wave-uniform: every group is at step t
+                    const int row = rr + lane;
+                    if (row <= (int)ld) {
+                        const int2 v = scr[row];
+                        blkH = v.x;
+                        blkF = v.y;
+                    }
+                    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0), on the block step only
+                }
+                const int src = (bsrc + t % G) * 4;
+                bH = __builtin_amdgcn_ds_bpermute(src, blkH);
+                bF = __builtin_amdgcn_ds_bpermute(src, blkF);
+            } else {
+                bH = bnext.x;
+                bF = bnext.y;
+                if (lane == 0 && t + 2 <= (int)ld) bnext = scr[t + 2];
+            }
+            const int32_t inF = shr1<G>(bF, pubF);  // I~(r, col0+1)
+            const int32_t inH = shr1<G>(bH, pubH);  // H~(r, col0)
+            if (r >= 1 && r <= (int)ld) {
+                int32_t F = inF;
+                uint32_t sg[8][4 * KD];
+#pragma unroll
+                for (int k = 0; k < K; ++k) {
+                    const uint32_t x = qc[k] ^ dch;
+                    const int32_t pen = kMinPen ? (int32_t)min(x, (uint32_t)pen_max) : (x ? pen_max : 0);
+                    const int32_t M = hd - pen;
+                    const int32_t I = F, D = Dn[k];
+                    const int32_t H = max(M, max(I, D));
+                    const int32_t tO = M + kOpen;
+                    if constexpr (kCodes != kCodesNone) {
+                        const int32_t Hc = H & ~1;
+                        const int32_t tOr = tO | 1;
+                        sg[0][k] = (uint32_t)(M - Hc);
+                        sg[1][k] = (uint32_t)(I - Hc);
+                        sg[2][k] = (uint32_t)(D - Hc);
+                        sg[4][k] = (uint32_t)(tOr - I);
+                        sg[6][k] = (uint32_t)(tOr - D);
+                        sg[7][k] = x - 1u;  // sign <=> q == d
+                        if constexpr (kCodes == kCodesFull) {
+                            const int32_t tOc = tO & ~1;
+                            sg[3][k] = (uint32_t)(I - tOc);
+                            sg[5][k] = (uint32_t)(D - tOc);
+                        } else {
+                            sg[3][k] = sg[5][k] = 0u;
+                        }
+                    }
+                    F = max(tO, I);
+                    Dn[k] = max(tO, D) + kDstep;
+                    hd = Hp[k];
+                    Hp[k] = H;
+                }
+                hd = inH;
+                pubF = F;
+                pubH = Hp[K - 1];
+                if constexpr (kCodes != kCodesNone) {
+#pragma unroll
+                    for (int k = K; k < 4 * KD; ++k)
+#pragma unroll
+                        for (int u = 0; u < 8; ++u) sg[u][k] = 0u;  // pad columns: never read
+                    MaskWords<K> mw;
+#pragma unroll
+                    for (int w = 0; w < KD; ++w) {
+                        uint32_t s4[8][4];
+#pragma unroll
+                        for (int u = 0; u < 8; ++u)
+#pragma unroll
+                            for (int k = 0; k < 4; ++k) s4[u][k] = sg[u][4 * w + k];
+                        mw.w[w] = stripe_code_word<kCodes>(s4);
+                    }
+                    *reinterpret_cast<MaskWords<K> *>(mseg + (uint64_t)(r - 1) * p.mask_rs) = mw;
+                }
+                if (lane == G - 1 && c + 1 < nch) scr[r] = make_int2(pubH, pubF);
+                if (c == c_end && (uint32_t)lane == l_end && r == (int)ld) {
+                    int32_t e = 0;
+#pragma unroll
+                    for (int k = 0; k < K; ++k)
+                        if ((uint32_t)k == k_end) e = Hp[k];
+                    end_h[first + gi] = e - alpha * (int32_t)ld - beta * (int32_t)lq;
+                }
+            }
+        }
+        if (c + 1 < nch) {
+            __builtin_amdgcn_s_waitcnt(0x0F70);  // the boundary column is stored
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+        }
+    }
+}
+
 // ------------------------------------------- long pairs: packed stripe fill
 // The column-stripe protocol of nw_fill_stripe_kernel with int16 pairs.  A
 // stripe's 256 columns are 128 virtual lanes of 2 columns: lane l holds
@@ -1961,10 +2021,27 @@ static bool packed_ok(uint32_t lq, uint32_t ld, const Scoring &sc);
 template <int G, int K>
 static void fill_i32(dim3 grid, hipStream_t s, const NwPairDesc *pairs, uint32_t first,
                      uint32_t count, const uint8_t *qs, const uint8_t *ds, uint8_t *mask,
-                     int2 *scratch, int32_t *end_h, saln_nw_result *res, uint32_t *cig,
-                     Scoring sc) {
-    nw_fill_kernel<G, K><<<grid, dim3(256), 0, s>>>(pairs, first, count, qs, ds, mask, scratch,
-                                                     end_h, res, cig, sc);
+                     int2 *scratch, int32_t *end_h, saln_nw_result *, uint32_t *, Scoring sc,
+                     int codes, uint32_t ld_max) {
+    const size_t lds = (size_t)(256 / G) * (ld_max + 2 * G);
+    const int32_t pen_max = 2 * (sc.match - sc.mismatch);
+    auto go = [&](auto codes_c, auto minpen_c, auto staged_c) {
+        nw_fill_lanes_kernel<G, K, decltype(codes_c)::value, decltype(minpen_c)::value,
+                             decltype(staged_c)::value>
+            <<<grid, dim3(256), decltype(staged_c)::value ? lds : 0, s>>>(
+                pairs, first, count, qs, ds, mask, scratch, end_h, sc, ld_max);
+    };
+    auto by_staged = [&](auto codes_c, auto minpen_c) {
+        if (lds <= 65536) go(codes_c, minpen_c, std::true_type{});
+        else go(codes_c, minpen_c, std::false_type{});
+    };
+    auto by_pen = [&](auto codes_c) {
+        if (pen_max >= 0 && pen_max <= 256) by_staged(codes_c, std::true_type{});
+        else by_staged(codes_c, std::false_type{});
+    };
+    if (codes == kCodesFull) by_pen(std::integral_constant<int, kCodesFull>{});
+    else if (codes == kCodesNone) by_pen(std::integral_constant<int, kCodesNone>{});
+    else by_pen(std::integral_constant<int, kCodesWalk>{});
 }
 
 template <int G, int K, int KS = K>
@@ -2107,9 +2184,9 @@ hipError_t launch_fill(int variant, const NwPairDesc *pairs, uint32_t first, uin
     const bool rebase = kPacked[variant] && !packed_ok(kVariants[variant].W(), ld_max, sc);
     hipError_t e = hipSuccess;
     switch (variant) {
-        case 0: fill_i32<16, 10>(grid, stream, pairs, first, count, qs, ds, mask, scratch, end_h, res, cig, sc); break;
-        case 1: fill_i32<16, 16>(grid, stream, pairs, first, count, qs, ds, mask, scratch, end_h, res, cig, sc); break;
-        case 2: fill_i32<64, 8>(grid, stream, pairs, first, count, qs, ds, mask, scratch, end_h, res, cig, sc); break;
+        case 0: fill_i32<16, 10>(grid, stream, pairs, first, count, qs, ds, mask, scratch, end_h, res, cig, sc, codes, ld_max); break;
+        case 1: fill_i32<16, 16>(grid, stream, pairs, first, count, qs, ds, mask, scratch, end_h, res, cig, sc, codes, ld_max); break;
+        case 2: fill_i32<64, 8>(grid, stream, pairs, first, count, qs, ds, mask, scratch, end_h, res, cig, sc, codes, ld_max); break;
         case 3: return hipErrorInvalidValue;  // stripes: launch_fill_stripes
         case 4: e = fill_pk<8, 19>(grid, stream, pairs, first, count, qs, ds, mask, end_h, res, cig, sc, codes, ld_max, rebase); break;
         case 5: e = fill_pk<16, 16>(grid, stream, pairs, first, count, qs, ds, mask, end_h, res, cig, sc, codes, ld_max, rebase); break;

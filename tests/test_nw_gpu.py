@@ -71,7 +71,8 @@ def test_golden_vectors(saln):
 @pytest.mark.parametrize("lq,ld", [(1, 1), (2, 3), (7, 5), (16, 16), (31, 40), (150, 150),
                                    (160, 150), (161, 20), (200, 180), (256, 100), (257, 64),
                                    (300, 300), (512, 90), (513, 70), (1000, 1000),
-                                   (1024, 30), (1025, 40), (2100, 33), (40, 2000)])
+                                   (1024, 30), (1025, 40), (2100, 33), (40, 2000),
+                                   (100, 2600), (300, 4200)])  # last two: i32 lanes
 def test_random_shapes(saln, oracle, lq, ld):
     rng = np.random.default_rng(lq * 7919 + ld)
     for rep in range(3):
