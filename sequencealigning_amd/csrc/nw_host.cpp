@@ -430,7 +430,11 @@ int saln_nw_execute(saln_nw_plan *p, const uint8_t *d_q, const uint8_t *d_db,
     if (p->n_pairs == 0) return SALN_OK;
     HIP_TRY(hipSetDevice(p->ctx->device));
     hipStream_t s = stream ? (hipStream_t)stream : p->ctx->stream;
-    hipStream_t t = p->ctx->tb_stream;
+    const size_t nsub = p->sub.size() - 1;  // >= 1 (an empty sub-batch if n_fill == 0)
+    // the traceback stream: the second one only when a traceback can overlap a
+    // fill (async plans, sub-batches); otherwise the same stream, so no
+    // cross-stream hand-off sits between the fill and the walk
+    hipStream_t t = (p->async_tb || nsub > 1) ? p->ctx->tb_stream : s;
     const int cur = p->async_tb ? p->buf : 0;
     uint8_t *mask = cur ? p->d_mask2 : p->d_mask;
     int32_t *endh = cur ? p->d_endh2 : p->d_endh;
@@ -446,9 +450,8 @@ int saln_nw_execute(saln_nw_plan *p, const uint8_t *d_q, const uint8_t *d_db,
         ev = p->ev_pool[p->ev_used++].data();
         HIP_TRY(hipEventRecord(ev[0], s));
     }
-    // Sub-batch k: fill on `s`, then its traceback on the context's second
-    // stream; the (latency-bound) traceback overlaps the next fill.
-    const size_t nsub = p->sub.size() - 1;  // >= 1 (an empty sub-batch if n_fill == 0)
+    // Sub-batch k: fill on `s`, then its traceback on `t`; with two streams
+    // the (latency-bound) traceback overlaps the next fill.
     for (size_t k = 0; k < nsub; ++k) {
         const uint32_t lo = p->sub[k], hi = p->sub[k + 1];
         for (int v = 0; v < kNumVariants; ++v) {
@@ -474,7 +477,7 @@ int saln_nw_execute(saln_nw_plan *p, const uint8_t *d_q, const uint8_t *d_db,
         }
         if (ev && k + 1 == nsub) HIP_TRY(hipEventRecord(ev[1], s));
         HIP_TRY(hipEventRecord(p->sync_ev[k], s));
-        HIP_TRY(hipStreamWaitEvent(t, p->sync_ev[k], 0));
+        if (t != s) HIP_TRY(hipStreamWaitEvent(t, p->sync_ev[k], 0));
         if (ev && k == 0) HIP_TRY(hipEventRecord(ev[2], t));
         for (int v = 0; v < kNumVariants; ++v) {
             const uint32_t a = std::max(lo, p->var_first[v]);
@@ -500,7 +503,7 @@ int saln_nw_execute(saln_nw_plan *p, const uint8_t *d_q, const uint8_t *d_db,
     if (p->async_tb) {
         p->buf ^= 1;  // results complete once saln_nw_plan_sync'ed
     } else {
-        HIP_TRY(hipStreamWaitEvent(s, p->tb_done(cur), 0));
+        if (t != s) HIP_TRY(hipStreamWaitEvent(s, p->tb_done(cur), 0));
         p->tb_pending[cur] = false;
     }
     return SALN_OK;
