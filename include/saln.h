@@ -86,7 +86,11 @@ typedef struct saln_context saln_context;
 
 /* Creates a context bound to HIP device `device` (one stream per context;
  * reentrant per context, not shared across threads).  Fails with
- * SALN_E_NO_DEVICE if no gfx950 device is present: there is no CPU path. */
+ * SALN_E_NO_DEVICE if no gfx950 device is present: there is no CPU path.
+ * Device blocks released by plans and host-buffer calls stay cached in the
+ * context (up to 32 GiB, reused by later requests of up to twice the size)
+ * until saln_context_destroy; an allocation that fails drops the cache and
+ * retries once. */
 int saln_context_create(int device, saln_context **out);
 int saln_context_destroy(saln_context *ctx);
 const char *saln_last_error(void);     /* thread-local message for the last error */
@@ -173,6 +177,7 @@ int saln_nw_plan_set_async(saln_nw_plan *plan, int enable);
  * (end_states = printed = cigar_len = 0, flags bit 3 set). */
 int saln_nw_plan_set_score_only(saln_nw_plan *plan, int enable);
 int saln_nw_plan_sync(saln_nw_plan *plan, void *stream, int keep_latest);
+/* Waits for the device, then returns the plan's blocks to its context. */
 int saln_nw_plan_destroy(saln_nw_plan *plan);
 
 /* ------------------------------------ NW: score-only all-vs-all (device, C5)
