@@ -675,23 +675,34 @@ __global__ __launch_bounds__(64 * NWV) void nw_traceback_coop_kernel(
         }
     };
     int ev;
+#ifdef SALN_COOP_PROF
+    uint32_t pf_iter = 0, pf_load = 0;
+    const uint64_t pf_t0 = __builtin_amdgcn_s_memtime();
+    uint64_t pf_tload = 0, pf_temit = 0;
+#endif
     for (;;) {
-        if (st == kStM) {
-            if (i == 0 && j == 0) { ev = kEvOrigin; break; }
-            if (i == 0 || j == 0) { ev = kEvDead; break; }
-        } else if (st == kStI) {
-            if (j == 0) { ev = i >= 1 ? kEvPanic : kEvDead; break; }
-            if (i == 0) { ev = kEvDead; break; }
-        } else {
-            if (i == 0) { ev = j >= 1 ? kEvPanic : kEvDead; break; }
-            if (j == 0) { ev = kEvDead; break; }
+#ifdef SALN_COOP_PROF
+        ++pf_iter;
+#endif
+        if (i == 0 || j == 0) {  // every end of the walk is on row or column 0
+            if (st == kStM) ev = i == 0 && j == 0 ? kEvOrigin : kEvDead;
+            else if (st == kStI) ev = j == 0 && i >= 1 ? kEvPanic : kEvDead;
+            else ev = i == 0 && j >= 1 ? kEvPanic : kEvDead;
+            break;
         }
         // steps l whose reads stay in the window (row / column 0 come from
         // the boundary formulas)
         const int32_t lim_i = r_lo == 1 ? i - 1 : i - 1 - r_lo;
         const int32_t lim_j = c_lo == 1 ? j - 1 : j - 1 - c_lo;
         if (i < r_lo || j < c_lo || (st != kStI && lim_i < 0)) {
+#ifdef SALN_COOP_PROF
+            ++pf_load;
+            const uint64_t pq = __builtin_amdgcn_s_memtime();
+#endif
             load(i, j);  // anchored at row i: lim_i >= 0 afterwards
+#ifdef SALN_COOP_PROF
+            pf_tload += __builtin_amdgcn_s_memtime() - pq;
+#endif
             continue;
         }
         // j == c_lo > 1 and the step reads column j-1: one step, lane 0,
@@ -700,7 +711,14 @@ __global__ __launch_bounds__(64 * NWV) void nw_traceback_coop_kernel(
         uint32_t eq0 = 0;
         if (edge) {  // j == c_lo > 1: this step reads column j-1 of the previous stripe
             if (st == kStM) eq0 = code(i, j) >> 7;  // (i, j) leaves the window now
+#ifdef SALN_COOP_PROF
+            ++pf_load;
+            const uint64_t pq = __builtin_amdgcn_s_memtime();
+#endif
             load(i, j - 1);
+#ifdef SALN_COOP_PROF
+            pf_tload += __builtin_amdgcn_s_memtime() - pq;
+#endif
         }
         int32_t lmax = edge ? 0 : st == kStM ? min(lim_i, lim_j) : st == kStI ? lim_j : lim_i;
         lmax = min(lmax, 63);
@@ -730,22 +748,37 @@ __global__ __launch_bounds__(64 * NWV) void nw_traceback_coop_kernel(
             stop = stop || lane == lmax;
         }
         const uint64_t sb = __builtin_amdgcn_ballot_w64(stop);
+#ifdef SALN_COOP_PROF
+        const uint64_t pe = __builtin_amdgcn_s_memtime();
+#endif
         const int32_t L = __builtin_ctzll(sb);  // last step of this run (lane lmax always stops)
         const uint32_t n = (uint32_t)L + 1;
         if (st == kStM) {
             const uint64_t lm = n >= 64 ? ~0ull : ((1ull << n) - 1);
             const uint64_t e = __builtin_amdgcn_ballot_w64(eq != 0) & lm;
-            uint64_t bnd = (e ^ (e << 1)) & lm & ~1ull;  // lanes whose op differs from the previous
-            uint32_t cur = (e & 1) ? SALN_CIGAR_EQ : SALN_CIGAR_X;
-            int32_t s0 = 0;
-            while (bnd) {
-                const int32_t b = __builtin_ctzll(bnd);
-                push(cur, (uint32_t)(b - s0));
-                cur = cur == SALN_CIGAR_EQ ? SALN_CIGAR_X : SALN_CIGAR_EQ;
-                s0 = b;
-                bnd &= bnd - 1;
+            const uint64_t bnd = (e ^ (e << 1)) & lm & ~1ull;  // steps whose op differs from the previous
+            const uint32_t cur0 = (e & 1) ? SALN_CIGAR_EQ : SALN_CIGAR_X;
+            const uint32_t other = cur0 == SALN_CIGAR_EQ ? SALN_CIGAR_X : SALN_CIGAR_EQ;
+            const uint32_t k = (uint32_t)__builtin_popcountll(bnd);
+            // segment 0 (up to the first boundary) joins or follows the pending run
+            push(cur0, k ? (uint32_t)__builtin_ctzll(bnd) : n);
+            if (k) {
+                // the pending run ends at the first boundary; segments 1..k-1
+                // are written in parallel by their boundary lanes; the last
+                // segment is the new pending run
+                if (lane == 0 && out) out[nops] = (run_len << 4) | run_op;
+                ++nops;
+                if ((bnd >> lane) & 1) {
+                    const uint32_t m = (uint32_t)__builtin_popcountll(bnd & ((1ull << lane) - 1)) + 1;
+                    if (m < k && out) {
+                        const uint32_t nb = (uint32_t)__builtin_ctzll(bnd & ~((2ull << lane) - 1));
+                        out[nops + m - 1] = ((nb - (uint32_t)lane) << 4) | ((m & 1) ? other : cur0);
+                    }
+                }
+                nops += k - 1;
+                run_op = (k & 1) ? other : cur0;
+                run_len = n - (uint32_t)(63 - __builtin_clzll(bnd));
             }
-            push(cur, n - (uint32_t)s0);
             i -= (int32_t)n;
             j -= (int32_t)n;
         } else if (st == kStI) {
@@ -756,6 +789,9 @@ __global__ __launch_bounds__(64 * NWV) void nw_traceback_coop_kernel(
             i -= (int32_t)n;
         }
         st = __builtin_amdgcn_readlane(nxt, L);
+#ifdef SALN_COOP_PROF
+        pf_temit += __builtin_amdgcn_s_memtime() - pe;
+#endif
     }
     if (NWV > 1) {  // release the loader waves
         if (lane == 0) req[0] = -1;
@@ -784,6 +820,15 @@ __global__ __launch_bounds__(64 * NWV) void nw_traceback_coop_kernel(
         r.printed = ev == kEvOrigin ? 1 : 0;
         r.flags = (ev == kEvDead ? 1 : 0) | ((ev == kEvPanic && !(hend & 1)) ? 2 : 0);
         r.reserved = 0;
+#ifdef SALN_COOP_PROF  // iterations, window loads, total / load clocks (>> 10)
+        r.cigar_len = pf_iter;
+        r.score = (int32_t)pf_load;
+        r.status = (int32_t)((__builtin_amdgcn_s_memtime() - pf_t0) >> 10);
+        r.end_states = (uint8_t)min((uint32_t)(pf_temit * 100 / max(1ull, __builtin_amdgcn_s_memtime() - pf_t0)), 255u);
+        r.printed = 0;
+        r.flags = 0;
+        r.reserved = (uint8_t)min((uint32_t)(pf_tload * 100 / max(1ull, __builtin_amdgcn_s_memtime() - pf_t0)), 255u);
+#endif
         results[p.pair_id] = r;
     }
 }
