@@ -354,6 +354,18 @@ def test_context_block_cache_reuse(saln, oracle):
             assert (int(r0["score"][k]), int(r0["end_states"][k])) == (o.score, o.end_states)
 
 
+@pytest.mark.parametrize("lq,ld", [(1, 5000), (5000, 1), (1025, 1), (1, 1025), (2, 3000),
+                                   (600, 1), (513, 2), (1024, 1024), (1023, 3), (3, 4096)])
+def test_degenerate_shapes_all_variants(saln, oracle, lq, ld):
+    """Thin and boundary-sized pairs on every fill path (packed, rebasing,
+    wide, i32 lanes, stripes), with N in the sequences: score, end states,
+    panics, first alignment and the full parent mask equal the oracle's."""
+    rng = np.random.default_rng(lq * 31 + ld)
+    q = bytes(rng.choice(list(b"ACGTN"), lq).astype(np.uint8))
+    d = bytes(rng.choice(list(b"ACGTN"), ld).astype(np.uint8))
+    _compare(saln, oracle, q, d, text=False)
+
+
 @pytest.mark.parametrize("L", [3000])
 def test_long_pair_stripes(saln, oracle, L):
     """A single long mutated pair through the column-stripe fill (12 stripes of
