@@ -38,6 +38,9 @@ namespace saln {
 namespace {
 
 constexpr int kRingMax = 16;
+// An empty range is (kEmptyLo, -kEmptyLo): min / max of ranges and the +-1
+// of the recurrences keep it empty without tests.
+constexpr int32_t kEmptyLo = 1 << 29;
 typedef __attribute__((address_space(3))) uint8_t lds_cu8_raw;
 typedef const lds_cu8_raw lds_cu8;
 typedef const __attribute__((address_space(3))) uint32_t lds_cu32;
@@ -100,8 +103,8 @@ __device__ __forceinline__ int32_t wfa_pair(P q, int32_t lq, P d, int32_t ld, co
     const int32_t kend = ld - lq;
     __builtin_amdgcn_wave_barrier();
     if (lane < 3 * kRingMax) {  // every slot empty
-        rng[2 * lane] = 1;
-        rng[2 * lane + 1] = 0;
+        rng[2 * lane] = kEmptyLo;
+        rng[2 * lane + 1] = -kEmptyLo;
     }
     // s = 0: M[0][0] = 0, extended
     if (lane == 0) {
@@ -125,8 +128,8 @@ __device__ __forceinline__ int32_t wfa_pair(P q, int32_t lq, P d, int32_t ld, co
                        int32_t &slot, int32_t &lo, int32_t &hi) __attribute__((always_inline)) {
             if (ts < 0) {
                 slot = 0;
-                lo = 1;
-                hi = 0;
+                lo = kEmptyLo;
+                hi = -kEmptyLo;
                 return;
             }
             slot = wrap(slot_now - back, ring);  // back < ring
@@ -138,40 +141,20 @@ __device__ __forceinline__ int32_t wfa_pair(P q, int32_t lq, P d, int32_t ld, co
         src(0, t - tx, sM, tx, prm.RM, sx, loMx, hiMx);
         src(1, t - te, sI, te, prm.RI, sie, loI, hiI);
         src(2, t - te, sI, te, prm.RI, sde, loD, hiD);
-        // new ranges
-        int32_t iLo = INT32_MAX, iHi = INT32_MIN, dLo = INT32_MAX, dHi = INT32_MIN;
-        if (loMo <= hiMo) {
-            iLo = min(iLo, loMo + 1);
-            iHi = max(iHi, hiMo + 1);
-            dLo = min(dLo, loMo - 1);
-            dHi = max(dHi, hiMo - 1);
-        }
-        if (loI <= hiI) {
-            iLo = min(iLo, loI + 1);
-            iHi = max(iHi, hiI + 1);
-        }
-        if (loD <= hiD) {
-            dLo = min(dLo, loD - 1);
-            dHi = max(dHi, hiD - 1);
-        }
-        iLo = max(iLo, -lq);
-        iHi = min(iHi, ld);
-        dLo = max(dLo, -lq);
-        dHi = min(dHi, ld);
-        if (iLo > iHi) iLo = 1, iHi = 0;
-        if (dLo > dHi) dLo = 1, dHi = 0;
-        int32_t mLo = INT32_MAX, mHi = INT32_MIN;
-        if (iLo <= iHi) mLo = min(mLo, iLo), mHi = max(mHi, iHi);
-        if (dLo <= dHi) mLo = min(mLo, dLo), mHi = max(mHi, dHi);
-        if (loMx <= hiMx) {
-            mLo = min(mLo, max(loMx, -lq));
-            mHi = max(mHi, min(hiMx, ld));
-        }
+        // new ranges (empty sources are (kEmptyLo, -kEmptyLo) and stay out of
+        // every min / max below; a clamp that empties a range is re-marked)
+        int32_t iLo = max(min(loMo, loI) + 1, -lq), iHi = min(max(hiMo, hiI) + 1, ld);
+        int32_t dLo = max(min(loMo, loD) - 1, -lq), dHi = min(max(hiMo, hiD) - 1, ld);
+        if (iLo > iHi) iLo = kEmptyLo, iHi = -kEmptyLo;
+        if (dLo > dHi) dLo = kEmptyLo, dHi = -kEmptyLo;
+        const int32_t xLo = max(loMx, -lq), xHi = min(hiMx, ld);
+        int32_t mLo = min(min(iLo, dLo), xLo <= xHi ? xLo : kEmptyLo);
+        int32_t mHi = max(max(iHi, dHi), xLo <= xHi ? xHi : -kEmptyLo);
         if (mLo > mHi) {  // nothing at this score
             if (lane == 0) {
-                rng[2 * sM] = 1, rng[2 * sM + 1] = 0;
-                rng[2 * (kRingMax + sI)] = 1, rng[2 * (kRingMax + sI) + 1] = 0;
-                rng[2 * (2 * kRingMax + sI)] = 1, rng[2 * (2 * kRingMax + sI) + 1] = 0;
+                rng[2 * sM] = kEmptyLo, rng[2 * sM + 1] = -kEmptyLo;
+                rng[2 * (kRingMax + sI)] = kEmptyLo, rng[2 * (kRingMax + sI) + 1] = -kEmptyLo;
+                rng[2 * (2 * kRingMax + sI)] = kEmptyLo, rng[2 * (2 * kRingMax + sI) + 1] = -kEmptyLo;
             }
             __builtin_amdgcn_s_waitcnt(0xC07F);
             __builtin_amdgcn_wave_barrier();
@@ -182,12 +165,8 @@ __device__ __forceinline__ int32_t wfa_pair(P q, int32_t lq, P d, int32_t ld, co
         // Predicates are arithmetic (one unsigned compare, or one max3 and a
         // compare) so they cost VALU only, no SALU mask combining.  An empty
         // source gets lo = 2^30, span 0: k - lo never passes.
-        auto span_of = [](int32_t &lo, int32_t hi) {
-            if (lo > hi) {
-                lo = 1 << 30;
-                return 0u;
-            }
-            return (uint32_t)(hi - lo);
+        auto span_of = [](int32_t &lo, int32_t hi) {  // empty: lo = 2^29, span 0
+            return (uint32_t)max(hi - lo, 0);
         };
         const uint32_t spMo = span_of(loMo, hiMo), spMx = span_of(loMx, hiMx);
         const uint32_t spI = span_of(loI, hiI), spD = span_of(loD, hiD);
