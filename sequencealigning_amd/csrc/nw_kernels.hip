@@ -722,31 +722,34 @@ __global__ __launch_bounds__(64 * NWV) void nw_traceback_coop_kernel(
         }
         int32_t lmax = edge ? 0 : st == kStM ? min(lim_i, lim_j) : st == kStI ? lim_j : lim_i;
         lmax = min(lmax, 63);
-        bool stop = true;
-        int32_t nxt = st;
+        // Every lane reads and decides (no divergent branches around the LDS
+        // reads); lanes past lmax read outside the window - LDS returns 0 for
+        // out-of-range addresses and their decisions are masked by `stop`.
+        bool stop;
+        int32_t nxt;
         uint32_t eq = 0;
-        if (lane <= lmax) {
-            if (st == kStM) {
-                const int32_t ni = i - lane - 1, nj = j - lane - 1;
-                eq = edge ? eq0 : code(i - lane, j - lane) >> 7;
-                const uint32_t a = ni == 0 ? argmax_row0(sc, (uint32_t)nj)
-                                 : nj == 0 ? argmax_col0(sc, (uint32_t)ni)
-                                           : code(ni, nj) & 7u;
-                nxt = (a & kArgD) ? kStD : ((a & kArgI) ? kStI : kStM);
-                stop = nxt != kStM || ni == 0 || nj == 0;
-            } else if (st == kStI) {
-                const int32_t cj = j - lane;
-                const uint32_t b = cj == 1 ? ibits_col1(sc, (uint32_t)i) : (code(i, cj - 1) >> 3) & 3u;
-                nxt = (b & 2) ? kStM : kStI;
-                stop = nxt != kStI || cj == 1;
-            } else {
-                const int32_t ci = i - lane;
-                const uint32_t b = ci == 1 ? dbits_row1(sc, (uint32_t)j) : (code(ci - 1, j) >> 5) & 3u;
-                nxt = (b & 2) ? kStM : kStD;
-                stop = nxt != kStD || ci == 1;
-            }
-            stop = stop || lane == lmax;
+        if (st == kStM) {  // wave-uniform
+            const int32_t ni = i - lane - 1, nj = j - lane - 1;
+            const uint32_t ce = code(i - lane, j - lane), cn = code(ni, nj);
+            eq = edge ? eq0 : ce >> 7;
+            const uint32_t ab = ni == 0 ? argmax_row0(sc, (uint32_t)nj) : argmax_col0(sc, (uint32_t)ni);
+            const uint32_t a = (ni == 0 || nj == 0) ? ab : cn & 7u;
+            nxt = (a & kArgD) ? kStD : ((a & kArgI) ? kStI : kStM);
+            stop = nxt != kStM || ni == 0 || nj == 0;
+        } else if (st == kStI) {
+            const int32_t cj = j - lane;
+            const uint32_t cc = code(i, cj - 1);
+            const uint32_t b = cj == 1 ? ibits_col1(sc, (uint32_t)i) : (cc >> 3) & 3u;
+            nxt = (b & 2) ? kStM : kStI;
+            stop = nxt != kStI || cj == 1;
+        } else {
+            const int32_t ci = i - lane;
+            const uint32_t cc = code(ci - 1, j);
+            const uint32_t b = ci == 1 ? dbits_row1(sc, (uint32_t)j) : (cc >> 5) & 3u;
+            nxt = (b & 2) ? kStM : kStD;
+            stop = nxt != kStD || ci == 1;
         }
+        stop = stop || lane >= lmax;
         const uint64_t sb = __builtin_amdgcn_ballot_w64(stop);
 #ifdef SALN_COOP_PROF
         const uint64_t pe = __builtin_amdgcn_s_memtime();
