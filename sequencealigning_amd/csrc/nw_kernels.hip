@@ -662,17 +662,14 @@ __global__ __launch_bounds__(64 * NWV) void nw_traceback_coop_kernel(
     int32_t st = (am_end & kArgD) ? kStD : ((am_end & kArgM) ? kStM : kStI);
     uint32_t *out = cigar ? cigar + p.cigar_off : nullptr;
     uint32_t nops = 0, run_op = 0, run_len = 0;
+    // The pending run is stored at out[nops] unconditionally (every lane, one
+    // address): when it merges or is empty the slot is simply rewritten later.
     auto push = [&](uint32_t op, uint32_t len) __attribute__((always_inline)) {
-        if (run_len && run_op == op) {
-            run_len += len;
-        } else {
-            if (run_len) {
-                if (lane == 0 && out) out[nops] = (run_len << 4) | run_op;
-                ++nops;
-            }
-            run_op = op;
-            run_len = len;
-        }
+        const bool merge = run_op == op;
+        if (out) out[nops] = (run_len << 4) | run_op;
+        nops += (!merge && run_len) ? 1u : 0u;
+        run_len = merge ? run_len + len : len;
+        run_op = op;
     };
     int ev;
 #ifdef SALN_COOP_PROF
@@ -769,7 +766,7 @@ __global__ __launch_bounds__(64 * NWV) void nw_traceback_coop_kernel(
                 // the pending run ends at the first boundary; segments 1..k-1
                 // are written in parallel by their boundary lanes; the last
                 // segment is the new pending run
-                if (lane == 0 && out) out[nops] = (run_len << 4) | run_op;
+                if (out) out[nops] = (run_len << 4) | run_op;
                 ++nops;
                 if ((bnd >> lane) & 1) {
                     const uint32_t m = (uint32_t)__builtin_popcountll(bnd & ((1ull << lane) - 1)) + 1;
