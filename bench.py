@@ -234,7 +234,7 @@ def main() -> None:
                          if not args.score_only else None},
             "status_counts": {"ok": int(statuses[0]), "ref_panic_boundary": int(statuses[2])},
         }
-        if not args.no_cpu_baseline:
+        if not args.no_cpu_baseline and world == 1:  # the CPU leg: rank 0 at N = 1 only
             out["cpu_baseline"] = cpu_baseline()
         print(json.dumps(out), flush=True)
     plan.close()
