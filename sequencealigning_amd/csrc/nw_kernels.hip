@@ -1319,16 +1319,25 @@ __device__ __forceinline__ uint32_t stripe_code_word(const uint32_t (&s)[8][4]) 
     return merge_walk<true>(w);
 }
 
-template <int K, int kCodes, bool kMinPen>
-__global__ __launch_bounds__(64) void nw_fill_stripe_kernel(
+// kSplit (parent codes, a few stripes): the stripe's wave keeps the
+// recurrence and hands each step's M / D of its columns, the first column's
+// I and the row's char to a second wave through an 8-step LDS ring; the
+// second wave rebuilds H, the gap candidates and the code words and stores
+// them.  The two waves meet at one barrier per four-step group.  It pays
+// only while the pipeline is short (C1: fill 0.42 -> 0.38 ms); one long
+// pair or a batch runs slower with it.
+template <int K, int kCodes, bool kMinPen, bool kSplit = false>
+__global__ __launch_bounds__(128) void nw_fill_stripe_kernel(
     const NwPairDesc *__restrict__ pairs, const uint2 *__restrict__ work,
     const uint8_t *__restrict__ qs, const uint8_t *__restrict__ ds, uint8_t *__restrict__ mask,
     int2 *__restrict__ scratch, uint32_t *__restrict__ prog, uint32_t *__restrict__ err,
     int32_t *__restrict__ end_h, Scoring sc) {
     static_assert(K == 4, "one code dword per lane and row");
+    static_assert(!kSplit || kCodes != kCodesNone, "the coder wave writes codes");
     constexpr int G = 64;
     constexpr Geom geo{G, K};
-    const int lane = threadIdx.x;
+    const int lane = threadIdx.x & 63;
+    __shared__ uint4 pay[kSplit ? 8 * 64 * 3 : 1];  // [step % 8][lane][M, D, (I0, char)]
     const uint2 wk = work[blockIdx.x];
     const NwPairDesc p = pairs[wk.x];
     const uint32_t c = wk.y;
@@ -1394,6 +1403,54 @@ __global__ __launch_bounds__(64) void nw_fill_stripe_kernel(
     // the query chars above arrive here: otherwise the wait for them lands
     // inside the loop, where it would also wait for every mask store
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+    if constexpr (kSplit) {
+        if (threadIdx.x >= 64) {  // the coder wave: group g after the stripe wave's barrier g
+            const int NG = (T + 3) / 4;
+            for (int g = 0; g < NG; ++g) {
+                __syncthreads();
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int tt = 4 * g + u;
+                    const int r = tt - lane + 1;
+                    if (tt < T && r >= 1 && r <= (int)ld) {
+                        const uint4 *sl = pay + ((tt & 7) * 64 + lane) * 3;
+                        const uint4 pm = sl[0], pd = sl[1], px = sl[2];
+                        const int32_t Mv[4] = {(int32_t)pm.x, (int32_t)pm.y, (int32_t)pm.z, (int32_t)pm.w};
+                        const int32_t Dv[4] = {(int32_t)pd.x, (int32_t)pd.y, (int32_t)pd.z, (int32_t)pd.w};
+                        int32_t I = (int32_t)px.x;
+                        const uint32_t dc = px.y;
+                        uint32_t sg[8][4];
+#pragma unroll
+                        for (int k = 0; k < K; ++k) {
+                            const int32_t M = Mv[k], D = Dv[k];
+                            const int32_t H = max(M, max(I, D));
+                            const int32_t tO = M + kOpen;
+                            const int32_t Hc = H & ~1;
+                            const int32_t tOr = tO | 1;
+                            sg[0][k] = (uint32_t)(M - Hc);
+                            sg[1][k] = (uint32_t)(I - Hc);
+                            sg[2][k] = (uint32_t)(D - Hc);
+                            sg[4][k] = (uint32_t)(tOr - I);
+                            sg[6][k] = (uint32_t)(tOr - D);
+                            sg[7][k] = (qc[k] ^ dc) - 1u;  // sign <=> q == d
+                            if constexpr (kCodes == kCodesFull) {
+                                const int32_t tOc = tO & ~1;
+                                sg[3][k] = (uint32_t)(I - tOc);
+                                sg[5][k] = (uint32_t)(D - tOc);
+                            } else {
+                                sg[3][k] = sg[5][k] = 0u;
+                            }
+                            I = max(tO, I);
+                        }
+                        *reinterpret_cast<uint32_t *>(mseg + (uint64_t)tt * p.mask_rs) =
+                            stripe_code_word<kCodes>(sg);
+                    }
+                }
+            }
+            __syncthreads();  // the stripe wave's last barrier
+            return;
+        }
+    }
     // Previous-row H: step t reads Hin (row r-1) and writes Hout (row r); a
     // two-step unroll swaps the arrays instead of rotating registers.
     int32_t HpB[K];
@@ -1445,6 +1502,7 @@ __global__ __launch_bounds__(64) void nw_fill_stripe_kernel(
         if (r >= 1 && r <= (int)ld) {
             int32_t F = inF;
             uint32_t sg[8][4];
+            int32_t Mk[K], Dk[K];  // kSplit: the coder wave's inputs
             int32_t diag = hd;  // H~(r-1, c-1) of column k
 #pragma unroll
             for (int k = 0; k < K; ++k) {
@@ -1456,7 +1514,10 @@ __global__ __launch_bounds__(64) void nw_fill_stripe_kernel(
                 const int32_t I = F, D = Dn[k];
                 const int32_t H = max(M, max(I, D));
                 const int32_t tO = M + kOpen;
-                if constexpr (kCodes != kCodesNone) {
+                if constexpr (kSplit) {
+                    Mk[k] = M;
+                    Dk[k] = D;
+                } else if constexpr (kCodes != kCodesNone) {
                     const int32_t Hc = H & ~1;
                     const int32_t tOr = tO | 1;
                     sg[0][k] = (uint32_t)(M - Hc);
@@ -1484,8 +1545,14 @@ __global__ __launch_bounds__(64) void nw_fill_stripe_kernel(
             if constexpr (kPos == 1) gH1 = pubH, gF1 = pubF;
             if constexpr (kPos == 2) gH2 = pubH, gF2 = pubF;
             if constexpr (kPos == 3) gH3 = pubH, gF3 = pubF;
-            if constexpr (kCodes != kCodesNone)
+            if constexpr (kSplit) {
+                uint4 *sl = pay + ((t & 7) * 64 + lane) * 3;
+                sl[0] = make_uint4((uint32_t)Mk[0], (uint32_t)Mk[1], (uint32_t)Mk[2], (uint32_t)Mk[3]);
+                sl[1] = make_uint4((uint32_t)Dk[0], (uint32_t)Dk[1], (uint32_t)Dk[2], (uint32_t)Dk[3]);
+                sl[2] = make_uint4((uint32_t)inF, dch, 0u, 0u);
+            } else if constexpr (kCodes != kCodesNone) {
                 *reinterpret_cast<uint32_t *>(mseg) = stripe_code_word<kCodes>(sg);
+            }
         } else {
 #pragma unroll
             for (int k = 0; k < K; ++k) Hout[k] = Hin[k];  // lane idle: keep row r-1
@@ -1532,6 +1599,7 @@ __global__ __launch_bounds__(64) void nw_fill_stripe_kernel(
         step(t + 2, Hp, HpB, (w >> 16) & 0xFFu, p2);
         step(t + 3, HpB, Hp, w >> 24, p3);
         publish(t, 4);
+        if constexpr (kSplit) __syncthreads();  // group ready for the coder wave
     }
     const int ntail = T - t;
     if (ntail > 0) {
@@ -1540,7 +1608,9 @@ __global__ __launch_bounds__(64) void nw_fill_stripe_kernel(
         if (ntail > 1) step(t + 1, HpB, Hp, (w >> 8) & 0xFFu, p1);
         if (ntail > 2) step(t + 2, Hp, HpB, (w >> 16) & 0xFFu, p2);
         publish(t, ntail);
+        if constexpr (kSplit) __syncthreads();
     }
+    if constexpr (kSplit) __syncthreads();  // the coder's last group is done
     if (end_lane) {  // every lane ends on row ld, in the array the last step wrote
         int32_t e = 0;
 #pragma unroll
@@ -2311,12 +2381,27 @@ hipError_t launch_fill_stripes(const NwPairDesc *pairs, const uint2 *work, uint3
     const dim3 grid(n_work), block(64);
     const int32_t pen_max = 2 * (sc.match - sc.mismatch);
     const bool pk = stripe_packed(sc);
+    // a coder wave per stripe while the pipeline is short (a few stripes in
+    // the launch: the C1 latency case)
+    static const int split_env = [] {  // experiment switch: SALN_STRIPE_SPLIT=0 / 1
+        const char *e = std::getenv("SALN_STRIPE_SPLIT");
+        return e ? (e[0] == '1' ? 1 : 0) : -1;
+    }();
+    const bool split = split_env >= 0 ? split_env == 1 : n_work <= 16;
     auto go = [&](auto codes_c, auto minpen_c) {
+        constexpr int kC = decltype(codes_c)::value;
         if (pk)
-            nw_fill_stripe_pk_kernel<decltype(codes_c)::value>
+            nw_fill_stripe_pk_kernel<kC>
                 <<<grid, block, 0, stream>>>(pairs, work, qs, ds, mask, scratch, prog, err, end_h, sc);
-        else
-            nw_fill_stripe_kernel<4, decltype(codes_c)::value, decltype(minpen_c)::value>
+        else if constexpr (kC != kCodesNone) {
+            if (split)
+                nw_fill_stripe_kernel<4, kC, decltype(minpen_c)::value, true>
+                    <<<grid, dim3(128), 0, stream>>>(pairs, work, qs, ds, mask, scratch, prog, err, end_h, sc);
+            else
+                nw_fill_stripe_kernel<4, kC, decltype(minpen_c)::value>
+                    <<<grid, block, 0, stream>>>(pairs, work, qs, ds, mask, scratch, prog, err, end_h, sc);
+        } else
+            nw_fill_stripe_kernel<4, kC, decltype(minpen_c)::value>
                 <<<grid, block, 0, stream>>>(pairs, work, qs, ds, mask, scratch, prog, err, end_h, sc);
     };
     auto by_codes = [&](auto minpen_c) {
