@@ -464,6 +464,14 @@ int saln_nw_execute(saln_nw_plan *p, const uint8_t *d_q, const uint8_t *d_db,
                     const uint32_t g1 = p->h_pairs[b - 1].reserved +
                                         variant_geom(v).n_chunks(p->h_pairs[b - 1].len_q);
                     HIP_TRY(hipMemsetAsync(p->d_prog + g0, 0, (g1 - g0) * sizeof(uint32_t), s));
+                    // boundary columns preset to kColEmpty: a row is published
+                    // once its value replaces the preset (nw_fill_stripe_kernel)
+                    const NwPairDesc &la = p->h_pairs[b - 1];
+                    const uint64_t c0 = p->h_pairs[a].scratch_off;
+                    const uint64_t c1 = la.scratch_off + (uint64_t)variant_geom(v).n_chunks(la.len_q) *
+                                                             (la.len_db + 2);
+                    HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)(p->d_scratch + c0), (int)0x80000000u,
+                                              2 * (c1 - c0), s));
                     HIP_TRY(launch_fill_stripes(p->d_pairs, p->d_work + w0, w1 - w0, d_q, d_db,
                                                 mask, p->d_scratch, p->d_prog, p->d_err, endh,
                                                 p->sc,

@@ -843,15 +843,20 @@ struct MaskWords {
 // One wave per column stripe of G*K = 64*K columns; all stripes of a pair run
 // concurrently as a pipeline down the rows (the "anti-diagonal tiling across
 // CUs" of configs[3]).  Stripe c's last lane publishes, per row, the H and
-// I-candidate leaving its last column (scratch column c, agent-coherent
-// stores) and, every kPub rows once those stores are complete, its progress
-// counter; stripe c+1 polls the counter and then reads 32-row blocks of that
-// column with agent-coherent loads.  (A release/acquire pair would write
-// back and invalidate the whole L2 at every publication.)  Work items
+// I-candidate leaving its last column as one 64-bit agent-coherent store into
+// scratch column c, which the host preset to kColEmpty: each row is its own
+// publication, so the producer never waits for its stores (a progress counter
+// behind a vmcnt(0) cost ~1 us per 32 rows on the critical path, 11 % of
+// configs[3]).  Stripe c+1 polls 32-row blocks of that column with
+// agent-coherent loads until no lane sees the preset.  (A release/acquire
+// pair would write back and invalidate the whole L2 at every publication.)
+// The opt-in packed stripe kernel keeps the counter (d_prog).  Work items
 // are ordered pair-major, chunk-ascending, so a stripe's predecessor always
 // has a lower workgroup id and has been dispatched before it (no deadlock);
 // a bounded spin turns a lost dependency into an error flag instead of a hang.
 constexpr uint32_t kPub = 32;
+// the boundary column's preset (H word): no fill value comes near INT32_MIN
+constexpr uint32_t kColEmpty = 0x80000000u;
 constexpr uint32_t kSpinCap = 1u << 24;
 
 // ------------------------------------------------------- packed-i16 fill
@@ -1347,8 +1352,6 @@ __global__ __launch_bounds__(128) void nw_fill_stripe_kernel(
     const uint32_t nch = geo.n_chunks(lq);
     const int2 *__restrict__ scr_in = c > 0 ? scratch + p.scratch_off + (uint64_t)(c - 1) * (ld + 2) : nullptr;
     int2 *__restrict__ scr_out = c + 1 < nch ? scratch + p.scratch_off + (uint64_t)c * (ld + 2) : nullptr;
-    uint32_t *prog_in = c > 0 ? prog + p.reserved + c - 1 : nullptr;
-    uint32_t *prog_out = prog + p.reserved + c;
     const int32_t beta = -2 * sc.gap_extend;
     const int32_t alpha = -2 * sc.match - beta;
     const int32_t pen_max = 2 * (sc.match - sc.mismatch);
@@ -1393,7 +1396,6 @@ __global__ __launch_bounds__(128) void nw_fill_stripe_kernel(
     };
     uint32_t dch = 0;
     int32_t blkH = 0, blkF = 0;  // lanes 0..31: the left column of the current 32-row block
-    uint32_t avail = 0;          // rows of the left column known to be published
     bool failed = false;
     // lane l's row t-l+1 at step t: mask_off + c*cs + l*bs + (t-l)*rs; in the
     // skewed stripe layout (nw_common.hpp) step t's dwords are line t
@@ -1471,22 +1473,22 @@ __global__ __launch_bounds__(128) void nw_fill_stripe_kernel(
             bH = hs_col0(sc, rr) + alpha * (int32_t)rr;
         } else {
             if (kGroupStart && (rr - 1) % kPub == 0 && rr <= ld) {  // new 32-row block of the left column
-                const uint32_t need = min(rr - 1 + kPub, ld);
-                uint32_t spins = 0;
-                while (avail < need && !failed) {
-                    avail = __hip_atomic_load(prog_in, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    avail = __builtin_amdgcn_readfirstlane(avail);
-                    if (avail < need) {
-                        __builtin_amdgcn_s_sleep(2);
-                        if (++spins > kSpinCap) failed = true;
-                    }
-                }
                 const uint32_t row = rr + (uint32_t)lane;
-                if (lane < (int)kPub && row <= ld) {
-                    const uint64_t v = __hip_atomic_load((const uint64_t *)(scr_in + row),
-                                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    blkH = (int32_t)(uint32_t)v;
-                    blkF = (int32_t)(uint32_t)(v >> 32);
+                // every row is its own publication: the column was preset to
+                // kColEmpty, so a lane's value is ready once it differs
+                uint32_t spins = 0;
+                for (;;) {
+                    bool ok = true;
+                    if (lane < (int)kPub && row <= ld) {
+                        const uint64_t v = __hip_atomic_load((const uint64_t *)(scr_in + row),
+                                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        blkH = (int32_t)(uint32_t)v;
+                        blkF = (int32_t)(uint32_t)(v >> 32);
+                        ok = (uint32_t)blkH != kColEmpty;
+                    }
+                    if (__builtin_amdgcn_ballot_w64(!ok) == 0 || failed) break;
+                    __builtin_amdgcn_s_sleep(2);
+                    if (++spins > kSpinCap) failed = true;
                 }
                 // wait here, on the block step only: otherwise the compiler
                 // puts a vmcnt(0) (every outstanding mask store) on the join
@@ -1560,9 +1562,8 @@ __global__ __launch_bounds__(128) void nw_fill_stripe_kernel(
         mseg += p.mask_rs;
     };
     // The last lane's rows of steps t0 .. t0+n-1 (rows t0-62 ..) to the
-    // boundary column, with agent-coherent (write-through) stores: the
-    // progress publication needs only these complete, not an L2 write-back.
-    // Progress goes out when the rows reach a 32-row block end or the db end.
+    // boundary column, with agent-coherent (write-through) stores; a stored
+    // row replaces the preset and is thereby published.
     auto publish = [&](int t0, int n) __attribute__((always_inline)) {
         if (lane == G - 1 && scr_out) {
             const int lo = max(t0 - (G - 2), 1), hi = min(t0 + n - 1 - (G - 2), (int)ld);
@@ -1578,11 +1579,6 @@ __global__ __launch_bounds__(128) void nw_fill_stripe_kernel(
                 put(1, gH1, gF1);
                 put(2, gH2, gF2);
                 put(3, gH3, gF3);
-                if (hi / (int)kPub != (lo - 1) / (int)kPub || hi == (int)ld) {
-                    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): column stores done
-                    __hip_atomic_store(prog_out, (uint32_t)hi, __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_AGENT);
-                }
             }
         }
     };
