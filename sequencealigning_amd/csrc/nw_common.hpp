@@ -23,6 +23,8 @@ namespace saln {
 
 constexpr int32_t kSentinel = -32768;  // i16::MIN as i32, needleman_wunsch_affine.rs:174
 constexpr int kNumVariants = 9;        // fill kernel variants (nw_kernels.hip)
+// plans with at least this many column-stripe waves use the packed stripe fill
+constexpr uint64_t kStripePkMinWaves = 1024;
 
 struct Scoring {
     int32_t match, mismatch, gap_open, gap_extend;

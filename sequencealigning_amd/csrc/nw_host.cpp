@@ -49,6 +49,7 @@ struct saln_nw_plan {
     uint8_t *d_mask2 = nullptr;  // second workspace for the async (2-deep) pipeline
     int32_t *d_endh2 = nullptr;
     bool async_tb = false;
+    bool stripe_pk = false;  // column stripes use the packed fill and layout
     bool full_codes = false;  // walk codes (default) or every parent set
     bool score_only = false;  // no parent codes / traceback (saln_nw_plan_set_score_only)
     int buf = 0;                           // workspace of the next execute (async mode)
@@ -254,6 +255,13 @@ int saln_nw_plan_create(saln_context *ctx, const uint64_t *q_off, uint64_t n_q,
         }
         p->h_pairs[r] = d;
     }
+    {
+        uint64_t waves = 0;  // stripe waves of the plan
+        for (uint32_t r = 0; r < p->var_count[kStripeVariant]; ++r)
+            waves += variant_geom(kStripeVariant)
+                         .n_chunks(p->h_pairs[p->var_first[kStripeVariant] + r].len_q);
+        p->stripe_pk = waves > 0 && stripe_packed(p->sc, waves);
+    }
     // Mask packs: up to 64 consecutive pairs of a variant (one traceback
     // wave) with interleaved segments (nw_common.hpp Geom), unless padding
     // them to the pack's longest db / widest query would cost over 25 % more
@@ -275,7 +283,7 @@ int saln_nw_plan_create(saln_context *ctx, const uint64_t *q_off, uint64_t n_q,
             if (v == kStripeVariant) {
                 // skewed, one region per stripe (nw_common.hpp): every fill
                 // step of a stripe wave writes one whole 256-byte line
-                const bool pk = stripe_packed(p->sc);
+                const bool pk = p->stripe_pk;
                 for (uint32_t s = 0; s < np; ++s) {
                     NwPairDesc &d = p->h_pairs[a + s];
                     d.mask_off = moff;
@@ -460,10 +468,6 @@ int saln_nw_execute(saln_nw_plan *p, const uint8_t *d_q, const uint8_t *d_db,
             if (a < b && v == kStripeVariant) {
                 const uint32_t w0 = p->work_first[a], w1 = p->work_first[b];
                 if (w1 > w0) {
-                    const uint32_t g0 = p->h_pairs[a].reserved;
-                    const uint32_t g1 = p->h_pairs[b - 1].reserved +
-                                        variant_geom(v).n_chunks(p->h_pairs[b - 1].len_q);
-                    HIP_TRY(hipMemsetAsync(p->d_prog + g0, 0, (g1 - g0) * sizeof(uint32_t), s));
                     // boundary columns preset to kColEmpty: a row is published
                     // once its value replaces the preset (nw_fill_stripe_kernel)
                     const NwPairDesc &la = p->h_pairs[b - 1];
@@ -475,7 +479,8 @@ int saln_nw_execute(saln_nw_plan *p, const uint8_t *d_q, const uint8_t *d_db,
                     HIP_TRY(launch_fill_stripes(p->d_pairs, p->d_work + w0, w1 - w0, d_q, d_db,
                                                 mask, p->d_scratch, p->d_prog, p->d_err, endh,
                                                 p->sc,
-                                                p->score_only ? 2 : p->full_codes ? 1 : 0, s));
+                                                p->score_only ? 2 : p->full_codes ? 1 : 0,
+                                                p->stripe_pk, s));
                 }
             } else if (a < b)
                 HIP_TRY(launch_fill(v, p->d_pairs, a, b - a, d_q, d_db, mask, p->d_scratch, endh,
@@ -494,7 +499,7 @@ int saln_nw_execute(saln_nw_plan *p, const uint8_t *d_q, const uint8_t *d_db,
                 HIP_TRY(launch_score_results(p->d_pairs, a, b - a, endh, d_results, p->sc, t));
             else if (a < b)
                 HIP_TRY(launch_traceback(v, p->d_pairs, a, b - a, d_q, d_db, mask, endh, p->d_ops,
-                                         d_results, d_cigar, p->sc, t));
+                                         d_results, d_cigar, p->sc, p->stripe_pk, t));
         }
     }
     // pairs with an empty side (boundary-only walk) ride on the traceback stream
@@ -503,7 +508,8 @@ int saln_nw_execute(saln_nw_plan *p, const uint8_t *d_q, const uint8_t *d_db,
                                      endh, d_results, p->sc, t));
     else if (p->n_pairs > p->n_fill)
         HIP_TRY(launch_traceback(-1, p->d_pairs, p->n_fill, (uint32_t)(p->n_pairs - p->n_fill),
-                                 d_q, d_db, mask, endh, p->d_ops, d_results, d_cigar, p->sc, t));
+                                 d_q, d_db, mask, endh, p->d_ops, d_results, d_cigar, p->sc,
+                                 p->stripe_pk, t));
     if (ev) HIP_TRY(hipEventRecord(ev[3], t));
     HIP_TRY(hipEventRecord(p->tb_done(cur), t));
     p->tb_pending[cur] = true;

@@ -69,13 +69,14 @@ hipError_t launch_fill_stripes(const NwPairDesc *pairs, const uint2 *work, uint3
                                const uint8_t *qs, const uint8_t *ds, uint8_t *mask,
                                int2 *scratch, uint32_t *prog, uint32_t *err, int32_t *end_h,
                                Scoring sc, int codes /* 0 walk, 1 full, 2 none */,
-                               hipStream_t stream);
+                               bool pk /* the packed stripe layout */, hipStream_t stream);
 hipError_t launch_cigar_compact(const saln_nw_result *res, const uint64_t *src_off,
                                 const uint64_t *dst_off, const uint32_t *src, uint32_t *dst,
                                 uint64_t n, hipStream_t stream);
 constexpr int kStripeVariant = 3;
-// column stripes run the packed (int16 halves) fill for this scoring
-bool stripe_packed(const Scoring &sc);
+// column stripes run the packed (int16 halves) fill for this scoring and
+// this many stripe waves in the plan (decided once per plan: it sets the layout)
+bool stripe_packed(const Scoring &sc, uint64_t n_waves);
 constexpr int kWidePackedVariant = 8;        // packed, 64-lane groups, up to 1,024 columns
 constexpr uint64_t kWidePackedMinPairs = 1536;  // fewer such pairs: column stripes (measured crossover 1,024-2,048)
 hipError_t launch_score_results(const NwPairDesc *pairs, uint32_t first, uint32_t n,
@@ -85,7 +86,7 @@ hipError_t launch_traceback(int variant, const NwPairDesc *pairs, uint32_t first
                             const uint8_t *qs,
                             const uint8_t *ds, const uint8_t *mask, const int32_t *end_h,
                             uint32_t *ops, saln_nw_result *results, uint32_t *cigar, Scoring sc,
-                            hipStream_t stream);
+                            bool stripe_pk, hipStream_t stream);
 // score-only all-vs-all (nw_avsa.cpp)
 hipError_t launch_avsa(int variant, const uint64_t *q_off, const uint64_t *d_off,
                        const uint32_t *q_ids, uint32_t nq, const uint32_t *d_ids,

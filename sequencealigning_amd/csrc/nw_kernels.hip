@@ -26,7 +26,7 @@
 #include "saln.h"
 
 namespace saln {
-bool stripe_packed(const Scoring &sc);
+bool stripe_packed(const Scoring &sc, uint64_t n_waves);
 }
 
 #ifndef SALN_PINGPONG
@@ -850,7 +850,7 @@ struct MaskWords {
 // configs[3]).  Stripe c+1 polls 32-row blocks of that column with
 // agent-coherent loads until no lane sees the preset.  (A release/acquire
 // pair would write back and invalidate the whole L2 at every publication.)
-// The opt-in packed stripe kernel keeps the counter (d_prog).  Work items
+// Work items
 // are ordered pair-major, chunk-ascending, so a stripe's predecessor always
 // has a lower workgroup id and has been dispatched before it (no deadlock);
 // a bounded spin turns a lost dependency into an error flag instead of a hang.
@@ -1821,8 +1821,6 @@ __global__ __launch_bounds__(64) void nw_fill_stripe_pk_kernel(
     const uint32_t nch = (lq + W - 1) / W;
     const int2 *__restrict__ scr_in = c > 0 ? scratch + p.scratch_off + (uint64_t)(c - 1) * (ld + 2) : nullptr;
     int2 *__restrict__ scr_out = c + 1 < nch ? scratch + p.scratch_off + (uint64_t)c * (ld + 2) : nullptr;
-    uint32_t *prog_in = c > 0 ? prog + p.reserved + c - 1 : nullptr;
-    uint32_t *prog_out = prog + p.reserved + c;
     const int32_t beta = -2 * sc.gap_extend;
     const int32_t alpha = -2 * sc.match - beta;
     const uint32_t kPen = cst2(2 * (sc.match - sc.mismatch));  // 2 <= pen <= 32
@@ -1863,7 +1861,6 @@ __global__ __launch_bounds__(64) void nw_fill_stripe_pk_kernel(
         return w;
     };
     int32_t blkH = 0, blkF = 0;
-    uint32_t avail = 0;
     bool failed = false;
     uint8_t *mseg = mask + p.mask_off + (uint64_t)c * p.mask_cs + (uint32_t)lane * 4u;
     const int T = (int)ld + 2 * G - 1;
@@ -1889,24 +1886,23 @@ __global__ __launch_bounds__(64) void nw_fill_stripe_pk_kernel(
                 bH = hs_col0(sc, rr) + alpha * (int32_t)rr;
             } else {
                 if (kPos == 0 && (rr - 1) % kPub == 0) {  // new 32-row block of the left column
-                    const uint32_t need = min(rr - 1 + kPub, ld);
-                    uint32_t spins = 0;
-                    while (avail < need && !failed) {
-                        avail = __hip_atomic_load(prog_in, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        avail = __builtin_amdgcn_readfirstlane(avail);
-                        if (avail < need) {
-                            __builtin_amdgcn_s_sleep(2);
-                            if (++spins > kSpinCap) failed = true;
-                        }
-                    }
+                    // rows are published by replacing the kColEmpty preset
+                    // (nw_fill_stripe_kernel)
                     const uint32_t row = rr + (uint32_t)lane;
-                    if (lane < (int)kPub && row <= ld) {
-                        const uint64_t v = __hip_atomic_load((const uint64_t *)(scr_in + row),
-                                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        blkH = (int32_t)(uint32_t)v;
-                        blkF = (int32_t)(uint32_t)(v >> 32);
+                    uint32_t spins = 0;
+                    for (;;) {
+                        bool ok = true;
+                        if (lane < (int)kPub && row <= ld) {
+                            const uint64_t v = __hip_atomic_load((const uint64_t *)(scr_in + row),
+                                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                            blkH = (int32_t)(uint32_t)v;
+                            blkF = (int32_t)(uint32_t)(v >> 32);
+                            ok = (uint32_t)blkH != kColEmpty;
+                        }
+                        if (__builtin_amdgcn_ballot_w64(!ok) == 0 || failed) break;
+                        __builtin_amdgcn_s_sleep(2);
+                        if (++spins > kSpinCap) failed = true;
                     }
-                    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0), on the block step only
                 }
                 const uint32_t sl = (rr - 1) % kPub;
                 bH = __builtin_amdgcn_readlane(blkH, sl);
@@ -2020,11 +2016,6 @@ __global__ __launch_bounds__(64) void nw_fill_stripe_pk_kernel(
                 put(1, gH1, gF1);
                 put(2, gH2, gF2);
                 put(3, gH3, gF3);
-                if (hi / (int)kPub != (lo - 1) / (int)kPub || hi == (int)ld) {
-                    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): column stores done
-                    __hip_atomic_store(prog_out, (uint32_t)hi, __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_AGENT);
-                }
             }
         }
     };
@@ -2327,7 +2318,7 @@ static void tb_lds(dim3 grid, hipStream_t s, const NwPairDesc *pairs, uint32_t f
 hipError_t launch_traceback(int variant, const NwPairDesc *pairs, uint32_t first, uint32_t n,
                             const uint8_t *qs, const uint8_t *ds, const uint8_t *mask,
                             const int32_t *end_h, uint32_t *ops, saln_nw_result *results,
-                            uint32_t *cigar, Scoring sc, hipStream_t stream) {
+                            uint32_t *cigar, Scoring sc, bool stripe_pk, hipStream_t stream) {
     if (n == 0) return hipSuccess;
     const dim3 grid((n + 255) / 256);
     switch (variant) {
@@ -2351,7 +2342,7 @@ hipError_t launch_traceback(int variant, const NwPairDesc *pairs, uint32_t first
                        stream>>>(pairs, first, mask, end_h, results, cigar, sc, rows);
                 return hipSuccess;
             };
-            const hipError_t e = stripe_packed(sc) ? go(std::true_type{}) : go(std::false_type{});
+            const hipError_t e = stripe_pk ? go(std::true_type{}) : go(std::false_type{});
             if (e != hipSuccess) return e;
             break;
         }
@@ -2372,11 +2363,10 @@ hipError_t launch_traceback(int variant, const NwPairDesc *pairs, uint32_t first
 hipError_t launch_fill_stripes(const NwPairDesc *pairs, const uint2 *work, uint32_t n_work,
                                const uint8_t *qs, const uint8_t *ds, uint8_t *mask,
                                int2 *scratch, uint32_t *prog, uint32_t *err, int32_t *end_h,
-                               Scoring sc, int codes, hipStream_t stream) {
+                               Scoring sc, int codes, bool pk, hipStream_t stream) {
     if (!n_work) return hipSuccess;
     const dim3 grid(n_work), block(64);
     const int32_t pen_max = 2 * (sc.match - sc.mismatch);
-    const bool pk = stripe_packed(sc);
     // a coder wave per stripe while the pipeline is short (a few stripes in
     // the launch: the C1 latency case)
     static const int split_env = [] {  // experiment switch: SALN_STRIPE_SPLIT=0 / 1
@@ -2438,13 +2428,15 @@ Geom variant_geom(int v) { return kVariants[v]; }
 // The packed stripe fill holds a row relative to the stripe's left input:
 // within 256 columns of it values span 256 * (2|m| + 4|ge|) plus the gap
 // and penalty offsets of M / I / D (see nw_fill_stripe_pk_kernel).
-// Opt-in (SALN_STRIPE_PK=1, read per plan): the 128-virtual-lane chain
-// doubles a stripe's skew, so one long pair (C4) fills slower (49.7 vs
-// 44.9 ms) although the step is cheaper; batches of 2-5 kbp pairs fill
-// 8-16 % faster but walk slower (+63 lines per window).
-bool stripe_packed(const Scoring &sc) {
+// The packed stripe fill: its 128-virtual-lane chain doubles a stripe's skew,
+// so one long pair (C4, 391 waves alone on their SIMDs) fills slower (45.4 vs
+// 40.1 ms) although the step is cheaper; once the stripe waves fill the chip
+// it wins (400 x 5 kbp pairs: 8.0 vs 9.2 ms end to end).  Chosen per plan
+// from the stripe-wave count; SALN_STRIPE_PK=0 / 1 forces it.
+bool stripe_packed(const Scoring &sc, uint64_t n_waves) {
     const char *e = std::getenv("SALN_STRIPE_PK");
-    if (!(e && e[0] == '1')) return false;
+    if (e && e[0] == '0') return false;
+    if (!(e && e[0] == '1') && n_waves < kStripePkMinWaves) return false;
     const int64_t pen = 2ll * (sc.match - sc.mismatch);
     if (pen < 2 || pen > 32 || sc.gap_extend > 0 || sc.gap_open > 0) return false;
     const int64_t m = std::abs(sc.match), ge = std::abs(sc.gap_extend), go = std::abs(sc.gap_open);
