@@ -308,7 +308,7 @@ def test_wide_packed_variant(saln, oracle):
 
 
 def test_packed_stripe_fill(saln, oracle, monkeypatch):
-    """The opt-in packed column-stripe fill (SALN_STRIPE_PK=1: int16 halves,
+    """The packed column-stripe fill, forced (SALN_STRIPE_PK=1: int16 halves,
     128 virtual lanes, per-row frames) and its mask layout: stripe pairs alone
     (full parent mask, first alignment) and in a batch through the cooperative
     walker equal the oracle."""
@@ -328,6 +328,29 @@ def test_packed_stripe_fill(saln, oracle, monkeypatch):
         assert (int(res["score"][k]), int(res["end_states"][k]), int(res["status"][k]) == 2) == \
             (o.score, o.end_states, o.panics), k
         assert (saln.cigar_ops_string(cig[k]) if res["printed"][k] else None) == o.first_ops, k
+
+
+def test_packed_stripes_auto_selected(saln, oracle, monkeypatch):
+    """A plan with >= 1,024 stripe waves (kStripePkMinWaves) takes the packed
+    stripe fill and layout by itself; a sample of its pairs equals the
+    oracle, and every score equals the forced unpacked run's."""
+    monkeypatch.delenv("SALN_STRIPE_PK", raising=False)
+    rng = np.random.default_rng(2024)
+    n = 220  # 1,100-column queries: 5 stripes each, 1,100 waves
+    qs = [rand_seq(rng, 1100) for _ in range(n)]
+    ds = [rand_seq(rng, int(rng.integers(200, 320))) for _ in range(n)]
+    pairs = [(k, k) for k in range(n)]
+    res, cig = saln.nw_align_batch(qs, ds, pairs=pairs)
+    for k in range(0, n, 11):
+        o = oracle.nw(qs[k], ds[k], literal_dfs=False)
+        assert (int(res["score"][k]), int(res["end_states"][k]), int(res["status"][k]) == 2) == \
+            (o.score, o.end_states, o.panics), k
+        assert (saln.cigar_ops_string(cig[k]) if res["printed"][k] else None) == o.first_ops, k
+    monkeypatch.setenv("SALN_STRIPE_PK", "0")
+    res0, cig0 = saln.nw_align_batch(qs, ds, pairs=pairs)
+    assert res0["score"].tolist() == res["score"].tolist()
+    assert res0["status"].tolist() == res["status"].tolist()
+    assert all(saln.cigar_ops_string(a) == saln.cigar_ops_string(b) for a, b in zip(cig, cig0))
 
 
 def test_context_block_cache_reuse(saln, oracle):
