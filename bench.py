@@ -1,22 +1,35 @@
 #!/usr/bin/env python3
 """Headline benchmark: GCUPS of the NW-affine hot path on MI355X.
 
-Workload (BASELINE.json configs[1]): 100,000 independent 150 x 150 G-iid DNA
-pairs per GPU (seed 0x5EED0002 + rank), sequences resident in HBM.  One step
-= one pass of the hot path over the batch: NW-affine matrix fill with the
-1 B/cell parent mask (nw_fill) + the reference's first-printed traceback per
-pair -> score, panic status, CIGAR (nw_traceback); with N > 1 ranks also the
-RCCL gather of the 16-byte per-pair result records to rank 0 (db sharded,
-SURVEY.md §8(e)).  value = all ranks' cells / max-over-ranks wall time.
+Headline workload (BASELINE.json configs[1]): 100,000 independent 150 x 150
+G-iid DNA pairs per GPU (seed 0x5EED0002 + rank), sequences resident in HBM.
+One step = one pass of the hot path over the batch: NW-affine matrix fill
+with the 1 B/cell parent mask (nw_fill) + the reference's first-printed
+traceback per pair -> score, panic status, CIGAR (nw_traceback); with N > 1
+ranks also the RCCL gather of the 16-byte per-pair result records to rank 0
+(db sharded).  value = all ranks' cells / max-over-ranks
+wall time.
 
-    python bench.py --gpus N --steps K --warmup W
+The other BASELINE.json configs ride along as extra keys under "configs"
+(SURVEY.md §8(d)), each timed here so the driver's clock covers them:
+  c5  configs[4]: 10k x 100k 150 bp score-only all-vs-all, db sharded over
+      the N ranks, {score, status} records gathered to rank 0 (every N);
+  c1  configs[0]: one 1 kbp pair, GPU latency + the oracle's reference-
+      structure CPU path on one core (N = 1);
+  c3  configs[2]: WFA (reference semantics) on 10^6 distinct 10 kbp G-mut
+      pairs (N = 1);
+  c4  configs[3]: one 100 kbp pair, fill + traceback, + the linear-memory
+      oracle on the host cores (N = 1);
+  host_path: configs[1] through the host-buffer C ABI (PCIe-inclusive; never
+      the value) (N = 1).
+
+    python bench.py --gpus N --steps K --warmup W [--legs c5,c1,c3,c4,host|none]
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
-import subprocess
 import sys
 import time
 
@@ -27,9 +40,19 @@ sys.path.insert(0, ROOT)
 
 METRIC = "GCUPS (affine-gap NW) at 1/2/4/8 MI355X; % of HBM roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
-VALU_PEAK_TOPS = 1024 * 16 * 2.4e9 / 1e12  # 39.3: 256 CUs x 4 SIMDs x 16 lanes x 2.4 GHz
+# VALU issue peak, MI355X_MICROARCH.md "Wave scheduling": a wave64 VALU op
+# issues over 2 cycles on a SIMD-32 -> 1,024 SIMDs x 32 lanes x 2.4 GHz.
+VALU_PEAK_TOPS = 1024 * 32 * 2.4e9 / 1e12  # 78.6 T lane-ops/s
+# The rate measured for the packed / VOP3 / DPP ops the fill's chain is made
+# of (tools/micro/valu_rate.hip: 4 cycles per wave64 op) -> 39.3 T.
+VALU_PK_TOPS = 1024 * 16 * 2.4e9 / 1e12
 N_PAIRS, LQ, LD = 100_000, 150, 150
 SEED = 0x5EED0002
+ALL_LEGS = ("c5", "c1", "c3", "c4", "host")
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
 
 
 def cpu_threads() -> int:
@@ -95,16 +118,280 @@ def pmc_traffic(kernel: str, field: str = "hbm_bytes"):
 
 def valu_roof(kernel: str, avg_s: float):
     """SURVEY.md 8(d) asks for the VALU fraction beside the HBM one: the fill's
-    VALU wave-instructions per launch (PMC SQ_INSTS_VALU) x 64 lanes over its
-    measured duration, against 1,024 SIMDs x 16 lanes x 2.4 GHz (one wave64
-    instruction per 4 cycles per SIMD; the 2-cycle ops the kernel favours can
-    exceed that rate, so frac may approach or pass 1 when issue-bound)."""
+    VALU wave-instructions per launch (PMC SQ_INSTS_VALU, committed PMC
+    summary) x 64 lanes over its measured duration, against the guide's
+    2-cycle wave64 issue peak (78.6 T lane-ops/s); frac_4cycle is the same
+    against the 4-cycle rate measured for packed / VOP3 / DPP ops."""
     n = pmc_traffic(kernel, "valu_wave_insts")
     if not n:
         return None
     achieved = n * 64 / avg_s / 1e12
     return {"wave_insts_per_launch": n, "achieved": round(achieved, 2),
-            "peak": VALU_PEAK_TOPS, "unit": "T int lane-ops/s", "frac": round(achieved / VALU_PEAK_TOPS, 4)}
+            "peak": round(VALU_PEAK_TOPS, 2), "unit": "T int lane-ops/s",
+            "frac": round(achieved / VALU_PEAK_TOPS, 4),
+            "frac_4cycle": round(achieved / VALU_PK_TOPS, 4),
+            "source": "SQ_INSTS_VALU from profiles/pmc_traffic.json (a rocprofv3 --pmc run of "
+                      "this command), duration measured in this run"}
+
+
+def verify_c2(res_np, cig_np, cigar_off, qs, qo, ds, do, n_check: int = 1000) -> dict:
+    """Untimed check of the benched run's own output: the first n_check
+    pairs' score, end states, panic status, printed flag and first printed
+    CIGAR against the oracle (oracle/refcheck.c, literal fill + memoised DFS;
+    a checker, never the measured path)."""
+    from oracle import refcpu  # checker only
+    from sequencealigning_amd import _lib
+    n = min(n_check, len(qo) - 1)
+    want = refcpu.check_pairs(qs[:int(qo[n])], qo[:n + 1], ds[:int(do[n])], do[:n + 1],
+                              threads=cpu_threads())
+    r = res_np.view(_lib.RESULT_DTYPE)[:n]
+    bad = 0
+    for k in range(n):
+        ok = (int(r["score"][k]) == int(want.score[k])
+              and int(r["end_states"][k]) == int(want.end_states[k])
+              and (int(r["status"][k]) == _lib.REF_PANIC_BOUNDARY) == bool(want.panics[k])
+              and bool(r["printed"][k]) == (want.cig_len[k] >= 0))
+        if ok and r["printed"][k]:
+            o0 = int(cigar_off[k])
+            ok = np.array_equal(cig_np[o0:o0 + int(r["cigar_len"][k])], want.cigar_words(k))
+        bad += not ok
+    return {"pairs": n, "mismatches": bad, "checker": "oracle/refcheck.c (untimed)"}
+
+
+def timed(fn, world, dist, torch, local):
+    """Barrier + synchronize on both sides; max over ranks of the wall time."""
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    fn()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    t = torch.tensor([dt], dtype=torch.float64, device=f"cuda:{local}")
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+# ------------------------------------------------------------------- legs
+def leg_c5(world, rank, local, dist, torch, nq=10_000, ndb=100_000, L=150):
+    """configs[4]: 10k queries x 100k db records of 150 bp (length assumed =
+    C2), G-iid (seed 0x5EED0004), score-only all-vs-all with
+    the db sharded over the ranks and the records gathered to rank 0
+    (dist.ShardedAllVsAll).  Total work is fixed as N grows (strong)."""
+    from sequencealigning_amd import synth
+    from sequencealigning_amd.dist import ShardedAllVsAll
+    seed = 0x5EED0004
+    qs = synth.random_bases(seed, nq * L)
+    qo = np.arange(nq + 1, dtype=np.uint64) * np.uint64(L)
+    do = np.arange(ndb + 1, dtype=np.uint64) * np.uint64(L)
+    # every rank draws only its own db block (same stream positions as the full db)
+    from sequencealigning_amd.dist import shard_db
+    lo, hi = shard_db(np.full(ndb, L), world, rank)
+    ds = np.zeros(ndb * L, np.uint8)
+    ds[lo * L:hi * L] = synth.random_bases(seed ^ 0xD5D5D5D5, (hi - lo) * L, start=lo * L)
+    t0 = time.perf_counter()
+    av = ShardedAllVsAll(qs, qo, ds, do, device=local)
+    setup = time.perf_counter() - t0
+    av.execute()  # warm: code objects, RCCL communicator
+    dt = timed(av.execute, world, dist, torch, local)
+    out = None
+    if rank == 0:
+        # checker: a seeded sample of the gathered records against the oracle
+        from oracle import refcpu  # checker only
+        rng = np.random.default_rng(4)
+        di = rng.integers(0, ndb, 256)
+        qi = rng.integers(0, nq, 256)
+        allq = qs.tobytes()
+        dsel = [synth.random_bases(seed ^ 0xD5D5D5D5, L, start=int(d) * L).tobytes() for d in di]
+        qsel = [allq[int(q) * L:(int(q) + 1) * L] for q in qi]
+        qo2 = np.arange(257, dtype=np.uint64) * np.uint64(L)
+        want = refcpu.check_pairs(b"".join(qsel), qo2, b"".join(dsel), qo2, threads=cpu_threads())
+        sc, st = av.lookup(di, qi)
+        bad = int(np.sum((sc != want.score) | ((st == 2) != want.panics)))
+        out = {"workload": f"configs[4]: {nq} x {ndb} score-only all-vs-all, {L} bp G-iid "
+                           f"(seed {seed:#x}), db sharded over {world} rank(s), records "
+                           f"gathered to rank 0" + (" over RCCL" if world > 1 else ""),
+               "value": round(av.cells / dt / 1e9, 1), "unit": "GCUPS", "seconds": round(dt, 4),
+               "pairs_per_s": round(nq * ndb / dt, 1), "cells": av.cells, "n_gpus": world,
+               "scaling": "strong", "setup_s": round(setup, 2),
+               "panic_frac": round(av.status_count(2) / (nq * ndb), 4),
+               "verified": {"pairs": 256, "mismatches": bad,
+                            "checker": "oracle/refcheck.c on a seeded sample (untimed)"}}
+    av.close()
+    del av
+    torch.cuda.empty_cache()
+    return out
+
+
+def _single_pair(torch, saln, q, d, reps, score_only=False):
+    qo = np.array([0, len(q)], np.uint64)
+    do = np.array([0, len(d)], np.uint64)
+    plan = saln.NwPlan(qo, do, pairs=[(0, 0)])
+    plan.set_score_only(score_only)
+    dq = torch.frombuffer(bytearray(q), dtype=torch.uint8).cuda()
+    dd = torch.frombuffer(bytearray(d), dtype=torch.uint8).cuda()
+    res = torch.zeros(4, dtype=torch.int32, device="cuda")
+    cig = torch.zeros(max(1, plan.cigar_words), dtype=torch.int32, device="cuda")
+    plan.execute(dq, dd, res, cig)
+    torch.cuda.synchronize()
+    plan.set_timing(True)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        plan.execute(dq, dd, res, cig)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / reps
+    f, _ = plan.kernel_time("nw_fill")
+    tb, _ = plan.kernel_time("nw_traceback")
+    r = res.cpu().numpy().view(saln._lib.RESULT_DTYPE)[0]
+    out = {"len_q": len(q), "len_db": len(d), "cells": plan.cells, "score": int(r["score"]),
+           "status": int(r["status"]), "printed": int(r["printed"]), "flags": int(r["flags"]),
+           "execute_ms": round(dt * 1e3, 4), "fill_ms": round(f / reps, 4),
+           "traceback_ms": round(tb / reps, 4), "gcups": round(plan.cells / dt / 1e9, 2)}
+    plan.close()
+    return out
+
+
+def leg_c1(torch, saln):
+    """configs[0]: one 1 kbp x 1 kbp pair (G-mut 5 %, seed 0x5EED0000; and a
+    G-iid pair), score + first-printed traceback on the GPU, next to the
+    reference-structure CPU path on one core (the oracle's literal fill +
+    DFS that prints every co-optimal alignment, needleman_wunsch_affine.rs
+    :424-437)."""
+    from oracle import refcpu  # cpu_baseline leg only
+    from sequencealigning_amd import synth
+    q = synth.random_bases(0x5EED0000, 1000).tobytes()
+    d = synth.mutate(q, 0.05, seed=1000)
+    gi = synth.random_bases(0x5EED0000 ^ 0x77, 1000).tobytes()
+    out = {"workload": "configs[0]: one 1 kbp x 1 kbp pair, score + first-printed traceback "
+                       "(G-mut 5 %; iid beside it)",
+           "gpu": _single_pair(torch, saln, q, d, 50),
+           "gpu_iid": _single_pair(torch, saln, q, gi, 50)}
+    qo = np.array([0, len(q)], np.uint64)
+    do = np.array([0, len(d)], np.uint64)
+    reps, t0 = 0, time.perf_counter()
+    while reps < 3 or time.perf_counter() - t0 < 2.0:
+        refcpu.run_pairs(q, qo, d, do, 1, max_pops=10_000_000)
+        reps += 1
+    cpu_s = (time.perf_counter() - t0) / reps
+    o = refcpu.nw(q, d, literal_dfs=False)
+    out["cpu_baseline"] = {"ms": round(cpu_s * 1e3, 3), "cores": 1, "kind": "port",
+                           "gcups": round(len(q) * len(d) / cpu_s / 1e9, 5),
+                           "sample": f"the same pair, {reps} runs of oracle/refcpu.c fill + "
+                                     "literal DFS (every co-optimal block)"}
+    out["matches_oracle"] = bool(out["gpu"]["score"] == o.score)
+    out["speedup_vs_cpu"] = round(cpu_s * 1e3 / out["gpu"]["execute_ms"], 1)
+    return out
+
+
+def leg_c4(torch, saln):
+    """configs[3]: one 100 kbp x 100 kbp pair (G-mut 5 %, seed 0x5EED0003),
+    fill + parent mask + first-printed traceback on one GPU, and the
+    linear-memory oracle (reflinear.c, column stripes on the host cores) on
+    the same pair for score parity and the CPU time."""
+    from oracle import refcpu  # cpu_baseline leg only
+    from sequencealigning_amd import synth
+    q = synth.random_bases(0x5EED0003, 100_000).tobytes()
+    d = synth.mutate(q, 0.05, seed=100_000)
+    g = _single_pair(torch, saln, q, d, 3)
+    torch.cuda.empty_cache()
+    T = cpu_threads()
+    t0 = time.perf_counter()
+    sc, es, pan = refcpu.nw_score_linear(q, d, threads=T)
+    cpu_s = time.perf_counter() - t0
+    return {"workload": "configs[3]: one 100 kbp x 100 kbp pair, G-mut 5 %, fill + 1 B/cell mask "
+                        "+ first-printed traceback", "gpu": g,
+            "value": g["gcups"], "unit": "GCUPS",
+            "matches_oracle": bool(g["score"] == sc and (g["status"] == 2) == pan),
+            "cpu_baseline": {"seconds": round(cpu_s, 2), "cores": T, "kind": "port",
+                             "gcups": round(len(q) * len(d) / cpu_s / 1e9, 3),
+                             "sample": "the whole pair, oracle/reflinear.c score-only in linear "
+                                       "memory (the reference-structure path needs ~TB)"}}
+
+
+def leg_c3(torch, saln, n_pairs=1_000_000, L=10_000):
+    """configs[2]: WFA with the reference's semantics (wfa.rs) on 10^6
+    distinct 10 kbp G-mut(5 %) pairs generated on the device (synth.
+    mut_pairs_torch = tools/bench_wfa.py's pairs), step cap 10^4, sequences
+    and results in HBM."""
+    from oracle import refcpu  # cpu_baseline leg only
+    from sequencealigning_amd import synth
+    t0 = time.perf_counter()
+    qs, qo, ds, do = synth.mut_pairs_torch(n_pairs, L, 0.05, 0x5EED0003, "cuda")
+    torch.cuda.synchronize()
+    gen_s = time.perf_counter() - t0
+    k = np.arange(n_pairs, dtype=np.uint32)
+    plan = saln.WfaPlan(qo, do, pairs=np.stack([k, k], 1), max_steps=10_000)
+    out_t = torch.zeros(n_pairs * 8, dtype=torch.int32, device="cuda")
+    plan.execute(qs, ds, out_t)
+    torch.cuda.synchronize()
+    reps = 3
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        plan.execute(qs, ds, out_t)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / reps
+    r = out_t.cpu().numpy().view(saln._lib.WFA_RESULT_DTYPE)
+    st, cnt = np.unique(r["status"], return_counts=True)
+    # CPU: the oracle's WFA (refwfa.c) on a sample of the same pairs, one core
+    samp = np.random.default_rng(3).choice(n_pairs, 200, replace=False)
+    bad, t0 = 0, time.perf_counter()
+    for p in samp:
+        qq = qs[int(qo[p]):int(qo[p + 1])].cpu().numpy().tobytes()
+        dd = ds[int(do[p]):int(do[p + 1])].cpu().numpy().tobytes()
+        o = refcpu.wfa(qq, dd, max_steps=10_000)
+        rr = r[p]
+        bad += not (int(rr["status"]) == o.status and int(rr["score"]) == o.score
+                    and int(rr["steps"]) == o.steps)
+    cpu_s = (time.perf_counter() - t0) / len(samp)
+    plan.close()
+    del qs, ds, out_t
+    torch.cuda.empty_cache()
+    return {"workload": f"configs[2]: {n_pairs} distinct WFA pairs of {L} bp G-mut(5 %), "
+                        "reference semantics, step cap 1e4",
+            "value": round(n_pairs / dt, 1), "unit": "pairs/s", "ms": round(dt * 1e3, 3),
+            "status_counts": {saln._lib.STATUS_NAMES.get(int(s), str(int(s))): int(c)
+                              for s, c in zip(st, cnt)},
+            "gen_s": round(gen_s, 2),
+            "verified": {"pairs": len(samp), "mismatches": bad,
+                         "checker": "oracle/refwfa.c status, printed score, steps (untimed)"},
+            "cpu_baseline": {"pairs_per_s": round(1 / cpu_s, 1), "cores": 1, "kind": "port",
+                             "sample": f"{len(samp)} of the pairs through oracle/refwfa.c "
+                                       "(its stdout text included)"}}
+
+
+def leg_host(saln):
+    """configs[1] through the host-buffer boundary (saln_nw_align_batch):
+    plan + H2D + fill + traceback + D2H of results and CIGARs.  The
+    PCIe-inclusive rate a caller with host arrays sees; never the value."""
+    import ctypes as C
+
+    from sequencealigning_amd import _lib, synth
+    n = N_PAIRS
+    qs, qo, ds, do = synth.iid_pairs(n, LQ, LD, seed=SEED)
+    pq = np.arange(n, dtype=np.uint32)
+    res = np.zeros(n, dtype=_lib.RESULT_DTYPE)
+    coff = np.zeros(n + 1, np.uint64)
+    coff[1:] = np.cumsum(np.full(n, LQ + LD, np.uint64))
+    cig = np.zeros(int(coff[-1]), np.uint32)
+    vp = lambda x: x.ctypes.data_as(C.c_void_p)  # noqa: E731
+    L, ctx = _lib.lib(), _lib.context(0)
+
+    def run():
+        _lib.check(L.saln_nw_align_batch(ctx, vp(qs), vp(qo), n, vp(ds), vp(do), n,
+                                         vp(pq), vp(pq), n, 0, None, vp(res), vp(cig),
+                                         vp(coff)), "saln_nw_align_batch")
+    run()
+    reps = 5
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        run()
+    dt = (time.perf_counter() - t0) / reps
+    return {"workload": f"configs[1] via saln_nw_align_batch (host buffers): {n} 150x150 pairs",
+            "value": round(n * LQ * LD / dt / 1e9, 1), "unit": "GCUPS (PCIe-inclusive)",
+            "ms": round(dt * 1e3, 2)}
 
 
 def main() -> None:
@@ -114,6 +401,9 @@ def main() -> None:
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--pairs", type=int, default=N_PAIRS)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--legs", default="auto",
+                    help="comma list of extra configs (c5,c1,c3,c4,host), 'none', or 'auto' "
+                         "(all at N = 1, c5 at N > 1)")
     ap.add_argument("--score-only", action="store_true",
                     help="score + panic status only (no parent codes / traceback; the C5 mode)")
     ap.add_argument("--pipeline", action="store_true",
@@ -133,6 +423,12 @@ def main() -> None:
     torch.cuda.set_device(local)
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    if args.legs == "auto":
+        legs = list(ALL_LEGS) if world == 1 else ["c5"]
+    elif args.legs == "none":
+        legs = []
+    else:
+        legs = [x for x in args.legs.split(",") if x]
 
     n = args.pairs
     qs, qo, ds, do = synth.iid_pairs(n, LQ, LD, seed=SEED + rank)
@@ -181,37 +477,32 @@ def main() -> None:
     drain()
     torch.cuda.synchronize()
     plan.set_timing(True)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    drain()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
+
+    def run_steps():
+        for _ in range(args.steps):
+            step()
+        drain()
+    dt = timed(run_steps, world, dist, torch, local)
     fill_ms, fill_n = plan.kernel_time("nw_fill")
     tb_ms, tb_n = plan.kernel_time("nw_traceback")
     ex_ms, ex_n = plan.kernel_time("nw_execute")
-    t = torch.tensor([dt], dtype=torch.float64, device=f"cuda:{local}")
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    dt = float(t.item())
     cells_rank = plan.cells
     total_cells = cells_rank * world * args.steps
     gcups = total_cells / dt / 1e9
     fill_avg_s = fill_ms / max(1, fill_n) / 1e3
     achieved = cells_rank * 1.0 / fill_avg_s / 1e9  # 1 B/cell parent mask, GB/s
+    out = None
     if rank == 0:
-        hr = res[(args.steps - 1) % nbuf].cpu().numpy()
+        last = (args.steps - 1) % nbuf if args.steps else 0
+        hr = res[last].cpu().numpy()
         statuses = np.bincount(hr[1::4] & 0xFF, minlength=3)
+        fill_kernel = "nw_fill_pk_kernel<16, 10,"
         out = {
             "metric": METRIC, "value": round(gcups, 3), "unit": "GCUPS", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(dt / args.steps * 1e3, 4), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "int16x2",
+            "scaling": "weak", "vs_baseline": None,
+            "dtype": "i32-exact (i16x2 packed arithmetic)",
             "data": "synthetic (splitmix64 G-iid ACGT)",
             "config": {"workload": ("configs[1]: independent 150x150 NW-affine pairs per GPU "
                                     "(fill + 1 B/cell parent mask + first-printed traceback/CIGAR)")
@@ -223,21 +514,58 @@ def main() -> None:
                                                                else "")},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": pmc_traffic("nw_fill_pk_kernel<16, 10,") if not args.score_only else None,
+                         "traffic": pmc_traffic(fill_kernel) if not args.score_only else None,
                          "traffic_unit": "bytes/launch (PMC FETCH_SIZE*2 + WRITE_SIZE)",
+                         "traffic_source": "profiles/pmc_traffic.json: rocprofv3 --pmc passes of "
+                                           "this command (tools/pmc.sh), not measured in this run",
                          "algorithmic_bytes": cells_rank, "kernel": "nw_fill",
                          "kernel_avg_ms": round(fill_avg_s * 1e3, 4),
                          "traceback_avg_ms": round(tb_ms / max(1, tb_n), 4),
                          "execute_avg_ms": round(ex_ms / max(1, ex_n), 4),
                          "pipelined": pipelined,
-                         "valu": valu_roof("nw_fill_pk_kernel<16, 10,", fill_avg_s)
+                         "valu": valu_roof(fill_kernel, fill_avg_s)
                          if not args.score_only else None},
             "status_counts": {"ok": int(statuses[0]), "ref_panic_boundary": int(statuses[2])},
         }
+        if not args.score_only:
+            out["verified"] = verify_c2(hr, cig[last].cpu().numpy().view(np.uint32),
+                                        plan.cigar_off, qs, qo, ds, do)
+    plan.close()
+    del res, cig, dq, dd
+    torch.cuda.empty_cache()
+
+    extra = {}
+    for leg in legs:
+        t0 = time.perf_counter()
+        try:
+            if leg == "c5":
+                r = leg_c5(world, rank, local, dist, torch)
+            elif rank != 0 or world > 1:
+                continue
+            elif leg == "c1":
+                r = leg_c1(torch, saln)
+            elif leg == "c3":
+                r = leg_c3(torch, saln)
+            elif leg == "c4":
+                r = leg_c4(torch, saln)
+            elif leg == "host":
+                r = leg_host(saln)
+            else:
+                raise ValueError(f"unknown leg {leg}")
+        except Exception as e:  # a failing extra leg must not hide the headline line
+            if world > 1:
+                raise
+            r = {"error": f"{type(e).__name__}: {e}"}
+        if rank == 0:
+            r["leg_wall_s"] = round(time.perf_counter() - t0, 2)
+            extra[leg] = r
+            log(f"[bench] {leg}: {json.dumps(r)[:300]}")
+    if rank == 0:
+        if extra:
+            out["configs"] = extra
         if not args.no_cpu_baseline and world == 1:  # the CPU leg: rank 0 at N = 1 only
             out["cpu_baseline"] = cpu_baseline()
         print(json.dumps(out), flush=True)
-    plan.close()
     if world > 1:
         dist.destroy_process_group()
 

@@ -143,7 +143,8 @@ int saln_nw_align_batch(saln_context *ctx, const uint8_t *q_seq, const uint64_t 
 /* -------------------------------------------------- NW: batched (device, plan)
  * For callers whose data is already resident in HBM (bench, multi-GPU
  * driver).  The plan is built once from host-side lengths; execute then only
- * launches kernels on `stream` (hipStream_t; NULL = the context's stream).
+ * launches kernels on `stream` (hipStream_t; NULL = the context's own
+ * non-blocking stream; pass hipStreamLegacy for the legacy null stream).
  * Device buffers: q_seq/db_seq (same CSR byte layout as the host offsets
  * given to the plan), results[n_pairs], cigar[plan cigar words] (may be
  * NULL: traceback still runs, ops are not stored). */

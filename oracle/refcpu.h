@@ -84,6 +84,14 @@ uint64_t ref_nw_run_pairs_mt(const uint8_t *qs, const uint64_t *q_off, const uin
                              const uint64_t *d_off, uint64_t n_pairs, uint64_t max_pops,
                              int threads);
 
+/* refcheck.c: per-pair score, end states, panic status and first printed
+ * alignment (CIGAR words (len << 4) | op, '=' 7 'X' 8 'I' 1 'D' 2; cig_len -1
+ * when nothing is printed) for every pair of a CSR batch, on threads. */
+int ref_nw_check_pairs_mt(const uint8_t *qs, const uint64_t *q_off, const uint8_t *ds,
+                          const uint64_t *d_off, uint64_t n_pairs, const uint64_t *cig_off,
+                          int32_t *score, uint8_t *end_states, uint8_t *panics, int32_t *cig_len,
+                          uint32_t *cig, int threads);
+
 /* Linear-memory score + end states + panic status of one pair with the
  * reference semantics (reflinear.c), on `threads` column stripes.  For
  * pairs too large for ref_nw_fill (C4).  Returns 0 on success. */

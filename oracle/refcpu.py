@@ -56,6 +56,10 @@ def lib():
         L.ref_nw_run_pairs_mt.argtypes = [u8p, C.POINTER(C.c_uint64), u8p, C.POINTER(C.c_uint64),
                                           C.c_uint64, C.c_uint64, C.c_int]
         L.ref_nw_run_pairs_mt.restype = C.c_uint64
+        L.ref_nw_check_pairs_mt.argtypes = [u8p, C.POINTER(C.c_uint64), u8p,
+                                            C.POINTER(C.c_uint64), C.c_uint64,
+                                            C.POINTER(C.c_uint64), C.POINTER(C.c_int32), u8p, u8p,
+                                            C.POINTER(C.c_int32), C.POINTER(C.c_uint32), C.c_int]
         L.ref_nw_score_linear.argtypes = [u8p, C.c_size_t, u8p, C.c_size_t, C.c_int,
                                           C.POINTER(C.c_int32), u8p, C.POINTER(C.c_int)]
         L.ref_parse_fasta.argtypes = [u8p, C.c_size_t, C.c_int, u8p, C.c_size_t,
@@ -170,6 +174,49 @@ def run_pairs_mt(qs: bytes, q_off: np.ndarray, ds: bytes, d_off: np.ndarray, n_p
     return L.ref_nw_run_pairs_mt(_u8(qs), qo.ctypes.data_as(C.POINTER(C.c_uint64)), _u8(ds),
                                  do.ctypes.data_as(C.POINTER(C.c_uint64)), n_pairs, max_pops,
                                  threads)
+
+
+@dataclass
+class BatchCheck:
+    score: np.ndarray       # int32[n]
+    end_states: np.ndarray  # uint8[n]
+    panics: np.ndarray      # bool[n]
+    cig_len: np.ndarray     # int32[n], -1 = nothing printed
+    cig_off: np.ndarray     # uint64[n+1]
+    cig: np.ndarray         # uint32 CIGAR words, pair p at cig_off[p]
+
+    def cigar_words(self, p: int) -> np.ndarray | None:
+        n = int(self.cig_len[p])
+        return None if n < 0 else self.cig[int(self.cig_off[p]):int(self.cig_off[p]) + n]
+
+
+def check_pairs(qs, q_off, ds, d_off, threads: int = 0) -> BatchCheck:
+    """Reference results of every pair (k-th query slice vs k-th db slice of
+    the CSR inputs): literal fill + memoised DFS (refcheck.c), on threads."""
+    if threads <= 0:
+        threads = min(16, os.cpu_count() or 1)
+    qs = np.ascontiguousarray(np.frombuffer(bytes(qs), np.uint8) if isinstance(qs, (bytes, bytearray)) else qs, np.uint8)
+    ds = np.ascontiguousarray(np.frombuffer(bytes(ds), np.uint8) if isinstance(ds, (bytes, bytearray)) else ds, np.uint8)
+    qo = np.ascontiguousarray(q_off, np.uint64)
+    do = np.ascontiguousarray(d_off, np.uint64)
+    n = len(qo) - 1
+    span = (qo[1:] - qo[:-1]) + (do[1:] - do[:-1])
+    co = np.zeros(n + 1, np.uint64)
+    co[1:] = np.cumsum(span)
+    out = BatchCheck(np.zeros(n, np.int32), np.zeros(n, np.uint8), np.zeros(n, np.uint8),
+                     np.zeros(n, np.int32), co, np.zeros(max(1, int(co[-1])), np.uint32))
+    P = lambda a, t: a.ctypes.data_as(C.POINTER(t))  # noqa: E731
+    rc = lib().ref_nw_check_pairs_mt(P(qs if len(qs) else np.zeros(1, np.uint8), C.c_uint8),
+                                      P(qo, C.c_uint64),
+                                      P(ds if len(ds) else np.zeros(1, np.uint8), C.c_uint8),
+                                      P(do, C.c_uint64), n, P(co, C.c_uint64),
+                                      P(out.score, C.c_int32), P(out.end_states, C.c_uint8),
+                                      P(out.panics, C.c_uint8), P(out.cig_len, C.c_int32),
+                                      P(out.cig, C.c_uint32), threads)
+    if rc != 0:
+        raise MemoryError("oracle check_pairs")
+    out.panics = out.panics.astype(bool)
+    return out
 
 
 def parse_fasta_bytes(data: bytes, valid_ext: bool = True):

@@ -208,6 +208,19 @@ def context(device: int = 0) -> C.c_void_p:
         return ctx
 
 
+HIP_STREAM_LEGACY = 1  # hipStreamLegacy (hip_runtime_api.h): the legacy null stream
+
+
+def torch_stream(device) -> int:
+    """torch's current stream on `device` as a libsaln stream argument.  The
+    C ABI reads NULL as "the context's own stream" (non-blocking, unordered
+    with torch's default stream), so torch's null stream is passed as
+    hipStreamLegacy: the kernels then run in order with torch's work."""
+    import torch
+    h = torch.cuda.current_stream(device).cuda_stream
+    return h if h else HIP_STREAM_LEGACY
+
+
 def scoring_arg(scoring) -> C.POINTER(NwScoring) | None:
     if scoring is None:
         return None

@@ -160,7 +160,7 @@ int saln_nw_avsa_execute(saln_nw_avsa *a, const uint8_t *d_q_seq, const uint8_t 
     if (!a || !d_out) return SALN_E_INVALID;
     if (a->n_q * a->n_db == 0) return SALN_OK;
     HIP_TRY(hipSetDevice(a->ctx->device));
-    hipStream_t s = stream ? (hipStream_t)stream : a->ctx->stream;
+    hipStream_t s = resolve_stream(stream, a->ctx);
     int2 *out = reinterpret_cast<int2 *>(d_out);
     const uint32_t nqt = (uint32_t)a->n_q;
     constexpr uint64_t kChunk = 1ull << 30;  // pairs per launch (uint32 index space)

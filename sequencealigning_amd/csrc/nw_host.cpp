@@ -437,7 +437,7 @@ int saln_nw_execute(saln_nw_plan *p, const uint8_t *d_q, const uint8_t *d_db,
     if (!p || !d_results || (!d_q && p->n_pairs) || (!d_db && p->n_pairs)) return SALN_E_INVALID;
     if (p->n_pairs == 0) return SALN_OK;
     HIP_TRY(hipSetDevice(p->ctx->device));
-    hipStream_t s = stream ? (hipStream_t)stream : p->ctx->stream;
+    hipStream_t s = resolve_stream(stream, p->ctx);
     const size_t nsub = p->sub.size() - 1;  // >= 1 (an empty sub-batch if n_fill == 0)
     // the traceback stream: the second one only when a traceback can overlap a
     // fill (async plans, sub-batches); otherwise the same stream, so no
@@ -544,7 +544,7 @@ int saln_nw_plan_set_async(saln_nw_plan *p, int enable) {
 int saln_nw_plan_sync(saln_nw_plan *p, void *stream, int keep_latest) {
     if (!p) return SALN_E_INVALID;
     HIP_TRY(hipSetDevice(p->ctx->device));
-    hipStream_t s = stream ? (hipStream_t)stream : p->ctx->stream;
+    hipStream_t s = resolve_stream(stream, p->ctx);
     for (int b = 0; b < 2; ++b) {
         if (!p->tb_pending[b] || (keep_latest && b == p->last_buf)) continue;
         HIP_TRY(hipStreamWaitEvent(s, p->tb_done(b), 0));

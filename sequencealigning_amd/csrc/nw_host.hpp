@@ -31,6 +31,16 @@ struct saln_context {
     size_t pinned_bytes = 0;
 };
 
+// A C-ABI stream argument: NULL = the context's own (non-blocking) stream;
+// hipStreamLegacy = the legacy null stream (torch's default stream), used as
+// the handle 0 that every HIP call accepts; anything else as given.
+inline hipStream_t resolve_stream(void *stream, const saln_context *ctx) {
+    if (!stream) return ctx->stream;
+    if ((hipStream_t)stream == hipStreamLegacy) return (hipStream_t)0;
+    return (hipStream_t)stream;
+}
+
+
 namespace saln {
 
 // SALN_HOST_TIMING=1: stage times of the host-side paths on stderr

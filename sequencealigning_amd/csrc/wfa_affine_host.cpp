@@ -177,7 +177,7 @@ int saln_wfa_affine_execute(saln_wfa_affine_plan *p, const uint8_t *d_q_seq,
                             const uint8_t *d_db_seq, int32_t *d_scores, void *stream) {
     if (!p || !d_scores || !d_q_seq || !d_db_seq) return SALN_E_INVALID;
     if (!p->n) return SALN_OK;
-    hipStream_t s = stream ? (hipStream_t)stream : p->ctx->stream;
+    hipStream_t s = resolve_stream(stream, p->ctx);
     TRY(hipSetDevice(p->ctx->device));
     TRY(launch_wfa_affine(p->d_pairs, (uint32_t)p->n, d_q_seq, d_db_seq, p->p1, p->wide, p->grid1,
                           nullptr, d_scores, s));

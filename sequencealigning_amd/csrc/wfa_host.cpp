@@ -388,7 +388,7 @@ int saln_wfa_execute(saln_wfa_plan *p, const uint8_t *d_q_seq, const uint8_t *d_
                      saln_wfa_result *d_results, void *stream) {
     if (!p || (p->n_pairs && (!d_q_seq || !d_db_seq || !d_results))) return SALN_E_INVALID;
     TRY_HIP(hipSetDevice(p->ctx->device));
-    hipStream_t s = stream ? (hipStream_t)stream : p->ctx->stream;
+    hipStream_t s = resolve_stream(stream, p->ctx);
     return wfa_device(p->ws, (const WfaPairDesc *)p->pairs.p, p->n_pairs, d_q_seq, d_db_seq,
                       p->max_steps, p->max_width, d_results, nullptr, nullptr, nullptr, 0, s);
 }

@@ -215,8 +215,7 @@ class NwPlan:
         int32[n_pairs*4] / int32[cigar_words]) or raw device pointers."""
         ptr = lambda t: None if t is None else (t if isinstance(t, int) else t.data_ptr())  # noqa
         if stream is None:
-            import torch
-            stream = torch.cuda.current_stream(self.device).cuda_stream
+            stream = _lib.torch_stream(self.device)
         _lib.check(self._L.saln_nw_execute(self._h, ptr(q_seq), ptr(db_seq), ptr(results),
                                            ptr(cigar), stream), "saln_nw_execute")
 
@@ -227,8 +226,7 @@ class NwPlan:
     def sync(self, stream=None, keep_latest: bool = False) -> None:
         """Make `stream` wait for the pending tracebacks (all, or all but the latest)."""
         if stream is None:
-            import torch
-            stream = torch.cuda.current_stream(self.device).cuda_stream
+            stream = _lib.torch_stream(self.device)
         _lib.check(self._L.saln_nw_plan_sync(self._h, stream, int(keep_latest)), "sync")
 
     def set_score_only(self, enable: bool) -> None:
@@ -280,8 +278,7 @@ class NwAllVsAll:
     def execute(self, q_seq, db_seq, out, stream=None) -> None:
         ptr = lambda t: t if isinstance(t, int) else t.data_ptr()  # noqa: E731
         if stream is None:
-            import torch
-            stream = torch.cuda.current_stream(self.device).cuda_stream
+            stream = _lib.torch_stream(self.device)
         _lib.check(self._L.saln_nw_avsa_execute(self._h, ptr(q_seq), ptr(db_seq), ptr(out),
                                                 stream), "saln_nw_avsa_execute")
 

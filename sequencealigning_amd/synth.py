@@ -60,3 +60,84 @@ def mutate(seq: bytes | np.ndarray, delta: float, seed: int) -> bytes:
 def mut_pair(length: int, delta: float, seed: int) -> tuple[bytes, bytes]:
     q = random_bases(seed, length).tobytes()
     return q, mutate(q, delta, seed ^ 0x5A5A5A5A)
+
+
+# ---- the same generators as torch ops, for batches too large to build on the
+# host (configs[2]: 10^6 pairs of 10 kbp); bit-identical to the numpy ones.
+def _s64(v: int) -> int:
+    return v - (1 << 64) if v >= 1 << 63 else v
+
+
+_M1, _M2, _GOLD = _s64(0xBF58476D1CE4E5B9), _s64(0x94D049BB133111EB), _s64(0x9E3779B97F4A7C15)
+
+
+def _shr(z, k: int):
+    """Logical right shift of int64 bit patterns."""
+    return (z >> k) & ((1 << (64 - k)) - 1)
+
+
+def splitmix64_torch(seed, idx):
+    """splitmix64 output idx + 1 of the stream seeded with `seed` (int64
+    tensors or ints, broadcast), as int64 bit patterns."""
+    z = seed + (idx + 1) * _GOLD
+    z = (z ^ _shr(z, 30)) * _M1
+    z = (z ^ _shr(z, 27)) * _M2
+    return z ^ _shr(z, 31)
+
+
+def mut_pairs_torch(n_pairs: int, length: int, delta: float, seed: int, device,
+                    chunk: int = 8192):
+    """configs[2]-style G-mut batch on `device`: query k = bases
+    [k*length, (k+1)*length) of random_bases(seed, n_pairs*length), db k =
+    mutate(query k, delta, seed=k) (tools/bench_wfa.py's pairs, every pair
+    distinct).  Returns (q_seq, q_off, db_seq, db_off): uint8 device tensors
+    and uint64 host offsets, equal to the numpy generators'."""
+    import torch
+    dev = torch.device(device)
+    bases = torch.tensor(list(b"ACGT"), dtype=torch.uint8, device=dev)
+    q_seq = torch.empty(n_pairs * length, dtype=torch.uint8, device=dev)
+    d_parts, d_lens = [], []
+    thr = float(delta)
+    for p0 in range(0, n_pairs, chunk):
+        p1 = min(n_pairs, p0 + chunk)
+        P = p1 - p0
+        idx = torch.arange(p0 * length, p1 * length, dtype=torch.int64, device=dev)
+        q = bases[_shr(splitmix64_torch(seed, idx), 62)].view(P, length)
+        q_seq[p0 * length:p1 * length] = q.reshape(-1)
+        # mutate(q_k, delta, seed=k): one stream of 3*length outputs per pair
+        ks = torch.arange(p0, p1, dtype=torch.int64, device=dev).view(P, 1)
+        j = torch.arange(length, dtype=torch.int64, device=dev).view(1, length)
+        u = _shr(splitmix64_torch(ks, j), 11).to(torch.float64) / float(1 << 53)
+        ev = _shr(splitmix64_torch(ks, j + length), 62)
+        rb = _shr(splitmix64_torch(ks, j + 2 * length), 60)
+        del j
+        hit = u < thr
+        del u
+        sub = hit & (ev <= 1)
+        ins = hit & (ev == 2)
+        dele = hit & (ev == 3)
+        del ev, hit
+        code = torch.searchsorted(bases, q.contiguous())
+        base = torch.where(sub, bases[(code + 1 + (rb % 3)) % 4], q)
+        del code, sub
+        cnt = torch.ones((P, length), dtype=torch.int64, device=dev)
+        cnt[ins] = 2
+        cnt[dele] = 0
+        row_len = cnt.sum(1)
+        csum = torch.cumsum(cnt, 1)
+        start = csum - cnt                                  # position within the row
+        row_off = torch.cumsum(row_len, 0) - row_len        # row start within the chunk
+        pos = start + row_off.view(P, 1)
+        out = torch.empty(int(row_len.sum()), dtype=torch.uint8, device=dev)
+        keep = cnt > 0
+        out[pos[keep]] = base[keep]
+        out[pos[ins] + 1] = bases[rb[ins] & 3]
+        d_parts.append(out)
+        d_lens.append(row_len.cpu())
+        del cnt, csum, start, pos, keep, ins, dele, rb, base, q
+    d_seq = torch.cat(d_parts) if d_parts else torch.empty(0, dtype=torch.uint8, device=dev)
+    lens = torch.cat(d_lens).numpy() if d_lens else np.zeros(0, np.int64)
+    q_off = np.arange(n_pairs + 1, dtype=np.uint64) * np.uint64(length)
+    d_off = np.zeros(n_pairs + 1, np.uint64)
+    d_off[1:] = np.cumsum(lens)
+    return q_seq, q_off, d_seq, d_off

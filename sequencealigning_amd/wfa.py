@@ -127,8 +127,7 @@ class WfaPlan:
     def execute(self, q_seq, db_seq, results, stream=None) -> None:
         ptr = lambda t: t if isinstance(t, int) else t.data_ptr()  # noqa: E731
         if stream is None:
-            import torch
-            stream = torch.cuda.current_stream(self.device).cuda_stream
+            stream = _lib.torch_stream(self.device)
         _lib.check(self._L.saln_wfa_execute(self._h, ptr(q_seq), ptr(db_seq), ptr(results),
                                             stream), "saln_wfa_execute")
 

@@ -94,8 +94,7 @@ class WfaAffinePlan:
         """d_q / d_db: device uint8 tensors (CSR bytes), d_scores: device int32[n_pairs]."""
         assert d_scores.numel() >= self.n_pairs and d_scores.dtype.itemsize == 4
         if stream is None:  # torch's current stream, like NwPlan.execute
-            import torch
-            stream = torch.cuda.current_stream(d_scores.device).cuda_stream
+            stream = _lib.torch_stream(d_scores.device)
         _lib.check(self._L.saln_wfa_affine_execute(
             self._h, C.c_void_p(d_q.data_ptr()), C.c_void_p(d_db.data_ptr()),
             C.c_void_p(d_scores.data_ptr()), C.c_void_p(stream)), "saln_wfa_affine_execute")

@@ -108,3 +108,142 @@ def test_sharded_nw_matches_single_process():
     want, want_cig = saln.nw_align_batch(queries, dbs)
     assert res == want.tolist()
     assert cig == want_cig
+
+
+class _OracleAvsaEngine:
+    """CPU stand-in for the per-rank GPU engine of ShardedAllVsAll: the
+    oracle's score + panic status of every (db, query) pair of the block, in
+    db-outer / query-inner order (test-only)."""
+
+    def __init__(self, q_seq, q_off, d_seq, d_off):
+        from oracle import refcpu
+        nq, nd = len(q_off) - 1, len(d_off) - 1
+        qs = [bytes(q_seq[int(q_off[k]):int(q_off[k + 1])]) for k in range(nq)]
+        ds = [bytes(d_seq[int(d_off[k]):int(d_off[k + 1])]) for k in range(nd)]
+        pq = [q for _ in ds for q in qs]
+        pd = [d for d in ds for _ in qs]
+        qo = np.zeros(len(pq) + 1, np.uint64); qo[1:] = np.cumsum([len(x) for x in pq])
+        do = np.zeros(len(pd) + 1, np.uint64); do[1:] = np.cumsum([len(x) for x in pd])
+        self.want = refcpu.check_pairs(b"".join(pq), qo, b"".join(pd), do, threads=2) \
+            if pq else None
+        self.cells = sum(len(q) * len(d) for q, d in zip(pq, pd))
+
+    def __call__(self, out):
+        import torch
+        if self.want is None:
+            return
+        rec = np.stack([self.want.score, np.where(self.want.panics, 2, 0).astype(np.int32)], 1)
+        out.copy_(torch.from_numpy(rec.reshape(-1)))
+
+    def close(self):
+        pass
+
+
+def _avsa_worker(rank, world, port, queries, dbs, out):
+    import torch.distributed as dist
+
+    from sequencealigning_amd.dist import nw_score_all_vs_all_sharded
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    got = nw_score_all_vs_all_sharded(queries, dbs, engine=_OracleAvsaEngine)
+    if rank == 0:
+        out.put((got[0].tolist(), got[1].tolist()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_all_vs_all_gather(world):
+    """configs[4] driver (ShardedAllVsAll) with gloo: db blocks per rank, the
+    records gathered to rank 0 equal the single-process all-vs-all (score +
+    panic status per (db, query), reference order), incl. empty records and
+    unequal blocks."""
+    from nw_check import rand_seq
+    from oracle import refcpu
+    rng = np.random.default_rng(8)
+    queries = [rand_seq(rng, int(n)) for n in [0, 3, 40, 150, 151, 90]]
+    dbs = [rand_seq(rng, int(n)) for n in [120, 0, 7, 150, 33, 200, 1, 64, 149]]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_avsa_worker, args=(r, world, port, queries, dbs, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    scores, status = q.get(timeout=180)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert np.asarray(scores).shape == (len(dbs), len(queries))
+    for di, d in enumerate(dbs):
+        for qi, qq in enumerate(queries):
+            o = refcpu.nw(qq, d, literal_dfs=False)
+            assert scores[di][qi] == o.score, (di, qi)
+            assert (status[di][qi] == 2) == o.panics, (di, qi)
+
+
+def _avsa_gpu_worker(rank, world, port, queries, dbs, out):
+    import torch
+    import torch.distributed as dist
+
+    from sequencealigning_amd.dist import nw_score_all_vs_all_sharded
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    got = nw_score_all_vs_all_sharded(queries, dbs, device=0)
+    if rank == 0:
+        out.put((got[0], got[1]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_sharded_all_vs_all_gpu_matches_single_process():
+    """Two ranks (gloo gather; both on cuda:0 of the box) running libsaln's
+    score-only all-vs-all on their db blocks give bit-for-bit the
+    single-process nw_score_all_vs_all, and a sample equals the oracle."""
+    import sequencealigning_amd as saln
+    from nw_check import rand_seq
+    from oracle import refcpu
+    rng = np.random.default_rng(21)
+    queries = [rand_seq(rng, int(n)) for n in rng.integers(100, 161, 40)] + [b"", b"ACGTN" * 60]
+    dbs = [rand_seq(rng, int(n)) for n in rng.integers(100, 161, 57)] + [b"", b"A" * 700]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_avsa_gpu_worker, args=(r, 2, port, queries, dbs, q))
+             for r in range(2)]
+    for p in procs:
+        p.start()
+    scores, status = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    want_s, want_st = saln.nw_score_all_vs_all(queries, dbs)
+    assert np.array_equal(scores, want_s) and np.array_equal(status, want_st)
+    for _ in range(30):
+        di, qi = int(rng.integers(len(dbs))), int(rng.integers(len(queries)))
+        o = refcpu.nw(queries[qi], dbs[di], literal_dfs=False)
+        assert scores[di, qi] == o.score and (status[di, qi] == 2) == o.panics
+
+
+def test_sharded_all_vs_all_without_process_group():
+    """One process, no process group (bench.py at N = 1): a single block, the
+    gather is a no-op, results and lookups in the reference order."""
+    from oracle import refcpu
+    from sequencealigning_amd.dist import ShardedAllVsAll
+    from sequencealigning_amd.nw import pack_csr
+    queries, dbs = [b"ACGT", b"AAC", b""], [b"AC", b"", b"GGTA", b"T"]
+    q, qo = pack_csr(queries)
+    d, do = pack_csr(dbs)
+    s = ShardedAllVsAll(q, qo, d, do, engine=_OracleAvsaEngine)
+    s.execute()
+    sc, st = s.result()
+    for di, dd in enumerate(dbs):
+        for qi, qq in enumerate(queries):
+            o = refcpu.nw(qq, dd, literal_dfs=False)
+            assert sc[di, qi] == o.score and (st[di, qi] == 2) == o.panics
+    ls, lst = s.lookup([3, 0, 2], [2, 1, 0])
+    assert ls.tolist() == [sc[3, 2], sc[0, 1], sc[2, 0]]

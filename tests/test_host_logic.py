@@ -67,3 +67,16 @@ def test_mutate_matches_per_base_definition():
     for seed, n, delta in [(1, 0, 0.1), (2, 1, 0.9), (3, 2000, 0.05), (4, 3000, 0.5)]:
         q = synth.random_bases(seed, n).tobytes()
         assert synth.mutate(q, delta, seed) == slow(q, delta, seed)
+
+
+def test_torch_mut_pairs_equal_numpy_generators():
+    """synth.mut_pairs_torch (bench's configs[2] generator, run on the GPU
+    there) is bit-identical to the numpy random_bases + mutate pairs."""
+    from sequencealigning_amd import synth
+    n, L = 23, 300
+    qs, qo, ds, do = synth.mut_pairs_torch(n, L, 0.05, 0x5EED0003, "cpu", chunk=7)
+    allq = synth.random_bases(0x5EED0003, n * L).tobytes()
+    for k in range(n):
+        q = allq[k * L:(k + 1) * L]
+        assert bytes(qs[int(qo[k]):int(qo[k + 1])].numpy()) == q
+        assert bytes(ds[int(do[k]):int(do[k + 1])].numpy()) == synth.mutate(q, 0.05, seed=k)
