@@ -67,8 +67,11 @@ typedef struct {
     int32_t status;     /* SALN_OK | SALN_REF_PANIC_BOUNDARY | SALN_NOT_IMPLEMENTED */
     uint32_t cigar_len; /* RLE ops written for the first printed alignment (0 if none) */
     uint8_t end_states; /* bit0 M, bit1 I, bit2 D: end states equal to score (:251-280) */
-    uint8_t printed;    /* 1 if the reference prints at least one alignment block */
-    uint8_t flags;      /* internal diagnostics (0) */
+    uint8_t printed;    /* 1 if the reference prints at least one alignment block; 0 when
+                           its DFS panics first or every co-optimal path is
+                           sentinel-rooted (dropped silently, :172-216) */
+    uint8_t flags;      /* bit 3: score-only result; bit 1: internal inconsistency
+                           (never set); all other bits 0 */
     uint8_t reserved;
 } saln_nw_result;
 

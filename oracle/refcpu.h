@@ -98,6 +98,15 @@ int ref_nw_check_pairs_mt(const uint8_t *qs, const uint64_t *q_off, const uint8_
 int ref_nw_score_linear(const uint8_t *q, size_t lq, const uint8_t *d, size_t ld, int threads,
                         int32_t *score, uint8_t *end_states, int *panics);
 
+/* ref_nw_score_linear plus the first event of the reference DFS over stored
+ * parent sets (1 B per cell of host memory): ops (forward, '=' 'X' 'I' 'D')
+ * of the first printed alignment, *ops_len = -1 if nothing is printed (the
+ * DFS panics first, or every path is sentinel-rooted); *dead_nodes = (cell,
+ * state) nodes the DFS exhausted without a terminal before that event. */
+int ref_nw_first_linear(const uint8_t *q, size_t lq, const uint8_t *d, size_t ld, int threads,
+                        int32_t *score, uint8_t *end_states, int *panics, char *ops,
+                        size_t ops_cap, int64_t *ops_len, uint64_t *dead_nodes);
+
 /* FASTA parser restatement (parse.rs:54-99) on an in-memory buffer.
  * has_valid_ext: result of the extension check (:55-60) done by the caller.
  * Records are returned as a flat byte stream: for each record

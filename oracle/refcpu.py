@@ -60,6 +60,10 @@ def lib():
                                             C.POINTER(C.c_uint64), C.c_uint64,
                                             C.POINTER(C.c_uint64), C.POINTER(C.c_int32), u8p, u8p,
                                             C.POINTER(C.c_int32), C.POINTER(C.c_uint32), C.c_int]
+        L.ref_nw_first_linear.argtypes = [u8p, C.c_size_t, u8p, C.c_size_t, C.c_int,
+                                          C.POINTER(C.c_int32), u8p, C.POINTER(C.c_int),
+                                          C.c_char_p, C.c_size_t, C.POINTER(C.c_int64),
+                                          C.POINTER(C.c_uint64)]
         L.ref_nw_score_linear.argtypes = [u8p, C.c_size_t, u8p, C.c_size_t, C.c_int,
                                           C.POINTER(C.c_int32), u8p, C.POINTER(C.c_int)]
         L.ref_parse_fasta.argtypes = [u8p, C.c_size_t, C.c_int, u8p, C.c_size_t,
@@ -153,6 +157,26 @@ def nw_score_linear(query: bytes, db: bytes, threads: int = 0) -> tuple[int, int
                                  C.byref(sc), C.byref(es), C.byref(pan)) != 0:
         raise MemoryError("oracle linear fill")
     return sc.value, es.value, bool(pan.value)
+
+
+def nw_first_linear(query: bytes, db: bytes, threads: int = 0):
+    """(score, end_states, panics, first_ops or None, dead_nodes) of one pair:
+    the linear-memory fill keeping 1 B of parent sets per cell and the
+    reference DFS's first event over them (reflinear.c), for pairs too large
+    for the full-matrix oracle; dead_nodes > 0 means the DFS backtracked out
+    of sentinel-rooted subtrees before its first event."""
+    if threads <= 0:
+        threads = min(16, os.cpu_count() or 1)
+    sc, es, pan = C.c_int32(0), C.c_uint8(0), C.c_int(0)
+    cap = len(query) + len(db) + 1
+    ops = C.create_string_buffer(cap)
+    olen, dead = C.c_int64(0), C.c_uint64(0)
+    if lib().ref_nw_first_linear(_u8(query), len(query), _u8(db), len(db), threads, C.byref(sc),
+                                 C.byref(es), C.byref(pan), ops, cap, C.byref(olen),
+                                 C.byref(dead)) != 0:
+        raise MemoryError("oracle linear first alignment")
+    first = ops.raw[:olen.value].decode() if olen.value >= 0 else None
+    return sc.value, es.value, bool(pan.value), first, dead.value
 
 
 def run_pairs(qs: bytes, q_off: np.ndarray, ds: bytes, d_off: np.ndarray, n_pairs: int,

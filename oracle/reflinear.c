@@ -14,6 +14,13 @@
  * Parallel form: the query columns are cut into T stripes, one thread each;
  * stripe t consumes the (M, I, D, bits) of the column left of it row by row
  * as stripe t-1 publishes them (a pipeline down the rows).
+ *
+ * ref_nw_first_linear additionally keeps every cell's parent sets (one byte:
+ * the refcpu.h pM / pI / pD bits, 1 B per cell, 10 GB at configs[3]) and runs
+ * the reference DFS (:246-329) over them with a "no terminal below" memo per
+ * (cell, state): the first event in DFS order (a printed block at the origin,
+ * or a boundary panic) and the first printed alignment, for pairs whose
+ * three full i32 matrices would not fit (ref_nw_dag_summary's statement).
  */
 #define _POSIX_C_SOURCE 200809L
 #include "refcpu.h"
@@ -42,6 +49,7 @@ typedef struct {
     lin_cell **col;         /* col[t][i]: column c0(t)-1 at row i, written by stripe t-1 */
     _Atomic size_t *prog;   /* prog[t]: rows of col[t] published */
     lin_cell end;           /* (ld, lq) */
+    uint8_t *codes;         /* optional: parent sets per cell, row-major (ld+1) x (lq+1) */
 } lin_job;
 
 typedef struct {
@@ -130,6 +138,17 @@ static void *lin_stripe(void *vp) {
             if (c.d == up.m + GO + GE && (up.f & 1)) f |= 4;
             c.f = f;
             cur[k] = c;
+            if (J->codes) { /* refcpu.h bit conventions, push order */
+                uint8_t b = 0;
+                if (c.m == dg.m + s) b |= 1;
+                if (c.m == dg.i + s) b |= 2;
+                if (c.m == dg.d + s) b |= 4;
+                if (c.i == lf.i + GE) b |= 8;
+                if (c.i == lf.m + GO + GE) b |= 16;
+                if (c.d == up.d + GE) b |= 32;
+                if (c.d == up.m + GO + GE) b |= 64;
+                J->codes[i * (J->lq + 1) + c0 + k - 1] = b;
+            }
         }
         if (out) {
             out[i] = cur[n];
@@ -146,14 +165,20 @@ static void *lin_stripe(void *vp) {
     return NULL;
 }
 
-int ref_nw_score_linear(const uint8_t *q, size_t lq, const uint8_t *d, size_t ld, int threads,
-                        int32_t *score, uint8_t *end_states, int *panics) {
+static int lin_run(lin_job *Jp, const uint8_t *q, size_t lq, const uint8_t *d, size_t ld,
+                   int threads, uint8_t *codes, int32_t *score, uint8_t *end_states, int *panics) {
     lin_job J;
     memset(&J, 0, sizeof(J));
     J.q = q;
     J.d = d;
     J.lq = lq;
     J.ld = ld;
+    J.codes = codes;
+    if (codes) { /* boundary parent sets (:183-216): D[0][j] <- D[0][j-1], I[i][0] <- I[i-1][0] */
+        codes[0] = 0;
+        for (size_t j = 1; j <= lq; ++j) codes[j] = 32;
+        for (size_t i = 1; i <= ld; ++i) codes[i * (lq + 1)] = 8;
+    }
     if (threads < 1) threads = 1;
     size_t w = (lq + (size_t)threads - 1) / (size_t)threads;
     if (w < 256) w = 256;
@@ -196,5 +221,109 @@ int ref_nw_score_linear(const uint8_t *q, size_t lq, const uint8_t *d, size_t ld
     *score = h;
     *end_states = e;
     *panics = pan;
+    if (Jp) *Jp = J;
     return 0;
+}
+
+int ref_nw_score_linear(const uint8_t *q, size_t lq, const uint8_t *d, size_t ld, int threads,
+                        int32_t *score, uint8_t *end_states, int *panics) {
+    return lin_run(NULL, q, lq, d, ld, threads, NULL, score, end_states, panics);
+}
+
+/* ---- the reference DFS over stored parent sets, first event only ---- */
+enum { LS_M = 0, LS_I = 1, LS_D = 2 };
+typedef struct {
+    uint32_t x, y;
+    uint8_t st, np, next;
+    uint8_t ps[3];
+} lin_frame;
+
+/* parents of (st, x, y) in pop order (reverse of the push order :287-328) */
+static int lin_parents(const uint8_t *codes, size_t W, int st, size_t x, size_t y, uint8_t *ps) {
+    const uint8_t b = codes[x * W + y];
+    int n = 0;
+    if (st == LS_M) { /* push M, I, D (:120-153) -> pop D, I, M */
+        if (b & 4) ps[n++] = LS_D;
+        if (b & 2) ps[n++] = LS_I;
+        if (b & 1) ps[n++] = LS_M;
+    } else if (st == LS_I) { /* push ext (I), open (M) (:108-119) -> pop open first */
+        if (b & 16) ps[n++] = LS_M;
+        if (b & 8) ps[n++] = LS_I;
+    } else { /* push ext (D), open (M) (:96-107) */
+        if (b & 64) ps[n++] = LS_M;
+        if (b & 32) ps[n++] = LS_D;
+    }
+    return n;
+}
+
+int ref_nw_first_linear(const uint8_t *q, size_t lq, const uint8_t *d, size_t ld, int threads,
+                        int32_t *score, uint8_t *end_states, int *panics, char *ops,
+                        size_t ops_cap, int64_t *ops_len, uint64_t *dead_nodes) {
+    const size_t W = lq + 1, n = (ld + 1) * W;
+    uint8_t *codes = (uint8_t *)malloc(n);
+    uint8_t *dead = (uint8_t *)calloc(n, 1); /* bit st: (cell, st) explored, no terminal */
+    lin_frame *stk = (lin_frame *)malloc((lq + ld + 2) * sizeof(lin_frame));
+    if (!codes || !dead || !stk) {
+        free(codes);
+        free(dead);
+        free(stk);
+        return -1;
+    }
+    int rc = lin_run(NULL, q, lq, d, ld, threads, codes, score, end_states, panics);
+    *ops_len = -1;
+    uint64_t ndead = 0;
+    if (rc == 0) {
+        const uint8_t es = *end_states;
+        const int order[3] = {LS_D, LS_M, LS_I}; /* end states pop order (:251-280) */
+        const uint8_t bit[3] = {4, 1, 2};
+        int found = 0; /* 1 origin, 2 panic */
+        size_t top = 0;
+        for (int e = 0; e < 3 && !found; ++e) {
+            if (!(es & bit[e])) continue;
+            top = 0;
+            lin_frame f0 = {(uint32_t)ld, (uint32_t)lq, (uint8_t)order[e], 0, 0, {0, 0, 0}};
+            f0.np = 255; /* not yet visited */
+            stk[top++] = f0;
+            while (top && !found) {
+                lin_frame *f = &stk[top - 1];
+                if (f->np == 255) { /* first visit (:282-303) */
+                    const size_t x = f->x, y = f->y;
+                    if (x == 0 && y == 0) { found = 1; break; } /* printed block :283-286 */
+                    if (dead[x * W + y] & (1u << f->st)) { --top; continue; }
+                    f->np = (uint8_t)lin_parents(codes, W, f->st, x, y, f->ps);
+                    f->next = 0;
+                    /* a boundary parent access panics (:299 seq2[x-1], :303 seq1[y-1]) */
+                    const int bad = f->st == LS_M ? (x == 0 || y == 0)
+                                  : f->st == LS_D ? x == 0 : y == 0;
+                    if (f->np && bad) { found = 2; break; }
+                }
+                if (f->next < f->np) {
+                    const uint8_t ps = f->ps[f->next++];
+                    lin_frame c = {f->x, f->y, ps, 255, 0, {0, 0, 0}};
+                    if (f->st == LS_M) { c.x -= 1; c.y -= 1; }
+                    else if (f->st == LS_I) c.y -= 1;
+                    else c.x -= 1;
+                    stk[top++] = c;
+                } else {
+                    dead[(size_t)f->x * W + f->y] |= (uint8_t)(1u << f->st);
+                    ++ndead;
+                    --top;
+                }
+            }
+        }
+        if (found == 1) { /* stack bottom = end cell = last column; the origin frame on top */
+            const size_t len = top - 1;
+            for (size_t k = 0; k < len && k < ops_cap; ++k) {
+                const lin_frame *f = &stk[len - 1 - k];
+                ops[k] = f->st == LS_M ? (q[f->y - 1] == d[f->x - 1] ? '=' : 'X')
+                       : f->st == LS_I ? 'I' : 'D';
+            }
+            *ops_len = (int64_t)len;
+        }
+    }
+    if (dead_nodes) *dead_nodes = ndead;
+    free(codes);
+    free(dead);
+    free(stk);
+    return rc;
 }

@@ -114,58 +114,12 @@ static int run_batch(saln_context *ctx, const uint8_t *q_seq, const uint64_t *q_
         }
     }
     clk.mark("scatter");
-    // per-pair masks are needed for host fix-ups (sentinel dead ends) and
-    // for the callers that render reference text.
-    std::vector<char> need(n_pairs, 0);
-    bool any = masks_out != nullptr;
-    for (uint64_t k = 0; k < n_pairs; ++k)
-        if (results[k].flags & 1) need[k] = 1, any = true;
-    if (any) {
-        // Sentinel dead ends need the full parent sets: re-fill just those
-        // pairs with full codes unless the main plan already has them.
-        PlanGuard g2;
-        std::vector<uint32_t> pq2, pd2, idx2(n_pairs, 0);
-        const saln_nw_plan *src = g.p;
-        if (!masks_out) {
-            for (uint64_t k = 0; k < n_pairs; ++k) {
-                if (!need[k]) continue;
-                idx2[k] = (uint32_t)pq2.size();
-                pq2.push_back((uint32_t)(pair_q ? pair_q[k] : k % n_q));
-                pd2.push_back((uint32_t)(pair_db ? pair_db[k] : k / n_q));
-            }
-            rc = saln_nw_plan_create(ctx, q_off, n_q, db_off, n_db, pq2.data(), pd2.data(),
-                                     pq2.size(), mode, scoring, &g2.p);
-            if (rc != SALN_OK) return rc;
-            plan_set_full_codes(g2.p, true);
-            DevBuf dr2(ctx);
-            TRY_HIP(dr2.alloc(pq2.size() * sizeof(saln_nw_result)));
-            rc = saln_nw_execute(g2.p, (const uint8_t *)dq.p, (const uint8_t *)dd.p,
-                                 (saln_nw_result *)dr2.p, nullptr, nullptr);
-            if (rc != SALN_OK) return rc;
-            TRY_HIP(hipDeviceSynchronize());
-            src = g2.p;
-        }
-        if (masks_out) masks_out->resize(n_pairs);
+    // callers that render reference text get every pair's full parent codes
+    if (masks_out) {
+        masks_out->resize(n_pairs);
         for (uint64_t k = 0; k < n_pairs; ++k) {
-            if (!need[k] && !masks_out) continue;
-            PairMask m;
-            rc = plan_pair_mask(src, masks_out ? k : idx2[k], &m);
+            rc = plan_pair_mask(g.p, k, &(*masks_out)[k]);
             if (rc != SALN_OK) return rc;
-            if (need[k]) {
-                const uint64_t qi = pair_q ? pair_q[k] : k % n_q;
-                const uint64_t di = pair_db ? pair_db[k] : k / n_q;
-                const HostMask hm(m, (uint32_t)(q_off[qi + 1] - q_off[qi]),
-                                  (uint32_t)(db_off[di + 1] - db_off[di]),
-                                  scoring_or_default(scoring));
-                std::vector<uint32_t> c;
-                const bool printed = first_alignment(hm, q_seq + q_off[qi], db_seq + db_off[di], &c);
-                results[k].printed = printed ? 1 : 0;
-                results[k].cigar_len = printed ? (uint32_t)c.size() : 0;
-                if (cigar)
-                    std::copy(c.begin(), c.end(), cigar + (cigar_off ? cigar_off[k] : coff[k]));
-                results[k].flags &= (uint8_t)~1u;
-            }
-            if (masks_out) (*masks_out)[k] = std::move(m);
         }
     }
     clk.mark("fixups");

@@ -8,6 +8,18 @@
 // flags of the tied maxima, which is exactly the "panic reachable" closure of
 // the reference's DFS (:281-329).  Constants are added scaled by 2, which
 // keeps the flag.  Equality with the max is tested against H' & ~1.
+//
+// The i32 fills (lanes, column stripes) carry a second, nested flag:
+// V'' = 4V + 2a + p, a = 1 iff a DFS terminal (the origin, :283-286, or a
+// panic node) is reachable ("alive").  Paths into the sentinel-valued roots
+// M[0][j>=1], I[0][j], M[i>=1][0], D[i][0] (no parents, :172-216) are dead:
+// the DFS drops them silently.  p implies a, so max() over (V, a, p) ORs both
+// flags.  Walk codes test ties against H'' & ~1: among the tied parents the
+// alive ones, if any; the greedy walk over those is the reference DFS's
+// first path even where the sentinel competes (x + y > ~5,450).  Full codes
+// (the reference's parent sets) test against & ~3.  A pair is sentinel-free
+// (every maximum real, every cell alive) while the boundary values of its
+// last column and row stay above the sentinel: then V' = 2V + p suffices.
 #pragma once
 #include <stdint.h>
 
@@ -118,7 +130,51 @@ SALN_HD int32_t is_col1(const Scoring &s, uint32_t i) {
     return imax(2 * kSentinel + 2 * s.gap_open, 2 * i_col0(s, i) + 1) + 2 * s.gap_extend;
 }
 
-// argmax-set bits of boundary cells.
+// A pair whose boundary row / column never falls to the sentinel: no
+// sentinel-derived value is ever a maximum, every path ends at the origin or
+// a panic node (the packed fills and the packed stripes take only these).
+SALN_HD bool sentinel_free(const Scoring &s, uint32_t len_q, uint32_t len_db) {
+    const int32_t floor = kSentinel + imax(0, s.gap_open);  // also M[0][j] + open (D row 1)
+    return (len_q == 0 || d_row0(s, len_q) > floor) && (len_db == 0 || i_col0(s, len_db) > floor);
+}
+
+// The i32 fills' V'' = 4V + 2a + p boundary values (origin alive, row-0 D and
+// column-0 I alive panic nodes, the sentinel roots dead).
+SALN_HD int32_t hs4_row0(const Scoring &s, uint32_t j) {
+    return j == 0 ? 2 : imax(4 * kSentinel, 4 * d_row0(s, j) + 3);
+}
+SALN_HD int32_t hs4_col0(const Scoring &s, uint32_t i) {
+    return i == 0 ? 2 : imax(4 * kSentinel, 4 * i_col0(s, i) + 3);
+}
+SALN_HD int32_t ds4_row1(const Scoring &s, uint32_t j) {
+    return imax(4 * kSentinel + 4 * s.gap_open, 4 * d_row0(s, j) + 3) + 4 * s.gap_extend;
+}
+SALN_HD int32_t is4_col1(const Scoring &s, uint32_t i) {
+    return imax(4 * kSentinel + 4 * s.gap_open, 4 * i_col0(s, i) + 3) + 4 * s.gap_extend;
+}
+// V'' -> V' (2V + p), the form the walkers and result kernels read.
+SALN_HD int32_t x4_to_x2(int32_t v) { return ((v >> 2) << 1) | (v & 1); }
+
+// Walk-code view of the boundary cells' bits: among tied candidates the
+// alive ones (the sentinel roots are dead, row-0 D / column-0 I alive).
+SALN_HD uint8_t argmax_row0_walk(const Scoring &s, uint32_t j) {
+    if (j == 0) return kArgM;
+    return d_row0(s, j) >= kSentinel ? kArgD : (uint8_t)(kArgM | kArgI);
+}
+SALN_HD uint8_t argmax_col0_walk(const Scoring &s, uint32_t i) {
+    if (i == 0) return kArgM;
+    return i_col0(s, i) >= kSentinel ? kArgI : (uint8_t)(kArgM | kArgD);
+}
+SALN_HD uint8_t ibits_col1_walk(const Scoring &s, uint32_t i) {  // open = M[i][0]: dead
+    const int32_t ext = i_col0(s, i), open = kSentinel + s.gap_open;
+    return (uint8_t)((ext >= open ? 1 : 0) | (open > ext ? 2 : 0));
+}
+SALN_HD uint8_t dbits_row1_walk(const Scoring &s, uint32_t j) {  // open = M[0][j]: dead
+    const int32_t ext = d_row0(s, j), open = kSentinel + s.gap_open;
+    return (uint8_t)((ext >= open ? 1 : 0) | (open > ext ? 2 : 0));
+}
+
+// argmax-set bits of boundary cells (the reference's tie sets).
 SALN_HD uint8_t argmax_row0(const Scoring &s, uint32_t j) {
     if (j == 0) return kArgM;
     const int32_t dv = d_row0(s, j), h = imax(kSentinel, dv);

@@ -257,10 +257,13 @@ int saln_nw_plan_create(saln_context *ctx, const uint64_t *q_off, uint64_t n_q,
     }
     {
         uint64_t waves = 0;  // stripe waves of the plan
-        for (uint32_t r = 0; r < p->var_count[kStripeVariant]; ++r)
-            waves += variant_geom(kStripeVariant)
-                         .n_chunks(p->h_pairs[p->var_first[kStripeVariant] + r].len_q);
-        p->stripe_pk = waves > 0 && stripe_packed(p->sc, waves);
+        bool free_all = true;  // the packed stripes carry no alive flag (nw_common.hpp)
+        for (uint32_t r = 0; r < p->var_count[kStripeVariant]; ++r) {
+            const NwPairDesc &d = p->h_pairs[p->var_first[kStripeVariant] + r];
+            waves += variant_geom(kStripeVariant).n_chunks(d.len_q);
+            free_all = free_all && sentinel_free(p->sc, d.len_q, d.len_db);
+        }
+        p->stripe_pk = waves > 0 && free_all && stripe_packed(p->sc, waves);
     }
     // Mask packs: up to 64 consecutive pairs of a variant (one traceback
     // wave) with interleaved segments (nw_common.hpp Geom), unless padding

@@ -76,45 +76,47 @@ struct MaskCell {
     uint32_t bs;
     uint64_t cs;
     Scoring sc;
-    // codes are stored inverted (bit set = parent absent)
+    // codes are stored inverted (bit set = parent absent); bit 7 = q == d
     __device__ uint8_t byte(uint32_t i, uint32_t j) const { return m[g.cell(i, j, rs, bs, cs)] ^ 0x7F; }
+    // walk-code view: boundary cells from the alive-preferring formulas
     __device__ uint8_t argmax(uint32_t i, uint32_t j) const {
-        if (i == 0) return argmax_row0(sc, j);
-        if (j == 0) return argmax_col0(sc, i);
+        if (i == 0) return argmax_row0_walk(sc, j);
+        if (j == 0) return argmax_col0_walk(sc, i);
         return byte(i, j) & 7;
     }
     __device__ uint8_t ibits(uint32_t i, uint32_t j) const {  // i, j >= 1
-        return j == 1 ? ibits_col1(sc, i) : (byte(i, j - 1) >> 3) & 3;
+        return j == 1 ? ibits_col1_walk(sc, i) : (byte(i, j - 1) >> 3) & 3;
     }
     __device__ uint8_t dbits(uint32_t i, uint32_t j) const {  // i, j >= 1
-        return i == 1 ? dbits_row1(sc, j) : (byte(i - 1, j) >> 5) & 3;
+        return i == 1 ? dbits_row1_walk(sc, j) : (byte(i - 1, j) >> 5) & 3;
     }
 };
 
 enum { kStM = 0, kStI = 1, kStD = 2 };
 enum { kEvOrigin = 0, kEvPanic = 1, kEvDead = 2 };
 
-// Canonical (first printed) alignment: the reference DFS pops end states in
-// the order D, M, I (:251-280 push I, M, D) and parents in reverse push order
-// (M: D>I>M; I: open>extend; D: open>extend).  While no sentinel cell is
-// reachable every DFS path ends at the origin or at a boundary panic node,
-// so the first path is this greedy walk.  A sentinel dead end (only possible
-// once len_q+len_db >~ 5,450) sets flags bit0 and the host redoes the walk
-// with backtracking.
-__device__ __forceinline__ void walk_pair(const NwPairDesc &p, int32_t hend,
-                                       const uint8_t *__restrict__ qs,
-                                       const uint8_t *__restrict__ ds,
-                                       const uint8_t *__restrict__ mask, Geom geo,
-                                       saln_nw_result *__restrict__ results,
-                                       uint32_t *__restrict__ cigar, Scoring sc) {
-    const uint32_t lq = p.len_q, ld = p.len_db;
-    const uint8_t *q = qs + p.q_off;
-    const uint8_t *d = ds + p.db_off;
-    const MaskCell mc{mask + p.mask_off, geo, p.mask_rs, p.mask_bs, p.mask_cs, sc};
-    const uint8_t am_end = mc.argmax(ld, lq);
-    int st = (am_end & kArgD) ? kStD : ((am_end & kArgM) ? kStM : kStI);
-    uint32_t i = ld, j = lq;
-    uint32_t *out = cigar ? cigar + p.cigar_off : nullptr;
+// End states in the order the reference DFS pops them (:251-280 push I, M, D).
+__device__ __forceinline__ int first_end_state(uint32_t es) {
+    return (es & kArgD) ? kStD : ((es & kArgM) ? kStM : kStI);
+}
+// The end states after `st` in that order (st itself and those before it removed).
+__device__ __forceinline__ uint32_t end_states_after(uint32_t es, int st) {
+    return st == kStD ? es & (kArgM | kArgI) : st == kStM ? es & kArgI : 0u;
+}
+
+struct WalkOut {
+    int ev;
+    uint32_t nops;
+};
+
+// Greedy walk from cell (i, j) in state st over walk codes (D > I > M in an M
+// cell, open > extend in I / D; the tied alive parents, nw_common.hpp), run-
+// length ops back to front into out.  '=' / 'X' from the sequences when
+// given, else from the codes' eq bit.  A walk started at an alive state ends
+// at the origin or a panic node; one started at a dead state (a sentinel-
+// rooted end state) ends at a sentinel root (kEvDead).
+__device__ WalkOut walk_greedy(const MaskCell &mc, int st, uint32_t i, uint32_t j,
+                               const uint8_t *q, const uint8_t *d, uint32_t *out) {
     uint32_t nops = 0, run_op = 0, run_len = 0;
     int ev;
     for (;;) {
@@ -122,7 +124,8 @@ __device__ __forceinline__ void walk_pair(const NwPairDesc &p, int32_t hend,
         if (st == kStM) {
             if (i == 0 && j == 0) { ev = kEvOrigin; break; }
             if (i == 0 || j == 0) { ev = kEvDead; break; }
-            op = q[j - 1] == d[i - 1] ? SALN_CIGAR_EQ : SALN_CIGAR_X;
+            const bool eq = q ? q[j - 1] == d[i - 1] : (mc.byte(i, j) >> 7) != 0;
+            op = eq ? SALN_CIGAR_EQ : SALN_CIGAR_X;
             const uint8_t a = mc.argmax(i - 1, j - 1);
             --i;
             --j;
@@ -163,15 +166,56 @@ __device__ __forceinline__ void walk_pair(const NwPairDesc &p, int32_t hend,
             out[b] = tmp;
         }
     }
+    return WalkOut{ev, nops};
+}
+
+// The reference DFS's first path from the end states `es` (the tied set),
+// tried in pop order D, M, I: the first that is not dead decides (printed at
+// the origin, or a panic with nothing printed); all dead = nothing printed.
+__device__ WalkOut walk_first(const MaskCell &mc, uint32_t es, uint32_t ld, uint32_t lq,
+                              const uint8_t *q, const uint8_t *d, uint32_t *out) {
+    WalkOut w{kEvDead, 0};
+    while (es) {
+        const int st = first_end_state(es);
+        w = walk_greedy(mc, st, ld, lq, q, d, out);
+        if (w.ev != kEvDead) break;
+        es = end_states_after(es, st);
+    }
+    return w;
+}
+
+__device__ __forceinline__ saln_nw_result make_result(int32_t hend, WalkOut w, uint32_t es) {
     saln_nw_result r;
     r.score = hend >> 1;
     r.status = (hend & 1) ? SALN_REF_PANIC_BOUNDARY : SALN_OK;
-    r.cigar_len = nops;
-    r.end_states = am_end;
-    r.printed = ev == kEvOrigin ? 1 : 0;
-    r.flags = (ev == kEvDead ? 1 : 0) | ((ev == kEvPanic && !(hend & 1)) ? 2 : 0);
+    r.cigar_len = w.nops;
+    r.end_states = (uint8_t)es;
+    r.printed = w.ev == kEvOrigin ? 1 : 0;
+    r.flags = (w.ev == kEvPanic && !(hend & 1)) ? 2 : 0;  // diagnostic: never set
     r.reserved = 0;
-    results[p.pair_id] = r;
+    return r;
+}
+
+// Canonical (first printed) alignment: the reference DFS pops end states in
+// the order D, M, I (:251-280 push I, M, D) and parents in reverse push order
+// (M: D>I>M; I: open>extend; D: open>extend).  Over walk codes (the alive
+// tied parents) the first path is this greedy walk from the first end state
+// that is not dead (walk_first).
+__device__ __forceinline__ void walk_pair(const NwPairDesc &p, int32_t hend,
+                                       const uint8_t *__restrict__ qs,
+                                       const uint8_t *__restrict__ ds,
+                                       const uint8_t *__restrict__ mask, Geom geo,
+                                       saln_nw_result *__restrict__ results,
+                                       uint32_t *__restrict__ cigar, Scoring sc) {
+    const uint32_t lq = p.len_q, ld = p.len_db;
+    const MaskCell mc{mask + p.mask_off, geo, p.mask_rs, p.mask_bs, p.mask_cs, sc};
+    // the reference's end states (true ties: boundary formulas, or the last
+    // row's codes, which the fills store unfiltered)
+    const uint8_t es = ld == 0 ? argmax_row0(sc, lq)
+                     : lq == 0 ? argmax_col0(sc, ld) : (mc.byte(ld, lq) & 7);
+    const WalkOut w = walk_first(mc, es, ld, lq, qs + p.q_off, ds + p.db_off,
+                                 cigar ? cigar + p.cigar_off : nullptr);
+    results[p.pair_id] = make_result(hend, w, es);
 }
 
 // LDS-window walker (segments of <= 16 bytes, i.e. K <= 16).  Lock-step
@@ -460,20 +504,35 @@ __device__ void walk_pair_lds(const NwPairDesc &p, int32_t hend, const uint8_t *
         ev = kEvOrigin;
     } else {
         if (st == kStM) {
-            const uint8_t a = ti == 0 ? argmax_row0(sc, tj) : argmax_col0(sc, ti);
+            const uint8_t a = ti == 0 ? argmax_row0_walk(sc, tj) : argmax_col0_walk(sc, ti);
             bst = (a & kArgD) ? kStD : ((a & kArgI) ? kStI : kStM);
         } else if (st == kStI) {
-            bst = (ibits_col1(sc, ti) & 2) ? kStM : kStI;
+            bst = (ibits_col1_walk(sc, ti) & 2) ? kStM : kStI;
         } else {
-            bst = (dbits_row1(sc, tj) & 2) ? kStM : kStD;
+            bst = (dbits_row1_walk(sc, tj) & 2) ? kStM : kStD;
         }
         if (bst == kStD && ti == 0 && tj >= 1) ev = kEvPanic;
         else if (bst == kStI && tj == 0 && ti >= 1) ev = kEvPanic;
         else ev = kEvDead;
     }
-    // CIGAR: the op stream read back in forward order (last recorded op first)
+    // the reference's end states: the last row's codes are stored unfiltered
+    const uint32_t es = (m[geo.cell(p.len_db, p.len_q, rs, bs, p.mask_cs)] ^ 0x7Fu) & 7u;
     uint32_t nops = 0;
-    if (ev == kEvOrigin) {
+    bool retried = false;
+    if (ev == kEvDead) {
+        // the first end state is sentinel-rooted (i32 lanes pairs only): the
+        // DFS goes on with the next tied end states (walk_first, byte loads)
+        const uint32_t rest = end_states_after(es, first_end_state(es));
+        if (rest) {
+            const MaskCell mc{m, geo, rs, bs, p.mask_cs, sc};
+            const WalkOut w = walk_first(mc, rest, p.len_db, p.len_q, nullptr, nullptr, out);
+            ev = w.ev;
+            nops = w.nops;
+            retried = true;
+        }
+    }
+    // CIGAR: the op stream read back in forward order (last recorded op first)
+    if (ev == kEvOrigin && !retried) {
         if (hf) counted_store(ops + wi - 1, full);
         if (sh3) counted_store(ops + wi, cur);
         asm volatile("s_waitcnt vmcnt(0)" : : : "memory");
@@ -502,14 +561,7 @@ __device__ void walk_pair_lds(const NwPairDesc &p, int32_t hend, const uint8_t *
             ++nops;
         }
     }
-    saln_nw_result r;
-    r.score = hend >> 1;
-    r.status = (hend & 1) ? SALN_REF_PANIC_BOUNDARY : SALN_OK;
-    r.cigar_len = nops;
-    r.end_states = (uint8_t)((m[geo.cell(p.len_db, p.len_q, rs, bs, p.mask_cs)] ^ 0x7Fu) & 7u);
-    r.printed = ev == kEvOrigin ? 1 : 0;
-    r.flags = (ev == kEvDead ? 1 : 0) | ((ev == kEvPanic && !(hend & 1)) ? 2 : 0);
-    r.reserved = 0;
+    saln_nw_result r = make_result(hend, WalkOut{ev, nops}, es);
 #ifdef SALN_WALK_PROF
     {
         const uint64_t tt = SALN_PROF_T() - p_t0;
@@ -658,8 +710,13 @@ __global__ __launch_bounds__(64 * NWV) void nw_traceback_coop_kernel(
     };
     int32_t i = ld, j = lq;
     load(i, j);
+    // the reference's end states (the last row's codes are unfiltered), tried
+    // in the DFS's pop order: a walk from a sentinel-rooted end state dead-ends
+    // and the next one is walked (walk_first)
     const uint32_t am_end = code(i, j) & 7u;
-    int32_t st = (am_end & kArgD) ? kStD : ((am_end & kArgM) ? kStM : kStI);
+    uint32_t es_left = am_end;
+    int32_t st = first_end_state(es_left);
+    es_left = end_states_after(es_left, st);
     uint32_t *out = cigar ? cigar + p.cigar_off : nullptr;
     uint32_t nops = 0, run_op = 0, run_len = 0;
     // The pending run is stored at out[nops] unconditionally (every lane, one
@@ -685,7 +742,15 @@ __global__ __launch_bounds__(64 * NWV) void nw_traceback_coop_kernel(
             if (st == kStM) ev = i == 0 && j == 0 ? kEvOrigin : kEvDead;
             else if (st == kStI) ev = j == 0 && i >= 1 ? kEvPanic : kEvDead;
             else ev = i == 0 && j >= 1 ? kEvPanic : kEvDead;
-            break;
+            if (ev != kEvDead || !es_left) break;
+            // dead end state: restart from the next tied end state
+            st = first_end_state(es_left);
+            es_left = end_states_after(es_left, st);
+            i = ld;
+            j = lq;
+            nops = run_op = run_len = 0;
+            load(i, j);
+            continue;
         }
         // steps l whose reads stay in the window (row / column 0 come from
         // the boundary formulas)
@@ -729,20 +794,21 @@ __global__ __launch_bounds__(64 * NWV) void nw_traceback_coop_kernel(
             const int32_t ni = i - lane - 1, nj = j - lane - 1;
             const uint32_t ce = code(i - lane, j - lane), cn = code(ni, nj);
             eq = edge ? eq0 : ce >> 7;
-            const uint32_t ab = ni == 0 ? argmax_row0(sc, (uint32_t)nj) : argmax_col0(sc, (uint32_t)ni);
+            const uint32_t ab = ni == 0 ? argmax_row0_walk(sc, (uint32_t)nj)
+                                        : argmax_col0_walk(sc, (uint32_t)ni);
             const uint32_t a = (ni == 0 || nj == 0) ? ab : cn & 7u;
             nxt = (a & kArgD) ? kStD : ((a & kArgI) ? kStI : kStM);
             stop = nxt != kStM || ni == 0 || nj == 0;
         } else if (st == kStI) {
             const int32_t cj = j - lane;
             const uint32_t cc = code(i, cj - 1);
-            const uint32_t b = cj == 1 ? ibits_col1(sc, (uint32_t)i) : (cc >> 3) & 3u;
+            const uint32_t b = cj == 1 ? ibits_col1_walk(sc, (uint32_t)i) : (cc >> 3) & 3u;
             nxt = (b & 2) ? kStM : kStI;
             stop = nxt != kStI || cj == 1;
         } else {
             const int32_t ci = i - lane;
             const uint32_t cc = code(ci - 1, j);
-            const uint32_t b = ci == 1 ? dbits_row1(sc, (uint32_t)j) : (cc >> 5) & 3u;
+            const uint32_t b = ci == 1 ? dbits_row1_walk(sc, (uint32_t)j) : (cc >> 5) & 3u;
             nxt = (b & 2) ? kStM : kStD;
             stop = nxt != kStD || ci == 1;
         }
@@ -812,14 +878,7 @@ __global__ __launch_bounds__(64 * NWV) void nw_traceback_coop_kernel(
         }
     }
     if (lane == 0) {
-        saln_nw_result r;
-        r.score = hend >> 1;
-        r.status = (hend & 1) ? SALN_REF_PANIC_BOUNDARY : SALN_OK;
-        r.cigar_len = nops;
-        r.end_states = (uint8_t)am_end;
-        r.printed = ev == kEvOrigin ? 1 : 0;
-        r.flags = (ev == kEvDead ? 1 : 0) | ((ev == kEvPanic && !(hend & 1)) ? 2 : 0);
-        r.reserved = 0;
+        saln_nw_result r = make_result(hend, WalkOut{ev, nops}, am_end);
 #ifdef SALN_COOP_PROF  // iterations, window loads, total / load clocks (>> 10)
         r.cigar_len = pf_iter;
         r.score = (int32_t)pf_load;
@@ -1352,13 +1411,18 @@ __global__ __launch_bounds__(128) void nw_fill_stripe_kernel(
     const uint32_t nch = geo.n_chunks(lq);
     const int2 *__restrict__ scr_in = c > 0 ? scratch + p.scratch_off + (uint64_t)(c - 1) * (ld + 2) : nullptr;
     int2 *__restrict__ scr_out = c + 1 < nch ? scratch + p.scratch_off + (uint64_t)c * (ld + 2) : nullptr;
-    const int32_t beta = -2 * sc.gap_extend;
-    const int32_t alpha = -2 * sc.match - beta;
-    const int32_t pen_max = 2 * (sc.match - sc.mismatch);
+    // V'' = 4V + 2a + p (nw_common.hpp): offsets and constants scaled by 4
+    const int32_t beta = -4 * sc.gap_extend;
+    const int32_t alpha = -4 * sc.match - beta;
+    const int32_t pen_max = 4 * (sc.match - sc.mismatch);
     // chars carried as c << 8: q ^ d is 0 or >= 256, so min() is the penalty
     // whenever 0 <= pen_max <= 256 (kMinPen); otherwise a select
-    const int32_t kOpen = 2 * sc.gap_open;
-    const int32_t kDstep = 2 * sc.gap_extend + alpha;
+    const int32_t kOpen = 4 * sc.gap_open;
+    const int32_t kDstep = 4 * sc.gap_extend + alpha;
+    // tie masks: walk codes keep the alive tied parents (& ~1) except on the
+    // last row, whose argmax bits only the end cell uses: the reference's
+    // end states (& ~3); full codes are the reference's parent sets
+    constexpr int32_t kTieOr = kCodes == kCodesFull ? 3 : 1;
     const uint32_t jend = lq - 1;
     const bool end_lane = jend / geo.W() == c && (uint32_t)lane == (jend % geo.W()) / K;
     const uint32_t k_end = jend % K;
@@ -1370,10 +1434,10 @@ __global__ __launch_bounds__(128) void nw_fill_stripe_kernel(
     for (int k = 0; k < K; ++k) {
         const uint32_t j = col0 + k + 1;
         qc[k] = j <= lq ? (uint32_t)q[j - 1] << 8 : 0xFFFFFF00u;
-        Hp[k] = hs_row0(sc, j) + beta * (int32_t)j;
-        Dn[k] = ds_row1(sc, j) + alpha + beta * (int32_t)j;
+        Hp[k] = hs4_row0(sc, j) + beta * (int32_t)j;
+        Dn[k] = ds4_row1(sc, j) + alpha + beta * (int32_t)j;
     }
-    int32_t hd = hs_row0(sc, col0) + beta * (int32_t)col0;
+    int32_t hd = hs4_row0(sc, col0) + beta * (int32_t)col0;
     int32_t pubF = 0, pubH = 0;
     // db chars: lane 0 needs d[t] at step t (wave-uniform).  Steps run in
     // groups of four; a group's four chars d[t..t+3] are one scalar word
@@ -1427,8 +1491,8 @@ __global__ __launch_bounds__(128) void nw_fill_stripe_kernel(
                             const int32_t M = Mv[k], D = Dv[k];
                             const int32_t H = max(M, max(I, D));
                             const int32_t tO = M + kOpen;
-                            const int32_t Hc = H & ~1;
-                            const int32_t tOr = tO | 1;
+                            const int32_t Hc = H & (kCodes == kCodesFull || r == (int)ld ? ~3 : ~1);
+                            const int32_t tOr = tO | kTieOr;
                             sg[0][k] = (uint32_t)(M - Hc);
                             sg[1][k] = (uint32_t)(I - Hc);
                             sg[2][k] = (uint32_t)(D - Hc);
@@ -1436,7 +1500,7 @@ __global__ __launch_bounds__(128) void nw_fill_stripe_kernel(
                             sg[6][k] = (uint32_t)(tOr - D);
                             sg[7][k] = (qc[k] ^ dc) - 1u;  // sign <=> q == d
                             if constexpr (kCodes == kCodesFull) {
-                                const int32_t tOc = tO & ~1;
+                                const int32_t tOc = tO & ~3;
                                 sg[3][k] = (uint32_t)(I - tOc);
                                 sg[5][k] = (uint32_t)(D - tOc);
                             } else {
@@ -1469,8 +1533,8 @@ __global__ __launch_bounds__(128) void nw_fill_stripe_kernel(
         int32_t bF, bH;
         const uint32_t rr = (uint32_t)t + 1;  // lane 0's row
         if (c == 0) {
-            bF = is_col1(sc, rr) + alpha * (int32_t)rr + beta;
-            bH = hs_col0(sc, rr) + alpha * (int32_t)rr;
+            bF = is4_col1(sc, rr) + alpha * (int32_t)rr + beta;
+            bH = hs4_col0(sc, rr) + alpha * (int32_t)rr;
         } else {
             if (kGroupStart && (rr - 1) % kPub == 0 && rr <= ld) {  // new 32-row block of the left column
                 const uint32_t row = rr + (uint32_t)lane;
@@ -1503,6 +1567,7 @@ __global__ __launch_bounds__(128) void nw_fill_stripe_kernel(
         const int32_t inH = shr1<G>(bH, pubH);
         if (r >= 1 && r <= (int)ld) {
             int32_t F = inF;
+            const int32_t hm = kCodes == kCodesFull || r == (int)ld ? ~3 : ~1;
             uint32_t sg[8][4];
             int32_t Mk[K], Dk[K];  // kSplit: the coder wave's inputs
             int32_t diag = hd;  // H~(r-1, c-1) of column k
@@ -1520,8 +1585,8 @@ __global__ __launch_bounds__(128) void nw_fill_stripe_kernel(
                     Mk[k] = M;
                     Dk[k] = D;
                 } else if constexpr (kCodes != kCodesNone) {
-                    const int32_t Hc = H & ~1;
-                    const int32_t tOr = tO | 1;
+                    const int32_t Hc = H & hm;
+                    const int32_t tOr = tO | kTieOr;
                     sg[0][k] = (uint32_t)(M - Hc);
                     sg[1][k] = (uint32_t)(I - Hc);
                     sg[2][k] = (uint32_t)(D - Hc);
@@ -1529,7 +1594,7 @@ __global__ __launch_bounds__(128) void nw_fill_stripe_kernel(
                     sg[6][k] = (uint32_t)(tOr - D);
                     sg[7][k] = x - 1u;  // sign <=> q == d
                     if constexpr (kCodes == kCodesFull) {
-                        const int32_t tOc = tO & ~1;
+                        const int32_t tOc = tO & ~3;
                         sg[3][k] = (uint32_t)(I - tOc);
                         sg[5][k] = (uint32_t)(D - tOc);
                     } else {
@@ -1612,7 +1677,7 @@ __global__ __launch_bounds__(128) void nw_fill_stripe_kernel(
 #pragma unroll
         for (int k = 0; k < K; ++k)
             if ((uint32_t)k == k_end) e = (ntail & 1) ? HpB[k] : Hp[k];
-        end_h[wk.x] = e - alpha * (int32_t)ld - beta * (int32_t)lq;
+        end_h[wk.x] = x4_to_x2(e - alpha * (int32_t)ld - beta * (int32_t)lq);
     }
     if (failed && lane == 0) atomicOr(err, 1u);
 }
@@ -1644,11 +1709,13 @@ __global__ __launch_bounds__(256) void nw_fill_lanes_kernel(
     uint8_t *__restrict__ mk = mask + p.mask_off;
     int2 *__restrict__ scr = scratch + p.scratch_off;
     const uint32_t nch = geo.n_chunks(lq);
-    const int32_t beta = -2 * sc.gap_extend;
-    const int32_t alpha = -2 * sc.match - beta;
-    const int32_t pen_max = 2 * (sc.match - sc.mismatch);
-    const int32_t kOpen = 2 * sc.gap_open;
-    const int32_t kDstep = 2 * sc.gap_extend + alpha;
+    // V'' = 4V + 2a + p (nw_common.hpp); tie masks as in the stripe fill
+    const int32_t beta = -4 * sc.gap_extend;
+    const int32_t alpha = -4 * sc.match - beta;
+    const int32_t pen_max = 4 * (sc.match - sc.mismatch);
+    const int32_t kOpen = 4 * sc.gap_open;
+    const int32_t kDstep = 4 * sc.gap_extend + alpha;
+    constexpr int32_t kTieOr = kCodes == kCodesFull ? 3 : 1;
     const uint32_t jend = lq - 1;
     const uint32_t c_end = jend / geo.W(), l_end = (jend % geo.W()) / K, k_end = jend % K;
     extern __shared__ uint8_t drow8[];  // kStaged: [GPB][G + ld_max + G] db chars
@@ -1670,10 +1737,10 @@ __global__ __launch_bounds__(256) void nw_fill_lanes_kernel(
         for (int k = 0; k < K; ++k) {
             const uint32_t j = col0 + k + 1;
             qc[k] = j <= lq ? (uint32_t)q[j - 1] << 8 : 0xFFFFFF00u;
-            Hp[k] = hs_row0(sc, j) + beta * (int32_t)j;
-            Dn[k] = ds_row1(sc, j) + alpha + beta * (int32_t)j;
+            Hp[k] = hs4_row0(sc, j) + beta * (int32_t)j;
+            Dn[k] = ds4_row1(sc, j) + alpha + beta * (int32_t)j;
         }
-        int32_t hd = hs_row0(sc, col0) + beta * (int32_t)col0;
+        int32_t hd = hs4_row0(sc, col0) + beta * (int32_t)col0;
         int32_t pubF = 0, pubH = 0;
         int32_t dnext = (!kStaged && lane == 0) ? (int32_t)d[0] : 0;
         int2 bnext = make_int2(0, 0);
@@ -1694,8 +1761,8 @@ __global__ __launch_bounds__(256) void nw_fill_lanes_kernel(
             int32_t bF, bH;
             const int32_t rr = t + 1;  // lane 0's row
             if (c == 0) {
-                bF = is_col1(sc, (uint32_t)rr) + alpha * rr + beta;
-                bH = hs_col0(sc, (uint32_t)rr) + alpha * rr;
+                bF = is4_col1(sc, (uint32_t)rr) + alpha * rr + beta;
+                bH = hs4_col0(sc, (uint32_t)rr) + alpha * rr;
             } else if constexpr (kStaged) {
                 if (t % G == 0 && rr <= (int)ld) {  // wave-uniform: every group is at step t
                     const int row = rr + lane;
@@ -1718,6 +1785,7 @@ __global__ __launch_bounds__(256) void nw_fill_lanes_kernel(
             const int32_t inH = shr1<G>(bH, pubH);  // H~(r, col0)
             if (r >= 1 && r <= (int)ld) {
                 int32_t F = inF;
+                const int32_t hm = kCodes == kCodesFull || r == (int)ld ? ~3 : ~1;
                 uint32_t sg[8][4 * KD];
 #pragma unroll
                 for (int k = 0; k < K; ++k) {
@@ -1728,8 +1796,8 @@ __global__ __launch_bounds__(256) void nw_fill_lanes_kernel(
                     const int32_t H = max(M, max(I, D));
                     const int32_t tO = M + kOpen;
                     if constexpr (kCodes != kCodesNone) {
-                        const int32_t Hc = H & ~1;
-                        const int32_t tOr = tO | 1;
+                        const int32_t Hc = H & hm;
+                        const int32_t tOr = tO | kTieOr;
                         sg[0][k] = (uint32_t)(M - Hc);
                         sg[1][k] = (uint32_t)(I - Hc);
                         sg[2][k] = (uint32_t)(D - Hc);
@@ -1737,7 +1805,7 @@ __global__ __launch_bounds__(256) void nw_fill_lanes_kernel(
                         sg[6][k] = (uint32_t)(tOr - D);
                         sg[7][k] = x - 1u;  // sign <=> q == d
                         if constexpr (kCodes == kCodesFull) {
-                            const int32_t tOc = tO & ~1;
+                            const int32_t tOc = tO & ~3;
                             sg[3][k] = (uint32_t)(I - tOc);
                             sg[5][k] = (uint32_t)(D - tOc);
                         } else {
@@ -1775,7 +1843,7 @@ __global__ __launch_bounds__(256) void nw_fill_lanes_kernel(
 #pragma unroll
                     for (int k = 0; k < K; ++k)
                         if ((uint32_t)k == k_end) e = Hp[k];
-                    end_h[first + gi] = e - alpha * (int32_t)ld - beta * (int32_t)lq;
+                    end_h[first + gi] = x4_to_x2(e - alpha * (int32_t)ld - beta * (int32_t)lq);
                 }
             }
         }
@@ -2126,7 +2194,7 @@ static void fill_i32(dim3 grid, hipStream_t s, const NwPairDesc *pairs, uint32_t
                      int2 *scratch, int32_t *end_h, saln_nw_result *, uint32_t *, Scoring sc,
                      int codes, uint32_t ld_max) {
     const size_t lds = (size_t)(256 / G) * (ld_max + 2 * G);
-    const int32_t pen_max = 2 * (sc.match - sc.mismatch);
+    const int32_t pen_max = 4 * (sc.match - sc.mismatch);  // the i32 fills' V'' scale
     auto go = [&](auto codes_c, auto minpen_c, auto staged_c) {
         nw_fill_lanes_kernel<G, K, decltype(codes_c)::value, decltype(minpen_c)::value,
                              decltype(staged_c)::value>
@@ -2366,7 +2434,7 @@ hipError_t launch_fill_stripes(const NwPairDesc *pairs, const uint2 *work, uint3
                                Scoring sc, int codes, bool pk, hipStream_t stream) {
     if (!n_work) return hipSuccess;
     const dim3 grid(n_work), block(64);
-    const int32_t pen_max = 2 * (sc.match - sc.mismatch);
+    const int32_t pen_max = 4 * (sc.match - sc.mismatch);  // the i32 fills' V'' scale
     // a coder wave per stripe while the pipeline is short (a few stripes in
     // the launch: the C1 latency case)
     static const int split_env = [] {  // experiment switch: SALN_STRIPE_SPLIT=0 / 1
@@ -2490,6 +2558,9 @@ int choose_variant(uint32_t len_q, uint32_t len_db, const Scoring &sc) {
         const char *e = std::getenv("SALN_NARROW_GROUPS");  // experiment switch: 8-lane groups
         return e && e[0] == '1' ? 1 : 0;
     }();
+    // the packed fills carry V' = 2V + p (no alive flag): sentinel-free pairs only
+    const bool free = sentinel_free(sc, len_q, len_db);
+    if (!free) return len_q <= 160 ? 0 : len_q <= 256 ? 1 : len_q <= 512 ? 2 : 3;
     if (packed_ok(len_q, len_db, sc)) {
         if (len_q <= 152 && narrow) return 4;
         if (len_q <= 160) return 7;

@@ -129,3 +129,35 @@ def test_check_pairs_matches_single_pair_oracle(oracle):
         first = None if w is None else "".join(ops[int(x) & 15] * (int(x) >> 4) for x in w)
         assert (int(got.score[k]), int(got.end_states[k]), bool(got.panics[k]), first) == \
             (o.score, o.end_states, o.panics, o.first_ops), k
+
+
+def test_linear_first_alignment_matches_full_oracle(oracle):
+    """reflinear.c's parent-set fill + literal DFS (the checker for pairs too
+    large for three full matrices) gives the full-matrix oracle's score, end
+    states, panic status and first printed alignment, tie-heavy alphabets
+    and empty sides included."""
+    rng = np.random.default_rng(23)
+    for k in range(200):
+        lq, ld = int(rng.integers(0, 50)), int(rng.integers(0, 50))
+        a = np.frombuffer([b"ACGT", b"AC", b"A", b"AAAC"][k % 4], np.uint8)
+        q = a[rng.integers(0, len(a), lq)].tobytes()
+        d = a[rng.integers(0, len(a), ld)].tobytes()
+        o = oracle.nw(q, d, literal_dfs=False)
+        sc, es, pan, first, _ = oracle.nw_first_linear(q, d, threads=2)
+        assert (sc, es, pan, first) == (o.score, o.end_states, o.panics, o.first_ops), k
+
+
+def test_deadend_fixtures(oracle):
+    """tests/golden/nw_deadend.json: pairs past the sentinel line whose DFS
+    meets sentinel-rooted subtrees (nothing printed, panics, and a block
+    printed after the DFS left a dead subtree); the linear oracle reproduces
+    the committed values (make_deadend.py checked both oracles)."""
+    with open(os.path.join(GOLDEN, "nw_deadend.json")) as f:
+        pairs = json.load(f)["pairs"]
+    assert any(p["dead"] and p["first_ops"] for p in pairs)
+    assert any(p["dead"] and p["panics"] for p in pairs)
+    for p in pairs:
+        sc, es, pan, first, dead = oracle.nw_first_linear(p["query"].encode(), p["db"].encode(),
+                                                          threads=2)
+        assert (sc, es, pan, first, dead) == (p["score"], p["end_states"], p["panics"],
+                                              p["first_ops"], p["dead"]), p["id"]
