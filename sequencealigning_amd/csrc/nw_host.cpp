@@ -50,6 +50,8 @@ struct saln_nw_plan {
     int32_t *d_endh2 = nullptr;
     bool async_tb = false;
     bool stripe_pk = false;  // column stripes use the packed fill and layout
+    int stripe_rows = 0;     // else: row fill with this many columns per lane (0 = skewed fill)
+    int stripe_layout() const { return stripe_pk ? 1 : stripe_rows ? 2 : 0; }
     bool full_codes = false;  // walk codes (default) or every parent set
     bool score_only = false;  // no parent codes / traceback (saln_nw_plan_set_score_only)
     int buf = 0;                           // workspace of the next execute (async mode)
@@ -242,11 +244,13 @@ int saln_nw_plan_create(saln_context *ctx, const uint64_t *q_off, uint64_t n_q,
             const Geom g = variant_geom((int)d.variant);
             d.ops_off = ooff;
             ooff += (d.len_q + d.len_db + 9) / 10 + 1;  // 3-bit ops, ten per word
-            if (g.n_chunks(d.len_q) > 1) {
+            if (g.n_chunks(d.len_q) > 1 || d.variant == kStripeVariant) {
+                soff = (soff + 3) & ~3ull;  // 32-byte aligned columns (nw_fill_rows_kernel)
                 d.scratch_off = soff;
                 // stripes run concurrently: one boundary column per chunk boundary
-                soff += (uint64_t)(d.variant == kStripeVariant ? g.n_chunks(d.len_q) : 1) *
-                        (d.len_db + 2);
+                soff += (uint64_t)(d.variant == kStripeVariant ? kStripeSubMax * g.n_chunks(d.len_q)
+                                                                : 1) *
+                        scratch_col(d.len_db);
             }
             if (p->var_count[d.variant] == 0) p->var_first[d.variant] = (uint32_t)r;
             p->var_count[d.variant]++;
@@ -264,6 +268,7 @@ int saln_nw_plan_create(saln_context *ctx, const uint64_t *q_off, uint64_t n_q,
             free_all = free_all && sentinel_free(p->sc, d.len_q, d.len_db);
         }
         p->stripe_pk = waves > 0 && free_all && stripe_packed(p->sc, waves);
+        p->stripe_rows = p->stripe_pk ? 0 : stripe_rows_k();
     }
     // Mask packs: up to 64 consecutive pairs of a variant (one traceback
     // wave) with interleaved segments (nw_common.hpp Geom), unless padding
@@ -286,12 +291,13 @@ int saln_nw_plan_create(saln_context *ctx, const uint64_t *q_off, uint64_t n_q,
             if (v == kStripeVariant) {
                 // skewed, one region per stripe (nw_common.hpp): every fill
                 // step of a stripe wave writes one whole 256-byte line
+                // (row fill: unskewed 256-column tiles, bs = 4, same region size)
                 const bool pk = p->stripe_pk;
                 for (uint32_t s = 0; s < np; ++s) {
                     NwPairDesc &d = p->h_pairs[a + s];
                     d.mask_off = moff;
                     d.mask_rs = g.W();
-                    d.mask_bs = pk ? 0u : (uint32_t)(g.W() + lb);
+                    d.mask_bs = pk ? 0u : p->stripe_rows ? (uint32_t)lb : (uint32_t)(g.W() + lb);
                     d.mask_cs = ((uint64_t)d.len_db + (pk ? 2 * g.G : g.G) - 1) * g.W();
                     moff += g.n_chunks(d.len_q) * d.mask_cs;
                 }
@@ -475,15 +481,16 @@ int saln_nw_execute(saln_nw_plan *p, const uint8_t *d_q, const uint8_t *d_db,
                     // once its value replaces the preset (nw_fill_stripe_kernel)
                     const NwPairDesc &la = p->h_pairs[b - 1];
                     const uint64_t c0 = p->h_pairs[a].scratch_off;
-                    const uint64_t c1 = la.scratch_off + (uint64_t)variant_geom(v).n_chunks(la.len_q) *
-                                                             (la.len_db + 2);
+                    const uint64_t c1 = la.scratch_off + (uint64_t)kStripeSubMax *
+                                                             variant_geom(v).n_chunks(la.len_q) *
+                                                             scratch_col(la.len_db);
                     HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)(p->d_scratch + c0), (int)0x80000000u,
                                               2 * (c1 - c0), s));
                     HIP_TRY(launch_fill_stripes(p->d_pairs, p->d_work + w0, w1 - w0, d_q, d_db,
                                                 mask, p->d_scratch, p->d_prog, p->d_err, endh,
                                                 p->sc,
                                                 p->score_only ? 2 : p->full_codes ? 1 : 0,
-                                                p->stripe_pk, s));
+                                                p->stripe_layout(), p->stripe_rows, s));
                 }
             } else if (a < b)
                 HIP_TRY(launch_fill(v, p->d_pairs, a, b - a, d_q, d_db, mask, p->d_scratch, endh,
@@ -502,7 +509,7 @@ int saln_nw_execute(saln_nw_plan *p, const uint8_t *d_q, const uint8_t *d_db,
                 HIP_TRY(launch_score_results(p->d_pairs, a, b - a, endh, d_results, p->sc, t));
             else if (a < b)
                 HIP_TRY(launch_traceback(v, p->d_pairs, a, b - a, d_q, d_db, mask, endh, p->d_ops,
-                                         d_results, d_cigar, p->sc, p->stripe_pk, t));
+                                         d_results, d_cigar, p->sc, p->stripe_layout(), t));
         }
     }
     // pairs with an empty side (boundary-only walk) ride on the traceback stream
@@ -512,7 +519,7 @@ int saln_nw_execute(saln_nw_plan *p, const uint8_t *d_q, const uint8_t *d_db,
     else if (p->n_pairs > p->n_fill)
         HIP_TRY(launch_traceback(-1, p->d_pairs, p->n_fill, (uint32_t)(p->n_pairs - p->n_fill),
                                  d_q, d_db, mask, endh, p->d_ops, d_results, d_cigar, p->sc,
-                                 p->stripe_pk, t));
+                                 p->stripe_layout(), t));
     if (ev) HIP_TRY(hipEventRecord(ev[3], t));
     HIP_TRY(hipEventRecord(p->tb_done(cur), t));
     p->tb_pending[cur] = true;

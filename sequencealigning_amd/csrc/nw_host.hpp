@@ -79,11 +79,17 @@ hipError_t launch_fill_stripes(const NwPairDesc *pairs, const uint2 *work, uint3
                                const uint8_t *qs, const uint8_t *ds, uint8_t *mask,
                                int2 *scratch, uint32_t *prog, uint32_t *err, int32_t *end_h,
                                Scoring sc, int codes /* 0 walk, 1 full, 2 none */,
-                               bool pk /* the packed stripe layout */, hipStream_t stream);
+                               int layout /* 0 skewed, 1 packed, 2 row-major tiles */,
+                               int rows_k /* layout 2: columns per lane */, hipStream_t stream);
 hipError_t launch_cigar_compact(const saln_nw_result *res, const uint64_t *src_off,
                                 const uint64_t *dst_off, const uint32_t *src, uint32_t *dst,
                                 uint64_t n, hipStream_t stream);
 constexpr int kStripeVariant = 3;
+// column-stripe pairs: boundary columns allocated per pair (the row fill cuts
+// each 256-column chunk into up to 4 stripes)
+constexpr uint32_t kStripeSubMax = 4;
+// row fill (nw_fill_rows_kernel) columns per lane, 0 = the skewed stripe fill
+int stripe_rows_k();
 // column stripes run the packed (int16 halves) fill for this scoring and
 // this many stripe waves in the plan (decided once per plan: it sets the layout)
 bool stripe_packed(const Scoring &sc, uint64_t n_waves);
@@ -96,7 +102,7 @@ hipError_t launch_traceback(int variant, const NwPairDesc *pairs, uint32_t first
                             const uint8_t *qs,
                             const uint8_t *ds, const uint8_t *mask, const int32_t *end_h,
                             uint32_t *ops, saln_nw_result *results, uint32_t *cigar, Scoring sc,
-                            bool stripe_pk, hipStream_t stream);
+                            int stripe_layout, hipStream_t stream);
 // score-only all-vs-all (nw_avsa.cpp)
 hipError_t launch_avsa(int variant, const uint64_t *q_off, const uint64_t *d_off,
                        const uint32_t *q_ids, uint32_t nq, const uint32_t *d_ids,

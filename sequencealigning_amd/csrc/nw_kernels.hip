@@ -637,14 +637,17 @@ __global__ __launch_bounds__(256) void nw_traceback_kernel(
 constexpr int32_t kCoopLine = 256;  // bytes per line (one stripe step)
 constexpr int32_t kCoopSlack = 64;  // rows loaded beyond a diagonal crossing of the stripe
 
-// kPk: the packed stripe layout (bs == 0): virtual lane v = (c - c0) / 2 of
-// row r sits on line r - 1 + v (127 lines of skew instead of 63).
-template <int NWV, bool kPk>
+// kLay: 0 the skewed stripe layout (row r of lane l on line r - 1 + l); 1 the
+// packed stripe layout (bs == 0): virtual lane v = (c - c0) / 2 of row r sits
+// on line r - 1 + v (127 lines of skew); 2 the row-major 256-column tiles of
+// nw_fill_rows_kernel (no skew: row r is line r - 1).
+template <int NWV, int kLay>
 __global__ __launch_bounds__(64 * NWV) void nw_traceback_coop_kernel(
     const NwPairDesc *__restrict__ pairs, uint32_t first, const uint8_t *__restrict__ mask,
     const int32_t *__restrict__ end_h, saln_nw_result *__restrict__ results,
     uint32_t *__restrict__ cigar, Scoring sc, int32_t kCoopRows) {
-    constexpr int32_t kSkew = kPk ? 127 : 63;  // lines from a row's first to its last block
+    constexpr bool kPk = kLay == 1;
+    constexpr int32_t kSkew = kLay == 1 ? 127 : kLay == 2 ? 0 : 63;  // lines from a row's first to its last block
     // kCoopRows + kSkew lines, rounded up to whole 4-line DMAs; then the
     // request words wave 0 posts to the loader waves
     extern __shared__ __attribute__((aligned(16))) uint8_t win[];
@@ -706,6 +709,7 @@ __global__ __launch_bounds__(64 * NWV) void nw_traceback_coop_kernel(
             return (uint32_t)win[(r - r_lo + v) * kCoopLine + 4 * (v & 63) + 2 * (o & 1) + (v >> 6)] ^
                    0x7Fu;
         }
+        if constexpr (kLay == 2) return (uint32_t)win[(r - r_lo) * kCoopLine + o] ^ 0x7Fu;
         return (uint32_t)win[(r - r_lo + (o >> 2)) * kCoopLine + o] ^ 0x7Fu;
     };
     int32_t i = ld, j = lq;
@@ -1409,8 +1413,8 @@ __global__ __launch_bounds__(128) void nw_fill_stripe_kernel(
     const uint8_t *__restrict__ q = qs + p.q_off;
     const uint8_t *__restrict__ d = ds + p.db_off;
     const uint32_t nch = geo.n_chunks(lq);
-    const int2 *__restrict__ scr_in = c > 0 ? scratch + p.scratch_off + (uint64_t)(c - 1) * (ld + 2) : nullptr;
-    int2 *__restrict__ scr_out = c + 1 < nch ? scratch + p.scratch_off + (uint64_t)c * (ld + 2) : nullptr;
+    const int2 *__restrict__ scr_in = c > 0 ? scratch + p.scratch_off + (uint64_t)(c - 1) * scratch_col(ld) : nullptr;
+    int2 *__restrict__ scr_out = c + 1 < nch ? scratch + p.scratch_off + (uint64_t)c * scratch_col(ld) : nullptr;
     // V'' = 4V + 2a + p (nw_common.hpp): offsets and constants scaled by 4
     const int32_t beta = -4 * sc.gap_extend;
     const int32_t alpha = -4 * sc.match - beta;
@@ -1682,6 +1686,307 @@ __global__ __launch_bounds__(128) void nw_fill_stripe_kernel(
     if (failed && lane == 0) atomicOr(err, 1u);
 }
 
+// ------------------------------------- long pairs: row-synchronous stripes
+// One wave per stripe of 64*K columns (K = 1, 2, 4), all 64 lanes on the same
+// row at the same step.  A stripe then has no internal skew: its right
+// neighbour starts row r as soon as row r's boundary arrives (lag = one
+// hand-off, not the 64 + 32 steps of nw_fill_stripe_kernel), so stripes can
+// be narrow and many (C4: 1,563 waves of 64 columns instead of 391 of 256).
+// Within a row, M~ = H~(r-1, c-1) - pen and D~ come from the previous row;
+// in the transformed recurrence (nw_fill_stripe_kernel) I~(r, c+1) =
+// max(I~(r, c), M~(r, c) + open) is the row's running max of the gap-open
+// candidates: a lane-local prefix over its K columns, a 64-lane DPP prefix max
+// of the lane totals (row_shr 1/2/4/8, row_bcast 15/31) and the I entering
+// from the left stripe.  i32 with V'' = 4V + 2a + p (nw_common.hpp).
+// Mask layout: 256-column tiles, row-major inside a tile (bs = 4, rs = 256):
+// cell (i, j) at (j-1)/256 * cs + (i-1) * 256 + (j-1) % 256, so a stripe's
+// row is 64K contiguous bytes.  Codes are built four cells at a time
+// (stripe_code_word): K = 4 one row, K = 2 two rows, K = 1 four rows.
+// Hand-off: the stripe's last lane stores (H~, I~) leaving its last column
+// per row as one 64-bit agent-coherent store into boundary column g (preset
+// to kColEmpty); stripe g+1 polls kRowsBlk-row blocks (nw_fill_stripe_kernel).
+constexpr int32_t kNegInf = INT32_MIN;
+#ifndef SALN_ROWS_OFF
+#define SALN_ROWS_OFF 0  // experiment switch: boundary row r stored at element r + this
+#endif
+constexpr uint32_t kRowsOff = SALN_ROWS_OFF;
+#ifndef SALN_ROWS_BCAST
+#define SALN_ROWS_BCAST 1  // experiment switch: branch-free boundary publication (0: lane 63 stores)
+#endif
+#ifndef SALN_ROWS_INDEP
+#define SALN_ROWS_INDEP 0  // experiment builds only: stripes ignore their left neighbour
+#endif
+
+// inclusive prefix max over the wave's 64 lanes (lane order)
+__device__ __forceinline__ int32_t wave_prefix_max(int32_t v) {
+    v = max(v, __builtin_amdgcn_update_dpp(kNegInf, v, 0x111 /*row_shr:1*/, 0xf, 0xf, false));
+    v = max(v, __builtin_amdgcn_update_dpp(kNegInf, v, 0x112 /*row_shr:2*/, 0xf, 0xf, false));
+    v = max(v, __builtin_amdgcn_update_dpp(kNegInf, v, 0x114 /*row_shr:4*/, 0xf, 0xf, false));
+    v = max(v, __builtin_amdgcn_update_dpp(kNegInf, v, 0x118 /*row_shr:8*/, 0xf, 0xf, false));
+    v = max(v, __builtin_amdgcn_update_dpp(kNegInf, v, 0x142 /*row_bcast:15*/, 0xa, 0xf, false));
+    v = max(v, __builtin_amdgcn_update_dpp(kNegInf, v, 0x143 /*row_bcast:31*/, 0xc, 0xf, false));
+    return v;
+}
+
+template <int K, int kCodes, bool kMinPen>
+__global__ __launch_bounds__(64) void nw_fill_rows_kernel(
+    const NwPairDesc *__restrict__ pairs, const uint2 *__restrict__ work,
+    const uint8_t *__restrict__ qs, const uint8_t *__restrict__ ds, uint8_t *__restrict__ mask,
+    int2 *__restrict__ scratch, uint32_t *__restrict__ err, int32_t *__restrict__ end_h,
+    Scoring sc) {
+    static_assert(K == 1 || K == 2 || K == 4, "4 cells per code word");
+    constexpr int S = 4 / K;   // stripes per 256-column chunk (work item)
+    constexpr int W = 64 * K;  // stripe width (4 / K rows per code word)
+    const int lane = (int)threadIdx.x;
+    const uint2 wk = work[blockIdx.x / S];
+    const NwPairDesc p = pairs[wk.x];
+    const uint32_t g = wk.y * S + blockIdx.x % S;  // stripe index
+    const uint32_t lq = p.len_q, ld = p.len_db;
+    const uint32_t c0 = g * W;  // the stripe's columns c0+1 .. c0+W
+    if (c0 >= lq) return;
+    const uint32_t nst = (lq + W - 1) / W;
+    const int2 *__restrict__ scr_in = g > 0 ? scratch + p.scratch_off + (uint64_t)(g - 1) * scratch_col(ld) : nullptr;
+    // (the last stripe too, into a column nobody reads: a fixed VMEM count per group)
+    int2 *__restrict__ scr_out = scratch + p.scratch_off + (uint64_t)g * scratch_col(ld);
+    (void)nst;
+    const int32_t beta = -4 * sc.gap_extend;
+    const int32_t alpha = -4 * sc.match - beta;
+    const int32_t pen_max = 4 * (sc.match - sc.mismatch);
+    const int32_t kOpen = 4 * sc.gap_open;
+    const int32_t kDstep = 4 * sc.gap_extend + alpha;
+    constexpr int32_t kTieOr = kCodes == kCodesFull ? 3 : 1;
+    const uint32_t col0 = c0 + (uint32_t)lane * K;  // my columns col0+1 .. col0+K
+    uint32_t qc[K];
+    int32_t Hp[K], Dn[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const uint32_t j = col0 + k + 1;
+        qc[k] = j <= lq ? (uint32_t)qs[p.q_off + j - 1] << 8 : 0xFFFFFF00u;
+        Hp[k] = hs4_row0(sc, j) + beta * (int32_t)j;
+        Dn[k] = ds4_row1(sc, j) + alpha + beta * (int32_t)j;
+    }
+    int32_t hb_prev = hs4_row0(sc, c0) + beta * (int32_t)c0;  // H~(r-1, c0): lane 0's diagonal
+    // my bytes of row 1 in the 256-column tile layout
+    uint8_t *mrow = mask + p.mask_off + (uint64_t)(c0 / 256) * p.mask_cs + (col0 % 256);
+    typedef const __attribute__((address_space(4))) uint32_t cu32;  // constant: scalar loads
+    const uint8_t *d = ds + p.db_off;
+    cu32 *dw = (cu32 *)((uintptr_t)d & ~(uintptr_t)3);
+    const uint32_t doff = 8u * (uint32_t)((uintptr_t)d & 3);
+    const uint32_t last_dw = ((uint32_t)ld - 1 + (uint32_t)((uintptr_t)d & 3)) >> 2;
+    uint32_t dnidx = min(1u, last_dw);
+    uint32_t dcur = dw[0], dnxt = dw[dnidx];
+
+    bool failed = false;
+    const uint32_t jend = lq - 1;
+    const bool end_lane = jend / W == g && (uint32_t)lane == (jend % W) / K;
+    const uint32_t k_end = jend % K;
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the query chars
+    uint32_t sg[8][4];  // sign words of the current code word's four cells
+    // one row: r (1-based), its db char, the left boundary (H~(r, c0), I~
+    // entering column c0+1) and u = its slot in the code word (compile time)
+    auto row = [&](uint32_t r, uint32_t dch, int32_t bH, int32_t bI, auto u_c, auto q_c) __attribute__((always_inline)) {
+        constexpr int u = decltype(u_c)::value;
+        constexpr int q = decltype(q_c)::value;  // row in its four-row group
+        const int32_t hm = (kCodes == kCodesFull || r == ld) ? ~3 : ~1;
+        int32_t M[K], tO[K], P[K];
+        int32_t diag = __builtin_amdgcn_update_dpp(hb_prev, Hp[K - 1], 0x138 /*wave_shr:1*/, 0xf, 0xf, false);
+        uint32_t x[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            x[k] = qc[k] ^ dch;
+            const int32_t pen = kMinPen ? (int32_t)min(x[k], (uint32_t)pen_max) : (x[k] ? pen_max : 0);
+            M[k] = (k == 0 ? diag : Hp[k - 1]) - pen;
+            tO[k] = M[k] + kOpen;
+            P[k] = k == 0 ? tO[0] : max(P[k - 1], tO[k]);
+        }
+        const int32_t S_incl = wave_prefix_max(P[K - 1]);
+        const int32_t Ein = max(__builtin_amdgcn_update_dpp(kNegInf, S_incl, 0x138, 0xf, 0xf, false), bI);
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const int32_t I = k == 0 ? Ein : max(Ein, P[k - 1]);
+            const int32_t D = Dn[k];
+            const int32_t H = max(M[k], max(I, D));
+            if constexpr (kCodes != kCodesNone) {
+                const int32_t Hc = H & hm;
+                const int32_t tOr = tO[k] | kTieOr;
+                const int e = u * K + k;  // cell slot in the code word (unrolled: constant)
+                sg[0][e] = (uint32_t)(M[k] - Hc);
+                sg[1][e] = (uint32_t)(I - Hc);
+                sg[2][e] = (uint32_t)(D - Hc);
+                sg[4][e] = (uint32_t)(tOr - I);
+                sg[6][e] = (uint32_t)(tOr - D);
+                sg[7][e] = x[k] - 1u;  // sign <=> q == d
+                if constexpr (kCodes == kCodesFull) {
+                    const int32_t tOc = tO[k] & ~3;
+                    sg[3][e] = (uint32_t)(I - tOc);
+                    sg[5][e] = (uint32_t)(D - tOc);
+                } else {
+                    sg[3][e] = sg[5][e] = 0u;
+                }
+            }
+            Dn[k] = max(tO[k], D) + kDstep;
+            Hp[k] = H;
+        }
+        hb_prev = bH;
+        (void)q;
+        // (H~, I~) leaving the stripe's last column (lane 63's values)
+#if SALN_ROWS_BCAST
+        {   // every lane stores the broadcast pair to the same address (one
+            // 8-byte write): no exec change, no branch splitting the group's
+            // straight-line code
+            const int32_t h63 = __builtin_amdgcn_readlane(Hp[K - 1], 63);
+            const int32_t i63 = max(__builtin_amdgcn_readlane(S_incl, 63), bI);
+            __hip_atomic_store((uint64_t *)(scr_out + r + kRowsOff),
+                               (uint64_t)(uint32_t)h63 | ((uint64_t)(uint32_t)i63 << 32),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+#else
+        if (lane == 63)
+            __hip_atomic_store((uint64_t *)(scr_out + r + kRowsOff),
+                               (uint64_t)(uint32_t)Hp[K - 1] | ((uint64_t)(uint32_t)max(S_incl, bI) << 32),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#endif
+    };
+    // store the code word of rows r0 .. r0+(4/K)-1 (n of them valid)
+    auto put = [&](uint32_t r0, uint32_t n) __attribute__((always_inline)) {
+        if constexpr (kCodes != kCodesNone) {
+            const uint32_t wv = stripe_code_word<kCodes>(sg);
+            uint8_t *a = mrow + (uint64_t)(r0 - 1) * 256;
+            if constexpr (K == 4) {
+                *reinterpret_cast<uint32_t *>(a) = wv;
+            } else if constexpr (K == 2) {
+                *reinterpret_cast<uint16_t *>(a) = (uint16_t)wv;
+                if (n > 1) *reinterpret_cast<uint16_t *>(a + 256) = (uint16_t)(wv >> 16);
+            } else {
+                a[0] = (uint8_t)wv;
+                if (n > 1) a[256] = (uint8_t)(wv >> 8);
+                if (n > 2) a[512] = (uint8_t)(wv >> 16);
+                if (n > 3) a[768] = (uint8_t)(wv >> 24);
+            }
+        }
+    };
+    const std::integral_constant<int, 0> u0;
+    const std::integral_constant<int, 1> u1;
+    const std::integral_constant<int, 2> u2;
+    const std::integral_constant<int, 3> u3;
+    const std::integral_constant<int, 0> q0;
+    const std::integral_constant<int, 1> q1;
+    const std::integral_constant<int, 2> q2;
+    const std::integral_constant<int, 3> q3;
+    // The left boundary arrives per four-row group: when a group starts,
+    // lanes 0-3 load the next group's four rows (agent-coherent sc1 loads,
+    // issued as inline asm so that the compiler adds no wait of its own: its
+    // wait would be a vmcnt(0) on every outstanding store); the next group
+    // waits for exactly that load with a counted vmcnt: a group issues eight
+    // VMEM operations after it (four mask stores, four boundary stores: every
+    // stripe publishes, the last one into a column nobody reads; score-only:
+    // the four boundary stores), so vmcnt(7) (3) covers it.  The count must
+    // be exact - a load still in flight after its wait would land in
+    // registers the compiler has reused.  Rows not yet published are
+    // re-polled with ordinary (compiler-waited) loads.
+    auto rows = [&](auto F) __attribute__((always_inline)) {
+        constexpr bool kFirst = decltype(F)::value || SALN_ROWS_INDEP;
+        uint64_t nv = 0;  // lanes 0-3: (H~, I~) of the next group's rows
+        auto fetch = [&](uint32_t r0) __attribute__((always_inline)) {
+            if (!kFirst && lane < 4 && r0 + (uint32_t)lane <= ld)
+                asm volatile("global_load_dwordx2 %0, %1, off sc1"
+                             : "=v"(nv) : "v"(scr_in + r0 + kRowsOff + lane) : "memory");
+        };
+        fetch(1);
+        if constexpr (!kFirst) asm volatile("s_waitcnt vmcnt(0)" : "+v"(nv) : : "memory");
+        int32_t bh[4], bi[4];  // the boundary of rows r .. r+3
+        auto group = [&](uint32_t r) __attribute__((always_inline)) {
+            if constexpr (kFirst) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    bi[q] = is4_col1(sc, r + q) + alpha * (int32_t)(r + q) + beta;
+                    bh[q] = hs4_col0(sc, r + q) + alpha * (int32_t)(r + q);
+                }
+            } else {
+                if constexpr (kCodes == kCodesNone)
+                    asm volatile("s_waitcnt vmcnt(3)" : "+v"(nv) : : "memory");
+                else
+                    asm volatile("s_waitcnt vmcnt(7)" : "+v"(nv) : : "memory");
+                int32_t cH = (int32_t)(uint32_t)nv, cI = (int32_t)(uint32_t)(nv >> 32);
+                bool ok = !(lane < 4 && r + (uint32_t)lane <= ld) || (uint32_t)cH != kColEmpty;
+                uint32_t spins = 0;
+                while (__builtin_amdgcn_ballot_w64(!ok) && !failed) {  // not yet published: poll
+                    __builtin_amdgcn_s_sleep(1);
+                    if (lane < 4 && r + (uint32_t)lane <= ld) {
+                        const uint64_t v = __hip_atomic_load((const uint64_t *)(scr_in + r + kRowsOff + lane),
+                                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        cH = (int32_t)(uint32_t)v;
+                        cI = (int32_t)(uint32_t)(v >> 32);
+                        ok = (uint32_t)cH != kColEmpty;
+                    }
+                    if (++spins > kSpinCap) failed = true;
+                }
+                fetch(r + 4);
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    bh[q] = __builtin_amdgcn_readlane(cH, q);
+                    bi[q] = __builtin_amdgcn_readlane(cI, q);
+                }
+            }
+        };
+    uint32_t r = 1;
+    for (; r + 3 <= ld; r += 4) {  // four rows: one scalar word of db chars
+        const uint32_t w = doff ? (dcur >> doff) | (dnxt << (32u - doff)) : dcur;
+        dcur = dnxt;
+        dnidx = min(dnidx + 1, last_dw);
+        dnxt = dw[dnidx];
+        group(r);
+        if constexpr (K == 4) {
+            row(r, (w & 0xFFu) << 8, bh[0], bi[0], u0, q0); put(r, 1);
+            row(r + 1, ((w >> 8) & 0xFFu) << 8, bh[1], bi[1], u0, q1); put(r + 1, 1);
+            row(r + 2, ((w >> 16) & 0xFFu) << 8, bh[2], bi[2], u0, q2); put(r + 2, 1);
+            row(r + 3, (w >> 24) << 8, bh[3], bi[3], u0, q3); put(r + 3, 1);
+        } else if constexpr (K == 2) {
+            row(r, (w & 0xFFu) << 8, bh[0], bi[0], u0, q0);
+            row(r + 1, ((w >> 8) & 0xFFu) << 8, bh[1], bi[1], u1, q1); put(r, 2);
+            row(r + 2, ((w >> 16) & 0xFFu) << 8, bh[2], bi[2], u0, q2);
+            row(r + 3, (w >> 24) << 8, bh[3], bi[3], u1, q3); put(r + 2, 2);
+        } else {
+            row(r, (w & 0xFFu) << 8, bh[0], bi[0], u0, q0);
+            row(r + 1, ((w >> 8) & 0xFFu) << 8, bh[1], bi[1], u1, q1);
+            row(r + 2, ((w >> 16) & 0xFFu) << 8, bh[2], bi[2], u2, q2);
+            row(r + 3, (w >> 24) << 8, bh[3], bi[3], u3, q3);
+            put(r, 4);
+        }
+    }
+    if (r <= ld) {  // 1-3 tail rows
+        const uint32_t w = doff ? (dcur >> doff) | (dnxt << (32u - doff)) : dcur;
+        const uint32_t n = ld - r + 1;
+        group(r);
+        if constexpr (K == 4) {
+            row(r, (w & 0xFFu) << 8, bh[0], bi[0], u0, q0); put(r, 1);
+            if (n > 1) { row(r + 1, ((w >> 8) & 0xFFu) << 8, bh[1], bi[1], u0, q1); put(r + 1, 1); }
+            if (n > 2) { row(r + 2, ((w >> 16) & 0xFFu) << 8, bh[2], bi[2], u0, q2); put(r + 2, 1); }
+        } else if constexpr (K == 2) {
+            row(r, (w & 0xFFu) << 8, bh[0], bi[0], u0, q0);
+            if (n > 1) row(r + 1, ((w >> 8) & 0xFFu) << 8, bh[1], bi[1], u1, q1);
+            put(r, min(n, 2u));
+            if (n > 2) { row(r + 2, ((w >> 16) & 0xFFu) << 8, bh[2], bi[2], u0, q2); put(r + 2, 1); }
+        } else {
+            row(r, (w & 0xFFu) << 8, bh[0], bi[0], u0, q0);
+            if (n > 1) row(r + 1, ((w >> 8) & 0xFFu) << 8, bh[1], bi[1], u1, q1);
+            if (n > 2) row(r + 2, ((w >> 16) & 0xFFu) << 8, bh[2], bi[2], u2, q2);
+            put(r, n);
+        }
+    }
+    };
+    if (g == 0) rows(std::true_type{});
+    else rows(std::false_type{});
+    if (end_lane) {
+        int32_t e = 0;
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+            if ((uint32_t)k == k_end) e = Hp[k];
+        end_h[wk.x] = x4_to_x2(e - alpha * (int32_t)ld - beta * (int32_t)lq);
+    }
+    if (failed && lane == 0) atomicOr(err, 1u);
+}
+
 // ------------------------------------------------------------ i32 lanes
 // Pairs the packed fills cannot hold (long dbs, wide penalties): one pair per
 // group of G lanes, K columns per lane, i32 with the transformed recurrence
@@ -1887,8 +2192,8 @@ __global__ __launch_bounds__(64) void nw_fill_stripe_pk_kernel(
     const uint8_t *__restrict__ q = qs + p.q_off;
     const uint8_t *__restrict__ d = ds + p.db_off;
     const uint32_t nch = (lq + W - 1) / W;
-    const int2 *__restrict__ scr_in = c > 0 ? scratch + p.scratch_off + (uint64_t)(c - 1) * (ld + 2) : nullptr;
-    int2 *__restrict__ scr_out = c + 1 < nch ? scratch + p.scratch_off + (uint64_t)c * (ld + 2) : nullptr;
+    const int2 *__restrict__ scr_in = c > 0 ? scratch + p.scratch_off + (uint64_t)(c - 1) * scratch_col(ld) : nullptr;
+    int2 *__restrict__ scr_out = c + 1 < nch ? scratch + p.scratch_off + (uint64_t)c * scratch_col(ld) : nullptr;
     const int32_t beta = -2 * sc.gap_extend;
     const int32_t alpha = -2 * sc.match - beta;
     const uint32_t kPen = cst2(2 * (sc.match - sc.mismatch));  // 2 <= pen <= 32
@@ -2386,7 +2691,7 @@ static void tb_lds(dim3 grid, hipStream_t s, const NwPairDesc *pairs, uint32_t f
 hipError_t launch_traceback(int variant, const NwPairDesc *pairs, uint32_t first, uint32_t n,
                             const uint8_t *qs, const uint8_t *ds, const uint8_t *mask,
                             const int32_t *end_h, uint32_t *ops, saln_nw_result *results,
-                            uint32_t *cigar, Scoring sc, bool stripe_pk, hipStream_t stream) {
+                            uint32_t *cigar, Scoring sc, int stripe_layout, hipStream_t stream) {
     if (n == 0) return hipSuccess;
     const dim3 grid((n + 255) / 256);
     switch (variant) {
@@ -2397,20 +2702,22 @@ hipError_t launch_traceback(int variant, const NwPairDesc *pairs, uint32_t first
             // a few pairs: the whole 160 KB (fewer window reloads); batches:
             // 48 KB windows, three waves per CU
             constexpr int kLoaders = 4;  // waves per pair: one walks, all load its windows
-            auto go = [&](auto pk_c) -> hipError_t {
-                constexpr bool kPk = decltype(pk_c)::value;
-                constexpr int32_t kSkew = kPk ? 127 : 63;
+            auto go = [&](auto lay_c) -> hipError_t {
+                constexpr int kLay = decltype(lay_c)::value;
+                constexpr int32_t kSkew = kLay == 1 ? 127 : kLay == 2 ? 0 : 63;
                 static const hipError_t attr = hipFuncSetAttribute(
-                    (const void *)nw_traceback_coop_kernel<kLoaders, kPk>,
+                    (const void *)nw_traceback_coop_kernel<kLoaders, kLay>,
                     hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
                 if (attr != hipSuccess) return attr;
                 const int32_t rows = n <= 256 ? 632 - (kSkew + 1) : 128;
-                nw_traceback_coop_kernel<kLoaders, kPk>
+                nw_traceback_coop_kernel<kLoaders, kLay>
                     <<<dim3(n), dim3(64 * kLoaders), (size_t)(rows + kSkew + 1) * kCoopLine + 16,
                        stream>>>(pairs, first, mask, end_h, results, cigar, sc, rows);
                 return hipSuccess;
             };
-            const hipError_t e = stripe_pk ? go(std::true_type{}) : go(std::false_type{});
+            const hipError_t e = stripe_layout == 1   ? go(std::integral_constant<int, 1>{})
+                                 : stripe_layout == 2 ? go(std::integral_constant<int, 2>{})
+                                                      : go(std::integral_constant<int, 0>{});
             if (e != hipSuccess) return e;
             break;
         }
@@ -2431,9 +2738,32 @@ hipError_t launch_traceback(int variant, const NwPairDesc *pairs, uint32_t first
 hipError_t launch_fill_stripes(const NwPairDesc *pairs, const uint2 *work, uint32_t n_work,
                                const uint8_t *qs, const uint8_t *ds, uint8_t *mask,
                                int2 *scratch, uint32_t *prog, uint32_t *err, int32_t *end_h,
-                               Scoring sc, int codes, bool pk, hipStream_t stream) {
+                               Scoring sc, int codes, int layout, int rows_k, hipStream_t stream) {
     if (!n_work) return hipSuccess;
     const dim3 grid(n_work), block(64);
+    const bool pk = layout == 1;
+    if (layout == 2) {  // row-synchronous stripes of 64 * rows_k columns
+        const int32_t pm = 4 * (sc.match - sc.mismatch);
+        auto go = [&](auto k_c, auto codes_c, auto minpen_c) {
+            constexpr int kK = decltype(k_c)::value;
+            nw_fill_rows_kernel<kK, decltype(codes_c)::value, decltype(minpen_c)::value>
+                <<<dim3(n_work * (4 / kK)), block, 0, stream>>>(pairs, work, qs, ds, mask, scratch,
+                                                               err, end_h, sc);
+        };
+        auto by_k = [&](auto codes_c, auto minpen_c) {
+            if (rows_k == 4) go(std::integral_constant<int, 4>{}, codes_c, minpen_c);
+            else if (rows_k == 2) go(std::integral_constant<int, 2>{}, codes_c, minpen_c);
+            else go(std::integral_constant<int, 1>{}, codes_c, minpen_c);
+        };
+        auto by_codes = [&](auto minpen_c) {
+            if (codes == kCodesFull) by_k(std::integral_constant<int, kCodesFull>{}, minpen_c);
+            else if (codes == kCodesNone) by_k(std::integral_constant<int, kCodesNone>{}, minpen_c);
+            else by_k(std::integral_constant<int, kCodesWalk>{}, minpen_c);
+        };
+        if (pm >= 0 && pm <= 256) by_codes(std::true_type{});
+        else by_codes(std::false_type{});
+        return hipGetLastError();
+    }
     const int32_t pen_max = 4 * (sc.match - sc.mismatch);  // the i32 fills' V'' scale
     // a coder wave per stripe while the pipeline is short (a few stripes in
     // the launch: the C1 latency case)
@@ -2501,6 +2831,16 @@ Geom variant_geom(int v) { return kVariants[v]; }
 // 40.1 ms) although the step is cheaper; once the stripe waves fill the chip
 // it wins (400 x 5 kbp pairs: 8.0 vs 9.2 ms end to end).  Chosen per plan
 // from the stripe-wave count; SALN_STRIPE_PK=0 / 1 forces it.
+int stripe_rows_k() {
+    static const int k = [] {  // SALN_ROWS_K = 0 (skewed stripe fill), 1, 2 or 4
+        const char *e = std::getenv("SALN_ROWS_K");
+        if (!e) return 1;
+        const int v = std::atoi(e);
+        return v == 0 || v == 2 || v == 4 ? v : 1;
+    }();
+    return k;
+}
+
 bool stripe_packed(const Scoring &sc, uint64_t n_waves) {
     const char *e = std::getenv("SALN_STRIPE_PK");
     if (e && e[0] == '0') return false;
