@@ -1713,6 +1713,10 @@ constexpr uint32_t kRowsOff = SALN_ROWS_OFF;
 #ifndef SALN_ROWS_BCAST
 #define SALN_ROWS_BCAST 1  // experiment switch: branch-free boundary publication (0: lane 63 stores)
 #endif
+#ifndef SALN_ROWS_G
+#define SALN_ROWS_G 8  // experiment switch: rows per boundary group (4, 8 or 16)
+#endif
+constexpr uint32_t kRowsGrp = SALN_ROWS_G;
 #ifndef SALN_ROWS_INDEP
 #define SALN_ROWS_INDEP 0  // experiment builds only: stripes ignore their left neighbour
 #endif
@@ -1886,33 +1890,40 @@ __global__ __launch_bounds__(64) void nw_fill_rows_kernel(
     // re-polled with ordinary (compiler-waited) loads.
     auto rows = [&](auto F) __attribute__((always_inline)) {
         constexpr bool kFirst = decltype(F)::value || SALN_ROWS_INDEP;
-        uint64_t nv = 0;  // lanes 0-3: (H~, I~) of the next group's rows
+        constexpr uint32_t kG = kRowsGrp;  // rows per boundary group
+        uint64_t nv = 0;  // lanes 0..kG-1: (H~, I~) of the next group's rows
         auto fetch = [&](uint32_t r0) __attribute__((always_inline)) {
-            if (!kFirst && lane < 4 && r0 + (uint32_t)lane <= ld)
+            if (!kFirst && lane < (int)kG && r0 + (uint32_t)lane <= ld)
                 asm volatile("global_load_dwordx2 %0, %1, off sc1"
                              : "=v"(nv) : "v"(scr_in + r0 + kRowsOff + lane) : "memory");
         };
         fetch(1);
         if constexpr (!kFirst) asm volatile("s_waitcnt vmcnt(0)" : "+v"(nv) : : "memory");
-        int32_t bh[4], bi[4];  // the boundary of rows r .. r+3
+        int32_t bh[kG], bi[kG];  // the boundary of rows r .. r+kG-1
         auto group = [&](uint32_t r) __attribute__((always_inline)) {
             if constexpr (kFirst) {
 #pragma unroll
-                for (int q = 0; q < 4; ++q) {
+                for (uint32_t q = 0; q < kG; ++q) {
                     bi[q] = is4_col1(sc, r + q) + alpha * (int32_t)(r + q) + beta;
                     bh[q] = hs4_col0(sc, r + q) + alpha * (int32_t)(r + q);
                 }
             } else {
-                if constexpr (kCodes == kCodesNone)
-                    asm volatile("s_waitcnt vmcnt(3)" : "+v"(nv) : : "memory");
-                else
-                    asm volatile("s_waitcnt vmcnt(7)" : "+v"(nv) : : "memory");
+                // kG mask stores and kG boundary stores followed the prefetch
+                if constexpr (kCodes == kCodesNone) {
+                    if constexpr (kG == 16) asm volatile("s_waitcnt vmcnt(15)" : "+v"(nv) : : "memory");
+                    else if constexpr (kG == 8) asm volatile("s_waitcnt vmcnt(7)" : "+v"(nv) : : "memory");
+                    else asm volatile("s_waitcnt vmcnt(3)" : "+v"(nv) : : "memory");
+                } else {
+                    if constexpr (kG == 16) asm volatile("s_waitcnt vmcnt(31)" : "+v"(nv) : : "memory");
+                    else if constexpr (kG == 8) asm volatile("s_waitcnt vmcnt(15)" : "+v"(nv) : : "memory");
+                    else asm volatile("s_waitcnt vmcnt(7)" : "+v"(nv) : : "memory");
+                }
                 int32_t cH = (int32_t)(uint32_t)nv, cI = (int32_t)(uint32_t)(nv >> 32);
-                bool ok = !(lane < 4 && r + (uint32_t)lane <= ld) || (uint32_t)cH != kColEmpty;
+                bool ok = !(lane < (int)kG && r + (uint32_t)lane <= ld) || (uint32_t)cH != kColEmpty;
                 uint32_t spins = 0;
                 while (__builtin_amdgcn_ballot_w64(!ok) && !failed) {  // not yet published: poll
                     __builtin_amdgcn_s_sleep(1);
-                    if (lane < 4 && r + (uint32_t)lane <= ld) {
+                    if (lane < (int)kG && r + (uint32_t)lane <= ld) {
                         const uint64_t v = __hip_atomic_load((const uint64_t *)(scr_in + r + kRowsOff + lane),
                                                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                         cH = (int32_t)(uint32_t)v;
@@ -1921,59 +1932,96 @@ __global__ __launch_bounds__(64) void nw_fill_rows_kernel(
                     }
                     if (++spins > kSpinCap) failed = true;
                 }
-                fetch(r + 4);
+                fetch(r + kG);
 #pragma unroll
-                for (int q = 0; q < 4; ++q) {
+                for (uint32_t q = 0; q < kG; ++q) {
                     bh[q] = __builtin_amdgcn_readlane(cH, q);
                     bi[q] = __builtin_amdgcn_readlane(cI, q);
                 }
             }
         };
-    uint32_t r = 1;
-    for (; r + 3 <= ld; r += 4) {  // four rows: one scalar word of db chars
-        const uint32_t w = doff ? (dcur >> doff) | (dnxt << (32u - doff)) : dcur;
-        dcur = dnxt;
-        dnidx = min(dnidx + 1, last_dw);
-        dnxt = dw[dnidx];
-        group(r);
-        if constexpr (K == 4) {
-            row(r, (w & 0xFFu) << 8, bh[0], bi[0], u0, q0); put(r, 1);
-            row(r + 1, ((w >> 8) & 0xFFu) << 8, bh[1], bi[1], u0, q1); put(r + 1, 1);
-            row(r + 2, ((w >> 16) & 0xFFu) << 8, bh[2], bi[2], u0, q2); put(r + 2, 1);
-            row(r + 3, (w >> 24) << 8, bh[3], bi[3], u0, q3); put(r + 3, 1);
-        } else if constexpr (K == 2) {
-            row(r, (w & 0xFFu) << 8, bh[0], bi[0], u0, q0);
-            row(r + 1, ((w >> 8) & 0xFFu) << 8, bh[1], bi[1], u1, q1); put(r, 2);
-            row(r + 2, ((w >> 16) & 0xFFu) << 8, bh[2], bi[2], u0, q2);
-            row(r + 3, (w >> 24) << 8, bh[3], bi[3], u1, q3); put(r + 2, 2);
-        } else {
-            row(r, (w & 0xFFu) << 8, bh[0], bi[0], u0, q0);
-            row(r + 1, ((w >> 8) & 0xFFu) << 8, bh[1], bi[1], u1, q1);
-            row(r + 2, ((w >> 16) & 0xFFu) << 8, bh[2], bi[2], u2, q2);
-            row(r + 3, (w >> 24) << 8, bh[3], bi[3], u3, q3);
-            put(r, 4);
+        // four rows r .. r+3 of a group (their boundary at bh/bi[o .. o+3])
+        auto quad = [&](uint32_t r, auto o_c) __attribute__((always_inline)) {
+            constexpr int o = decltype(o_c)::value;
+            const uint32_t w = doff ? (dcur >> doff) | (dnxt << (32u - doff)) : dcur;
+            dcur = dnxt;
+            dnidx = min(dnidx + 1, last_dw);
+            dnxt = dw[dnidx];
+            if constexpr (K == 4) {
+                row(r, (w & 0xFFu) << 8, bh[o], bi[o], u0, q0); put(r, 1);
+                row(r + 1, ((w >> 8) & 0xFFu) << 8, bh[o + 1], bi[o + 1], u0, q1); put(r + 1, 1);
+                row(r + 2, ((w >> 16) & 0xFFu) << 8, bh[o + 2], bi[o + 2], u0, q2); put(r + 2, 1);
+                row(r + 3, (w >> 24) << 8, bh[o + 3], bi[o + 3], u0, q3); put(r + 3, 1);
+            } else if constexpr (K == 2) {
+                row(r, (w & 0xFFu) << 8, bh[o], bi[o], u0, q0);
+                row(r + 1, ((w >> 8) & 0xFFu) << 8, bh[o + 1], bi[o + 1], u1, q1); put(r, 2);
+                row(r + 2, ((w >> 16) & 0xFFu) << 8, bh[o + 2], bi[o + 2], u0, q2);
+                row(r + 3, (w >> 24) << 8, bh[o + 3], bi[o + 3], u1, q3); put(r + 2, 2);
+            } else {
+                row(r, (w & 0xFFu) << 8, bh[o], bi[o], u0, q0);
+                row(r + 1, ((w >> 8) & 0xFFu) << 8, bh[o + 1], bi[o + 1], u1, q1);
+                row(r + 2, ((w >> 16) & 0xFFu) << 8, bh[o + 2], bi[o + 2], u2, q2);
+                row(r + 3, (w >> 24) << 8, bh[o + 3], bi[o + 3], u3, q3);
+                put(r, 4);
+            }
+        };
+        // the last 1-3 rows (boundary at bh/bi[o ..])
+        auto tail = [&](uint32_t r, auto o_c) __attribute__((always_inline)) {
+            constexpr int o = decltype(o_c)::value;
+            const uint32_t w = doff ? (dcur >> doff) | (dnxt << (32u - doff)) : dcur;
+            const uint32_t n = ld - r + 1;
+            if constexpr (K == 4) {
+                row(r, (w & 0xFFu) << 8, bh[o], bi[o], u0, q0); put(r, 1);
+                if (n > 1) { row(r + 1, ((w >> 8) & 0xFFu) << 8, bh[o + 1], bi[o + 1], u0, q1); put(r + 1, 1); }
+                if (n > 2) { row(r + 2, ((w >> 16) & 0xFFu) << 8, bh[o + 2], bi[o + 2], u0, q2); put(r + 2, 1); }
+            } else if constexpr (K == 2) {
+                row(r, (w & 0xFFu) << 8, bh[o], bi[o], u0, q0);
+                if (n > 1) row(r + 1, ((w >> 8) & 0xFFu) << 8, bh[o + 1], bi[o + 1], u1, q1);
+                put(r, min(n, 2u));
+                if (n > 2) { row(r + 2, ((w >> 16) & 0xFFu) << 8, bh[o + 2], bi[o + 2], u0, q2); put(r + 2, 1); }
+            } else {
+                row(r, (w & 0xFFu) << 8, bh[o], bi[o], u0, q0);
+                if (n > 1) row(r + 1, ((w >> 8) & 0xFFu) << 8, bh[o + 1], bi[o + 1], u1, q1);
+                if (n > 2) row(r + 2, ((w >> 16) & 0xFFu) << 8, bh[o + 2], bi[o + 2], u2, q2);
+                put(r, n);
+            }
+        };
+        const std::integral_constant<int, 0> o0;
+        const std::integral_constant<int, 4> o4;
+        const std::integral_constant<int, 8> o8;
+        const std::integral_constant<int, 12> o12;
+        uint32_t r = 1;
+        for (; r + kG - 1 <= ld; r += kG) {
+            group(r);
+            quad(r, o0);
+            if constexpr (kG >= 8) quad(r + 4, o4);
+            if constexpr (kG >= 16) {
+                quad(r + 8, o8);
+                quad(r + 12, o12);
+            }
         }
-    }
-    if (r <= ld) {  // 1-3 tail rows
-        const uint32_t w = doff ? (dcur >> doff) | (dnxt << (32u - doff)) : dcur;
-        const uint32_t n = ld - r + 1;
-        group(r);
-        if constexpr (K == 4) {
-            row(r, (w & 0xFFu) << 8, bh[0], bi[0], u0, q0); put(r, 1);
-            if (n > 1) { row(r + 1, ((w >> 8) & 0xFFu) << 8, bh[1], bi[1], u0, q1); put(r + 1, 1); }
-            if (n > 2) { row(r + 2, ((w >> 16) & 0xFFu) << 8, bh[2], bi[2], u0, q2); put(r + 2, 1); }
-        } else if constexpr (K == 2) {
-            row(r, (w & 0xFFu) << 8, bh[0], bi[0], u0, q0);
-            if (n > 1) row(r + 1, ((w >> 8) & 0xFFu) << 8, bh[1], bi[1], u1, q1);
-            put(r, min(n, 2u));
-            if (n > 2) { row(r + 2, ((w >> 16) & 0xFFu) << 8, bh[2], bi[2], u0, q2); put(r + 2, 1); }
-        } else {
-            row(r, (w & 0xFFu) << 8, bh[0], bi[0], u0, q0);
-            if (n > 1) row(r + 1, ((w >> 8) & 0xFFu) << 8, bh[1], bi[1], u1, q1);
-            if (n > 2) row(r + 2, ((w >> 16) & 0xFFu) << 8, bh[2], bi[2], u2, q2);
-            put(r, n);
+        if (r <= ld) {  // fewer than kG rows left: one partial group
+            group(r);
+            const uint32_t nq = (ld - r + 1) / 4;  // full quads, < kG / 4
+            const bool t = (ld - r + 1) % 4 != 0;
+            if (nq == 0) {
+                tail(r, o0);
+            } else if constexpr (kG == 8) {
+                quad(r, o0);
+                if (t) tail(r + 4, o4);
+            } else if constexpr (kG >= 16) {
+                quad(r, o0);
+                if (nq > 1) quad(r + 4, o4);
+                if (nq == 1) {
+                    if (t) tail(r + 4, o4);
+                } else if (nq == 2) {
+                    if (t) tail(r + 8, o8);
+                } else {
+                    quad(r + 8, o8);
+                    if (t) tail(r + 12, o12);
+                }
+            }
         }
-    }
     };
     if (g == 0) rows(std::true_type{});
     else rows(std::false_type{});
@@ -2834,9 +2882,9 @@ Geom variant_geom(int v) { return kVariants[v]; }
 int stripe_rows_k() {
     static const int k = [] {  // SALN_ROWS_K = 0 (skewed stripe fill), 1, 2 or 4
         const char *e = std::getenv("SALN_ROWS_K");
-        if (!e) return 1;
+        if (!e) return 2;
         const int v = std::atoi(e);
-        return v == 0 || v == 2 || v == 4 ? v : 1;
+        return v == 0 || v == 1 || v == 4 ? v : 2;
     }();
     return k;
 }
