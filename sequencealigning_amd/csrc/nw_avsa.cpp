@@ -163,7 +163,10 @@ int saln_nw_avsa_execute(saln_nw_avsa *a, const uint8_t *d_q_seq, const uint8_t 
     hipStream_t s = resolve_stream(stream, a->ctx);
     int2 *out = reinterpret_cast<int2 *>(d_out);
     const uint32_t nqt = (uint32_t)a->n_q;
-    constexpr uint64_t kChunk = 1ull << 30;  // pairs per launch (uint32 index space)
+    // pairs per launch: the dispatch packet's grid size is a 32-bit count of
+    // work-items (a larger grid is silently truncated), and a 256-thread block
+    // of the packed fill covers 2 * (256 / G) >= 8 pairs
+    constexpr uint64_t kChunk = 1ull << 28;
     for (const auto &c : a->classes) {
         const uint64_t total = (uint64_t)c.nq * a->n_dn;
         for (uint64_t base = 0; base < total; base += kChunk) {

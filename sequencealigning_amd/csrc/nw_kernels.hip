@@ -2606,6 +2606,7 @@ static hipError_t avsa_pk(const AvsaSrc &src, uint32_t count, const uint8_t *qs,
     const uint32_t sup = 8 * blocks_per_pack(2 * gpb);
     const uint32_t groups = (count + 1) / 2;
     const dim3 grid(((groups + gpb - 1) / gpb + sup - 1) / sup * sup);
+    if ((uint64_t)grid.x * 256 > 0xFFFFFFFFull) return hipErrorInvalidConfiguration;  // 32-bit grid
     const bool rebase = !packed_ok(G * K, ld_max, sc);
     const size_t lds = (size_t)gpb * (ld_max + 2 * G) * (rebase ? 2 : 4);
     if (lds > kPackedLdsMax) return hipErrorInvalidValue;

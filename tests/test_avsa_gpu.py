@@ -54,3 +54,34 @@ def test_avsa_matches_plan_at_scale(saln, oracle):
         di, qi = int(rng.integers(nd)), int(rng.integers(nq))
         o = oracle.nw(queries[qi], dbs[di], literal_dfs=False)
         assert scores[di, qi] == o.score
+
+
+def test_avsa_full_configs4_sample(saln, oracle):
+    """configs[4] at full size (10^4 x 10^5 pairs of 150 bp, 10^9 pairs, an
+    8 GB result): a seeded sample of pairs spread over the whole index space
+    equals the oracle (guards the launch chunking: a dispatch's grid is a
+    32-bit work-item count)."""
+    import torch
+    from sequencealigning_amd import synth
+    L, nq, ndb, seed = 150, 10_000, 100_000, 0x5EED0004
+    qs = synth.random_bases(seed, nq * L)
+    ds = synth.random_bases(seed ^ 0xD5D5D5D5, ndb * L)
+    qo = np.arange(nq + 1, dtype=np.uint64) * np.uint64(L)
+    do = np.arange(ndb + 1, dtype=np.uint64) * np.uint64(L)
+    av = saln.NwAllVsAll(qo, do)
+    out = torch.zeros(nq * ndb * 2, dtype=torch.int32, device="cuda")
+    av.execute(torch.from_numpy(qs).cuda(), torch.from_numpy(ds).cuda(), out)
+    torch.cuda.synchronize()
+    rng = np.random.default_rng(7)
+    di = np.concatenate([rng.integers(0, ndb, 200), [ndb - 1, ndb - 1, 0]])
+    qi = np.concatenate([rng.integers(0, nq, 200), [nq - 1, 0, nq - 1]])
+    pos = torch.from_numpy((di * nq * 2 + qi * 2).astype(np.int64)).cuda()
+    sc = out[pos].cpu().numpy()
+    st = out[pos + 1].cpu().numpy()
+    allq, alld = qs.tobytes(), ds.tobytes()
+    o2 = np.arange(len(di) + 1, dtype=np.uint64) * np.uint64(L)
+    want = oracle.check_pairs(b"".join(allq[int(q) * L:(int(q) + 1) * L] for q in qi), o2,
+                              b"".join(alld[int(d) * L:(int(d) + 1) * L] for d in di), o2)
+    assert np.array_equal(sc, want.score)
+    assert np.array_equal(st == saln._lib.REF_PANIC_BOUNDARY, want.panics)
+    av.close()
