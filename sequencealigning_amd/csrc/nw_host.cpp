@@ -260,14 +260,20 @@ int saln_nw_plan_create(saln_context *ctx, const uint64_t *q_off, uint64_t n_q,
         p->h_pairs[r] = d;
     }
     {
-        uint64_t waves = 0;  // stripe waves of the plan
+        uint64_t waves = 0, cols = 0;  // 256-column stripe chunks, query columns
         bool free_all = true;  // the packed stripes carry no alive flag (nw_common.hpp)
         for (uint32_t r = 0; r < p->var_count[kStripeVariant]; ++r) {
             const NwPairDesc &d = p->h_pairs[p->var_first[kStripeVariant] + r];
             waves += variant_geom(kStripeVariant).n_chunks(d.len_q);
+            cols += d.len_q;
             free_all = free_all && sentinel_free(p->sc, d.len_q, d.len_db);
         }
-        p->stripe_pk = waves > 0 && free_all && stripe_packed(p->sc, waves);
+        // packed stripes (int16x2, throughput) for batches of wide pairs; the
+        // row fill (i32, latency) otherwise: 400 x 2 kbp^2 828 vs 678 GCUPS,
+        // 400 x 5 kbp^2 953 vs 1,204 (one box, round 2)
+        const bool wide = p->var_count[kStripeVariant] &&
+                          cols / p->var_count[kStripeVariant] >= 3000;
+        p->stripe_pk = waves > 0 && free_all && stripe_packed(p->sc, waves, wide);
         p->stripe_rows = p->stripe_pk ? 0 : stripe_rows_k();
     }
     // Mask packs: up to 64 consecutive pairs of a variant (one traceback

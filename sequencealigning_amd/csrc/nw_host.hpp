@@ -92,7 +92,7 @@ constexpr uint32_t kStripeSubMax = 4;
 int stripe_rows_k();
 // column stripes run the packed (int16 halves) fill for this scoring and
 // this many stripe waves in the plan (decided once per plan: it sets the layout)
-bool stripe_packed(const Scoring &sc, uint64_t n_waves);
+bool stripe_packed(const Scoring &sc, uint64_t n_waves, bool wide);
 constexpr int kWidePackedVariant = 8;        // packed, 64-lane groups, up to 1,024 columns
 constexpr uint64_t kWidePackedMinPairs = 1536;  // fewer such pairs: column stripes (measured crossover 1,024-2,048)
 hipError_t launch_score_results(const NwPairDesc *pairs, uint32_t first, uint32_t n,

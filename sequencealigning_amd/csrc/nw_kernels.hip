@@ -26,7 +26,7 @@
 #include "saln.h"
 
 namespace saln {
-bool stripe_packed(const Scoring &sc, uint64_t n_waves);
+bool stripe_packed(const Scoring &sc, uint64_t n_waves, bool wide);
 }
 
 #ifndef SALN_PINGPONG
@@ -2890,10 +2890,10 @@ int stripe_rows_k() {
     return k;
 }
 
-bool stripe_packed(const Scoring &sc, uint64_t n_waves) {
+bool stripe_packed(const Scoring &sc, uint64_t n_waves, bool wide) {
     const char *e = std::getenv("SALN_STRIPE_PK");
     if (e && e[0] == '0') return false;
-    if (!(e && e[0] == '1') && n_waves < kStripePkMinWaves) return false;
+    if (!(e && e[0] == '1') && (n_waves < kStripePkMinWaves || !wide)) return false;
     const int64_t pen = 2ll * (sc.match - sc.mismatch);
     if (pen < 2 || pen > 32 || sc.gap_extend > 0 || sc.gap_open > 0) return false;
     const int64_t m = std::abs(sc.match), ge = std::abs(sc.gap_extend), go = std::abs(sc.gap_open);

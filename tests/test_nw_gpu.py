@@ -329,17 +329,18 @@ def test_packed_stripe_fill(saln, oracle, monkeypatch):
 
 
 def test_packed_stripes_auto_selected(saln, oracle, monkeypatch):
-    """A plan with >= 1,024 stripe waves (kStripePkMinWaves) takes the packed
-    stripe fill and layout by itself; a sample of its pairs equals the
-    oracle, and every score equals the forced unpacked run's."""
+    """A plan with >= 1,024 stripe waves (kStripePkMinWaves) of wide
+    (>= 3,000-column) queries takes the packed stripe fill and layout by
+    itself; a sample of its pairs equals the oracle, and every score equals
+    the forced row-fill run's."""
     monkeypatch.delenv("SALN_STRIPE_PK", raising=False)
     rng = np.random.default_rng(2024)
-    n = 220  # 1,100-column queries: 5 stripes each, 1,100 waves
-    qs = [rand_seq(rng, 1100) for _ in range(n)]
+    n = 90  # 3,100-column queries: 13 chunks each, 1,170 waves
+    qs = [rand_seq(rng, 3100) for _ in range(n)]
     ds = [rand_seq(rng, int(rng.integers(200, 320))) for _ in range(n)]
     pairs = [(k, k) for k in range(n)]
     res, cig = saln.nw_align_batch(qs, ds, pairs=pairs)
-    for k in range(0, n, 11):
+    for k in range(0, n, 9):
         o = oracle.nw(qs[k], ds[k], literal_dfs=False)
         assert (int(res["score"][k]), int(res["end_states"][k]), int(res["status"][k]) == 2) == \
             (o.score, o.end_states, o.panics), k
