@@ -1376,15 +1376,26 @@ __global__ __launch_bounds__(256) void nw_fill_pk_kernel(Src src, uint32_t count
 // absent, flag-free comparisons as in the packed fill); per source, two
 // v_perm gather the bit-31 signs of the four columns into 0x00/0xFF bytes and
 // a v_bfi chain merges the sources.
-template <int kCodes>
+// kArgM = false (walk codes of rows that hold no end cell): bit 0 (argM,
+// read only at the end cell) is not gathered; merge_walk copies bit 1 there.
+template <int kCodes, bool kArgM>
 __device__ __forceinline__ uint32_t stripe_code_word(const uint32_t (&s)[8][4]) {
     uint32_t w[8];
 #pragma unroll
-    for (int t = 0; t < 8; ++t)
+    for (int t = 0; t < 8; ++t) {
+        if (t == 0 && kCodes != kCodesFull && !kArgM) {
+            w[0] = 0u;
+            continue;
+        }
         w[t] = __builtin_amdgcn_perm(s[t][1], s[t][0], 0x0C0C0B09u) |
                __builtin_amdgcn_perm(s[t][3], s[t][2], 0x0B090C0Cu);
+    }
     if constexpr (kCodes == kCodesFull) return merge_full(w);
-    return merge_walk<true>(w);
+    return merge_walk<kArgM>(w);
+}
+template <int kCodes>
+__device__ __forceinline__ uint32_t stripe_code_word(const uint32_t (&s)[8][4]) {
+    return stripe_code_word<kCodes, true>(s);
 }
 
 // kSplit (parent codes, a few stripes): the stripe's wave keeps the
@@ -1714,7 +1725,7 @@ constexpr uint32_t kRowsOff = SALN_ROWS_OFF;
 #define SALN_ROWS_BCAST 1  // experiment switch: branch-free boundary publication (0: lane 63 stores)
 #endif
 #ifndef SALN_ROWS_G
-#define SALN_ROWS_G 8  // experiment switch: rows per boundary group (4, 8 or 16)
+#define SALN_ROWS_G 8  // experiment switch: rows per boundary group (4 or 8)
 #endif
 constexpr uint32_t kRowsGrp = SALN_ROWS_G;
 #ifndef SALN_ROWS_INDEP
@@ -1788,10 +1799,15 @@ __global__ __launch_bounds__(64) void nw_fill_rows_kernel(
     uint32_t sg[8][4];  // sign words of the current code word's four cells
     // one row: r (1-based), its db char, the left boundary (H~(r, c0), I~
     // entering column c0+1) and u = its slot in the code word (compile time)
-    auto row = [&](uint32_t r, uint32_t dch, int32_t bH, int32_t bI, auto u_c, auto q_c) __attribute__((always_inline)) {
+    // m: the row may be the last one (argM bits and the reference's tie
+    // sets for the end states); every other row stores walk codes without
+    // argM, tied against H'' & ~1 with no per-row test
+    auto row = [&](uint32_t r, uint32_t dch, int32_t bH, int32_t bI, auto u_c, auto q_c,
+                   auto m_c) __attribute__((always_inline)) {
         constexpr int u = decltype(u_c)::value;
         constexpr int q = decltype(q_c)::value;  // row in its four-row group
-        const int32_t hm = (kCodes == kCodesFull || r == ld) ? ~3 : ~1;
+        constexpr bool kM = decltype(m_c)::value;
+        const int32_t hm = (kCodes == kCodesFull || (kM && r == ld)) ? ~3 : ~1;
         int32_t M[K], tO[K], P[K];
         int32_t diag = __builtin_amdgcn_update_dpp(hb_prev, Hp[K - 1], 0x138 /*wave_shr:1*/, 0xf, 0xf, false);
         uint32_t x[K];
@@ -1814,7 +1830,7 @@ __global__ __launch_bounds__(64) void nw_fill_rows_kernel(
                 const int32_t Hc = H & hm;
                 const int32_t tOr = tO[k] | kTieOr;
                 const int e = u * K + k;  // cell slot in the code word (unrolled: constant)
-                sg[0][e] = (uint32_t)(M[k] - Hc);
+                sg[0][e] = (kCodes == kCodesFull || kM) ? (uint32_t)(M[k] - Hc) : 0u;
                 sg[1][e] = (uint32_t)(I - Hc);
                 sg[2][e] = (uint32_t)(D - Hc);
                 sg[4][e] = (uint32_t)(tOr - I);
@@ -1852,9 +1868,9 @@ __global__ __launch_bounds__(64) void nw_fill_rows_kernel(
 #endif
     };
     // store the code word of rows r0 .. r0+(4/K)-1 (n of them valid)
-    auto put = [&](uint32_t r0, uint32_t n) __attribute__((always_inline)) {
+    auto put = [&](uint32_t r0, uint32_t n, auto m_c) __attribute__((always_inline)) {
         if constexpr (kCodes != kCodesNone) {
-            const uint32_t wv = stripe_code_word<kCodes>(sg);
+            const uint32_t wv = stripe_code_word<kCodes, decltype(m_c)::value>(sg);
             uint8_t *a = mrow + (uint64_t)(r0 - 1) * 256;
             if constexpr (K == 4) {
                 *reinterpret_cast<uint32_t *>(a) = wv;
@@ -1910,12 +1926,10 @@ __global__ __launch_bounds__(64) void nw_fill_rows_kernel(
             } else {
                 // kG mask stores and kG boundary stores followed the prefetch
                 if constexpr (kCodes == kCodesNone) {
-                    if constexpr (kG == 16) asm volatile("s_waitcnt vmcnt(15)" : "+v"(nv) : : "memory");
-                    else if constexpr (kG == 8) asm volatile("s_waitcnt vmcnt(7)" : "+v"(nv) : : "memory");
+                    if constexpr (kG == 8) asm volatile("s_waitcnt vmcnt(7)" : "+v"(nv) : : "memory");
                     else asm volatile("s_waitcnt vmcnt(3)" : "+v"(nv) : : "memory");
                 } else {
-                    if constexpr (kG == 16) asm volatile("s_waitcnt vmcnt(31)" : "+v"(nv) : : "memory");
-                    else if constexpr (kG == 8) asm volatile("s_waitcnt vmcnt(15)" : "+v"(nv) : : "memory");
+                    if constexpr (kG == 8) asm volatile("s_waitcnt vmcnt(15)" : "+v"(nv) : : "memory");
                     else asm volatile("s_waitcnt vmcnt(7)" : "+v"(nv) : : "memory");
                 }
                 int32_t cH = (int32_t)(uint32_t)nv, cI = (int32_t)(uint32_t)(nv >> 32);
@@ -1941,86 +1955,78 @@ __global__ __launch_bounds__(64) void nw_fill_rows_kernel(
             }
         };
         // four rows r .. r+3 of a group (their boundary at bh/bi[o .. o+3])
-        auto quad = [&](uint32_t r, auto o_c) __attribute__((always_inline)) {
+        auto quad = [&](uint32_t r, auto o_c, auto m_c) __attribute__((always_inline)) {
             constexpr int o = decltype(o_c)::value;
             const uint32_t w = doff ? (dcur >> doff) | (dnxt << (32u - doff)) : dcur;
             dcur = dnxt;
             dnidx = min(dnidx + 1, last_dw);
             dnxt = dw[dnidx];
             if constexpr (K == 4) {
-                row(r, (w & 0xFFu) << 8, bh[o], bi[o], u0, q0); put(r, 1);
-                row(r + 1, ((w >> 8) & 0xFFu) << 8, bh[o + 1], bi[o + 1], u0, q1); put(r + 1, 1);
-                row(r + 2, ((w >> 16) & 0xFFu) << 8, bh[o + 2], bi[o + 2], u0, q2); put(r + 2, 1);
-                row(r + 3, (w >> 24) << 8, bh[o + 3], bi[o + 3], u0, q3); put(r + 3, 1);
+                row(r, (w & 0xFFu) << 8, bh[o], bi[o], u0, q0, m_c); put(r, 1, m_c);
+                row(r + 1, ((w >> 8) & 0xFFu) << 8, bh[o + 1], bi[o + 1], u0, q1, m_c); put(r + 1, 1, m_c);
+                row(r + 2, ((w >> 16) & 0xFFu) << 8, bh[o + 2], bi[o + 2], u0, q2, m_c); put(r + 2, 1, m_c);
+                row(r + 3, (w >> 24) << 8, bh[o + 3], bi[o + 3], u0, q3, m_c); put(r + 3, 1, m_c);
             } else if constexpr (K == 2) {
-                row(r, (w & 0xFFu) << 8, bh[o], bi[o], u0, q0);
-                row(r + 1, ((w >> 8) & 0xFFu) << 8, bh[o + 1], bi[o + 1], u1, q1); put(r, 2);
-                row(r + 2, ((w >> 16) & 0xFFu) << 8, bh[o + 2], bi[o + 2], u0, q2);
-                row(r + 3, (w >> 24) << 8, bh[o + 3], bi[o + 3], u1, q3); put(r + 2, 2);
+                row(r, (w & 0xFFu) << 8, bh[o], bi[o], u0, q0, m_c);
+                row(r + 1, ((w >> 8) & 0xFFu) << 8, bh[o + 1], bi[o + 1], u1, q1, m_c); put(r, 2, m_c);
+                row(r + 2, ((w >> 16) & 0xFFu) << 8, bh[o + 2], bi[o + 2], u0, q2, m_c);
+                row(r + 3, (w >> 24) << 8, bh[o + 3], bi[o + 3], u1, q3, m_c); put(r + 2, 2, m_c);
             } else {
-                row(r, (w & 0xFFu) << 8, bh[o], bi[o], u0, q0);
-                row(r + 1, ((w >> 8) & 0xFFu) << 8, bh[o + 1], bi[o + 1], u1, q1);
-                row(r + 2, ((w >> 16) & 0xFFu) << 8, bh[o + 2], bi[o + 2], u2, q2);
-                row(r + 3, (w >> 24) << 8, bh[o + 3], bi[o + 3], u3, q3);
-                put(r, 4);
+                row(r, (w & 0xFFu) << 8, bh[o], bi[o], u0, q0, m_c);
+                row(r + 1, ((w >> 8) & 0xFFu) << 8, bh[o + 1], bi[o + 1], u1, q1, m_c);
+                row(r + 2, ((w >> 16) & 0xFFu) << 8, bh[o + 2], bi[o + 2], u2, q2, m_c);
+                row(r + 3, (w >> 24) << 8, bh[o + 3], bi[o + 3], u3, q3, m_c);
+                put(r, 4, m_c);
             }
         };
         // the last 1-3 rows (boundary at bh/bi[o ..])
-        auto tail = [&](uint32_t r, auto o_c) __attribute__((always_inline)) {
+        auto tail = [&](uint32_t r, auto o_c, auto m_c) __attribute__((always_inline)) {
             constexpr int o = decltype(o_c)::value;
             const uint32_t w = doff ? (dcur >> doff) | (dnxt << (32u - doff)) : dcur;
             const uint32_t n = ld - r + 1;
             if constexpr (K == 4) {
-                row(r, (w & 0xFFu) << 8, bh[o], bi[o], u0, q0); put(r, 1);
-                if (n > 1) { row(r + 1, ((w >> 8) & 0xFFu) << 8, bh[o + 1], bi[o + 1], u0, q1); put(r + 1, 1); }
-                if (n > 2) { row(r + 2, ((w >> 16) & 0xFFu) << 8, bh[o + 2], bi[o + 2], u0, q2); put(r + 2, 1); }
+                row(r, (w & 0xFFu) << 8, bh[o], bi[o], u0, q0, m_c); put(r, 1, m_c);
+                if (n > 1) { row(r + 1, ((w >> 8) & 0xFFu) << 8, bh[o + 1], bi[o + 1], u0, q1, m_c); put(r + 1, 1, m_c); }
+                if (n > 2) { row(r + 2, ((w >> 16) & 0xFFu) << 8, bh[o + 2], bi[o + 2], u0, q2, m_c); put(r + 2, 1, m_c); }
             } else if constexpr (K == 2) {
-                row(r, (w & 0xFFu) << 8, bh[o], bi[o], u0, q0);
-                if (n > 1) row(r + 1, ((w >> 8) & 0xFFu) << 8, bh[o + 1], bi[o + 1], u1, q1);
-                put(r, min(n, 2u));
-                if (n > 2) { row(r + 2, ((w >> 16) & 0xFFu) << 8, bh[o + 2], bi[o + 2], u0, q2); put(r + 2, 1); }
+                row(r, (w & 0xFFu) << 8, bh[o], bi[o], u0, q0, m_c);
+                if (n > 1) row(r + 1, ((w >> 8) & 0xFFu) << 8, bh[o + 1], bi[o + 1], u1, q1, m_c);
+                put(r, min(n, 2u), m_c);
+                if (n > 2) { row(r + 2, ((w >> 16) & 0xFFu) << 8, bh[o + 2], bi[o + 2], u0, q2, m_c); put(r + 2, 1, m_c); }
             } else {
-                row(r, (w & 0xFFu) << 8, bh[o], bi[o], u0, q0);
-                if (n > 1) row(r + 1, ((w >> 8) & 0xFFu) << 8, bh[o + 1], bi[o + 1], u1, q1);
-                if (n > 2) row(r + 2, ((w >> 16) & 0xFFu) << 8, bh[o + 2], bi[o + 2], u2, q2);
-                put(r, n);
+                row(r, (w & 0xFFu) << 8, bh[o], bi[o], u0, q0, m_c);
+                if (n > 1) row(r + 1, ((w >> 8) & 0xFFu) << 8, bh[o + 1], bi[o + 1], u1, q1, m_c);
+                if (n > 2) row(r + 2, ((w >> 16) & 0xFFu) << 8, bh[o + 2], bi[o + 2], u2, q2, m_c);
+                put(r, n, m_c);
             }
         };
         const std::integral_constant<int, 0> o0;
         const std::integral_constant<int, 4> o4;
-        const std::integral_constant<int, 8> o8;
-        const std::integral_constant<int, 12> o12;
+        const std::false_type M0;  // rows that cannot be the last one
+        const std::true_type M1;   // the last group (holds row ld)
+        static_assert(kG == 4 || kG == 8, "four or eight rows per boundary group");
         uint32_t r = 1;
-        for (; r + kG - 1 <= ld; r += kG) {
+        for (; r + kG - 1 < ld; r += kG) {  // full groups before the one holding row ld
             group(r);
-            quad(r, o0);
-            if constexpr (kG >= 8) quad(r + 4, o4);
-            if constexpr (kG >= 16) {
-                quad(r + 8, o8);
-                quad(r + 12, o12);
-            }
+            quad(r, o0, M0);
+            if constexpr (kG == 8) quad(r + 4, o4, M0);
         }
-        if (r <= ld) {  // fewer than kG rows left: one partial group
-            group(r);
-            const uint32_t nq = (ld - r + 1) / 4;  // full quads, < kG / 4
-            const bool t = (ld - r + 1) % 4 != 0;
-            if (nq == 0) {
-                tail(r, o0);
-            } else if constexpr (kG == 8) {
-                quad(r, o0);
-                if (t) tail(r + 4, o4);
-            } else if constexpr (kG >= 16) {
-                quad(r, o0);
-                if (nq > 1) quad(r + 4, o4);
-                if (nq == 1) {
-                    if (t) tail(r + 4, o4);
-                } else if (nq == 2) {
-                    if (t) tail(r + 8, o8);
-                } else {
-                    quad(r + 8, o8);
-                    if (t) tail(r + 12, o12);
-                }
+        // the last group: 1 .. kG rows, row ld among them
+        group(r);
+        const uint32_t nq = (ld - r + 1) / 4;  // full quads
+        const bool t = (ld - r + 1) % 4 != 0;
+        if (nq == 0) {
+            tail(r, o0, M1);
+        } else if constexpr (kG == 8) {
+            if (nq == 1) {
+                quad(r, o0, M1);
+                if (t) tail(r + 4, o4, M1);
+            } else {
+                quad(r, o0, M1);
+                quad(r + 4, o4, M1);
             }
+        } else {
+            quad(r, o0, M1);
         }
     };
     if (g == 0) rows(std::true_type{});
