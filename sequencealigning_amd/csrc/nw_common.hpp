@@ -65,6 +65,42 @@ struct NwPairDesc {
     uint64_t mask_cs;        // bytes from query chunk c to c+1 (G*bs unless skewed)
 };
 
+// Speculative stripe walks of a long column-stripe pair (nw_kernels.hip,
+// nw_traceback_coop_kernel<.., kSpec = true>): every 256-column walker stripe
+// of the pair walks at once from an entry (cell, kind); pass 1 guesses the
+// entries, pass k enters stripe s where pass k-1 left stripe s+1.
+enum : int32_t {
+    kSpecM = 0, kSpecI = 1, kSpecD = 2,  // state known
+    kSpecViaM = 3,  // arrived by a diagonal step: state = argmax of the cell
+    kSpecViaI = 4,  // arrived by a horizontal step: state from the I bits
+    kSpecEnd = 5,   // the pair's end cell, first end state
+    kSpecEv = 8,    // exit: walk ended (kSpecEv + event)
+    kSpecNone = 16, // no entry (the walk ended in a stripe to the right)
+};
+constexpr uint32_t kSpecOpsCap = 2 * 256 + 8;  // run words per stripe (>= 2 per column + 2)
+constexpr uint32_t kSpecMaxStripes = 4096;     // per pair (the link scan's LDS)
+constexpr uint32_t kSpecMinStripes = 8;        // shorter pairs: the cooperative walker alone
+constexpr uint32_t kSpecMaxPairs = 16;         // more column-stripe pairs walk in parallel anyway
+struct SpecStripe {
+    int32_t in_i, in_j, in_k;              // entry of the stored walk
+    int32_t out_i[2], out_j[2], out_k[2];  // exit, per pass parity
+    uint32_t nops;                         // run words (walk order, pending run last)
+    uint32_t am_end;                       // last stripe: end cell argmax set
+    int32_t base, k0;                      // link: walk-order slot of word 0, first word kept
+    uint32_t open_w;                       // link: final value of the stripe's last word
+};
+struct SpecPair {
+    uint32_t plan_idx, n_stripes, stripe_base, reserved;
+};
+struct SpecArgs {
+    const uint2 *blocks;     // spec block -> (spec pair, stripe)
+    const SpecPair *pairs;
+    SpecStripe *stripes;
+    uint32_t *ops;           // kSpecOpsCap words per stripe
+    const uint32_t *done;    // plan index -> walk finished by the spec passes
+    int32_t pass;
+};
+
 // Kernel geometry of one fill variant: G lanes per pair, K query columns per
 // lane, KD = ceil(K/4) mask dwords per lane-row segment (LB = 4*KD bytes).
 // A pair's query is cut in chunks of W = G*K columns; column block

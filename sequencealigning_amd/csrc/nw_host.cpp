@@ -66,6 +66,14 @@ struct saln_nw_plan {
     uint32_t *d_prog = nullptr, *d_err = nullptr;
     uint64_t n_prog = 0;
     uint32_t *d_ops = nullptr;  // traceback op-stream scratch (one traceback at a time)
+    // speculative stripe walks (a few long column-stripe pairs): block map,
+    // pairs, stripe records, run words, per-pair done flags (plan order)
+    uint32_t spec_pairs = 0, spec_blocks = 0;
+    int spec_passes = 0;
+    uint2 *d_spec_blocks = nullptr;
+    SpecPair *d_spec_pairs = nullptr;
+    SpecStripe *d_spec_stripes = nullptr;
+    uint32_t *d_spec_ops = nullptr, *d_spec_done = nullptr;
     uint64_t scratch_elems = 0;
     int32_t *d_endh = nullptr;
     std::vector<uint64_t> cigar_off;  // results order, n_pairs + 1
@@ -135,7 +143,9 @@ int saln_nw_plan_destroy(saln_nw_plan *p) {
     (void)hipDeviceSynchronize();  // the blocks go back to the context cache
     for (void *b : {(void *)p->d_pairs, (void *)p->d_mask, (void *)p->d_mask2, (void *)p->d_endh2,
                     (void *)p->d_scratch, (void *)p->d_work, (void *)p->d_prog, (void *)p->d_err,
-                    (void *)p->d_ops, (void *)p->d_endh})
+                    (void *)p->d_ops, (void *)p->d_endh, (void *)p->d_spec_blocks,
+                    (void *)p->d_spec_pairs, (void *)p->d_spec_stripes, (void *)p->d_spec_ops,
+                    (void *)p->d_spec_done})
         dev_free(p->ctx, b);
     for (auto &e : p->sync_ev) (void)hipEventDestroy(e);
     for (auto &t : p->ev_pool)
@@ -405,6 +415,45 @@ int saln_nw_plan_create(saln_context *ctx, const uint64_t *q_off, uint64_t n_q,
         return fail(e, "hipMalloc(scratch)");
     if (ooff && (e = dev_alloc(p->ctx, (void **)&p->d_ops, ooff * sizeof(uint32_t))) != hipSuccess)
         return fail(e, "hipMalloc(op stream)");
+    {
+        // Speculative stripe walks: a few long column-stripe pairs walk all
+        // their 256-column stripes at once (nw_traceback_coop_kernel kSpec)
+        // instead of one stripe after another (C4: walk 3.8 ms).  Off with
+        // SALN_SPEC=0; SALN_SPEC_PASSES walk passes (default 3).
+        const char *env = std::getenv("SALN_SPEC");
+        const char *pe = std::getenv("SALN_SPEC_PASSES");
+        const int passes = pe ? std::atoi(pe) : 3;
+        const uint32_t nv = p->var_count[kStripeVariant];
+        std::vector<SpecPair> sp;
+        std::vector<uint2> blocks;
+        if ((!env || std::atoi(env) != 0) && passes > 0 && nv && nv <= kSpecMaxPairs &&
+            p->sub.size() == 2) {
+            for (uint32_t r = p->var_first[kStripeVariant]; r < p->var_first[kStripeVariant] + nv; ++r) {
+                const NwPairDesc &d = p->h_pairs[r];
+                const uint32_t S = (d.len_q + 255) / 256;
+                if (S < kSpecMinStripes || S > kSpecMaxStripes) continue;
+                sp.push_back(SpecPair{r, S, (uint32_t)blocks.size(), 0});
+                for (uint32_t s = 0; s < S; ++s) blocks.push_back(make_uint2((uint32_t)sp.size() - 1, s));
+            }
+        }
+        if (!sp.empty()) {
+            p->spec_pairs = (uint32_t)sp.size();
+            p->spec_blocks = (uint32_t)blocks.size();
+            p->spec_passes = passes;
+            if ((e = dev_alloc(p->ctx, (void **)&p->d_spec_blocks, blocks.size() * sizeof(uint2))) != hipSuccess ||
+                (e = hipMemcpy(p->d_spec_blocks, blocks.data(), blocks.size() * sizeof(uint2),
+                               hipMemcpyHostToDevice)) != hipSuccess ||
+                (e = dev_alloc(p->ctx, (void **)&p->d_spec_pairs, sp.size() * sizeof(SpecPair))) != hipSuccess ||
+                (e = hipMemcpy(p->d_spec_pairs, sp.data(), sp.size() * sizeof(SpecPair),
+                               hipMemcpyHostToDevice)) != hipSuccess ||
+                (e = dev_alloc(p->ctx, (void **)&p->d_spec_stripes, blocks.size() * sizeof(SpecStripe))) != hipSuccess ||
+                (e = dev_alloc(p->ctx, (void **)&p->d_spec_ops,
+                               blocks.size() * kSpecOpsCap * sizeof(uint32_t))) != hipSuccess ||
+                (e = dev_alloc(p->ctx, (void **)&p->d_spec_done, n_pairs * sizeof(uint32_t))) != hipSuccess ||
+                (e = hipMemset(p->d_spec_done, 0, n_pairs * sizeof(uint32_t))) != hipSuccess)
+                return fail(e, "speculative walk tables");
+        }
+    }
     *out = p;
     return SALN_OK;
 }
@@ -511,11 +560,20 @@ int saln_nw_execute(saln_nw_plan *p, const uint8_t *d_q, const uint8_t *d_db,
         for (int v = 0; v < kNumVariants; ++v) {
             const uint32_t a = std::max(lo, p->var_first[v]);
             const uint32_t b = std::min(hi, p->var_first[v] + p->var_count[v]);
+            const bool spec = v == kStripeVariant && p->spec_pairs && !p->score_only;
+            if (a < b && spec)
+                HIP_TRY(launch_traceback_spec(
+                    p->d_pairs,
+                    SpecArgs{p->d_spec_blocks, p->d_spec_pairs, p->d_spec_stripes, p->d_spec_ops,
+                             p->d_spec_done, 0},
+                    p->spec_blocks, p->spec_pairs, p->d_spec_done, p->spec_passes, d_q, d_db, mask,
+                    endh, d_results, d_cigar, p->sc, p->stripe_layout(), t));
             if (a < b && p->score_only)
                 HIP_TRY(launch_score_results(p->d_pairs, a, b - a, endh, d_results, p->sc, t));
             else if (a < b)
                 HIP_TRY(launch_traceback(v, p->d_pairs, a, b - a, d_q, d_db, mask, endh, p->d_ops,
-                                         d_results, d_cigar, p->sc, p->stripe_layout(), t));
+                                         d_results, d_cigar, p->sc, p->stripe_layout(), t,
+                                         spec ? p->d_spec_done : nullptr));
         }
     }
     // pairs with an empty side (boundary-only walk) ride on the traceback stream

@@ -641,21 +641,77 @@ constexpr int32_t kCoopSlack = 64;  // rows loaded beyond a diagonal crossing of
 // packed stripe layout (bs == 0): virtual lane v = (c - c0) / 2 of row r sits
 // on line r - 1 + v (127 lines of skew); 2 the row-major 256-column tiles of
 // nw_fill_rows_kernel (no skew: row r is line r - 1).
-template <int NWV, int kLay>
+// kSpec: one block per walker stripe of a long pair (SpecArgs, nw_common.hpp):
+// the walk starts at the stripe's entry and stops where it leaves the stripe
+// (the crossing step is the stripe's last op) or ends; it writes its run
+// words and exit to the stripe's record.  A pass whose entry equals the one
+// of the stored walk keeps it (the walk is a function of (cell, state)).
+template <int NWV, int kLay, bool kSpec = false>
 __global__ __launch_bounds__(64 * NWV) void nw_traceback_coop_kernel(
     const NwPairDesc *__restrict__ pairs, uint32_t first, const uint8_t *__restrict__ mask,
     const int32_t *__restrict__ end_h, saln_nw_result *__restrict__ results,
-    uint32_t *__restrict__ cigar, Scoring sc, int32_t kCoopRows) {
+    uint32_t *__restrict__ cigar, Scoring sc, int32_t kCoopRows,
+    const uint8_t *__restrict__ qs, const uint8_t *__restrict__ ds, SpecArgs sa) {
     constexpr bool kPk = kLay == 1;
     constexpr int32_t kSkew = kLay == 1 ? 127 : kLay == 2 ? 0 : 63;  // lines from a row's first to its last block
     // kCoopRows + kSkew lines, rounded up to whole 4-line DMAs; then the
     // request words wave 0 posts to the loader waves
     extern __shared__ __attribute__((aligned(16))) uint8_t win[];
     int32_t *req = reinterpret_cast<int32_t *>(win + (kCoopRows + kSkew + 1) * kCoopLine);
+    // kLay 2: the row fill's walk codes carry no eq bit; '=' / 'X' come from
+    // the sequence bytes of the window, staged beside it: q[c_lo-2 ..
+    // c_lo+254] (the stripe's columns and the one before) and d[r_lo-2 .. i-1]
+    uint8_t *qwin = win + (kCoopRows + kSkew + 1) * kCoopLine + 16;
+    uint8_t *dwin = qwin + 272;
     const int32_t lane = (int32_t)threadIdx.x % 64, wv = (int32_t)threadIdx.x / 64;
-    const uint32_t idx = first + blockIdx.x;
+    uint32_t idx = first + blockIdx.x;
+    SpecStripe *rec = nullptr;
+    int32_t ei = 0, ej = 0, ek = 0, s_id = 0;  // kSpec: entry, stripe
+    if constexpr (kSpec) {
+        const uint2 b = sa.blocks[blockIdx.x];
+        const SpecPair sp = sa.pairs[b.x];
+        idx = sp.plan_idx;
+        s_id = (int32_t)b.y;
+        rec = sa.stripes + sp.stripe_base + b.y;
+    } else if (sa.done && sa.done[idx]) {
+        return;  // walked by the speculative passes
+    }
     const NwPairDesc p = pairs[idx];
     const uint8_t *__restrict__ m = mask + p.mask_off;
+    if constexpr (kSpec) {
+        // every wave reads the same entry (nothing writes it in this pass)
+        const int32_t lqp = (int32_t)p.len_q, ldp = (int32_t)p.len_db;
+        const int32_t par = (sa.pass - 1) & 1, cur = sa.pass & 1;
+        if (s_id == (lqp - 1) / kCoopLine) {
+            ei = ldp;
+            ej = lqp;
+            ek = kSpecEnd;
+        } else if (sa.pass == 1) {  // guess: the proportional row, state M
+            ej = kCoopLine * (s_id + 1);
+            ei = (int32_t)min((int64_t)ldp, max((int64_t)1, (int64_t)ej * ldp / lqp));
+            ek = kSpecM;
+        } else {
+            ei = rec[1].out_i[par];
+            ej = rec[1].out_j[par];
+            ek = rec[1].out_k[par];
+        }
+        if (ek >= kSpecEv) {  // the walk ends to the right of this stripe
+            if (threadIdx.x == 0) {
+                rec->in_k = kSpecNone;
+                rec->out_k[cur] = kSpecNone;
+                rec->nops = 0;
+            }
+            return;
+        }
+        if (sa.pass > 1 && rec->in_i == ei && rec->in_j == ej && rec->in_k == ek) {
+            if (threadIdx.x == 0) {  // same entry: the stored walk stands
+                rec->out_i[cur] = rec->out_i[par];
+                rec->out_j[cur] = rec->out_j[par];
+                rec->out_k[cur] = rec->out_k[par];
+            }
+            return;
+        }
+    }
     int32_t r_lo = 1, c_lo = 1;  // window: rows [r_lo, i], the stripe's columns [c_lo, c_lo+255]
     // Wave w's share of the window for cell (i, j): every NWV-th 4-line DMA.
     auto dma = [&](int32_t i, int32_t j, int32_t w) __attribute__((always_inline)) {
@@ -672,6 +728,17 @@ __global__ __launch_bounds__(64 * NWV) void nw_traceback_coop_kernel(
             const int32_t t = min(t_lo + 4 * mm + lane / 16, t_hi);  // clamped: stay in the region
             __builtin_amdgcn_global_load_lds(reg + (uint64_t)t * kCoopLine + 16 * (lane % 16),
                                              (lds_v *)(win + 4 * mm * kCoopLine), 16, 0, 0);
+        }
+        if constexpr (kLay == 2) {
+            const int32_t lqp = (int32_t)p.len_q, ldp = (int32_t)p.len_db;
+            for (int32_t k = w * 64 + lane; k < 257; k += NWV * 64) {
+                const int32_t jq = c_lo - 2 + k;  // q index
+                qwin[k] = jq >= 0 && jq < lqp ? qs[p.q_off + jq] : 0;
+            }
+            for (int32_t k = w * 64 + lane; k <= i - r_lo + 1; k += NWV * 64) {
+                const int32_t id = r_lo - 2 + k;  // d index
+                dwin[k] = id >= 0 && id < ldp ? ds[p.db_off + id] : 1;
+            }
         }
         __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): my share has landed
     };
@@ -712,16 +779,29 @@ __global__ __launch_bounds__(64 * NWV) void nw_traceback_coop_kernel(
         if constexpr (kLay == 2) return (uint32_t)win[(r - r_lo) * kCoopLine + o] ^ 0x7Fu;
         return (uint32_t)win[(r - r_lo + (o >> 2)) * kCoopLine + o] ^ 0x7Fu;
     };
-    int32_t i = ld, j = lq;
+    int32_t i = kSpec ? ei : ld, j = kSpec ? ej : lq;
     load(i, j);
     // the reference's end states (the last row's codes are unfiltered), tried
     // in the DFS's pop order: a walk from a sentinel-rooted end state dead-ends
     // and the next one is walked (walk_first)
-    const uint32_t am_end = code(i, j) & 7u;
-    uint32_t es_left = am_end;
-    int32_t st = first_end_state(es_left);
-    es_left = end_states_after(es_left, st);
-    uint32_t *out = cigar ? cigar + p.cigar_off : nullptr;
+    uint32_t am_end = 0, es_left = 0;
+    int32_t st;
+    if (!kSpec || ek == kSpecEnd) {
+        am_end = code(i, j) & 7u;
+        es_left = am_end;
+        st = first_end_state(es_left);
+        es_left = end_states_after(es_left, st);
+    } else if (ek == kSpecViaM) {  // the step into (i, j) was diagonal: its argmax
+        const uint32_t a = i == 0 ? argmax_row0_walk(sc, (uint32_t)j) : code(i, j) & 7u;
+        st = (a & kArgD) ? kStD : ((a & kArgI) ? kStI : kStM);
+    } else if (ek == kSpecViaI) {  // horizontal: the I bits of (i, j+1) sit at (i, j)
+        st = ((code(i, j) >> 3) & 2u) ? kStM : kStI;
+    } else {
+        st = ek;
+    }
+    int32_t xi = 0, xj = 0, xk = kSpecNone;  // kSpec: exit
+    uint32_t *out = kSpec ? sa.ops + (uint64_t)(rec - sa.stripes) * kSpecOpsCap
+                          : cigar ? cigar + p.cigar_off : nullptr;
     uint32_t nops = 0, run_op = 0, run_len = 0;
     // The pending run is stored at out[nops] unconditionally (every lane, one
     // address): when it merges or is empty the slot is simply rewritten later.
@@ -746,7 +826,7 @@ __global__ __launch_bounds__(64 * NWV) void nw_traceback_coop_kernel(
             if (st == kStM) ev = i == 0 && j == 0 ? kEvOrigin : kEvDead;
             else if (st == kStI) ev = j == 0 && i >= 1 ? kEvPanic : kEvDead;
             else ev = i == 0 && j >= 1 ? kEvPanic : kEvDead;
-            if (ev != kEvDead || !es_left) break;
+            if (kSpec || ev != kEvDead || !es_left) break;  // kSpec: the link checks
             // dead end state: restart from the next tied end state
             st = first_end_state(es_left);
             es_left = end_states_after(es_left, st);
@@ -775,8 +855,32 @@ __global__ __launch_bounds__(64 * NWV) void nw_traceback_coop_kernel(
         // that column from global memory
         const bool edge = st != kStD && lim_j < 0;
         uint32_t eq0 = 0;
+        if constexpr (kSpec) {
+            if (edge) {  // the crossing step is this stripe's last op
+                if (st == kStM) {
+                    push((kLay == 2 ? qwin[j - c_lo + 1] == dwin[i - r_lo + 1] : (code(i, j) >> 7) != 0)
+                             ? SALN_CIGAR_EQ : SALN_CIGAR_X, 1);
+                    xi = i - 1;
+                    xk = kSpecViaM;
+                } else {
+                    push(SALN_CIGAR_I, 1);
+                    xi = i;
+                    xk = kSpecViaI;
+                }
+                xj = j - 1;
+                ev = -1;
+                break;
+            }
+        }
+        // q == d of cell (r, c) inside the window (kLay 2: from the staged bytes)
+        auto eqbit = [&](int32_t r, int32_t c) __attribute__((always_inline)) -> uint32_t {
+            if constexpr (kLay == 2)
+                return qwin[c - c_lo + 1] == dwin[r - r_lo + 1] ? 1u : 0u;
+            else
+                return code(r, c) >> 7;
+        };
         if (edge) {  // j == c_lo > 1: this step reads column j-1 of the previous stripe
-            if (st == kStM) eq0 = code(i, j) >> 7;  // (i, j) leaves the window now
+            if (st == kStM) eq0 = eqbit(i, j);  // (i, j) leaves the window now
 #ifdef SALN_COOP_PROF
             ++pf_load;
             const uint64_t pq = __builtin_amdgcn_s_memtime();
@@ -796,8 +900,8 @@ __global__ __launch_bounds__(64 * NWV) void nw_traceback_coop_kernel(
         uint32_t eq = 0;
         if (st == kStM) {  // wave-uniform
             const int32_t ni = i - lane - 1, nj = j - lane - 1;
-            const uint32_t ce = code(i - lane, j - lane), cn = code(ni, nj);
-            eq = edge ? eq0 : ce >> 7;
+            const uint32_t cn = code(ni, nj);
+            eq = edge ? eq0 : eqbit(i - lane, j - lane);
             const uint32_t ab = ni == 0 ? argmax_row0_walk(sc, (uint32_t)nj)
                                         : argmax_col0_walk(sc, (uint32_t)ni);
             const uint32_t a = (ni == 0 || nj == 0) ? ab : cn & 7u;
@@ -871,6 +975,20 @@ __global__ __launch_bounds__(64 * NWV) void nw_traceback_coop_kernel(
         if (lane == 0 && out) out[nops] = (run_len << 4) | run_op;
         ++nops;
     }
+    if constexpr (kSpec) {
+        if (lane == 0) {
+            const int32_t cur = sa.pass & 1;
+            rec->in_i = ei;
+            rec->in_j = ej;
+            rec->in_k = ek;
+            rec->out_i[cur] = xi;
+            rec->out_j[cur] = xj;
+            rec->out_k[cur] = ev < 0 ? xk : kSpecEv + ev;
+            rec->nops = nops;
+            rec->am_end = am_end;
+        }
+        return;
+    }
     if (ev != kEvOrigin) nops = 0;
     if (out && nops > 1) {  // words were produced back to front
         __builtin_amdgcn_s_waitcnt(0x0F70);
@@ -894,6 +1012,103 @@ __global__ __launch_bounds__(64 * NWV) void nw_traceback_coop_kernel(
 #endif
         results[p.pair_id] = r;
     }
+}
+
+// Link of the speculative stripe walks of one pair (one block): the passes'
+// walks form the sequential walk when, from the last stripe (entered at the
+// end cell) down to the stripe t where the walk ends, each stripe's stored
+// walk started where the final pass left the stripe after it.  Then the
+// stripes' run words, concatenated in walk order with runs of one op merged
+// across stripe boundaries, are the walk's CIGAR back to front: a serial scan
+// places each stripe's words (base, k0, the merged value of its last word)
+// and nw_spec_copy_kernel writes them.  Otherwise, or when the walk ends dead
+// (the next tied end state would be walked), the cooperative walker runs.
+__global__ __launch_bounds__(256) void nw_spec_link_kernel(
+    const NwPairDesc *__restrict__ pairs, SpecArgs sa, uint32_t *__restrict__ done,
+    const int32_t *__restrict__ end_h, saln_nw_result *__restrict__ results) {
+    __shared__ uint32_t s_n[kSpecMaxStripes], s_first[kSpecMaxStripes], s_last[kSpecMaxStripes];
+    __shared__ int32_t t_sh, bad_sh;
+    const SpecPair sp = sa.pairs[blockIdx.x];
+    const int32_t S = (int32_t)sp.n_stripes, P = sa.pass & 1;
+    SpecStripe *rec = sa.stripes + sp.stripe_base;
+    const uint32_t *ops = sa.ops + (uint64_t)sp.stripe_base * kSpecOpsCap;
+    const int32_t tid = (int32_t)threadIdx.x;
+    if (tid == 0) {
+        t_sh = -1;
+        bad_sh = 0;
+    }
+    __syncthreads();
+    for (int32_t s = tid; s < S; s += 256)
+        if (rec[s].out_k[P] >= kSpecEv) atomicMax(&t_sh, s);
+    __syncthreads();
+    const int32_t t = t_sh;
+    const int32_t tk = t >= 0 ? rec[t].out_k[P] : kSpecNone;
+    bool bad = t < 0 || tk == kSpecNone || tk == kSpecEv + kEvDead;
+    for (int32_t s = max(t, 0) + tid; !bad && s < S - 1; s += 256) {
+        const SpecStripe &a = rec[s], &b = rec[s + 1];
+        if (a.in_i != b.out_i[P] || a.in_j != b.out_j[P] || a.in_k != b.out_k[P]) bad_sh = 1;
+    }
+    __syncthreads();
+    const uint32_t idx = sp.plan_idx;
+    if (bad || bad_sh) {
+        if (tid == 0) done[idx] = 0u;
+        return;
+    }
+    for (int32_t s = tid; s < S; s += 256) {
+        const uint32_t n = s >= t ? rec[s].nops : 0u;
+        s_n[s] = n;
+        s_first[s] = n ? ops[(uint64_t)s * kSpecOpsCap] : 0u;
+        s_last[s] = n ? ops[(uint64_t)s * kSpecOpsCap + n - 1] : 0u;
+        if (s < t) rec[s].k0 = (int32_t)n;  // nothing to copy
+    }
+    __syncthreads();
+    if (tid == 0) {
+        // walk order: stripes S-1 .. t; the open word is the last word of
+        // stripe `os`, merged with the first words of the stripes after it
+        int32_t g = 0, os = -1;
+        uint32_t oop = 0, olen = 0;
+        for (int32_t s = S - 1; s >= t; --s) {
+            const uint32_t n = s_n[s];
+            int32_t k0 = 0;
+            if (n && os >= 0 && (s_first[s] & 15u) == oop) {
+                olen += s_first[s] >> 4;
+                k0 = 1;
+            }
+            rec[s].base = g - k0;
+            rec[s].k0 = k0;
+            if ((int32_t)n > k0) {
+                if (os >= 0) rec[os].open_w = (olen << 4) | oop;
+                g += (int32_t)n - k0;
+                os = s;
+                oop = s_last[s] & 15u;
+                olen = s_last[s] >> 4;
+            }
+        }
+        if (os >= 0) rec[os].open_w = (olen << 4) | oop;
+        const NwPairDesc p = pairs[idx];
+        const int ev = tk - kSpecEv;
+        results[p.pair_id] = make_result(end_h[idx], WalkOut{ev, ev == kEvOrigin ? (uint32_t)g : 0u},
+                                         rec[S - 1].am_end);
+        done[idx] = 1u;
+    }
+}
+
+// Writes the linked stripes' run words front to back (one block per stripe).
+__global__ __launch_bounds__(64) void nw_spec_copy_kernel(
+    const NwPairDesc *__restrict__ pairs, SpecArgs sa, const saln_nw_result *__restrict__ results,
+    uint32_t *__restrict__ cigar) {
+    const uint2 b = sa.blocks[blockIdx.x];
+    const SpecPair sp = sa.pairs[b.x];
+    if (!sa.done[sp.plan_idx]) return;
+    const NwPairDesc p = pairs[sp.plan_idx];
+    const int32_t N = (int32_t)results[p.pair_id].cigar_len;
+    const SpecStripe &r = sa.stripes[sp.stripe_base + b.y];
+    const int32_t n = (int32_t)r.nops;
+    if (N == 0 || r.k0 >= n) return;
+    const uint32_t *w = sa.ops + (uint64_t)(sp.stripe_base + b.y) * kSpecOpsCap;
+    uint32_t *out = cigar + p.cigar_off;
+    for (int32_t k = r.k0 + (int32_t)threadIdx.x; k < n; k += 64)
+        out[N - 1 - (r.base + k)] = k == n - 1 ? r.open_w : w[k];
 }
 
 template <int K>
@@ -1378,19 +1593,28 @@ __global__ __launch_bounds__(256) void nw_fill_pk_kernel(Src src, uint32_t count
 // a v_bfi chain merges the sources.
 // kArgM = false (walk codes of rows that hold no end cell): bit 0 (argM,
 // read only at the end cell) is not gathered; merge_walk copies bit 1 there.
-template <int kCodes, bool kArgM>
+// kEq = false (walk codes of the row fill): no eq bit (bit 7), the
+// cooperative walker compares the sequence bytes instead.
+template <int kCodes, bool kArgM, bool kEq = true>
 __device__ __forceinline__ uint32_t stripe_code_word(const uint32_t (&s)[8][4]) {
     uint32_t w[8];
 #pragma unroll
     for (int t = 0; t < 8; ++t) {
-        if (t == 0 && kCodes != kCodesFull && !kArgM) {
-            w[0] = 0u;
+        if ((t == 0 && kCodes != kCodesFull && !kArgM) || (t == 7 && kCodes != kCodesFull && !kEq) ||
+            ((t == 3 || t == 5) && kCodes != kCodesFull)) {
+            w[t] = 0u;
             continue;
         }
         w[t] = __builtin_amdgcn_perm(s[t][1], s[t][0], 0x0C0C0B09u) |
                __builtin_amdgcn_perm(s[t][3], s[t][2], 0x0B090C0Cu);
     }
     if constexpr (kCodes == kCodesFull) return merge_full(w);
+    if constexpr (!kEq) {  // merge_walk without its last (eq) step
+        uint32_t r = kArgM ? bfi(0x01010101u, w[0], w[1]) : w[1];
+        r = bfi(0x03030303u, r, w[2]);
+        r = bfi(0x07070707u, r, w[4]);
+        return bfi(0x1F1F1F1Fu, r, w[6]);
+    }
     return merge_walk<kArgM>(w);
 }
 template <int kCodes>
@@ -1835,7 +2059,7 @@ __global__ __launch_bounds__(64) void nw_fill_rows_kernel(
                 sg[2][e] = (uint32_t)(D - Hc);
                 sg[4][e] = (uint32_t)(tOr - I);
                 sg[6][e] = (uint32_t)(tOr - D);
-                sg[7][e] = x[k] - 1u;  // sign <=> q == d
+                sg[7][e] = kCodes == kCodesFull ? x[k] - 1u : 0u;  // sign <=> q == d (full codes)
                 if constexpr (kCodes == kCodesFull) {
                     const int32_t tOc = tO[k] & ~3;
                     sg[3][e] = (uint32_t)(I - tOc);
@@ -1870,7 +2094,7 @@ __global__ __launch_bounds__(64) void nw_fill_rows_kernel(
     // store the code word of rows r0 .. r0+(4/K)-1 (n of them valid)
     auto put = [&](uint32_t r0, uint32_t n, auto m_c) __attribute__((always_inline)) {
         if constexpr (kCodes != kCodesNone) {
-            const uint32_t wv = stripe_code_word<kCodes, decltype(m_c)::value>(sg);
+            const uint32_t wv = stripe_code_word<kCodes, decltype(m_c)::value, false>(sg);
             uint8_t *a = mrow + (uint64_t)(r0 - 1) * 256;
             if constexpr (K == 4) {
                 *reinterpret_cast<uint32_t *>(a) = wv;
@@ -2746,7 +2970,8 @@ static void tb_lds(dim3 grid, hipStream_t s, const NwPairDesc *pairs, uint32_t f
 hipError_t launch_traceback(int variant, const NwPairDesc *pairs, uint32_t first, uint32_t n,
                             const uint8_t *qs, const uint8_t *ds, const uint8_t *mask,
                             const int32_t *end_h, uint32_t *ops, saln_nw_result *results,
-                            uint32_t *cigar, Scoring sc, int stripe_layout, hipStream_t stream) {
+                            uint32_t *cigar, Scoring sc, int stripe_layout, hipStream_t stream,
+                            const uint32_t *spec_done) {
     if (n == 0) return hipSuccess;
     const dim3 grid((n + 255) / 256);
     switch (variant) {
@@ -2764,10 +2989,14 @@ hipError_t launch_traceback(int variant, const NwPairDesc *pairs, uint32_t first
                     (const void *)nw_traceback_coop_kernel<kLoaders, kLay>,
                     hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
                 if (attr != hipSuccess) return attr;
-                const int32_t rows = n <= 256 ? 632 - (kSkew + 1) : 128;
+                // kLay 2: the window's sequence bytes (272 + rows + 8) beside it
+                const int32_t rows = n <= 256 ? (kLay == 2 ? 628 : 632 - (kSkew + 1)) : 128;
+                const size_t seq = kLay == 2 ? 272 + (size_t)rows + 16 : 0;
                 nw_traceback_coop_kernel<kLoaders, kLay>
-                    <<<dim3(n), dim3(64 * kLoaders), (size_t)(rows + kSkew + 1) * kCoopLine + 16,
-                       stream>>>(pairs, first, mask, end_h, results, cigar, sc, rows);
+                    <<<dim3(n), dim3(64 * kLoaders),
+                       (size_t)(rows + kSkew + 1) * kCoopLine + 16 + seq, stream>>>(
+                        pairs, first, mask, end_h, results, cigar, sc, rows, qs, ds,
+                        SpecArgs{nullptr, nullptr, nullptr, nullptr, spec_done, 0});
                 return hipSuccess;
             };
             const hipError_t e = stripe_layout == 1   ? go(std::integral_constant<int, 1>{})
@@ -2786,6 +3015,46 @@ hipError_t launch_traceback(int variant, const NwPairDesc *pairs, uint32_t first
             nw_traceback_kernel<<<grid, dim3(256), 0, stream>>>(pairs, first, n, qs, ds, mask,
                                                                 end_h, results, cigar, sc, gt);
         }
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_traceback_spec(const NwPairDesc *pairs, SpecArgs sa, uint32_t n_blocks,
+                                 uint32_t n_spec_pairs, uint32_t *done, int passes,
+                                 const uint8_t *qs, const uint8_t *ds, const uint8_t *mask,
+                                 const int32_t *end_h, saln_nw_result *results, uint32_t *cigar,
+                                 Scoring sc, int stripe_layout, hipStream_t stream) {
+    if (n_blocks == 0 || passes < 1) return hipSuccess;
+    constexpr int kLoaders = 4;
+    // a stripe walk from its right edge needs ~256 + kCoopSlack rows: two
+    // blocks per CU
+    constexpr int32_t rows = 296;
+    auto go = [&](auto lay_c) -> hipError_t {
+        constexpr int kLay = decltype(lay_c)::value;
+        constexpr int32_t kSkew = kLay == 1 ? 127 : kLay == 2 ? 0 : 63;
+        const size_t lds = (size_t)(rows + kSkew + 1) * kCoopLine + 16 +
+                           (kLay == 2 ? 272 + (size_t)rows + 16 : 0);
+        static const hipError_t attr = hipFuncSetAttribute(
+            (const void *)nw_traceback_coop_kernel<kLoaders, kLay, true>,
+            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        if (attr != hipSuccess) return attr;
+        for (int k = 1; k <= passes; ++k) {
+            sa.pass = k;
+            nw_traceback_coop_kernel<kLoaders, kLay, true>
+                <<<dim3(n_blocks), dim3(64 * kLoaders), lds, stream>>>(
+                    pairs, 0, mask, end_h, results, cigar, sc, rows, qs, ds, sa);
+        }
+        return hipGetLastError();
+    };
+    const hipError_t e = stripe_layout == 1   ? go(std::integral_constant<int, 1>{})
+                         : stripe_layout == 2 ? go(std::integral_constant<int, 2>{})
+                                              : go(std::integral_constant<int, 0>{});
+    if (e != hipSuccess) return e;
+    sa.pass = passes;
+    nw_spec_link_kernel<<<dim3(n_spec_pairs), dim3(256), 0, stream>>>(pairs, sa, done, end_h, results);
+    if (cigar) {
+        sa.done = done;
+        nw_spec_copy_kernel<<<dim3(n_blocks), dim3(64), 0, stream>>>(pairs, sa, results, cigar);
     }
     return hipGetLastError();
 }

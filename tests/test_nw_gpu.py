@@ -435,6 +435,42 @@ def test_very_long_pair_linear_oracle(saln, oracle, shape):
         assert ok and s == r.score
 
 
+@pytest.mark.parametrize("passes", ["3", "1", "2"])
+def test_speculative_stripe_walks_equal_sequential(saln, monkeypatch, passes):
+    """The speculative stripe walks of long column-stripe pairs (every
+    256-column stripe walks at once, nw_traceback_coop_kernel kSpec) give the
+    sequential walker's results exactly: accepted when linked (default 3
+    passes), left to the cooperative walker when not (1 pass from guessed
+    entries rarely links).  Single pairs and one plan of several."""
+    from sequencealigning_amd import synth
+    cases = []
+    q = synth.random_bases(0x5EED0007, 30_000).tobytes()
+    cases.append((q, synth.mutate(q, 0.05, seed=7)))
+    q = synth.random_bases(0x5EED0008, 12_000).tobytes()
+    cases.append((q, synth.mutate(q, 0.15, seed=8)))
+    cases.append((synth.random_bases(41, 6_000).tobytes(), synth.random_bases(42, 6_500).tobytes()))
+    base = synth.random_bases(43, 20_000).tobytes()
+    cases.append((base, synth.mutate(base, 0.1, seed=44)[:2_500]))
+    cases.append((base[:2_300], synth.mutate(base, 0.1, seed=45)))
+
+    def run():
+        single = [saln.n_w_align(q, d) for q, d in cases]
+        res, cig = saln.nw_align_batch([c[0] for c in cases], [c[1] for c in cases],
+                                       pairs=[(k, k) for k in range(len(cases))])
+        return single, res, cig
+
+    monkeypatch.setenv("SALN_SPEC", "0")
+    seq = run()
+    monkeypatch.setenv("SALN_SPEC", "1")
+    monkeypatch.setenv("SALN_SPEC_PASSES", passes)
+    spec = run()
+    for a, b in zip(seq[0], spec[0]):
+        assert (a.score, a.end_states, a.panics, a.printed) == (b.score, b.end_states, b.panics, b.printed)
+        assert list(a.cigar) == list(b.cigar)
+    assert np.array_equal(seq[1], spec[1])
+    assert seq[2] == spec[2]
+
+
 def test_deadend_pairs_device_plan(saln, oracle):
     """Pairs whose reference DFS leaves sentinel-rooted subtrees
     (tests/golden/nw_deadend.json, oracle-pinned): nothing printed, a panic
