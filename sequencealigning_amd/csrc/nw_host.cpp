@@ -291,6 +291,13 @@ int saln_nw_plan_create(saln_context *ctx, const uint64_t *q_off, uint64_t n_q,
     // them to the pack's longest db / widest query would cost over 25 % more
     // than storing them apart.
     uint64_t moff = 0;
+    // SALN_PK_SKEW=1 (experiment): packed fills write skewed per-wave regions.
+    // C2 fill 0.97 -> 0.92 ms, but the walker's pack loses its adjacent
+    // segments (0.25 -> 0.31 ms): no net gain, the interleaved rows stay
+    const bool pk_skew = [] {
+        const char *e = std::getenv("SALN_PK_SKEW");
+        return e && std::atoi(e) != 0;
+    }();
     for (int v = 0; v < kNumVariants; ++v) {
         const Geom g = variant_geom(v);
         const uint64_t lb = g.LB();
@@ -316,6 +323,31 @@ int saln_nw_plan_create(saln_context *ctx, const uint64_t *q_off, uint64_t n_q,
                     d.mask_bs = pk ? 0u : p->stripe_rows ? (uint32_t)lb : (uint32_t)(g.W() + lb);
                     d.mask_cs = ((uint64_t)d.len_db + (pk ? 2 * g.G : g.G) - 1) * g.W();
                     moff += g.n_chunks(d.len_q) * d.mask_cs;
+                }
+            } else if (pk_skew && variant_packed(v) && v != 4) {
+                // packed fills: one region per fill wave (its 128 / G lane
+                // groups' 2 pairs each), skewed like the stripes: line t holds
+                // the segments every lane of the wave stores at step t (lane l
+                // at row t - l + 1, block l), [block][pair slot], so a store
+                // instruction writes one contiguous line instead of 64
+                // scattered segments.  Segment (i, b) of slot s is at
+                // (i - 1 + b) * rs + b * P * LB + s * LB: rs = line, bs = rs + P * LB.
+                const uint32_t P = 128 / g.G;  // pairs per fill wave
+                const uint64_t line = (uint64_t)g.G * P * lb;
+                for (uint32_t w0 = 0; w0 < np; w0 += P) {
+                    const uint32_t nw = std::min<uint32_t>(P, np - w0);
+                    uint64_t ldw = 0;
+                    for (uint32_t s = 0; s < nw; ++s)
+                        ldw = std::max<uint64_t>(ldw, p->h_pairs[a + w0 + s].len_db);
+                    const uint64_t lines = ldw + g.G - 1;
+                    for (uint32_t s = 0; s < nw; ++s) {
+                        NwPairDesc &d = p->h_pairs[a + w0 + s];
+                        d.mask_off = moff + s * lb;
+                        d.mask_rs = line;
+                        d.mask_bs = (uint32_t)(line + P * lb);
+                        d.mask_cs = lines * line;
+                    }
+                    moff += (lines * line + 255) & ~255ull;
                 }
             } else if (4 * packed <= 5 * own + 4096) {
                 for (uint32_t s = 0; s < np; ++s) {
@@ -682,10 +714,21 @@ int plan_pair_mask(const saln_nw_plan *p, uint64_t pair_id, PairMask *pm) {
         HIP_TRY(hipMemcpy(pm->m.data(), p->d_mask + d.mask_off, pm->m.size(), hipMemcpyDeviceToHost));
         return SALN_OK;
     }
+    const uint64_t lb = pm->g.LB();
+    if (d.mask_bs > d.mask_rs) {  // skewed packed regions: block b's rows are rs-pitched
+        const uint64_t nb = pm->g.n_blocks(d.len_q);
+        pm->rs = nb * lb;
+        pm->cs = (uint64_t)pm->g.G * lb;
+        pm->m.assign((uint64_t)d.len_db * nb * lb, 0);
+        HIP_TRY(hipSetDevice(p->ctx->device));
+        for (uint64_t b = 0; b < nb; ++b)
+            HIP_TRY(hipMemcpy2D(pm->m.data() + b * lb, nb * lb, p->d_mask + d.mask_off + b * d.mask_bs,
+                                d.mask_rs, lb, d.len_db, hipMemcpyDeviceToHost));
+        return SALN_OK;
+    }
     // every row holds rs / bs blocks (the pack's width); copy them all as
     // LB-byte rows of one bs-pitched 2-D region
     const uint64_t nb = d.mask_rs / d.mask_bs;
-    const uint64_t lb = pm->g.LB();
     pm->rs = nb * lb;
     pm->cs = (uint64_t)pm->g.G * lb;
     pm->m.resize((uint64_t)d.len_db * nb * lb);

@@ -23,7 +23,7 @@ step shapes_b 600 python tools/bench_shapes.py --shape 1000x1000 --shape 600x600
 SALN_STRIPE_PK=0 step shapes_c 600 python tools/bench_shapes.py --shape 2000x2000 --shape 5000x5000 --pairs 400
 tail -2 $O/shapes_a.log $O/shapes_b.log $O/shapes_c.log
 if [[ ${PMC:-1} == 1 ]]; then
-  PMC_SETS="FETCH_SIZE;WRITE_SIZE;SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU" step pmc 900 bash tools/pmc.sh
+  PMC_SETS="FETCH_SIZE;WRITE_SIZE;SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU;SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU" step pmc 900 bash tools/pmc.sh
   python3 tools/pmc_traffic.py gpurun_out/pmc $O/pmc_traffic.json r02 > /dev/null || exit 1
 fi
 echo done

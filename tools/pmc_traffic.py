@@ -30,9 +30,20 @@ def main(d="gpurun_out/pmc", out="profiles/pmc_traffic.json", tag=""):
         res[k] = {"read_bytes": round(fetch), "write_bytes": round(write),
                   "hbm_bytes": round(fetch + write), "dispatches": len(cs["FETCH_SIZE"])}
         for c, key in (("SQ_INSTS_VALU", "valu_wave_insts"), ("SQ_INSTS_SALU", "salu_wave_insts"),
-                       ("SQ_WAVES", "waves")):
-            if c in cs:  # per-launch means of the instruction-count pass
+                       ("SQ_WAVES", "waves"), ("SQ_WAVE_CYCLES", "wave_cycles_q"),
+                       ("SQ_BUSY_CYCLES", "busy_cycles_q"), ("SQ_WAIT_INST_ANY", "wait_inst_any_q"),
+                       ("SQ_WAIT_ANY", "wait_any_q"), ("SQ_ACTIVE_INST_VALU", "active_inst_valu_q"),
+                       ("SQ_ACTIVE_INST_ANY", "active_inst_any_q")):
+            if c in cs:  # per-launch means (SQ cycle counters in quad-cycles)
                 res[k][key] = round(sum(cs[c]) / len(cs[c]))
+        r = res[k]
+        if "wave_cycles_q" in r and r["wave_cycles_q"]:
+            # shares of the waves' lifetime: issue-stalled on a dependency /
+            # parked in s_waitcnt / issuing (disjoint, MI355X_MICROARCH.md SQ row)
+            wc = r["wave_cycles_q"]
+            for key in ("wait_inst_any_q", "wait_any_q", "active_inst_any_q", "active_inst_valu_q"):
+                if key in r:
+                    r[key.replace("_q", "_frac")] = round(r[key] / wc, 4)
     doc = {"source": "tools/pmc.sh (rocprofv3 --pmc, one counter group per pass) on "
                      "tools/prof_nw.py: 100000 x 150x150 G-iid pairs, seed 0x5EED0002",
            "round": tag, "kernels": res}
