@@ -1019,7 +1019,7 @@ __global__ __launch_bounds__(64 * NWV) void nw_traceback_coop_kernel(
 // end cell) down to the stripe t where the walk ends, each stripe's stored
 // walk started where the final pass left the stripe after it.  Then the
 // stripes' run words, concatenated in walk order with runs of one op merged
-// across stripe boundaries, are the walk's CIGAR back to front: a serial scan
+// across stripe boundaries, are the walk's CIGAR back to front: a block scan
 // places each stripe's words (base, k0, the merged value of its last word)
 // and nw_spec_copy_kernel writes them.  Otherwise, or when the walk ends dead
 // (the next tied end state would be walked), the cooperative walker runs.
@@ -1027,6 +1027,8 @@ __global__ __launch_bounds__(256) void nw_spec_link_kernel(
     const NwPairDesc *__restrict__ pairs, SpecArgs sa, uint32_t *__restrict__ done,
     const int32_t *__restrict__ end_h, saln_nw_result *__restrict__ results) {
     __shared__ uint32_t s_n[kSpecMaxStripes], s_first[kSpecMaxStripes], s_last[kSpecMaxStripes];
+    __shared__ uint8_t s_k0[kSpecMaxStripes];
+    __shared__ uint32_t s_part[256];
     __shared__ int32_t t_sh, bad_sh;
     const SpecPair sp = sa.pairs[blockIdx.x];
     const int32_t S = (int32_t)sp.n_stripes, P = sa.pass & 1;
@@ -1062,32 +1064,50 @@ __global__ __launch_bounds__(256) void nw_spec_link_kernel(
         if (s < t) rec[s].k0 = (int32_t)n;  // nothing to copy
     }
     __syncthreads();
-    if (tid == 0) {
-        // walk order: stripes S-1 .. t; the open word is the last word of
-        // stripe `os`, merged with the first words of the stripes after it
-        int32_t g = 0, os = -1;
-        uint32_t oop = 0, olen = 0;
-        for (int32_t s = S - 1; s >= t; --s) {
-            const uint32_t n = s_n[s];
-            int32_t k0 = 0;
-            if (n && os >= 0 && (s_first[s] & 15u) == oop) {
-                olen += s_first[s] >> 4;
-                k0 = 1;
+    // Walk order is stripe S-1 down to t.  After a non-empty stripe the open
+    // (last) output word has the op of the stripe's last word whether or not
+    // the stripe merged into it, so stripe s merges its first word (k0 = 1)
+    // iff its op is that of stripe s+1's last word (every stripe above t
+    // holds its crossing step, so s+1 is never empty).  A stripe starts
+    // c = n - k0 output words; base(s) = (words of the stripes above) - k0.
+    for (int32_t s = tid; s < S; s += 256)
+        s_k0[s] = (s >= t && s < S - 1 && s_n[s] && (s_first[s] & 15u) == (s_last[s + 1] & 15u))
+                      ? 1u : 0u;
+    __syncthreads();
+    // suffix sums of c over chunks of consecutive stripes (walk order)
+    const int32_t C = (S + 255) / 256;
+    const int32_t u0 = tid * C, u1 = min(S, u0 + C);  // u = S - 1 - s
+    uint32_t part = 0;
+    for (int32_t u = u0; u < u1; ++u) part += s_n[S - 1 - u] - s_k0[S - 1 - u];
+    s_part[tid] = part;
+    __syncthreads();
+    for (int32_t d = 1; d < 256; d <<= 1) {  // inclusive scan of the chunk sums
+        const uint32_t v = tid >= d ? s_part[tid - d] : 0u;
+        __syncthreads();
+        s_part[tid] += v;
+        __syncthreads();
+    }
+    uint32_t g = s_part[tid] - part;  // words before my chunk
+    for (int32_t u = u0; u < u1; ++u) {
+        const int32_t s = S - 1 - u;
+        const uint32_t n = s_n[s], k0 = s_k0[s];
+        rec[s].base = (int32_t)g - (int32_t)k0;
+        rec[s].k0 = (int32_t)k0;
+        if (n > k0) {  // my last word opens an output word: add the first words merged into it
+            uint32_t len = s_last[s] >> 4;
+            for (int32_t r = s - 1; r >= t && s_k0[r]; --r) {
+                len += s_first[r] >> 4;
+                if (s_n[r] != 1u) break;
             }
-            rec[s].base = g - k0;
-            rec[s].k0 = k0;
-            if ((int32_t)n > k0) {
-                if (os >= 0) rec[os].open_w = (olen << 4) | oop;
-                g += (int32_t)n - k0;
-                os = s;
-                oop = s_last[s] & 15u;
-                olen = s_last[s] >> 4;
-            }
+            rec[s].open_w = (len << 4) | (s_last[s] & 15u);
         }
-        if (os >= 0) rec[os].open_w = (olen << 4) | oop;
+        g += n - k0;
+    }
+    if (tid == 255) {
+        const uint32_t N = s_part[255];
         const NwPairDesc p = pairs[idx];
         const int ev = tk - kSpecEv;
-        results[p.pair_id] = make_result(end_h[idx], WalkOut{ev, ev == kEvOrigin ? (uint32_t)g : 0u},
+        results[p.pair_id] = make_result(end_h[idx], WalkOut{ev, ev == kEvOrigin ? N : 0u},
                                          rec[S - 1].am_end);
         done[idx] = 1u;
     }

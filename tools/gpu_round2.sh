@@ -17,11 +17,11 @@ step() { local name=$1 lim=$2; shift 2; timeout -k 10 $lim "$@" > $O/$name.log 2
 step bench 900 python bench.py --steps 20 --warmup 3
 tail -1 $O/bench.log | cut -c1-600
 step prof_c2 600 rocprofv3 --kernel-trace --stats -d $O/prof_c2 -o run --output-format csv -- python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline --legs none
-step prof_c4 600 rocprofv3 --kernel-trace --stats -d $O/prof_c4 -o run --output-format csv -- python3 tools/bench_long.py --len 100000 --reps 3
+step prof_c4 600 rocprofv3 --kernel-trace --stats -d $O/prof_c4 -o run --output-format csv -- python3 tools/bench_long.py --len 100000 --reps 10
 step shapes_a 600 python tools/bench_shapes.py --shape 2000x2000 --shape 5000x5000 --pairs 400
 step shapes_b 600 python tools/bench_shapes.py --shape 1000x1000 --shape 600x600 --pairs 8000
 SALN_STRIPE_PK=0 step shapes_c 600 python tools/bench_shapes.py --shape 2000x2000 --shape 5000x5000 --pairs 400
-tail -2 $O/shapes_a.log $O/shapes_b.log $O/shapes_c.log
+tail -n 2 $O/shapes_a.log $O/shapes_b.log $O/shapes_c.log
 if [[ ${PMC:-1} == 1 ]]; then
   PMC_SETS="FETCH_SIZE;WRITE_SIZE;SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU;SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU" step pmc 900 bash tools/pmc.sh
   python3 tools/pmc_traffic.py gpurun_out/pmc $O/pmc_traffic.json r02 > /dev/null || exit 1
