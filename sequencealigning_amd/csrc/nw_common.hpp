@@ -231,10 +231,10 @@ SALN_HD uint8_t dbits_row1(const Scoring &s, uint32_t j) {
     return (uint8_t)((ext >= open ? 1 : 0) | (open >= ext ? 2 : 0));
 }
 
-// int2 elements per boundary column of a multi-chunk / column-stripe pair
-// (rows 1..len_db; the row fill stores rows at r + 3 in 16-byte pairs, so the
-// stride is a multiple of four elements and at least len_db + 7).
-SALN_HD uint64_t scratch_col(uint32_t len_db) { return ((uint64_t)len_db + 10) & ~(uint64_t)3; }
+// int2 elements per boundary column of a multi-chunk / column-stripe pair:
+// rows 1..len_db, then the row fill's pad slots len_db + 1 .. len_db + 8
+// (where its lanes other than 63 publish); a multiple of four elements.
+SALN_HD uint64_t scratch_col(uint32_t len_db) { return ((uint64_t)len_db + 13) & ~(uint64_t)3; }
 
 // Scaled end value H'(len_db, len_q) when a length is 0.
 SALN_HD int32_t hs_boundary_end(const Scoring &s, uint32_t len_q, uint32_t len_db) {

@@ -1966,7 +1966,9 @@ constexpr int32_t kNegInf = INT32_MIN;
 #endif
 constexpr uint32_t kRowsOff = SALN_ROWS_OFF;
 #ifndef SALN_ROWS_BCAST
-#define SALN_ROWS_BCAST 1  // experiment switch: branch-free boundary publication (0: lane 63 stores)
+// boundary publication: 2 every lane stores (lane 63 the row, the others a
+// pad slot), 1 every lane stores lane 63's broadcast value, 0 lane 63 stores
+#define SALN_ROWS_BCAST 2
 #endif
 #ifndef SALN_ROWS_G
 #define SALN_ROWS_G 8  // experiment switch: rows per boundary group (4 or 8)
@@ -2036,6 +2038,10 @@ __global__ __launch_bounds__(64) void nw_fill_rows_kernel(
     uint32_t dcur = dw[0], dnxt = dw[dnidx];
 
     bool failed = false;
+    // SALN_ROWS_BCAST 2: the group's publication base (row r0) and my offset
+    // from it: 0 for lane 63, the pad slots ld + 1 .. ld + 8 for the others
+    const int2 *pub_base = scr_out;
+    uint32_t pub_voff = 0;
     const uint32_t jend = lq - 1;
     const bool end_lane = jend / W == g && (uint32_t)lane == (jend % W) / K;
     const uint32_t k_end = jend % K;
@@ -2049,7 +2055,7 @@ __global__ __launch_bounds__(64) void nw_fill_rows_kernel(
     auto row = [&](uint32_t r, uint32_t dch, int32_t bH, int32_t bI, auto u_c, auto q_c,
                    auto m_c) __attribute__((always_inline)) {
         constexpr int u = decltype(u_c)::value;
-        constexpr int q = decltype(q_c)::value;  // row in its four-row group
+        constexpr int q = decltype(q_c)::value;  // row in its boundary group
         constexpr bool kM = decltype(m_c)::value;
         const int32_t hm = (kCodes == kCodesFull || (kM && r == ld)) ? ~3 : ~1;
         int32_t M[K], tO[K], P[K];
@@ -2092,9 +2098,21 @@ __global__ __launch_bounds__(64) void nw_fill_rows_kernel(
             Hp[k] = H;
         }
         hb_prev = bH;
-        (void)q;
         // (H~, I~) leaving the stripe's last column (lane 63's values)
-#if SALN_ROWS_BCAST
+#if SALN_ROWS_BCAST == 2
+        {   // every lane stores its own (H~, I~) with one instruction: lane 63
+            // at row r of the column, the others at a pad slot past the db
+            // (pub_voff, set per group); no readlane, no exec change, the
+            // row's address an immediate offset from the group's base
+            const int32_t iv = max(S_incl, bI);
+            const uint64_t val = (uint64_t)(uint32_t)Hp[K - 1] | ((uint64_t)(uint32_t)iv << 32);
+            const uint32_t vo = pub_voff;  // (asm operands take locals, not captures)
+            const int2 *pb = pub_base;
+            // (a 64-bit store has no data hazard with the VALU around it)
+            asm volatile("global_store_dwordx2 %0, %1, %2 offset:%3 sc1"
+                         : : "v"(vo), "v"(val), "s"(pb), "i"(8 * q) : "memory");
+        }
+#elif SALN_ROWS_BCAST
         {   // every lane stores the broadcast pair to the same address (one
             // 8-byte write): no exec change, no branch splitting the group's
             // straight-line code
@@ -2133,10 +2151,6 @@ __global__ __launch_bounds__(64) void nw_fill_rows_kernel(
     const std::integral_constant<int, 1> u1;
     const std::integral_constant<int, 2> u2;
     const std::integral_constant<int, 3> u3;
-    const std::integral_constant<int, 0> q0;
-    const std::integral_constant<int, 1> q1;
-    const std::integral_constant<int, 2> q2;
-    const std::integral_constant<int, 3> q3;
     // The left boundary arrives per four-row group: when a group starts,
     // lanes 0-3 load the next group's four rows (agent-coherent sc1 loads,
     // issued as inline asm so that the compiler adds no wait of its own: its
@@ -2161,6 +2175,8 @@ __global__ __launch_bounds__(64) void nw_fill_rows_kernel(
         if constexpr (!kFirst) asm volatile("s_waitcnt vmcnt(0)" : "+v"(nv) : : "memory");
         int32_t bh[kG], bi[kG];  // the boundary of rows r .. r+kG-1
         auto group = [&](uint32_t r) __attribute__((always_inline)) {
+            pub_base = scr_out + r;
+            pub_voff = lane == 63 ? 0u : (ld + 1u - r) * 8u;
             if constexpr (kFirst) {
 #pragma unroll
                 for (uint32_t q = 0; q < kG; ++q) {
@@ -2201,6 +2217,10 @@ __global__ __launch_bounds__(64) void nw_fill_rows_kernel(
         // four rows r .. r+3 of a group (their boundary at bh/bi[o .. o+3])
         auto quad = [&](uint32_t r, auto o_c, auto m_c) __attribute__((always_inline)) {
             constexpr int o = decltype(o_c)::value;
+            const std::integral_constant<int, o> q0;  // rows of the boundary group
+            const std::integral_constant<int, o + 1> q1;
+            const std::integral_constant<int, o + 2> q2;
+            const std::integral_constant<int, o + 3> q3;
             const uint32_t w = doff ? (dcur >> doff) | (dnxt << (32u - doff)) : dcur;
             dcur = dnxt;
             dnidx = min(dnidx + 1, last_dw);
@@ -2226,6 +2246,9 @@ __global__ __launch_bounds__(64) void nw_fill_rows_kernel(
         // the last 1-3 rows (boundary at bh/bi[o ..])
         auto tail = [&](uint32_t r, auto o_c, auto m_c) __attribute__((always_inline)) {
             constexpr int o = decltype(o_c)::value;
+            const std::integral_constant<int, o> q0;
+            const std::integral_constant<int, o + 1> q1;
+            const std::integral_constant<int, o + 2> q2;
             const uint32_t w = doff ? (dcur >> doff) | (dnxt << (32u - doff)) : dcur;
             const uint32_t n = ld - r + 1;
             if constexpr (K == 4) {
