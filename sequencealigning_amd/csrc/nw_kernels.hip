@@ -1978,9 +1978,13 @@ constexpr uint32_t kRowsGrp = SALN_ROWS_G;
 #define SALN_ROWS_INDEP 0  // experiment builds only: stripes ignore their left neighbour
 #endif
 
-// inclusive prefix max over the wave's 64 lanes (lane order)
-__device__ __forceinline__ int32_t wave_prefix_max(int32_t v) {
+// inclusive prefix max over the wave's 64 lanes (lane order).  `fill`:
+// independent work placed inside the chain, where each dependent DPP step
+// would otherwise wait two issue slots (s_nop)
+template <class Fill>
+__device__ __forceinline__ int32_t wave_prefix_max(int32_t v, Fill &&fill) {
     v = max(v, __builtin_amdgcn_update_dpp(kNegInf, v, 0x111 /*row_shr:1*/, 0xf, 0xf, false));
+    fill();
     v = max(v, __builtin_amdgcn_update_dpp(kNegInf, v, 0x112 /*row_shr:2*/, 0xf, 0xf, false));
     v = max(v, __builtin_amdgcn_update_dpp(kNegInf, v, 0x114 /*row_shr:4*/, 0xf, 0xf, false));
     v = max(v, __builtin_amdgcn_update_dpp(kNegInf, v, 0x118 /*row_shr:8*/, 0xf, 0xf, false));
@@ -2053,7 +2057,7 @@ __global__ __launch_bounds__(64) void nw_fill_rows_kernel(
     // sets for the end states); every other row stores walk codes without
     // argM, tied against H'' & ~1 with no per-row test
     auto row = [&](uint32_t r, uint32_t dch, int32_t bH, int32_t bI, auto u_c, auto q_c,
-                   auto m_c) __attribute__((always_inline)) {
+                   auto m_c, auto &&fill) __attribute__((always_inline)) {
         constexpr int u = decltype(u_c)::value;
         constexpr int q = decltype(q_c)::value;  // row in its boundary group
         constexpr bool kM = decltype(m_c)::value;
@@ -2069,7 +2073,7 @@ __global__ __launch_bounds__(64) void nw_fill_rows_kernel(
             tO[k] = M[k] + kOpen;
             P[k] = k == 0 ? tO[0] : max(P[k - 1], tO[k]);
         }
-        const int32_t S_incl = wave_prefix_max(P[K - 1]);
+        const int32_t S_incl = wave_prefix_max(P[K - 1], fill);
         const int32_t Ein = max(__builtin_amdgcn_update_dpp(kNegInf, S_incl, 0x138, 0xf, 0xf, false), bI);
 #pragma unroll
         for (int k = 0; k < K; ++k) {
@@ -2147,6 +2151,7 @@ __global__ __launch_bounds__(64) void nw_fill_rows_kernel(
             }
         }
     };
+    auto nofill = []() __attribute__((always_inline)) {};
     const std::integral_constant<int, 0> u0;
     const std::integral_constant<int, 1> u1;
     const std::integral_constant<int, 2> u2;
@@ -2215,8 +2220,13 @@ __global__ __launch_bounds__(64) void nw_fill_rows_kernel(
             }
         };
         // four rows r .. r+3 of a group (their boundary at bh/bi[o .. o+3])
-        auto quad = [&](uint32_t r, auto o_c, auto m_c) __attribute__((always_inline)) {
+        // K = 2: fill0 runs inside row r's prefix chain (the previous quad's
+        // last code word); kFlush = false leaves rows r+2, r+3's code word to
+        // the caller (the next quad's fill0)
+        auto quad = [&](uint32_t r, auto o_c, auto m_c, auto &&fill0, auto flush_c)
+                        __attribute__((always_inline)) {
             constexpr int o = decltype(o_c)::value;
+            constexpr bool kFlush = decltype(flush_c)::value;
             const std::integral_constant<int, o> q0;  // rows of the boundary group
             const std::integral_constant<int, o + 1> q1;
             const std::integral_constant<int, o + 2> q2;
@@ -2226,20 +2236,23 @@ __global__ __launch_bounds__(64) void nw_fill_rows_kernel(
             dnidx = min(dnidx + 1, last_dw);
             dnxt = dw[dnidx];
             if constexpr (K == 4) {
-                row(r, (w & 0xFFu) << 8, bh[o], bi[o], u0, q0, m_c); put(r, 1, m_c);
-                row(r + 1, ((w >> 8) & 0xFFu) << 8, bh[o + 1], bi[o + 1], u0, q1, m_c); put(r + 1, 1, m_c);
-                row(r + 2, ((w >> 16) & 0xFFu) << 8, bh[o + 2], bi[o + 2], u0, q2, m_c); put(r + 2, 1, m_c);
-                row(r + 3, (w >> 24) << 8, bh[o + 3], bi[o + 3], u0, q3, m_c); put(r + 3, 1, m_c);
+                row(r, (w & 0xFFu) << 8, bh[o], bi[o], u0, q0, m_c, nofill); put(r, 1, m_c);
+                row(r + 1, ((w >> 8) & 0xFFu) << 8, bh[o + 1], bi[o + 1], u0, q1, m_c, nofill); put(r + 1, 1, m_c);
+                row(r + 2, ((w >> 16) & 0xFFu) << 8, bh[o + 2], bi[o + 2], u0, q2, m_c, nofill); put(r + 2, 1, m_c);
+                row(r + 3, (w >> 24) << 8, bh[o + 3], bi[o + 3], u0, q3, m_c, nofill); put(r + 3, 1, m_c);
             } else if constexpr (K == 2) {
-                row(r, (w & 0xFFu) << 8, bh[o], bi[o], u0, q0, m_c);
-                row(r + 1, ((w >> 8) & 0xFFu) << 8, bh[o + 1], bi[o + 1], u1, q1, m_c); put(r, 2, m_c);
-                row(r + 2, ((w >> 16) & 0xFFu) << 8, bh[o + 2], bi[o + 2], u0, q2, m_c);
-                row(r + 3, (w >> 24) << 8, bh[o + 3], bi[o + 3], u1, q3, m_c); put(r + 2, 2, m_c);
+                // rows r, r+1's code word is built inside row r+2's prefix chain
+                row(r, (w & 0xFFu) << 8, bh[o], bi[o], u0, q0, m_c, fill0);
+                row(r + 1, ((w >> 8) & 0xFFu) << 8, bh[o + 1], bi[o + 1], u1, q1, m_c, nofill);
+                row(r + 2, ((w >> 16) & 0xFFu) << 8, bh[o + 2], bi[o + 2], u0, q2, m_c,
+                    [&]() __attribute__((always_inline)) { put(r, 2, m_c); });
+                row(r + 3, (w >> 24) << 8, bh[o + 3], bi[o + 3], u1, q3, m_c, nofill);
+                if constexpr (kFlush) put(r + 2, 2, m_c);
             } else {
-                row(r, (w & 0xFFu) << 8, bh[o], bi[o], u0, q0, m_c);
-                row(r + 1, ((w >> 8) & 0xFFu) << 8, bh[o + 1], bi[o + 1], u1, q1, m_c);
-                row(r + 2, ((w >> 16) & 0xFFu) << 8, bh[o + 2], bi[o + 2], u2, q2, m_c);
-                row(r + 3, (w >> 24) << 8, bh[o + 3], bi[o + 3], u3, q3, m_c);
+                row(r, (w & 0xFFu) << 8, bh[o], bi[o], u0, q0, m_c, nofill);
+                row(r + 1, ((w >> 8) & 0xFFu) << 8, bh[o + 1], bi[o + 1], u1, q1, m_c, nofill);
+                row(r + 2, ((w >> 16) & 0xFFu) << 8, bh[o + 2], bi[o + 2], u2, q2, m_c, nofill);
+                row(r + 3, (w >> 24) << 8, bh[o + 3], bi[o + 3], u3, q3, m_c, nofill);
                 put(r, 4, m_c);
             }
         };
@@ -2252,18 +2265,18 @@ __global__ __launch_bounds__(64) void nw_fill_rows_kernel(
             const uint32_t w = doff ? (dcur >> doff) | (dnxt << (32u - doff)) : dcur;
             const uint32_t n = ld - r + 1;
             if constexpr (K == 4) {
-                row(r, (w & 0xFFu) << 8, bh[o], bi[o], u0, q0, m_c); put(r, 1, m_c);
-                if (n > 1) { row(r + 1, ((w >> 8) & 0xFFu) << 8, bh[o + 1], bi[o + 1], u0, q1, m_c); put(r + 1, 1, m_c); }
-                if (n > 2) { row(r + 2, ((w >> 16) & 0xFFu) << 8, bh[o + 2], bi[o + 2], u0, q2, m_c); put(r + 2, 1, m_c); }
+                row(r, (w & 0xFFu) << 8, bh[o], bi[o], u0, q0, m_c, nofill); put(r, 1, m_c);
+                if (n > 1) { row(r + 1, ((w >> 8) & 0xFFu) << 8, bh[o + 1], bi[o + 1], u0, q1, m_c, nofill); put(r + 1, 1, m_c); }
+                if (n > 2) { row(r + 2, ((w >> 16) & 0xFFu) << 8, bh[o + 2], bi[o + 2], u0, q2, m_c, nofill); put(r + 2, 1, m_c); }
             } else if constexpr (K == 2) {
-                row(r, (w & 0xFFu) << 8, bh[o], bi[o], u0, q0, m_c);
-                if (n > 1) row(r + 1, ((w >> 8) & 0xFFu) << 8, bh[o + 1], bi[o + 1], u1, q1, m_c);
+                row(r, (w & 0xFFu) << 8, bh[o], bi[o], u0, q0, m_c, nofill);
+                if (n > 1) row(r + 1, ((w >> 8) & 0xFFu) << 8, bh[o + 1], bi[o + 1], u1, q1, m_c, nofill);
                 put(r, min(n, 2u), m_c);
-                if (n > 2) { row(r + 2, ((w >> 16) & 0xFFu) << 8, bh[o + 2], bi[o + 2], u0, q2, m_c); put(r + 2, 1, m_c); }
+                if (n > 2) { row(r + 2, ((w >> 16) & 0xFFu) << 8, bh[o + 2], bi[o + 2], u0, q2, m_c, nofill); put(r + 2, 1, m_c); }
             } else {
-                row(r, (w & 0xFFu) << 8, bh[o], bi[o], u0, q0, m_c);
-                if (n > 1) row(r + 1, ((w >> 8) & 0xFFu) << 8, bh[o + 1], bi[o + 1], u1, q1, m_c);
-                if (n > 2) row(r + 2, ((w >> 16) & 0xFFu) << 8, bh[o + 2], bi[o + 2], u2, q2, m_c);
+                row(r, (w & 0xFFu) << 8, bh[o], bi[o], u0, q0, m_c, nofill);
+                if (n > 1) row(r + 1, ((w >> 8) & 0xFFu) << 8, bh[o + 1], bi[o + 1], u1, q1, m_c, nofill);
+                if (n > 2) row(r + 2, ((w >> 16) & 0xFFu) << 8, bh[o + 2], bi[o + 2], u2, q2, m_c, nofill);
                 put(r, n, m_c);
             }
         };
@@ -2275,8 +2288,15 @@ __global__ __launch_bounds__(64) void nw_fill_rows_kernel(
         uint32_t r = 1;
         for (; r + kG - 1 < ld; r += kG) {  // full groups before the one holding row ld
             group(r);
-            quad(r, o0, M0);
-            if constexpr (kG == 8) quad(r + 4, o4, M0);
+            if constexpr (kG == 8 && K == 2) {
+                // rows r+2, r+3's code word goes into row r+4's prefix chain
+                quad(r, o0, M0, nofill, std::false_type{});
+                quad(r + 4, o4, M0, [&]() __attribute__((always_inline)) { put(r + 2, 2, M0); },
+                     std::true_type{});
+            } else {
+                quad(r, o0, M0, nofill, std::true_type{});
+                if constexpr (kG == 8) quad(r + 4, o4, M0, nofill, std::true_type{});
+            }
         }
         // the last group: 1 .. kG rows, row ld among them
         group(r);
@@ -2286,14 +2306,14 @@ __global__ __launch_bounds__(64) void nw_fill_rows_kernel(
             tail(r, o0, M1);
         } else if constexpr (kG == 8) {
             if (nq == 1) {
-                quad(r, o0, M1);
+                quad(r, o0, M1, nofill, std::true_type{});
                 if (t) tail(r + 4, o4, M1);
             } else {
-                quad(r, o0, M1);
-                quad(r + 4, o4, M1);
+                quad(r, o0, M1, nofill, std::true_type{});
+                quad(r + 4, o4, M1, nofill, std::true_type{});
             }
         } else {
-            quad(r, o0, M1);
+            quad(r, o0, M1, nofill, std::true_type{});
         }
     };
     if (g == 0) rows(std::true_type{});
