@@ -2062,7 +2062,9 @@ __global__ __launch_bounds__(64) void nw_fill_rows_kernel(
         constexpr int q = decltype(q_c)::value;  // row in its boundary group
         constexpr bool kM = decltype(m_c)::value;
         const int32_t hm = (kCodes == kCodesFull || (kM && r == ld)) ? ~3 : ~1;
-        int32_t M[K], tO[K], P[K];
+        int32_t M[K], tO[K], P[K], Dv[K];
+        uint32_t s6[K];  // D-open signs (sg[6] is written after the chain: the
+                         // chain's filler may still read the previous rows' sg)
         int32_t diag = __builtin_amdgcn_update_dpp(hb_prev, Hp[K - 1], 0x138 /*wave_shr:1*/, 0xf, 0xf, false);
         uint32_t x[K];
 #pragma unroll
@@ -2072,13 +2074,18 @@ __global__ __launch_bounds__(64) void nw_fill_rows_kernel(
             M[k] = (k == 0 ? diag : Hp[k - 1]) - pen;
             tO[k] = M[k] + kOpen;
             P[k] = k == 0 ? tO[0] : max(P[k - 1], tO[k]);
+            // what does not need the row's I: the D step and its open sign
+            // (independent of the prefix chain below, so they can fill its slots)
+            Dv[k] = Dn[k];
+            s6[k] = (uint32_t)((tO[k] | kTieOr) - Dv[k]);
+            Dn[k] = max(tO[k], Dv[k]) + kDstep;
         }
         const int32_t S_incl = wave_prefix_max(P[K - 1], fill);
         const int32_t Ein = max(__builtin_amdgcn_update_dpp(kNegInf, S_incl, 0x138, 0xf, 0xf, false), bI);
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             const int32_t I = k == 0 ? Ein : max(Ein, P[k - 1]);
-            const int32_t D = Dn[k];
+            const int32_t D = Dv[k];
             const int32_t H = max(M[k], max(I, D));
             if constexpr (kCodes != kCodesNone) {
                 const int32_t Hc = H & hm;
@@ -2088,7 +2095,7 @@ __global__ __launch_bounds__(64) void nw_fill_rows_kernel(
                 sg[1][e] = (uint32_t)(I - Hc);
                 sg[2][e] = (uint32_t)(D - Hc);
                 sg[4][e] = (uint32_t)(tOr - I);
-                sg[6][e] = (uint32_t)(tOr - D);
+                sg[6][e] = s6[k];
                 sg[7][e] = kCodes == kCodesFull ? x[k] - 1u : 0u;  // sign <=> q == d (full codes)
                 if constexpr (kCodes == kCodesFull) {
                     const int32_t tOc = tO[k] & ~3;
@@ -2098,7 +2105,6 @@ __global__ __launch_bounds__(64) void nw_fill_rows_kernel(
                     sg[3][e] = sg[5][e] = 0u;
                 }
             }
-            Dn[k] = max(tO[k], D) + kDstep;
             Hp[k] = H;
         }
         hb_prev = bH;
