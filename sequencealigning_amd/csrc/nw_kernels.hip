@@ -2177,6 +2177,10 @@ __global__ __launch_bounds__(64) void nw_fill_rows_kernel(
         constexpr bool kFirst = decltype(F)::value || SALN_ROWS_INDEP;
         constexpr uint32_t kG = kRowsGrp;  // rows per boundary group
         uint64_t nv = 0;  // lanes 0..kG-1: (H~, I~) of the next group's rows
+        // only the group's own rows (a branch-free variant where every lane
+        // loaded a clamped row - rows of later groups, not yet published,
+        // included - gave wrong boundary values in batches,
+        // test_packed_stripes_auto_selected; the cause was not isolated)
         auto fetch = [&](uint32_t r0) __attribute__((always_inline)) {
             if (!kFirst && lane < (int)kG && r0 + (uint32_t)lane <= ld)
                 asm volatile("global_load_dwordx2 %0, %1, off sc1"
@@ -2204,18 +2208,21 @@ __global__ __launch_bounds__(64) void nw_fill_rows_kernel(
                     else asm volatile("s_waitcnt vmcnt(7)" : "+v"(nv) : : "memory");
                 }
                 int32_t cH = (int32_t)(uint32_t)nv, cI = (int32_t)(uint32_t)(nv >> 32);
-                bool ok = !(lane < (int)kG && r + (uint32_t)lane <= ld) || (uint32_t)cH != kColEmpty;
-                uint32_t spins = 0;
-                while (__builtin_amdgcn_ballot_w64(!ok) && !failed) {  // not yet published: poll
-                    __builtin_amdgcn_s_sleep(1);
-                    if (lane < (int)kG && r + (uint32_t)lane <= ld) {
-                        const uint64_t v = __hip_atomic_load((const uint64_t *)(scr_in + r + kRowsOff + lane),
-                                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        cH = (int32_t)(uint32_t)v;
-                        cI = (int32_t)(uint32_t)(v >> 32);
-                        ok = (uint32_t)cH != kColEmpty;
-                    }
-                    if (++spins > kSpinCap) failed = true;
+                const bool mine = lane < (int)kG && r + (uint32_t)lane <= ld;
+                bool ok = !mine || (uint32_t)cH != kColEmpty;
+                if (__builtin_expect(__builtin_amdgcn_ballot_w64(!ok) != 0, 0) && !failed) {
+                    uint32_t spins = 0;  // not yet published: poll (rare)
+                    do {
+                        __builtin_amdgcn_s_sleep(1);
+                        if (mine) {
+                            const uint64_t v = __hip_atomic_load((const uint64_t *)(scr_in + r + kRowsOff + lane),
+                                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                            cH = (int32_t)(uint32_t)v;
+                            cI = (int32_t)(uint32_t)(v >> 32);
+                            ok = (uint32_t)cH != kColEmpty;
+                        }
+                        if (++spins > kSpinCap) failed = true;
+                    } while (__builtin_amdgcn_ballot_w64(!ok) && !failed);
                 }
                 fetch(r + kG);
 #pragma unroll
