@@ -70,6 +70,7 @@ struct saln_nw_plan {
     // pairs, stripe records, run words, per-pair done flags (plan order)
     uint32_t spec_pairs = 0, spec_blocks = 0;
     int spec_passes = 0;
+    bool spec_strict = false;  // SALN_SPEC_STRICT=1: a pair left to the cooperative walker is an error
     uint2 *d_spec_blocks = nullptr;
     SpecPair *d_spec_pairs = nullptr;
     SpecStripe *d_spec_stripes = nullptr;
@@ -472,6 +473,8 @@ int saln_nw_plan_create(saln_context *ctx, const uint64_t *q_off, uint64_t n_q,
             p->spec_pairs = (uint32_t)sp.size();
             p->spec_blocks = (uint32_t)blocks.size();
             p->spec_passes = passes;
+            const char *st = std::getenv("SALN_SPEC_STRICT");
+            p->spec_strict = st && std::atoi(st) != 0;
             if ((e = dev_alloc(p->ctx, (void **)&p->d_spec_blocks, blocks.size() * sizeof(uint2))) != hipSuccess ||
                 (e = hipMemcpy(p->d_spec_blocks, blocks.data(), blocks.size() * sizeof(uint2),
                                hipMemcpyHostToDevice)) != hipSuccess ||
@@ -599,7 +602,8 @@ int saln_nw_execute(saln_nw_plan *p, const uint8_t *d_q, const uint8_t *d_db,
                     SpecArgs{p->d_spec_blocks, p->d_spec_pairs, p->d_spec_stripes, p->d_spec_ops,
                              p->d_spec_done, 0},
                     p->spec_blocks, p->spec_pairs, p->d_spec_done, p->spec_passes, d_q, d_db, mask,
-                    endh, d_results, d_cigar, p->sc, p->stripe_layout(), t));
+                    endh, d_results, d_cigar, p->sc, p->stripe_layout(),
+                    p->spec_strict ? p->d_err : nullptr, t));
             if (a < b && p->score_only)
                 HIP_TRY(launch_score_results(p->d_pairs, a, b - a, endh, d_results, p->sc, t));
             else if (a < b)
@@ -931,8 +935,12 @@ int plan_check_error(const saln_nw_plan *p) {
     if (!p || !p->d_err) return SALN_OK;
     uint32_t v = 0;
     HIP_TRY(hipMemcpy(&v, p->d_err, sizeof v, hipMemcpyDeviceToHost));
-    if (v) {
+    if (v & 1u) {
         set_error("column-stripe dependency wait timed out");
+        return SALN_E_HIP;
+    }
+    if (v & 2u) {
+        set_error("speculative stripe walk did not link (SALN_SPEC_STRICT=1)");
         return SALN_E_HIP;
     }
     return SALN_OK;

@@ -106,12 +106,14 @@ hipError_t launch_traceback(int variant, const NwPairDesc *pairs, uint32_t first
                             const uint32_t *spec_done = nullptr);
 // speculative stripe walks of the plan's long column-stripe pairs: `passes`
 // walk passes, the link (accept or leave to the cooperative walker, `done`)
-// and the CIGAR copy
+// and the CIGAR copy; strict_err (SALN_SPEC_STRICT=1, tests): bit 1 set when a
+// pair did not link
 hipError_t launch_traceback_spec(const NwPairDesc *pairs, SpecArgs sa, uint32_t n_blocks,
                                  uint32_t n_spec_pairs, uint32_t *done, int passes,
                                  const uint8_t *qs, const uint8_t *ds, const uint8_t *mask,
                                  const int32_t *end_h, saln_nw_result *results, uint32_t *cigar,
-                                 Scoring sc, int stripe_layout, hipStream_t stream);
+                                 Scoring sc, int stripe_layout, uint32_t *strict_err,
+                                 hipStream_t stream);
 // score-only all-vs-all (nw_avsa.cpp)
 hipError_t launch_avsa(int variant, const uint64_t *q_off, const uint64_t *d_off,
                        const uint32_t *q_ids, uint32_t nq, const uint32_t *d_ids,

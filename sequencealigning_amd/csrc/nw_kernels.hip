@@ -1025,7 +1025,8 @@ __global__ __launch_bounds__(64 * NWV) void nw_traceback_coop_kernel(
 // (the next tied end state would be walked), the cooperative walker runs.
 __global__ __launch_bounds__(256) void nw_spec_link_kernel(
     const NwPairDesc *__restrict__ pairs, SpecArgs sa, uint32_t *__restrict__ done,
-    const int32_t *__restrict__ end_h, saln_nw_result *__restrict__ results) {
+    const int32_t *__restrict__ end_h, saln_nw_result *__restrict__ results,
+    uint32_t *__restrict__ strict_err) {
     __shared__ uint32_t s_n[kSpecMaxStripes], s_first[kSpecMaxStripes], s_last[kSpecMaxStripes];
     __shared__ uint8_t s_k0[kSpecMaxStripes];
     __shared__ uint32_t s_part[256];
@@ -1053,7 +1054,10 @@ __global__ __launch_bounds__(256) void nw_spec_link_kernel(
     __syncthreads();
     const uint32_t idx = sp.plan_idx;
     if (bad || bad_sh) {
-        if (tid == 0) done[idx] = 0u;
+        if (tid == 0) {
+            done[idx] = 0u;
+            if (strict_err) atomicOr(strict_err, 2u);  // SALN_SPEC_STRICT: report the fallback
+        }
         return;
     }
     for (int32_t s = tid; s < S; s += 256) {
@@ -3099,7 +3103,8 @@ hipError_t launch_traceback_spec(const NwPairDesc *pairs, SpecArgs sa, uint32_t 
                                  uint32_t n_spec_pairs, uint32_t *done, int passes,
                                  const uint8_t *qs, const uint8_t *ds, const uint8_t *mask,
                                  const int32_t *end_h, saln_nw_result *results, uint32_t *cigar,
-                                 Scoring sc, int stripe_layout, hipStream_t stream) {
+                                 Scoring sc, int stripe_layout, uint32_t *strict_err,
+                                 hipStream_t stream) {
     if (n_blocks == 0 || passes < 1) return hipSuccess;
     constexpr int kLoaders = 4;
     // a stripe walk from its right edge needs ~256 + kCoopSlack rows: two
@@ -3127,7 +3132,8 @@ hipError_t launch_traceback_spec(const NwPairDesc *pairs, SpecArgs sa, uint32_t 
                                               : go(std::integral_constant<int, 0>{});
     if (e != hipSuccess) return e;
     sa.pass = passes;
-    nw_spec_link_kernel<<<dim3(n_spec_pairs), dim3(256), 0, stream>>>(pairs, sa, done, end_h, results);
+    nw_spec_link_kernel<<<dim3(n_spec_pairs), dim3(256), 0, stream>>>(pairs, sa, done, end_h,
+                                                                       results, strict_err);
     if (cigar) {
         sa.done = done;
         nw_spec_copy_kernel<<<dim3(n_blocks), dim3(64), 0, stream>>>(pairs, sa, results, cigar);

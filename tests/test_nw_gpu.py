@@ -471,6 +471,21 @@ def test_speculative_stripe_walks_equal_sequential(saln, monkeypatch, passes):
     assert seq[2] == spec[2]
 
 
+def test_speculative_stripe_walks_link(saln, monkeypatch):
+    """On mutated long pairs the three default passes link (SALN_SPEC_STRICT=1
+    turns a pair left to the cooperative walker into an error), so the
+    speculative path, not the fallback, produced these results."""
+    from sequencealigning_amd import synth
+    monkeypatch.setenv("SALN_SPEC", "1")
+    monkeypatch.delenv("SALN_SPEC_PASSES", raising=False)
+    monkeypatch.setenv("SALN_SPEC_STRICT", "1")
+    q = synth.random_bases(0x5EED0009, 40_000).tobytes()
+    d = synth.mutate(q, 0.05, seed=9)
+    r = saln.n_w_align(q, d)
+    s, ok = path_score(q, d, r.cigar)
+    assert r.printed and ok and s == r.score
+
+
 def test_deadend_pairs_device_plan(saln, oracle):
     """Pairs whose reference DFS leaves sentinel-rooted subtrees
     (tests/golden/nw_deadend.json, oracle-pinned): nothing printed, a panic
