@@ -51,6 +51,7 @@ struct saln_nw_plan {
     bool async_tb = false;
     bool stripe_pk = false;  // column stripes use the packed fill and layout
     int stripe_rows = 0;     // else: row fill with this many columns per lane (0 = skewed fill)
+    uint32_t stripe_sub = kStripeSubMax;  // boundary columns per 256-column chunk
     int stripe_layout() const { return stripe_pk ? 1 : stripe_rows ? 2 : 0; }
     bool full_codes = false;  // walk codes (default) or every parent set
     bool score_only = false;  // no parent codes / traceback (saln_nw_plan_set_score_only)
@@ -286,6 +287,23 @@ int saln_nw_plan_create(saln_context *ctx, const uint64_t *q_off, uint64_t n_q,
                           cols / p->var_count[kStripeVariant] >= 3000;
         p->stripe_pk = waves > 0 && free_all && stripe_packed(p->sc, waves, wide);
         p->stripe_rows = p->stripe_pk ? 0 : stripe_rows_k();
+        // boundary columns per 256-column chunk: the row fill's 4 / K stripes,
+        // else one; the scratch offsets above reserved kStripeSubMax
+        p->stripe_sub = p->stripe_rows ? 4u / (uint32_t)p->stripe_rows : 1u;
+        if (p->stripe_sub != kStripeSubMax) {
+            uint64_t so = 0;
+            for (uint64_t r = 0; r < p->n_fill; ++r) {
+                NwPairDesc &d = p->h_pairs[r];
+                const Geom g = variant_geom((int)d.variant);
+                if (g.n_chunks(d.len_q) > 1 || d.variant == kStripeVariant) {
+                    so = (so + 3) & ~3ull;
+                    d.scratch_off = so;
+                    so += (uint64_t)(d.variant == kStripeVariant ? p->stripe_sub * g.n_chunks(d.len_q) : 1) *
+                          scratch_col(d.len_db);
+                }
+            }
+            soff = so;
+        }
     }
     // Mask packs: up to 64 consecutive pairs of a variant (one traceback
     // wave) with interleaved segments (nw_common.hpp Geom), unless padding
@@ -571,7 +589,7 @@ int saln_nw_execute(saln_nw_plan *p, const uint8_t *d_q, const uint8_t *d_db,
                     // once its value replaces the preset (nw_fill_stripe_kernel)
                     const NwPairDesc &la = p->h_pairs[b - 1];
                     const uint64_t c0 = p->h_pairs[a].scratch_off;
-                    const uint64_t c1 = la.scratch_off + (uint64_t)kStripeSubMax *
+                    const uint64_t c1 = la.scratch_off + (uint64_t)p->stripe_sub *
                                                              variant_geom(v).n_chunks(la.len_q) *
                                                              scratch_col(la.len_db);
                     HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)(p->d_scratch + c0), (int)0x80000000u,

@@ -2035,6 +2035,10 @@ __global__ __launch_bounds__(64) void nw_fill_rows_kernel(
         Dn[k] = ds4_row1(sc, j) + alpha + beta * (int32_t)j;
     }
     int32_t hb_prev = hs4_row0(sc, c0) + beta * (int32_t)c0;  // H~(r-1, c0): lane 0's diagonal
+    // stripes with a left neighbour: the loaded boundary rows stay in lanes
+    // 0..7 (cH_v, the previous group's in cH_prev_v); row q of a group takes
+    // H~(r-1, c0) from lane q-1 with one DPP row_shl instead of a readlane
+    int32_t cH_v = hb_prev, cH_prev_v = hb_prev;
     // my bytes of row 1 in the 256-column tile layout
     uint8_t *mrow = mask + p.mask_off + (uint64_t)(c0 / 256) * p.mask_cs + (col0 % 256);
     typedef const __attribute__((address_space(4))) uint32_t cu32;  // constant: scalar loads
@@ -2061,7 +2065,7 @@ __global__ __launch_bounds__(64) void nw_fill_rows_kernel(
     // sets for the end states); every other row stores walk codes without
     // argM, tied against H'' & ~1 with no per-row test
     auto row = [&](uint32_t r, uint32_t dch, int32_t bH, int32_t bI, auto u_c, auto q_c,
-                   auto m_c, auto &&fill) __attribute__((always_inline)) {
+                   auto m_c, auto &&fill, auto vb_c) __attribute__((always_inline)) {
         constexpr int u = decltype(u_c)::value;
         constexpr int q = decltype(q_c)::value;  // row in its boundary group
         constexpr bool kM = decltype(m_c)::value;
@@ -2069,7 +2073,18 @@ __global__ __launch_bounds__(64) void nw_fill_rows_kernel(
         int32_t M[K], tO[K], P[K], Dv[K];
         uint32_t s6[K];  // D-open signs (sg[6] is written after the chain: the
                          // chain's filler may still read the previous rows' sg)
-        int32_t diag = __builtin_amdgcn_update_dpp(hb_prev, Hp[K - 1], 0x138 /*wave_shr:1*/, 0xf, 0xf, false);
+        int32_t hbv;  // lane 0: H~(r-1, c0)
+        if constexpr (decltype(vb_c)::value) {
+            if constexpr (q == 0)
+                hbv = __builtin_amdgcn_update_dpp(0, cH_prev_v, 0x107 /*row_shl:7*/, 0xf, 0xf, true);
+            else if constexpr (q == 1)
+                hbv = cH_v;
+            else
+                hbv = __builtin_amdgcn_update_dpp(0, cH_v, 0x100 + (q - 1) /*row_shl*/, 0xf, 0xf, true);
+        } else {
+            hbv = hb_prev;
+        }
+        int32_t diag = __builtin_amdgcn_update_dpp(hbv, Hp[K - 1], 0x138 /*wave_shr:1*/, 0xf, 0xf, false);
         uint32_t x[K];
 #pragma unroll
         for (int k = 0; k < K; ++k) {
@@ -2179,6 +2194,7 @@ __global__ __launch_bounds__(64) void nw_fill_rows_kernel(
     // re-polled with ordinary (compiler-waited) loads.
     auto rows = [&](auto F) __attribute__((always_inline)) {
         constexpr bool kFirst = decltype(F)::value || SALN_ROWS_INDEP;
+        const std::integral_constant<bool, !kFirst> VB;  // boundary rows kept in cH_v
         constexpr uint32_t kG = kRowsGrp;  // rows per boundary group
         uint64_t nv = 0;  // lanes 0..kG-1: (H~, I~) of the next group's rows
         // only the group's own rows (a branch-free variant where every lane
@@ -2229,9 +2245,11 @@ __global__ __launch_bounds__(64) void nw_fill_rows_kernel(
                     } while (__builtin_amdgcn_ballot_w64(!ok) && !failed);
                 }
                 fetch(r + kG);
+                cH_prev_v = cH_v;
+                cH_v = cH;
 #pragma unroll
                 for (uint32_t q = 0; q < kG; ++q) {
-                    bh[q] = __builtin_amdgcn_readlane(cH, q);
+                    bh[q] = 0;  // (rows take H~ from cH_v)
                     bi[q] = __builtin_amdgcn_readlane(cI, q);
                 }
             }
@@ -2253,23 +2271,23 @@ __global__ __launch_bounds__(64) void nw_fill_rows_kernel(
             dnidx = min(dnidx + 1, last_dw);
             dnxt = dw[dnidx];
             if constexpr (K == 4) {
-                row(r, (w & 0xFFu) << 8, bh[o], bi[o], u0, q0, m_c, nofill); put(r, 1, m_c);
-                row(r + 1, ((w >> 8) & 0xFFu) << 8, bh[o + 1], bi[o + 1], u0, q1, m_c, nofill); put(r + 1, 1, m_c);
-                row(r + 2, ((w >> 16) & 0xFFu) << 8, bh[o + 2], bi[o + 2], u0, q2, m_c, nofill); put(r + 2, 1, m_c);
-                row(r + 3, (w >> 24) << 8, bh[o + 3], bi[o + 3], u0, q3, m_c, nofill); put(r + 3, 1, m_c);
+                row(r, (w & 0xFFu) << 8, bh[o], bi[o], u0, q0, m_c, nofill, VB); put(r, 1, m_c);
+                row(r + 1, ((w >> 8) & 0xFFu) << 8, bh[o + 1], bi[o + 1], u0, q1, m_c, nofill, VB); put(r + 1, 1, m_c);
+                row(r + 2, ((w >> 16) & 0xFFu) << 8, bh[o + 2], bi[o + 2], u0, q2, m_c, nofill, VB); put(r + 2, 1, m_c);
+                row(r + 3, (w >> 24) << 8, bh[o + 3], bi[o + 3], u0, q3, m_c, nofill, VB); put(r + 3, 1, m_c);
             } else if constexpr (K == 2) {
                 // rows r, r+1's code word is built inside row r+2's prefix chain
-                row(r, (w & 0xFFu) << 8, bh[o], bi[o], u0, q0, m_c, fill0);
-                row(r + 1, ((w >> 8) & 0xFFu) << 8, bh[o + 1], bi[o + 1], u1, q1, m_c, nofill);
+                row(r, (w & 0xFFu) << 8, bh[o], bi[o], u0, q0, m_c, fill0, VB);
+                row(r + 1, ((w >> 8) & 0xFFu) << 8, bh[o + 1], bi[o + 1], u1, q1, m_c, nofill, VB);
                 row(r + 2, ((w >> 16) & 0xFFu) << 8, bh[o + 2], bi[o + 2], u0, q2, m_c,
-                    [&]() __attribute__((always_inline)) { put(r, 2, m_c); });
-                row(r + 3, (w >> 24) << 8, bh[o + 3], bi[o + 3], u1, q3, m_c, nofill);
+                    [&]() __attribute__((always_inline)) { put(r, 2, m_c); }, VB);
+                row(r + 3, (w >> 24) << 8, bh[o + 3], bi[o + 3], u1, q3, m_c, nofill, VB);
                 if constexpr (kFlush) put(r + 2, 2, m_c);
             } else {
-                row(r, (w & 0xFFu) << 8, bh[o], bi[o], u0, q0, m_c, nofill);
-                row(r + 1, ((w >> 8) & 0xFFu) << 8, bh[o + 1], bi[o + 1], u1, q1, m_c, nofill);
-                row(r + 2, ((w >> 16) & 0xFFu) << 8, bh[o + 2], bi[o + 2], u2, q2, m_c, nofill);
-                row(r + 3, (w >> 24) << 8, bh[o + 3], bi[o + 3], u3, q3, m_c, nofill);
+                row(r, (w & 0xFFu) << 8, bh[o], bi[o], u0, q0, m_c, nofill, VB);
+                row(r + 1, ((w >> 8) & 0xFFu) << 8, bh[o + 1], bi[o + 1], u1, q1, m_c, nofill, VB);
+                row(r + 2, ((w >> 16) & 0xFFu) << 8, bh[o + 2], bi[o + 2], u2, q2, m_c, nofill, VB);
+                row(r + 3, (w >> 24) << 8, bh[o + 3], bi[o + 3], u3, q3, m_c, nofill, VB);
                 put(r, 4, m_c);
             }
         };
@@ -2282,18 +2300,18 @@ __global__ __launch_bounds__(64) void nw_fill_rows_kernel(
             const uint32_t w = doff ? (dcur >> doff) | (dnxt << (32u - doff)) : dcur;
             const uint32_t n = ld - r + 1;
             if constexpr (K == 4) {
-                row(r, (w & 0xFFu) << 8, bh[o], bi[o], u0, q0, m_c, nofill); put(r, 1, m_c);
-                if (n > 1) { row(r + 1, ((w >> 8) & 0xFFu) << 8, bh[o + 1], bi[o + 1], u0, q1, m_c, nofill); put(r + 1, 1, m_c); }
-                if (n > 2) { row(r + 2, ((w >> 16) & 0xFFu) << 8, bh[o + 2], bi[o + 2], u0, q2, m_c, nofill); put(r + 2, 1, m_c); }
+                row(r, (w & 0xFFu) << 8, bh[o], bi[o], u0, q0, m_c, nofill, VB); put(r, 1, m_c);
+                if (n > 1) { row(r + 1, ((w >> 8) & 0xFFu) << 8, bh[o + 1], bi[o + 1], u0, q1, m_c, nofill, VB); put(r + 1, 1, m_c); }
+                if (n > 2) { row(r + 2, ((w >> 16) & 0xFFu) << 8, bh[o + 2], bi[o + 2], u0, q2, m_c, nofill, VB); put(r + 2, 1, m_c); }
             } else if constexpr (K == 2) {
-                row(r, (w & 0xFFu) << 8, bh[o], bi[o], u0, q0, m_c, nofill);
-                if (n > 1) row(r + 1, ((w >> 8) & 0xFFu) << 8, bh[o + 1], bi[o + 1], u1, q1, m_c, nofill);
+                row(r, (w & 0xFFu) << 8, bh[o], bi[o], u0, q0, m_c, nofill, VB);
+                if (n > 1) row(r + 1, ((w >> 8) & 0xFFu) << 8, bh[o + 1], bi[o + 1], u1, q1, m_c, nofill, VB);
                 put(r, min(n, 2u), m_c);
-                if (n > 2) { row(r + 2, ((w >> 16) & 0xFFu) << 8, bh[o + 2], bi[o + 2], u0, q2, m_c, nofill); put(r + 2, 1, m_c); }
+                if (n > 2) { row(r + 2, ((w >> 16) & 0xFFu) << 8, bh[o + 2], bi[o + 2], u0, q2, m_c, nofill, VB); put(r + 2, 1, m_c); }
             } else {
-                row(r, (w & 0xFFu) << 8, bh[o], bi[o], u0, q0, m_c, nofill);
-                if (n > 1) row(r + 1, ((w >> 8) & 0xFFu) << 8, bh[o + 1], bi[o + 1], u1, q1, m_c, nofill);
-                if (n > 2) row(r + 2, ((w >> 16) & 0xFFu) << 8, bh[o + 2], bi[o + 2], u2, q2, m_c, nofill);
+                row(r, (w & 0xFFu) << 8, bh[o], bi[o], u0, q0, m_c, nofill, VB);
+                if (n > 1) row(r + 1, ((w >> 8) & 0xFFu) << 8, bh[o + 1], bi[o + 1], u1, q1, m_c, nofill, VB);
+                if (n > 2) row(r + 2, ((w >> 16) & 0xFFu) << 8, bh[o + 2], bi[o + 2], u2, q2, m_c, nofill, VB);
                 put(r, n, m_c);
             }
         };
