@@ -1335,8 +1335,13 @@ __host__ __device__ inline int32_t rebase_center(const Scoring &sc, int32_t W) {
     return (W * (2 * m + 4 * ge) / 2) & ~1;
 }
 
+#ifndef SALN_PK_WAVES
+// experiment switch: min waves per SIMD the packed fill is built for.  At 124
+// VGPRs it runs 4; 5 (96 VGPRs) spills 26 registers: C2 fill 0.97 -> 1.57 ms
+#define SALN_PK_WAVES 1
+#endif
 template <int G, int K, int kCodes, typename Src, int KS, bool kRebase = false>
-__global__ __launch_bounds__(256) void nw_fill_pk_kernel(Src src, uint32_t count,
+__global__ __launch_bounds__(256, SALN_PK_WAVES) void nw_fill_pk_kernel(Src src, uint32_t count,
                                                          const uint8_t *__restrict__ qs,
                                                          const uint8_t *__restrict__ ds,
                                                          uint8_t *__restrict__ mask, Scoring sc,
