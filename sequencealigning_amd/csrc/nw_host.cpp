@@ -272,11 +272,12 @@ int saln_nw_plan_create(saln_context *ctx, const uint64_t *q_off, uint64_t n_q,
         p->h_pairs[r] = d;
     }
     {
-        uint64_t waves = 0, cols = 0;  // 256-column stripe chunks, query columns
+        uint64_t waves = 0, cols = 0, waves_k1 = 0;  // 256-column chunks, columns, 64-column stripes
         bool free_all = true;  // the packed stripes carry no alive flag (nw_common.hpp)
         for (uint32_t r = 0; r < p->var_count[kStripeVariant]; ++r) {
             const NwPairDesc &d = p->h_pairs[p->var_first[kStripeVariant] + r];
             waves += variant_geom(kStripeVariant).n_chunks(d.len_q);
+            waves_k1 += (d.len_q + 63) / 64;
             cols += d.len_q;
             free_all = free_all && sentinel_free(p->sc, d.len_q, d.len_db);
         }
@@ -286,7 +287,7 @@ int saln_nw_plan_create(saln_context *ctx, const uint64_t *q_off, uint64_t n_q,
         const bool wide = p->var_count[kStripeVariant] &&
                           cols / p->var_count[kStripeVariant] >= 3000;
         p->stripe_pk = waves > 0 && free_all && stripe_packed(p->sc, waves, wide);
-        p->stripe_rows = p->stripe_pk ? 0 : stripe_rows_k();
+        p->stripe_rows = p->stripe_pk ? 0 : stripe_rows_k(waves_k1);
         // boundary columns per 256-column chunk: the row fill's 4 / K stripes,
         // else one; the scratch offsets above reserved kStripeSubMax
         p->stripe_sub = p->stripe_rows ? 4u / (uint32_t)p->stripe_rows : 1u;

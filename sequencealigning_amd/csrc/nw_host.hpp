@@ -88,8 +88,9 @@ constexpr int kStripeVariant = 3;
 // column-stripe pairs: boundary columns allocated per pair (the row fill cuts
 // each 256-column chunk into up to 4 stripes)
 constexpr uint32_t kStripeSubMax = 4;
-// row fill (nw_fill_rows_kernel) columns per lane, 0 = the skewed stripe fill
-int stripe_rows_k();
+// row fill (nw_fill_rows_kernel) columns per lane, 0 = the skewed stripe fill;
+// waves_k1: the plan's stripe waves at one column per lane
+int stripe_rows_k(uint64_t waves_k1);
 // column stripes run the packed (int16 halves) fill for this scoring and
 // this many stripe waves in the plan (decided once per plan: it sets the layout)
 bool stripe_packed(const Scoring &sc, uint64_t n_waves, bool wide);

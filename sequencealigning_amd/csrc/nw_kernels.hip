@@ -2289,11 +2289,11 @@ __global__ __launch_bounds__(64) void nw_fill_rows_kernel(
                 row(r + 3, (w >> 24) << 8, bh[o + 3], bi[o + 3], u1, q3, m_c, nofill, VB);
                 if constexpr (kFlush) put(r + 2, 2, m_c);
             } else {
-                row(r, (w & 0xFFu) << 8, bh[o], bi[o], u0, q0, m_c, nofill, VB);
+                row(r, (w & 0xFFu) << 8, bh[o], bi[o], u0, q0, m_c, fill0, VB);
                 row(r + 1, ((w >> 8) & 0xFFu) << 8, bh[o + 1], bi[o + 1], u1, q1, m_c, nofill, VB);
                 row(r + 2, ((w >> 16) & 0xFFu) << 8, bh[o + 2], bi[o + 2], u2, q2, m_c, nofill, VB);
                 row(r + 3, (w >> 24) << 8, bh[o + 3], bi[o + 3], u3, q3, m_c, nofill, VB);
-                put(r, 4, m_c);
+                if constexpr (kFlush) put(r, 4, m_c);
             }
         };
         // the last 1-3 rows (boundary at bh/bi[o ..])
@@ -2328,10 +2328,14 @@ __global__ __launch_bounds__(64) void nw_fill_rows_kernel(
         uint32_t r = 1;
         for (; r + kG - 1 < ld; r += kG) {  // full groups before the one holding row ld
             group(r);
-            if constexpr (kG == 8 && K == 2) {
-                // rows r+2, r+3's code word goes into row r+4's prefix chain
+            if constexpr (kG == 8 && K <= 2) {
+                // the first quad's last code word goes into row r+4's prefix chain
                 quad(r, o0, M0, nofill, std::false_type{});
-                quad(r + 4, o4, M0, [&]() __attribute__((always_inline)) { put(r + 2, 2, M0); },
+                quad(r + 4, o4, M0,
+                     [&]() __attribute__((always_inline)) {
+                         if constexpr (K == 2) put(r + 2, 2, M0);
+                         else put(r, 4, M0);
+                     },
                      std::true_type{});
             } else {
                 quad(r, o0, M0, nofill, std::true_type{});
@@ -3260,14 +3264,20 @@ Geom variant_geom(int v) { return kVariants[v]; }
 // 40.1 ms) although the step is cheaper; once the stripe waves fill the chip
 // it wins (400 x 5 kbp pairs: 8.0 vs 9.2 ms end to end).  Chosen per plan
 // from the stripe-wave count; SALN_STRIPE_PK=0 / 1 forces it.
-int stripe_rows_k() {
-    static const int k = [] {  // SALN_ROWS_K = 0 (skewed stripe fill), 1, 2 or 4
+// Row-fill columns per lane: K = 1 (64-column stripes) while every stripe
+// wave of the plan has a SIMD to itself (a shorter row step: C1 0.197 ->
+// 0.188 ms, 5 kbp 0.75 -> 0.70 ms), else K = 2 (C4: 1,564 K = 1 waves share
+// SIMDs, 19.5 vs 14.5 ms).  SALN_ROWS_K = 0 (skewed stripe fill), 1, 2 or 4
+// forces it.
+int stripe_rows_k(uint64_t waves_k1) {
+    static const int forced = [] {
         const char *e = std::getenv("SALN_ROWS_K");
-        if (!e) return 2;
+        if (!e) return -1;
         const int v = std::atoi(e);
         return v == 0 || v == 1 || v == 4 ? v : 2;
     }();
-    return k;
+    if (forced >= 0) return forced;
+    return waves_k1 <= 1024 ? 1 : 2;
 }
 
 bool stripe_packed(const Scoring &sc, uint64_t n_waves, bool wide) {
