@@ -2975,8 +2975,10 @@ hipError_t launch_avsa(int variant, const uint64_t *q_off, const uint64_t *d_off
         case 4: e = avsa_pk<8, 19>(src, count, qs, ds, sc, ld_max, stream); break;
         case 5: e = avsa_pk<16, 16>(src, count, qs, ds, sc, ld_max, stream); break;
         case 6: e = avsa_pk<32, 16>(src, count, qs, ds, sc, ld_max, stream); break;
-#if SALN_V7_NARROW
+#if SALN_V7_NARROW || SALN_AVSA_NARROW == 1
         case 7: e = avsa_pk<8, 20>(src, count, qs, ds, sc, ld_max, stream); break;
+#elif SALN_AVSA_NARROW == 2  // experiment: queries <= 152 columns only
+        case 7: e = avsa_pk<8, 19>(src, count, qs, ds, sc, ld_max, stream); break;
 #else
         case 7: e = avsa_pk<16, 10>(src, count, qs, ds, sc, ld_max, stream); break;
 #endif
