@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <memory>
 #include <numeric>
 #include <vector>
@@ -96,6 +97,10 @@ int saln_nw_avsa_create(saln_context *ctx, const uint64_t *q_off, uint64_t n_q,
     });
     std::vector<std::vector<uint32_t>> cls(kNumVariants);
     std::vector<uint32_t> fbq;
+    const bool avsa_narrow = [] {  // SALN_AVSA_V4=1: 8 x 19 groups for <= 152 columns
+        const char *e = std::getenv("SALN_AVSA_V4");
+        return e && std::atoi(e) != 0;
+    }();
     for (uint64_t q = 0; q < n_q; ++q) {
         const uint64_t lq = q_off[q + 1] - q_off[q];
         if (lq > 0x7FFFFFFFull) {
@@ -107,7 +112,10 @@ int saln_nw_avsa_create(saln_context *ctx, const uint64_t *q_off, uint64_t n_q,
             zq.push_back((uint32_t)q);
             continue;
         }
-        const int v = choose_variant((uint32_t)lq, a->ld_max, a->sc);
+        int v = choose_variant((uint32_t)lq, a->ld_max, a->sc);
+        // score-only queries of <= 152 columns: 8-lane groups of 19 columns
+        // (variant 4's geometry; no mask, so no walker segment limit)
+        if (v == 7 && lq <= 152 && avsa_narrow) v = 4;
         (variant_packed(v) ? cls[v] : fbq).push_back((uint32_t)q);
     }
     a->cells = sum_q * sum_d;
