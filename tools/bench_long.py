@@ -20,6 +20,7 @@ def main():
     ap.add_argument("--len", type=int, default=1000)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--score-only", action="store_true")
+    ap.add_argument("--ldb", type=int, default=0, help="db length (default: the mutated query)")
     a = ap.parse_args()
     import torch
     import sequencealigning_amd as saln
@@ -27,6 +28,8 @@ def main():
     L = a.len
     q = synth.random_bases(0x5EED0000 + (3 if L > 10_000 else 0), L).tobytes()
     d = synth.mutate(q, 0.05, seed=L)
+    if a.ldb:  # a rectangular pair: the db is the mutated query cut or repeated to ldb
+        d = (d * (a.ldb // max(1, len(d)) + 1))[:a.ldb]
     qo = np.array([0, len(q)], np.uint64)
     do = np.array([0, len(d)], np.uint64)
     plan = saln.NwPlan(qo, do, pairs=[(0, 0)])
