@@ -118,7 +118,9 @@ int saln_nw_avsa_create(saln_context *ctx, const uint64_t *q_off, uint64_t n_q,
         int v = choose_variant((uint32_t)lq, a->ld_max, a->sc);
         // score-only queries of <= 152 columns: 8-lane groups of 19 columns
         // (variant 4's geometry; no mask, so no walker segment limit)
-        if (v == 7 && lq <= 152 && avsa_narrow) v = 4;
+        // (32 groups per block stage their db rows in LDS: 4 B per row while
+        // the db stays inside one int16 frame, <= 80 KB per block)
+        if (v == 7 && lq <= 152 && avsa_narrow && a->ld_max <= 600) v = 4;
         (variant_packed(v) ? cls[v] : fbq).push_back((uint32_t)q);
     }
     a->cells = sum_q * sum_d;

@@ -3272,13 +3272,10 @@ Geom variant_geom(int v) { return kVariants[v]; }
 // SIMDs, 19.5 vs 14.5 ms).  SALN_ROWS_K = 0 (skewed stripe fill), 1, 2 or 4
 // forces it.
 int stripe_rows_k(uint64_t waves_k1) {
-    static const int forced = [] {
-        const char *e = std::getenv("SALN_ROWS_K");
-        if (!e) return -1;
+    if (const char *e = std::getenv("SALN_ROWS_K")) {  // read per plan
         const int v = std::atoi(e);
         return v == 0 || v == 1 || v == 4 ? v : 2;
-    }();
-    if (forced >= 0) return forced;
+    }
     return waves_k1 <= 1024 ? 1 : 2;
 }
 
