@@ -1436,7 +1436,11 @@ __global__ __launch_bounds__(256, SALN_PK_WAVES) void nw_fill_pk_kernel(Src src,
                                (int64_t)lane * (int64_t)pb.mask_rs;
     const uint32_t *__restrict__ rowp = myrow - lane;  // word of row r-1 at step 0
     const uint16_t *__restrict__ rowp16 = myrow16 - lane;
+#if SALN_EXP_NOSKEW  // timing experiment only (wrong results): no pipeline ramp
+    const int T = ldM;
+#else
     const int T = (int)geo.steps((uint32_t)ldM);
+#endif
     // Previous-row H: step t reads Hin (row r-1) and writes Hout (row r).
     // SALN_PINGPONG: a two-step unroll swaps two arrays (no register
     // rotation, more live registers); otherwise in place.
