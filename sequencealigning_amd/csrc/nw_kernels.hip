@@ -1441,6 +1441,12 @@ __global__ __launch_bounds__(256, SALN_PK_WAVES) void nw_fill_pk_kernel(Src src,
 #else
     const int T = (int)geo.steps((uint32_t)ldM);
 #endif
+    // Walk codes: a lane whose columns all lie past a pair's query stores
+    // nothing for it (no walker reads past column len_q; 16 x 10 groups on
+    // 150-column queries: one store of 16 saved).  Full codes keep every
+    // segment defined.
+    const int ldAs = (kCodes == kCodesWalk && col0 >= lqA) ? 0 : ldA;
+    const int ldBs = (kCodes == kCodesWalk && col0 >= lqB) ? 0 : ldB;
     // Previous-row H: step t reads Hin (row r-1) and writes Hout (row r).
     // SALN_PINGPONG: a two-step unroll swaps two arrays (no register
     // rotation, more live registers); otherwise in place.
@@ -1567,12 +1573,12 @@ __global__ __launch_bounds__(256, SALN_PK_WAVES) void nw_fill_pk_kernel(Src src,
                     for (int w = 0; w < (KS + 3) / 4; ++w)
                         asm volatile("" : : "v"(wa[sg].w[w]), "v"(wb[sg].w[w]));
 #else
-                if (r <= ldA) {
+                if (r <= ldAs) {
 #pragma unroll
                     for (int sg = 0; sg < NS; ++sg)
                         *reinterpret_cast<PkMask<KS> *>(mA + (uint64_t)sg * pa.mask_bs) = wa[sg];
                 }
-                if (r <= ldB) {
+                if (r <= ldBs) {
 #pragma unroll
                     for (int sg = 0; sg < NS; ++sg)
                         *reinterpret_cast<PkMask<KS> *>(mB + (uint64_t)sg * pb.mask_bs) = wb[sg];
