@@ -2535,7 +2535,9 @@ __global__ __launch_bounds__(256) void nw_fill_lanes_kernel(
                             for (int k = 0; k < 4; ++k) s4[u][k] = sg[u][4 * w + k];
                         mw.w[w] = stripe_code_word<kCodes>(s4);
                     }
-                    *reinterpret_cast<MaskWords<K> *>(mseg + (uint64_t)(r - 1) * p.mask_rs) = mw;
+                    // walk codes: lanes wholly past the query store nothing (as the packed fill)
+                    if (kCodes != kCodesWalk || col0 < lq)
+                        *reinterpret_cast<MaskWords<K> *>(mseg + (uint64_t)(r - 1) * p.mask_rs) = mw;
                 }
                 if (lane == G - 1 && c + 1 < nch) scr[r] = make_int2(pubH, pubF);
                 if (c == c_end && (uint32_t)lane == l_end && r == (int)ld) {
