@@ -243,6 +243,7 @@ def _single_pair(torch, saln, q, d, reps, score_only=False):
         plan.execute(dq, dd, res, cig)
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / reps
+    plan.check()  # a column-stripe dependency timeout raises here
     f, _ = plan.kernel_time("nw_fill")
     tb, _ = plan.kernel_time("nw_traceback")
     r = res.cpu().numpy().view(saln._lib.RESULT_DTYPE)[0]
@@ -410,6 +411,9 @@ def main() -> None:
                     help="overlap step k's traceback with step k+1's fill on a second stream "
                          "(measured slower on MI355X: the walk slows the VALU-bound fill)")
     args = ap.parse_args()
+    if os.environ.get("SALN_LIB"):
+        sys.exit("bench.py: SALN_LIB is set (an instrumented tools/ build); the bench measures "
+                 "the product library sequencealigning_amd/libsaln.so only")
 
     import torch
     import torch.distributed as dist
@@ -483,6 +487,7 @@ def main() -> None:
             step()
         drain()
     dt = timed(run_steps, world, dist, torch, local)
+    plan.check()  # device-side status of every timed execute (raises on a timeout)
     fill_ms, fill_n = plan.kernel_time("nw_fill")
     tb_ms, tb_n = plan.kernel_time("nw_traceback")
     ex_ms, ex_n = plan.kernel_time("nw_execute")

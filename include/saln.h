@@ -49,8 +49,17 @@ typedef enum {
     SALN_E_CAPACITY = -4,  /* caller buffer too small */
     SALN_E_IO = -5,        /* file could not be read */
     SALN_E_FASTA = -6,     /* AlignerError::FastaError (bad extension), parse.rs:55-60 */
-    SALN_E_FASTA_CHARS = -7 /* AlignerError::CharError; records are still returned, parse.rs:92-97 */
+    SALN_E_FASTA_CHARS = -7, /* AlignerError::CharError; records are still returned, parse.rs:92-97 */
+    SALN_E_DEVICE_WAIT = -8  /* a kernel's inter-workgroup dependency wait gave up: the results
+                                of the executes since the last status check are invalid
+                                (saln_nw_plan_status; message: saln_last_error) */
 } saln_status;
+
+/* Device error flags (saln_nw_plan_status, saln_nw_avsa_status). */
+#define SALN_FLAG_WAIT_TIMEOUT 1u  /* a column-stripe fill's wait for its left neighbour's
+                                      boundary rows exceeded the plan's wait limit */
+#define SALN_FLAG_SPEC_UNLINKED 2u /* test builds only (SALN_SPEC_STRICT=1): a speculative
+                                      stripe walk fell back to the sequential walker */
 
 /* ScoringScheme, needleman_wunsch_affine.rs:15-20 / :382-388.
  * NULL everywhere means the reference SCHEME {5, -4, -8, -6}. */
@@ -181,6 +190,20 @@ int saln_nw_plan_set_async(saln_nw_plan *plan, int enable);
  * (end_states = printed = cigar_len = 0, flags bit 3 set). */
 int saln_nw_plan_set_score_only(saln_nw_plan *plan, int enable);
 int saln_nw_plan_sync(saln_nw_plan *plan, void *stream, int keep_latest);
+/* Device-side status of the plan's executes.  Waits (host-blocking) for every
+ * execute issued since the previous call, then returns the device error
+ * flags they raised (SALN_FLAG_*) in *flags (may be NULL) and clears them:
+ * read-and-clear, so each execute is reported exactly once.  Returns
+ * SALN_E_DEVICE_WAIT when a flag is set, SALN_OK otherwise.  The host-buffer
+ * entry points (saln_nw_align, saln_nw_align_batch, ...) check it themselves;
+ * device-plan callers call it after their executes (the kernels cannot fail
+ * a stream).  A column-stripe fill never hangs: its bounded wait sets the
+ * flag and the launch drains with wrong values for that pair. */
+int saln_nw_plan_status(saln_nw_plan *plan, uint32_t *flags);
+/* Polls a column-stripe dependency wait may spend before it gives up
+ * (default 2^24, each poll sleeping ~64 clocks).  Test hook: 0 makes any wait
+ * that finds its row unpublished fail, which injects SALN_FLAG_WAIT_TIMEOUT. */
+int saln_nw_plan_set_wait_limit(saln_nw_plan *plan, uint32_t polls);
 /* Waits for the device, then returns the plan's blocks to its context. */
 int saln_nw_plan_destroy(saln_nw_plan *plan);
 
@@ -202,6 +225,14 @@ int saln_nw_avsa_execute(saln_nw_avsa *a, const uint8_t *d_q_seq, const uint8_t 
 /* cells = sum over all pairs of len_q * len_db; fallback_pairs = pairs that
  * take the plan path. */
 int saln_nw_avsa_info(const saln_nw_avsa *a, uint64_t *cells, uint64_t *fallback_pairs);
+/* Launch geometry of a packed query class (fill variant 4-8; include/saln.h
+ * has no variant enum, the numbers are nw_kernels.hip's): the most pairs one
+ * launch takes and the workgroups (256 threads) that launch has.  Introspection
+ * for tests: blocks * 256 must stay a 32-bit work-item count. */
+int saln_nw_avsa_launch_geometry(int variant, uint64_t *chunk_pairs, uint64_t *grid_blocks);
+/* saln_nw_plan_status of the internal plan (SALN_OK without one); the packed
+ * classes have no inter-workgroup waits. */
+int saln_nw_avsa_status(saln_nw_avsa *a, uint32_t *flags);
 int saln_nw_avsa_destroy(saln_nw_avsa *a);
 
 /* ----------------------------------------------------------------------- WFA

@@ -12,7 +12,8 @@ import os
 import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-# SALN_LIB: an instrumented / experimental in-tree build (tools/) instead of libsaln.so
+# SALN_LIB: an instrumented in-tree build (tools/) instead of libsaln.so;
+# bench.py refuses to run with it set
 LIB_PATH = os.environ.get("SALN_LIB") or os.path.join(_HERE, "libsaln.so")
 
 # saln_status (include/saln.h)
@@ -30,13 +31,16 @@ E_CAPACITY = -4
 E_IO = -5
 E_FASTA = -6
 E_FASTA_CHARS = -7
+E_DEVICE_WAIT = -8
+FLAG_WAIT_TIMEOUT = 1   # SALN_FLAG_WAIT_TIMEOUT
+FLAG_SPEC_UNLINKED = 2  # SALN_FLAG_SPEC_UNLINKED
 
 STATUS_NAMES = {
     OK: "OK", NOT_IMPLEMENTED: "NOT_IMPLEMENTED", REF_PANIC_BOUNDARY: "REF_PANIC_BOUNDARY",
     REF_PANIC_TRIM: "REF_PANIC_TRIM", REF_PANIC_SLICE: "REF_PANIC_SLICE",
     NONCONVERGED: "NONCONVERGED", ENUM_CAP: "ENUM_CAP", E_INVALID: "E_INVALID", E_HIP: "E_HIP",
     E_NO_DEVICE: "E_NO_DEVICE", E_CAPACITY: "E_CAPACITY", E_IO: "E_IO", E_FASTA: "E_FASTA",
-    E_FASTA_CHARS: "E_FASTA_CHARS",
+    E_FASTA_CHARS: "E_FASTA_CHARS", E_DEVICE_WAIT: "E_DEVICE_WAIT",
 }
 
 CIGAR_OPS = {7: "=", 8: "X", 1: "I", 2: "D"}
@@ -75,7 +79,9 @@ EXPORTS = [
     "saln_nw_plan_create", "saln_nw_plan_info", "saln_nw_cigar_offsets", "saln_nw_execute",
     "saln_nw_plan_set_timing", "saln_nw_plan_kernel_time", "saln_nw_plan_set_async",
     "saln_nw_plan_set_score_only", "saln_nw_plan_sync", "saln_nw_plan_destroy",
+    "saln_nw_plan_status", "saln_nw_plan_set_wait_limit",
     "saln_nw_avsa_create", "saln_nw_avsa_execute", "saln_nw_avsa_info", "saln_nw_avsa_destroy",
+    "saln_nw_avsa_status", "saln_nw_avsa_launch_geometry",
     "saln_wfa_align_batch", "saln_wfa_render", "saln_wfa_plan_create", "saln_wfa_execute",
     "saln_wfa_plan_destroy",
     "saln_wfa_affine_batch", "saln_wfa_affine_plan_create", "saln_wfa_affine_execute",
@@ -148,6 +154,10 @@ def lib() -> C.CDLL:
         L.saln_nw_plan_sync.argtypes = [vp, vp, C.c_int]
         L.saln_nw_plan_set_score_only.argtypes = [vp, C.c_int]
         L.saln_nw_plan_destroy.argtypes = [vp]
+        L.saln_nw_plan_status.argtypes = [vp, u32p]
+        L.saln_nw_plan_set_wait_limit.argtypes = [vp, C.c_uint32]
+        L.saln_nw_avsa_status.argtypes = [vp, u32p]
+        L.saln_nw_avsa_launch_geometry.argtypes = [C.c_int, u64p, u64p]
         L.saln_nw_avsa_create.argtypes = [vp, vp, C.c_uint64, vp, C.c_uint64, C.c_int32,
                                           C.POINTER(NwScoring), C.POINTER(vp)]
         L.saln_nw_avsa_execute.argtypes = [vp, vp, vp, vp, vp]

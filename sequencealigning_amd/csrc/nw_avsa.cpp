@@ -176,11 +176,10 @@ int saln_nw_avsa_execute(saln_nw_avsa *a, const uint8_t *d_q_seq, const uint8_t 
     hipStream_t s = resolve_stream(stream, a->ctx);
     int2 *out = reinterpret_cast<int2 *>(d_out);
     const uint32_t nqt = (uint32_t)a->n_q;
-    // pairs per launch: the dispatch packet's grid size is a 32-bit count of
-    // work-items (a larger grid is silently truncated), and a 256-thread block
-    // of the packed fill covers 2 * (256 / G) >= 8 pairs
-    constexpr uint64_t kChunk = 1ull << 28;
     for (const auto &c : a->classes) {
+        // pairs per launch: the dispatch packet's grid size is a 32-bit count
+        // of work-items, so the chunk depends on the class's pairs per block
+        const uint64_t kChunk = avsa_chunk_pairs(c.variant);
         const uint64_t total = (uint64_t)c.nq * a->n_dn;
         for (uint64_t base = 0; base < total; base += kChunk) {
             const uint32_t n = (uint32_t)std::min<uint64_t>(kChunk, total - base);
@@ -194,7 +193,10 @@ int saln_nw_avsa_execute(saln_nw_avsa *a, const uint8_t *d_q_seq, const uint8_t 
     HIP_TRY(launch_avsa_boundary(a->d_qoff, a->d_doff, a->d_zero_q, a->n_zq, a->d_dids,
                                  (uint64_t)a->n_zq * a->n_dn, nqt, out, a->sc, s));
     if (a->fb) {
-        const int rc = saln_nw_execute(a->fb, d_q_seq, d_db_seq, a->d_fb_res, nullptr, s);
+        // the caller's stream argument as given: `s` is the resolved handle,
+        // and a resolved legacy null stream (0) would read as "the context's
+        // own stream" there, unordered with the scatter below
+        const int rc = saln_nw_execute(a->fb, d_q_seq, d_db_seq, a->d_fb_res, nullptr, stream);
         if (rc != SALN_OK) return rc;
         HIP_TRY(launch_avsa_scatter(a->d_fb_res, a->d_fb_qids, a->n_fb, a->d_dids,
                                     (uint64_t)a->n_fb * a->n_dn, nqt, out, s));
@@ -207,6 +209,20 @@ int saln_nw_avsa_info(const saln_nw_avsa *a, uint64_t *cells, uint64_t *fallback
     if (cells) *cells = a->cells;
     if (fallback_pairs) *fallback_pairs = (uint64_t)a->n_fb * a->n_dn;
     return SALN_OK;
+}
+
+int saln_nw_avsa_launch_geometry(int variant, uint64_t *chunk_pairs, uint64_t *grid_blocks) {
+    const uint64_t c = avsa_chunk_pairs(variant);
+    if (!c) return SALN_E_INVALID;
+    if (chunk_pairs) *chunk_pairs = c;
+    if (grid_blocks) *grid_blocks = avsa_launch_blocks(variant, c);
+    return SALN_OK;
+}
+
+int saln_nw_avsa_status(saln_nw_avsa *a, uint32_t *flags) {
+    if (flags) *flags = 0;
+    if (!a) return SALN_E_INVALID;
+    return a->fb ? saln_nw_plan_status(a->fb, flags) : SALN_OK;
 }
 
 int saln_nw_avsa_destroy(saln_nw_avsa *a) {

@@ -37,6 +37,9 @@ constexpr int32_t kSentinel = -32768;  // i16::MIN as i32, needleman_wunsch_affi
 constexpr int kNumVariants = 9;        // fill kernel variants (nw_kernels.hip)
 // plans with at least this many column-stripe waves use the packed stripe fill
 constexpr uint64_t kStripePkMinWaves = 1024;
+// polls a column-stripe dependency wait spends before it sets the plan's
+// timeout flag (saln_nw_plan_set_wait_limit; each poll sleeps ~64 clocks)
+constexpr uint32_t kWaitLimitDefault = 1u << 24;
 
 struct Scoring {
     int32_t match, mismatch, gap_open, gap_extend;

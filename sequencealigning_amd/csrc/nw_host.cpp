@@ -29,6 +29,21 @@ Scoring scoring_or_default(const saln_nw_scoring *s) {
     return Scoring{s->match, s->mismatch, s->gap_open, s->gap_extend};
 }
 
+// The i32 fills carry V'' = 4V + 2a + p plus the position offsets alpha*r +
+// beta*c (nw_common.hpp).  |V| is at most the sentinel plus one step's
+// largest change per row and column of the path; a pair passes while that
+// bound, scaled and offset, stays inside int32 (the reference's own i32
+// arithmetic is exact far beyond it: the pairs rejected here are ~10^8 long
+// or carry penalties of ~10^4).
+bool scores_fit_i32(const Scoring &s, uint64_t lq, uint64_t ld) {
+    auto a = [](int64_t v) { return v < 0 ? -v : v; };
+    const int64_t step = std::max({a(s.match), a(s.mismatch), a(s.gap_open) + a(s.gap_extend)});
+    const long double v = 32768.0L + (long double)(lq + ld) * (long double)step;
+    const long double off = 4.0L * (a(s.match) + 2 * a(s.gap_extend)) * (long double)ld +
+                            4.0L * a(s.gap_extend) * (long double)lq;
+    return 4.0L * v + 3.0L + off < 2147483647.0L;
+}
+
 }  // namespace saln
 
 using namespace saln;
@@ -64,7 +79,12 @@ struct saln_nw_plan {
     // per-pair first work item (plan order, n_pairs+1), progress counters
     uint2 *d_work = nullptr;
     std::vector<uint32_t> work_first;
+    // d_err[0]: device error flags since the last saln_nw_plan_status (bit 0
+    // a dependency wait timed out, bit 1 an unlinked speculative walk under
+    // SALN_SPEC_STRICT); d_err[1]: the wait limit the fills read
     uint32_t *d_prog = nullptr, *d_err = nullptr;
+    uint32_t wait_limit = kWaitLimitDefault;
+    bool unchecked[2] = {false, false};  // executes on workspace b since the last status
     uint64_t n_prog = 0;
     uint32_t *d_ops = nullptr;  // traceback op-stream scratch (one traceback at a time)
     // speculative stripe walks (a few long column-stripe pairs): block map,
@@ -197,6 +217,12 @@ int saln_nw_plan_create(saln_context *ctx, const uint64_t *q_off, uint64_t n_q,
         if (lq > 0x7FFFFFFFull || ld > 0x7FFFFFFFull) {
             delete p;
             set_error("sequence too long");
+            return SALN_E_INVALID;
+        }
+        if (!scores_fit_i32(p->sc, lq, ld)) {
+            delete p;
+            set_error("pair too long for these penalties: its scores could leave the engine's "
+                      "int32 range");
             return SALN_E_INVALID;
         }
         d.len_q = (uint32_t)lq;
@@ -332,15 +358,15 @@ int saln_nw_plan_create(saln_context *ctx, const uint64_t *q_off, uint64_t n_q,
             }
             const uint64_t packed = rows * nbm * np * lb;
             if (v == kStripeVariant) {
-                // skewed, one region per stripe (nw_common.hpp): every fill
-                // step of a stripe wave writes one whole 256-byte line
-                // (row fill: unskewed 256-column tiles, bs = 4, same region size)
+                // one region per 256-column chunk: the row fill's unskewed
+                // 256-column tiles (bs = 4), or the packed stripes' skewed
+                // lines (bs = 0: every fill step writes one whole line)
                 const bool pk = p->stripe_pk;
                 for (uint32_t s = 0; s < np; ++s) {
                     NwPairDesc &d = p->h_pairs[a + s];
                     d.mask_off = moff;
                     d.mask_rs = g.W();
-                    d.mask_bs = pk ? 0u : p->stripe_rows ? (uint32_t)lb : (uint32_t)(g.W() + lb);
+                    d.mask_bs = pk ? 0u : (uint32_t)lb;
                     d.mask_cs = ((uint64_t)d.len_db + (pk ? 2 * g.G : g.G) - 1) * g.W();
                     moff += g.n_chunks(d.len_q) * d.mask_cs;
                 }
@@ -454,8 +480,9 @@ int saln_nw_plan_create(saln_context *ctx, const uint64_t *q_off, uint64_t n_q,
                 (e = hipMemcpy(p->d_work, work.data(), work.size() * sizeof(uint2),
                                hipMemcpyHostToDevice)) != hipSuccess ||
                 (e = dev_alloc(p->ctx, (void **)&p->d_prog, p->n_prog * sizeof(uint32_t))) != hipSuccess ||
-                (e = dev_alloc(p->ctx, (void **)&p->d_err, sizeof(uint32_t))) != hipSuccess ||
-                (e = hipMemset(p->d_err, 0, sizeof(uint32_t))) != hipSuccess)
+                (e = dev_alloc(p->ctx, (void **)&p->d_err, 2 * sizeof(uint32_t))) != hipSuccess ||
+                (e = hipMemcpy(p->d_err, std::array<uint32_t, 2>{0u, kWaitLimitDefault}.data(),
+                               2 * sizeof(uint32_t), hipMemcpyHostToDevice)) != hipSuccess)
                 return fail(e, "stripe work list");
             if ((e = hipMemcpy(p->d_pairs, p->h_pairs.data(), n_pairs * sizeof(NwPairDesc),
                                hipMemcpyHostToDevice)) != hipSuccess)
@@ -642,6 +669,7 @@ int saln_nw_execute(saln_nw_plan *p, const uint8_t *d_q, const uint8_t *d_db,
     if (ev) HIP_TRY(hipEventRecord(ev[3], t));
     HIP_TRY(hipEventRecord(p->tb_done(cur), t));
     p->tb_pending[cur] = true;
+    p->unchecked[cur] = true;
     p->last_buf = cur;
     if (p->async_tb) {
         p->buf ^= 1;  // results complete once saln_nw_plan_sync'ed
@@ -667,6 +695,39 @@ int saln_nw_plan_set_async(saln_nw_plan *p, int enable) {
     }
     p->async_tb = enable != 0;
     p->buf = 0;
+    return SALN_OK;
+}
+
+int saln_nw_plan_status(saln_nw_plan *p, uint32_t *flags) {
+    if (flags) *flags = 0;
+    if (!p) return SALN_E_INVALID;
+    HIP_TRY(hipSetDevice(p->ctx->device));
+    for (int b = 0; b < 2; ++b)
+        if (p->unchecked[b]) HIP_TRY(hipEventSynchronize(p->tb_done(b)));
+    p->unchecked[0] = p->unchecked[1] = false;
+    uint32_t v = 0;
+    if (p->d_err) {
+        HIP_TRY(hipMemcpy(&v, p->d_err, sizeof v, hipMemcpyDeviceToHost));
+        if (v) HIP_TRY(hipMemset(p->d_err, 0, sizeof v));  // read and clear
+    }
+    if (flags) *flags = v;
+    if (v & SALN_FLAG_WAIT_TIMEOUT) {
+        set_error("column-stripe dependency wait timed out (results of the executes since the "
+                  "last status are invalid)");
+        return SALN_E_DEVICE_WAIT;
+    }
+    if (v & SALN_FLAG_SPEC_UNLINKED) {
+        set_error("speculative stripe walk did not link (SALN_SPEC_STRICT=1)");
+        return SALN_E_DEVICE_WAIT;
+    }
+    return SALN_OK;
+}
+
+int saln_nw_plan_set_wait_limit(saln_nw_plan *p, uint32_t polls) {
+    if (!p) return SALN_E_INVALID;
+    HIP_TRY(hipSetDevice(p->ctx->device));
+    p->wait_limit = polls;
+    if (p->d_err) HIP_TRY(hipMemcpy(p->d_err + 1, &polls, sizeof polls, hipMemcpyHostToDevice));
     return SALN_OK;
 }
 
@@ -950,20 +1011,7 @@ bool first_alignment(const HostMask &hm, const uint8_t *q, const uint8_t *d,
 }  // namespace saln
 
 namespace saln {
-int plan_check_error(const saln_nw_plan *p) {
-    if (!p || !p->d_err) return SALN_OK;
-    uint32_t v = 0;
-    HIP_TRY(hipMemcpy(&v, p->d_err, sizeof v, hipMemcpyDeviceToHost));
-    if (v & 1u) {
-        set_error("column-stripe dependency wait timed out");
-        return SALN_E_HIP;
-    }
-    if (v & 2u) {
-        set_error("speculative stripe walk did not link (SALN_SPEC_STRICT=1)");
-        return SALN_E_HIP;
-    }
-    return SALN_OK;
-}
+int plan_check_error(saln_nw_plan *p) { return saln_nw_plan_status(p, nullptr); }
 }  // namespace saln
 
 namespace saln {

@@ -115,7 +115,10 @@ hipError_t launch_traceback_spec(const NwPairDesc *pairs, SpecArgs sa, uint32_t 
                                  const int32_t *end_h, saln_nw_result *results, uint32_t *cigar,
                                  Scoring sc, int stripe_layout, uint32_t *strict_err,
                                  hipStream_t stream);
-// score-only all-vs-all (nw_avsa.cpp)
+// score-only all-vs-all (nw_avsa.cpp); avsa_chunk_pairs: the most pairs one
+// launch of a packed class may take (0: not a packed variant)
+uint64_t avsa_chunk_pairs(int variant);
+uint64_t avsa_launch_blocks(int variant, uint64_t count);  // workgroups of one launch
 hipError_t launch_avsa(int variant, const uint64_t *q_off, const uint64_t *d_off,
                        const uint32_t *q_ids, uint32_t nq, const uint32_t *d_ids,
                        uint32_t nq_total, uint64_t base, uint32_t count, const uint8_t *qs,
@@ -183,8 +186,9 @@ struct HostMask {
     void to_dense(uint8_t *out) const;
 };
 
-// SALN_E_HIP if a column-stripe fill hit its dependency-wait bound.
-int plan_check_error(const saln_nw_plan *plan);
+// saln_nw_plan_status without the flags: SALN_E_DEVICE_WAIT if a column-stripe
+// fill hit its dependency-wait bound since the last check.
+int plan_check_error(saln_nw_plan *plan);
 
 // Full parent codes (every parent set, needed by the host DFS and the dense
 // export) instead of the walk codes a plan stores by default.

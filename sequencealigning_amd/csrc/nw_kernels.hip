@@ -29,16 +29,6 @@ namespace saln {
 bool stripe_packed(const Scoring &sc, uint64_t n_waves, bool wide);
 }
 
-#ifndef SALN_PINGPONG
-#define SALN_PINGPONG 1
-#endif
-#ifndef SALN_PAIRMAP
-#define SALN_PAIRMAP 0
-#endif
-#ifndef SALN_EXP_NOSTORE
-#define SALN_EXP_NOSTORE 0  // experiment builds only: fill without mask stores
-#endif
-
 namespace saln {
 
 // lane i <- lane i-1 within the group; the group's lane 0 keeps `old`.
@@ -637,7 +627,7 @@ __global__ __launch_bounds__(256) void nw_traceback_kernel(
 constexpr int32_t kCoopLine = 256;  // bytes per line (one stripe step)
 constexpr int32_t kCoopSlack = 64;  // rows loaded beyond a diagonal crossing of the stripe
 
-// kLay: 0 the skewed stripe layout (row r of lane l on line r - 1 + l); 1 the
+// kLay: 1 the
 // packed stripe layout (bs == 0): virtual lane v = (c - c0) / 2 of row r sits
 // on line r - 1 + v (127 lines of skew); 2 the row-major 256-column tiles of
 // nw_fill_rows_kernel (no skew: row r is line r - 1).
@@ -652,8 +642,9 @@ __global__ __launch_bounds__(64 * NWV) void nw_traceback_coop_kernel(
     const int32_t *__restrict__ end_h, saln_nw_result *__restrict__ results,
     uint32_t *__restrict__ cigar, Scoring sc, int32_t kCoopRows,
     const uint8_t *__restrict__ qs, const uint8_t *__restrict__ ds, SpecArgs sa) {
+    static_assert(kLay == 1 || kLay == 2, "round 1's skewed i32 stripe layout is retired");
     constexpr bool kPk = kLay == 1;
-    constexpr int32_t kSkew = kLay == 1 ? 127 : kLay == 2 ? 0 : 63;  // lines from a row's first to its last block
+    constexpr int32_t kSkew = kLay == 1 ? 127 : 0;  // lines from a row's first to its last block
     // kCoopRows + kSkew lines, rounded up to whole 4-line DMAs; then the
     // request words wave 0 posts to the loader waves
     extern __shared__ __attribute__((aligned(16))) uint8_t win[];
@@ -1159,7 +1150,9 @@ struct MaskWords {
 constexpr uint32_t kPub = 32;
 // the boundary column's preset (H word): no fill value comes near INT32_MIN
 constexpr uint32_t kColEmpty = 0x80000000u;
-constexpr uint32_t kSpinCap = 1u << 24;
+// err[0]: flags (bit 0: a dependency wait timed out), err[1]: the polls a
+// wait may spend before it gives up (the plan's wait limit, default 2^24;
+// tests set it to 0 to inject a timeout)
 
 // ------------------------------------------------------- packed-i16 fill
 // Two pairs per lane group: pair A in the low 16 bits of every register,
@@ -1335,13 +1328,10 @@ __host__ __device__ inline int32_t rebase_center(const Scoring &sc, int32_t W) {
     return (W * (2 * m + 4 * ge) / 2) & ~1;
 }
 
-#ifndef SALN_PK_WAVES
-// experiment switch: min waves per SIMD the packed fill is built for.  At 124
-// VGPRs it runs 4; 5 (96 VGPRs) spills 26 registers: C2 fill 0.97 -> 1.57 ms
-#define SALN_PK_WAVES 1
-#endif
+// (Built for one wave per SIMD: at 124 VGPRs it runs 4; built for 5, 96
+// VGPRs, it spills 26 registers: C2 fill 0.97 -> 1.57 ms, round 1.)
 template <int G, int K, int kCodes, typename Src, int KS, bool kRebase = false>
-__global__ __launch_bounds__(256, SALN_PK_WAVES) void nw_fill_pk_kernel(Src src, uint32_t count,
+__global__ __launch_bounds__(256) void nw_fill_pk_kernel(Src src, uint32_t count,
                                                          const uint8_t *__restrict__ qs,
                                                          const uint8_t *__restrict__ ds,
                                                          uint8_t *__restrict__ mask, Scoring sc,
@@ -1351,14 +1341,7 @@ __global__ __launch_bounds__(256, SALN_PK_WAVES) void nw_fill_pk_kernel(Src src,
     extern __shared__ uint32_t drow[];  // [GPB][G + ld_max + G] packed db chars (dch) per row
     const int lane = threadIdx.x % G;
     const uint32_t gi = pack_block(blocks_per_pack(2 * GPB)) * GPB + threadIdx.x / G;
-#if SALN_PAIRMAP
-    // the GW groups of a wave hold pairs w*2GW + g (A) and + GW (B): each
-    // mask store instruction writes GW adjacent segments per (row, block)
-    constexpr uint32_t GW = 64 / G;
-    const uint32_t ia = (gi / GW) * 2 * GW + gi % GW, ib = ia + GW;
-#else
     const uint32_t ia = 2 * gi, ib = 2 * gi + 1;
-#endif
     if (ia >= count) return;  // whole group
     const bool hasB = ib < count;
     const NwPairDesc pa = src.pair(ia);
@@ -1436,20 +1419,15 @@ __global__ __launch_bounds__(256, SALN_PK_WAVES) void nw_fill_pk_kernel(Src src,
                                (int64_t)lane * (int64_t)pb.mask_rs;
     const uint32_t *__restrict__ rowp = myrow - lane;  // word of row r-1 at step 0
     const uint16_t *__restrict__ rowp16 = myrow16 - lane;
-#if SALN_EXP_NOSKEW  // timing experiment only (wrong results): no pipeline ramp
-    const int T = ldM;
-#else
     const int T = (int)geo.steps((uint32_t)ldM);
-#endif
     // Walk codes: a lane whose columns all lie past a pair's query stores
     // nothing for it (no walker reads past column len_q; 16 x 10 groups on
     // 150-column queries: one store of 16 saved).  Full codes keep every
     // segment defined.
     const int ldAs = (kCodes == kCodesWalk && col0 >= lqA) ? 0 : ldA;
     const int ldBs = (kCodes == kCodesWalk && col0 >= lqB) ? 0 : ldB;
-    // Previous-row H: step t reads Hin (row r-1) and writes Hout (row r).
-    // SALN_PINGPONG: a two-step unroll swaps two arrays (no register
-    // rotation, more live registers); otherwise in place.
+    // Previous-row H: step t reads Hin (row r-1) and writes Hout (row r); a
+    // two-step unroll swaps two arrays (no register rotation).
     uint32_t HpB[K];
 
     auto step = [&](int t, uint32_t(&Hin)[K], uint32_t(&Hout)[K]) __attribute__((always_inline)) {
@@ -1566,13 +1544,6 @@ __global__ __launch_bounds__(256, SALN_PK_WAVES) void nw_fill_pk_kernel(Src src,
                         wb[sg].w[w] = __builtin_amdgcn_perm(hi, lo, 0x07050301u);
                     }
                 }
-#if SALN_EXP_NOSTORE
-#pragma unroll
-                for (int sg = 0; sg < NS; ++sg)
-#pragma unroll
-                    for (int w = 0; w < (KS + 3) / 4; ++w)
-                        asm volatile("" : : "v"(wa[sg].w[w]), "v"(wb[sg].w[w]));
-#else
                 if (r <= ldAs) {
 #pragma unroll
                     for (int sg = 0; sg < NS; ++sg)
@@ -1583,7 +1554,6 @@ __global__ __launch_bounds__(256, SALN_PK_WAVES) void nw_fill_pk_kernel(Src src,
                     for (int sg = 0; sg < NS; ++sg)
                         *reinterpret_cast<PkMask<KS> *>(mB + (uint64_t)sg * pb.mask_bs) = wb[sg];
                 }
-#endif
             }
             if (t == tEA) {
                 int32_t e = 0;
@@ -1606,17 +1576,12 @@ __global__ __launch_bounds__(256, SALN_PK_WAVES) void nw_fill_pk_kernel(Src src,
         mA += pa.mask_rs;
         mB += pb.mask_rs;
     };
-#if SALN_PINGPONG
     int t = 0;
     for (; t + 1 < T; t += 2) {
         step(t, Hp, HpB);
         step(t + 1, HpB, Hp);
     }
     if (t < T) step(t, Hp, HpB);
-#else
-    (void)HpB;
-    for (int t = 0; t < T; ++t) step(t, Hp, Hp);
-#endif
 }
 
 // Column-stripe fill (declared with the stripe protocol above), i32 lanes.
@@ -1661,305 +1626,6 @@ __device__ __forceinline__ uint32_t stripe_code_word(const uint32_t (&s)[8][4]) 
     return stripe_code_word<kCodes, true>(s);
 }
 
-// kSplit (parent codes, a few stripes): the stripe's wave keeps the
-// recurrence and hands each step's M / D of its columns, the first column's
-// I and the row's char to a second wave through an 8-step LDS ring; the
-// second wave rebuilds H, the gap candidates and the code words and stores
-// them.  The two waves meet at one barrier per four-step group.  It pays
-// only while the pipeline is short (C1: fill 0.42 -> 0.38 ms); one long
-// pair or a batch runs slower with it.
-template <int K, int kCodes, bool kMinPen, bool kSplit = false>
-__global__ __launch_bounds__(128) void nw_fill_stripe_kernel(
-    const NwPairDesc *__restrict__ pairs, const uint2 *__restrict__ work,
-    const uint8_t *__restrict__ qs, const uint8_t *__restrict__ ds, uint8_t *__restrict__ mask,
-    int2 *__restrict__ scratch, uint32_t *__restrict__ prog, uint32_t *__restrict__ err,
-    int32_t *__restrict__ end_h, Scoring sc) {
-    static_assert(K == 4, "one code dword per lane and row");
-    static_assert(!kSplit || kCodes != kCodesNone, "the coder wave writes codes");
-    constexpr int G = 64;
-    constexpr Geom geo{G, K};
-    const int lane = threadIdx.x & 63;
-    __shared__ uint4 pay[kSplit ? 8 * 64 * 3 : 1];  // [step % 8][lane][M, D, (I0, char)]
-    const uint2 wk = work[blockIdx.x];
-    const NwPairDesc p = pairs[wk.x];
-    const uint32_t c = wk.y;
-    const uint32_t lq = p.len_q, ld = p.len_db;
-    const uint8_t *__restrict__ q = qs + p.q_off;
-    const uint8_t *__restrict__ d = ds + p.db_off;
-    const uint32_t nch = geo.n_chunks(lq);
-    const int2 *__restrict__ scr_in = c > 0 ? scratch + p.scratch_off + (uint64_t)(c - 1) * scratch_col(ld) : nullptr;
-    int2 *__restrict__ scr_out = c + 1 < nch ? scratch + p.scratch_off + (uint64_t)c * scratch_col(ld) : nullptr;
-    // V'' = 4V + 2a + p (nw_common.hpp): offsets and constants scaled by 4
-    const int32_t beta = -4 * sc.gap_extend;
-    const int32_t alpha = -4 * sc.match - beta;
-    const int32_t pen_max = 4 * (sc.match - sc.mismatch);
-    // chars carried as c << 8: q ^ d is 0 or >= 256, so min() is the penalty
-    // whenever 0 <= pen_max <= 256 (kMinPen); otherwise a select
-    const int32_t kOpen = 4 * sc.gap_open;
-    const int32_t kDstep = 4 * sc.gap_extend + alpha;
-    // tie masks: walk codes keep the alive tied parents (& ~1) except on the
-    // last row, whose argmax bits only the end cell uses: the reference's
-    // end states (& ~3); full codes are the reference's parent sets
-    constexpr int32_t kTieOr = kCodes == kCodesFull ? 3 : 1;
-    const uint32_t jend = lq - 1;
-    const bool end_lane = jend / geo.W() == c && (uint32_t)lane == (jend % geo.W()) / K;
-    const uint32_t k_end = jend % K;
-
-    const uint32_t col0 = c * geo.W() + (uint32_t)lane * K;  // my columns: col0+1 .. col0+K
-    uint32_t qc[K];
-    int32_t Hp[K], Dn[K];
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-        const uint32_t j = col0 + k + 1;
-        qc[k] = j <= lq ? (uint32_t)q[j - 1] << 8 : 0xFFFFFF00u;
-        Hp[k] = hs4_row0(sc, j) + beta * (int32_t)j;
-        Dn[k] = ds4_row1(sc, j) + alpha + beta * (int32_t)j;
-    }
-    int32_t hd = hs4_row0(sc, col0) + beta * (int32_t)col0;
-    int32_t pubF = 0, pubH = 0;
-    // db chars: lane 0 needs d[t] at step t (wave-uniform).  Steps run in
-    // groups of four; a group's four chars d[t..t+3] are one scalar word
-    // funnel-shifted from a rolling pair of aligned dwords (the next loaded a
-    // group ahead), so a step spends one constant-shift extract on its char;
-    // the other lanes take their row's char from the left neighbour's
-    // previous step (DPP).
-    typedef const __attribute__((address_space(4))) uint32_t cu32;  // constant: scalar loads
-    cu32 *dw = (cu32 *)((uintptr_t)d & ~(uintptr_t)3);
-    const uint32_t doff = 8u * (uint32_t)((uintptr_t)d & 3);  // bit offset of d[0] in dw[0]
-    const uint32_t last_dw = ((uint32_t)ld - 1 + (uint32_t)((uintptr_t)d & 3)) >> 2;
-    uint32_t dnidx = min(1u, last_dw);  // dword index of dnxt
-    uint32_t dcur = dw[0], dnxt = dw[dnidx];
-    auto group_chars = [&]() __attribute__((always_inline)) {
-        const uint32_t w = doff ? (dcur >> doff) | (dnxt << (32u - doff)) : dcur;
-        dcur = dnxt;  // past the db's last dword the bytes are unused
-        dnidx = min(dnidx + 1, last_dw);
-        dnxt = dw[dnidx];
-        return w;
-    };
-    uint32_t dch = 0;
-    int32_t blkH = 0, blkF = 0;  // lanes 0..31: the left column of the current 32-row block
-    bool failed = false;
-    // lane l's row t-l+1 at step t: mask_off + c*cs + l*bs + (t-l)*rs; in the
-    // skewed stripe layout (nw_common.hpp) step t's dwords are line t
-    uint8_t *mseg = mask + p.mask_off + (uint64_t)c * p.mask_cs + (uint64_t)lane * p.mask_bs -
-                    (int64_t)lane * (int64_t)p.mask_rs;
-    const int T = (int)geo.steps(ld);
-    // the query chars above arrive here: otherwise the wait for them lands
-    // inside the loop, where it would also wait for every mask store
-    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
-    if constexpr (kSplit) {
-        if (threadIdx.x >= 64) {  // the coder wave: group g after the stripe wave's barrier g
-            const int NG = (T + 3) / 4;
-            for (int g = 0; g < NG; ++g) {
-                __syncthreads();
-#pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    const int tt = 4 * g + u;
-                    const int r = tt - lane + 1;
-                    if (tt < T && r >= 1 && r <= (int)ld) {
-                        const uint4 *sl = pay + ((tt & 7) * 64 + lane) * 3;
-                        const uint4 pm = sl[0], pd = sl[1], px = sl[2];
-                        const int32_t Mv[4] = {(int32_t)pm.x, (int32_t)pm.y, (int32_t)pm.z, (int32_t)pm.w};
-                        const int32_t Dv[4] = {(int32_t)pd.x, (int32_t)pd.y, (int32_t)pd.z, (int32_t)pd.w};
-                        int32_t I = (int32_t)px.x;
-                        const uint32_t dc = px.y;
-                        uint32_t sg[8][4];
-#pragma unroll
-                        for (int k = 0; k < K; ++k) {
-                            const int32_t M = Mv[k], D = Dv[k];
-                            const int32_t H = max(M, max(I, D));
-                            const int32_t tO = M + kOpen;
-                            const int32_t Hc = H & (kCodes == kCodesFull || r == (int)ld ? ~3 : ~1);
-                            const int32_t tOr = tO | kTieOr;
-                            sg[0][k] = (uint32_t)(M - Hc);
-                            sg[1][k] = (uint32_t)(I - Hc);
-                            sg[2][k] = (uint32_t)(D - Hc);
-                            sg[4][k] = (uint32_t)(tOr - I);
-                            sg[6][k] = (uint32_t)(tOr - D);
-                            sg[7][k] = (qc[k] ^ dc) - 1u;  // sign <=> q == d
-                            if constexpr (kCodes == kCodesFull) {
-                                const int32_t tOc = tO & ~3;
-                                sg[3][k] = (uint32_t)(I - tOc);
-                                sg[5][k] = (uint32_t)(D - tOc);
-                            } else {
-                                sg[3][k] = sg[5][k] = 0u;
-                            }
-                            I = max(tO, I);
-                        }
-                        *reinterpret_cast<uint32_t *>(mseg + (uint64_t)tt * p.mask_rs) =
-                            stripe_code_word<kCodes>(sg);
-                    }
-                }
-            }
-            __syncthreads();  // the stripe wave's last barrier
-            return;
-        }
-    }
-    // Previous-row H: step t reads Hin (row r-1) and writes Hout (row r); a
-    // two-step unroll swaps the arrays instead of rotating registers.
-    int32_t HpB[K];
-    // the last lane's outputs of a group's four steps, published per group
-    // (named registers, not an array: the compiler put an array in scratch)
-    int32_t gH0 = 0, gH1 = 0, gH2 = 0, gH3 = 0, gF0 = 0, gF1 = 0, gF2 = 0, gF3 = 0;
-    // pos = t % 4; only a group start can open a 32-row block
-    auto step = [&](int t, int32_t(&Hin)[K], int32_t(&Hout)[K], uint32_t dt,
-                    auto pos_c) __attribute__((always_inline)) {
-        constexpr int kPos = decltype(pos_c)::value;
-        constexpr bool kGroupStart = kPos == 0;
-        const int r = t - lane + 1;
-        dch = (uint32_t)shr1<G>((int32_t)(dt << 8), (int32_t)dch);  // d[r-1]
-        int32_t bF, bH;
-        const uint32_t rr = (uint32_t)t + 1;  // lane 0's row
-        if (c == 0) {
-            bF = is4_col1(sc, rr) + alpha * (int32_t)rr + beta;
-            bH = hs4_col0(sc, rr) + alpha * (int32_t)rr;
-        } else {
-            if (kGroupStart && (rr - 1) % kPub == 0 && rr <= ld) {  // new 32-row block of the left column
-                const uint32_t row = rr + (uint32_t)lane;
-                // every row is its own publication: the column was preset to
-                // kColEmpty, so a lane's value is ready once it differs
-                uint32_t spins = 0;
-                for (;;) {
-                    bool ok = true;
-                    if (lane < (int)kPub && row <= ld) {
-                        const uint64_t v = __hip_atomic_load((const uint64_t *)(scr_in + row),
-                                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        blkH = (int32_t)(uint32_t)v;
-                        blkF = (int32_t)(uint32_t)(v >> 32);
-                        ok = (uint32_t)blkH != kColEmpty;
-                    }
-                    if (__builtin_amdgcn_ballot_w64(!ok) == 0 || failed) break;
-                    __builtin_amdgcn_s_sleep(2);
-                    if (++spins > kSpinCap) failed = true;
-                }
-                // wait here, on the block step only: otherwise the compiler
-                // puts a vmcnt(0) (every outstanding mask store) on the join
-                // path of every step, before the readlanes below
-                __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
-            }
-            const uint32_t sl = (rr - 1) % kPub;
-            bH = __builtin_amdgcn_readlane(blkH, sl);
-            bF = __builtin_amdgcn_readlane(blkF, sl);
-        }
-        const int32_t inF = shr1<G>(bF, pubF);
-        const int32_t inH = shr1<G>(bH, pubH);
-        if (r >= 1 && r <= (int)ld) {
-            int32_t F = inF;
-            const int32_t hm = kCodes == kCodesFull || r == (int)ld ? ~3 : ~1;
-            uint32_t sg[8][4];
-            int32_t Mk[K], Dk[K];  // kSplit: the coder wave's inputs
-            int32_t diag = hd;  // H~(r-1, c-1) of column k
-#pragma unroll
-            for (int k = 0; k < K; ++k) {
-                const int32_t hdk = diag;
-                diag = Hin[k];
-                const uint32_t x = qc[k] ^ dch;
-                const int32_t pen = kMinPen ? (int32_t)min(x, (uint32_t)pen_max) : (x ? pen_max : 0);
-                const int32_t M = hdk - pen;
-                const int32_t I = F, D = Dn[k];
-                const int32_t H = max(M, max(I, D));
-                const int32_t tO = M + kOpen;
-                if constexpr (kSplit) {
-                    Mk[k] = M;
-                    Dk[k] = D;
-                } else if constexpr (kCodes != kCodesNone) {
-                    const int32_t Hc = H & hm;
-                    const int32_t tOr = tO | kTieOr;
-                    sg[0][k] = (uint32_t)(M - Hc);
-                    sg[1][k] = (uint32_t)(I - Hc);
-                    sg[2][k] = (uint32_t)(D - Hc);
-                    sg[4][k] = (uint32_t)(tOr - I);
-                    sg[6][k] = (uint32_t)(tOr - D);
-                    sg[7][k] = x - 1u;  // sign <=> q == d
-                    if constexpr (kCodes == kCodesFull) {
-                        const int32_t tOc = tO & ~3;
-                        sg[3][k] = (uint32_t)(I - tOc);
-                        sg[5][k] = (uint32_t)(D - tOc);
-                    } else {
-                        sg[3][k] = sg[5][k] = 0u;
-                    }
-                }
-                F = max(tO, I);
-                Dn[k] = max(tO, D) + kDstep;
-                Hout[k] = H;
-            }
-            hd = inH;
-            pubF = F;
-            pubH = Hout[K - 1];
-            if constexpr (kPos == 0) gH0 = pubH, gF0 = pubF;
-            if constexpr (kPos == 1) gH1 = pubH, gF1 = pubF;
-            if constexpr (kPos == 2) gH2 = pubH, gF2 = pubF;
-            if constexpr (kPos == 3) gH3 = pubH, gF3 = pubF;
-            if constexpr (kSplit) {
-                uint4 *sl = pay + ((t & 7) * 64 + lane) * 3;
-                sl[0] = make_uint4((uint32_t)Mk[0], (uint32_t)Mk[1], (uint32_t)Mk[2], (uint32_t)Mk[3]);
-                sl[1] = make_uint4((uint32_t)Dk[0], (uint32_t)Dk[1], (uint32_t)Dk[2], (uint32_t)Dk[3]);
-                sl[2] = make_uint4((uint32_t)inF, dch, 0u, 0u);
-            } else if constexpr (kCodes != kCodesNone) {
-                *reinterpret_cast<uint32_t *>(mseg) = stripe_code_word<kCodes>(sg);
-            }
-        } else {
-#pragma unroll
-            for (int k = 0; k < K; ++k) Hout[k] = Hin[k];  // lane idle: keep row r-1
-        }
-        mseg += p.mask_rs;
-    };
-    // The last lane's rows of steps t0 .. t0+n-1 (rows t0-62 ..) to the
-    // boundary column, with agent-coherent (write-through) stores; a stored
-    // row replaces the preset and is thereby published.
-    auto publish = [&](int t0, int n) __attribute__((always_inline)) {
-        if (lane == G - 1 && scr_out) {
-            const int lo = max(t0 - (G - 2), 1), hi = min(t0 + n - 1 - (G - 2), (int)ld);
-            if (hi >= lo) {
-                auto put = [&](int q, int32_t h, int32_t f) __attribute__((always_inline)) {
-                    const int r = t0 + q - (G - 2);
-                    if (q < n && r >= lo && r <= hi)
-                        __hip_atomic_store((uint64_t *)(scr_out + r),
-                                           (uint64_t)(uint32_t)h | ((uint64_t)(uint32_t)f << 32),
-                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                };
-                put(0, gH0, gF0);
-                put(1, gH1, gF1);
-                put(2, gH2, gF2);
-                put(3, gH3, gF3);
-            }
-        }
-    };
-    static_assert(kPub % 4 == 0, "block starts fall on group starts");
-    const std::integral_constant<int, 0> p0;
-    const std::integral_constant<int, 1> p1;
-    const std::integral_constant<int, 2> p2;
-    const std::integral_constant<int, 3> p3;
-    int t = 0;
-    for (; t + 3 < T; t += 4) {
-        const uint32_t w = group_chars();
-        step(t, Hp, HpB, w & 0xFFu, p0);
-        step(t + 1, HpB, Hp, (w >> 8) & 0xFFu, p1);
-        step(t + 2, Hp, HpB, (w >> 16) & 0xFFu, p2);
-        step(t + 3, HpB, Hp, w >> 24, p3);
-        publish(t, 4);
-        if constexpr (kSplit) __syncthreads();  // group ready for the coder wave
-    }
-    const int ntail = T - t;
-    if (ntail > 0) {
-        const uint32_t w = group_chars();
-        step(t, Hp, HpB, w & 0xFFu, p0);
-        if (ntail > 1) step(t + 1, HpB, Hp, (w >> 8) & 0xFFu, p1);
-        if (ntail > 2) step(t + 2, Hp, HpB, (w >> 16) & 0xFFu, p2);
-        publish(t, ntail);
-        if constexpr (kSplit) __syncthreads();
-    }
-    if constexpr (kSplit) __syncthreads();  // the coder's last group is done
-    if (end_lane) {  // every lane ends on row ld, in the array the last step wrote
-        int32_t e = 0;
-#pragma unroll
-        for (int k = 0; k < K; ++k)
-            if ((uint32_t)k == k_end) e = (ntail & 1) ? HpB[k] : Hp[k];
-        end_h[wk.x] = x4_to_x2(e - alpha * (int32_t)ld - beta * (int32_t)lq);
-    }
-    if (failed && lane == 0) atomicOr(err, 1u);
-}
-
 // ------------------------------------- long pairs: row-synchronous stripes
 // One wave per stripe of 64*K columns (K = 1, 2, 4), all 64 lanes on the same
 // row at the same step.  A stripe then has no internal skew: its right
@@ -1980,22 +1646,8 @@ __global__ __launch_bounds__(128) void nw_fill_stripe_kernel(
 // per row as one 64-bit agent-coherent store into boundary column g (preset
 // to kColEmpty); stripe g+1 polls kRowsBlk-row blocks (nw_fill_stripe_kernel).
 constexpr int32_t kNegInf = INT32_MIN;
-#ifndef SALN_ROWS_OFF
-#define SALN_ROWS_OFF 0  // experiment switch: boundary row r stored at element r + this
-#endif
-constexpr uint32_t kRowsOff = SALN_ROWS_OFF;
-#ifndef SALN_ROWS_BCAST
-// boundary publication: 2 every lane stores (lane 63 the row, the others a
-// pad slot), 1 every lane stores lane 63's broadcast value, 0 lane 63 stores
-#define SALN_ROWS_BCAST 2
-#endif
-#ifndef SALN_ROWS_G
-#define SALN_ROWS_G 8  // experiment switch: rows per boundary group (4 or 8)
-#endif
-constexpr uint32_t kRowsGrp = SALN_ROWS_G;
-#ifndef SALN_ROWS_INDEP
-#define SALN_ROWS_INDEP 0  // experiment builds only: stripes ignore their left neighbour
-#endif
+constexpr uint32_t kRowsOff = 0;  // boundary row r at element r of the column
+constexpr uint32_t kRowsGrp = 8;  // rows per boundary group (round 2: 4 was slower)
 
 // inclusive prefix max over the wave's 64 lanes (lane order).  `fill`:
 // independent work placed inside the chain, where each dependent DPP step
@@ -2143,7 +1795,6 @@ __global__ __launch_bounds__(64) void nw_fill_rows_kernel(
         }
         hb_prev = bH;
         // (H~, I~) leaving the stripe's last column (lane 63's values)
-#if SALN_ROWS_BCAST == 2
         {   // every lane stores its own (H~, I~) with one instruction: lane 63
             // at row r of the column, the others at a pad slot past the db
             // (pub_voff, set per group); no readlane, no exec change, the
@@ -2156,22 +1807,6 @@ __global__ __launch_bounds__(64) void nw_fill_rows_kernel(
             asm volatile("global_store_dwordx2 %0, %1, %2 offset:%3 sc1"
                          : : "v"(vo), "v"(val), "s"(pb), "i"(8 * q) : "memory");
         }
-#elif SALN_ROWS_BCAST
-        {   // every lane stores the broadcast pair to the same address (one
-            // 8-byte write): no exec change, no branch splitting the group's
-            // straight-line code
-            const int32_t h63 = __builtin_amdgcn_readlane(Hp[K - 1], 63);
-            const int32_t i63 = max(__builtin_amdgcn_readlane(S_incl, 63), bI);
-            __hip_atomic_store((uint64_t *)(scr_out + r + kRowsOff),
-                               (uint64_t)(uint32_t)h63 | ((uint64_t)(uint32_t)i63 << 32),
-                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-#else
-        if (lane == 63)
-            __hip_atomic_store((uint64_t *)(scr_out + r + kRowsOff),
-                               (uint64_t)(uint32_t)Hp[K - 1] | ((uint64_t)(uint32_t)max(S_incl, bI) << 32),
-                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#endif
     };
     // store the code word of rows r0 .. r0+(4/K)-1 (n of them valid)
     auto put = [&](uint32_t r0, uint32_t n, auto m_c) __attribute__((always_inline)) {
@@ -2208,14 +1843,17 @@ __global__ __launch_bounds__(64) void nw_fill_rows_kernel(
     // registers the compiler has reused.  Rows not yet published are
     // re-polled with ordinary (compiler-waited) loads.
     auto rows = [&](auto F) __attribute__((always_inline)) {
-        constexpr bool kFirst = decltype(F)::value || SALN_ROWS_INDEP;
+        constexpr bool kFirst = decltype(F)::value;
         const std::integral_constant<bool, !kFirst> VB;  // boundary rows kept in cH_v
         constexpr uint32_t kG = kRowsGrp;  // rows per boundary group
         uint64_t nv = 0;  // lanes 0..kG-1: (H~, I~) of the next group's rows
-        // only the group's own rows (a branch-free variant where every lane
-        // loaded a clamped row - rows of later groups, not yet published,
-        // included - gave wrong boundary values in batches,
-        // test_packed_stripes_auto_selected; the cause was not isolated)
+        // only the group's own rows.  (A round-2 branch-free variant in which
+        // every lane loaded a clamped row gave wrong boundary values in
+        // batches.  Cause, from the ISA (tools/isa_check.py): the last
+        // group's prefetch - dead here, no lane passes the guard - became a
+        // live load of row ld, still in flight when the compiler reused its
+        // destination VGPRs for the last group's rows; it landed over them.
+        // The last group now issues no prefetch.)
         auto fetch = [&](uint32_t r0) __attribute__((always_inline)) {
             if (!kFirst && lane < (int)kG && r0 + (uint32_t)lane <= ld)
                 asm volatile("global_load_dwordx2 %0, %1, off sc1"
@@ -2224,7 +1862,12 @@ __global__ __launch_bounds__(64) void nw_fill_rows_kernel(
         fetch(1);
         if constexpr (!kFirst) asm volatile("s_waitcnt vmcnt(0)" : "+v"(nv) : : "memory");
         int32_t bh[kG], bi[kG];  // the boundary of rows r .. r+kG-1
-        auto group = [&](uint32_t r) __attribute__((always_inline)) {
+        // kNext: prefetch the next group's rows.  The last group issues no
+        // prefetch at all: an asm load still in flight when its registers are
+        // reused corrupts whatever the compiler put there (the
+        // hand-off rules; tests/test_isa_handoff.py checks the ISA)
+        auto group = [&](uint32_t r, auto next_c) __attribute__((always_inline)) {
+            constexpr bool kNext = decltype(next_c)::value;
             pub_base = scr_out + r;
             pub_voff = lane == 63 ? 0u : (ld + 1u - r) * 8u;
             if constexpr (kFirst) {
@@ -2234,13 +1877,15 @@ __global__ __launch_bounds__(64) void nw_fill_rows_kernel(
                     bh[q] = hs4_col0(sc, r + q) + alpha * (int32_t)(r + q);
                 }
             } else {
-                // kG mask stores and kG boundary stores followed the prefetch
+                // kG mask stores and kG boundary stores followed the prefetch:
+                // with that many younger VMEM ops outstanding it has landed
+                // (GFX9 vmcnt retires in issue order)
                 if constexpr (kCodes == kCodesNone) {
-                    if constexpr (kG == 8) asm volatile("s_waitcnt vmcnt(7)" : "+v"(nv) : : "memory");
-                    else asm volatile("s_waitcnt vmcnt(3)" : "+v"(nv) : : "memory");
+                    if constexpr (kG == 8) asm volatile("s_waitcnt vmcnt(8)" : "+v"(nv) : : "memory");
+                    else asm volatile("s_waitcnt vmcnt(4)" : "+v"(nv) : : "memory");
                 } else {
-                    if constexpr (kG == 8) asm volatile("s_waitcnt vmcnt(15)" : "+v"(nv) : : "memory");
-                    else asm volatile("s_waitcnt vmcnt(7)" : "+v"(nv) : : "memory");
+                    if constexpr (kG == 8) asm volatile("s_waitcnt vmcnt(16)" : "+v"(nv) : : "memory");
+                    else asm volatile("s_waitcnt vmcnt(8)" : "+v"(nv) : : "memory");
                 }
                 int32_t cH = (int32_t)(uint32_t)nv, cI = (int32_t)(uint32_t)(nv >> 32);
                 const bool mine = lane < (int)kG && r + (uint32_t)lane <= ld;
@@ -2256,10 +1901,10 @@ __global__ __launch_bounds__(64) void nw_fill_rows_kernel(
                             cI = (int32_t)(uint32_t)(v >> 32);
                             ok = (uint32_t)cH != kColEmpty;
                         }
-                        if (++spins > kSpinCap) failed = true;
+                        if (++spins > err[1]) failed = true;
                     } while (__builtin_amdgcn_ballot_w64(!ok) && !failed);
                 }
-                fetch(r + kG);
+                if constexpr (kNext) fetch(r + kG);
                 cH_prev_v = cH_v;
                 cH_v = cH;
 #pragma unroll
@@ -2337,7 +1982,7 @@ __global__ __launch_bounds__(64) void nw_fill_rows_kernel(
         static_assert(kG == 4 || kG == 8, "four or eight rows per boundary group");
         uint32_t r = 1;
         for (; r + kG - 1 < ld; r += kG) {  // full groups before the one holding row ld
-            group(r);
+            group(r, std::true_type{});
             if constexpr (kG == 8 && K <= 2) {
                 // the first quad's last code word goes into row r+4's prefix chain
                 quad(r, o0, M0, nofill, std::false_type{});
@@ -2353,7 +1998,7 @@ __global__ __launch_bounds__(64) void nw_fill_rows_kernel(
             }
         }
         // the last group: 1 .. kG rows, row ld among them
-        group(r);
+        group(r, std::false_type{});
         const uint32_t nq = (ld - r + 1) / 4;  // full quads
         const bool t = (ld - r + 1) % 4 != 0;
         if (nq == 0) {
@@ -2671,7 +2316,7 @@ __global__ __launch_bounds__(64) void nw_fill_stripe_pk_kernel(
                         }
                         if (__builtin_amdgcn_ballot_w64(!ok) == 0 || failed) break;
                         __builtin_amdgcn_s_sleep(2);
-                        if (++spins > kSpinCap) failed = true;
+                        if (++spins > err[1]) failed = true;
                     }
                 }
                 const uint32_t sl = (rr - 1) % kPub;
@@ -2876,15 +2521,10 @@ hipError_t launch_score_results(const NwPairDesc *pairs, uint32_t first, uint32_
 constexpr Geom kVariants[kNumVariants] = {{16, 10}, {16, 16}, {64, 8}, {64, 4},
                                           {8, 19},  {16, 16}, {32, 16}, {16, 10}, {64, 16}};
 constexpr bool kPacked[kNumVariants] = {false, false, false, false, true, true, true, true, true};
-// Lanes per pair of each variant's fill kernel.  SALN_V7_NARROW fills
-// variant 7 (<= 160 columns, layout 16 lanes x 10 columns) with 8-lane groups
-// of 20 columns: half the pipeline skew and the per-step overhead over twice
-// the columns, the mask layout (and the walker) unchanged.  Measured equal
-// (1.07 ms per 10^5 150x150 pairs): the 202 VGPRs halve the occupancy.
-#ifndef SALN_V7_NARROW
-#define SALN_V7_NARROW 0
-#endif
-constexpr uint32_t kFillG[kNumVariants] = {16, 16, 64, 64, 8, 16, 32, SALN_V7_NARROW ? 8u : 16u, 64};
+// Lanes per pair of each variant's fill kernel.  (8-lane groups of 20
+// columns writing variant 7's layout measured equal in round 1: 202 VGPRs
+// halve the occupancy.)
+constexpr uint32_t kFillG[kNumVariants] = {16, 16, 64, 64, 8, 16, 32, 16, 64};
 
 // Dynamic LDS cap of the packed fill's staged db rows: two workgroups per CU.
 constexpr size_t kPackedLdsMax = 80 * 1024;
@@ -2948,14 +2588,48 @@ static hipError_t fill_pk(dim3 grid, hipStream_t s, const NwPairDesc *pairs, uin
     return rebase ? by_codes(std::true_type{}) : by_codes(std::false_type{});
 }
 
+// Blocks of a score-only all-vs-all launch of `count` pairs with G-lane
+// groups: two pairs per group, 256 / G groups per block, rounded up to whole
+// XCD super-blocks of 8 * blocks_per_pack blocks (pack_block).
+static uint64_t avsa_blocks(uint32_t G, uint64_t count) {
+    const uint64_t gpb = 256 / G, sup = 8 * blocks_per_pack(2 * (uint32_t)gpb);
+    const uint64_t groups = (count + 1) / 2;
+    return ((groups + gpb - 1) / gpb + sup - 1) / sup * sup;
+}
+
+static uint32_t avsa_lanes(int variant) {
+    switch (variant) {
+        case 4: return 8;
+        case 5: case 7: return 16;
+        case 6: return 32;
+        case 8: return 64;
+        default: return 0;
+    }
+}
+
+// The most pairs one launch of a packed class may take: the dispatch packet's
+// grid size is a 32-bit count of work-items (blocks * 256 <= 2^32 - 1), so
+// the largest whole number of super-blocks below that, two pairs per group.
+uint64_t avsa_chunk_pairs(int variant) {
+    const uint32_t G = avsa_lanes(variant);
+    if (!G) return 0;
+    const uint64_t gpb = 256 / G, sup = 8 * blocks_per_pack(2 * (uint32_t)gpb);
+    const uint64_t blocks = (0xFFFFFFFFull / 256) / sup * sup;
+    return std::min<uint64_t>(blocks * gpb * 2, 0x80000000ull);  // count is a uint32
+}
+
+uint64_t avsa_launch_blocks(int variant, uint64_t count) {
+    const uint32_t G = avsa_lanes(variant);
+    return G ? avsa_blocks(G, count) : 0;
+}
+
 template <int G, int K>
 static hipError_t avsa_pk(const AvsaSrc &src, uint32_t count, const uint8_t *qs, const uint8_t *ds,
                           Scoring sc, uint32_t ld_max, hipStream_t s) {
     constexpr uint32_t gpb = 256 / G;
-    const uint32_t sup = 8 * blocks_per_pack(2 * gpb);
-    const uint32_t groups = (count + 1) / 2;
-    const dim3 grid(((groups + gpb - 1) / gpb + sup - 1) / sup * sup);
-    if ((uint64_t)grid.x * 256 > 0xFFFFFFFFull) return hipErrorInvalidConfiguration;  // 32-bit grid
+    const uint64_t blocks = avsa_blocks(G, count);
+    if (blocks * 256 > 0xFFFFFFFFull) return hipErrorInvalidConfiguration;  // 32-bit grid
+    const dim3 grid((uint32_t)blocks);
     const bool rebase = !packed_ok(G * K, ld_max, sc);
     const size_t lds = (size_t)gpb * (ld_max + 2 * G) * (rebase ? 2 : 4);
     if (lds > kPackedLdsMax) return hipErrorInvalidValue;
@@ -2987,13 +2661,7 @@ hipError_t launch_avsa(int variant, const uint64_t *q_off, const uint64_t *d_off
         case 4: e = avsa_pk<8, 19>(src, count, qs, ds, sc, ld_max, stream); break;
         case 5: e = avsa_pk<16, 16>(src, count, qs, ds, sc, ld_max, stream); break;
         case 6: e = avsa_pk<32, 16>(src, count, qs, ds, sc, ld_max, stream); break;
-#if SALN_V7_NARROW || SALN_AVSA_NARROW == 1
-        case 7: e = avsa_pk<8, 20>(src, count, qs, ds, sc, ld_max, stream); break;
-#elif SALN_AVSA_NARROW == 2  // experiment: queries <= 152 columns only
-        case 7: e = avsa_pk<8, 19>(src, count, qs, ds, sc, ld_max, stream); break;
-#else
         case 7: e = avsa_pk<16, 10>(src, count, qs, ds, sc, ld_max, stream); break;
-#endif
         case 8: e = avsa_pk<64, 16>(src, count, qs, ds, sc, ld_max, stream); break;
         default: return hipErrorInvalidValue;
     }
@@ -3065,11 +2733,7 @@ hipError_t launch_fill(int variant, const NwPairDesc *pairs, uint32_t first, uin
         case 3: return hipErrorInvalidValue;  // stripes: launch_fill_stripes
         case 4: e = fill_pk<8, 19>(grid, stream, pairs, first, count, qs, ds, mask, end_h, res, cig, sc, codes, ld_max, rebase); break;
         case 5: e = fill_pk<16, 16>(grid, stream, pairs, first, count, qs, ds, mask, end_h, res, cig, sc, codes, ld_max, rebase); break;
-#if SALN_V7_NARROW
-        case 7: e = fill_pk<8, 20, 10>(grid, stream, pairs, first, count, qs, ds, mask, end_h, res, cig, sc, codes, ld_max, rebase); break;
-#else
         case 7: e = fill_pk<16, 10>(grid, stream, pairs, first, count, qs, ds, mask, end_h, res, cig, sc, codes, ld_max, rebase); break;
-#endif
         case 8: e = fill_pk<64, 16>(grid, stream, pairs, first, count, qs, ds, mask, end_h, res, cig, sc, codes, ld_max, rebase); break;
         default: e = fill_pk<32, 16>(grid, stream, pairs, first, count, qs, ds, mask, end_h, res, cig, sc, codes, ld_max, rebase); break;
     }
@@ -3122,7 +2786,7 @@ hipError_t launch_traceback(int variant, const NwPairDesc *pairs, uint32_t first
             };
             const hipError_t e = stripe_layout == 1   ? go(std::integral_constant<int, 1>{})
                                  : stripe_layout == 2 ? go(std::integral_constant<int, 2>{})
-                                                      : go(std::integral_constant<int, 0>{});
+                                                      : hipErrorInvalidValue;
             if (e != hipSuccess) return e;
             break;
         }
@@ -3170,7 +2834,7 @@ hipError_t launch_traceback_spec(const NwPairDesc *pairs, SpecArgs sa, uint32_t 
     };
     const hipError_t e = stripe_layout == 1   ? go(std::integral_constant<int, 1>{})
                          : stripe_layout == 2 ? go(std::integral_constant<int, 2>{})
-                                              : go(std::integral_constant<int, 0>{});
+                                              : hipErrorInvalidValue;
     if (e != hipSuccess) return e;
     sa.pass = passes;
     nw_spec_link_kernel<<<dim3(n_spec_pairs), dim3(256), 0, stream>>>(pairs, sa, done, end_h,
@@ -3211,37 +2875,13 @@ hipError_t launch_fill_stripes(const NwPairDesc *pairs, const uint2 *work, uint3
         else by_codes(std::false_type{});
         return hipGetLastError();
     }
-    const int32_t pen_max = 4 * (sc.match - sc.mismatch);  // the i32 fills' V'' scale
-    // a coder wave per stripe while the pipeline is short (a few stripes in
-    // the launch: the C1 latency case)
-    static const int split_env = [] {  // experiment switch: SALN_STRIPE_SPLIT=0 / 1
-        const char *e = std::getenv("SALN_STRIPE_SPLIT");
-        return e ? (e[0] == '1' ? 1 : 0) : -1;
-    }();
-    const bool split = split_env >= 0 ? split_env == 1 : n_work <= 16;
-    auto go = [&](auto codes_c, auto minpen_c) {
-        constexpr int kC = decltype(codes_c)::value;
-        if (pk)
-            nw_fill_stripe_pk_kernel<kC>
-                <<<grid, block, 0, stream>>>(pairs, work, qs, ds, mask, scratch, prog, err, end_h, sc);
-        else if constexpr (kC != kCodesNone) {
-            if (split)
-                nw_fill_stripe_kernel<4, kC, decltype(minpen_c)::value, true>
-                    <<<grid, dim3(128), 0, stream>>>(pairs, work, qs, ds, mask, scratch, prog, err, end_h, sc);
-            else
-                nw_fill_stripe_kernel<4, kC, decltype(minpen_c)::value>
-                    <<<grid, block, 0, stream>>>(pairs, work, qs, ds, mask, scratch, prog, err, end_h, sc);
-        } else
-            nw_fill_stripe_kernel<4, kC, decltype(minpen_c)::value>
-                <<<grid, block, 0, stream>>>(pairs, work, qs, ds, mask, scratch, prog, err, end_h, sc);
-    };
-    auto by_codes = [&](auto minpen_c) {
-        if (codes == kCodesFull) go(std::integral_constant<int, kCodesFull>{}, minpen_c);
-        else if (codes == kCodesNone) go(std::integral_constant<int, kCodesNone>{}, minpen_c);
-        else go(std::integral_constant<int, kCodesWalk>{}, minpen_c);
-    };
-    if (pen_max >= 0 && pen_max <= 256) by_codes(std::true_type{});
-    else by_codes(std::false_type{});
+    if (!pk) return hipErrorInvalidValue;  // (round 1's skewed i32 stripes are retired)
+    if (codes == kCodesFull)
+        nw_fill_stripe_pk_kernel<kCodesFull><<<grid, block, 0, stream>>>(pairs, work, qs, ds, mask, scratch, prog, err, end_h, sc);
+    else if (codes == kCodesNone)
+        nw_fill_stripe_pk_kernel<kCodesNone><<<grid, block, 0, stream>>>(pairs, work, qs, ds, mask, scratch, prog, err, end_h, sc);
+    else
+        nw_fill_stripe_pk_kernel<kCodesWalk><<<grid, block, 0, stream>>>(pairs, work, qs, ds, mask, scratch, prog, err, end_h, sc);
     return hipGetLastError();
 }
 
@@ -3281,12 +2921,12 @@ Geom variant_geom(int v) { return kVariants[v]; }
 // Row-fill columns per lane: K = 1 (64-column stripes) while every stripe
 // wave of the plan has a SIMD to itself (a shorter row step: C1 0.197 ->
 // 0.188 ms, 5 kbp 0.75 -> 0.70 ms), else K = 2 (C4: 1,564 K = 1 waves share
-// SIMDs, 19.5 vs 14.5 ms).  SALN_ROWS_K = 0 (skewed stripe fill), 1, 2 or 4
+// SIMDs, 19.5 vs 14.5 ms).  SALN_ROWS_K = 1, 2 or 4
 // forces it.
 int stripe_rows_k(uint64_t waves_k1) {
     if (const char *e = std::getenv("SALN_ROWS_K")) {  // read per plan
         const int v = std::atoi(e);
-        return v == 0 || v == 1 || v == 4 ? v : 2;
+        return v == 1 || v == 4 ? v : 2;
     }
     return waves_k1 <= 1024 ? 1 : 2;
 }

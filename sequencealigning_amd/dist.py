@@ -127,6 +127,17 @@ def _avsa_engine(device: int, scoring=None):
             if out.numel():
                 self.av.execute(self.q, self.d, out)
 
+        def status(self) -> int:
+            """Device error flags of the executes since the last call (blocks)."""
+            import ctypes as C
+
+            from . import _lib
+            f = C.c_uint32()
+            rc = _lib.lib().saln_nw_avsa_status(self.av._h, C.byref(f))
+            if rc not in (_lib.OK, _lib.E_DEVICE_WAIT):
+                _lib.check(rc, "saln_nw_avsa_status")
+            return f.value
+
         def close(self):
             self.av.close()
 
@@ -146,8 +157,14 @@ class ShardedAllVsAll:
 
     ``engine`` (tests) replaces the per-rank compute: a class built as
     engine(q_seq, q_off, d_seq, d_off) with ``cells``, ``__call__(out)`` that
-    fills out (int32[n_block_db * n_q * 2], on the engine's device) and
-    ``close()``."""
+    fills out (int32[n_block_db * n_q * 2], on the engine's device),
+    ``close()`` and optionally ``status()`` (device error flags since the
+    last call, include/saln.h saln_nw_avsa_status).
+
+    ``execute`` checks the device status of every rank's block before the
+    gather (a MAX all-reduce of one flag word): a rank whose column-stripe
+    fill timed out makes every rank raise instead of gathering wrong
+    records, or hanging in the gather."""
 
     def __init__(self, q_seq, q_off, db_seq, db_off, *, scoring=None, device: int | None = None,
                  engine=None, dst: int = 0):
@@ -196,10 +213,30 @@ class ShardedAllVsAll:
         """Cells of all ranks (sum over pairs of len_q * len_db)."""
         return self.cells_total
 
-    def execute(self, gather: bool = True) -> None:
+    def execute(self, gather: bool = True, check: bool = True) -> None:
         self.engine(self.local[:self.counts[self.rank]])
+        if check:
+            self.check()
         if gather:
             self.gather()
+
+    def check(self) -> None:
+        """Raise on every rank if any rank's engine reported a device error
+        (SALN_E_DEVICE_WAIT) since the last check."""
+        import torch
+        import torch.distributed as dist
+
+        from . import _lib
+        status = getattr(self.engine, "status", None)
+        flags = int(status()) if status is not None else 0
+        if self.pg:
+            t = torch.tensor([flags], dtype=torch.int64, device=self.comm_dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            flags = int(t.item())
+        if flags:
+            raise _lib.SalnError(_lib.E_DEVICE_WAIT,
+                                 f"ShardedAllVsAll execute: device flags {flags:#x} on some rank "
+                                 "(a column-stripe dependency wait timed out)")
 
     def gather(self) -> None:
         import torch.distributed as dist

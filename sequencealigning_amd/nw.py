@@ -219,6 +219,26 @@ class NwPlan:
         _lib.check(self._L.saln_nw_execute(self._h, ptr(q_seq), ptr(db_seq), ptr(results),
                                            ptr(cigar), stream), "saln_nw_execute")
 
+    def status(self) -> int:
+        """Wait for every execute since the last call; return and clear the
+        device error flags they raised (include/saln.h saln_nw_plan_status)."""
+        f = C.c_uint32()
+        rc = self._L.saln_nw_plan_status(self._h, C.byref(f))
+        if rc not in (_lib.OK, _lib.E_DEVICE_WAIT):
+            _lib.check(rc, "saln_nw_plan_status")
+        return f.value
+
+    def check(self) -> None:
+        """Raise SalnError(E_DEVICE_WAIT) if any execute since the last
+        check/status hit a device-side dependency timeout: its results are
+        invalid.  Blocks until those executes finish."""
+        _lib.check(self._L.saln_nw_plan_status(self._h, None), "NwPlan execute (device status)")
+
+    def set_wait_limit(self, polls: int) -> None:
+        """Polls a column-stripe dependency wait may spend (test hook: 0
+        injects a timeout on any wait that finds its row unpublished)."""
+        _lib.check(self._L.saln_nw_plan_set_wait_limit(self._h, polls), "set_wait_limit")
+
     def set_async(self, enable: bool) -> None:
         """2-deep pipeline: traceback of execute n overlaps the fill of n+1."""
         _lib.check(self._L.saln_nw_plan_set_async(self._h, int(enable)), "set_async")
@@ -282,6 +302,12 @@ class NwAllVsAll:
         _lib.check(self._L.saln_nw_avsa_execute(self._h, ptr(q_seq), ptr(db_seq), ptr(out),
                                                 stream), "saln_nw_avsa_execute")
 
+    def check(self) -> None:
+        """Raise SalnError(E_DEVICE_WAIT) if an execute since the last check
+        hit a device-side dependency timeout (the internal plan's column
+        stripes; saln_nw_avsa_status).  Blocks until those executes finish."""
+        _lib.check(self._L.saln_nw_avsa_status(self._h, None), "NwAllVsAll execute (device status)")
+
     def close(self) -> None:
         if self._h:
             self._L.saln_nw_avsa_destroy(self._h)
@@ -306,6 +332,7 @@ def nw_score_all_vs_all(queries, dbs, *, scoring=None, device: int = 0):
     td = torch.from_numpy(d_seq.copy()).to(dev)
     out = torch.empty(max(1, a.n_q * a.n_db * 2), dtype=torch.int32, device=dev)
     a.execute(tq, td, out)
+    a.check()
     torch.cuda.synchronize(dev)
     h = out.cpu().numpy()[:a.n_q * a.n_db * 2].reshape(a.n_db, a.n_q, 2)
     a.close()

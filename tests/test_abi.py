@@ -59,3 +59,25 @@ def test_cli_help():
     r = subprocess.run([cli, "--help"], capture_output=True, text=True)
     assert r.returncode == 0
     assert "--query-file" in r.stdout and "--algo" in r.stdout
+
+
+def test_avsa_launch_geometry_fits_32bit_grid(saln):
+    """Every packed all-vs-all class launches at most a 32-bit work-item
+    count per chunk (nw_avsa.cpp: the chunk derives from the class's pairs
+    per block); pure host logic, no device needed."""
+    from sequencealigning_amd import _lib
+    L = _lib.lib()
+    for v in (4, 5, 6, 7, 8):
+        chunk, blocks = ctypes.c_uint64(), ctypes.c_uint64()
+        assert L.saln_nw_avsa_launch_geometry(v, ctypes.byref(chunk), ctypes.byref(blocks)) == 0
+        assert blocks.value * 256 <= 0xFFFFFFFF, v
+        assert chunk.value >= 1 << 24 and chunk.value <= 1 << 31, v
+    for v in (-1, 0, 3, 9):
+        assert L.saln_nw_avsa_launch_geometry(v, None, None) == _lib.E_INVALID
+
+
+def test_status_codes_match_header():
+    src = open(os.path.join(ROOT, "include", "saln.h")).read()
+    from sequencealigning_amd import _lib
+    assert re.search(r"SALN_E_DEVICE_WAIT = (-\d+)", src).group(1) == str(_lib.E_DEVICE_WAIT)
+    assert re.search(r"SALN_FLAG_WAIT_TIMEOUT (\d+)u", src).group(1) == str(_lib.FLAG_WAIT_TIMEOUT)
