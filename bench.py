@@ -11,25 +11,35 @@ ranks also the RCCL gather of the 16-byte per-pair result records to rank 0
 wall time.
 
 The other BASELINE.json configs ride along as extra keys under "configs"
-(SURVEY.md §8(d)), each timed here so the driver's clock covers them:
+(SURVEY.md §8(d)), each timed here so the driver's clock covers them, each
+with its own `roofline` (the dominant kernel against the HBM or VALU peak)
+and `cpu_baseline`:
   c5  configs[4]: 10k x 100k 150 bp score-only all-vs-all, db sharded over
       the N ranks, {score, status} records gathered to rank 0 (every N);
   c1  configs[0]: one 1 kbp pair, GPU latency + the oracle's reference-
       structure CPU path on one core (N = 1);
   c3  configs[2]: WFA (reference semantics) on 10^6 distinct 10 kbp G-mut
       pairs (N = 1);
+  c3_affine  the same 10^6 pairs through the corrected gap-affine WFA
+      (SURVEY.md §8(f) row 4; not reference parity) (N = 1);
   c4  configs[3]: one 100 kbp pair, fill + traceback, + the linear-memory
       oracle on the host cores (N = 1);
   host_path: configs[1] through the host-buffer C ABI (PCIe-inclusive; never
       the value) (N = 1).
 
-    python bench.py --gpus N --steps K --warmup W [--legs c5,c1,c3,c4,host|none]
+    python bench.py --gpus N --steps K --warmup W [--legs c5,c1,c3,c3_affine,c4,host|none]
+
+With --gpus N > 1 and no WORLD_SIZE in the environment this process starts
+the N ranks itself (torch.distributed.run on 127.0.0.1, as a child process;
+nothing here touches the GPU first) and exits with their status.  Under an
+external launcher WORLD_SIZE must equal --gpus.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import subprocess
 import sys
 import time
 
@@ -48,7 +58,8 @@ VALU_PEAK_TOPS = 1024 * 32 * 2.4e9 / 1e12  # 78.6 T lane-ops/s
 VALU_PK_TOPS = 1024 * 16 * 2.4e9 / 1e12
 N_PAIRS, LQ, LD = 100_000, 150, 150
 SEED = 0x5EED0002
-ALL_LEGS = ("c5", "c1", "c3", "c4", "host")
+ALL_LEGS = ("c5", "c1", "c3", "c3_affine", "c4", "host")
+PMC_FILES = ("pmc_traffic.json", "pmc_legs.json")  # under profiles/
 
 
 def log(*a):
@@ -100,38 +111,72 @@ def cpu_baseline(budget_s: float = 12.0) -> dict:
                       f"fill + literal DFS (<=1e5 pops/pair)"}
 
 
-def pmc_traffic(kernel: str, field: str = "hbm_bytes"):
-    """A per-launch PMC figure of `kernel` (HBM bytes, or VALU wave-instructions
-    with field="valu_wave_insts") from the committed PMC summary
-    (profiles/pmc_traffic.json, written by tools/pmc_traffic.py from the
-    rocprofv3 --pmc passes of tools/pmc.sh on this workload), or None."""
-    try:
-        with open(os.path.join(ROOT, "profiles", "pmc_traffic.json")) as fh:
-            doc = json.load(fh)
-    except (OSError, ValueError):
-        return None
-    for name, v in doc.get("kernels", {}).items():
-        if kernel in name:
-            return v.get(field)
+# ------------------------------------------------------------- rooflines
+def _pmc_docs():
+    for f in PMC_FILES:
+        try:
+            with open(os.path.join(ROOT, "profiles", f)) as fh:
+                yield f, json.load(fh)
+        except (OSError, ValueError):
+            continue
+
+
+def pmc(kernel: str, field: str = "hbm_bytes"):
+    """A per-launch PMC figure of `kernel` (HBM bytes, VALU wave-instructions
+    with field="valu_wave_insts", their sum over the profiled run with
+    "valu_wave_insts_sum") from the committed PMC summaries (profiles/
+    pmc_traffic.json: the headline command; profiles/pmc_legs.json: the
+    legs, tools/prof_legs.py), written by tools/pmc_traffic.py from separate
+    rocprofv3 --pmc passes (tools/pmc.sh), or None."""
+    for _, doc in _pmc_docs():
+        for name, v in doc.get("kernels", {}).items():
+            if kernel in name and field in v:
+                return v[field]
     return None
 
 
-def valu_roof(kernel: str, avg_s: float):
-    """SURVEY.md 8(d) asks for the VALU fraction beside the HBM one: the fill's
-    VALU wave-instructions per launch (PMC SQ_INSTS_VALU, committed PMC
-    summary) x 64 lanes over its measured duration, against the guide's
-    2-cycle wave64 issue peak (78.6 T lane-ops/s); frac_4cycle is the same
-    against the 4-cycle rate measured for packed / VOP3 / DPP ops."""
-    n = pmc_traffic(kernel, "valu_wave_insts")
+def pmc_executes(leg: str):
+    """Executes of `leg`'s workload in the profiled run (profiles/pmc_legs.json)."""
+    for _, doc in _pmc_docs():
+        if leg in doc.get("executes", {}):
+            return doc["executes"][leg]
+    return None
+
+
+def roof_hbm(nbytes: float, secs: float, kernel: str, traffic=None, **extra) -> dict:
+    """HBM roofline of one kernel launch: algorithmic bytes / its duration."""
+    a = nbytes / secs / 1e9
+    d = {"bound": "hbm", "achieved": round(a, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+         "frac": round(a / HBM_PEAK_GBS, 5), "traffic": traffic, "kernel": kernel,
+         "kernel_avg_ms": round(secs * 1e3, 4), "algorithmic_bytes": int(nbytes)}
+    d.update(extra)
+    return d
+
+
+def valu_roof(kernel: str, secs: float, wave_insts=None, **extra):
+    """VALU roofline: wave-instructions (PMC SQ_INSTS_VALU from the committed
+    summaries) x 64 lanes over the measured duration, against the guide's
+    2-cycle wave64 issue peak (78.6 T lane-ops/s); frac_4cycle against the
+    4-cycle rate of packed / VOP3 / DPP ops."""
+    n = wave_insts if wave_insts is not None else pmc(kernel, "valu_wave_insts")
     if not n:
         return None
-    achieved = n * 64 / avg_s / 1e12
-    return {"wave_insts_per_launch": n, "achieved": round(achieved, 2),
-            "peak": round(VALU_PEAK_TOPS, 2), "unit": "T int lane-ops/s",
-            "frac": round(achieved / VALU_PEAK_TOPS, 4),
-            "frac_4cycle": round(achieved / VALU_PK_TOPS, 4),
-            "source": "SQ_INSTS_VALU from profiles/pmc_traffic.json (a rocprofv3 --pmc run of "
-                      "this command), duration measured in this run"}
+    a = n * 64 / secs / 1e12
+    d = {"bound": "valu", "achieved": round(a, 3), "peak": round(VALU_PEAK_TOPS, 2),
+         "unit": "T int lane-ops/s", "frac": round(a / VALU_PEAK_TOPS, 5),
+         "frac_4cycle": round(a / VALU_PK_TOPS, 5), "kernel": kernel,
+         "wave_insts": int(n), "seconds": round(secs, 6),
+         "source": "SQ_INSTS_VALU from profiles/pmc_*.json (rocprofv3 --pmc of this workload), "
+                   "duration measured in this run"}
+    d.update(extra)
+    return d
+
+
+def valu_per_execute(kernel: str, leg: str):
+    """VALU wave-instructions of one execute of `leg` (all launches of
+    `kernel`): the profiled run's sum over its executes."""
+    s, ex = pmc(kernel, "valu_wave_insts_sum"), pmc_executes(leg)
+    return s / ex if s and ex else None
 
 
 def verify_c2(res_np, cig_np, cigar_off, qs, qo, ds, do, n_check: int = 1000) -> dict:
@@ -175,20 +220,31 @@ def timed(fn, world, dist, torch, local):
     return float(t.item())
 
 
+def event_time(torch, fn, reps: int) -> float:
+    """Seconds per call of fn over `reps` calls, from hipEvents on torch's
+    current stream (the stream the plans launch on when given none)."""
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(reps):
+        fn()
+    b.record()
+    b.synchronize()
+    return a.elapsed_time(b) / 1e3 / reps
+
+
 # ------------------------------------------------------------------- legs
-def leg_c5(world, rank, local, dist, torch, nq=10_000, ndb=100_000, L=150):
+def leg_c5(world, rank, local, dist, torch, nq=10_000, ndb=100_000, L=150, cpu=True):
     """configs[4]: 10k queries x 100k db records of 150 bp (length assumed =
     C2), G-iid (seed 0x5EED0004), score-only all-vs-all with
     the db sharded over the ranks and the records gathered to rank 0
     (dist.ShardedAllVsAll).  Total work is fixed as N grows (strong)."""
     from sequencealigning_amd import synth
-    from sequencealigning_amd.dist import ShardedAllVsAll
+    from sequencealigning_amd.dist import ShardedAllVsAll, shard_db
     seed = 0x5EED0004
     qs = synth.random_bases(seed, nq * L)
     qo = np.arange(nq + 1, dtype=np.uint64) * np.uint64(L)
     do = np.arange(ndb + 1, dtype=np.uint64) * np.uint64(L)
     # every rank draws only its own db block (same stream positions as the full db)
-    from sequencealigning_amd.dist import shard_db
     lo, hi = shard_db(np.full(ndb, L), world, rank)
     ds = np.zeros(ndb * L, np.uint8)
     ds[lo * L:hi * L] = synth.random_bases(seed ^ 0xD5D5D5D5, (hi - lo) * L, start=lo * L)
@@ -197,33 +253,76 @@ def leg_c5(world, rank, local, dist, torch, nq=10_000, ndb=100_000, L=150):
     setup = time.perf_counter() - t0
     av.execute()  # warm: code objects, RCCL communicator
     dt = timed(av.execute, world, dist, torch, local)
+    # the fill of this rank's block alone (one launch per query class; events
+    # on torch's stream, the stream the engine launches on)
+    fill_s = event_time(torch, lambda: av.execute(gather=False, check=False), 1)
+    av.check()
     out = None
     if rank == 0:
-        # checker: a seeded sample of the gathered records against the oracle
-        from oracle import refcpu  # checker only
-        rng = np.random.default_rng(4)
-        di = rng.integers(0, ndb, 256)
-        qi = rng.integers(0, nq, 256)
-        allq = qs.tobytes()
-        dsel = [synth.random_bases(seed ^ 0xD5D5D5D5, L, start=int(d) * L).tobytes() for d in di]
-        qsel = [allq[int(q) * L:(int(q) + 1) * L] for q in qi]
-        qo2 = np.arange(257, dtype=np.uint64) * np.uint64(L)
-        want = refcpu.check_pairs(b"".join(qsel), qo2, b"".join(dsel), qo2, threads=cpu_threads())
-        sc, st = av.lookup(di, qi)
-        bad = int(np.sum((sc != want.score) | ((st == 2) != want.panics)))
+        kern = "nw_fill_pk_kernel<8, 19, 2, saln::AvsaSrc, 19"
+        ins = valu_per_execute(kern, "c5")
+        if ins is not None and world > 1:
+            ins *= (hi - lo) / ndb  # this rank's share of the profiled (N = 1) launch
         out = {"workload": f"configs[4]: {nq} x {ndb} score-only all-vs-all, {L} bp G-iid "
                            f"(seed {seed:#x}), db sharded over {world} rank(s), records "
                            f"gathered to rank 0" + (" over RCCL" if world > 1 else ""),
                "value": round(av.cells / dt / 1e9, 1), "unit": "GCUPS", "seconds": round(dt, 4),
                "pairs_per_s": round(nq * ndb / dt, 1), "cells": av.cells, "n_gpus": world,
                "scaling": "strong", "setup_s": round(setup, 2),
-               "panic_frac": round(av.status_count(2) / (nq * ndb), 4),
-               "verified": {"pairs": 256, "mismatches": bad,
-                            "checker": "oracle/refcheck.c on a seeded sample (untimed)"}}
+               "panic_frac": round(av.status_count(2) / (nq * ndb), 4), "executes": 3,
+               "roofline": valu_roof(kern, fill_s, ins, note="score-only: no mask, HBM traffic "
+                                     "~0 B/cell; the packed fill's VALU issue is the bound",
+                                     gcups_fill=round(av.cells_local / fill_s / 1e9, 1))}
+        if cpu:
+            # checker: a seeded sample of the gathered records against the oracle
+            from oracle import refcpu  # checker only
+            rng = np.random.default_rng(4)
+            di = rng.integers(0, ndb, 256)
+            qi = rng.integers(0, nq, 256)
+            allq = qs.tobytes()
+            dsel = [synth.random_bases(seed ^ 0xD5D5D5D5, L, start=int(d) * L).tobytes() for d in di]
+            qsel = [allq[int(q) * L:(int(q) + 1) * L] for q in qi]
+            qo2 = np.arange(257, dtype=np.uint64) * np.uint64(L)
+            want = refcpu.check_pairs(b"".join(qsel), qo2, b"".join(dsel), qo2,
+                                      threads=cpu_threads())
+            sc, st = av.lookup(di, qi)
+            bad = int(np.sum((sc != want.score) | ((st == 2) != want.panics)))
+            out["verified"] = {"pairs": 256, "mismatches": bad,
+                               "checker": "oracle/refcheck.c on a seeded sample (untimed)"}
+            out["cpu_baseline"] = c5_cpu_baseline(seed, nq, ndb, L)
     av.close()
     del av
     torch.cuda.empty_cache()
     return out
+
+
+def c5_cpu_baseline(seed, nq, ndb, L, budget_s: float = 8.0) -> dict:
+    """The oracle's literal three-matrix fill (oracle/refcpu.c, the reference
+    structure; score-only: its DFS stops after one pop) over a seeded slice of
+    the C5 pair space on the box's cores, as many pairs as ~budget_s allows."""
+    from oracle import refcpu  # cpu_baseline leg only
+    from sequencealigning_amd import synth
+    T = cpu_threads()
+    rng = np.random.default_rng(5)
+    allq = synth.random_bases(seed, nq * L)
+    n, cells, t_all = 0, 0, 0.0
+    chunk = T * 256
+    while t_all < budget_s and n < 200_000:
+        di = rng.integers(0, ndb, chunk)
+        qi = rng.integers(0, nq, chunk)
+        dsel = np.concatenate([synth.random_bases(seed ^ 0xD5D5D5D5, L, start=int(d) * L)
+                               for d in di]).tobytes()
+        qsel = np.concatenate([allq[int(q) * L:(int(q) + 1) * L] for q in qi]).tobytes()
+        off = np.arange(chunk + 1, dtype=np.uint64) * np.uint64(L)
+        t0 = time.perf_counter()
+        cells += refcpu.run_pairs_mt(qsel, off, dsel, off, chunk, max_pops=1, threads=T)
+        t_all += time.perf_counter() - t0
+        n += chunk
+    return {"value": round(cells / t_all / 1e9, 4), "unit": "GCUPS", "cores": T, "kind": "port",
+            "seconds": round(t_all, 2),
+            "sample": f"{n} pairs drawn from the {nq} x {ndb} pair space (seeded), "
+                      f"oracle/refcpu.c literal 3-matrix fill + parent lists (score-only: the DFS "
+                      f"stops after one pop) on {T} threads"}
 
 
 def _single_pair(torch, saln, q, d, reps, score_only=False):
@@ -247,120 +346,216 @@ def _single_pair(torch, saln, q, d, reps, score_only=False):
     f, _ = plan.kernel_time("nw_fill")
     tb, _ = plan.kernel_time("nw_traceback")
     r = res.cpu().numpy().view(saln._lib.RESULT_DTYPE)[0]
+    words = cig.cpu().numpy().view(np.uint32)[:int(r["cigar_len"])]
+    ops = saln.cigar_ops_string(saln.nw._decode_cigar(words)) if r["printed"] else None
     out = {"len_q": len(q), "len_db": len(d), "cells": plan.cells, "score": int(r["score"]),
            "status": int(r["status"]), "printed": int(r["printed"]), "flags": int(r["flags"]),
            "execute_ms": round(dt * 1e3, 4), "fill_ms": round(f / reps, 4),
            "traceback_ms": round(tb / reps, 4), "gcups": round(plan.cells / dt / 1e9, 2)}
     plan.close()
-    return out
+    return out, ops
 
 
-def leg_c1(torch, saln):
+def leg_c1(torch, saln, reps=50, cpu=True):
     """configs[0]: one 1 kbp x 1 kbp pair (G-mut 5 %, seed 0x5EED0000; and a
     G-iid pair), score + first-printed traceback on the GPU, next to the
     reference-structure CPU path on one core (the oracle's literal fill +
     DFS that prints every co-optimal alignment, needleman_wunsch_affine.rs
     :424-437)."""
-    from oracle import refcpu  # cpu_baseline leg only
     from sequencealigning_amd import synth
     q = synth.random_bases(0x5EED0000, 1000).tobytes()
     d = synth.mutate(q, 0.05, seed=1000)
     gi = synth.random_bases(0x5EED0000 ^ 0x77, 1000).tobytes()
+    g, ops = _single_pair(torch, saln, q, d, reps)
+    g_iid, ops_iid = _single_pair(torch, saln, q, gi, reps)
+    kern = "nw_fill_rows_kernel<1, 0, true>"
+    fill_s = g["fill_ms"] / 1e3
     out = {"workload": "configs[0]: one 1 kbp x 1 kbp pair, score + first-printed traceback "
                        "(G-mut 5 %; iid beside it)",
-           "gpu": _single_pair(torch, saln, q, d, 50),
-           "gpu_iid": _single_pair(torch, saln, q, gi, 50)}
+           "gpu": g, "gpu_iid": g_iid, "executes": 2 * (1 + reps),
+           "roofline": roof_hbm(g["cells"], fill_s, kern, pmc(kern),
+                                note="latency-bound: one pair's 998-row chain through 16 "
+                                     "64-column stripes (1,024 SIMDs, 16 waves)",
+                                valu=valu_roof(kern, fill_s, valu_per_execute(kern, "c1")))}
+    if not cpu:
+        return out
+    from oracle import refcpu  # cpu_baseline leg only
     qo = np.array([0, len(q)], np.uint64)
     do = np.array([0, len(d)], np.uint64)
-    reps, t0 = 0, time.perf_counter()
-    while reps < 3 or time.perf_counter() - t0 < 2.0:
+    n, t0 = 0, time.perf_counter()
+    while n < 3 or time.perf_counter() - t0 < 2.0:
         refcpu.run_pairs(q, qo, d, do, 1, max_pops=10_000_000)
-        reps += 1
-    cpu_s = (time.perf_counter() - t0) / reps
+        n += 1
+    cpu_s = (time.perf_counter() - t0) / n
     o = refcpu.nw(q, d, literal_dfs=False)
+    oi = refcpu.nw(q, gi, literal_dfs=False)
     out["cpu_baseline"] = {"ms": round(cpu_s * 1e3, 3), "cores": 1, "kind": "port",
                            "gcups": round(len(q) * len(d) / cpu_s / 1e9, 5),
-                           "sample": f"the same pair, {reps} runs of oracle/refcpu.c fill + "
+                           "sample": f"the same pair, {n} runs of oracle/refcpu.c fill + "
                                      "literal DFS (every co-optimal block)"}
-    out["matches_oracle"] = bool(out["gpu"]["score"] == o.score)
-    out["speedup_vs_cpu"] = round(cpu_s * 1e3 / out["gpu"]["execute_ms"], 1)
+    out["matches_oracle"] = bool(
+        g["score"] == o.score and (g["status"] == 2) == o.panics and ops == o.first_ops
+        and g_iid["score"] == oi.score and (g_iid["status"] == 2) == oi.panics
+        and ops_iid == oi.first_ops)
+    out["checked"] = "score, panic status and the first printed CIGAR of both pairs"
+    out["speedup_vs_cpu"] = round(cpu_s * 1e3 / g["execute_ms"], 1)
     return out
 
 
-def leg_c4(torch, saln):
+def leg_c4(torch, saln, reps=3, cpu=True):
     """configs[3]: one 100 kbp x 100 kbp pair (G-mut 5 %, seed 0x5EED0003),
     fill + parent mask + first-printed traceback on one GPU, and the
-    linear-memory oracle (reflinear.c, column stripes on the host cores) on
-    the same pair for score parity and the CPU time."""
-    from oracle import refcpu  # cpu_baseline leg only
+    linear-memory oracle (reflinear.c: column stripes on the host cores,
+    1 B of parent sets per cell, the reference DFS's first event) on the same
+    pair for score + CIGAR parity and the CPU time."""
     from sequencealigning_amd import synth
     q = synth.random_bases(0x5EED0003, 100_000).tobytes()
     d = synth.mutate(q, 0.05, seed=100_000)
-    g = _single_pair(torch, saln, q, d, 3)
+    g, ops = _single_pair(torch, saln, q, d, reps)
     torch.cuda.empty_cache()
+    kern = "nw_fill_rows_kernel<2, 0, true>"
+    fill_s = g["fill_ms"] / 1e3
+    out = {"workload": "configs[3]: one 100 kbp x 100 kbp pair, G-mut 5 %, fill + 1 B/cell mask "
+                       "+ first-printed traceback", "gpu": g, "executes": 1 + reps,
+           "value": g["gcups"], "unit": "GCUPS",
+           "roofline": roof_hbm(g["cells"], fill_s, kern, pmc(kern),
+                                note="bound by the 100,001-row chain of lone stripe waves "
+                                     "(DESIGN.md §3), not by HBM",
+                                valu=valu_roof(kern, fill_s, valu_per_execute(kern, "c4")))}
+    if not cpu:
+        return out
+    from oracle import refcpu  # cpu_baseline leg only
     T = cpu_threads()
     t0 = time.perf_counter()
-    sc, es, pan = refcpu.nw_score_linear(q, d, threads=T)
+    sc, es, pan, first, _ = refcpu.nw_first_linear(q, d, threads=T)
     cpu_s = time.perf_counter() - t0
-    return {"workload": "configs[3]: one 100 kbp x 100 kbp pair, G-mut 5 %, fill + 1 B/cell mask "
-                        "+ first-printed traceback", "gpu": g,
-            "value": g["gcups"], "unit": "GCUPS",
-            "matches_oracle": bool(g["score"] == sc and (g["status"] == 2) == pan),
-            "cpu_baseline": {"seconds": round(cpu_s, 2), "cores": T, "kind": "port",
-                             "gcups": round(len(q) * len(d) / cpu_s / 1e9, 3),
-                             "sample": "the whole pair, oracle/reflinear.c score-only in linear "
-                                       "memory (the reference-structure path needs ~TB)"}}
+    out["matches_oracle"] = bool(g["score"] == sc and (g["status"] == 2) == pan and ops == first)
+    out["checked"] = "score, panic status and the first printed CIGAR (~101k ops)"
+    out["cpu_baseline"] = {"seconds": round(cpu_s, 2), "cores": T, "kind": "port",
+                           "gcups": round(len(q) * len(d) / cpu_s / 1e9, 3),
+                           "sample": "the whole pair, oracle/reflinear.c: linear-memory fill "
+                                     "keeping 1 B of parent sets per cell + the reference DFS's "
+                                     "first alignment (the reference-structure path needs ~TB)"}
+    return out
 
 
-def leg_c3(torch, saln, n_pairs=1_000_000, L=10_000):
-    """configs[2]: WFA with the reference's semantics (wfa.rs) on 10^6
-    distinct 10 kbp G-mut(5 %) pairs generated on the device (synth.
-    mut_pairs_torch = tools/bench_wfa.py's pairs), step cap 10^4, sequences
-    and results in HBM."""
-    from oracle import refcpu  # cpu_baseline leg only
+_C3_PAIRS = {}
+
+
+def c3_pairs(torch, n_pairs, L):
+    """configs[2]'s 10^6 distinct 10 kbp G-mut(5 %) pairs, generated on the
+    device once (synth.mut_pairs_torch) and shared by c3 and c3_affine."""
     from sequencealigning_amd import synth
-    t0 = time.perf_counter()
-    qs, qo, ds, do = synth.mut_pairs_torch(n_pairs, L, 0.05, 0x5EED0003, "cuda")
-    torch.cuda.synchronize()
-    gen_s = time.perf_counter() - t0
+    key = (n_pairs, L)
+    if key not in _C3_PAIRS:
+        _C3_PAIRS.clear()
+        t0 = time.perf_counter()
+        p = synth.mut_pairs_torch(n_pairs, L, 0.05, 0x5EED0003, "cuda")
+        torch.cuda.synchronize()
+        _C3_PAIRS[key] = p + (time.perf_counter() - t0,)
+    return _C3_PAIRS[key]
+
+
+def leg_c3(torch, saln, n_pairs=1_000_000, L=10_000, reps=3, cpu=True):
+    """configs[2]: WFA with the reference's semantics (wfa.rs) on 10^6
+    distinct 10 kbp G-mut(5 %) pairs generated on the device, step cap 10^4,
+    sequences and results in HBM."""
+    qs, qo, ds, do, gen_s = c3_pairs(torch, n_pairs, L)
     k = np.arange(n_pairs, dtype=np.uint32)
     plan = saln.WfaPlan(qo, do, pairs=np.stack([k, k], 1), max_steps=10_000)
     out_t = torch.zeros(n_pairs * 8, dtype=torch.int32, device="cuda")
     plan.execute(qs, ds, out_t)
     torch.cuda.synchronize()
-    reps = 3
     t0 = time.perf_counter()
     for _ in range(reps):
         plan.execute(qs, ds, out_t)
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / reps
+    ev_s = event_time(torch, lambda: plan.execute(qs, ds, out_t), 1)
     r = out_t.cpu().numpy().view(saln._lib.WFA_RESULT_DTYPE)
     st, cnt = np.unique(r["status"], return_counts=True)
-    # CPU: the oracle's WFA (refwfa.c) on a sample of the same pairs, one core
-    samp = np.random.default_rng(3).choice(n_pairs, 200, replace=False)
-    bad, t0 = 0, time.perf_counter()
-    for p in samp:
-        qq = qs[int(qo[p]):int(qo[p + 1])].cpu().numpy().tobytes()
-        dd = ds[int(do[p]):int(do[p + 1])].cpu().numpy().tobytes()
-        o = refcpu.wfa(qq, dd, max_steps=10_000)
-        rr = r[p]
-        bad += not (int(rr["status"]) == o.status and int(rr["score"]) == o.score
-                    and int(rr["steps"]) == o.steps)
-    cpu_s = (time.perf_counter() - t0) / len(samp)
+    kern = "wfa_kernel"
+    out = {"workload": f"configs[2]: {n_pairs} distinct WFA pairs of {L} bp G-mut(5 %), "
+                       "reference semantics, step cap 1e4",
+           "value": round(n_pairs / dt, 1), "unit": "pairs/s", "ms": round(dt * 1e3, 3),
+           "status_counts": {saln._lib.STATUS_NAMES.get(int(s), str(int(s))): int(c)
+                             for s, c in zip(st, cnt)},
+           "gen_s": round(gen_s, 2), "executes": 2 + reps,
+           "roofline": valu_roof(kern, ev_s, valu_per_execute(kern, "c3"),
+                                 note="every pair ends in REF_PANIC_TRIM at s = 20 (wfa.rs:603): "
+                                      "20 score steps of one lane per pair")}
+    if cpu:
+        from oracle import refcpu  # cpu_baseline leg only
+        samp = np.random.default_rng(3).choice(n_pairs, 200, replace=False)
+        bad, t0 = 0, time.perf_counter()
+        for p in samp:
+            qq = qs[int(qo[p]):int(qo[p + 1])].cpu().numpy().tobytes()
+            dd = ds[int(do[p]):int(do[p + 1])].cpu().numpy().tobytes()
+            o = refcpu.wfa(qq, dd, max_steps=10_000)
+            rr = r[p]
+            bad += not (int(rr["status"]) == o.status and int(rr["score"]) == o.score
+                        and int(rr["steps"]) == o.steps)
+        cpu_s = (time.perf_counter() - t0) / len(samp)
+        out["verified"] = {"pairs": len(samp), "mismatches": bad,
+                           "checker": "oracle/refwfa.c status, printed score, steps (untimed)"}
+        out["cpu_baseline"] = {"pairs_per_s": round(1 / cpu_s, 1), "cores": 1, "kind": "port",
+                               "sample": f"{len(samp)} of the pairs through oracle/refwfa.c "
+                                         "(its stdout text included)"}
     plan.close()
-    del qs, ds, out_t
+    del out_t
     torch.cuda.empty_cache()
-    return {"workload": f"configs[2]: {n_pairs} distinct WFA pairs of {L} bp G-mut(5 %), "
-                        "reference semantics, step cap 1e4",
-            "value": round(n_pairs / dt, 1), "unit": "pairs/s", "ms": round(dt * 1e3, 3),
-            "status_counts": {saln._lib.STATUS_NAMES.get(int(s), str(int(s))): int(c)
-                              for s, c in zip(st, cnt)},
-            "gen_s": round(gen_s, 2),
-            "verified": {"pairs": len(samp), "mismatches": bad,
-                         "checker": "oracle/refwfa.c status, printed score, steps (untimed)"},
-            "cpu_baseline": {"pairs_per_s": round(1 / cpu_s, 1), "cores": 1, "kind": "port",
-                             "sample": f"{len(samp)} of the pairs through oracle/refwfa.c "
-                                       "(its stdout text included)"}}
+    return out
+
+
+def leg_c3_affine(torch, saln, n_pairs=1_000_000, L=10_000, reps=1, cpu=True):
+    """configs[2]'s pairs through the corrected gap-affine WFA (SURVEY.md
+    §8(f) row 4; not reference parity): the minimum penalty with wfa.rs:14-21's
+    x = 4, o = 2, e = 6, sequences and scores in HBM.  A seeded sample of 200
+    pairs is checked against the Gotoh DP (oracle/refaffine.c), which is also
+    the CPU baseline (on the box's cores)."""
+    from sequencealigning_amd.wfa_affine import WfaAffinePlan
+    qs, qo, ds, do, gen_s = c3_pairs(torch, n_pairs, L)
+    k = np.arange(n_pairs, dtype=np.uint32)
+    plan = WfaAffinePlan(qo, do, np.stack([k, k], 1))
+    sc = torch.zeros(n_pairs, dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    ev_s = event_time(torch, lambda: plan.execute(qs, ds, sc), reps)
+    dt = (time.perf_counter() - t0) / reps
+    s = sc.cpu().numpy()
+    kern = "wfa_affine_kernel"
+    out = {"workload": f"configs[2] pairs ({n_pairs} distinct, {L} bp G-mut 5 %) through the "
+                       "corrected gap-affine WFA (x=4, o=2, e=6; score only; not reference parity)",
+           "value": round(n_pairs / dt, 1), "unit": "pairs/s", "seconds": round(dt, 3),
+           "penalty_mean": round(float(s[s >= 0].mean()), 1) if (s >= 0).any() else None,
+           "over_limits": int((s < 0).sum()), "executes": reps,
+           "roofline": valu_roof(kern, ev_s, valu_per_execute(kern, "c3_affine"),
+                                 note="one wave per pair over diagonal groups of 4 x 64 lanes; "
+                                      "issue and LDS latency (DESIGN.md §3b)")}
+    if cpu:
+        from oracle import refcpu  # checker + cpu_baseline only
+        samp = np.sort(np.random.default_rng(6).choice(n_pairs, 200, replace=False))
+        qh = np.concatenate([qs[int(qo[p]):int(qo[p + 1])].cpu().numpy() for p in samp])
+        dh = np.concatenate([ds[int(do[p]):int(do[p + 1])].cpu().numpy() for p in samp])
+        ql = np.array([int(qo[p + 1] - qo[p]) for p in samp], np.uint64)
+        dl = np.array([int(do[p + 1] - do[p]) for p in samp], np.uint64)
+        qo2 = np.concatenate([[0], np.cumsum(ql)]).astype(np.uint64)
+        do2 = np.concatenate([[0], np.cumsum(dl)]).astype(np.uint64)
+        idx = np.arange(len(samp), dtype=np.uint32)
+        T = cpu_threads()
+        t0 = time.perf_counter()
+        want = refcpu.affine_run_pairs(qh, qo2, dh, do2, idx, idx, threads=T)
+        cpu_s = time.perf_counter() - t0
+        out["verified"] = {"pairs": len(samp), "mismatches": int(np.sum(want != s[samp])),
+                           "checker": "oracle/refaffine.c Gotoh DP (untimed)"}
+        out["cpu_baseline"] = {"pairs_per_s": round(len(samp) / cpu_s, 2), "cores": T,
+                               "kind": "port", "seconds": round(cpu_s, 2),
+                               "sample": f"{len(samp)} of the pairs through oracle/refaffine.c "
+                                         f"(O(n*m) Gotoh DP) on {T} threads"}
+    plan.close()
+    del sc
+    torch.cuda.empty_cache()
+    return out
 
 
 def leg_host(saln):
@@ -395,6 +590,46 @@ def leg_host(saln):
             "ms": round(dt * 1e3, 2)}
 
 
+# --------------------------------------------------------------- launcher
+def launch_ranks(n: int) -> int:
+    """Start n ranks of this command (torch.distributed.run, one process per
+    GPU, rendezvous on 127.0.0.1) as a child and return its exit status.
+    The parent never initialises the GPU (it must not, before a child that
+    will use it starts)."""
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}",
+           os.path.abspath(__file__)] + sys.argv[1:]
+    log(f"[bench] launching {n} ranks: torch.distributed.run --nproc-per-node={n} ...")
+    return subprocess.call(cmd, env=env)
+
+
+def launch_selftest(backend: str) -> None:
+    """--selftest-launch: the ranks meet, agree on the world and print one
+    JSON line (rank 0); no GPU work.  tests/test_bench_launch.py runs it on
+    gloo."""
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if world > 1:
+        dist.init_process_group(backend)
+        t = torch.tensor([rank], dtype=torch.int64)
+        ranks = [torch.zeros_like(t) for _ in range(world)]
+        dist.all_gather(ranks, t)
+        ranks = sorted(int(x.item()) for x in ranks)
+        dist.destroy_process_group()
+    else:
+        ranks = [0]
+    if rank == 0:
+        print(json.dumps({"launch_selftest": True, "n_gpus": world, "ranks": ranks}), flush=True)
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -403,17 +638,28 @@ def main() -> None:
     ap.add_argument("--pairs", type=int, default=N_PAIRS)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--legs", default="auto",
-                    help="comma list of extra configs (c5,c1,c3,c4,host), 'none', or 'auto' "
-                         "(all at N = 1, c5 at N > 1)")
+                    help="comma list of extra configs (c5,c1,c3,c3_affine,c4,host), 'none', or "
+                         "'auto' (all at N = 1, c5 at N > 1)")
     ap.add_argument("--score-only", action="store_true",
                     help="score + panic status only (no parent codes / traceback; the C5 mode)")
     ap.add_argument("--pipeline", action="store_true",
                     help="overlap step k's traceback with step k+1's fill on a second stream "
                          "(measured slower on MI355X: the walk slows the VALU-bound fill)")
+    ap.add_argument("--selftest-launch", action="store_true",
+                    help="only start the ranks and report the world (no GPU work; tests)")
+    ap.add_argument("--backend", default="nccl", help="torch.distributed backend (nccl = RCCL)")
     args = ap.parse_args()
     if os.environ.get("SALN_LIB"):
         sys.exit("bench.py: SALN_LIB is set (an instrumented tools/ build); the bench measures "
                  "the product library sequencealigning_amd/libsaln.so only")
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))
+    if env_world is not None and int(env_world) != args.gpus:
+        sys.exit(f"bench.py: WORLD_SIZE={env_world} but --gpus {args.gpus}")
+    if args.selftest_launch:
+        launch_selftest(args.backend)
+        return
 
     import torch
     import torch.distributed as dist
@@ -426,7 +672,7 @@ def main() -> None:
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        dist.init_process_group(args.backend, device_id=torch.device("cuda", local))
     if args.legs == "auto":
         legs = list(ALL_LEGS) if world == 1 else ["c5"]
     elif args.legs == "none":
@@ -495,13 +741,21 @@ def main() -> None:
     total_cells = cells_rank * world * args.steps
     gcups = total_cells / dt / 1e9
     fill_avg_s = fill_ms / max(1, fill_n) / 1e3
-    achieved = cells_rank * 1.0 / fill_avg_s / 1e9  # 1 B/cell parent mask, GB/s
     out = None
     if rank == 0:
         last = (args.steps - 1) % nbuf if args.steps else 0
         hr = res[last].cpu().numpy()
         statuses = np.bincount(hr[1::4] & 0xFF, minlength=3)
         fill_kernel = "nw_fill_pk_kernel<16, 10,"
+        roof = roof_hbm(cells_rank, fill_avg_s, "nw_fill",
+                        pmc(fill_kernel) if not args.score_only else None,
+                        traffic_unit="bytes/launch (PMC FETCH_SIZE*2 + WRITE_SIZE)",
+                        traffic_source="profiles/pmc_traffic.json: rocprofv3 --pmc passes of "
+                                       "this command (tools/pmc.sh), not measured in this run",
+                        traceback_avg_ms=round(tb_ms / max(1, tb_n), 4),
+                        execute_avg_ms=round(ex_ms / max(1, ex_n), 4), pipelined=pipelined,
+                        valu=valu_roof(fill_kernel, fill_avg_s) if not args.score_only else None)
+        roof["frac"] = round(roof["frac"], 4)
         out = {
             "metric": METRIC, "value": round(gcups, 3), "unit": "GCUPS", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup,
@@ -517,19 +771,7 @@ def main() -> None:
                        "pairs_per_gpu": n, "len_q": LQ, "len_db": LD, "seed": hex(SEED),
                        "parallelism": f"db-sharded x{world}" + (" + RCCL gather" if world > 1
                                                                else "")},
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": pmc_traffic(fill_kernel) if not args.score_only else None,
-                         "traffic_unit": "bytes/launch (PMC FETCH_SIZE*2 + WRITE_SIZE)",
-                         "traffic_source": "profiles/pmc_traffic.json: rocprofv3 --pmc passes of "
-                                           "this command (tools/pmc.sh), not measured in this run",
-                         "algorithmic_bytes": cells_rank, "kernel": "nw_fill",
-                         "kernel_avg_ms": round(fill_avg_s * 1e3, 4),
-                         "traceback_avg_ms": round(tb_ms / max(1, tb_n), 4),
-                         "execute_avg_ms": round(ex_ms / max(1, ex_n), 4),
-                         "pipelined": pipelined,
-                         "valu": valu_roof(fill_kernel, fill_avg_s)
-                         if not args.score_only else None},
+            "roofline": roof,
             "status_counts": {"ok": int(statuses[0]), "ref_panic_boundary": int(statuses[2])},
         }
         if not args.score_only:
@@ -539,20 +781,23 @@ def main() -> None:
     del res, cig, dq, dd
     torch.cuda.empty_cache()
 
+    cpu = not args.no_cpu_baseline
     extra = {}
     for leg in legs:
         t0 = time.perf_counter()
         try:
             if leg == "c5":
-                r = leg_c5(world, rank, local, dist, torch)
+                r = leg_c5(world, rank, local, dist, torch, cpu=cpu)
             elif rank != 0 or world > 1:
                 continue
             elif leg == "c1":
-                r = leg_c1(torch, saln)
+                r = leg_c1(torch, saln, cpu=cpu)
             elif leg == "c3":
-                r = leg_c3(torch, saln)
+                r = leg_c3(torch, saln, cpu=cpu)
+            elif leg == "c3_affine":
+                r = leg_c3_affine(torch, saln, cpu=cpu)
             elif leg == "c4":
-                r = leg_c4(torch, saln)
+                r = leg_c4(torch, saln, cpu=cpu)
             elif leg == "host":
                 r = leg_host(saln)
             else:
@@ -565,10 +810,11 @@ def main() -> None:
             r["leg_wall_s"] = round(time.perf_counter() - t0, 2)
             extra[leg] = r
             log(f"[bench] {leg}: {json.dumps(r)[:300]}")
+    _C3_PAIRS.clear()
     if rank == 0:
         if extra:
             out["configs"] = extra
-        if not args.no_cpu_baseline and world == 1:  # the CPU leg: rank 0 at N = 1 only
+        if cpu and world == 1:  # the CPU leg: rank 0 at N = 1 only
             out["cpu_baseline"] = cpu_baseline()
         print(json.dumps(out), flush=True)
     if world > 1:

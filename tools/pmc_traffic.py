@@ -14,7 +14,16 @@ import sys
 from collections import defaultdict
 
 
-def main(d="gpurun_out/pmc", out="profiles/pmc_traffic.json", tag=""):
+SOURCES = {
+    "nw": "tools/pmc.sh (rocprofv3 --pmc, one counter group per pass) on tools/prof_nw.py: "
+          "100000 x 150x150 G-iid pairs, seed 0x5EED0002",
+    "legs": "tools/pmc.sh (rocprofv3 --pmc, one counter group per pass) on tools/prof_legs.py: "
+            "bench.py's legs without their CPU parts; executes = runs of each leg's workload "
+            "in one pass",
+}
+
+
+def main(d="gpurun_out/pmc", out="profiles/pmc_traffic.json", tag="", source="nw"):
     acc = defaultdict(lambda: defaultdict(list))
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         with open(f) as fh:
@@ -36,6 +45,9 @@ def main(d="gpurun_out/pmc", out="profiles/pmc_traffic.json", tag=""):
                        ("SQ_ACTIVE_INST_ANY", "active_inst_any_q")):
             if c in cs:  # per-launch means (SQ cycle counters in quad-cycles)
                 res[k][key] = round(sum(cs[c]) / len(cs[c]))
+        if "SQ_INSTS_VALU" in cs:  # over the whole profiled run (legs: / its executes)
+            res[k]["valu_wave_insts_sum"] = round(sum(cs["SQ_INSTS_VALU"]))
+            res[k]["valu_dispatches"] = len(cs["SQ_INSTS_VALU"])
         r = res[k]
         if "wave_cycles_q" in r and r["wave_cycles_q"]:
             # shares of the waves' lifetime: issue-stalled on a dependency /
@@ -44,9 +56,11 @@ def main(d="gpurun_out/pmc", out="profiles/pmc_traffic.json", tag=""):
             for key in ("wait_inst_any_q", "wait_any_q", "active_inst_any_q", "active_inst_valu_q"):
                 if key in r:
                     r[key.replace("_q", "_frac")] = round(r[key] / wc, 4)
-    doc = {"source": "tools/pmc.sh (rocprofv3 --pmc, one counter group per pass) on "
-                     "tools/prof_nw.py: 100000 x 150x150 G-iid pairs, seed 0x5EED0002",
-           "round": tag, "kernels": res}
+    doc = {"source": SOURCES.get(source, source), "round": tag, "kernels": res}
+    ex = os.path.join(d, "executes.json")  # tools/prof_legs.py
+    if os.path.exists(ex):
+        with open(ex) as fh:
+            doc["executes"] = json.load(fh)
     with open(out, "w") as fh:
         json.dump(doc, fh, indent=1)
     print(json.dumps(doc, indent=1))

@@ -1,0 +1,49 @@
+"""Profiling driver for bench.py's legs (c1, c3, c3_affine, c4, c5): each
+leg's GPU workload exactly as the bench runs it, without its CPU baseline and
+checks; used under rocprofv3 (--kernel-trace --stats, and the --pmc passes of
+tools/pmc.sh).  Writes {leg: executes} (runs of the leg's workload) to
+$PMC_EXECUTES (default gpurun_out/pmc/executes.json) so tools/pmc_traffic.py
+can turn the counters' per-run sums into per-execute figures.
+
+    python tools/prof_legs.py [--legs c1,c3,c3_affine,c4,c5]
+"""
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--legs", default="c1,c3,c3_affine,c4,c5")
+    a = ap.parse_args()
+    import torch
+    import sequencealigning_amd as saln
+    import bench
+    ex = {}
+    for leg in a.legs.split(","):
+        if leg == "c5":
+            r = bench.leg_c5(1, 0, 0, None, torch, cpu=False)
+        elif leg == "c1":
+            r = bench.leg_c1(torch, saln, cpu=False)
+        elif leg == "c3":
+            r = bench.leg_c3(torch, saln, cpu=False)
+        elif leg == "c3_affine":
+            r = bench.leg_c3_affine(torch, saln, cpu=False)
+        elif leg == "c4":
+            r = bench.leg_c4(torch, saln, cpu=False)
+        else:
+            raise SystemExit(f"unknown leg {leg}")
+        ex[leg] = r["executes"]
+        print(leg, json.dumps(r)[:400], flush=True)
+    path = os.environ.get("PMC_EXECUTES", os.path.join(ROOT, "gpurun_out", "pmc", "executes.json"))
+    os.makedirs(os.path.dirname(path), exist_ok=True)
+    with open(path, "w") as fh:
+        json.dump(ex, fh)
+
+
+if __name__ == "__main__":
+    main()
