@@ -593,6 +593,22 @@ int saln_nw_execute(saln_nw_plan *p, const uint8_t *d_q, const uint8_t *d_db,
     int32_t *endh = cur ? p->d_endh2 : p->d_endh;
     // this workspace may still be read by the traceback of execute n-2
     if (p->tb_pending[cur]) HIP_TRY(hipStreamWaitEvent(s, p->tb_done(cur), 0));
+    // boundary columns preset to kColEmpty: a row is published once its value
+    // replaces the preset (nw_fill_rows_kernel).  Issued ahead of the timing
+    // events, so "nw_fill" times the fill kernels alone.
+    for (size_t k = 0; k + 1 < p->sub.size(); ++k) {
+        const uint32_t a = std::max(p->sub[k], p->var_first[kStripeVariant]);
+        const uint32_t b = std::min(p->sub[k + 1], p->var_first[kStripeVariant] +
+                                                       p->var_count[kStripeVariant]);
+        if (a >= b || p->work_first[b] <= p->work_first[a]) continue;
+        const NwPairDesc &la = p->h_pairs[b - 1];
+        const uint64_t c0 = p->h_pairs[a].scratch_off;
+        const uint64_t c1 = la.scratch_off + (uint64_t)p->stripe_sub *
+                                                 variant_geom(kStripeVariant).n_chunks(la.len_q) *
+                                                 scratch_col(la.len_db);
+        HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)(p->d_scratch + c0), (int)0x80000000u,
+                                  2 * (c1 - c0), s));
+    }
     hipEvent_t *ev = nullptr;
     if (p->timing) {
         if (p->ev_used == p->ev_pool.size()) {
@@ -613,15 +629,6 @@ int saln_nw_execute(saln_nw_plan *p, const uint8_t *d_q, const uint8_t *d_db,
             if (a < b && v == kStripeVariant) {
                 const uint32_t w0 = p->work_first[a], w1 = p->work_first[b];
                 if (w1 > w0) {
-                    // boundary columns preset to kColEmpty: a row is published
-                    // once its value replaces the preset (nw_fill_stripe_kernel)
-                    const NwPairDesc &la = p->h_pairs[b - 1];
-                    const uint64_t c0 = p->h_pairs[a].scratch_off;
-                    const uint64_t c1 = la.scratch_off + (uint64_t)p->stripe_sub *
-                                                             variant_geom(v).n_chunks(la.len_q) *
-                                                             scratch_col(la.len_db);
-                    HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)(p->d_scratch + c0), (int)0x80000000u,
-                                              2 * (c1 - c0), s));
                     HIP_TRY(launch_fill_stripes(p->d_pairs, p->d_work + w0, w1 - w0, d_q, d_db,
                                                 mask, p->d_scratch, p->d_prog, p->d_err, endh,
                                                 p->sc,

@@ -60,8 +60,10 @@ def test_c3_shape_trim_panic(saln, oracle):
     res, _ = saln.wfa_align_batch(q, d, pairs=[(k, k) for k in range(n)])
     assert (res["status"] == 3).all()
     assert (res["steps"] == 20).all()
-    o = oracle.wfa(q[0], d[0], max_steps=64)
-    assert o.status == 3 and o.steps == 20
+    for k in range(n):  # every pair against the oracle (refwfa.c), not a property only
+        o = oracle.wfa(q[k], d[k], max_steps=64)
+        assert (int(res["status"][k]), int(res["steps"][k]), int(res["score"][k])) == \
+            (o.status, o.steps, o.score), k
 
 
 def test_modes(saln):

@@ -28,7 +28,8 @@ def main(d="gpurun_out/pmc", out="profiles/pmc_traffic.json", tag="", source="nw
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         with open(f) as fh:
             for row in csv.DictReader(fh):
-                name = row.get("Kernel_Name", "?").split("(")[0].replace("void ", "")
+                name = row.get("Kernel_Name", "?").replace("(anonymous namespace)::", "")
+                name = name.split("(")[0].replace("void ", "")
                 acc[name][row["Counter_Name"]].append(float(row["Counter_Value"]))
     res = {}
     for k, cs in acc.items():
