@@ -254,7 +254,10 @@ struct WalkGeo {
     static constexpr uint32_t kWinBytes = W * kSlotBytes;    // one window of a wave
     static constexpr uint32_t kWaveLds = NW * kWinBytes;
     static constexpr uint32_t kVmcnt = NW * (W - 1);
-    static_assert(LB <= 16, "LDS window slots hold at most 16 bytes per lane");
+    // segments wider than a 16-byte slot (K = 19: 20 bytes): a slot holds
+    // bytes [off, off + 16) of its segment, off = 0 or 4 per (window, slot)
+    static constexpr bool kWide = LB > 16;
+    static_assert(LB <= 20, "LDS window slots hold 16 bytes of a segment of at most 20");
 };
 
 typedef __attribute__((address_space(3))) uint8_t lds_u8;
@@ -347,6 +350,10 @@ __device__ void walk_pair_lds(const NwPairDesc &p, int32_t hend, const uint8_t *
     uint32_t col = (tj - 1) % K;  // target column inside block B
     uint32_t wc = B % NW;         // window of block B (block b lives in window b % NW)
     uint32_t valid = kAll;        // bit 8w+s: slot s of window w holds its block
+    // kWide: bit 8w+s set = slot s of window w holds bytes [4, 20) of its
+    // segment (the lane was at a column >= 16 of block B when it was loaded,
+    // or the window held block B-1, entered at its last column); else [0, 16)
+    uint32_t woff = 0;
     const uint32_t wbase = lds_off(win) + (threadIdx.x & 63u) * 16u;
     uint32_t wrow = 0;            // LDS address of (window wc, slot S, my lane)
     uint64_t p_twait = 0, p_tsync = 0, p_t0 = SALN_PROF_T();
@@ -376,6 +383,13 @@ __device__ void walk_pair_lds(const NwPairDesc &p, int32_t hend, const uint8_t *
 #define SALN_REFILL(S, ROW)                                                                    \
     {                                                                                          \
         const void *a0 = seg(bp0, ROW), *a1 = seg(bp1, ROW);                                   \
+        if constexpr (WG::kWide) {                                                             \
+            const bool hi = col >= 16u;                                                        \
+            a0 = (const uint8_t *)a0 + (hi ? 4 : 0);                                           \
+            a1 = (const uint8_t *)a1 + 4;                                                      \
+            woff = (woff & ~(0x101u << (S))) | (1u << ((wc ^ 1u) * 8u + (S))) |                \
+                   ((hi ? 1u : 0u) << (wc * 8u + (S)));                                        \
+        }                                                                                      \
         if constexpr (NW == 2) {                                                               \
             SALN_DMA(0, S, wc ? a1 : a0);                                                      \
             SALN_DMA(1, S, wc ? a0 : a1);                                                      \
@@ -390,11 +404,16 @@ __device__ void walk_pair_lds(const NwPairDesc &p, int32_t hend, const uint8_t *
     // slot S of window wc not refreshed since a crossing: load it now.
     // Independent ifs (not if/else): the compiler must not merge the calls
     // into one DMA with a per-lane (then readfirstlane'd) LDS base.
-#define SALN_ENSURE(S)                                                                         \
+#define SALN_ENSURE(S, ECOL)                                                                   \
     if (!(valid & (1u << (wc * 8u + (S))))) {                                                  \
         const uint64_t tq0 = SALN_PROF_T();                                                    \
         ++p_sync;                                                                              \
         const void *ac = seg(bp0, (int32_t)(base - (S)));                                      \
+        if constexpr (WG::kWide) {                                                             \
+            const bool hi = (ECOL) >= 16u;                                                     \
+            ac = (const uint8_t *)ac + (hi ? 4 : 0);                                           \
+            woff = (woff & ~(1u << (wc * 8u + (S)))) | ((hi ? 1u : 0u) << (wc * 8u + (S)));    \
+        }                                                                                      \
         if (wc == 0) { SALN_DMA(0, S, ac); }                                                   \
         __builtin_amdgcn_sched_barrier(0);                                                     \
         if (wc == 1) { SALN_DMA(1, S, ac); }                                                   \
@@ -409,10 +428,18 @@ __device__ void walk_pair_lds(const NwPairDesc &p, int32_t hend, const uint8_t *
 #define SALN_PHASE(S)                                                                          \
     wrow = wbase + wc * WG::kWinBytes + (S) * WG::kSlotBytes;                                  \
     if (walking) {                                                                             \
-        SALN_ENSURE(S)                                                                         \
+        SALN_ENSURE(S, col)                                                                    \
         for (;;) {                                                                             \
             const uint64_t tw0 = SALN_PROF_T();                                                \
-            uint32_t raw = window_raw<WG::kVmcnt>(wrow + col);                                 \
+            uint32_t raw;                                                                      \
+            if constexpr (WG::kWide) {                                                         \
+                const uint32_t off = (woff >> (wc * 8u + (S))) & 1u ? 4u : 0u;                 \
+                raw = window_raw<WG::kVmcnt>(wrow + col - (col >= off ? off : 0u));            \
+                if (col < off) /* left the slot's 16 bytes (a long gap): read HBM */           \
+                    raw = m[geo.cell(ti, tj, rs, bs, p.mask_cs)];                              \
+            } else {                                                                           \
+                raw = window_raw<WG::kVmcnt>(wrow + col);                                      \
+            }                                                                                  \
             p_twait += SALN_PROF_T() - tw0;                                                    \
             ++p_iter;                                                                          \
             SALN_WALK_CHECK_HOOK(S)                                                            \
@@ -446,7 +473,7 @@ __device__ void walk_pair_lds(const NwPairDesc &p, int32_t hend, const uint8_t *
                     bp1 = bp2;                                                                 \
                     bp2 = blk_base(B >= 2 ? B - 2 : 0);                                        \
                 }                                                                              \
-                SALN_ENSURE(S)                                                                 \
+                SALN_ENSURE(S, K - 1u) /* entered at the block's last column */               \
             }                                                                                  \
             col = left ? (col == 0 ? K - 1 : col - 1) : col;                                   \
             if (up || done) break; /* up one row: next phase */                                \
@@ -1664,16 +1691,32 @@ __device__ __forceinline__ int32_t wave_prefix_max(int32_t v, Fill &&fill) {
     return v;
 }
 
-template <int K, int kCodes, bool kMinPen>
-__global__ __launch_bounds__(64) void nw_fill_rows_kernel(
+// kSplit (walk codes; round 3): a second wave per stripe builds and stores
+// the parent codes.  The stripe's lone recurrence wave (wave 0) hands every
+// cell's M~, I~ and D~ to it through an LDS ring of two 8-row groups and
+// meets it at one barrier per group; the coder wave (wave 1) recomputes H~
+// and the gap-open candidates from them and runs the sign gather.  The
+// recurrence wave's row then carries no code instructions and no mask
+// stores: the row chain that bounds a long pair gets shorter.
+template <int K>
+struct RowRing {  // one row of the ring per lane: {M, I} of my K columns, and D
+    typedef typename std::conditional<K == 1, int2, int4>::type MI;
+    typedef typename std::conditional<K == 1, int, int2>::type Dv;
+    MI mi[2][kRowsGrp][64];
+    Dv d[2][kRowsGrp][64];
+};
+
+template <int K, int kCodes, bool kMinPen, bool kSplit = false>
+__global__ __launch_bounds__(kSplit ? 128 : 64) void nw_fill_rows_kernel(
     const NwPairDesc *__restrict__ pairs, const uint2 *__restrict__ work,
     const uint8_t *__restrict__ qs, const uint8_t *__restrict__ ds, uint8_t *__restrict__ mask,
     int2 *__restrict__ scratch, uint32_t *__restrict__ err, int32_t *__restrict__ end_h,
     Scoring sc) {
     static_assert(K == 1 || K == 2 || K == 4, "4 cells per code word");
+    static_assert(!kSplit || (kCodes == kCodesWalk && K <= 2), "the coder wave builds walk codes");
     constexpr int S = 4 / K;   // stripes per 256-column chunk (work item)
     constexpr int W = 64 * K;  // stripe width (4 / K rows per code word)
-    const int lane = (int)threadIdx.x;
+    const int lane = (int)(threadIdx.x & 63u);
     const uint2 wk = work[blockIdx.x / S];
     const NwPairDesc p = pairs[wk.x];
     const uint32_t g = wk.y * S + blockIdx.x % S;  // stripe index
@@ -1726,6 +1769,82 @@ __global__ __launch_bounds__(64) void nw_fill_rows_kernel(
     const uint32_t k_end = jend % K;
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the query chars
     uint32_t sg[8][4];  // sign words of the current code word's four cells
+    constexpr bool kCodesHere = kCodes != kCodesNone && !kSplit;  // this wave builds codes
+    __shared__ typename std::conditional<kSplit, RowRing<K>, int>::type ring_lds;
+    RowRing<K> *ring = reinterpret_cast<RowRing<K> *>(&ring_lds);
+    (void)ring;
+    uint32_t gbuf = 0;  // kSplit: the ring half of the current group
+    // kSplit: LDS writes done, then meet the other wave (no fence: a
+    // __syncthreads would wait for this wave's boundary stores and prefetch)
+    auto ring_barrier = [&]() __attribute__((always_inline)) {
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" : : : "memory");
+        gbuf ^= 1u;
+    };
+    if constexpr (kSplit) {
+        if (threadIdx.x >= 64) {  // the coder wave: one ring group per barrier
+            const int32_t kOp = kOpen;
+            auto code_rows = [&](uint32_t r0, uint32_t nrows, auto m_c) __attribute__((always_inline)) {
+                constexpr bool kM = decltype(m_c)::value;
+                constexpr uint32_t R = 4 / K;  // rows per code word
+#pragma unroll
+                for (uint32_t w0 = 0; w0 < kRowsGrp; w0 += R) {
+                    if (w0 >= nrows) break;
+                    uint32_t cs[8][4];
+#pragma unroll
+                    for (uint32_t u = 0; u < R; ++u) {
+                        const uint32_t q = w0 + u;
+                        const uint32_t r = r0 + q;
+                        int32_t Mv[K], Ic[K], Dc[K];
+                        if constexpr (K == 1) {
+                            const int2 mi = ring->mi[gbuf][q][lane];
+                            Mv[0] = mi.x; Ic[0] = mi.y;
+                            Dc[0] = ring->d[gbuf][q][lane];
+                        } else {
+                            const int4 mi = ring->mi[gbuf][q][lane];
+                            const int2 dd = ring->d[gbuf][q][lane];
+                            Mv[0] = mi.x; Mv[1] = mi.y; Ic[0] = mi.z; Ic[1] = mi.w;
+                            Dc[0] = dd.x; Dc[1] = dd.y;
+                        }
+                        const int32_t hm = (kM && r == ld) ? ~3 : ~1;
+#pragma unroll
+                        for (int k = 0; k < K; ++k) {
+                            const int32_t H = max(Mv[k], max(Ic[k], Dc[k]));
+                            const int32_t Hc = H & hm;
+                            const int32_t tOr = (Mv[k] + kOp) | 1;
+                            const int e = (int)u * K + k;
+                            cs[0][e] = kM ? (uint32_t)(Mv[k] - Hc) : 0u;
+                            cs[1][e] = (uint32_t)(Ic[k] - Hc);
+                            cs[2][e] = (uint32_t)(Dc[k] - Hc);
+                            cs[3][e] = cs[5][e] = cs[7][e] = 0u;
+                            cs[4][e] = (uint32_t)(tOr - Ic[k]);
+                            cs[6][e] = (uint32_t)(tOr - Dc[k]);
+                        }
+                    }
+                    const uint32_t wv = stripe_code_word<kCodesWalk, kM, false>(cs);
+                    const uint32_t n = nrows - w0;
+                    uint8_t *a = mrow + (uint64_t)(r0 + w0 - 1) * 256;
+                    if constexpr (K == 2) {
+                        *reinterpret_cast<uint16_t *>(a) = (uint16_t)wv;
+                        if (n > 1) *reinterpret_cast<uint16_t *>(a + 256) = (uint16_t)(wv >> 16);
+                    } else {
+                        a[0] = (uint8_t)wv;
+                        if (n > 1) a[256] = (uint8_t)(wv >> 8);
+                        if (n > 2) a[512] = (uint8_t)(wv >> 16);
+                        if (n > 3) a[768] = (uint8_t)(wv >> 24);
+                    }
+                }
+            };
+            uint32_t r = 1;
+            for (; r + kRowsGrp - 1 < ld; r += kRowsGrp) {
+                asm volatile("s_barrier" : : : "memory");
+                code_rows(r, kRowsGrp, std::false_type{});
+                gbuf ^= 1u;
+            }
+            asm volatile("s_barrier" : : : "memory");
+            code_rows(r, ld - r + 1, std::true_type{});
+            return;
+        }
+    }
     // one row: r (1-based), its db char, the left boundary (H~(r, c0), I~
     // entering column c0+1) and u = its slot in the code word (compile time)
     // m: the row may be the last one (argM bits and the reference's tie
@@ -1768,12 +1887,14 @@ __global__ __launch_bounds__(64) void nw_fill_rows_kernel(
         }
         const int32_t S_incl = wave_prefix_max(P[K - 1], fill);
         const int32_t Ein = max(__builtin_amdgcn_update_dpp(kNegInf, S_incl, 0x138, 0xf, 0xf, false), bI);
+        int32_t Iv[K];
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             const int32_t I = k == 0 ? Ein : max(Ein, P[k - 1]);
             const int32_t D = Dv[k];
             const int32_t H = max(M[k], max(I, D));
-            if constexpr (kCodes != kCodesNone) {
+            Iv[k] = I;
+            if constexpr (kCodesHere) {
                 const int32_t Hc = H & hm;
                 const int32_t tOr = tO[k] | kTieOr;
                 const int e = u * K + k;  // cell slot in the code word (unrolled: constant)
@@ -1793,6 +1914,15 @@ __global__ __launch_bounds__(64) void nw_fill_rows_kernel(
             }
             Hp[k] = H;
         }
+        if constexpr (kSplit) {  // the row's cells to the coder wave
+            if constexpr (K == 1) {
+                ring->mi[gbuf][q][lane] = make_int2(M[0], Iv[0]);
+                ring->d[gbuf][q][lane] = Dv[0];
+            } else {
+                ring->mi[gbuf][q][lane] = make_int4(M[0], M[1], Iv[0], Iv[1]);
+                ring->d[gbuf][q][lane] = make_int2(Dv[0], Dv[1]);
+            }
+        }
         hb_prev = bH;
         // (H~, I~) leaving the stripe's last column (lane 63's values)
         {   // every lane stores its own (H~, I~) with one instruction: lane 63
@@ -1810,7 +1940,7 @@ __global__ __launch_bounds__(64) void nw_fill_rows_kernel(
     };
     // store the code word of rows r0 .. r0+(4/K)-1 (n of them valid)
     auto put = [&](uint32_t r0, uint32_t n, auto m_c) __attribute__((always_inline)) {
-        if constexpr (kCodes != kCodesNone) {
+        if constexpr (kCodesHere) {
             const uint32_t wv = stripe_code_word<kCodes, decltype(m_c)::value, false>(sg);
             uint8_t *a = mrow + (uint64_t)(r0 - 1) * 256;
             if constexpr (K == 4) {
@@ -1880,7 +2010,7 @@ __global__ __launch_bounds__(64) void nw_fill_rows_kernel(
                 // kG mask stores and kG boundary stores followed the prefetch:
                 // with that many younger VMEM ops outstanding it has landed
                 // (GFX9 vmcnt retires in issue order)
-                if constexpr (kCodes == kCodesNone) {
+                if constexpr (kCodes == kCodesNone || kSplit) {  // no mask stores in this wave
                     if constexpr (kG == 8) asm volatile("s_waitcnt vmcnt(8)" : "+v"(nv) : : "memory");
                     else asm volatile("s_waitcnt vmcnt(4)" : "+v"(nv) : : "memory");
                 } else {
@@ -1996,6 +2126,7 @@ __global__ __launch_bounds__(64) void nw_fill_rows_kernel(
                 quad(r, o0, M0, nofill, std::true_type{});
                 if constexpr (kG == 8) quad(r + 4, o4, M0, nofill, std::true_type{});
             }
+            if constexpr (kSplit) ring_barrier();
         }
         // the last group: 1 .. kG rows, row ld among them
         group(r, std::false_type{});
@@ -2014,6 +2145,7 @@ __global__ __launch_bounds__(64) void nw_fill_rows_kernel(
         } else {
             quad(r, o0, M1, nofill, std::true_type{});
         }
+        if constexpr (kSplit) ring_barrier();
     };
     if (g == 0) rows(std::true_type{});
     else rows(std::false_type{});
@@ -2790,11 +2922,12 @@ hipError_t launch_traceback(int variant, const NwPairDesc *pairs, uint32_t first
             if (e != hipSuccess) return e;
             break;
         }
+        case 4: tb_lds<8, 19>(grid, stream, pairs, first, n, mask, end_h, ops, results, cigar, sc); break;
         case 5: tb_lds<16, 16>(grid, stream, pairs, first, n, mask, end_h, ops, results, cigar, sc); break;
         case 6: tb_lds<32, 16>(grid, stream, pairs, first, n, mask, end_h, ops, results, cigar, sc); break;
         case 7: tb_lds<16, 10>(grid, stream, pairs, first, n, mask, end_h, ops, results, cigar, sc); break;
         case 8: tb_lds<64, 16>(grid, stream, pairs, first, n, mask, end_h, ops, results, cigar, sc); break;
-        default: {  // variant 4 (20-byte segments) and empty-side pairs
+        default: {  // empty-side pairs
             GeomTable gt;
             for (int v = 0; v < kNumVariants; ++v) gt.g[v] = kVariants[v];
             nw_traceback_kernel<<<grid, dim3(256), 0, stream>>>(pairs, first, n, qs, ds, mask,
@@ -2855,9 +2988,23 @@ hipError_t launch_fill_stripes(const NwPairDesc *pairs, const uint2 *work, uint3
     const bool pk = layout == 1;
     if (layout == 2) {  // row-synchronous stripes of 64 * rows_k columns
         const int32_t pm = 4 * (sc.match - sc.mismatch);
+        // walk codes: a coder wave per stripe (kSplit); SALN_ROWS_SPLIT=0 / 1
+        static const int split_env = [] {
+            const char *e = std::getenv("SALN_ROWS_SPLIT");
+            return e ? (e[0] == '1' ? 1 : 0) : 0;
+        }();
         auto go = [&](auto k_c, auto codes_c, auto minpen_c) {
             constexpr int kK = decltype(k_c)::value;
-            nw_fill_rows_kernel<kK, decltype(codes_c)::value, decltype(minpen_c)::value>
+            constexpr int kC = decltype(codes_c)::value;
+            if constexpr (kC == kCodesWalk && kK <= 2) {
+                if (split_env == 1) {
+                    nw_fill_rows_kernel<kK, kC, decltype(minpen_c)::value, true>
+                        <<<dim3(n_work * (4 / kK)), dim3(128), 0, stream>>>(
+                            pairs, work, qs, ds, mask, scratch, err, end_h, sc);
+                    return;
+                }
+            }
+            nw_fill_rows_kernel<kK, kC, decltype(minpen_c)::value>
                 <<<dim3(n_work * (4 / kK)), block, 0, stream>>>(pairs, work, qs, ds, mask, scratch,
                                                                err, end_h, sc);
         };
