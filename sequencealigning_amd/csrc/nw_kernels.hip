@@ -1691,29 +1691,13 @@ __device__ __forceinline__ int32_t wave_prefix_max(int32_t v, Fill &&fill) {
     return v;
 }
 
-// kSplit (walk codes; round 3): a second wave per stripe builds and stores
-// the parent codes.  The stripe's lone recurrence wave (wave 0) hands every
-// cell's M~, I~ and D~ to it through an LDS ring of two 8-row groups and
-// meets it at one barrier per group; the coder wave (wave 1) recomputes H~
-// and the gap-open candidates from them and runs the sign gather.  The
-// recurrence wave's row then carries no code instructions and no mask
-// stores: the row chain that bounds a long pair gets shorter.
-template <int K>
-struct RowRing {  // one row of the ring per lane: {M, I} of my K columns, and D
-    typedef typename std::conditional<K == 1, int2, int4>::type MI;
-    typedef typename std::conditional<K == 1, int, int2>::type Dv;
-    MI mi[2][kRowsGrp][64];
-    Dv d[2][kRowsGrp][64];
-};
-
-template <int K, int kCodes, bool kMinPen, bool kSplit = false>
-__global__ __launch_bounds__(kSplit ? 128 : 64) void nw_fill_rows_kernel(
+template <int K, int kCodes, bool kMinPen>
+__global__ __launch_bounds__(64) void nw_fill_rows_kernel(
     const NwPairDesc *__restrict__ pairs, const uint2 *__restrict__ work,
     const uint8_t *__restrict__ qs, const uint8_t *__restrict__ ds, uint8_t *__restrict__ mask,
     int2 *__restrict__ scratch, uint32_t *__restrict__ err, int32_t *__restrict__ end_h,
     Scoring sc) {
     static_assert(K == 1 || K == 2 || K == 4, "4 cells per code word");
-    static_assert(!kSplit || (kCodes == kCodesWalk && K <= 2), "the coder wave builds walk codes");
     constexpr int S = 4 / K;   // stripes per 256-column chunk (work item)
     constexpr int W = 64 * K;  // stripe width (4 / K rows per code word)
     const int lane = (int)(threadIdx.x & 63u);
@@ -1769,82 +1753,7 @@ __global__ __launch_bounds__(kSplit ? 128 : 64) void nw_fill_rows_kernel(
     const uint32_t k_end = jend % K;
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the query chars
     uint32_t sg[8][4];  // sign words of the current code word's four cells
-    constexpr bool kCodesHere = kCodes != kCodesNone && !kSplit;  // this wave builds codes
-    __shared__ typename std::conditional<kSplit, RowRing<K>, int>::type ring_lds;
-    RowRing<K> *ring = reinterpret_cast<RowRing<K> *>(&ring_lds);
-    (void)ring;
-    uint32_t gbuf = 0;  // kSplit: the ring half of the current group
-    // kSplit: LDS writes done, then meet the other wave (no fence: a
-    // __syncthreads would wait for this wave's boundary stores and prefetch)
-    auto ring_barrier = [&]() __attribute__((always_inline)) {
-        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" : : : "memory");
-        gbuf ^= 1u;
-    };
-    if constexpr (kSplit) {
-        if (threadIdx.x >= 64) {  // the coder wave: one ring group per barrier
-            const int32_t kOp = kOpen;
-            auto code_rows = [&](uint32_t r0, uint32_t nrows, auto m_c) __attribute__((always_inline)) {
-                constexpr bool kM = decltype(m_c)::value;
-                constexpr uint32_t R = 4 / K;  // rows per code word
-#pragma unroll
-                for (uint32_t w0 = 0; w0 < kRowsGrp; w0 += R) {
-                    if (w0 >= nrows) break;
-                    uint32_t cs[8][4];
-#pragma unroll
-                    for (uint32_t u = 0; u < R; ++u) {
-                        const uint32_t q = w0 + u;
-                        const uint32_t r = r0 + q;
-                        int32_t Mv[K], Ic[K], Dc[K];
-                        if constexpr (K == 1) {
-                            const int2 mi = ring->mi[gbuf][q][lane];
-                            Mv[0] = mi.x; Ic[0] = mi.y;
-                            Dc[0] = ring->d[gbuf][q][lane];
-                        } else {
-                            const int4 mi = ring->mi[gbuf][q][lane];
-                            const int2 dd = ring->d[gbuf][q][lane];
-                            Mv[0] = mi.x; Mv[1] = mi.y; Ic[0] = mi.z; Ic[1] = mi.w;
-                            Dc[0] = dd.x; Dc[1] = dd.y;
-                        }
-                        const int32_t hm = (kM && r == ld) ? ~3 : ~1;
-#pragma unroll
-                        for (int k = 0; k < K; ++k) {
-                            const int32_t H = max(Mv[k], max(Ic[k], Dc[k]));
-                            const int32_t Hc = H & hm;
-                            const int32_t tOr = (Mv[k] + kOp) | 1;
-                            const int e = (int)u * K + k;
-                            cs[0][e] = kM ? (uint32_t)(Mv[k] - Hc) : 0u;
-                            cs[1][e] = (uint32_t)(Ic[k] - Hc);
-                            cs[2][e] = (uint32_t)(Dc[k] - Hc);
-                            cs[3][e] = cs[5][e] = cs[7][e] = 0u;
-                            cs[4][e] = (uint32_t)(tOr - Ic[k]);
-                            cs[6][e] = (uint32_t)(tOr - Dc[k]);
-                        }
-                    }
-                    const uint32_t wv = stripe_code_word<kCodesWalk, kM, false>(cs);
-                    const uint32_t n = nrows - w0;
-                    uint8_t *a = mrow + (uint64_t)(r0 + w0 - 1) * 256;
-                    if constexpr (K == 2) {
-                        *reinterpret_cast<uint16_t *>(a) = (uint16_t)wv;
-                        if (n > 1) *reinterpret_cast<uint16_t *>(a + 256) = (uint16_t)(wv >> 16);
-                    } else {
-                        a[0] = (uint8_t)wv;
-                        if (n > 1) a[256] = (uint8_t)(wv >> 8);
-                        if (n > 2) a[512] = (uint8_t)(wv >> 16);
-                        if (n > 3) a[768] = (uint8_t)(wv >> 24);
-                    }
-                }
-            };
-            uint32_t r = 1;
-            for (; r + kRowsGrp - 1 < ld; r += kRowsGrp) {
-                asm volatile("s_barrier" : : : "memory");
-                code_rows(r, kRowsGrp, std::false_type{});
-                gbuf ^= 1u;
-            }
-            asm volatile("s_barrier" : : : "memory");
-            code_rows(r, ld - r + 1, std::true_type{});
-            return;
-        }
-    }
+    constexpr bool kCodesHere = kCodes != kCodesNone;
     // one row: r (1-based), its db char, the left boundary (H~(r, c0), I~
     // entering column c0+1) and u = its slot in the code word (compile time)
     // m: the row may be the last one (argM bits and the reference's tie
@@ -1887,13 +1796,11 @@ __global__ __launch_bounds__(kSplit ? 128 : 64) void nw_fill_rows_kernel(
         }
         const int32_t S_incl = wave_prefix_max(P[K - 1], fill);
         const int32_t Ein = max(__builtin_amdgcn_update_dpp(kNegInf, S_incl, 0x138, 0xf, 0xf, false), bI);
-        int32_t Iv[K];
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             const int32_t I = k == 0 ? Ein : max(Ein, P[k - 1]);
             const int32_t D = Dv[k];
             const int32_t H = max(M[k], max(I, D));
-            Iv[k] = I;
             if constexpr (kCodesHere) {
                 const int32_t Hc = H & hm;
                 const int32_t tOr = tO[k] | kTieOr;
@@ -1913,15 +1820,6 @@ __global__ __launch_bounds__(kSplit ? 128 : 64) void nw_fill_rows_kernel(
                 }
             }
             Hp[k] = H;
-        }
-        if constexpr (kSplit) {  // the row's cells to the coder wave
-            if constexpr (K == 1) {
-                ring->mi[gbuf][q][lane] = make_int2(M[0], Iv[0]);
-                ring->d[gbuf][q][lane] = Dv[0];
-            } else {
-                ring->mi[gbuf][q][lane] = make_int4(M[0], M[1], Iv[0], Iv[1]);
-                ring->d[gbuf][q][lane] = make_int2(Dv[0], Dv[1]);
-            }
         }
         hb_prev = bH;
         // (H~, I~) leaving the stripe's last column (lane 63's values)
@@ -2010,7 +1908,7 @@ __global__ __launch_bounds__(kSplit ? 128 : 64) void nw_fill_rows_kernel(
                 // kG mask stores and kG boundary stores followed the prefetch:
                 // with that many younger VMEM ops outstanding it has landed
                 // (GFX9 vmcnt retires in issue order)
-                if constexpr (kCodes == kCodesNone || kSplit) {  // no mask stores in this wave
+                if constexpr (kCodes == kCodesNone) {  // no mask stores
                     if constexpr (kG == 8) asm volatile("s_waitcnt vmcnt(8)" : "+v"(nv) : : "memory");
                     else asm volatile("s_waitcnt vmcnt(4)" : "+v"(nv) : : "memory");
                 } else {
@@ -2126,7 +2024,6 @@ __global__ __launch_bounds__(kSplit ? 128 : 64) void nw_fill_rows_kernel(
                 quad(r, o0, M0, nofill, std::true_type{});
                 if constexpr (kG == 8) quad(r + 4, o4, M0, nofill, std::true_type{});
             }
-            if constexpr (kSplit) ring_barrier();
         }
         // the last group: 1 .. kG rows, row ld among them
         group(r, std::false_type{});
@@ -2145,7 +2042,6 @@ __global__ __launch_bounds__(kSplit ? 128 : 64) void nw_fill_rows_kernel(
         } else {
             quad(r, o0, M1, nofill, std::true_type{});
         }
-        if constexpr (kSplit) ring_barrier();
     };
     if (g == 0) rows(std::true_type{});
     else rows(std::false_type{});
@@ -2988,23 +2884,9 @@ hipError_t launch_fill_stripes(const NwPairDesc *pairs, const uint2 *work, uint3
     const bool pk = layout == 1;
     if (layout == 2) {  // row-synchronous stripes of 64 * rows_k columns
         const int32_t pm = 4 * (sc.match - sc.mismatch);
-        // walk codes: a coder wave per stripe (kSplit); SALN_ROWS_SPLIT=0 / 1
-        static const int split_env = [] {
-            const char *e = std::getenv("SALN_ROWS_SPLIT");
-            return e ? (e[0] == '1' ? 1 : 0) : 0;
-        }();
         auto go = [&](auto k_c, auto codes_c, auto minpen_c) {
             constexpr int kK = decltype(k_c)::value;
-            constexpr int kC = decltype(codes_c)::value;
-            if constexpr (kC == kCodesWalk && kK <= 2) {
-                if (split_env == 1) {
-                    nw_fill_rows_kernel<kK, kC, decltype(minpen_c)::value, true>
-                        <<<dim3(n_work * (4 / kK)), dim3(128), 0, stream>>>(
-                            pairs, work, qs, ds, mask, scratch, err, end_h, sc);
-                    return;
-                }
-            }
-            nw_fill_rows_kernel<kK, kC, decltype(minpen_c)::value>
+            nw_fill_rows_kernel<kK, decltype(codes_c)::value, decltype(minpen_c)::value>
                 <<<dim3(n_work * (4 / kK)), block, 0, stream>>>(pairs, work, qs, ds, mask, scratch,
                                                                err, end_h, sc);
         };

@@ -45,28 +45,25 @@ def rows_kernels():
     funcs = isa_check.load_functions(OBJ)
     out = {}
     for name, insns in funcs.items():
-        m = re.search(r"nw_fill_rows_kernelILi(\d)ELi(\d)ELb(\d)ELb(\d)E", name)
+        m = re.search(r"nw_fill_rows_kernelILi(\d)ELi(\d)ELb(\d)E", name)
         if m:
-            out[tuple(int(m.group(i)) for i in range(1, 5))] = insns
+            out[tuple(int(m.group(i)) for i in range(1, 4))] = insns
     return out
 
 
-# (K, codes, minpen, split): every plain instantiation, and the split (coder
-# wave) ones: walk codes, K = 1 and 2
-KEYS = [(k, c, p, 0) for k in (1, 2, 4) for c in (0, 1, 2) for p in (0, 1)] + \
-       [(k, 0, p, 1) for k in (1, 2) for p in (0, 1)]
+# (K, codes, minpen): every instantiation
+KEYS = [(k, c, p) for k in (1, 2, 4) for c in (0, 1, 2) for p in (0, 1)]
 
 
 def test_all_row_fill_instantiations_present(rows_kernels):
     assert set(rows_kernels) == set(KEYS)
 
 
-@pytest.mark.parametrize("key", KEYS, ids=lambda k: f"K{k[0]}_codes{k[1]}_minpen{k[2]}_split{k[3]}")
+@pytest.mark.parametrize("key", KEYS, ids=lambda k: f"K{k[0]}_codes{k[1]}_minpen{k[2]}")
 def test_prefetch_counted_wait_exact(rows_kernels, key):
     import isa_check
     insns = rows_kernels[key]
-    # boundary stores only: score-only, or the recurrence wave of a split stripe
-    expect = 8 if key[1] == 2 or key[3] else 16
+    expect = 8 if key[1] == 2 else 16  # kCodesNone: boundary stores only
     reps = isa_check.check_function(
         insns, pick=lambda i: i.op == "global_load_dwordx2" and i.args.rstrip().endswith("sc1"))
     assert reps, "no sc1 boundary loads found"
