@@ -247,3 +247,45 @@ def test_sharded_all_vs_all_without_process_group():
             assert sc[di, qi] == o.score and (st[di, qi] == 2) == o.panics
     ls, lst = s.lookup([3, 0, 2], [2, 1, 0])
     assert ls.tolist() == [sc[3, 2], sc[0, 1], sc[2, 0]]
+
+
+def _nccl_worker(port, queries, dbs, out):
+    import torch
+    import torch.distributed as dist
+
+    from sequencealigning_amd.dist import nw_align_sharded, nw_score_all_vs_all_sharded
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    assert dist.get_backend() == "nccl"
+    sc, st = nw_score_all_vs_all_sharded(queries, dbs, device=0)
+    res, cig = nw_align_sharded(queries, dbs, device=0)
+    out.put((sc, st, res["score"].copy(), res["status"].copy(), cig))
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_rccl_backend_single_rank():
+    """The nccl (= RCCL on ROCm) backend path of the multi-GPU drivers, one
+    rank on the box's GPU: ShardedAllVsAll's device-buffer gather and status
+    all-reduce, and nw_align_sharded's gather_records (all_gather of the
+    sizes, gather of the records) all run through RCCL, and the results equal
+    the single-process engine's."""
+    import sequencealigning_amd as saln
+    from nw_check import rand_seq
+    rng = np.random.default_rng(22)
+    queries = [rand_seq(rng, int(n)) for n in rng.integers(100, 161, 23)] + [b"ACGT" * 300]
+    dbs = [rand_seq(rng, int(n)) for n in rng.integers(100, 161, 31)] + [b""]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_nccl_worker, args=(_free_port(), queries, dbs, q))
+    p.start()
+    sc, st, rs, rt, cig = q.get(timeout=300)
+    p.join(timeout=120)
+    assert p.exitcode == 0
+    want_s, want_st = saln.nw_score_all_vs_all(queries, dbs)
+    assert np.array_equal(sc, want_s) and np.array_equal(st, want_st)
+    res, want_cig = saln.nw_align_batch(queries, dbs)
+    assert np.array_equal(rs, res["score"]) and np.array_equal(rt, res["status"])
+    assert cig == want_cig
