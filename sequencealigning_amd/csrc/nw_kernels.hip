@@ -1362,7 +1362,7 @@ __global__ __launch_bounds__(256) void nw_fill_pk_kernel(Src src, uint32_t count
                                                          const uint8_t *__restrict__ qs,
                                                          const uint8_t *__restrict__ ds,
                                                          uint8_t *__restrict__ mask, Scoring sc,
-                                                         uint32_t ld_max) {
+                                                         uint32_t ld_max, bool sc_steady) {
     constexpr int GPB = 256 / G;
     constexpr Geom geo{G, K};
     extern __shared__ uint32_t drow[];  // [GPB][G + ld_max + G] packed db chars (dch) per row
@@ -1457,7 +1457,12 @@ __global__ __launch_bounds__(256) void nw_fill_pk_kernel(Src src, uint32_t count
     // two-step unroll swaps two arrays (no register rotation).
     uint32_t HpB[K];
 
-    auto step = [&](int t, uint32_t(&Hin)[K], uint32_t(&Hout)[K]) __attribute__((always_inline)) {
+    // kSteady (steps where every lane holds a row of both pairs below their
+    // last row): no per-lane activity test, no end cells, so the row result
+    // is computed straight into Hout (no copies through a divergent branch)
+    auto step = [&](int t, uint32_t(&Hin)[K], uint32_t(&Hout)[K], auto steady_c)
+                    __attribute__((always_inline)) {
+        constexpr bool kSteady = decltype(steady_c)::value;
         const int r = t - lane + 1;
         uint32_t dch;
         if constexpr (kRebase)  // [A, 0, B, 0] << 5
@@ -1484,7 +1489,7 @@ __global__ __launch_bounds__(256) void nw_fill_pk_kernel(Src src, uint32_t count
         const int32_t bH = hs_col0(sc, (uint32_t)rb) + alpha * rb - base;
         const uint32_t inF = gshift<G>(pkb(bF, bF), pubF, gstart);
         const uint32_t inH = gshift<G>(pkb(bH, bH), pubH, gstart);
-        if (r >= 1 && r <= ldM) {
+        if (kSteady || (r >= 1 && r <= ldM)) {
             uint32_t F = inF;
             PkMask<KS> wa[NS], wb[NS];
             // code words of column pairs: bytes [A_2c, B_2c, A_2c+1, B_2c+1]
@@ -1546,7 +1551,9 @@ __global__ __launch_bounds__(256) void nw_fill_pk_kernel(Src src, uint32_t count
                 Hout[k] = H;
             }
             };
-            if constexpr (kCodes == kCodesWalk) {
+            if constexpr (kCodes == kCodesWalk && kSteady) {
+                columns(std::false_type{});
+            } else if constexpr (kCodes == kCodesWalk) {
                 const bool endcell = t == tEA || t == tEB;
                 if (__builtin_amdgcn_ballot_w64(endcell))
                     columns(std::true_type{});
@@ -1582,14 +1589,14 @@ __global__ __launch_bounds__(256) void nw_fill_pk_kernel(Src src, uint32_t count
                         *reinterpret_cast<PkMask<KS> *>(mB + (uint64_t)sg * pb.mask_bs) = wb[sg];
                 }
             }
-            if (t == tEA) {
+            if (!kSteady && t == tEA) {
                 int32_t e = 0;
 #pragma unroll
                 for (int k = 0; k < K; ++k)
                     if (k == kA) e = (int32_t)(Hout[k] & 0xFFFFu) - 32768;
                 src.end(ia, pa, e + base - alpha * ldA - beta * lqA);
             }
-            if (t == tEB) {
+            if (!kSteady && t == tEB) {
                 int32_t e = 0;
 #pragma unroll
                 for (int k = 0; k < K; ++k)
@@ -1603,12 +1610,27 @@ __global__ __launch_bounds__(256) void nw_fill_pk_kernel(Src src, uint32_t count
         mA += pa.mask_rs;
         mB += pb.mask_rs;
     };
+    // steps [tS0, tS1) are steady: every lane at a row in [1, min(ldA, ldB) - 1]
+    // (bounds even: the ping-pong pairs keep their parity)
+    const std::false_type G0;
+    const std::true_type S1;
+    const int ldm = ldA < (hasB ? ldB : ldA) ? ldA : (hasB ? ldB : ldA);
+    const int tS0 = min((G + 1) & ~1, T & ~1);
+    const int tS1 = sc_steady ? max(tS0, tS0 + ((ldm - 1 - tS0) & ~1) * (ldm - 1 > tS0 ? 1 : 0)) : tS0;
     int t = 0;
-    for (; t + 1 < T; t += 2) {
-        step(t, Hp, HpB);
-        step(t + 1, HpB, Hp);
+    for (; t < tS0; t += 2) {
+        step(t, Hp, HpB, G0);
+        step(t + 1, HpB, Hp, G0);
     }
-    if (t < T) step(t, Hp, HpB);
+    for (; t < tS1; t += 2) {
+        step(t, Hp, HpB, S1);
+        step(t + 1, HpB, Hp, S1);
+    }
+    for (; t + 1 < T; t += 2) {
+        step(t, Hp, HpB, G0);
+        step(t + 1, HpB, Hp, G0);
+    }
+    if (t < T) step(t, Hp, HpB, G0);
 }
 
 // Column-stripe fill (declared with the stripe protocol above), i32 lanes.
@@ -2554,6 +2576,16 @@ constexpr bool kPacked[kNumVariants] = {false, false, false, false, true, true, 
 // halve the occupancy.)
 constexpr uint32_t kFillG[kNumVariants] = {16, 16, 64, 64, 8, 16, 32, 16, 64};
 
+// The packed fill's steady-state steps (nw_fill_pk_kernel kSteady);
+// SALN_PK_STEADY=0 turns them off (A/B switch, same results)
+static bool pk_steady() {
+    static const bool on = [] {
+        const char *e = std::getenv("SALN_PK_STEADY");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
 // Dynamic LDS cap of the packed fill's staged db rows: two workgroups per CU.
 constexpr size_t kPackedLdsMax = 80 * 1024;
 static bool packed_ok(uint32_t lq, uint32_t ld, const Scoring &sc);
@@ -2605,7 +2637,7 @@ static hipError_t fill_pk(dim3 grid, hipStream_t s, const NwPairDesc *pairs, uin
                                                      (int)kPackedLdsMax);
             if (e != hipSuccess) return e;
         }
-        kern<<<grid, dim3(256), lds, s>>>(src, count, qs, ds, mask, sc, ld_max);
+        kern<<<grid, dim3(256), lds, s>>>(src, count, qs, ds, mask, sc, ld_max, pk_steady());
         return hipSuccess;
     };
     auto by_codes = [&](auto rebase_c) {
@@ -2669,7 +2701,7 @@ static hipError_t avsa_pk(const AvsaSrc &src, uint32_t count, const uint8_t *qs,
                                                      (int)kPackedLdsMax);
             if (e != hipSuccess) return e;
         }
-        kern<<<grid, dim3(256), lds, s>>>(src, count, qs, ds, nullptr, sc, ld_max);
+        kern<<<grid, dim3(256), lds, s>>>(src, count, qs, ds, nullptr, sc, ld_max, pk_steady());
         return hipSuccess;
     };
     return rebase ? go(std::true_type{}) : go(std::false_type{});
