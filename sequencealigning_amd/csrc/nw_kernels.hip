@@ -1460,12 +1460,21 @@ __global__ __launch_bounds__(256) void nw_fill_pk_kernel(Src src, uint32_t count
     // kSteady (steps where every lane holds a row of both pairs below their
     // last row): no per-lane activity test, no end cells, so the row result
     // is computed straight into Hout (no copies through a divergent branch)
-    auto step = [&](int t, uint32_t(&Hin)[K], uint32_t(&Hout)[K], auto steady_c)
+    // Steady steps of the single-frame fill also take their row's db word
+    // from the caller (read a step ahead) and the group-start inputs from
+    // running packed values (the boundary column is linear inside the pair's
+    // rows: sentinel-free), advanced by one row's drift per step.
+    uint32_t sF = 0, sH = 0;
+    const uint32_t kRowAdd = cst2(drift);
+    auto step = [&](int t, uint32_t(&Hin)[K], uint32_t(&Hout)[K], auto steady_c, uint32_t dch_in)
                     __attribute__((always_inline)) {
         constexpr bool kSteady = decltype(steady_c)::value;
+        constexpr bool kRun = kSteady && !kRebase;  // running inputs, prefetched db word
         const int r = t - lane + 1;
         uint32_t dch;
-        if constexpr (kRebase)  // [A, 0, B, 0] << 5
+        if constexpr (kRun)
+            dch = dch_in;
+        else if constexpr (kRebase)  // [A, 0, B, 0] << 5
             dch = __builtin_amdgcn_perm(0u, (uint32_t)rowp16[t], 0x0C010C00u) << 5;
         else
             dch = rowp[t];
@@ -1485,10 +1494,20 @@ __global__ __launch_bounds__(256) void nw_fill_pk_kernel(Src src, uint32_t count
         }
         // group-start inputs for row t+1: I~(r,1) and H~(r,0) (same for A and B)
         const int32_t rb = t + 1;
-        const int32_t bF = is_col1(sc, (uint32_t)rb) + alpha * rb + beta - base;
-        const int32_t bH = hs_col0(sc, (uint32_t)rb) + alpha * rb - base;
-        const uint32_t inF = gshift<G>(pkb(bF, bF), pubF, gstart);
-        const uint32_t inH = gshift<G>(pkb(bH, bH), pubH, gstart);
+        uint32_t gF, gH;
+        if constexpr (kRun) {
+            gF = sF;
+            gH = sH;
+            sF += kRowAdd;
+            sH += kRowAdd;
+        } else {
+            const int32_t bF = is_col1(sc, (uint32_t)rb) + alpha * rb + beta - base;
+            const int32_t bH = hs_col0(sc, (uint32_t)rb) + alpha * rb - base;
+            gF = pkb(bF, bF);
+            gH = pkb(bH, bH);
+        }
+        const uint32_t inF = gshift<G>(gF, pubF, gstart);
+        const uint32_t inH = gshift<G>(gH, pubH, gstart);
         if (kSteady || (r >= 1 && r <= ldM)) {
             uint32_t F = inF;
             PkMask<KS> wa[NS], wb[NS];
@@ -1578,12 +1597,13 @@ __global__ __launch_bounds__(256) void nw_fill_pk_kernel(Src src, uint32_t count
                         wb[sg].w[w] = __builtin_amdgcn_perm(hi, lo, 0x07050301u);
                     }
                 }
-                if (r <= ldAs) {
+                // (steady: r < min(ldA, ldB), so only the lane's columns decide)
+                if (kSteady ? ldAs != 0 : r <= ldAs) {
 #pragma unroll
                     for (int sg = 0; sg < NS; ++sg)
                         *reinterpret_cast<PkMask<KS> *>(mA + (uint64_t)sg * pa.mask_bs) = wa[sg];
                 }
-                if (r <= ldBs) {
+                if (kSteady ? ldBs != 0 : r <= ldBs) {
 #pragma unroll
                     for (int sg = 0; sg < NS; ++sg)
                         *reinterpret_cast<PkMask<KS> *>(mB + (uint64_t)sg * pb.mask_bs) = wb[sg];
@@ -1619,18 +1639,30 @@ __global__ __launch_bounds__(256) void nw_fill_pk_kernel(Src src, uint32_t count
     const int tS1 = sc_steady ? max(tS0, tS0 + ((ldm - 1 - tS0) & ~1) * (ldm - 1 > tS0 ? 1 : 0)) : tS0;
     int t = 0;
     for (; t < tS0; t += 2) {
-        step(t, Hp, HpB, G0);
-        step(t + 1, HpB, Hp, G0);
+        step(t, Hp, HpB, G0, 0u);
+        step(t + 1, HpB, Hp, G0, 0u);
     }
-    for (; t < tS1; t += 2) {
-        step(t, Hp, HpB, S1);
-        step(t + 1, HpB, Hp, S1);
+    if (tS1 > tS0) {
+        if constexpr (!kRebase) {
+            const int32_t rb = tS0 + 1;
+            const int32_t bF = is_col1(sc, (uint32_t)rb) + alpha * rb + beta;
+            const int32_t bH = hs_col0(sc, (uint32_t)rb) + alpha * rb;
+            sF = pkb(bF, bF);
+            sH = pkb(bH, bH);
+        }
+        uint32_t d0 = kRebase ? 0u : rowp[t];
+        for (; t < tS1; t += 2) {
+            const uint32_t d1 = kRebase ? 0u : rowp[t + 1];
+            step(t, Hp, HpB, S1, d0);
+            d0 = kRebase ? 0u : rowp[t + 2];
+            step(t + 1, HpB, Hp, S1, d1);
+        }
     }
     for (; t + 1 < T; t += 2) {
-        step(t, Hp, HpB, G0);
-        step(t + 1, HpB, Hp, G0);
+        step(t, Hp, HpB, G0, 0u);
+        step(t + 1, HpB, Hp, G0, 0u);
     }
-    if (t < T) step(t, Hp, HpB, G0);
+    if (t < T) step(t, Hp, HpB, G0, 0u);
 }
 
 // Column-stripe fill (declared with the stripe protocol above), i32 lanes.
