@@ -1247,13 +1247,12 @@ __device__ __forceinline__ uint32_t col_pair_signs(uint32_t hi, uint32_t lo) {
     return __builtin_amdgcn_perm(hi, lo, 0x0B0A0908u);
 }
 
-// (m & a) | (~m & b) as one v_bfi_b32 (written out, the compiler turns a
-// chain of these into an and per source plus or3s).  m: a loop-invariant
-// constant, kept in an SGPR.
+// (m & a) | (~m & b) as one v_bitop3_b32 (truth table 0xCA over m, a, b).
+// Written as the gfx950 builtin: plain C makes the compiler turn a chain of
+// these into an and per source plus or3s, and inline asm (round 2) made it
+// pad dependent ops with s_nop (it cannot see an asm instruction's hazards).
 __device__ __forceinline__ uint32_t bfi(uint32_t m, uint32_t a, uint32_t b) {
-    uint32_t r;
-    asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "s"(m), "v"(a), "v"(b));
-    return r;
+    return __builtin_amdgcn_bitop3_b32(m, a, b, 0xCA);
 }
 
 // Merge the sign-byte words of the code sources (bit t of every cell byte

@@ -1,0 +1,53 @@
+"""A/B timing harness for the configs[1] step (tools only, never the bench):
+the same plan / execute / hipEvent timing as bench.py's headline loop, for
+the library SALN_LIB names (an experiment build) or the in-tree one.
+
+    SALN_LIB=... python tools/ab_c2.py [--steps 40] [--warmup 5] [--tag name]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--steps", type=int, default=40)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--pairs", type=int, default=100_000)
+    ap.add_argument("--tag", default="")
+    a = ap.parse_args()
+    import torch
+    import sequencealigning_amd as saln
+    from sequencealigning_amd import _lib, synth
+    n, L = a.pairs, 150
+    qs, qo, ds, do = synth.iid_pairs(n, L, L, seed=0x5EED0002)
+    plan = saln.NwPlan(qo, do, pairs=np.stack([np.arange(n)] * 2, 1))
+    dq, dd = torch.from_numpy(qs).cuda(), torch.from_numpy(ds).cuda()
+    res = torch.zeros(n * 4, dtype=torch.int32, device="cuda")
+    cig = torch.zeros(max(1, plan.cigar_words), dtype=torch.int32, device="cuda")
+    for _ in range(a.warmup):
+        plan.execute(dq, dd, res, cig)
+    torch.cuda.synchronize()
+    plan.set_timing(True)
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        plan.execute(dq, dd, res, cig)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / a.steps
+    plan.check()
+    f, fn = plan.kernel_time("nw_fill")
+    tb, tn = plan.kernel_time("nw_traceback")
+    print(json.dumps({"tag": a.tag, "lib": os.path.basename(_lib.LIB_PATH),
+                      "gcups": round(plan.cells / dt / 1e9, 1), "ms_per_step": round(dt * 1e3, 4),
+                      "fill_ms": round(f / fn, 4), "traceback_ms": round(tb / tn, 4)}))
+
+
+if __name__ == "__main__":
+    main()
