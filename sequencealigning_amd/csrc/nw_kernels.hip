@@ -208,9 +208,9 @@ __device__ __forceinline__ void walk_pair(const NwPairDesc &p, int32_t hend,
     results[p.pair_id] = make_result(hend, w, es);
 }
 
-// LDS-window walker (segments of <= 16 bytes, i.e. K <= 16).  Lock-step
-// phases: every lane of the wave is in the same window phase S (0..W-1) with
-// its target row == base - S (phases unrolled).  The windows live in LDS, filled by LDS-DMA (global_load_lds_dwordx{3,4}:
+// LDS-window walker (walk_pack_lds; segments of <= 16 bytes, i.e. K <= 16).
+// Lock-step phases: every lane of the wave is in the same window phase S
+// (0..W-1) with its target row == base - S (phases unrolled).  The windows live in LDS, filled by LDS-DMA (global_load_lds_dwordx{3,4}:
 // lane l's bytes land at slot base + 16*l; the slot base is wave-uniform
 // because all lanes are in the same phase).  Block b lives in window b % NW
 // (WalkGeo); at the end of phase S every lane refills slot S of every window
@@ -221,8 +221,8 @@ __device__ __forceinline__ void walk_pair(const NwPairDesc &p, int32_t hend,
 // back to a synchronous load.
 // Decisions are table lookups on the raw code byte: three bits at a
 // state-dependent offset index kNextLut (no branches on the state).  The
-// walk records 3-bit ops (state | eq << 2, ten per word) and stores a word
-// once it is complete, at a phase end, before the DMAs; the CIGAR (forward
+// walk records 3-bit ops (state | eq << 2, ten per word) and stores complete
+// words at phase ends, before the DMAs; the CIGAR (forward
 // order, run-length words) is produced from that stream after the walk.
 // Exactly NW DMAs per phase (the init issues the same group per slot) keep
 // >= NW*(W-1) younger VMEM operations behind any slot a phase reads, so the
@@ -254,30 +254,12 @@ struct WalkGeo {
     static constexpr uint32_t kWinBytes = W * kSlotBytes;    // one window of a wave
     static constexpr uint32_t kWaveLds = NW * kWinBytes;
     static constexpr uint32_t kVmcnt = NW * (W - 1);
-    // segments wider than a 16-byte slot (K = 19: 20 bytes): a slot holds
-    // bytes [off, off + 16) of its segment, off = 0 or 4 per (window, slot)
-    static constexpr bool kWide = LB > 16;
-    static_assert(LB <= 20, "LDS window slots hold 16 bytes of a segment of at most 20");
+    static_assert(LB <= 16, "LDS window slots hold 16 bytes per lane");
 };
 
 typedef __attribute__((address_space(3))) uint8_t lds_u8;
 
 __device__ __forceinline__ uint32_t lds_off(const lds_u8 *p) { return (uint32_t)(uintptr_t)p; }
-
-// Raw code byte (bits 0-6 stored inverted: 1 = parent absent; bit 7 = eq),
-// once at most N younger VMEM operations are outstanding.
-template <uint32_t N>
-__device__ __forceinline__ uint32_t window_raw(uint32_t addr) {
-    static_assert(N == 6 || N == 14, "add the immediate below");
-    uint32_t v;
-    if constexpr (N == 6)
-        asm volatile("s_waitcnt vmcnt(6)\n\tds_read_u8 %0, %1\n\ts_waitcnt lgkmcnt(0)"
-                     : "=v"(v) : "v"(addr) : "memory");
-    else
-        asm volatile("s_waitcnt vmcnt(14)\n\tds_read_u8 %0, %1\n\ts_waitcnt lgkmcnt(0)"
-                     : "=v"(v) : "v"(addr) : "memory");
-    return v;
-}
 
 // A store the compiler can neither merge nor drop: the walker's vmcnt
 // arithmetic counts every one of them.
@@ -304,218 +286,244 @@ __host__ __device__ constexpr uint64_t make_next_lut() {
 }
 constexpr uint64_t kNextLut = make_next_lut();
 
-#ifdef SALN_WALK_PROF
-// profiling build: shader-clock time in the window waits / sync loads
-#define SALN_PROF_T() __builtin_amdgcn_s_memtime()
-#else
-#define SALN_PROF_T() 0ull
-#endif
+// One 16-byte read of the lane's slot (the segment of its block at the
+// phase's row), once at most N younger VMEM operations are outstanding.
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+template <uint32_t N>
+__device__ __forceinline__ u32x4 window_seg(uint32_t addr) {
+    static_assert(N == 6 || N == 14, "add the immediate below");
+    u32x4 v;
+    if constexpr (N == 6)
+        asm volatile("s_waitcnt vmcnt(6)\n\tds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)"
+                     : "=v"(v) : "v"(addr) : "memory");
+    else
+        asm volatile("s_waitcnt vmcnt(14)\n\tds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)"
+                     : "=v"(v) : "v"(addr) : "memory");
+    return v;
+}
 
-#ifdef SALN_WALK_CHECK
-// debug build: compare every window read with the byte in HBM
-#define SALN_WALK_CHECK_HOOK(S)                                                          \
-    {                                                                                    \
-        const uint32_t tru = (uint32_t)m[geo.cell(ti, tj, rs, bs, p.mask_cs)];                     \
-        if (tru != raw) {                                                                \
-            const uint32_t par = wc;                                                     \
-            if (!dbg_n) dbg_info = (S) | (par << 3) | (((valid >> (par * 8u + (S))) & 1u) << 5) | \
-                                   ((ti & 0xFFFu) << 8) | ((tj & 0xFFFu) << 20);          \
-            ++dbg_n;                                                                     \
-            raw = tru;                                                                   \
-        }                                                                                \
-    }
-#else
-#define SALN_WALK_CHECK_HOOK(S)
-#endif
-
+// The walk (round 3: one iteration per row, and a shorter instruction stream
+// than the round-2 walker; the windows, refills and counted waits are kept).  A
+// wave iterates while any of its 64 lanes is still in the row, and an I step
+// (a gap in the query: a move left) keeps a lane in its row, so the wave
+// used to run ~2.8 iterations per row for ~1.05 per lane (PMC: 441 LDS reads
+// per wave for ~157 rows).  Here an iteration reads the lane's whole segment
+// (ds_read_b128) and, after the cell step of an M / D / end-cell state, walks
+// an I run to its end within the block at once: the I-open bits of the
+// segment's bytes (bit 4, stored inverted) are gathered into a mask whose
+// highest set bit at or left of the lane's column is the cell where the run
+// opens (at most nine cells per iteration, so the ops fit the accumulator).
+// Only a run that leaves the block takes another iteration.
+// - addresses are 64-bit lane pointers updated by adds: the row pointer of
+//   the phase (one subtract per phase) and the block offsets held by window
+//   0 / 1 (a crossing recomputes only the one it hands to block B-2);
+// - the op stream is a 64-bit accumulator (stored 30 bits = ten ops at a time).
 template <int G, int K>
-__device__ void walk_pair_lds(const NwPairDesc &p, int32_t hend, const uint8_t *__restrict__ mask,
+__device__ void walk_pack_lds(const NwPairDesc &p, int32_t hend, const uint8_t *__restrict__ mask,
                               uint32_t *__restrict__ ops_all, saln_nw_result *__restrict__ results,
                               uint32_t *__restrict__ cigar, Scoring sc, lds_u8 *win) {
     using WG = WalkGeo<K>;
+    static_assert(WG::NW == 2, "two windows: blocks B and B-1");
     constexpr Geom geo{G, K};
-    constexpr uint32_t NW = WG::NW, kW = WG::W;
-    constexpr uint32_t kAll = (1u << (8 * NW)) - 1u;
-    const uint64_t rs = p.mask_rs;
+    constexpr uint32_t kW = WG::W;
+    constexpr uint32_t kWin = WG::kWinBytes, kSlot = WG::kSlotBytes;
+    constexpr uint64_t kMask30 = (1u << 30) - 1u;
+    const uint64_t rs = p.mask_rs, cs = p.mask_cs;
     const uint32_t bs = p.mask_bs;
     const uint8_t *__restrict__ m = mask + p.mask_off;
     uint32_t *out = cigar ? cigar + p.cigar_off : nullptr;
     uint32_t *const ops = ops_all + p.ops_off;
-    // op stream: `cur` = word wi (sh3/3 ops so far); `full` = word wi-1 while not yet stored
-    uint32_t wi = 0, sh3 = 0, cur = 0, full = 0, hf = 0;  // hf: `full` pending
+    // block b's segment at row 1, relative to m
+    auto boff = [&](uint32_t b) __attribute__((always_inline)) {
+        return (uint64_t)(b / G) * cs + (uint64_t)((b % G) * bs);
+    };
+    uint64_t acc = 0;        // pending 3-bit ops (state | eq << 2), oldest lowest
+    uint32_t sh = 0, wi = 0; // acc's bit count; op words stored
     uint32_t ti = p.len_db, tj = p.len_q;
-    uint32_t st = 3, lsh = 0;  // state (3 = at the end cell) and its code-bit offset
+    uint32_t sidx = 3u * 16u, lsh = 0;  // kNextLut row of the state (3: end cell), its bits
     uint32_t walking = 1;
-    uint32_t B = (tj - 1) / K, base = ti;
-    uint32_t col = (tj - 1) % K;  // target column inside block B
-    uint32_t wc = B % NW;         // window of block B (block b lives in window b % NW)
-    uint32_t valid = kAll;        // bit 8w+s: slot s of window w holds its block
-    // kWide: bit 8w+s set = slot s of window w holds bytes [4, 20) of its
-    // segment (the lane was at a column >= 16 of block B when it was loaded,
-    // or the window held block B-1, entered at its last column); else [0, 16)
-    uint32_t woff = 0;
+    uint32_t B = (tj - 1) / K, col = (tj - 1) % K;
+    uint32_t wc = B & 1u;    // window of block B; window wc ^ 1 holds B - 1
+    uint32_t valid = 0xFFFFu;  // bit 8w + s: slot s of window w holds its assigned block
+    const uint64_t ob = boff(B), ob1 = boff(B >= 1 ? B - 1 : 0);
+    uint64_t ow0 = wc ? ob1 : ob, ow1 = wc ? ob : ob1;  // block offsets of windows 0 / 1
     const uint32_t wbase = lds_off(win) + (threadIdx.x & 63u) * 16u;
-    uint32_t wrow = 0;            // LDS address of (window wc, slot S, my lane)
-    uint64_t p_twait = 0, p_tsync = 0, p_t0 = SALN_PROF_T();
-    uint32_t p_iter = 0, p_sync = 0;
-    (void)p_twait, (void)p_tsync, (void)p_t0, (void)p_iter, (void)p_sync;
-#ifdef SALN_WALK_CHECK
-    uint32_t dbg_n = 0, dbg_info = 0;
-#endif
-    // per-block segment bases for B, B-1, B-2
-    auto blk_base = [&](uint32_t blk) __attribute__((always_inline)) {
-        return m + (uint64_t)(blk / G) * p.mask_cs + (uint64_t)(blk % G) * bs;
+    uint32_t wl = wbase + wc * kWin;  // my slot 0 in the current window
+    // the phase's row pointer (row ti at a phase start), W rows ahead for the refills
+    // (row counts on after the lane's walk ends; rows below 1 load row 1)
+    const uint8_t *rp = m + (uint64_t)(ti - 1) * rs;
+    int32_t row = (int32_t)ti;
+    const uint64_t rsW = (uint64_t)kW * rs;
+    auto dma = [&](auto win_c, auto slot_c, const uint8_t *a) __attribute__((always_inline)) {
+        constexpr uint32_t w = decltype(win_c)::value, s = decltype(slot_c)::value;
+        __builtin_amdgcn_global_load_lds(
+            a, (__attribute__((address_space(3))) void *)(win + w * kWin + s * kSlot), WG::SB, 0,
+            0);
     };
-    const uint8_t *bp0 = blk_base(B), *bp1 = blk_base(B >= 1 ? B - 1 : 0);
-    const uint8_t *bp2 = blk_base(B >= 2 ? B - 2 : 0);
-    (void)bp2;
-    // global address of a block's segment at `row` (clamped to >= 1)
-    auto seg = [&](const uint8_t *bp, int32_t row) __attribute__((always_inline)) {
-        return (const void *)(bp + (uint64_t)((uint32_t)max(row, 1) - 1) * rs);
+    auto refill = [&](auto slot_c, const uint8_t *row) __attribute__((always_inline)) {
+        dma(std::integral_constant<uint32_t, 0>{}, slot_c, row + ow0);
+        dma(std::integral_constant<uint32_t, 1>{}, slot_c, row + ow1);
     };
-#define SALN_ROW(S2, S) ((int32_t)((S2) >= (S) ? base - (S2) : base - (S2) - kW))
-#define SALN_DMA(WIN, SLOT, ADDR)                                                              \
-    __builtin_amdgcn_global_load_lds(                                                          \
-        ADDR, (__attribute__((address_space(3))) void *)(win + (WIN) * WG::kWinBytes +         \
-                                                         (SLOT) * WG::kSlotBytes),             \
-        WalkGeo<K>::SB, 0, 0)
-    // window w holds the resident block congruent to w (mod NW)
-#define SALN_REFILL(S, ROW)                                                                    \
-    {                                                                                          \
-        const void *a0 = seg(bp0, ROW), *a1 = seg(bp1, ROW);                                   \
-        if constexpr (WG::kWide) {                                                             \
-            const bool hi = col >= 16u;                                                        \
-            a0 = (const uint8_t *)a0 + (hi ? 4 : 0);                                           \
-            a1 = (const uint8_t *)a1 + 4;                                                      \
-            woff = (woff & ~(0x101u << (S))) | (1u << ((wc ^ 1u) * 8u + (S))) |                \
-                   ((hi ? 1u : 0u) << (wc * 8u + (S)));                                        \
-        }                                                                                      \
-        if constexpr (NW == 2) {                                                               \
-            SALN_DMA(0, S, wc ? a1 : a0);                                                      \
-            SALN_DMA(1, S, wc ? a0 : a1);                                                      \
-        } else {                                                                               \
-            const void *a2 = seg(bp2, ROW);                                                    \
-            /* window w gets block B - ((wc - w) mod 3) */                                     \
-            SALN_DMA(0, S, wc == 0 ? a0 : wc == 1 ? a1 : a2);                                  \
-            SALN_DMA(1, S, wc == 1 ? a0 : wc == 2 ? a1 : a2);                                  \
-            SALN_DMA(2, S, wc == 2 ? a0 : wc == 0 ? a1 : a2);                                  \
-        }                                                                                      \
-    }
-    // slot S of window wc not refreshed since a crossing: load it now.
-    // Independent ifs (not if/else): the compiler must not merge the calls
-    // into one DMA with a per-lane (then readfirstlane'd) LDS base.
-#define SALN_ENSURE(S, ECOL)                                                                   \
-    if (!(valid & (1u << (wc * 8u + (S))))) {                                                  \
-        const uint64_t tq0 = SALN_PROF_T();                                                    \
-        ++p_sync;                                                                              \
-        const void *ac = seg(bp0, (int32_t)(base - (S)));                                      \
-        if constexpr (WG::kWide) {                                                             \
-            const bool hi = (ECOL) >= 16u;                                                     \
-            ac = (const uint8_t *)ac + (hi ? 4 : 0);                                           \
-            woff = (woff & ~(1u << (wc * 8u + (S)))) | ((hi ? 1u : 0u) << (wc * 8u + (S)));    \
-        }                                                                                      \
-        if (wc == 0) { SALN_DMA(0, S, ac); }                                                   \
-        __builtin_amdgcn_sched_barrier(0);                                                     \
-        if (wc == 1) { SALN_DMA(1, S, ac); }                                                   \
-        if constexpr (NW == 3) {                                                               \
-            __builtin_amdgcn_sched_barrier(0);                                                 \
-            if (wc == 2) { SALN_DMA(2, S, ac); }                                               \
-        }                                                                                      \
-        asm volatile("s_waitcnt vmcnt(0)" : : : "memory");                                     \
-        valid |= 1u << (wc * 8u + (S));                                                        \
-        p_tsync += SALN_PROF_T() - tq0;                                                        \
-    }
-#define SALN_PHASE(S)                                                                          \
-    wrow = wbase + wc * WG::kWinBytes + (S) * WG::kSlotBytes;                                  \
-    if (walking) {                                                                             \
-        SALN_ENSURE(S, col)                                                                    \
-        for (;;) {                                                                             \
-            const uint64_t tw0 = SALN_PROF_T();                                                \
-            uint32_t raw;                                                                      \
-            if constexpr (WG::kWide) {                                                         \
-                const uint32_t off = (woff >> (wc * 8u + (S))) & 1u ? 4u : 0u;                 \
-                raw = window_raw<WG::kVmcnt>(wrow + col - (col >= off ? off : 0u));            \
-                if (col < off) /* left the slot's 16 bytes (a long gap): read HBM */           \
-                    raw = m[geo.cell(ti, tj, rs, bs, p.mask_cs)];                              \
-            } else {                                                                           \
-                raw = window_raw<WG::kVmcnt>(wrow + col);                                      \
-            }                                                                                  \
-            p_twait += SALN_PROF_T() - tw0;                                                    \
-            ++p_iter;                                                                          \
-            SALN_WALK_CHECK_HOOK(S)                                                            \
-            const uint32_t f3 = __builtin_amdgcn_ubfe(raw, lsh, 3);                            \
-            const uint32_t nx = (uint32_t)(kNextLut >> (f3 * 2u + st * 16u)) & 3u;             \
-            cur |= (nx | ((raw >> 5) & 4u)) << sh3;                                            \
-            sh3 += 3;                                                                          \
-            const bool wrap = sh3 == 3 * kOpsPerWord;                                          \
-            if (wrap && hf) counted_store(ops + wi - 1, full); /* > 10 ops in one row */      \
-            full = wrap ? cur : full;                                                          \
-            cur = wrap ? 0u : cur;                                                             \
-            sh3 = wrap ? 0u : sh3;                                                             \
-            wi += wrap ? 1u : 0u;                                                              \
-            hf = wrap ? 1u : hf;                                                               \
-            st = nx;                                                                           \
-            lsh = 2u * nx + 1u;                                                                \
-            const bool up = nx != kStI, left = nx != kStD;                                     \
-            ti -= up ? 1u : 0u;                                                                \
-            tj -= left ? 1u : 0u;                                                              \
-            const bool done = ti == 0 || tj == 0;                                              \
-            walking = done ? 0u : 1u;                                                          \
-            if (left && col == 0 && !done) { /* crossed into B-1; B's window gets B-NW */     \
-                valid &= ~(0xFFu << (wc * 8u));                                                \
-                --B;                                                                           \
-                wc = wc ? wc - 1u : NW - 1u;                                                   \
-                wrow = wbase + wc * WG::kWinBytes + (S) * WG::kSlotBytes;                      \
-                bp0 = bp1;                                                                     \
-                if constexpr (NW == 2) {                                                       \
-                    bp1 = blk_base(B >= 1 ? B - 1 : 0);                                        \
-                } else {                                                                       \
-                    bp1 = bp2;                                                                 \
-                    bp2 = blk_base(B >= 2 ? B - 2 : 0);                                        \
-                }                                                                              \
-                SALN_ENSURE(S, K - 1u) /* entered at the block's last column */               \
-            }                                                                                  \
-            col = left ? (col == 0 ? K - 1 : col - 1) : col;                                   \
-            if (up || done) break; /* up one row: next phase */                                \
-        }                                                                                      \
-    }                                                                                          \
-    /* the completed op word (if any), then exactly NW DMAs per phase */                       \
-    {                                                                                          \
-        const uint64_t te0 = SALN_PROF_T();                                                    \
-        SALN_FLUSH()                                                                           \
-        SALN_REFILL(S, (int32_t)(base - (S) - kW))                                             \
-        p_tsync += SALN_PROF_T() - te0;                                                        \
-    }                                                                                          \
-    valid |= (kAll / 0xFFu) << (S);
-#define SALN_FLUSH()                                                                           \
-    if (hf) {                                                                                  \
-        counted_store(ops + wi - 1, full);                                                     \
-        hf = 0;                                                                                \
-    }
-#define SALN_INIT(S2) SALN_REFILL(S2, SALN_ROW(S2, 0))
-    static_assert(kW == 4 || kW == 8, "phases are unrolled below");
-    SALN_INIT(0) SALN_INIT(1) SALN_INIT(2) SALN_INIT(3)
-    if constexpr (kW == 8) { SALN_INIT(4) SALN_INIT(5) SALN_INIT(6) SALN_INIT(7) }
-    while (walking) {
-        SALN_PHASE(0)
-        SALN_PHASE(1)
-        SALN_PHASE(2)
-        SALN_PHASE(3)
-        if constexpr (kW == 8) {
-            SALN_PHASE(4)
-            SALN_PHASE(5)
-            SALN_PHASE(6)
-            SALN_PHASE(7)
+    // slot S of the current window not refreshed since a crossing: load it now
+    auto ensure = [&](auto slot_c) __attribute__((always_inline)) {
+        constexpr uint32_t S = decltype(slot_c)::value;
+        if (!((valid >> (wc * 8u + S)) & 1u)) {
+            const uint8_t *a = rp + (wc ? ow1 : ow0);
+            if (wc == 0) dma(std::integral_constant<uint32_t, 0>{}, slot_c, a);
+            __builtin_amdgcn_sched_barrier(0);
+            if (wc == 1) dma(std::integral_constant<uint32_t, 1>{}, slot_c, a);
+            asm volatile("s_waitcnt vmcnt(0)" : : : "memory");
+            valid |= 1u << (wc * 8u + S);
         }
-        base -= kW;
+    };
+    auto flush = [&]() __attribute__((always_inline)) {
+        counted_store(ops + wi, (uint32_t)(acc & kMask30));
+        acc >>= 30;
+        sh -= 30;
+        ++wi;
+    };
+    // into block B-1 (window wc ^ 1) at its last column; window wc takes B-2
+    auto cross = [&]() __attribute__((always_inline)) {
+        const uint64_t o2 = boff(B >= 2 ? B - 2 : 0);
+        ow0 = wc ? ow0 : o2;
+        ow1 = wc ? o2 : ow1;
+        valid &= ~(0xFFu << (wc * 8u));
+        wc ^= 1u;
+        wl = wbase + wc * kWin;
+        --B;
+        col = K - 1;
+    };
+    auto pick = [](const u32x4 &v, uint32_t k) __attribute__((always_inline)) {
+        if constexpr (WG::LB <= 8) return k == 0 ? v.x : v.y;
+        else if constexpr (WG::LB <= 12) return k == 0 ? v.x : k == 1 ? v.y : v.z;
+        else return k == 0 ? v.x : k == 1 ? v.y : k == 2 ? v.z : v.w;
+    };
+    // bit c set: the I-open parent of byte c is present (bit 4 clear); the
+    // multiply gathers bits 4, 12, 20, 28 of a dword into bits 25..28
+    auto iopen = [](uint32_t d) __attribute__((always_inline)) {
+        return __builtin_amdgcn_ubfe((~d & 0x10101010u) * 0x00204081u, 25, 4);
+    };
+    auto iopen_mask = [&](const u32x4 &v) __attribute__((always_inline)) {
+        uint32_t pm = iopen(v.x) | (iopen(v.y) << 4);
+        if constexpr (WG::LB > 8) pm |= iopen(v.z) << 8;
+        if constexpr (WG::LB > 12) pm |= iopen(v.w) << 12;
+        return pm;
+    };
+    constexpr uint32_t kOnes3 = 0x09249249u;  // op I (1) in each of nine 3-bit slots
+    auto phase = [&](auto slot_c) __attribute__((always_inline)) {
+        constexpr uint32_t S = decltype(slot_c)::value;
+        // the row W phases ahead (rows below 1 load row 1: the count stays exact)
+        const uint8_t *ahead = row > (int32_t)kW ? rp - rsW : m;
+        if (walking) {
+            ensure(slot_c);
+            for (;;) {
+                if (sh >= 30) flush();  // at most 30 bits per iteration follow
+                const u32x4 seg = window_seg<WG::kVmcnt>(wl + S * kSlot);
+                if (sidx != 16u) {  // a cell step in state M, D or at the end cell
+                    const uint32_t dw = pick(seg, col >> 2), b8 = (col & 3u) * 8u;
+                    const uint32_t f3 = __builtin_amdgcn_ubfe(dw, b8 + lsh, 3);
+                    const uint32_t nx = (uint32_t)(kNextLut >> (f3 * 2u + sidx)) & 3u;
+                    acc |= (uint64_t)(nx | (__builtin_amdgcn_ubfe(dw, b8 + 7u, 1) << 2)) << sh;
+                    sh += 3;
+                    sidx = nx * 16u;
+                    lsh = 2u * nx + 1u;
+                    const bool up = nx != kStI, left = nx != kStD;
+                    ti -= up ? 1u : 0u;
+                    tj -= left ? 1u : 0u;
+                    const bool done = ti == 0 || tj == 0;
+                    bool crossed = false;
+                    if (left && !done) {
+                        if (col == 0) {
+                            cross();
+                            crossed = true;
+                        } else {
+                            --col;
+                        }
+                    }
+                    if (up || done) {
+                        walking = done ? 0u : 1u;
+                        break;
+                    }
+                    if (crossed) {  // the run goes on in the other window
+                        ensure(slot_c);
+                        continue;
+                    }
+                }
+                // state I at column col: extends up to the first present I-open
+                const uint32_t lo = col >= 8u ? col - 8u : 0u;
+                const uint32_t pm = iopen_mask(seg) & ((2u << col) - 1u) & (~0u << lo);
+                if (pm) {  // opens at c1: ops I x (col - c1), then M, diagonal from c1
+                    const uint32_t c1 = 31u - (uint32_t)__builtin_clz(pm), n = col - c1;
+                    const uint32_t eqb =
+                        __builtin_amdgcn_ubfe(pick(seg, c1 >> 2), (c1 & 3u) * 8u + 7u, 1);
+                    acc |= (uint64_t)((kOnes3 & ((1u << (3u * n)) - 1u)) | (eqb << (3u * n + 2u)))
+                           << sh;
+                    sh += 3u * (n + 1u);
+                    sidx = 0;
+                    lsh = 1;
+                    ti -= 1;
+                    tj -= n + 1u;
+                    const bool done = ti == 0 || tj == 0;
+                    if (!done) {
+                        if (c1 == 0) cross();
+                        else col = c1 - 1u;
+                    }
+                    walking = done ? 0u : 1u;
+                    break;
+                }
+                const uint32_t n = col - lo + 1u;  // extends through column lo
+                acc |= (uint64_t)(kOnes3 & ((1u << (3u * n)) - 1u)) << sh;
+                sh += 3u * n;
+                tj -= n;
+                if (tj == 0) {
+                    walking = 0;
+                    break;
+                }
+                if (lo == 0) cross();
+                else col = lo - 1u;
+                ensure(slot_c);
+            }
+        }
+        if (sh >= 30) flush();
+        refill(slot_c, ahead);
+        rp -= rs;
+        --row;
+        valid |= 0x101u << S;
+    };
+    // the first W rows; then exactly NW DMAs per phase, for every lane still walking
+    {
+        const uint8_t *r = rp;
+        refill(std::integral_constant<uint32_t, 0>{}, r);
+        r = ti > 1 ? r - rs : m;
+        refill(std::integral_constant<uint32_t, 1>{}, r);
+        r = ti > 2 ? r - rs : m;
+        refill(std::integral_constant<uint32_t, 2>{}, r);
+        r = ti > 3 ? r - rs : m;
+        refill(std::integral_constant<uint32_t, 3>{}, r);
+        if constexpr (kW == 8) {
+            r = ti > 4 ? r - rs : m;
+            refill(std::integral_constant<uint32_t, 4>{}, r);
+            r = ti > 5 ? r - rs : m;
+            refill(std::integral_constant<uint32_t, 5>{}, r);
+            r = ti > 6 ? r - rs : m;
+            refill(std::integral_constant<uint32_t, 6>{}, r);
+            r = ti > 7 ? r - rs : m;
+            refill(std::integral_constant<uint32_t, 7>{}, r);
+        }
     }
-#undef SALN_INIT
-#undef SALN_FLUSH
-#undef SALN_PHASE
-#undef SALN_ENSURE
-#undef SALN_REFILL
-#undef SALN_DMA
-#undef SALN_ROW
+    while (walking) {
+        phase(std::integral_constant<uint32_t, 0>{});
+        phase(std::integral_constant<uint32_t, 1>{});
+        phase(std::integral_constant<uint32_t, 2>{});
+        phase(std::integral_constant<uint32_t, 3>{});
+        if constexpr (kW == 8) {
+            phase(std::integral_constant<uint32_t, 4>{});
+            phase(std::integral_constant<uint32_t, 5>{});
+            phase(std::integral_constant<uint32_t, 6>{});
+            phase(std::integral_constant<uint32_t, 7>{});
+        }
+    }
+    const uint32_t st = sidx / 16u;
     int ev, bst;
     if (st == kStM && ti == 0 && tj == 0) {
         ev = kEvOrigin;
@@ -533,7 +541,7 @@ __device__ void walk_pair_lds(const NwPairDesc &p, int32_t hend, const uint8_t *
         else ev = kEvDead;
     }
     // the reference's end states: the last row's codes are stored unfiltered
-    const uint32_t es = (m[geo.cell(p.len_db, p.len_q, rs, bs, p.mask_cs)] ^ 0x7Fu) & 7u;
+    const uint32_t es = (m[geo.cell(p.len_db, p.len_q, rs, bs, cs)] ^ 0x7Fu) & 7u;
     uint32_t nops = 0;
     bool retried = false;
     if (ev == kEvDead) {
@@ -541,7 +549,7 @@ __device__ void walk_pair_lds(const NwPairDesc &p, int32_t hend, const uint8_t *
         // DFS goes on with the next tied end states (walk_first, byte loads)
         const uint32_t rest = end_states_after(es, first_end_state(es));
         if (rest) {
-            const MaskCell mc{m, geo, rs, bs, p.mask_cs, sc};
+            const MaskCell mc{m, geo, rs, bs, cs, sc};
             const WalkOut w = walk_first(mc, rest, p.len_db, p.len_q, nullptr, nullptr, out);
             ev = w.ev;
             nops = w.nops;
@@ -550,10 +558,10 @@ __device__ void walk_pair_lds(const NwPairDesc &p, int32_t hend, const uint8_t *
     }
     // CIGAR: the op stream read back in forward order (last recorded op first)
     if (ev == kEvOrigin && !retried) {
-        if (hf) counted_store(ops + wi - 1, full);
-        if (sh3) counted_store(ops + wi, cur);
+        const uint32_t nrec = wi * kOpsPerWord + sh / 3;
+        if (sh) counted_store(ops + wi, (uint32_t)(acc & kMask30));
+        if (sh > 30) counted_store(ops + wi + 1, (uint32_t)(acc >> 30));
         asm volatile("s_waitcnt vmcnt(0)" : : : "memory");
-        const uint32_t nrec = wi * kOpsPerWord + sh3 / 3;
         uint32_t run_op = 0, run_len = 0;
         for (int32_t w = (int32_t)((nrec - 1u) / kOpsPerWord); w >= 0; --w) {
             const uint32_t word = ops[w];
@@ -578,25 +586,7 @@ __device__ void walk_pair_lds(const NwPairDesc &p, int32_t hend, const uint8_t *
             ++nops;
         }
     }
-    saln_nw_result r = make_result(hend, WalkOut{ev, nops}, es);
-#ifdef SALN_WALK_PROF
-    {
-        const uint64_t tt = SALN_PROF_T() - p_t0;
-        r.score = (int32_t)(tt >> 4);
-        r.status = (int32_t)(p_twait >> 4);
-        r.cigar_len = (uint32_t)(p_tsync >> 4);
-        r.flags = (uint8_t)min(p_sync, 255u);
-        r.reserved = (uint8_t)min(p_iter >> 2, 255u);
-    }
-#endif
-#ifdef SALN_WALK_CHECK
-    if (dbg_n) {
-        r.flags |= 4;
-        r.reserved = (uint8_t)(dbg_n > 255 ? 255 : dbg_n);
-        r.cigar_len = dbg_info;
-    }
-#endif
-    results[p.pair_id] = r;
+    results[p.pair_id] = make_result(hend, WalkOut{ev, nops}, es);
 }
 
 // Per-variant traceback for filled pairs whose segments fit an LDS slot.
@@ -615,8 +605,8 @@ __global__ __launch_bounds__(256) void nw_traceback_lds_kernel(
     // behind the fill's instructions.
     __builtin_amdgcn_s_setprio(3);
     const NwPairDesc p = pairs[idx];
-    walk_pair_lds<G, K>(p, end_h[idx], mask, ops, results, cigar, sc,
-                        (lds_u8 *)(win_all + (threadIdx.x / 64u) * kWave));
+    lds_u8 *win = (lds_u8 *)(win_all + (threadIdx.x / 64u) * kWave);
+    walk_pack_lds<G, K>(p, end_h[idx], mask, ops, results, cigar, sc, win);
 }
 
 // One walker per pair.  Pairs with an empty side have no mask and take the
@@ -2822,7 +2812,7 @@ hipError_t launch_fill(int variant, const NwPairDesc *pairs, uint32_t first, uin
         case 1: fill_i32<16, 16>(grid, stream, pairs, first, count, qs, ds, mask, scratch, end_h, res, cig, sc, codes, ld_max); break;
         case 2: fill_i32<64, 8>(grid, stream, pairs, first, count, qs, ds, mask, scratch, end_h, res, cig, sc, codes, ld_max); break;
         case 3: return hipErrorInvalidValue;  // stripes: launch_fill_stripes
-        case 4: e = fill_pk<8, 19>(grid, stream, pairs, first, count, qs, ds, mask, end_h, res, cig, sc, codes, ld_max, rebase); break;
+        case 4: return hipErrorInvalidValue;  // 8 x 19 groups: the all-vs-all only (nw_avsa.cpp)
         case 5: e = fill_pk<16, 16>(grid, stream, pairs, first, count, qs, ds, mask, end_h, res, cig, sc, codes, ld_max, rebase); break;
         case 7: e = fill_pk<16, 10>(grid, stream, pairs, first, count, qs, ds, mask, end_h, res, cig, sc, codes, ld_max, rebase); break;
         case 8: e = fill_pk<64, 16>(grid, stream, pairs, first, count, qs, ds, mask, end_h, res, cig, sc, codes, ld_max, rebase); break;
@@ -2881,7 +2871,7 @@ hipError_t launch_traceback(int variant, const NwPairDesc *pairs, uint32_t first
             if (e != hipSuccess) return e;
             break;
         }
-        case 4: tb_lds<8, 19>(grid, stream, pairs, first, n, mask, end_h, ops, results, cigar, sc); break;
+        case 4: return hipErrorInvalidValue;  // no plan fills variant 4
         case 5: tb_lds<16, 16>(grid, stream, pairs, first, n, mask, end_h, ops, results, cigar, sc); break;
         case 6: tb_lds<32, 16>(grid, stream, pairs, first, n, mask, end_h, ops, results, cigar, sc); break;
         case 7: tb_lds<16, 10>(grid, stream, pairs, first, n, mask, end_h, ops, results, cigar, sc); break;
@@ -3076,15 +3066,10 @@ static bool packed_ok_rebase(uint32_t lq, uint32_t ld, const Scoring &sc, uint32
 }
 
 int choose_variant(uint32_t len_q, uint32_t len_db, const Scoring &sc) {
-    static const int narrow = [] {
-        const char *e = std::getenv("SALN_NARROW_GROUPS");  // experiment switch: 8-lane groups
-        return e && e[0] == '1' ? 1 : 0;
-    }();
     // the packed fills carry V' = 2V + p (no alive flag): sentinel-free pairs only
     const bool free = sentinel_free(sc, len_q, len_db);
     if (!free) return len_q <= 160 ? 0 : len_q <= 256 ? 1 : len_q <= 512 ? 2 : 3;
     if (packed_ok(len_q, len_db, sc)) {
-        if (len_q <= 152 && narrow) return 4;
         if (len_q <= 160) return 7;
         if (len_q <= 256) return 5;
         if (len_q <= 512) return 6;

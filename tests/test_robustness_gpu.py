@@ -9,6 +9,7 @@
   stream when that is torch's legacy null stream.
 * ShardedAllVsAll's default engine (no process group) equals
   nw_score_all_vs_all, which the oracle pins (main.rs:61-67).
+* The pipelined plan (async traceback) equals sequential executes.
 """
 import numpy as np
 import pytest
@@ -132,3 +133,36 @@ def test_sharded_all_vs_all_default_engine_single_rank(saln):
     ls, lt = s.lookup(di, qi)
     assert np.array_equal(ls, want_s[di, qi]) and np.array_equal(lt, want_t[di, qi])
     s.close()
+
+
+def test_pipelined_plan_matches_sequential(saln):
+    """The 2-deep pipeline (saln_nw_plan_set_async: the traceback of execute
+    n beside the fill of n+1, double-buffered workspace) gives every
+    execute's results and CIGARs exactly as sequential executes do."""
+    import torch
+    from sequencealigning_amd import synth
+    n = 3000
+    qs, qo, ds, do = synth.iid_pairs(n, 150, 150, seed=0x5EED0035)
+    pairs = np.stack([np.arange(n)] * 2, 1)
+    dq = torch.from_numpy(qs).cuda()
+    dd = torch.from_numpy(ds).cuda()
+    ref = saln.NwPlan(qo, do, pairs=pairs)
+    r0 = torch.zeros(n * 4, dtype=torch.int32, device="cuda")
+    c0 = torch.zeros(ref.cigar_words, dtype=torch.int32, device="cuda")
+    ref.execute(dq, dd, r0, c0)
+    torch.cuda.synchronize()
+    want_r, want_c = r0.cpu().numpy(), c0.cpu().numpy()
+    ref.close()
+    plan = saln.NwPlan(qo, do, pairs=pairs)
+    plan.set_async(True)
+    res = [torch.full((n * 4,), -1, dtype=torch.int32, device="cuda") for _ in range(2)]
+    cig = [torch.zeros(plan.cigar_words, dtype=torch.int32, device="cuda") for _ in range(2)]
+    for k in range(6):
+        plan.execute(dq, dd, res[k % 2], cig[k % 2])
+    plan.sync()
+    plan.check()
+    torch.cuda.synchronize()
+    for b in range(2):
+        assert np.array_equal(res[b].cpu().numpy(), want_r)
+        assert np.array_equal(cig[b].cpu().numpy(), want_c)
+    plan.close()
