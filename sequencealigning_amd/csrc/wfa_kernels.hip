@@ -79,6 +79,35 @@ struct LaneArena {
     }
 };
 
+// A source front's header read once per tensor (the arena is written while a
+// tensor is built, so the compiler cannot keep these in registers itself):
+// get_element (:154-158) against it needs only the element's own words.
+struct SrcFront {
+    bool ok;        // the tensor exists and the front is Some
+    int32_t lo, n;  // first diagonal, element count
+    uint32_t slot;
+    int f;
+    __device__ Elem get(const LaneArena &L, int32_t idx) const {
+        Elem e{false, 0, 0};
+        const int64_t k = (int64_t)idx - lo;
+        if (!ok || k < 0 || k >= n) return e;
+        const uint32_t m = L.Mt(slot, f, (uint32_t)k);
+        if (!(m & 1u)) return e;
+        e.some = true;
+        e.offset = L.O(slot, f, (uint32_t)k);
+        e.meta = m;
+        return e;
+    }
+};
+__device__ __forceinline__ SrcFront src_front(const LaneArena &L, bool ok, uint32_t slot, int f) {
+    SrcFront r{ok, 0, 0, slot, f};
+    if (ok) {
+        r.lo = L.H(slot, f, 1);
+        r.n = L.H(slot, f, 3);
+    }
+    return r;
+}
+
 // x(diag), y(diag) (:85-90) as sign-extended 64-bit (Rust `as usize`)
 __device__ __forceinline__ int64_t ex(int32_t off, int32_t diag) { return (int64_t)(off - min(diag, 0)); }
 __device__ __forceinline__ int64_t ey(int32_t off, int32_t diag) { return (int64_t)(off + max(diag, 0)); }
@@ -158,10 +187,12 @@ __device__ bool tensor_new(const LaneArena &L, int64_t s, uint32_t ns, int32_t *
     int32_t il = lo, ih = hi, dl = lo, dh = hi, ml = lo, mh = hi;
     bool iset = false, dset = false, mset = false;
     uint32_t mpos = 0;
+    const SrcFront sm_o = src_front(L, om, po, FM), sd_e = src_front(L, ed, pe, FD);
+    const SrcFront si_e = src_front(L, ei, pe, FI), sm_x = src_front(L, xm, px, FM);
     for (int32_t idx = lo; lo <= hi; ++idx) {
         const uint32_t k = (uint32_t)(idx - lo);
         {  // D (:268-306)
-            const Elem a = L.get(om, po, FM, idx + 1), b = L.get(ed, pe, FD, idx + 1);
+            const Elem a = sm_o.get(L, idx + 1), b = sd_e.get(L, idx + 1);
             bool h = false;
             int32_t v = 0;
             omax(h, v, a.some, a.offset);
@@ -178,7 +209,7 @@ __device__ bool tensor_new(const LaneArena &L, int64_t s, uint32_t ns, int32_t *
             L.put(ns, FD, k, w);
         }
         {  // I (:308-347)
-            const Elem a = L.get(om, po, FM, idx - 1), b = L.get(ei, pe, FI, idx - 1);
+            const Elem a = sm_o.get(L, idx - 1), b = si_e.get(L, idx - 1);
             bool h = false;
             int32_t v = 0;
             omax(h, v, a.some, a.offset);
@@ -195,7 +226,7 @@ __device__ bool tensor_new(const LaneArena &L, int64_t s, uint32_t ns, int32_t *
             L.put(ns, FI, k, w);
         }
         {  // M (:348-395): X.m[idx]+1 (as state M), I[idx], D[idx] of this tensor
-            const Elem xa = L.get(xm, px, FM, idx);
+            const Elem xa = sm_x.get(L, idx);
             const Elem ib = L.at(ns, FI, k), db = L.at(ns, FD, k);
             bool h = false;
             int32_t v = 0;
@@ -237,7 +268,20 @@ __device__ bool tensor_new(const LaneArena &L, int64_t s, uint32_t ns, int32_t *
     return true;
 }
 
-// WaveFront::expand (:127-139) on the M front of slot ns
+// Four sequence bytes from s + pos (pos + 4 <= length) as one word, byte 0
+// lowest: two aligned dword loads and a byte funnel shift.  Each dword holds a
+// byte of the range, so no load leaves the sequence's own aligned words.
+__device__ __forceinline__ uint32_t load4(const uint8_t *s, int64_t pos) {
+    const uintptr_t a = (uintptr_t)(s + pos);
+    const uint32_t *w = reinterpret_cast<const uint32_t *>(a & ~(uintptr_t)3);
+    const uint32_t sh = (uint32_t)(a & 3u);
+    const uint32_t lo = w[0], hi = sh ? w[1] : 0u;
+    return __builtin_amdgcn_alignbyte(hi, lo, sh);
+}
+
+// WaveFront::expand (:127-139) on the M front of slot ns: the offset advances
+// while s1[y] == s2[x] inside both sequences.  Compared four bytes per round
+// trip (the first differing byte ends the run, as the byte loop would).
 __device__ void extend_m(const LaneArena &L, uint32_t ns, const uint8_t *s1, int32_t l1,
                          const uint8_t *s2, int32_t l2) {
     if (!L.H(ns, FM, 0)) return;
@@ -249,7 +293,17 @@ __device__ void extend_m(const LaneArena &L, uint32_t ns, const uint8_t *s1, int
         int32_t off = L.O(ns, FM, (uint32_t)k);
         for (;;) {
             const int64_t y = ey(off, diag), x = ex(off, diag);
-            if (y < 0 || y >= l1 || x < 0 || x >= l2 || s1[y] != s2[x]) break;
+            if (y < 0 || x < 0 || y >= l1 || x >= l2) break;
+            if (y + 4 <= l1 && x + 4 <= l2) {
+                const uint32_t d = load4(s1, y) ^ load4(s2, x);
+                if (d == 0) {
+                    off += 4;
+                    continue;
+                }
+                off += (int32_t)(__builtin_ctz(d) >> 3);
+                break;
+            }
+            if (s1[y] != s2[x]) break;
             ++off;
         }
         L.O(ns, FM, (uint32_t)k) = off;
