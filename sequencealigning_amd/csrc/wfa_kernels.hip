@@ -186,27 +186,29 @@ __device__ bool tensor_new(const LaneArena &L, int64_t s, uint32_t ns, int32_t *
     if (lo <= hi && (int64_t)hi - lo + 1 > (int64_t)L.A.W) return false;
     int32_t il = lo, ih = hi, dl = lo, dh = hi, ml = lo, mh = hi;
     bool iset = false, dset = false, mset = false;
-    uint32_t mpos = 0;
+    // Each front is written from its first Some element on (I, D as the
+    // reference leaves them after rotate_left(lo.abs_diff(x.lo)): positions
+    // past the truncated length are never read), so no rotation is needed.
+    uint32_t mpos = 0, ipos = 0, dpos = 0;
     const SrcFront sm_o = src_front(L, om, po, FM), sd_e = src_front(L, ed, pe, FD);
     const SrcFront si_e = src_front(L, ei, pe, FI), sm_x = src_front(L, xm, px, FM);
     for (int32_t idx = lo; lo <= hi; ++idx) {
-        const uint32_t k = (uint32_t)(idx - lo);
+        Elem wd{false, 0, 0}, wi{false, 0, 0};
         {  // D (:268-306)
             const Elem a = sm_o.get(L, idx + 1), b = sd_e.get(L, idx + 1);
             bool h = false;
             int32_t v = 0;
             omax(h, v, a.some, a.offset);
             omax(h, v, b.some, b.offset);
-            Elem w{false, 0, 0};
             if (h) {
                 uint32_t np = 0, par = 0;
                 if (a.some && a.offset == v) par |= m_state(a.meta) << (2 * np++);
                 if (b.some && b.offset == v) par |= m_state(b.meta) << (2 * np++);
-                w = Elem{true, v, mk_meta(SD, np, par)};
+                wd = Elem{true, v, mk_meta(SD, np, par)};
                 dh = idx;
                 if (!dset) dl = idx, dset = true;
             }
-            L.put(ns, FD, k, w);
+            if (dset) L.put(ns, FD, dpos++, wd);
         }
         {  // I (:308-347)
             const Elem a = sm_o.get(L, idx - 1), b = si_e.get(L, idx - 1);
@@ -214,30 +216,28 @@ __device__ bool tensor_new(const LaneArena &L, int64_t s, uint32_t ns, int32_t *
             int32_t v = 0;
             omax(h, v, a.some, a.offset);
             omax(h, v, b.some, b.offset);
-            Elem w{false, 0, 0};
             if (h) {
                 uint32_t np = 0, par = 0;
                 if (a.some && a.offset == v) par |= m_state(a.meta) << (2 * np++);
                 if (b.some && b.offset == v) par |= m_state(b.meta) << (2 * np++);
-                w = Elem{true, v + 1, mk_meta(SI, np, par)};
+                wi = Elem{true, v + 1, mk_meta(SI, np, par)};
                 ih = idx;
                 if (!iset) il = idx, iset = true;
             }
-            L.put(ns, FI, k, w);
+            if (iset) L.put(ns, FI, ipos++, wi);
         }
         {  // M (:348-395): X.m[idx]+1 (as state M), I[idx], D[idx] of this tensor
             const Elem xa = sm_x.get(L, idx);
-            const Elem ib = L.at(ns, FI, k), db = L.at(ns, FD, k);
             bool h = false;
             int32_t v = 0;
             omax(h, v, xa.some, xa.offset + 1);
-            omax(h, v, ib.some, ib.offset);
-            omax(h, v, db.some, db.offset);
+            omax(h, v, wi.some, wi.offset);
+            omax(h, v, wd.some, wd.offset);
             if (h) {
                 uint32_t np = 0, par = 0;
                 if (xa.some && xa.offset + 1 == v) par |= (uint32_t)SM << (2 * np++);
-                if (ib.some && ib.offset == v) par |= m_state(ib.meta) << (2 * np++);
-                if (db.some && db.offset == v) par |= m_state(db.meta) << (2 * np++);
+                if (wi.some && wi.offset == v) par |= m_state(wi.meta) << (2 * np++);
+                if (wd.some && wd.offset == v) par |= m_state(wd.meta) << (2 * np++);
                 L.put(ns, FM, mpos++, Elem{true, v, mk_meta(SM, np, par)});
                 mh = idx;
                 if (!mset) ml = idx, mset = true;
@@ -248,9 +248,6 @@ __device__ bool tensor_new(const LaneArena &L, int64_t s, uint32_t ns, int32_t *
         if (idx == hi) break;
     }
     const uint32_t len = lo <= hi ? (uint32_t)(hi - lo + 1) : 0u;
-    // I, D: rotate_left(lo.abs_diff(x.lo)) then truncate(x.hi - x.lo + 1)
-    rotate_left(L, ns, FI, len, adiff(lo, il));
-    rotate_left(L, ns, FD, len, adiff(lo, dl));
     L.H(ns, FI, 0) = iset;
     L.H(ns, FI, 1) = il;
     L.H(ns, FI, 2) = ih;
