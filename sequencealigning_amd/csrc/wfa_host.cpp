@@ -39,12 +39,12 @@ struct DevBuf {
 };
 
 constexpr uint32_t kDefaultSteps = 64, kDefaultWidth = 64;
-constexpr uint64_t kArenaBudget = 8ull << 30;  // bytes of tensor history per launch
+constexpr uint64_t kArenaBudget = 32ull << 30;  // bytes of tensor history per launch (288 GB HBM)
 // Batch runs start every pair with this step cap (a small arena, many lanes
 // per launch); the pairs that reach it are re-run with the caller's cap.
 // Essentially every realistic pair ends far earlier (REF_PANIC_TRIM at s = 20,
 // SURVEY.md §8.5), so the big arena is only paid for the few that need it.
-constexpr uint32_t kFirstPassSteps = 64;
+constexpr uint32_t kFirstPassSteps = 32;
 
 uint32_t ev_cap_for(uint32_t max_steps) { return 7 * (max_steps / 4 + 2) + 8; }
 
