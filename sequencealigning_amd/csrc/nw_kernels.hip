@@ -21,6 +21,7 @@
 #include <algorithm>
 #include <cstdlib>
 #include <type_traits>
+#include <utility>
 
 #include "nw_common.hpp"
 #include "saln.h"
@@ -231,30 +232,35 @@ __device__ __forceinline__ void walk_pair(const NwPairDesc &p, int32_t hend,
 // (op-stream stores, fallback loads) only make that wait more conservative.
 constexpr uint32_t kOpsPerWord = 10;                     // 3-bit ops per op-stream word
 
-// Window geometry of the walker for K columns per block: NW = 2 windows
-// (blocks B, B-1 resident) of W slots (rows).  A slot holds 16 bytes per lane
+// Window geometry of the walker for K columns per block: NW windows (blocks
+// B, .., B-NW+1 resident) of W slots (rows).  A slot holds 16 bytes per lane
 // (the LDS-DMA lane stride, also for dwordx3).  Each phase end issues the NW
 // DMAs (always) after the op-stream store (only when a word is complete), so
 // a phase reads the slot its DMA filled W-1 phases earlier behind >= NW*(W-1)
-// younger VMEM operations.  The walk is bound by L2 request throughput (one
-// request per lane per DMA), so W is kept small: with 10-column blocks a
-// diagonal path crosses a block every ~10 rows and W = 4 lets the window of
-// B-2 refill before the next crossing.
+// younger VMEM operations.  A phase waits for a DMA issued W-1 phases earlier,
+// but at the C2 scale the walk is bound by the DMA stream itself, not by that
+// latency: round 3 measured (NW x W) 2 x 4 0.26 ms, 2 x 8 0.28, 3 x 4 0.30,
+// 3 x 6 0.30 (tools/exp_ab_c2.sh, one box), so the default is the leanest.
+// NW = 3 keeps block B-2 resident too (no synchronous reload when a path
+// crosses two blocks within W rows); SALN_WALK_NW / SALN_WALK_W select it.
 #ifndef SALN_WALK_W
-#define SALN_WALK_W 0  // experiment switch: force the window depth
+#define SALN_WALK_W 0  // experiment switches: force the window depth / count
 #endif
-constexpr uint32_t kWalkW = SALN_WALK_W;
+#ifndef SALN_WALK_NW
+#define SALN_WALK_NW 0
+#endif
 template <int K>
 struct WalkGeo {
     static constexpr uint32_t LB = (K + 3) / 4 * 4;
-    static constexpr uint32_t NW = 2;
-    static constexpr uint32_t W = kWalkW ? kWalkW : (K < 16 ? 4 : 8);
+    static constexpr uint32_t NW = SALN_WALK_NW ? SALN_WALK_NW : 2;
+    static constexpr uint32_t W = SALN_WALK_W ? SALN_WALK_W : (K < 16 ? 4 : 8);
     static constexpr uint32_t SB = LB == 12 ? 12 : 16;        // DMA bytes per lane
     static constexpr uint32_t kSlotBytes = 64 * 16;          // one slot of a wave
     static constexpr uint32_t kWinBytes = W * kSlotBytes;    // one window of a wave
     static constexpr uint32_t kWaveLds = NW * kWinBytes;
     static constexpr uint32_t kVmcnt = NW * (W - 1);
     static_assert(LB <= 16, "LDS window slots hold 16 bytes per lane");
+    static_assert((NW == 2 || NW == 3) && W >= 2 && W <= 8, "8 valid bits per window");
 };
 
 typedef __attribute__((address_space(3))) uint8_t lds_u8;
@@ -291,15 +297,16 @@ constexpr uint64_t kNextLut = make_next_lut();
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 template <uint32_t N>
 __device__ __forceinline__ u32x4 window_seg(uint32_t addr) {
-    static_assert(N == 6 || N == 14, "add the immediate below");
+    static_assert(N < 64, "vmcnt immediate");
     u32x4 v;
-    if constexpr (N == 6)
-        asm volatile("s_waitcnt vmcnt(6)\n\tds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)"
-                     : "=v"(v) : "v"(addr) : "memory");
-    else
-        asm volatile("s_waitcnt vmcnt(14)\n\tds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)"
-                     : "=v"(v) : "v"(addr) : "memory");
+    asm volatile("s_waitcnt vmcnt(%2)\n\tds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)"
+                 : "=v"(v) : "v"(addr), "n"(N) : "memory");
     return v;
+}
+
+template <typename F, uint32_t... I>
+__device__ __forceinline__ void unroll_each(F &&f, std::integer_sequence<uint32_t, I...>) {
+    (f(std::integral_constant<uint32_t, I>{}), ...);
 }
 
 // The walk (round 3: one iteration per row, and a shorter instruction stream
@@ -323,9 +330,8 @@ __device__ void walk_pack_lds(const NwPairDesc &p, int32_t hend, const uint8_t *
                               uint32_t *__restrict__ ops_all, saln_nw_result *__restrict__ results,
                               uint32_t *__restrict__ cigar, Scoring sc, lds_u8 *win) {
     using WG = WalkGeo<K>;
-    static_assert(WG::NW == 2, "two windows: blocks B and B-1");
     constexpr Geom geo{G, K};
-    constexpr uint32_t kW = WG::W;
+    constexpr uint32_t kW = WG::W, NW = WG::NW;
     constexpr uint32_t kWin = WG::kWinBytes, kSlot = WG::kSlotBytes;
     constexpr uint64_t kMask30 = (1u << 30) - 1u;
     const uint64_t rs = p.mask_rs, cs = p.mask_cs;
@@ -343,10 +349,21 @@ __device__ void walk_pack_lds(const NwPairDesc &p, int32_t hend, const uint8_t *
     uint32_t sidx = 3u * 16u, lsh = 0;  // kNextLut row of the state (3: end cell), its bits
     uint32_t walking = 1;
     uint32_t B = (tj - 1) / K, col = (tj - 1) % K;
-    uint32_t wc = B & 1u;    // window of block B; window wc ^ 1 holds B - 1
-    uint32_t valid = 0xFFFFu;  // bit 8w + s: slot s of window w holds its assigned block
-    const uint64_t ob = boff(B), ob1 = boff(B >= 1 ? B - 1 : 0);
-    uint64_t ow0 = wc ? ob1 : ob, ow1 = wc ? ob : ob1;  // block offsets of windows 0 / 1
+    // block b lives in window b % NW: wc holds B, the windows below it (mod
+    // NW) B-1 (and B-2); ow<w> is the block offset window w is loaded from
+    uint32_t wc = B % NW;
+    uint32_t valid = NW == 3 ? 0xFFFFFFu : 0xFFFFu;  // bit 8w + s: slot s of window w is current
+    uint64_t ow0 = 0, ow1 = 0, ow2 = 0;
+    auto set_ow = [&](uint32_t w, uint64_t o) __attribute__((always_inline)) {
+        ow0 = w == 0 ? o : ow0;
+        ow1 = w == 1 ? o : ow1;
+        if constexpr (NW == 3) ow2 = w == 2 ? o : ow2;
+    };
+    auto get_ow = [&](uint32_t w) __attribute__((always_inline)) {
+        return NW == 3 ? (w == 0 ? ow0 : w == 1 ? ow1 : ow2) : (w == 0 ? ow0 : ow1);
+    };
+    for (uint32_t b = 0; b < NW; ++b)  // blocks B, B-1, .. (clamped to block 0)
+        set_ow((B + NW - b) % NW, boff(B >= b ? B - b : 0));
     const uint32_t wbase = lds_off(win) + (threadIdx.x & 63u) * 16u;
     uint32_t wl = wbase + wc * kWin;  // my slot 0 in the current window
     // the phase's row pointer (row ti at a phase start), W rows ahead for the refills
@@ -363,15 +380,20 @@ __device__ void walk_pack_lds(const NwPairDesc &p, int32_t hend, const uint8_t *
     auto refill = [&](auto slot_c, const uint8_t *row) __attribute__((always_inline)) {
         dma(std::integral_constant<uint32_t, 0>{}, slot_c, row + ow0);
         dma(std::integral_constant<uint32_t, 1>{}, slot_c, row + ow1);
+        if constexpr (NW == 3) dma(std::integral_constant<uint32_t, 2>{}, slot_c, row + ow2);
     };
     // slot S of the current window not refreshed since a crossing: load it now
     auto ensure = [&](auto slot_c) __attribute__((always_inline)) {
         constexpr uint32_t S = decltype(slot_c)::value;
         if (!((valid >> (wc * 8u + S)) & 1u)) {
-            const uint8_t *a = rp + (wc ? ow1 : ow0);
+            const uint8_t *a = rp + get_ow(wc);
             if (wc == 0) dma(std::integral_constant<uint32_t, 0>{}, slot_c, a);
             __builtin_amdgcn_sched_barrier(0);
             if (wc == 1) dma(std::integral_constant<uint32_t, 1>{}, slot_c, a);
+            if constexpr (NW == 3) {
+                __builtin_amdgcn_sched_barrier(0);
+                if (wc == 2) dma(std::integral_constant<uint32_t, 2>{}, slot_c, a);
+            }
             asm volatile("s_waitcnt vmcnt(0)" : : : "memory");
             valid |= 1u << (wc * 8u + S);
         }
@@ -382,13 +404,11 @@ __device__ void walk_pack_lds(const NwPairDesc &p, int32_t hend, const uint8_t *
         sh -= 30;
         ++wi;
     };
-    // into block B-1 (window wc ^ 1) at its last column; window wc takes B-2
+    // into block B-1 (the window below wc) at its last column; window wc takes B-NW
     auto cross = [&]() __attribute__((always_inline)) {
-        const uint64_t o2 = boff(B >= 2 ? B - 2 : 0);
-        ow0 = wc ? ow0 : o2;
-        ow1 = wc ? o2 : ow1;
+        set_ow(wc, boff(B >= NW ? B - NW : 0));
         valid &= ~(0xFFu << (wc * 8u));
-        wc ^= 1u;
+        wc = wc == 0 ? NW - 1 : wc - 1;
         wl = wbase + wc * kWin;
         --B;
         col = K - 1;
@@ -488,41 +508,14 @@ __device__ void walk_pack_lds(const NwPairDesc &p, int32_t hend, const uint8_t *
         refill(slot_c, ahead);
         rp -= rs;
         --row;
-        valid |= 0x101u << S;
+        valid |= (NW == 3 ? 0x10101u : 0x101u) << S;
     };
     // the first W rows; then exactly NW DMAs per phase, for every lane still walking
-    {
-        const uint8_t *r = rp;
-        refill(std::integral_constant<uint32_t, 0>{}, r);
-        r = ti > 1 ? r - rs : m;
-        refill(std::integral_constant<uint32_t, 1>{}, r);
-        r = ti > 2 ? r - rs : m;
-        refill(std::integral_constant<uint32_t, 2>{}, r);
-        r = ti > 3 ? r - rs : m;
-        refill(std::integral_constant<uint32_t, 3>{}, r);
-        if constexpr (kW == 8) {
-            r = ti > 4 ? r - rs : m;
-            refill(std::integral_constant<uint32_t, 4>{}, r);
-            r = ti > 5 ? r - rs : m;
-            refill(std::integral_constant<uint32_t, 5>{}, r);
-            r = ti > 6 ? r - rs : m;
-            refill(std::integral_constant<uint32_t, 6>{}, r);
-            r = ti > 7 ? r - rs : m;
-            refill(std::integral_constant<uint32_t, 7>{}, r);
-        }
-    }
-    while (walking) {
-        phase(std::integral_constant<uint32_t, 0>{});
-        phase(std::integral_constant<uint32_t, 1>{});
-        phase(std::integral_constant<uint32_t, 2>{});
-        phase(std::integral_constant<uint32_t, 3>{});
-        if constexpr (kW == 8) {
-            phase(std::integral_constant<uint32_t, 4>{});
-            phase(std::integral_constant<uint32_t, 5>{});
-            phase(std::integral_constant<uint32_t, 6>{});
-            phase(std::integral_constant<uint32_t, 7>{});
-        }
-    }
+    unroll_each([&](auto slot_c) __attribute__((always_inline)) {
+        constexpr uint32_t S = decltype(slot_c)::value;
+        refill(slot_c, ti > S ? rp - (uint64_t)S * rs : m);
+    }, std::make_integer_sequence<uint32_t, kW>{});
+    while (walking) unroll_each(phase, std::make_integer_sequence<uint32_t, kW>{});
     const uint32_t st = sidx / 16u;
     int ev, bst;
     if (st == kStM && ti == 0 && tj == 0) {
