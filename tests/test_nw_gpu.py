@@ -569,3 +569,37 @@ def test_long_pairs_cooperative_walker(saln, oracle, packed):
         o = oracle.nw(q, d, literal_dfs=False)
         assert got[k][:3] == (o.score, o.end_states, o.panics), k
         assert got[k][3] == o.first_ops, k
+
+
+def test_long_gaps_lds_walker(saln, oracle):
+    """The LDS walker's I-run step (round 3: a run resolved from the lane's
+    16-byte segment, at most nine cells per iteration, crossings into the
+    previous block mid-run) and long D runs: pairs with gaps of 1-60 bases,
+    at the ends too, through batches of packed variants 7 / 5 / 6 (10- and
+    16-column blocks) and the i32 lanes, against the oracle's first printed
+    alignment."""
+    rng = np.random.default_rng(0x6A95)
+    qs, ds = [], []
+    for k in range(240):
+        lq = int(rng.choice([150, 160, 240, 500]))
+        base = rand_seq(rng, lq + 80)
+        q = base[:lq]
+        d = bytearray(q)
+        for _ in range(int(rng.integers(1, 4))):
+            at = int(rng.integers(0, len(d) + 1))
+            g = int(rng.integers(1, 61))
+            if rng.random() < 0.5 and len(d) > g + 1:  # deletion from the db: an I run
+                del d[at:at + g]
+            else:                                      # insertion into the db: a D run
+                d[at:at] = rand_seq(rng, g)
+        if k % 7 == 0:
+            d = bytes(d)[:max(1, len(d) - int(rng.integers(1, 40)))]  # gap at the end
+        qs.append(q)
+        ds.append(bytes(d))
+    res, cig = saln.nw_align_batch(qs, ds, pairs=[(k, k) for k in range(len(qs))])
+    for k in range(len(qs)):
+        o = oracle.nw(qs[k], ds[k], literal_dfs=False)
+        assert int(res["score"][k]) == o.score, k
+        assert int(res["end_states"][k]) == o.end_states, k
+        assert (int(res["status"][k]) == 2) == o.panics, k
+        assert (expand(cig[k]) if res["printed"][k] else None) == o.first_ops, k
