@@ -8,6 +8,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "nw_host.hpp"
@@ -108,9 +109,23 @@ static int run_batch(saln_context *ctx, const uint8_t *q_seq, const uint64_t *q_
     }
     clk.mark("d2h");
     if (cigar && hc) {
-        for (uint64_t k = 0; k < n_pairs; ++k) {
-            const uint64_t dst = cigar_off ? cigar_off[k] : coff[k];
-            std::memcpy(cigar + dst, hc + doff[k], results[k].cigar_len * 4);
+        // ~10^5 small copies (a few hundred bytes each): split over host threads
+        auto scatter = [&](uint64_t a, uint64_t b) {
+            for (uint64_t k = a; k < b; ++k) {
+                const uint64_t dst = cigar_off ? cigar_off[k] : coff[k];
+                std::memcpy(cigar + dst, hc + doff[k], results[k].cigar_len * 4);
+            }
+        };
+        const uint64_t nt = std::min<uint64_t>(
+            std::max(1u, std::min(16u, std::thread::hardware_concurrency())), n_pairs / 4096 + 1);
+        if (nt <= 1) {
+            scatter(0, n_pairs);
+        } else {
+            std::vector<std::thread> th;
+            for (uint64_t t = 1; t < nt; ++t)
+                th.emplace_back(scatter, n_pairs * t / nt, n_pairs * (t + 1) / nt);
+            scatter(0, n_pairs / nt);
+            for (auto &x : th) x.join();
         }
     }
     clk.mark("scatter");

@@ -201,6 +201,11 @@ int saln_nw_plan_create(saln_context *ctx, const uint64_t *q_off, uint64_t n_q,
     p->cigar_off.resize(n_pairs + 1);
     std::vector<NwPairDesc> descs(n_pairs);
     uint64_t cig = 0;
+    // the range check and the variant depend on the shape only: batches of
+    // alike pairs (the usual case) decide once per shape, not per pair
+    uint64_t memo_lq = ~0ull, memo_ld = ~0ull;
+    bool memo_fit = false;
+    int memo_var = 0;
     for (uint64_t k = 0; k < n_pairs; ++k) {
         const uint64_t qi = pair_q ? pair_q[k] : k % n_q;
         const uint64_t di = pair_db ? pair_db[k] : k / n_q;
@@ -219,7 +224,13 @@ int saln_nw_plan_create(saln_context *ctx, const uint64_t *q_off, uint64_t n_q,
             set_error("sequence too long");
             return SALN_E_INVALID;
         }
-        if (!scores_fit_i32(p->sc, lq, ld)) {
+        if (lq != memo_lq || ld != memo_ld) {
+            memo_lq = lq;
+            memo_ld = ld;
+            memo_fit = scores_fit_i32(p->sc, lq, ld);
+            memo_var = memo_fit ? choose_variant((uint32_t)lq, (uint32_t)ld, p->sc) : 0;
+        }
+        if (!memo_fit) {
             delete p;
             set_error("pair too long for these penalties: its scores could leave the engine's "
                       "int32 range");
@@ -228,7 +239,7 @@ int saln_nw_plan_create(saln_context *ctx, const uint64_t *q_off, uint64_t n_q,
         d.len_q = (uint32_t)lq;
         d.len_db = (uint32_t)ld;
         d.pair_id = (uint32_t)k;
-        d.variant = (uint32_t)choose_variant(d.len_q, d.len_db, p->sc);
+        d.variant = (uint32_t)memo_var;
         d.cigar_off = cig;
         p->cigar_off[k] = cig;
         cig += lq + ld;
@@ -266,17 +277,22 @@ int saln_nw_plan_create(saln_context *ctx, const uint64_t *q_off, uint64_t n_q,
         skey[k] = (uint64_t)(empty ? (uint32_t)kNumVariants : d.variant) << 56 |
                   ((~nch) & 0xFFFFFFull) << 32 | (uint32_t)~d.len_db;
     }
-    std::vector<uint32_t> order(n_pairs);
-    std::iota(order.begin(), order.end(), 0u);
-    if (!std::is_sorted(skey.begin(), skey.end()))
+    std::vector<uint32_t> order;
+    const bool in_order = std::is_sorted(skey.begin(), skey.end());
+    if (in_order) {
+        p->h_pairs = std::move(descs);  // plan order = results order: no copy
+    } else {
+        order.resize(n_pairs);
+        std::iota(order.begin(), order.end(), 0u);
         std::sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) {
             return skey[a] != skey[b] ? skey[a] < skey[b] : a < b;
         });
+        p->h_pairs.resize(n_pairs);
+    }
     clk.mark("plan: sort");
-    p->h_pairs.resize(n_pairs);
     uint64_t soff = 0, ooff = 0;
     for (uint64_t r = 0; r < n_pairs; ++r) {
-        NwPairDesc d = descs[order[r]];
+        NwPairDesc d = in_order ? p->h_pairs[r] : descs[order[r]];
         const bool empty = d.len_q == 0 || d.len_db == 0;
         if (!empty) {
             const Geom g = variant_geom((int)d.variant);
