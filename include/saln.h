@@ -235,6 +235,79 @@ int saln_nw_avsa_launch_geometry(int variant, uint64_t *chunk_pairs, uint64_t *g
 int saln_nw_avsa_status(saln_nw_avsa *a, uint32_t *flags);
 int saln_nw_avsa_destroy(saln_nw_avsa *a);
 
+/* ------------------------- NW: one long pair split by columns (multi-GPU, f3)
+ * The fill loop of one pair (needleman_wunsch_affine.rs:217-236) and its
+ * traceback (:242-334) cut into column spans, one per GPU (SURVEY.md §8(f)
+ * #3): span r owns query columns col_lo+1 .. col_hi (col_lo a multiple of
+ * 256), keeps only its part of the 1 B/cell parent mask, and runs the row
+ * fill's column stripes over every db row.  Its first stripe takes the
+ * boundary entering column col_lo+1 from the span's INBOX column, its last
+ * stripe publishes the boundary leaving column col_hi into its OUTBOX column;
+ * a caller moves outbox rows of span r into the inbox of span r+1 while both
+ * fills run (RCCL send/recv per row band, or a device copy).  Boundary
+ * columns hold one 8-byte element per db row r at element r (the engine's
+ * internal (H, I) form; an unpublished row reads 0x80000000 in its low word),
+ * saln_nw_span_boundary_elems elements per column.
+ *
+ * The traceback crosses the spans right to left: the span holding the end
+ * cell walks from it (entry SALN_SPAN_END) until the walk leaves its first
+ * column; its exit is the entry of the span to the left; the span where the
+ * walk ends reports kind SALN_SPAN_EXIT + event.  Concatenating the spans'
+ * op words in walk order (last span first, runs of one op merged at the
+ * seams) and reversing gives the pair's CIGAR. */
+typedef struct saln_nw_span saln_nw_span;
+/* walk cursor kinds (entry / exit) */
+#define SALN_SPAN_M 0         /* state known: M, I or D at (i, j) */
+#define SALN_SPAN_I 1
+#define SALN_SPAN_D 2
+#define SALN_SPAN_VIA_M 3     /* arrived at (i, j) by a diagonal step: state = its argmax */
+#define SALN_SPAN_VIA_I 4     /* arrived by a horizontal step: state from (i, j+1)'s I bits */
+#define SALN_SPAN_END 5       /* the pair's end cell, first end state (the reference's order) */
+#define SALN_SPAN_EXIT 8      /* exit: the walk ended; + 0 origin, + 1 panic, + 2 dead end */
+typedef struct {
+    int32_t i, j;   /* cell (db row, query column) */
+    int32_t kind;   /* SALN_SPAN_* */
+    uint32_t end_states; /* exit of the end cell's span: the end cell's state set
+                            (bit0 M, bit1 I, bit2 D), else 0 */
+} saln_nw_span_cursor;
+/* Elements (8 bytes each) of one boundary column for a db of len_db rows. */
+uint64_t saln_nw_span_boundary_elems(uint64_t len_db);
+/* d_boundary: caller-owned device buffer of (stripes + 1) boundary columns
+ * (saln_nw_span_info), column 0 the inbox, the last column the outbox; NULL:
+ * the span allocates it. */
+int saln_nw_span_create(saln_context *ctx, uint64_t len_q, uint64_t len_db, uint64_t col_lo,
+                        uint64_t col_hi, const saln_nw_scoring *scoring, void *d_boundary,
+                        saln_nw_span **out);
+int saln_nw_span_info(const saln_nw_span *s, uint64_t *mask_bytes, uint64_t *boundary_cols,
+                      uint64_t *ops_cap);
+/* Device addresses of the inbox (column 0) and outbox (last column). */
+int saln_nw_span_boundary(const saln_nw_span *s, void **inbox, void **outbox);
+/* Presets both boundary columns to "unpublished" on `stream`.  Must precede
+ * any write into the inbox and the fill. */
+int saln_nw_span_reset(saln_nw_span *s, void *stream);
+/* Launches the span's fill (q / db: the whole pair's sequences on the
+ * device).  A span with col_lo > 0 waits, row by row, for its inbox. */
+int saln_nw_span_fill(saln_nw_span *s, const uint8_t *d_q, const uint8_t *d_db, void *stream);
+/* Launches a one-wave kernel that returns once outbox rows row_lo .. row_hi
+ * are published (bounded by the wait limit: then the timeout flag is set),
+ * so work queued behind it on `stream` may read them. */
+int saln_nw_span_watch(saln_nw_span *s, uint64_t row_lo, uint64_t row_hi, void *stream);
+/* Walks this span from `entry` (host-blocking, after the fill completed);
+ * ops (host, ops_cap words) receive the run words in walk order (back to
+ * front); *exit the cursor where the walk left the span or ended. */
+int saln_nw_span_walk(saln_nw_span *s, const uint8_t *d_q, const uint8_t *d_db,
+                      const saln_nw_span_cursor *entry, saln_nw_span_cursor *exit, uint32_t *ops,
+                      uint64_t ops_cap, uint64_t *n_ops, void *stream);
+/* The span holding the end cell: score and panic status of the pair once the
+ * fill queued on `stream` has finished (host-blocking; SALN_E_INVALID on
+ * another span). */
+int saln_nw_span_score(saln_nw_span *s, int32_t *score, int32_t *status, void *stream);
+/* As saln_nw_plan_status / saln_nw_plan_set_wait_limit for the span's fill
+ * and watch waits. */
+int saln_nw_span_status(saln_nw_span *s, uint32_t *flags);
+int saln_nw_span_set_wait_limit(saln_nw_span *s, uint32_t polls);
+int saln_nw_span_destroy(saln_nw_span *s);
+
 /* ----------------------------------------------------------------------- WFA
  * Replaces `pub fn wfa_align(seq1: &Record, seq2: &Record, mode: Mode)`
  * (wfa.rs:23-42) with the reference's exact (quirky) semantics: wavefront

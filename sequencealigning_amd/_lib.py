@@ -57,6 +57,12 @@ class NwResult(C.Structure):
                 ("reserved", C.c_uint8)]
 
 
+class SpanCursor(C.Structure):
+    """saln_nw_span_cursor: a span walk's entry / exit."""
+    _fields_ = [("i", C.c_int32), ("j", C.c_int32), ("kind", C.c_int32),
+                ("end_states", C.c_uint32)]
+
+
 # numpy view of saln_nw_result
 RESULT_DTYPE = [("score", "<i4"), ("status", "<i4"), ("cigar_len", "<u4"), ("end_states", "u1"),
                 ("printed", "u1"), ("flags", "u1"), ("reserved", "u1")]
@@ -82,6 +88,10 @@ EXPORTS = [
     "saln_nw_plan_status", "saln_nw_plan_set_wait_limit",
     "saln_nw_avsa_create", "saln_nw_avsa_execute", "saln_nw_avsa_info", "saln_nw_avsa_destroy",
     "saln_nw_avsa_status", "saln_nw_avsa_launch_geometry",
+    "saln_nw_span_boundary_elems", "saln_nw_span_create", "saln_nw_span_info",
+    "saln_nw_span_boundary", "saln_nw_span_reset", "saln_nw_span_fill", "saln_nw_span_watch",
+    "saln_nw_span_walk", "saln_nw_span_score", "saln_nw_span_status",
+    "saln_nw_span_set_wait_limit", "saln_nw_span_destroy",
     "saln_wfa_align_batch", "saln_wfa_render", "saln_wfa_plan_create", "saln_wfa_execute",
     "saln_wfa_plan_destroy",
     "saln_wfa_affine_batch", "saln_wfa_affine_plan_create", "saln_wfa_affine_execute",
@@ -163,6 +173,21 @@ def lib() -> C.CDLL:
         L.saln_nw_avsa_execute.argtypes = [vp, vp, vp, vp, vp]
         L.saln_nw_avsa_info.argtypes = [vp, u64p, u64p]
         L.saln_nw_avsa_destroy.argtypes = [vp]
+        L.saln_nw_span_boundary_elems.argtypes = [C.c_uint64]
+        L.saln_nw_span_boundary_elems.restype = C.c_uint64
+        L.saln_nw_span_create.argtypes = [vp, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64,
+                                          C.POINTER(NwScoring), vp, C.POINTER(vp)]
+        L.saln_nw_span_info.argtypes = [vp, u64p, u64p, u64p]
+        L.saln_nw_span_boundary.argtypes = [vp, C.POINTER(vp), C.POINTER(vp)]
+        L.saln_nw_span_reset.argtypes = [vp, vp]
+        L.saln_nw_span_fill.argtypes = [vp, vp, vp, vp]
+        L.saln_nw_span_watch.argtypes = [vp, C.c_uint64, C.c_uint64, vp]
+        L.saln_nw_span_walk.argtypes = [vp, vp, vp, C.POINTER(SpanCursor), C.POINTER(SpanCursor),
+                                        u32p, C.c_uint64, u64p, vp]
+        L.saln_nw_span_score.argtypes = [vp, i32p, i32p, vp]
+        L.saln_nw_span_status.argtypes = [vp, u32p]
+        L.saln_nw_span_set_wait_limit.argtypes = [vp, C.c_uint32]
+        L.saln_nw_span_destroy.argtypes = [vp]
         L.saln_wfa_plan_create.argtypes = [vp, vp, C.c_uint64, vp, C.c_uint64, vp, vp,
                                            C.c_uint64, C.c_int32, C.c_uint32, C.c_uint32,
                                            C.POINTER(vp)]

@@ -102,6 +102,9 @@ struct SpecArgs {
     uint32_t *ops;           // kSpecOpsCap words per stripe
     const uint32_t *done;    // plan index -> walk finished by the spec passes
     int32_t pass;
+    // column-span walks (nw_span.cpp): span != 0 stops the walk only where
+    // it leaves column span_c0 + 1 (the span's first), not at every stripe edge
+    int32_t span, span_c0;
 };
 
 // Kernel geometry of one fill variant: G lanes per pair, K query columns per

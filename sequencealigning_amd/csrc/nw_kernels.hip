@@ -857,7 +857,9 @@ __global__ __launch_bounds__(64 * NWV) void nw_traceback_coop_kernel(
         const bool edge = st != kStD && lim_j < 0;
         uint32_t eq0 = 0;
         if constexpr (kSpec) {
-            if (edge) {  // the crossing step is this stripe's last op
+            // the crossing step is this stripe's last op (a span walk: only
+            // where it leaves the span's first column)
+            if (edge && (!sa.span || c_lo - 1 <= sa.span_c0)) {
                 if (st == kStM) {
                     push((kLay == 2 ? qwin[j - c_lo + 1] == dwin[i - r_lo + 1] : (code(i, j) >> 7) != 0)
                              ? SALN_CIGAR_EQ : SALN_CIGAR_X, 1);
@@ -2918,6 +2920,57 @@ hipError_t launch_traceback_spec(const NwPairDesc *pairs, SpecArgs sa, uint32_t 
         sa.done = done;
         nw_spec_copy_kernel<<<dim3(n_blocks), dim3(64), 0, stream>>>(pairs, sa, results, cigar);
     }
+    return hipGetLastError();
+}
+
+// Column spans (nw_span.cpp): one walk from the entry in sa.stripes[1]
+// (pass 2 reads the previous pass's exit slot) to where it leaves the span.
+hipError_t launch_span_walk(const NwPairDesc *pairs, SpecArgs sa, const uint8_t *qs,
+                            const uint8_t *ds, const uint8_t *mask, const int32_t *end_h,
+                            Scoring sc, hipStream_t stream) {
+    constexpr int kLoaders = 4;
+    constexpr int32_t rows = 296;
+    const size_t lds = (size_t)(rows + 1) * kCoopLine + 16 + 272 + (size_t)rows + 16;
+    static const hipError_t attr = hipFuncSetAttribute(
+        (const void *)nw_traceback_coop_kernel<kLoaders, 2, true>,
+        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    if (attr != hipSuccess) return attr;
+    sa.pass = 2;
+    sa.span = 1;
+    nw_traceback_coop_kernel<kLoaders, 2, true><<<dim3(1), dim3(64 * kLoaders), lds, stream>>>(
+        pairs, 0, mask, end_h, nullptr, nullptr, sc, rows, qs, ds, sa);
+    return hipGetLastError();
+}
+
+// Returns once rows r0 .. r1 of a boundary column are published (the row
+// fill's 8-byte (H~, I~) elements, preset to kColEmpty), so that work queued
+// behind it (an RCCL send of those rows) reads them.  Bounded like the fill's
+// own waits: err[1] polls, then err[0] bit 0.
+__global__ __launch_bounds__(64) void nw_span_watch_kernel(const int2 *__restrict__ col,
+                                                           uint32_t r0, uint32_t r1,
+                                                           uint32_t *__restrict__ err) {
+    const uint32_t lim = err[1];
+    uint32_t spins = 0;
+    bool failed = false;
+    for (uint32_t r = r0 + threadIdx.x; r <= r1 && !failed; r += 64) {
+        for (;;) {
+            const uint64_t v = __hip_atomic_load((const uint64_t *)(col + r), __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT);
+            if ((uint32_t)v != kColEmpty) break;
+            if (++spins > lim) {
+                failed = true;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(8);
+        }
+    }
+    if (__builtin_amdgcn_ballot_w64(failed) && threadIdx.x == 0) atomicOr(err, 1u);
+}
+
+hipError_t launch_span_watch(const int2 *col, uint32_t r0, uint32_t r1, uint32_t *err,
+                             hipStream_t stream) {
+    if (r1 < r0) return hipSuccess;
+    nw_span_watch_kernel<<<dim3(1), dim3(64), 0, stream>>>(col, r0, r1, err);
     return hipGetLastError();
 }
 

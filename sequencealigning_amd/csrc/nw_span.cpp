@@ -1,0 +1,301 @@
+// Column spans of one long pair (include/saln.h "one long pair split by
+// columns").
+//
+// The reference fills one pair row by row, query inner
+// (needleman_wunsch_affine.rs:217-236), and walks it back from the end cell
+// (:242-334).  A span is the row fill (nw_fill_rows_kernel) restricted to the
+// column stripes of query columns col_lo+1 .. col_hi: its work items are the
+// pair's 256-column chunks of that range, and its kernel arguments are
+// rebased so that
+//   - the stripe left of its first one reads boundary column 0 (the inbox),
+//     which a peer fills row by row while the fill runs (the same polled
+//     8-byte elements as between two stripes of one GPU), and its last stripe
+//     publishes into the last column (the outbox);
+//   - its mask holds only its own 256-column tiles (a pair whose 1 B/cell
+//     mask exceeds one GPU's HBM spreads over the spans' GPUs).
+// The walk is the speculative stripe walker with a known entry (the exit of
+// the span to the right) that stops only where it leaves the span.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <vector>
+
+#include "nw_host.hpp"
+
+namespace saln {
+bool scores_fit_i32(const Scoring &s, uint64_t lq, uint64_t ld);
+}
+using namespace saln;
+
+struct saln_nw_span {
+    saln_context *ctx = nullptr;
+    Scoring sc{};
+    uint32_t lq = 0, ld = 0, col_lo = 0, col_hi = 0;
+    int K = 2;                  // row-fill columns per lane (stripe width 64 K)
+    uint32_t g0 = 0, nst = 0;   // first stripe (pair-wide index), stripes
+    uint32_t t0 = 0, ntiles = 0;  // first 256-column mask tile, tiles
+    uint64_t scol = 0, cs = 0, mask_bytes = 0, ops_cap = 0;
+    bool own_bnd = false;
+    int2 *d_bnd = nullptr;      // nst + 1 boundary columns
+    uint8_t *d_mask = nullptr;
+    NwPairDesc *d_pair = nullptr;
+    uint2 *d_work = nullptr;
+    uint32_t n_work = 0;
+    uint32_t *d_err = nullptr;  // [flags, wait limit] (the fill's and the watch's waits)
+    int32_t *d_endh = nullptr;
+    uint2 *d_blocks = nullptr;
+    SpecPair *d_sp = nullptr;
+    SpecStripe *d_rec = nullptr;  // [0] this span's walk, [1] its entry (pass-2 exit slot)
+    uint32_t *d_ops = nullptr;
+
+    // kernel arguments rebased to the span: tile t of the pair at d_mask +
+    // (t - t0) * cs; stripe g's output column g - g0 + 1 (its input g - g0)
+    uint8_t *mask_arg() const { return (uint8_t *)((uintptr_t)d_mask - (uint64_t)t0 * cs); }
+    int2 *scratch_arg() const {
+        return (int2 *)((uintptr_t)d_bnd + (uint64_t)(1 - (int64_t)g0) * scol * sizeof(int2));
+    }
+    int2 *inbox() const { return d_bnd; }
+    int2 *outbox() const { return d_bnd + (uint64_t)nst * scol; }
+    void release() {
+        for (void *b : {(void *)d_mask, (void *)d_pair, (void *)d_work, (void *)d_err,
+                        (void *)d_endh, (void *)d_blocks, (void *)d_sp, (void *)d_rec,
+                        (void *)d_ops})
+            if (b) dev_free(ctx, b);
+        if (own_bnd && d_bnd) dev_free(ctx, d_bnd);
+    }
+};
+
+extern "C" {
+
+uint64_t saln_nw_span_boundary_elems(uint64_t len_db) {
+    return len_db > 0xFFFFFFFFull ? 0 : scratch_col((uint32_t)len_db);
+}
+
+int saln_nw_span_create(saln_context *ctx, uint64_t len_q, uint64_t len_db, uint64_t col_lo,
+                        uint64_t col_hi, const saln_nw_scoring *scoring, void *d_boundary,
+                        saln_nw_span **out) {
+    if (!ctx || !out) return SALN_E_INVALID;
+    *out = nullptr;
+    if (len_q <= 256 || len_db == 0 || len_q > 0x7FFFFFFFull || len_db > 0x7FFFFFFFull) {
+        set_error("span: a pair of more than 256 query columns and at least one db row "
+                  "(shorter pairs: saln_nw_plan_create)");
+        return SALN_E_INVALID;
+    }
+    if (col_lo % 256 || col_lo >= col_hi || col_hi > len_q || (col_hi != len_q && col_hi % 256)) {
+        set_error("span: columns col_lo+1 .. col_hi with col_lo and col_hi (unless len_q) "
+                  "multiples of 256");
+        return SALN_E_INVALID;
+    }
+    const Scoring sc = scoring_or_default(scoring);
+    if (!scores_fit_i32(sc, len_q, len_db)) {
+        set_error("pair too long for these penalties: its scores could leave the engine's int32 "
+                  "range");
+        return SALN_E_INVALID;
+    }
+    HIP_TRY(hipSetDevice(ctx->device));
+    auto *s = new saln_nw_span;
+    s->ctx = ctx;
+    s->sc = sc;
+    s->lq = (uint32_t)len_q;
+    s->ld = (uint32_t)len_db;
+    s->col_lo = (uint32_t)col_lo;
+    s->col_hi = (uint32_t)col_hi;
+    // K = 1 while every 64-column stripe of the span has a SIMD to itself
+    s->K = stripe_rows_k((col_hi - col_lo + 63) / 64);
+    const uint32_t W = 64u * (uint32_t)s->K;
+    s->g0 = s->col_lo / W;
+    s->nst = (s->col_hi + W - 1) / W - s->g0;
+    s->t0 = s->col_lo / 256;
+    s->ntiles = (s->col_hi + 255) / 256 - s->t0;
+    s->scol = scratch_col(s->ld);
+    s->cs = ((uint64_t)s->ld + 63) * 256;  // the plan's tile stride (nw_host.cpp)
+    s->mask_bytes = (uint64_t)s->ntiles * s->cs;
+    s->ops_cap = (uint64_t)(s->col_hi - s->col_lo) + s->ld + 16;
+    auto fail = [&](hipError_t e, const char *what) {
+        set_error(std::string("span: ") + what + ": " + hipGetErrorString(e));
+        s->release();
+        delete s;
+        return SALN_E_HIP;
+    };
+    hipError_t e;
+    if (d_boundary) {
+        s->d_bnd = (int2 *)d_boundary;
+    } else {
+        s->own_bnd = true;
+        if ((e = dev_alloc(ctx, (void **)&s->d_bnd, (s->nst + 1) * s->scol * sizeof(int2))) != hipSuccess)
+            return fail(e, "boundary columns");
+    }
+    NwPairDesc d;
+    std::memset(&d, 0, sizeof d);
+    d.len_q = s->lq;
+    d.len_db = s->ld;
+    d.mask_rs = 256;
+    d.mask_bs = 4;
+    d.mask_cs = s->cs;
+    d.variant = kStripeVariant;
+    std::vector<uint2> work;
+    for (uint32_t t = 0; t < s->ntiles; ++t) work.push_back(make_uint2(0u, s->t0 + t));
+    s->n_work = (uint32_t)work.size();
+    const uint32_t err0[2] = {0u, kWaitLimitDefault};
+    const uint2 blk = make_uint2(0u, 0u);
+    const SpecPair sp{0u, 1u, 0u, 0u};
+    if ((e = dev_alloc(ctx, (void **)&s->d_mask, s->mask_bytes + 64)) != hipSuccess)
+        return fail(e, "mask");
+    if ((e = dev_alloc(ctx, (void **)&s->d_pair, sizeof d)) != hipSuccess ||
+        (e = hipMemcpy(s->d_pair, &d, sizeof d, hipMemcpyHostToDevice)) != hipSuccess ||
+        (e = dev_alloc(ctx, (void **)&s->d_work, work.size() * sizeof(uint2))) != hipSuccess ||
+        (e = hipMemcpy(s->d_work, work.data(), work.size() * sizeof(uint2), hipMemcpyHostToDevice)) != hipSuccess ||
+        (e = dev_alloc(ctx, (void **)&s->d_err, sizeof err0)) != hipSuccess ||
+        (e = hipMemcpy(s->d_err, err0, sizeof err0, hipMemcpyHostToDevice)) != hipSuccess ||
+        (e = dev_alloc(ctx, (void **)&s->d_endh, sizeof(int32_t))) != hipSuccess ||
+        (e = dev_alloc(ctx, (void **)&s->d_blocks, sizeof blk)) != hipSuccess ||
+        (e = hipMemcpy(s->d_blocks, &blk, sizeof blk, hipMemcpyHostToDevice)) != hipSuccess ||
+        (e = dev_alloc(ctx, (void **)&s->d_sp, sizeof sp)) != hipSuccess ||
+        (e = hipMemcpy(s->d_sp, &sp, sizeof sp, hipMemcpyHostToDevice)) != hipSuccess ||
+        (e = dev_alloc(ctx, (void **)&s->d_rec, 2 * sizeof(SpecStripe))) != hipSuccess ||
+        (e = dev_alloc(ctx, (void **)&s->d_ops, (s->ops_cap + 8) * sizeof(uint32_t))) != hipSuccess)
+        return fail(e, "tables");
+    *out = s;
+    return SALN_OK;
+}
+
+int saln_nw_span_info(const saln_nw_span *s, uint64_t *mask_bytes, uint64_t *boundary_cols,
+                      uint64_t *ops_cap) {
+    if (!s) return SALN_E_INVALID;
+    if (mask_bytes) *mask_bytes = s->mask_bytes;
+    if (boundary_cols) *boundary_cols = (uint64_t)s->nst + 1;
+    if (ops_cap) *ops_cap = s->ops_cap;
+    return SALN_OK;
+}
+
+int saln_nw_span_boundary(const saln_nw_span *s, void **inbox, void **outbox) {
+    if (!s) return SALN_E_INVALID;
+    if (inbox) *inbox = s->inbox();
+    if (outbox) *outbox = s->outbox();
+    return SALN_OK;
+}
+
+int saln_nw_span_reset(saln_nw_span *s, void *stream) {
+    if (!s) return SALN_E_INVALID;
+    HIP_TRY(hipSetDevice(s->ctx->device));
+    // every column: the inbox, the columns between the span's stripes, the outbox
+    HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)s->d_bnd, (int)0x80000000u,
+                              2 * (s->nst + 1) * s->scol, resolve_stream(stream, s->ctx)));
+    return SALN_OK;
+}
+
+int saln_nw_span_fill(saln_nw_span *s, const uint8_t *d_q, const uint8_t *d_db, void *stream) {
+    if (!s || !d_q || !d_db) return SALN_E_INVALID;
+    HIP_TRY(hipSetDevice(s->ctx->device));
+    HIP_TRY(launch_fill_stripes(s->d_pair, s->d_work, s->n_work, d_q, d_db, s->mask_arg(),
+                                s->scratch_arg(), nullptr, s->d_err, s->d_endh, s->sc,
+                                0 /* walk codes */, 2 /* row-major tiles */, s->K,
+                                resolve_stream(stream, s->ctx)));
+    return SALN_OK;
+}
+
+int saln_nw_span_watch(saln_nw_span *s, uint64_t row_lo, uint64_t row_hi, void *stream) {
+    if (!s || row_lo < 1 || row_hi > s->ld || row_lo > row_hi) return SALN_E_INVALID;
+    HIP_TRY(hipSetDevice(s->ctx->device));
+    HIP_TRY(launch_span_watch(s->outbox(), (uint32_t)row_lo, (uint32_t)row_hi, s->d_err,
+                              resolve_stream(stream, s->ctx)));
+    return SALN_OK;
+}
+
+int saln_nw_span_walk(saln_nw_span *s, const uint8_t *d_q, const uint8_t *d_db,
+                      const saln_nw_span_cursor *entry, saln_nw_span_cursor *exit, uint32_t *ops,
+                      uint64_t ops_cap, uint64_t *n_ops, void *stream) {
+    if (!s || !d_q || !d_db || !entry || !exit || !n_ops) return SALN_E_INVALID;
+    *n_ops = 0;
+    if (entry->kind >= SALN_SPAN_EXIT) {  // the walk ended in a span to the right
+        *exit = *entry;
+        return SALN_OK;
+    }
+    const bool end = entry->kind == SALN_SPAN_END;
+    const bool at_end = entry->i == (int32_t)s->ld && entry->j == (int32_t)s->lq;
+    if (entry->kind < 0 || entry->kind > SALN_SPAN_END || (end && !at_end) ||
+        entry->i < 0 || entry->i > (int32_t)s->ld || entry->j <= (int32_t)s->col_lo ||
+        entry->j > (int32_t)s->col_hi) {
+        set_error("span walk: entry outside the span");
+        return SALN_E_INVALID;
+    }
+    HIP_TRY(hipSetDevice(s->ctx->device));
+    hipStream_t st = resolve_stream(stream, s->ctx);
+    SpecStripe rec[2];
+    std::memset(rec, 0, sizeof rec);
+    rec[0].in_k = kSpecNone;  // no stored walk to keep
+    rec[1].out_i[1] = entry->i;
+    rec[1].out_j[1] = entry->j;
+    rec[1].out_k[1] = entry->kind;
+    HIP_TRY(hipMemcpyAsync(s->d_rec, rec, sizeof rec, hipMemcpyHostToDevice, st));
+    SpecArgs sa{s->d_blocks, s->d_sp, s->d_rec, s->d_ops, nullptr, 2, 1, (int32_t)s->col_lo};
+    HIP_TRY(launch_span_walk(s->d_pair, sa, d_q, d_db, s->mask_arg(), s->d_endh, s->sc, st));
+    HIP_TRY(hipMemcpyAsync(rec, s->d_rec, sizeof(SpecStripe), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    const uint64_t n = rec[0].nops;
+    if (n > s->ops_cap) {
+        set_error("span walk: op stream overflow");
+        return SALN_E_HIP;
+    }
+    if (ops && n > ops_cap) {
+        set_error("span walk: ops buffer too small (saln_nw_span_info ops_cap)");
+        return SALN_E_CAPACITY;
+    }
+    if (ops && n)
+        HIP_TRY(hipMemcpy(ops, s->d_ops, n * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    *n_ops = n;
+    exit->i = rec[0].out_i[0];
+    exit->j = rec[0].out_j[0];
+    exit->kind = rec[0].out_k[0];
+    exit->end_states = end ? rec[0].am_end : 0u;
+    return SALN_OK;
+}
+
+int saln_nw_span_score(saln_nw_span *s, int32_t *score, int32_t *status, void *stream) {
+    if (!s || s->col_hi != s->lq) {
+        set_error("span score: only the span holding the end cell has it");
+        return SALN_E_INVALID;
+    }
+    HIP_TRY(hipSetDevice(s->ctx->device));
+    HIP_TRY(hipStreamSynchronize(resolve_stream(stream, s->ctx)));
+    int32_t h = 0;
+    HIP_TRY(hipMemcpy(&h, s->d_endh, sizeof h, hipMemcpyDeviceToHost));
+    if (score) *score = h >> 1;  // V' = 2V + p (make_result, nw_kernels.hip)
+    if (status) *status = (h & 1) ? SALN_REF_PANIC_BOUNDARY : SALN_OK;
+    return SALN_OK;
+}
+
+int saln_nw_span_status(saln_nw_span *s, uint32_t *flags) {
+    if (flags) *flags = 0;
+    if (!s) return SALN_E_INVALID;
+    HIP_TRY(hipSetDevice(s->ctx->device));
+    HIP_TRY(hipDeviceSynchronize());
+    uint32_t v = 0;
+    HIP_TRY(hipMemcpy(&v, s->d_err, sizeof v, hipMemcpyDeviceToHost));
+    if (v) HIP_TRY(hipMemset(s->d_err, 0, sizeof v));  // read and clear
+    if (flags) *flags = v;
+    if (v & SALN_FLAG_WAIT_TIMEOUT) {
+        set_error("span: a boundary wait timed out (the fill's results are invalid)");
+        return SALN_E_DEVICE_WAIT;
+    }
+    return SALN_OK;
+}
+
+int saln_nw_span_set_wait_limit(saln_nw_span *s, uint32_t polls) {
+    if (!s) return SALN_E_INVALID;
+    HIP_TRY(hipSetDevice(s->ctx->device));
+    HIP_TRY(hipMemcpy(s->d_err + 1, &polls, sizeof polls, hipMemcpyHostToDevice));
+    return SALN_OK;
+}
+
+int saln_nw_span_destroy(saln_nw_span *s) {
+    if (!s) return SALN_OK;
+    (void)hipSetDevice(s->ctx->device);
+    (void)hipDeviceSynchronize();
+    s->release();
+    delete s;
+    return SALN_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,194 @@
+"""GPU: one long pair split by query columns (SURVEY.md §8(f) #3,
+saln_nw_span_* / sequencealigning_amd/span.py) against the oracle and the
+single-GPU plan path (n_w_align), on the box's one GPU: the spans' fills run
+concurrently and hand boundary rows over in bands (device copies behind
+watch kernels), or one after another; 2-process gloo relay and 1-rank RCCL
+runs of ShardedLongPair."""
+import multiprocessing as mp
+import os
+import socket
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _mut(rng, q, rate):
+    from nw_check import rand_seq
+    out = bytearray()
+    for c in q:
+        u = rng.random()
+        if u < rate / 2:
+            out.append(ord("ACGT"[(int(rng.integers(1, 4)) + "ACGT".index(chr(c))) % 4]))
+        elif u < 3 * rate / 4:
+            out.append(c)
+            out += rand_seq(rng, 1)
+        elif u < rate:
+            continue
+        else:
+            out.append(c)
+    return bytes(out)
+
+
+def _same(a, b):
+    assert (a.score, a.status, a.end_states, a.printed) == (b.score, b.status, b.end_states,
+                                                            b.printed)
+    assert a.cigar == b.cigar
+
+
+def _vs_oracle(r, qs, ds):
+    from oracle import refcpu
+
+    from sequencealigning_amd.nw import cigar_ops_string
+    o = refcpu.nw(qs, ds, literal_dfs=False)
+    assert r.score == o.score and (r.status == 2) == o.panics and r.end_states == o.end_states
+    assert r.printed == (o.first_ops is not None)
+    if r.printed:
+        assert cigar_ops_string(r.cigar) == o.first_ops
+
+
+@pytest.mark.parametrize("pipelined", [True, False])
+def test_span_chain_matches_oracle(pipelined):
+    """2-4 spans of mutated and iid pairs (up to 1.6 kbp): score, panic
+    status, end states and first printed alignment equal the oracle's."""
+    import sequencealigning_amd as saln
+    from nw_check import rand_seq
+
+    from sequencealigning_amd.span import nw_align_long_spans
+    rng = np.random.default_rng(41)
+    cases = []
+    for lq, rate in [(1600, 0.05), (1100, 0.15), (800, 0.0)]:
+        q = rand_seq(rng, lq)
+        cases.append((q, _mut(rng, q, rate)))
+    cases.append((rand_seq(rng, 900), rand_seq(rng, 1200)))  # iid, tall
+    cases.append((rand_seq(rng, 1300), rand_seq(rng, 150)))  # iid, wide: end gaps, panics
+    cases.append((b"ACGTN" * 120, b"AC" * 40))
+    for qs, ds in cases:
+        for n in (2, 3, 4):
+            if (len(qs) + 255) // 256 < n:
+                continue
+            r = nw_align_long_spans(qs, ds, n, band_rows=128, pipelined=pipelined)
+            _vs_oracle(r, qs, ds)
+            _same(r, saln.n_w_align(qs, ds))
+
+
+def test_span_chain_long_pairs_match_plan():
+    """20-30 kbp pairs over 3-8 spans (pipelined, 2,048-row bands) give the
+    single-GPU plan's result word for word; a mask-free oracle pins the score."""
+    import sequencealigning_amd as saln
+    from nw_check import rand_seq
+    from oracle import refcpu
+
+    from sequencealigning_amd.span import nw_align_long_spans
+    rng = np.random.default_rng(42)
+    for lq, ld_rate, n in [(30_000, 0.05, 8), (20_000, 0.10, 3)]:
+        q = rand_seq(rng, lq)
+        d = _mut(rng, q, ld_rate)
+        r = nw_align_long_spans(q, d, n, band_rows=2048)
+        _same(r, saln.n_w_align(q, d))
+        sc, es, pan = refcpu.nw_score_linear(q, d)
+        assert r.score == sc and r.end_states == es and (r.status == 2) == pan
+
+
+def test_span_injected_timeout_raises():
+    """A span whose inbox never arrives (no left neighbour ran) with a wait
+    limit of 0 reports SALN_E_DEVICE_WAIT instead of hanging."""
+    import torch
+
+    from sequencealigning_amd import _lib
+    from sequencealigning_amd.span import NwSpan
+    q = torch.randint(65, 70, (1024,), dtype=torch.uint8, device="cuda")
+    d = torch.randint(65, 70, (500,), dtype=torch.uint8, device="cuda")
+    sp = NwSpan(1024, 500, 512, 1024, device=0)
+    sp.set_wait_limit(0)
+    sp.reset()
+    sp.fill(q, d)
+    with pytest.raises(_lib.SalnError, match="E_DEVICE_WAIT"):
+        sp.check()
+    sp.set_wait_limit(1 << 24)
+    assert sp.status() == 0  # read and clear
+    sp.close()
+
+
+def _relay_worker(rank, world, port, q, d, out):
+    import torch
+    import torch.distributed as dist
+
+    from sequencealigning_amd.span import ShardedLongPair
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    sp = ShardedLongPair(q, d, device=0, band_rows=1000)
+    r = sp.align()
+    sp.close()
+    if rank == 0:
+        out.put((r.score, r.status, r.end_states, r.printed, r.cigar))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_sharded_long_pair_gloo_relay_gpu():
+    """Two ranks (gloo; both on cuda:0) each fill one span of a 6 kbp pair on
+    the GPU, boundary bands relayed through host memory: the result on rank 0
+    equals the single-process plan's."""
+    import sequencealigning_amd as saln
+    from nw_check import rand_seq
+    rng = np.random.default_rng(43)
+    q = rand_seq(rng, 6000)
+    d = _mut(rng, q, 0.08)
+    ctx = mp.get_context("spawn")
+    qu = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_relay_worker, args=(r, 2, port, q, d, qu)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = qu.get(timeout=300)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    want = saln.n_w_align(q, d)
+    assert got == (want.score, want.status, want.end_states, want.printed, want.cigar)
+
+
+def _nccl_worker(port, q, d, out):
+    import torch
+    import torch.distributed as dist
+
+    from sequencealigning_amd.span import ShardedLongPair
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    sp = ShardedLongPair(q, d, device=0)
+    r = sp.align()
+    sp.close()
+    out.put((r.score, r.status, r.end_states, r.printed, r.cigar))
+    dist.destroy_process_group()
+
+
+def test_sharded_long_pair_rccl_single_rank():
+    """ShardedLongPair's nccl (RCCL) path on one rank: the fill through the
+    stream-ordered pipeline, the broadcasts and the gather of the run words
+    over RCCL; equal to the plan path."""
+    import sequencealigning_amd as saln
+    from nw_check import rand_seq
+    rng = np.random.default_rng(44)
+    q = rand_seq(rng, 3000)
+    d = _mut(rng, q, 0.05)
+    ctx = mp.get_context("spawn")
+    qu = ctx.Queue()
+    p = ctx.Process(target=_nccl_worker, args=(_free_port(), q, d, qu))
+    p.start()
+    got = qu.get(timeout=300)
+    p.join(timeout=120)
+    assert p.exitcode == 0
+    want = saln.n_w_align(q, d)
+    assert got == (want.score, want.status, want.end_states, want.printed, want.cigar)
