@@ -86,8 +86,9 @@ class LoadReport:
 
 def code_object(obj: str = OBJ, out_dir: str = "/tmp") -> str:
     """The gfx950 code object inside a hipcc object file's offload bundle."""
-    fat = os.path.join(out_dir, "saln_isa_check.fatbin")
-    co = os.path.join(out_dir, "saln_isa_check.co")
+    # per process: parallel test workers must not overwrite each other's files
+    fat = os.path.join(out_dir, f"saln_isa_check.{os.getpid()}.fatbin")
+    co = os.path.join(out_dir, f"saln_isa_check.{os.getpid()}.co")
     subprocess.run([f"{LLVM}/llvm-objcopy", f"--dump-section=.hip_fatbin={fat}", obj, "/dev/null"],
                    check=True, capture_output=True)
     subprocess.run([f"{LLVM}/clang-offload-bundler", "--type=o",
