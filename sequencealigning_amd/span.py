@@ -159,7 +159,11 @@ class NwSpan:
         import torch
         if stream is None:
             return _lib.torch_stream(self.device)
-        return stream.cuda_stream if isinstance(stream, torch.cuda.Stream) else stream
+        if isinstance(stream, torch.cuda.Stream):
+            # torch's null stream is handle 0, which the C ABI reads as "the
+            # context's own stream": pass it as hipStreamLegacy (_lib.torch_stream)
+            return stream.cuda_stream or _lib.HIP_STREAM_LEGACY
+        return stream
 
     def reset(self, stream=None) -> None:
         _lib.check(_lib.lib().saln_nw_span_reset(self._h, self._s(stream)), "saln_nw_span_reset")
