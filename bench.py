@@ -24,10 +24,12 @@ and `cpu_baseline`:
       (SURVEY.md §8(f) row 4; not reference parity) (N = 1);
   c4  configs[3]: one 100 kbp pair, fill + traceback, + the linear-memory
       oracle on the host cores (N = 1);
+  c4_spans  the same pair as 8 column spans (SURVEY.md §8(f) row 3's layout,
+      all on this GPU: the band hand-off's cost; 1/8 of the mask per span) (N = 1);
   host_path: configs[1] through the host-buffer C ABI (PCIe-inclusive; never
       the value) (N = 1).
 
-    python bench.py --gpus N --steps K --warmup W [--legs c5,c1,c3,c3_affine,c4,host|none]
+    python bench.py --gpus N --steps K --warmup W [--legs c5,c1,c3,c3_affine,c4,c4_spans,host|none]
 
 With --gpus N > 1 and no WORLD_SIZE in the environment this process starts
 the N ranks itself (torch.distributed.run on 127.0.0.1, as a child process;
@@ -58,7 +60,7 @@ VALU_PEAK_TOPS = 1024 * 32 * 2.4e9 / 1e12  # 78.6 T lane-ops/s
 VALU_PK_TOPS = 1024 * 16 * 2.4e9 / 1e12
 N_PAIRS, LQ, LD = 100_000, 150, 150
 SEED = 0x5EED0002
-ALL_LEGS = ("c5", "c1", "c3", "c3_affine", "c4", "host")
+ALL_LEGS = ("c5", "c1", "c3", "c3_affine", "c4", "c4_spans", "host")
 PMC_FILES = ("pmc_traffic.json", "pmc_legs.json")  # under profiles/
 
 
@@ -439,6 +441,69 @@ def leg_c4(torch, saln, reps=3, cpu=True):
     return out
 
 
+def leg_c4_spans(torch, saln, n_spans=8, reps=3, band_rows=4096):
+    """configs[3]'s pair split by query columns into `n_spans` spans
+    (span.py SpanChain): the spans' fills run
+    concurrently on this GPU and hand their boundary rows over in bands
+    (device copies behind watch kernels), then the walk crosses the spans
+    right to left.  The 8-GPU layout on one GPU: each span keeps 1/8 of the
+    mask; the time is the hand-off protocol's cost over the one-plan fill
+    (c4).  Checked word for word against the plan path (n_w_align)."""
+    from sequencealigning_amd import synth
+    from sequencealigning_amd.span import SpanChain
+    q = synth.random_bases(0x5EED0003, 100_000).tobytes()
+    d = synth.mutate(q, 0.05, seed=100_000)
+    ch = SpanChain(q, d, n_spans, band_rows=band_rows)
+    fills, walks, r = [], [], None
+    for k in range(1 + reps):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        ch.fill(pipelined=True)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        r = ch.walk()
+        t2 = time.perf_counter()
+        if k:
+            fills.append(t1 - t0)
+            walks.append(t2 - t1)
+    # each span alone on the GPU (its inbox complete): the fill time of a GPU
+    # that holds one span, as on an R-GPU node (one span per GPU)
+    main = torch.cuda.current_stream()
+    alone = []
+    for k in range(2):
+        evs = []
+        for s in ch.spans:
+            s.reset(main)
+        for r, s in enumerate(ch.spans):
+            if r:
+                s.inbox.copy_(ch.spans[r - 1].outbox)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(main)
+            s.fill(ch.q, ch.d, main)
+            e1.record(main)
+            evs.append((e0, e1))
+        torch.cuda.synchronize()
+        ch.check()
+        if k:
+            alone = [a.elapsed_time(b) for a, b in evs]
+    span_mask = max(s.mask_bytes for s in ch.spans)
+    ch.close()
+    torch.cuda.empty_cache()
+    want = saln.n_w_align(q, d)
+    fill_s, walk_s = float(np.mean(fills)), float(np.mean(walks))
+    cells = len(q) * len(d)
+    return {"workload": f"configs[3]'s pair as {n_spans} column spans on one GPU, "
+                        f"{band_rows}-row boundary bands", "value": round(cells / (fill_s + walk_s) / 1e9, 1),
+            "unit": "GCUPS", "fill_ms": round(fill_s * 1e3, 3), "walk_ms": round(walk_s * 1e3, 3),
+            "executes": 1 + reps + 2, "span_fill_alone_ms": [round(x, 3) for x in alone],
+            "mask_bytes_per_span": int(span_mask),
+            "mask_bytes_pair": cells,
+            "matches_plan": bool((r.score, r.status, r.end_states, r.printed, r.cigar) ==
+                                 (want.score, want.status, want.end_states, want.printed,
+                                  want.cigar)),
+            "checked": "score, status, end states and the first printed CIGAR vs n_w_align"}
+
+
 _C3_PAIRS = {}
 
 
@@ -798,6 +863,8 @@ def main() -> None:
                 r = leg_c3_affine(torch, saln, cpu=cpu)
             elif leg == "c4":
                 r = leg_c4(torch, saln, cpu=cpu)
+            elif leg == "c4_spans":
+                r = leg_c4_spans(torch, saln)
             elif leg == "host":
                 r = leg_host(saln)
             else:
