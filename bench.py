@@ -474,9 +474,9 @@ def leg_c4_spans(torch, saln, n_spans=8, reps=3, band_rows=4096):
         evs = []
         for s in ch.spans:
             s.reset(main)
-        for r, s in enumerate(ch.spans):
-            if r:
-                s.inbox.copy_(ch.spans[r - 1].outbox)
+        for k_s, s in enumerate(ch.spans):
+            if k_s:
+                s.inbox.copy_(ch.spans[k_s - 1].outbox)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(main)
             s.fill(ch.q, ch.d, main)
