@@ -105,6 +105,10 @@ struct SpecArgs {
     // column-span walks (nw_span.cpp): span != 0 stops the walk only where
     // it leaves column span_c0 + 1 (the span's first), not at every stripe edge
     int32_t span, span_c0;
+    // speculative passes over a span's stripes: stripe entry_s1 - 1 (the
+    // span's rightmost) takes its entry from the record after it on every
+    // pass (0: none)
+    int32_t entry_s1;
 };
 
 // Kernel geometry of one fill variant: G lanes per pair, K query columns per

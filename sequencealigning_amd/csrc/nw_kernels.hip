@@ -683,7 +683,11 @@ __global__ __launch_bounds__(64 * NWV) void nw_traceback_coop_kernel(
         // every wave reads the same entry (nothing writes it in this pass)
         const int32_t lqp = (int32_t)p.len_q, ldp = (int32_t)p.len_db;
         const int32_t par = (sa.pass - 1) & 1, cur = sa.pass & 1;
-        if (s_id == (lqp - 1) / kCoopLine) {
+        if (sa.entry_s1 && s_id == sa.entry_s1 - 1) {  // a span's rightmost stripe: its given entry
+            ei = rec[1].out_i[par];
+            ej = rec[1].out_j[par];
+            ek = rec[1].out_k[par];
+        } else if (s_id == (lqp - 1) / kCoopLine) {
             ei = ldp;
             ej = lqp;
             ek = kSpecEnd;
@@ -2939,6 +2943,28 @@ hipError_t launch_span_walk(const NwPairDesc *pairs, SpecArgs sa, const uint8_t 
     sa.span = 1;
     nw_traceback_coop_kernel<kLoaders, 2, true><<<dim3(1), dim3(64 * kLoaders), lds, stream>>>(
         pairs, 0, mask, end_h, nullptr, nullptr, sc, rows, qs, ds, sa);
+    return hipGetLastError();
+}
+
+// Column spans: `passes` speculative passes over the span's walker stripes
+// (one block each, sa.blocks), the rightmost entered at sa.entry_s1's given
+// entry; the host links the stored walks (nw_span.cpp).
+hipError_t launch_span_spec(const NwPairDesc *pairs, SpecArgs sa, uint32_t n_blocks, int passes,
+                            const uint8_t *qs, const uint8_t *ds, const uint8_t *mask,
+                            const int32_t *end_h, Scoring sc, hipStream_t stream) {
+    constexpr int kLoaders = 4;
+    constexpr int32_t rows = 296;
+    const size_t lds = (size_t)(rows + 1) * kCoopLine + 16 + 272 + (size_t)rows + 16;
+    static const hipError_t attr = hipFuncSetAttribute(
+        (const void *)nw_traceback_coop_kernel<kLoaders, 2, true>,
+        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    if (attr != hipSuccess) return attr;
+    sa.span = 0;  // every stripe stops at its own left edge
+    for (int k = 1; k <= passes; ++k) {
+        sa.pass = k;
+        nw_traceback_coop_kernel<kLoaders, 2, true><<<dim3(n_blocks), dim3(64 * kLoaders), lds, stream>>>(
+            pairs, 0, mask, end_h, nullptr, nullptr, sc, rows, qs, ds, sa);
+    }
     return hipGetLastError();
 }
 

@@ -13,11 +13,14 @@
 //     publishes into the last column (the outbox);
 //   - its mask holds only its own 256-column tiles (a pair whose 1 B/cell
 //     mask exceeds one GPU's HBM spreads over the spans' GPUs).
-// The walk is the speculative stripe walker with a known entry (the exit of
-// the span to the right) that stops only where it leaves the span.
+// The walk enters at a known cell (the exit of the span to the right): the
+// speculative stripe walker's passes over the span's 256-column stripes,
+// linked on the host (span_walk_spec), or, when they do not link, one walk
+// through the span that stops only where it leaves it.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -48,6 +51,15 @@ struct saln_nw_span {
     SpecPair *d_sp = nullptr;
     SpecStripe *d_rec = nullptr;  // [0] this span's walk, [1] its entry (pass-2 exit slot)
     uint32_t *d_ops = nullptr;
+    // speculative passes over the span's walker stripes (one record per
+    // stripe + the entry record after the rightmost), linked on the host
+    int spec_passes = 0;
+    uint2 *d_sblocks = nullptr;
+    SpecPair *d_ssp = nullptr;
+    SpecStripe *d_srec = nullptr;
+    uint32_t *d_sops = nullptr;
+    std::vector<SpecStripe> h_srec;
+    std::vector<uint32_t> h_sops;
 
     // kernel arguments rebased to the span: tile t of the pair at d_mask +
     // (t - t0) * cs; stripe g's output column g - g0 + 1 (its input g - g0)
@@ -60,11 +72,72 @@ struct saln_nw_span {
     void release() {
         for (void *b : {(void *)d_mask, (void *)d_pair, (void *)d_work, (void *)d_err,
                         (void *)d_endh, (void *)d_blocks, (void *)d_sp, (void *)d_rec,
-                        (void *)d_ops})
+                        (void *)d_ops, (void *)d_sblocks, (void *)d_ssp, (void *)d_srec,
+                        (void *)d_sops})
             if (b) dev_free(ctx, b);
         if (own_bnd && d_bnd) dev_free(ctx, d_bnd);
     }
 };
+
+// The span's walk from the speculative passes: every walker stripe walks at
+// once (the rightmost from the given entry, the others from a guess, then
+// from their right neighbour's previous exit); the stored walks form the
+// sequential walk when, from the rightmost stripe leftwards, each stripe's
+// stored entry is where the walk left the stripe after it.  Returns SALN_OK,
+// an error, or 1 when they do not link (the caller walks sequentially).
+static int span_walk_spec(saln_nw_span *s, const uint8_t *d_q, const uint8_t *d_db,
+                          const saln_nw_span_cursor *entry, saln_nw_span_cursor *exit,
+                          uint32_t *ops, uint64_t ops_cap, uint64_t *n_ops, hipStream_t st) {
+    const uint32_t n = s->ntiles;
+    for (uint32_t t = 0; t < n; ++t) {
+        s->h_srec[t] = SpecStripe{};
+        s->h_srec[t].in_k = kSpecNone;  // no stored walk to keep
+    }
+    SpecStripe &d = s->h_srec[n];
+    d = SpecStripe{};
+    d.out_i[0] = d.out_i[1] = entry->i;
+    d.out_j[0] = d.out_j[1] = entry->j;
+    d.out_k[0] = d.out_k[1] = entry->kind;
+    HIP_TRY(hipMemcpyAsync(s->d_srec, s->h_srec.data(), (n + 1) * sizeof(SpecStripe),
+                           hipMemcpyHostToDevice, st));
+    // the kernel indexes records and op slots by the pair-wide stripe t:
+    // tables rebased so that stripe t0 is element 0 (never read below it)
+    SpecStripe *rec0 = (SpecStripe *)((uintptr_t)s->d_srec - (uint64_t)s->t0 * sizeof(SpecStripe));
+    uint32_t *ops0 = (uint32_t *)((uintptr_t)s->d_sops -
+                                  (uint64_t)s->t0 * kSpecOpsCap * sizeof(uint32_t));
+    SpecArgs sa{s->d_sblocks, s->d_ssp, rec0, ops0, nullptr, 0, 0, 0, (int32_t)(s->t0 + n)};
+    HIP_TRY(launch_span_spec(s->d_pair, sa, n, s->spec_passes, d_q, d_db, s->mask_arg(),
+                             s->d_endh, s->sc, st));
+    HIP_TRY(hipMemcpyAsync(s->h_srec.data(), s->d_srec, n * sizeof(SpecStripe),
+                           hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(s->h_sops.data(), s->d_sops, s->h_sops.size() * sizeof(uint32_t),
+                           hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    const int cf = s->spec_passes & 1;  // exit slot of the last pass
+    int32_t ci = entry->i, cj = entry->j, ck = entry->kind;
+    uint64_t nw = 0;
+    for (int t = (int)n - 1;; --t) {
+        const SpecStripe &r = s->h_srec[t];
+        if (r.in_i != ci || r.in_j != cj || r.in_k != ck || r.nops > kSpecOpsCap) return 1;
+        if (ops && nw + r.nops > ops_cap) {
+            set_error("span walk: ops buffer too small (saln_nw_span_info ops_cap)");
+            return SALN_E_CAPACITY;
+        }
+        if (ops) std::memcpy(ops + nw, s->h_sops.data() + (size_t)t * kSpecOpsCap, r.nops * sizeof(uint32_t));
+        nw += r.nops;
+        ci = r.out_i[cf];
+        cj = r.out_j[cf];
+        ck = r.out_k[cf];
+        if (ck >= kSpecEv || t == 0) break;  // ended, or left the span
+    }
+    if (ck == kSpecNone) return 1;
+    *n_ops = nw;
+    exit->i = ci;
+    exit->j = cj;
+    exit->kind = ck;
+    exit->end_states = entry->kind == SALN_SPAN_END ? s->h_srec[n - 1].am_end : 0u;
+    return SALN_OK;
+}
 
 extern "C" {
 
@@ -156,6 +229,31 @@ int saln_nw_span_create(saln_context *ctx, uint64_t len_q, uint64_t len_db, uint
         (e = dev_alloc(ctx, (void **)&s->d_rec, 2 * sizeof(SpecStripe))) != hipSuccess ||
         (e = dev_alloc(ctx, (void **)&s->d_ops, (s->ops_cap + 8) * sizeof(uint32_t))) != hipSuccess)
         return fail(e, "tables");
+    // speculative walk passes (SALN_SPEC=0 off, SALN_SPEC_PASSES, default 3)
+    // for spans of at least two walker stripes
+    {
+        const char *env = std::getenv("SALN_SPEC");
+        const char *pe = std::getenv("SALN_SPEC_PASSES");
+        const int passes = pe ? std::atoi(pe) : 3;
+        if ((!env || std::atoi(env) != 0) && passes > 0 && s->ntiles >= 2) {
+            s->spec_passes = passes;
+            std::vector<uint2> blocks;
+            for (uint32_t t = 0; t < s->ntiles; ++t) blocks.push_back(make_uint2(0u, s->t0 + t));
+            // stripe t's record at index t - t0 (span_walk_spec rebases the
+            // table pointers by t0), the entry record at ntiles
+            const SpecPair ssp{0u, s->ntiles, 0u, 0u};
+            s->h_srec.resize(s->ntiles + 1);
+            s->h_sops.resize((size_t)s->ntiles * kSpecOpsCap);
+            if ((e = dev_alloc(ctx, (void **)&s->d_sblocks, blocks.size() * sizeof(uint2))) != hipSuccess ||
+                (e = hipMemcpy(s->d_sblocks, blocks.data(), blocks.size() * sizeof(uint2),
+                               hipMemcpyHostToDevice)) != hipSuccess ||
+                (e = dev_alloc(ctx, (void **)&s->d_ssp, sizeof ssp)) != hipSuccess ||
+                (e = hipMemcpy(s->d_ssp, &ssp, sizeof ssp, hipMemcpyHostToDevice)) != hipSuccess ||
+                (e = dev_alloc(ctx, (void **)&s->d_srec, s->h_srec.size() * sizeof(SpecStripe))) != hipSuccess ||
+                (e = dev_alloc(ctx, (void **)&s->d_sops, s->h_sops.size() * sizeof(uint32_t))) != hipSuccess)
+                return fail(e, "speculative walk tables");
+        }
+    }
     *out = s;
     return SALN_OK;
 }
@@ -222,6 +320,10 @@ int saln_nw_span_walk(saln_nw_span *s, const uint8_t *d_q, const uint8_t *d_db,
     }
     HIP_TRY(hipSetDevice(s->ctx->device));
     hipStream_t st = resolve_stream(stream, s->ctx);
+    if (s->spec_passes) {
+        const int rc = span_walk_spec(s, d_q, d_db, entry, exit, ops, ops_cap, n_ops, st);
+        if (rc != 1) return rc;  // 1: the passes did not link, walk sequentially
+    }
     SpecStripe rec[2];
     std::memset(rec, 0, sizeof rec);
     rec[0].in_k = kSpecNone;  // no stored walk to keep

@@ -79,9 +79,13 @@ def test_span_chain_matches_oracle(pipelined):
             _same(r, saln.n_w_align(qs, ds))
 
 
-def test_span_chain_long_pairs_match_plan():
+@pytest.mark.parametrize("spec", ["1", "0"])
+def test_span_chain_long_pairs_match_plan(spec, monkeypatch):
     """20-30 kbp pairs over 3-8 spans (pipelined, 2,048-row bands) give the
-    single-GPU plan's result word for word; a mask-free oracle pins the score."""
+    single-GPU plan's result word for word, with the speculative span walks
+    and with the sequential walker alone (SALN_SPEC=0); a mask-free oracle
+    pins the score."""
+    monkeypatch.setenv("SALN_SPEC", spec)
     import sequencealigning_amd as saln
     from nw_check import rand_seq
     from oracle import refcpu
