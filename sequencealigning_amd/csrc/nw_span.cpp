@@ -58,8 +58,8 @@ struct saln_nw_span {
     SpecPair *d_ssp = nullptr;
     SpecStripe *d_srec = nullptr;
     uint32_t *d_sops = nullptr;
-    std::vector<SpecStripe> h_srec;
-    std::vector<uint32_t> h_sops;
+    SpecStripe *h_srec = nullptr;  // pinned host copies (ntiles + 1 records, ntiles op slots)
+    uint32_t *h_sops = nullptr;
 
     // kernel arguments rebased to the span: tile t of the pair at d_mask +
     // (t - t0) * cs; stripe g's output column g - g0 + 1 (its input g - g0)
@@ -76,6 +76,8 @@ struct saln_nw_span {
                         (void *)d_sops})
             if (b) dev_free(ctx, b);
         if (own_bnd && d_bnd) dev_free(ctx, d_bnd);
+        if (h_srec) (void)hipHostFree(h_srec);
+        if (h_sops) (void)hipHostFree(h_sops);
     }
 };
 
@@ -98,7 +100,7 @@ static int span_walk_spec(saln_nw_span *s, const uint8_t *d_q, const uint8_t *d_
     d.out_i[0] = d.out_i[1] = entry->i;
     d.out_j[0] = d.out_j[1] = entry->j;
     d.out_k[0] = d.out_k[1] = entry->kind;
-    HIP_TRY(hipMemcpyAsync(s->d_srec, s->h_srec.data(), (n + 1) * sizeof(SpecStripe),
+    HIP_TRY(hipMemcpyAsync(s->d_srec, s->h_srec, (n + 1) * sizeof(SpecStripe),
                            hipMemcpyHostToDevice, st));
     // the kernel indexes records and op slots by the pair-wide stripe t:
     // tables rebased so that stripe t0 is element 0 (never read below it)
@@ -108,9 +110,9 @@ static int span_walk_spec(saln_nw_span *s, const uint8_t *d_q, const uint8_t *d_
     SpecArgs sa{s->d_sblocks, s->d_ssp, rec0, ops0, nullptr, 0, 0, 0, (int32_t)(s->t0 + n)};
     HIP_TRY(launch_span_spec(s->d_pair, sa, n, s->spec_passes, d_q, d_db, s->mask_arg(),
                              s->d_endh, s->sc, st));
-    HIP_TRY(hipMemcpyAsync(s->h_srec.data(), s->d_srec, n * sizeof(SpecStripe),
-                           hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipMemcpyAsync(s->h_sops.data(), s->d_sops, s->h_sops.size() * sizeof(uint32_t),
+    HIP_TRY(hipMemcpyAsync(s->h_srec, s->d_srec, n * sizeof(SpecStripe), hipMemcpyDeviceToHost,
+                           st));
+    HIP_TRY(hipMemcpyAsync(s->h_sops, s->d_sops, (size_t)n * kSpecOpsCap * sizeof(uint32_t),
                            hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
     const int cf = s->spec_passes & 1;  // exit slot of the last pass
@@ -123,7 +125,7 @@ static int span_walk_spec(saln_nw_span *s, const uint8_t *d_q, const uint8_t *d_
             set_error("span walk: ops buffer too small (saln_nw_span_info ops_cap)");
             return SALN_E_CAPACITY;
         }
-        if (ops) std::memcpy(ops + nw, s->h_sops.data() + (size_t)t * kSpecOpsCap, r.nops * sizeof(uint32_t));
+        if (ops) std::memcpy(ops + nw, s->h_sops + (size_t)t * kSpecOpsCap, r.nops * sizeof(uint32_t));
         nw += r.nops;
         ci = r.out_i[cf];
         cj = r.out_j[cf];
@@ -242,15 +244,15 @@ int saln_nw_span_create(saln_context *ctx, uint64_t len_q, uint64_t len_db, uint
             // stripe t's record at index t - t0 (span_walk_spec rebases the
             // table pointers by t0), the entry record at ntiles
             const SpecPair ssp{0u, s->ntiles, 0u, 0u};
-            s->h_srec.resize(s->ntiles + 1);
-            s->h_sops.resize((size_t)s->ntiles * kSpecOpsCap);
             if ((e = dev_alloc(ctx, (void **)&s->d_sblocks, blocks.size() * sizeof(uint2))) != hipSuccess ||
                 (e = hipMemcpy(s->d_sblocks, blocks.data(), blocks.size() * sizeof(uint2),
                                hipMemcpyHostToDevice)) != hipSuccess ||
                 (e = dev_alloc(ctx, (void **)&s->d_ssp, sizeof ssp)) != hipSuccess ||
                 (e = hipMemcpy(s->d_ssp, &ssp, sizeof ssp, hipMemcpyHostToDevice)) != hipSuccess ||
-                (e = dev_alloc(ctx, (void **)&s->d_srec, s->h_srec.size() * sizeof(SpecStripe))) != hipSuccess ||
-                (e = dev_alloc(ctx, (void **)&s->d_sops, s->h_sops.size() * sizeof(uint32_t))) != hipSuccess)
+                (e = dev_alloc(ctx, (void **)&s->d_srec, (s->ntiles + 1) * sizeof(SpecStripe))) != hipSuccess ||
+                (e = dev_alloc(ctx, (void **)&s->d_sops, (size_t)s->ntiles * kSpecOpsCap * sizeof(uint32_t))) != hipSuccess ||
+                (e = hipHostMalloc((void **)&s->h_srec, (s->ntiles + 1) * sizeof(SpecStripe), 0)) != hipSuccess ||
+                (e = hipHostMalloc((void **)&s->h_sops, (size_t)s->ntiles * kSpecOpsCap * sizeof(uint32_t), 0)) != hipSuccess)
                 return fail(e, "speculative walk tables");
         }
     }

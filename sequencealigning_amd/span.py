@@ -72,18 +72,17 @@ def merge_walk_ops(segments) -> list[tuple[int, str]]:
     """CIGAR (forward) from the spans' run words in walk order (each segment
     back to front, segments from the end cell's span leftwards): runs of one
     op continuing across a seam are merged, then the order is reversed."""
-    runs: list[list[int]] = []
-    for seg in segments:
-        for w in np.asarray(seg, np.uint32).tolist():
-            n, op = w >> 4, w & 15
-            if n == 0:
-                continue
-            if runs and runs[-1][1] == op:
-                runs[-1][0] += n
-            else:
-                runs.append([n, op])
-    runs.reverse()
-    return _decode_cigar([(n << 4) | op for n, op in runs])
+    w = np.concatenate([np.asarray(x, np.uint32).ravel() for x in segments] or
+                       [np.zeros(0, np.uint32)])
+    n, op = (w >> 4).astype(np.int64), w & 15
+    keep = n > 0
+    n, op = n[keep], op[keep]
+    if not len(n):
+        return []
+    starts = np.flatnonzero(np.r_[True, op[1:] != op[:-1]])
+    lens = np.add.reduceat(n, starts)[::-1]
+    ops = op[starts][::-1]
+    return [(int(a), _lib.CIGAR_OPS[int(b)]) for a, b in zip(lens.tolist(), ops.tolist())]
 
 
 def walk_spans(walkers, len_q: int, len_db: int):
