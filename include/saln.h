@@ -272,6 +272,10 @@ typedef struct {
 } saln_nw_span_cursor;
 /* Elements (8 bytes each) of one boundary column for a db of len_db rows. */
 uint64_t saln_nw_span_boundary_elems(uint64_t len_db);
+/* Boundary columns (stripes + 1) of the span col_lo+1 .. col_hi: the size of a
+ * caller-owned d_boundary is cols * saln_nw_span_boundary_elems(len_db)
+ * elements (host-only, no device needed). */
+uint64_t saln_nw_span_boundary_cols(uint64_t col_lo, uint64_t col_hi);
 /* d_boundary: caller-owned device buffer of (stripes + 1) boundary columns
  * (saln_nw_span_info), column 0 the inbox, the last column the outbox; NULL:
  * the span allocates it. */

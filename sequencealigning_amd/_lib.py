@@ -88,7 +88,7 @@ EXPORTS = [
     "saln_nw_plan_status", "saln_nw_plan_set_wait_limit",
     "saln_nw_avsa_create", "saln_nw_avsa_execute", "saln_nw_avsa_info", "saln_nw_avsa_destroy",
     "saln_nw_avsa_status", "saln_nw_avsa_launch_geometry",
-    "saln_nw_span_boundary_elems", "saln_nw_span_create", "saln_nw_span_info",
+    "saln_nw_span_boundary_elems", "saln_nw_span_boundary_cols", "saln_nw_span_create", "saln_nw_span_info",
     "saln_nw_span_boundary", "saln_nw_span_reset", "saln_nw_span_fill", "saln_nw_span_watch",
     "saln_nw_span_walk", "saln_nw_span_score", "saln_nw_span_status",
     "saln_nw_span_set_wait_limit", "saln_nw_span_destroy",
@@ -175,6 +175,8 @@ def lib() -> C.CDLL:
         L.saln_nw_avsa_destroy.argtypes = [vp]
         L.saln_nw_span_boundary_elems.argtypes = [C.c_uint64]
         L.saln_nw_span_boundary_elems.restype = C.c_uint64
+        L.saln_nw_span_boundary_cols.argtypes = [C.c_uint64, C.c_uint64]
+        L.saln_nw_span_boundary_cols.restype = C.c_uint64
         L.saln_nw_span_create.argtypes = [vp, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64,
                                           C.POINTER(NwScoring), vp, C.POINTER(vp)]
         L.saln_nw_span_info.argtypes = [vp, u64p, u64p, u64p]

@@ -141,10 +141,20 @@ static int span_walk_spec(saln_nw_span *s, const uint8_t *d_q, const uint8_t *d_
     return SALN_OK;
 }
 
+// Row-fill columns per lane of a span: K = 1 while every 64-column stripe of
+// the span has a SIMD to itself (stripe_rows_k)
+static int span_k(uint64_t col_lo, uint64_t col_hi) { return stripe_rows_k((col_hi - col_lo + 63) / 64); }
+
 extern "C" {
 
 uint64_t saln_nw_span_boundary_elems(uint64_t len_db) {
     return len_db > 0xFFFFFFFFull ? 0 : scratch_col((uint32_t)len_db);
+}
+
+uint64_t saln_nw_span_boundary_cols(uint64_t col_lo, uint64_t col_hi) {
+    if (col_hi <= col_lo) return 0;
+    const uint64_t W = 64u * (uint64_t)span_k(col_lo, col_hi);
+    return (col_hi + W - 1) / W - col_lo / W + 1;
 }
 
 int saln_nw_span_create(saln_context *ctx, uint64_t len_q, uint64_t len_db, uint64_t col_lo,
@@ -176,8 +186,7 @@ int saln_nw_span_create(saln_context *ctx, uint64_t len_q, uint64_t len_db, uint
     s->ld = (uint32_t)len_db;
     s->col_lo = (uint32_t)col_lo;
     s->col_hi = (uint32_t)col_hi;
-    // K = 1 while every 64-column stripe of the span has a SIMD to itself
-    s->K = stripe_rows_k((col_hi - col_lo + 63) / 64);
+    s->K = span_k(col_lo, col_hi);
     const uint32_t W = 64u * (uint32_t)s->K;
     s->g0 = s->col_lo / W;
     s->nst = (s->col_hi + W - 1) / W - s->g0;

@@ -134,22 +134,16 @@ class NwSpan:
         self.dev = torch.device("cuda", device)
         self.ctx = _lib.context(device)
         self.scol = int(L.saln_nw_span_boundary_elems(len_db))
-        # the span's stripe count decides the column count: a probe span with
-        # its own boundary buffer reports it, then the real one uses torch's
-        probe = C.c_void_p()
-        _lib.check(L.saln_nw_span_create(self.ctx, len_q, len_db, col_lo, col_hi,
-                                         _lib.scoring_arg(scoring), None, C.byref(probe)),
-                   "saln_nw_span_create")
-        ncol, mb, cap = C.c_uint64(), C.c_uint64(), C.c_uint64()
-        L.saln_nw_span_info(probe, C.byref(mb), C.byref(ncol), C.byref(cap))
-        L.saln_nw_span_destroy(probe)
-        self.ncol, self.mask_bytes, self.ops_cap = ncol.value, mb.value, cap.value
+        self.ncol = int(L.saln_nw_span_boundary_cols(col_lo, col_hi))
         self.boundary = torch.empty(self.ncol * self.scol, dtype=torch.int64, device=self.dev)
         self._h = C.c_void_p()
         _lib.check(L.saln_nw_span_create(self.ctx, len_q, len_db, col_lo, col_hi,
                                          _lib.scoring_arg(scoring),
                                          C.c_void_p(self.boundary.data_ptr()), C.byref(self._h)),
                    "saln_nw_span_create")
+        mb, cap = C.c_uint64(), C.c_uint64()
+        L.saln_nw_span_info(self._h, C.byref(mb), None, C.byref(cap))
+        self.mask_bytes, self.ops_cap = mb.value, cap.value
         self.inbox = self.boundary[:self.scol]
         self.outbox = self.boundary[(self.ncol - 1) * self.scol:]
         self._ops = (C.c_uint32 * max(1, self.ops_cap))()

@@ -254,6 +254,20 @@ def test_single_engine_matches_oracle():
             assert cigar_ops_string(S.merge_walk_ops(segs)) == o.first_ops
 
 
+def test_span_boundary_geometry(saln):
+    """Host-only span geometry (no device): boundary columns = stripes + 1,
+    64-column stripes (K = 1) while a span has at most 1,024 of them, else
+    128-column ones; a caller-owned boundary buffer's size."""
+    from sequencealigning_amd import _lib
+    L = _lib.lib()
+    assert L.saln_nw_span_boundary_cols(0, 12288) == 12288 // 64 + 1
+    assert L.saln_nw_span_boundary_cols(0, 100_000) == (100_000 + 127) // 128 + 1
+    assert L.saln_nw_span_boundary_cols(256, 300) == 2
+    assert L.saln_nw_span_boundary_cols(512, 512) == 0
+    assert L.saln_nw_span_boundary_elems(100_001) % 4 == 0
+    assert L.saln_nw_span_boundary_elems(100_001) >= 100_001 + 9  # rows 1..ld + the pad slots
+
+
 def test_span_columns_and_merge():
     from sequencealigning_amd import span as S
     assert S.span_columns(100_000, 8)[0] == (0, 12288)
