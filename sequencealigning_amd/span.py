@@ -350,6 +350,17 @@ class _DeviceSpanEngine:
         self.span.close()
 
 
+_EDGES: dict = {}
+
+
+def _edge_groups(world: int):
+    import torch.distributed as dist
+    key = (id(dist.group.WORLD), world)
+    if key not in _EDGES:
+        _EDGES[key] = [dist.new_group([e, e + 1]) for e in range(world - 1)]
+    return _EDGES[key]
+
+
 class ShardedLongPair:
     """One pair split by query columns over the ranks of the default process
     group (one process per GPU).  Rank r fills span r;
@@ -385,7 +396,9 @@ class ShardedLongPair:
             self.tdev = torch.device("cpu")
         # one two-rank group per edge (r, r+1): sends to the right and
         # receives from the left run on different communicators / streams
-        self.edges = [dist.new_group([e, e + 1]) for e in range(self.world - 1)]
+        # (created once per process group: every rank builds them in the same
+        # order, and later pairs reuse them)
+        self.edges = _edge_groups(self.world)
         self.left = self.edges[self.rank - 1] if self.rank > 0 else None
         self.right = self.edges[self.rank] if self.rank + 1 < self.world else None
 
