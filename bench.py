@@ -447,8 +447,11 @@ def leg_c4_spans(torch, saln, n_spans=8, reps=3, band_rows=4096):
     concurrently on this GPU and hand their boundary rows over in bands
     (device copies behind watch kernels), then the walk crosses the spans
     right to left.  The 8-GPU layout on one GPU: each span keeps 1/8 of the
-    mask; the time is the hand-off protocol's cost over the one-plan fill
-    (c4).  Checked word for word against the plan path (n_w_align)."""
+    mask, the stripes are 128 columns wide (the whole pair's stripes share
+    this GPU's SIMDs) and the time is the hand-off protocol's cost over the
+    one-plan fill (c4); span_fill_alone_ms: each span alone with 64-column
+    stripes, as on a GPU of its own.  Checked word for word against the plan
+    path (n_w_align)."""
     from sequencealigning_amd import synth
     from sequencealigning_amd.span import SpanChain
     q = synth.random_bases(0x5EED0003, 100_000).tobytes()
@@ -466,26 +469,28 @@ def leg_c4_spans(torch, saln, n_spans=8, reps=3, band_rows=4096):
         if k:
             fills.append(t1 - t0)
             walks.append(t2 - t1)
-    # each span alone on the GPU (its inbox complete): the fill time of a GPU
-    # that holds one span, as on an R-GPU node (one span per GPU)
+    # each span alone on the GPU with the stripe width of a GPU that holds
+    # only it (its inbox the chain's boundary): the fill time of one GPU of an
+    # n_spans-GPU node
+    from sequencealigning_amd.span import NwSpan
     main = torch.cuda.current_stream()
     alone = []
-    for k in range(2):
-        evs = []
-        for s in ch.spans:
-            s.reset(main)
-        for k_s, s in enumerate(ch.spans):
+    for k_s, (lo, hi) in enumerate(ch.cols):
+        sp = NwSpan(len(q), len(d), lo, hi, device=torch.cuda.current_device())
+        ms = []
+        for k in range(2):
+            sp.reset(main)
             if k_s:
-                s.inbox.copy_(ch.spans[k_s - 1].outbox)
+                sp.inbox.copy_(ch.spans[k_s - 1].outbox)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(main)
-            s.fill(ch.q, ch.d, main)
+            sp.fill(ch.q, ch.d, main)
             e1.record(main)
-            evs.append((e0, e1))
-        torch.cuda.synchronize()
-        ch.check()
-        if k:
-            alone = [a.elapsed_time(b) for a, b in evs]
+            torch.cuda.synchronize()
+            sp.check()
+            ms.append(e0.elapsed_time(e1))
+        alone.append(ms[-1])
+        sp.close()
     span_mask = max(s.mask_bytes for s in ch.spans)
     ch.close()
     torch.cuda.empty_cache()

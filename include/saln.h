@@ -274,14 +274,17 @@ typedef struct {
 uint64_t saln_nw_span_boundary_elems(uint64_t len_db);
 /* Boundary columns (stripes + 1) of the span col_lo+1 .. col_hi: the size of a
  * caller-owned d_boundary is cols * saln_nw_span_boundary_elems(len_db)
- * elements (host-only, no device needed). */
-uint64_t saln_nw_span_boundary_cols(uint64_t col_lo, uint64_t col_hi);
+ * elements (host-only, no device needed).  device_cols: the query columns of
+ * every span that fills on the same device at the same time (0: this span
+ * alone); the stripe width follows from it (64 columns while each stripe
+ * has a SIMD of its own, else 128). */
+uint64_t saln_nw_span_boundary_cols(uint64_t col_lo, uint64_t col_hi, uint64_t device_cols);
 /* d_boundary: caller-owned device buffer of (stripes + 1) boundary columns
  * (saln_nw_span_info), column 0 the inbox, the last column the outbox; NULL:
  * the span allocates it. */
 int saln_nw_span_create(saln_context *ctx, uint64_t len_q, uint64_t len_db, uint64_t col_lo,
-                        uint64_t col_hi, const saln_nw_scoring *scoring, void *d_boundary,
-                        saln_nw_span **out);
+                        uint64_t col_hi, uint64_t device_cols, const saln_nw_scoring *scoring,
+                        void *d_boundary, saln_nw_span **out);
 int saln_nw_span_info(const saln_nw_span *s, uint64_t *mask_bytes, uint64_t *boundary_cols,
                       uint64_t *ops_cap);
 /* Device addresses of the inbox (column 0) and outbox (last column). */

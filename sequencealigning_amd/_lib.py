@@ -175,10 +175,10 @@ def lib() -> C.CDLL:
         L.saln_nw_avsa_destroy.argtypes = [vp]
         L.saln_nw_span_boundary_elems.argtypes = [C.c_uint64]
         L.saln_nw_span_boundary_elems.restype = C.c_uint64
-        L.saln_nw_span_boundary_cols.argtypes = [C.c_uint64, C.c_uint64]
+        L.saln_nw_span_boundary_cols.argtypes = [C.c_uint64, C.c_uint64, C.c_uint64]
         L.saln_nw_span_boundary_cols.restype = C.c_uint64
         L.saln_nw_span_create.argtypes = [vp, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64,
-                                          C.POINTER(NwScoring), vp, C.POINTER(vp)]
+                                          C.c_uint64, C.POINTER(NwScoring), vp, C.POINTER(vp)]
         L.saln_nw_span_info.argtypes = [vp, u64p, u64p, u64p]
         L.saln_nw_span_boundary.argtypes = [vp, C.POINTER(vp), C.POINTER(vp)]
         L.saln_nw_span_reset.argtypes = [vp, vp]

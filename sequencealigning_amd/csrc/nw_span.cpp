@@ -143,7 +143,9 @@ static int span_walk_spec(saln_nw_span *s, const uint8_t *d_q, const uint8_t *d_
 
 // Row-fill columns per lane of a span: K = 1 while every 64-column stripe of
 // the span has a SIMD to itself (stripe_rows_k)
-static int span_k(uint64_t col_lo, uint64_t col_hi) { return stripe_rows_k((col_hi - col_lo + 63) / 64); }
+static int span_k(uint64_t col_lo, uint64_t col_hi, uint64_t device_cols) {
+    return stripe_rows_k((std::max(col_hi - col_lo, device_cols) + 63) / 64);
+}
 
 extern "C" {
 
@@ -151,15 +153,15 @@ uint64_t saln_nw_span_boundary_elems(uint64_t len_db) {
     return len_db > 0xFFFFFFFFull ? 0 : scratch_col((uint32_t)len_db);
 }
 
-uint64_t saln_nw_span_boundary_cols(uint64_t col_lo, uint64_t col_hi) {
+uint64_t saln_nw_span_boundary_cols(uint64_t col_lo, uint64_t col_hi, uint64_t device_cols) {
     if (col_hi <= col_lo) return 0;
-    const uint64_t W = 64u * (uint64_t)span_k(col_lo, col_hi);
+    const uint64_t W = 64u * (uint64_t)span_k(col_lo, col_hi, device_cols);
     return (col_hi + W - 1) / W - col_lo / W + 1;
 }
 
 int saln_nw_span_create(saln_context *ctx, uint64_t len_q, uint64_t len_db, uint64_t col_lo,
-                        uint64_t col_hi, const saln_nw_scoring *scoring, void *d_boundary,
-                        saln_nw_span **out) {
+                        uint64_t col_hi, uint64_t device_cols, const saln_nw_scoring *scoring,
+                        void *d_boundary, saln_nw_span **out) {
     if (!ctx || !out) return SALN_E_INVALID;
     *out = nullptr;
     if (len_q <= 256 || len_db == 0 || len_q > 0x7FFFFFFFull || len_db > 0x7FFFFFFFull) {
@@ -186,7 +188,7 @@ int saln_nw_span_create(saln_context *ctx, uint64_t len_q, uint64_t len_db, uint
     s->ld = (uint32_t)len_db;
     s->col_lo = (uint32_t)col_lo;
     s->col_hi = (uint32_t)col_hi;
-    s->K = span_k(col_lo, col_hi);
+    s->K = span_k(col_lo, col_hi, device_cols);
     const uint32_t W = 64u * (uint32_t)s->K;
     s->g0 = s->col_lo / W;
     s->nst = (s->col_hi + W - 1) / W - s->g0;

@@ -126,7 +126,7 @@ class NwSpan:
     rows of them."""
 
     def __init__(self, len_q: int, len_db: int, col_lo: int, col_hi: int, *, scoring=None,
-                 device: int = 0):
+                 device: int = 0, device_cols: int = 0):
         import torch
         L = _lib.lib()
         self.len_q, self.len_db, self.col_lo, self.col_hi = len_q, len_db, col_lo, col_hi
@@ -134,10 +134,12 @@ class NwSpan:
         self.dev = torch.device("cuda", device)
         self.ctx = _lib.context(device)
         self.scol = int(L.saln_nw_span_boundary_elems(len_db))
-        self.ncol = int(L.saln_nw_span_boundary_cols(col_lo, col_hi))
+        # device_cols: the columns of every span filling on this device at
+        # once (SpanChain: the whole pair), which sets the stripe width
+        self.ncol = int(L.saln_nw_span_boundary_cols(col_lo, col_hi, device_cols))
         self.boundary = torch.empty(self.ncol * self.scol, dtype=torch.int64, device=self.dev)
         self._h = C.c_void_p()
-        _lib.check(L.saln_nw_span_create(self.ctx, len_q, len_db, col_lo, col_hi,
+        _lib.check(L.saln_nw_span_create(self.ctx, len_q, len_db, col_lo, col_hi, device_cols,
                                          _lib.scoring_arg(scoring),
                                          C.c_void_p(self.boundary.data_ptr()), C.byref(self._h)),
                    "saln_nw_span_create")
@@ -239,8 +241,10 @@ class SpanChain:
         self.q = torch.frombuffer(bytearray(self.q_bytes), dtype=torch.uint8).to(dev)
         self.d = torch.frombuffer(bytearray(self.d_bytes), dtype=torch.uint8).to(dev)
         self.cols = span_columns(self.len_q, n_spans)
-        self.spans = [NwSpan(self.len_q, self.len_db, lo, hi, scoring=scoring, device=device)
-                      for lo, hi in self.cols]
+        # all spans fill on this one device at once: stripe widths for the
+        # whole pair's columns
+        self.spans = [NwSpan(self.len_q, self.len_db, lo, hi, scoring=scoring, device=device,
+                             device_cols=self.len_q) for lo, hi in self.cols]
         self.bands = _bands(self.len_db, band_rows)
         self.streams = [torch.cuda.Stream(device=dev) for _ in range(2 * n_spans)]
 

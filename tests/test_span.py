@@ -260,10 +260,12 @@ def test_span_boundary_geometry(saln):
     128-column ones; a caller-owned boundary buffer's size."""
     from sequencealigning_amd import _lib
     L = _lib.lib()
-    assert L.saln_nw_span_boundary_cols(0, 12288) == 12288 // 64 + 1
-    assert L.saln_nw_span_boundary_cols(0, 100_000) == (100_000 + 127) // 128 + 1
-    assert L.saln_nw_span_boundary_cols(256, 300) == 2
-    assert L.saln_nw_span_boundary_cols(512, 512) == 0
+    assert L.saln_nw_span_boundary_cols(0, 12288, 0) == 12288 // 64 + 1
+    # the same span sharing its GPU with the rest of a 100 kbp pair: 128-column stripes
+    assert L.saln_nw_span_boundary_cols(0, 12288, 100_000) == 12288 // 128 + 1
+    assert L.saln_nw_span_boundary_cols(0, 100_000, 0) == (100_000 + 127) // 128 + 1
+    assert L.saln_nw_span_boundary_cols(256, 300, 0) == 2
+    assert L.saln_nw_span_boundary_cols(512, 512, 0) == 0
     assert L.saln_nw_span_boundary_elems(100_001) % 4 == 0
     assert L.saln_nw_span_boundary_elems(100_001) >= 100_001 + 9  # rows 1..ld + the pad slots
 
