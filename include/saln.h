@@ -314,6 +314,17 @@ int saln_nw_span_score(saln_nw_span *s, int32_t *score, int32_t *status, void *s
 int saln_nw_span_status(saln_nw_span *s, uint32_t *flags);
 int saln_nw_span_set_wait_limit(saln_nw_span *s, uint32_t polls);
 int saln_nw_span_destroy(saln_nw_span *s);
+/* Spans of one pair on ONE device (tests, the single-GPU emulation of the
+ * multi-GPU chain): queues on `stream` a watch of src's outbox rows row_lo ..
+ * row_hi and their copy into dst's inbox. */
+int saln_nw_span_forward(saln_nw_span *src, saln_nw_span *dst, uint64_t row_lo, uint64_t row_hi,
+                         void *stream);
+/* Compute units of the context's device, and a stream whose kernels run only
+ * on CUs cu_lo .. cu_hi-1 (hipExtStreamCreateWithCUMask): one device split
+ * into per-span partitions. */
+int saln_device_cu_count(saln_context *ctx, uint32_t *n);
+int saln_stream_create_cu_range(saln_context *ctx, uint32_t cu_lo, uint32_t cu_hi, void **stream);
+int saln_stream_destroy(saln_context *ctx, void *stream);
 
 /* ----------------------------------------------------------------------- WFA
  * Replaces `pub fn wfa_align(seq1: &Record, seq2: &Record, mode: Mode)`

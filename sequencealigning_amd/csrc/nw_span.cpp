@@ -404,6 +404,49 @@ int saln_nw_span_set_wait_limit(saln_nw_span *s, uint32_t polls) {
     return SALN_OK;
 }
 
+int saln_nw_span_forward(saln_nw_span *src, saln_nw_span *dst, uint64_t row_lo, uint64_t row_hi,
+                         void *stream) {
+    if (!src || !dst || src->ctx != dst->ctx || src->ld != dst->ld || src->col_hi != dst->col_lo ||
+        row_lo < 1 || row_hi > src->ld || row_lo > row_hi)
+        return SALN_E_INVALID;
+    HIP_TRY(hipSetDevice(src->ctx->device));
+    hipStream_t st = resolve_stream(stream, src->ctx);
+    HIP_TRY(launch_span_watch(src->outbox(), (uint32_t)row_lo, (uint32_t)row_hi, src->d_err, st));
+    HIP_TRY(hipMemcpyAsync(dst->inbox() + row_lo, src->outbox() + row_lo,
+                           (row_hi - row_lo + 1) * sizeof(int2), hipMemcpyDeviceToDevice, st));
+    return SALN_OK;
+}
+
+int saln_device_cu_count(saln_context *ctx, uint32_t *n) {
+    if (!ctx || !n) return SALN_E_INVALID;
+    int v = 0;
+    HIP_TRY(hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, ctx->device));
+    *n = (uint32_t)v;
+    return SALN_OK;
+}
+
+int saln_stream_create_cu_range(saln_context *ctx, uint32_t cu_lo, uint32_t cu_hi, void **stream) {
+    if (!ctx || !stream || cu_lo >= cu_hi) return SALN_E_INVALID;
+    uint32_t n = 0;
+    const int rc = saln_device_cu_count(ctx, &n);
+    if (rc != SALN_OK) return rc;
+    if (cu_hi > n) return SALN_E_INVALID;
+    std::vector<uint32_t> mask((n + 31) / 32, 0u);
+    for (uint32_t c = cu_lo; c < cu_hi; ++c) mask[c / 32] |= 1u << (c % 32);
+    HIP_TRY(hipSetDevice(ctx->device));
+    hipStream_t s = nullptr;
+    HIP_TRY(hipExtStreamCreateWithCUMask(&s, (uint32_t)mask.size(), mask.data()));
+    *stream = s;
+    return SALN_OK;
+}
+
+int saln_stream_destroy(saln_context *ctx, void *stream) {
+    if (!ctx || !stream) return SALN_E_INVALID;
+    HIP_TRY(hipSetDevice(ctx->device));
+    HIP_TRY(hipStreamDestroy((hipStream_t)stream));
+    return SALN_OK;
+}
+
 int saln_nw_span_destroy(saln_nw_span *s) {
     if (!s) return SALN_OK;
     (void)hipSetDevice(s->ctx->device);

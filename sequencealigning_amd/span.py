@@ -228,11 +228,15 @@ class SpanChain:
     run concurrently, each on its own stream, the outbox -> inbox hand-off of
     every band a device copy behind a watch kernel on the edge's stream
     (queued fill 0, hand-offs 0 -> 1, fill 1, ...: each kernel after the work
-    it waits for).  ``pipelined=False`` runs the spans one after another on
-    one stream (every inbox complete before its fill starts)."""
+    it waits for).  ``cu_split`` (default) gives span r its own slice of the
+    device's CUs (a CU-masked stream: its own hardware queue, its stripes on
+    its own SIMDs), the single-GPU emulation of one span per GPU; otherwise
+    the spans' kernels share the device's queues and CUs.
+    ``pipelined=False`` runs the spans one after another on one stream (every
+    inbox complete before its fill starts)."""
 
     def __init__(self, q: bytes, d: bytes, n_spans: int, *, scoring=None, device: int = 0,
-                 band_rows: int = 2048):
+                 band_rows: int = 2048, cu_split: bool = True):
         import torch
         self.q_bytes, self.d_bytes = bytes(q), bytes(d)
         self.len_q, self.len_db = len(q), len(d)
@@ -247,12 +251,37 @@ class SpanChain:
                              device_cols=self.len_q) for lo, hi in self.cols]
         self.bands = _bands(self.len_db, band_rows)
         self.streams = [torch.cuda.Stream(device=dev) for _ in range(2 * n_spans)]
+        self.cu_streams = []
+        if cu_split:
+            L, ctx = _lib.lib(), _lib.context(device)
+            n = C.c_uint32()
+            _lib.check(L.saln_device_cu_count(ctx, C.byref(n)), "saln_device_cu_count")
+            if n.value >= n_spans:
+                for r in range(n_spans):
+                    h = C.c_void_p()
+                    _lib.check(L.saln_stream_create_cu_range(
+                        ctx, n.value * r // n_spans, n.value * (r + 1) // n_spans, C.byref(h)),
+                        "saln_stream_create_cu_range")
+                    self.cu_streams.append(h)
 
     def fill(self, pipelined: bool = True) -> None:
         import torch
         main = torch.cuda.current_stream(self.device)
         for s in self.spans:
             s.reset(main)
+        if pipelined and self.cu_streams:
+            L = _lib.lib()
+            torch.cuda.synchronize(self.device)  # the resets precede every watch
+            xs = self.streams[1::2]
+            for r, s in enumerate(self.spans):
+                s.fill(self.q, self.d, self.cu_streams[r].value)
+                if r + 1 < len(self.spans):
+                    for a, b in self.bands:
+                        _lib.check(L.saln_nw_span_forward(s._h, self.spans[r + 1]._h, a, b,
+                                                          xs[r].cuda_stream),
+                                   "saln_nw_span_forward")
+            torch.cuda.synchronize(self.device)
+            return
         if not pipelined:
             for r, s in enumerate(self.spans):
                 if r:
@@ -295,13 +324,22 @@ class SpanChain:
     def close(self) -> None:
         for s in self.spans:
             s.close()
+        if self.cu_streams:
+            import torch
+            torch.cuda.synchronize(self.device)
+            L, ctx = _lib.lib(), _lib.context(self.device)
+            for h in self.cu_streams:
+                L.saln_stream_destroy(ctx, h)
+            self.cu_streams = []
 
 
 def nw_align_long_spans(q: bytes, d: bytes, n_spans: int, *, scoring=None, device: int = 0,
-                        band_rows: int = 2048, pipelined: bool = True) -> NwAlignment:
+                        band_rows: int = 2048, pipelined: bool = True,
+                        cu_split: bool = True) -> NwAlignment:
     """n_w_align of one pair (needleman_wunsch_affine.rs:424) through n_spans
     column spans on one device (SpanChain)."""
-    ch = SpanChain(q, d, n_spans, scoring=scoring, device=device, band_rows=band_rows)
+    ch = SpanChain(q, d, n_spans, scoring=scoring, device=device, band_rows=band_rows,
+                   cu_split=cu_split)
     try:
         return ch.align(pipelined)
     finally:

@@ -54,8 +54,8 @@ def _vs_oracle(r, qs, ds):
         assert cigar_ops_string(r.cigar) == o.first_ops
 
 
-@pytest.mark.parametrize("pipelined", [True, False])
-def test_span_chain_matches_oracle(pipelined):
+@pytest.mark.parametrize("pipelined,cu_split", [(True, True), (True, False), (False, False)])
+def test_span_chain_matches_oracle(pipelined, cu_split):
     """2-4 spans of mutated and iid pairs (up to 1.6 kbp): score, panic
     status, end states and first printed alignment equal the oracle's."""
     import sequencealigning_amd as saln
@@ -74,7 +74,8 @@ def test_span_chain_matches_oracle(pipelined):
         for n in (2, 3, 4):
             if (len(qs) + 255) // 256 < n:
                 continue
-            r = nw_align_long_spans(qs, ds, n, band_rows=128, pipelined=pipelined)
+            r = nw_align_long_spans(qs, ds, n, band_rows=128, pipelined=pipelined,
+                                    cu_split=cu_split)
             _vs_oracle(r, qs, ds)
             _same(r, saln.n_w_align(qs, ds))
 
