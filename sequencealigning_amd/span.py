@@ -251,18 +251,23 @@ class SpanChain:
                              device_cols=self.len_q) for lo, hi in self.cols]
         self.bands = _bands(self.len_db, band_rows)
         self.streams = [torch.cuda.Stream(device=dev) for _ in range(2 * n_spans)]
-        self.cu_streams = []
+        self.cu_streams, self.edge_streams = [], []
         if cu_split:
+            # span r's fills on CUs [r n / R, (r+1) n / R); the hand-offs of each
+            # edge on a stream of its own (all CUs).  CU-masked streams are not
+            # shared with other streams' hardware queues: no edge's forwards
+            # queue behind another edge's, or behind a fill
             L, ctx = _lib.lib(), _lib.context(device)
             n = C.c_uint32()
             _lib.check(L.saln_device_cu_count(ctx, C.byref(n)), "saln_device_cu_count")
             if n.value >= n_spans:
-                for r in range(n_spans):
+                for lo, hi in [(n.value * r // n_spans, n.value * (r + 1) // n_spans)
+                               for r in range(n_spans)] + [(0, n.value)] * (n_spans - 1):
                     h = C.c_void_p()
-                    _lib.check(L.saln_stream_create_cu_range(
-                        ctx, n.value * r // n_spans, n.value * (r + 1) // n_spans, C.byref(h)),
-                        "saln_stream_create_cu_range")
-                    self.cu_streams.append(h)
+                    _lib.check(L.saln_stream_create_cu_range(ctx, lo, hi, C.byref(h)),
+                               "saln_stream_create_cu_range")
+                    (self.cu_streams if len(self.cu_streams) < n_spans
+                     else self.edge_streams).append(h)
 
     def fill(self, pipelined: bool = True) -> None:
         import torch
@@ -272,13 +277,12 @@ class SpanChain:
         if pipelined and self.cu_streams:
             L = _lib.lib()
             torch.cuda.synchronize(self.device)  # the resets precede every watch
-            xs = self.streams[1::2]
             for r, s in enumerate(self.spans):
                 s.fill(self.q, self.d, self.cu_streams[r].value)
                 if r + 1 < len(self.spans):
                     for a, b in self.bands:
                         _lib.check(L.saln_nw_span_forward(s._h, self.spans[r + 1]._h, a, b,
-                                                          xs[r].cuda_stream),
+                                                          self.edge_streams[r].value),
                                    "saln_nw_span_forward")
             torch.cuda.synchronize(self.device)
             return
@@ -328,9 +332,9 @@ class SpanChain:
             import torch
             torch.cuda.synchronize(self.device)
             L, ctx = _lib.lib(), _lib.context(self.device)
-            for h in self.cu_streams:
+            for h in self.cu_streams + self.edge_streams:
                 L.saln_stream_destroy(ctx, h)
-            self.cu_streams = []
+            self.cu_streams, self.edge_streams = [], []
 
 
 def nw_align_long_spans(q: bytes, d: bytes, n_spans: int, *, scoring=None, device: int = 0,
