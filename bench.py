@@ -441,7 +441,7 @@ def leg_c4(torch, saln, reps=3, cpu=True):
     return out
 
 
-def leg_c4_spans(torch, saln, n_spans=8, reps=3, band_rows=4096):
+def leg_c4_spans(torch, saln, n_spans=8, reps=3, band_rows=1024):
     """configs[3]'s pair split by query columns into `n_spans` spans
     (span.py SpanChain): the spans' fills run
     concurrently on this GPU and hand their boundary rows over in bands
