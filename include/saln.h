@@ -315,8 +315,9 @@ int saln_nw_span_status(saln_nw_span *s, uint32_t *flags);
 int saln_nw_span_set_wait_limit(saln_nw_span *s, uint32_t polls);
 int saln_nw_span_destroy(saln_nw_span *s);
 /* Spans of one pair on ONE device (tests, the single-GPU emulation of the
- * multi-GPU chain): queues on `stream` a watch of src's outbox rows row_lo ..
- * row_hi and their copy into dst's inbox. */
+ * multi-GPU chain): queues on `stream` a one-wave kernel that copies src's
+ * outbox rows row_lo .. row_hi into dst's inbox as they are published (64
+ * rows per round). */
 int saln_nw_span_forward(saln_nw_span *src, saln_nw_span *dst, uint64_t row_lo, uint64_t row_hi,
                          void *stream);
 /* Compute units of the context's device, and a stream whose kernels run only

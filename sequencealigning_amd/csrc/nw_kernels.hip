@@ -2993,6 +2993,46 @@ __global__ __launch_bounds__(64) void nw_span_watch_kernel(const int2 *__restric
     if (__builtin_amdgcn_ballot_w64(failed) && threadIdx.x == 0) atomicOr(err, 1u);
 }
 
+// One device, two spans: forwards rows r0 .. r1 of src's outbox into dst's
+// inbox as they are published, 64 rows per round (one wave; each row one
+// 8-byte sc1 load once published and one sc1 store, the form of the fill's
+// own publication), so dst's first stripe sees them row by row.
+__global__ __launch_bounds__(64) void nw_span_relay_kernel(const int2 *__restrict__ src,
+                                                           int2 *__restrict__ dst, uint32_t r0,
+                                                           uint32_t r1, uint32_t *__restrict__ err) {
+    const uint32_t lim = err[1];
+    uint32_t spins = 0;
+    bool failed = false;
+    for (uint32_t base = r0; base <= r1 && !failed; base += 64) {
+        const uint32_t r = base + threadIdx.x;
+        if (r <= r1) {
+            uint64_t v;
+            for (;;) {
+                v = __hip_atomic_load((const uint64_t *)(src + r), __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_AGENT);
+                if ((uint32_t)v != kColEmpty) break;
+                if (++spins > lim) {
+                    failed = true;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(2);
+            }
+            if (!failed)
+                __hip_atomic_store((uint64_t *)(dst + r), v, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+        }
+        failed = __builtin_amdgcn_ballot_w64(failed) != 0;
+    }
+    if (failed && threadIdx.x == 0) atomicOr(err, 1u);
+}
+
+hipError_t launch_span_relay(const int2 *src, int2 *dst, uint32_t r0, uint32_t r1, uint32_t *err,
+                             hipStream_t stream) {
+    if (r1 < r0) return hipSuccess;
+    nw_span_relay_kernel<<<dim3(1), dim3(64), 0, stream>>>(src, dst, r0, r1, err);
+    return hipGetLastError();
+}
+
 hipError_t launch_span_watch(const int2 *col, uint32_t r0, uint32_t r1, uint32_t *err,
                              hipStream_t stream) {
     if (r1 < r0) return hipSuccess;

@@ -411,9 +411,8 @@ int saln_nw_span_forward(saln_nw_span *src, saln_nw_span *dst, uint64_t row_lo, 
         return SALN_E_INVALID;
     HIP_TRY(hipSetDevice(src->ctx->device));
     hipStream_t st = resolve_stream(stream, src->ctx);
-    HIP_TRY(launch_span_watch(src->outbox(), (uint32_t)row_lo, (uint32_t)row_hi, src->d_err, st));
-    HIP_TRY(hipMemcpyAsync(dst->inbox() + row_lo, src->outbox() + row_lo,
-                           (row_hi - row_lo + 1) * sizeof(int2), hipMemcpyDeviceToDevice, st));
+    HIP_TRY(launch_span_relay(src->outbox(), dst->inbox(), (uint32_t)row_lo, (uint32_t)row_hi,
+                              src->d_err, st));
     return SALN_OK;
 }
 

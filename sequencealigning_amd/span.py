@@ -279,11 +279,10 @@ class SpanChain:
             torch.cuda.synchronize(self.device)  # the resets precede every watch
             for r, s in enumerate(self.spans):
                 s.fill(self.q, self.d, self.cu_streams[r].value)
-                if r + 1 < len(self.spans):
-                    for a, b in self.bands:
-                        _lib.check(L.saln_nw_span_forward(s._h, self.spans[r + 1]._h, a, b,
-                                                          self.edge_streams[r].value),
-                                   "saln_nw_span_forward")
+                if r + 1 < len(self.spans):  # one relay of every row per edge
+                    _lib.check(L.saln_nw_span_forward(s._h, self.spans[r + 1]._h, 1, self.len_db,
+                                                      self.edge_streams[r].value),
+                               "saln_nw_span_forward")
             torch.cuda.synchronize(self.device)
             return
         if not pipelined:
