@@ -498,8 +498,8 @@ def leg_c4_spans(torch, saln, n_spans=8, reps=3, band_rows=1024):
     fill_s, walk_s = float(np.mean(fills)), float(np.mean(walks))
     cells = len(q) * len(d)
     return {"workload": f"configs[3]'s pair as {n_spans} column spans on one GPU, each on "
-                        f"1/{n_spans} of its CUs (CU-masked streams), {band_rows}-row boundary "
-                        f"bands", "value": round(cells / (fill_s + walk_s) / 1e9, 1),
+                        f"1/{n_spans} of its CUs (CU-masked streams), boundary rows relayed "
+                        f"span to span as they are published (one relay kernel per edge)", "value": round(cells / (fill_s + walk_s) / 1e9, 1),
             "unit": "GCUPS", "fill_ms": round(fill_s * 1e3, 3), "walk_ms": round(walk_s * 1e3, 3),
             "walk_ms_reps": [round(x * 1e3, 3) for x in walks],
             "executes": 1 + reps + 2, "span_fill_alone_ms": [round(x, 3) for x in alone],
