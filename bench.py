@@ -444,9 +444,9 @@ def leg_c4(torch, saln, reps=3, cpu=True):
 def leg_c4_spans(torch, saln, n_spans=8, reps=3, band_rows=1024):
     """configs[3]'s pair split by query columns into `n_spans` spans
     (span.py SpanChain): the spans' fills run
-    concurrently on this GPU and hand their boundary rows over in bands
-    (device copies behind watch kernels), then the walk crosses the spans
-    right to left.  The 8-GPU layout on one GPU: each span keeps 1/8 of the
+    concurrently on this GPU, each on its own slice of the CUs, and a relay
+    kernel per edge hands each boundary row over as it is published; then the
+    walk crosses the spans right to left.  The 8-GPU layout on one GPU: each span keeps 1/8 of the
     mask, the stripes are 128 columns wide (the whole pair's stripes share
     this GPU's SIMDs) and the time is the hand-off protocol's cost over the
     one-plan fill (c4); span_fill_alone_ms: each span alone with 64-column
