@@ -197,3 +197,38 @@ def test_sharded_long_pair_rccl_single_rank():
     assert p.exitcode == 0
     want = saln.n_w_align(q, d)
     assert got == (want.score, want.status, want.end_states, want.printed, want.cigar)
+
+
+@pytest.mark.parametrize("shape,n", [("c4_mut_100k", 8), ("iid_20k", 4), ("wide_50k_x_3k", 8),
+                                     ("tall_3k_x_50k", 4)])
+def test_span_chain_very_long_linear_oracle(shape, n):
+    """configs[3]'s 100 kbp pair and other pairs too large for the full-matrix
+    oracle, through n CU-partitioned spans: score, end states, panic status
+    and the first printed alignment equal the linear-memory oracle's
+    (oracle/reflinear.c parent-set fill + the reference DFS's first event),
+    incl. an iid pair whose walks meet sentinel-rooted states."""
+    from nw_check import path_score
+    from oracle import refcpu
+
+    from sequencealigning_amd import synth
+    from sequencealigning_amd.nw import cigar_ops_string
+    from sequencealigning_amd.span import nw_align_long_spans
+    if shape == "c4_mut_100k":
+        q = synth.random_bases(0x5EED0003, 100_000).tobytes()
+        d = synth.mutate(q, 0.05, seed=100_000)
+    elif shape == "iid_20k":
+        q = synth.random_bases(21, 20_000).tobytes()
+        d = synth.random_bases(22, 20_000).tobytes()
+    else:
+        lq, ld = {"wide_50k_x_3k": (50_000, 3_000), "tall_3k_x_50k": (3_000, 50_000)}[shape]
+        base = synth.random_bases(31, max(lq, ld)).tobytes()
+        q = base[:lq]
+        d = synth.mutate(base, 0.1, seed=32)[:ld]
+    r = nw_align_long_spans(q, d, n, band_rows=1024)
+    sc, es, pan, first, _ = refcpu.nw_first_linear(q, d)
+    assert (r.score, r.end_states, r.status == 2) == (sc, es, pan)
+    assert r.printed == (first is not None)
+    if first is not None:
+        assert cigar_ops_string(r.cigar) == first
+        s, ok = path_score(q, d, r.cigar)
+        assert ok and s == r.score
