@@ -818,15 +818,7 @@ __global__ __launch_bounds__(64 * NWV) void nw_traceback_coop_kernel(
         run_op = op;
     };
     int ev;
-#ifdef SALN_COOP_PROF
-    uint32_t pf_iter = 0, pf_load = 0;
-    const uint64_t pf_t0 = __builtin_amdgcn_s_memtime();
-    uint64_t pf_tload = 0, pf_temit = 0;
-#endif
     for (;;) {
-#ifdef SALN_COOP_PROF
-        ++pf_iter;
-#endif
         if (i == 0 || j == 0) {  // every end of the walk is on row or column 0
             if (st == kStM) ev = i == 0 && j == 0 ? kEvOrigin : kEvDead;
             else if (st == kStI) ev = j == 0 && i >= 1 ? kEvPanic : kEvDead;
@@ -846,14 +838,7 @@ __global__ __launch_bounds__(64 * NWV) void nw_traceback_coop_kernel(
         const int32_t lim_i = r_lo == 1 ? i - 1 : i - 1 - r_lo;
         const int32_t lim_j = c_lo == 1 ? j - 1 : j - 1 - c_lo;
         if (i < r_lo || j < c_lo || (st != kStI && lim_i < 0)) {
-#ifdef SALN_COOP_PROF
-            ++pf_load;
-            const uint64_t pq = __builtin_amdgcn_s_memtime();
-#endif
             load(i, j);  // anchored at row i: lim_i >= 0 afterwards
-#ifdef SALN_COOP_PROF
-            pf_tload += __builtin_amdgcn_s_memtime() - pq;
-#endif
             continue;
         }
         // j == c_lo > 1 and the step reads column j-1: one step, lane 0,
@@ -888,14 +873,7 @@ __global__ __launch_bounds__(64 * NWV) void nw_traceback_coop_kernel(
         };
         if (edge) {  // j == c_lo > 1: this step reads column j-1 of the previous stripe
             if (st == kStM) eq0 = eqbit(i, j);  // (i, j) leaves the window now
-#ifdef SALN_COOP_PROF
-            ++pf_load;
-            const uint64_t pq = __builtin_amdgcn_s_memtime();
-#endif
             load(i, j - 1);
-#ifdef SALN_COOP_PROF
-            pf_tload += __builtin_amdgcn_s_memtime() - pq;
-#endif
         }
         int32_t lmax = edge ? 0 : st == kStM ? min(lim_i, lim_j) : st == kStI ? lim_j : lim_i;
         lmax = min(lmax, 63);
@@ -929,9 +907,6 @@ __global__ __launch_bounds__(64 * NWV) void nw_traceback_coop_kernel(
         }
         stop = stop || lane >= lmax;
         const uint64_t sb = __builtin_amdgcn_ballot_w64(stop);
-#ifdef SALN_COOP_PROF
-        const uint64_t pe = __builtin_amdgcn_s_memtime();
-#endif
         const int32_t L = __builtin_ctzll(sb);  // last step of this run (lane lmax always stops)
         const uint32_t n = (uint32_t)L + 1;
         if (st == kStM) {
@@ -970,9 +945,6 @@ __global__ __launch_bounds__(64 * NWV) void nw_traceback_coop_kernel(
             i -= (int32_t)n;
         }
         st = __builtin_amdgcn_readlane(nxt, L);
-#ifdef SALN_COOP_PROF
-        pf_temit += __builtin_amdgcn_s_memtime() - pe;
-#endif
     }
     if (NWV > 1) {  // release the loader waves
         if (lane == 0) req[0] = -1;
@@ -1008,15 +980,6 @@ __global__ __launch_bounds__(64 * NWV) void nw_traceback_coop_kernel(
     }
     if (lane == 0) {
         saln_nw_result r = make_result(hend, WalkOut{ev, nops}, am_end);
-#ifdef SALN_COOP_PROF  // iterations, window loads, total / load clocks (>> 10)
-        r.cigar_len = pf_iter;
-        r.score = (int32_t)pf_load;
-        r.status = (int32_t)((__builtin_amdgcn_s_memtime() - pf_t0) >> 10);
-        r.end_states = (uint8_t)min((uint32_t)(pf_temit * 100 / max(1ull, __builtin_amdgcn_s_memtime() - pf_t0)), 255u);
-        r.printed = 0;
-        r.flags = 0;
-        r.reserved = (uint8_t)min((uint32_t)(pf_tload * 100 / max(1ull, __builtin_amdgcn_s_memtime() - pf_t0)), 255u);
-#endif
         results[p.pair_id] = r;
     }
 }
