@@ -335,6 +335,12 @@ class SpanChain:
                 L.saln_stream_destroy(ctx, h)
             self.cu_streams, self.edge_streams = [], []
 
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
 
 def nw_align_long_spans(q: bytes, d: bytes, n_spans: int, *, scoring=None, device: int = 0,
                         band_rows: int = 2048, pipelined: bool = True,
