@@ -508,7 +508,11 @@ def leg_c4_spans(torch, saln, n_spans=8, reps=3, band_rows=1024):
             "matches_plan": bool((r.score, r.status, r.end_states, r.printed, r.cigar) ==
                                  (want.score, want.status, want.end_states, want.printed,
                                   want.cigar)),
-            "checked": "score, status, end states and the first printed CIGAR vs n_w_align"}
+            "checked": "score, status, end states and the first printed CIGAR vs n_w_align",
+            "roofline": roof_hbm(cells, fill_s, "nw_fill_rows_kernel (8 spans, CU-partitioned)",
+                                 note="1 B/cell of mask over the spans' concurrent fills; bound "
+                                      "by the row chain like c4 (DESIGN.md §6)"),
+            "cpu_baseline": "the c4 leg's (the same pair)"}
 
 
 _C3_PAIRS = {}
