@@ -113,11 +113,6 @@ struct saln_nw_plan {
     // [0, n_fill) and one sync event per sub-batch (+1 for the final join)
     std::vector<uint32_t> sub;
     std::vector<hipEvent_t> sync_ev;
-    // the last sub-batch is the remainder past whole dispatch rounds of the
-    // fill: its traceback runs on the context's third stream beside the
-    // first sub-batch's, and tail_ev marks it done
-    bool tail_split = false;
-    hipEvent_t tail_ev = nullptr;
 };
 
 extern "C" {
@@ -143,8 +138,7 @@ int saln_context_create(int device, saln_context **out) {
     auto *c = new saln_context;
     c->device = device;
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipStreamCreateWithFlags(&c->tb_stream, hipStreamNonBlocking) != hipSuccess ||
-        hipStreamCreateWithFlags(&c->tb_stream2, hipStreamNonBlocking) != hipSuccess) {
+        hipStreamCreateWithFlags(&c->tb_stream, hipStreamNonBlocking) != hipSuccess) {
         delete c;
         set_error("hipStreamCreate failed");
         return SALN_E_HIP;
@@ -161,7 +155,6 @@ int saln_context_destroy(saln_context *ctx) {
     if (ctx->pinned) (void)hipHostFree(ctx->pinned);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     if (ctx->tb_stream) (void)hipStreamDestroy(ctx->tb_stream);
-    if (ctx->tb_stream2) (void)hipStreamDestroy(ctx->tb_stream2);
     delete ctx;
     return SALN_OK;
 }
@@ -177,7 +170,6 @@ int saln_nw_plan_destroy(saln_nw_plan *p) {
                     (void *)p->d_spec_done})
         dev_free(p->ctx, b);
     for (auto &e : p->sync_ev) (void)hipEventDestroy(e);
-    if (p->tail_ev) (void)hipEventDestroy(p->tail_ev);
     for (auto &t : p->ev_pool)
         for (auto &e : t) (void)hipEventDestroy(e);
     delete p;
@@ -445,36 +437,12 @@ int saln_nw_plan_create(saln_context *ctx, const uint64_t *q_off, uint64_t n_q,
         // (SALN_TB_CHUNKS, default 1); boundaries kept even so packed groups
         // stay paired
         uint32_t nsub = 1;
-        const char *tc = std::getenv("SALN_TB_CHUNKS");
-        if (tc) nsub = std::max(1, std::atoi(tc));
+        if (const char *e = std::getenv("SALN_TB_CHUNKS")) nsub = std::max(1, std::atoi(e));
         const uint32_t step = ((p->n_fill + nsub - 1) / nsub + 1) & ~1u;
         p->sub.push_back(0);
         for (uint32_t b = step; b < p->n_fill; b += step) p->sub.push_back(b);
-        // A batch of one packed variant a little past whole dispatch rounds
-        // (C2: 10^5 pairs = 4 rounds of 24,576 + 1,696) runs the remainder as
-        // a second sub-batch: its fill starts once the rounds are done, beside
-        // the first sub-batch's traceback, and its own traceback runs on a
-        // third stream (the walker is latency-bound: a second launch after the
-        // first would add its whole latency).  SALN_TAIL_SPLIT=0: off.
-        const char *ts = std::getenv("SALN_TAIL_SPLIT");
-        if (!tc && !(ts && ts[0] == '0') && p->n_fill && p->var_count[7] == p->n_fill) {
-            const uint64_t round = fill_round_pairs(7, p->var_maxld[7], p->ctx->device);
-            if (round && p->n_fill > round) {
-                const uint64_t tail = p->n_fill % round;
-                if (tail && tail * 4 <= round) {
-                    p->sub.push_back((uint32_t)(p->n_fill - tail));
-                    p->tail_split = true;
-                }
-            }
-        }
         p->sub.push_back(p->n_fill);
         p->sync_ev.resize(p->sub.size() + 1);
-        if (p->tail_split && hipEventCreateWithFlags(&p->tail_ev, hipEventDisableTiming) != hipSuccess) {
-            p->tail_ev = nullptr;
-            set_error("hipEventCreate");
-            saln_nw_plan_destroy(p);
-            return SALN_E_HIP;
-        }
         for (auto &e : p->sync_ev) {
             if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
                 e = nullptr;
@@ -691,10 +659,7 @@ int saln_nw_execute(saln_nw_plan *p, const uint8_t *d_q, const uint8_t *d_db,
         }
         if (ev && k + 1 == nsub) HIP_TRY(hipEventRecord(ev[1], s));
         HIP_TRY(hipEventRecord(p->sync_ev[k], s));
-        // the tail sub-batch's traceback: on the third stream, beside the
-        // first sub-batch's (joined into t below)
-        const hipStream_t tk = (p->tail_split && k + 1 == nsub) ? p->ctx->tb_stream2 : t;
-        if (tk != s) HIP_TRY(hipStreamWaitEvent(tk, p->sync_ev[k], 0));
+        if (t != s) HIP_TRY(hipStreamWaitEvent(t, p->sync_ev[k], 0));
         if (ev && k == 0) HIP_TRY(hipEventRecord(ev[2], t));
         for (int v = 0; v < kNumVariants; ++v) {
             const uint32_t a = std::max(lo, p->var_first[v]);
@@ -707,18 +672,14 @@ int saln_nw_execute(saln_nw_plan *p, const uint8_t *d_q, const uint8_t *d_db,
                              p->d_spec_done, 0},
                     p->spec_blocks, p->spec_pairs, p->d_spec_done, p->spec_passes, d_q, d_db, mask,
                     endh, d_results, d_cigar, p->sc, p->stripe_layout(),
-                    p->spec_strict ? p->d_err : nullptr, tk));
+                    p->spec_strict ? p->d_err : nullptr, t));
             if (a < b && p->score_only)
-                HIP_TRY(launch_score_results(p->d_pairs, a, b - a, endh, d_results, p->sc, tk));
+                HIP_TRY(launch_score_results(p->d_pairs, a, b - a, endh, d_results, p->sc, t));
             else if (a < b)
                 HIP_TRY(launch_traceback(v, p->d_pairs, a, b - a, d_q, d_db, mask, endh, p->d_ops,
-                                         d_results, d_cigar, p->sc, p->stripe_layout(), tk,
+                                         d_results, d_cigar, p->sc, p->stripe_layout(), t,
                                          spec ? p->d_spec_done : nullptr));
         }
-    }
-    if (p->tail_split) {
-        HIP_TRY(hipEventRecord(p->tail_ev, p->ctx->tb_stream2));
-        HIP_TRY(hipStreamWaitEvent(t, p->tail_ev, 0));
     }
     // pairs with an empty side (boundary-only walk) ride on the traceback stream
     if (p->n_pairs > p->n_fill && p->score_only)

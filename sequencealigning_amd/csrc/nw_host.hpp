@@ -19,7 +19,6 @@ struct saln_context {
     int device = 0;
     hipStream_t stream = nullptr;
     hipStream_t tb_stream = nullptr;  // traceback stream (pipelined NW plans)
-    hipStream_t tb_stream2 = nullptr; // the tail sub-batch's traceback (plans split at a round)
     // Device blocks released by plans / host-path calls, kept for reuse
     // (hipMalloc + hipFree of a 3 GB mask workspace cost more than the C2
     // kernels): size -> block; `live` maps handed-out blocks to their size.
@@ -145,10 +144,6 @@ hipError_t launch_avsa_scatter(const saln_nw_result *res, const uint32_t *q_ids,
                                const uint32_t *d_ids, uint64_t n, uint32_t nq_total, int2 *out,
                                hipStream_t stream);
 Geom variant_geom(int v);
-// Pairs the single-frame packed fill of `variant` (walk codes) holds resident
-// on `device` at once (workgroups per CU x CUs x pairs per workgroup); 0 when
-// not known for that variant
-uint64_t fill_round_pairs(int variant, uint32_t ld_max, int device);
 bool variant_packed(int v);
 int choose_variant(uint32_t len_q, uint32_t len_db, const Scoring &sc);
 

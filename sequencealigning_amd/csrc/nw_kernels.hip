@@ -3067,20 +3067,6 @@ hipError_t launch_cigar_compact(const saln_nw_result *res, const uint64_t *src_o
 
 Geom variant_geom(int v) { return kVariants[v]; }
 
-uint64_t fill_round_pairs(int variant, uint32_t ld_max, int device) {
-    if (variant != 7) return 0;  // the 16 x 10 packed fill (configs[1])
-    constexpr int G = 16, K = 10;
-    const size_t lds = (size_t)(256 / G) * (ld_max + 2 * G) * 4;
-    if (lds > kPackedLdsMax) return 0;
-    int blocks = 0, cus = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
-            &blocks, (const void *)nw_fill_pk_kernel<G, K, kCodesWalk, PlanSrc, K, false>, 256,
-            lds) != hipSuccess ||
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess)
-        return 0;
-    return (uint64_t)blocks * (uint64_t)cus * 2u * (256u / G);  // two pairs per lane group
-}
-
 // The packed stripe fill holds a row relative to the stripe's left input:
 // within 256 columns of it values span 256 * (2|m| + 4|ge|) plus the gap
 // and penalty offsets of M / I / D (see nw_fill_stripe_pk_kernel).
