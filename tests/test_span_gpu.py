@@ -232,3 +232,21 @@ def test_span_chain_very_long_linear_oracle(shape, n):
         assert cigar_ops_string(r.cigar) == first
         s, ok = path_score(q, d, r.cigar)
         assert ok and s == r.score
+
+
+@pytest.mark.parametrize("scoring", [(2, -3, -5, -2), (5, -4, -8, -20), (1, -1, -2, -1)])
+def test_span_chain_custom_scoring_matches_plan(scoring):
+    """Other scoring schemes through the spans equal the single-GPU plan's
+    result word for word, incl. gap penalties large enough that the
+    boundary row / column fall to the reference's -32768 sentinel inside a
+    4 kbp pair (dead-end end states, nothing printed)."""
+    import sequencealigning_amd as saln
+    from nw_check import rand_seq
+
+    from sequencealigning_amd.span import nw_align_long_spans
+    rng = np.random.default_rng(45)
+    q = rand_seq(rng, 4000)
+    for d in (_mut(rng, q, 0.05), rand_seq(rng, 3500)):
+        for n in (2, 5):
+            r = nw_align_long_spans(q, d, n, scoring=scoring, band_rows=512)
+            _same(r, saln.n_w_align(q, d, scoring=scoring))
