@@ -323,6 +323,14 @@ int saln_nw_span_forward(saln_nw_span *src, saln_nw_span *dst, uint64_t row_lo, 
 /* Compute units of the context's device, and a stream whose kernels run only
  * on CUs cu_lo .. cu_hi-1 (hipExtStreamCreateWithCUMask): one device split
  * into per-span partitions. */
+/* The walk over all n spans of a pair on ONE device at once: every span's
+ * speculative stripe passes run together over a shared record table, linked
+ * on the host from the end cell to the walk's end.  Returns SALN_OK with the
+ * run words in walk order (from the end cell) and the final exit, 1 when the
+ * passes do not link (walk span by span with saln_nw_span_walk), or an error. */
+int saln_nw_spans_walk(saln_nw_span *const *spans, uint32_t n, const uint8_t *d_q,
+                       const uint8_t *d_db, saln_nw_span_cursor *exit, uint32_t *ops,
+                       uint64_t ops_cap, uint64_t *n_ops, void *stream);
 int saln_device_cu_count(saln_context *ctx, uint32_t *n);
 int saln_stream_create_cu_range(saln_context *ctx, uint32_t cu_lo, uint32_t cu_hi, void **stream);
 int saln_stream_destroy(saln_context *ctx, void *stream);

@@ -91,7 +91,7 @@ EXPORTS = [
     "saln_nw_span_boundary_elems", "saln_nw_span_boundary_cols", "saln_nw_span_create", "saln_nw_span_info",
     "saln_nw_span_boundary", "saln_nw_span_reset", "saln_nw_span_fill", "saln_nw_span_watch",
     "saln_nw_span_walk", "saln_nw_span_score", "saln_nw_span_status",
-    "saln_nw_span_set_wait_limit", "saln_nw_span_destroy", "saln_nw_span_forward",
+    "saln_nw_span_set_wait_limit", "saln_nw_span_destroy", "saln_nw_span_forward", "saln_nw_spans_walk",
     "saln_device_cu_count", "saln_stream_create_cu_range", "saln_stream_destroy",
     "saln_wfa_align_batch", "saln_wfa_render", "saln_wfa_plan_create", "saln_wfa_execute",
     "saln_wfa_plan_destroy",
@@ -192,6 +192,8 @@ def lib() -> C.CDLL:
         L.saln_nw_span_set_wait_limit.argtypes = [vp, C.c_uint32]
         L.saln_nw_span_destroy.argtypes = [vp]
         L.saln_nw_span_forward.argtypes = [vp, vp, C.c_uint64, C.c_uint64, vp]
+        L.saln_nw_spans_walk.argtypes = [C.POINTER(vp), C.c_uint32, vp, vp, C.POINTER(SpanCursor),
+                                         u32p, C.c_uint64, u64p, vp]
         L.saln_device_cu_count.argtypes = [vp, u32p]
         L.saln_stream_create_cu_range.argtypes = [vp, C.c_uint32, C.c_uint32, C.POINTER(vp)]
         L.saln_stream_destroy.argtypes = [vp, vp]

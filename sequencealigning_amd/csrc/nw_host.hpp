@@ -126,7 +126,8 @@ hipError_t launch_span_relay(const int2 *src, int2 *dst, uint32_t r0, uint32_t r
                              hipStream_t stream);
 hipError_t launch_span_spec(const NwPairDesc *pairs, SpecArgs sa, uint32_t n_blocks, int passes,
                             const uint8_t *qs, const uint8_t *ds, const uint8_t *mask,
-                            const int32_t *end_h, Scoring sc, hipStream_t stream);
+                            const int32_t *end_h, Scoring sc, hipStream_t stream,
+                            int pass_lo = 1);
 // score-only all-vs-all (nw_avsa.cpp); avsa_chunk_pairs: the most pairs one
 // launch of a packed class may take (0: not a packed variant)
 uint64_t avsa_chunk_pairs(int variant);

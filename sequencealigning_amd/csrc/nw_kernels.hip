@@ -2914,7 +2914,7 @@ hipError_t launch_span_walk(const NwPairDesc *pairs, SpecArgs sa, const uint8_t 
 // entry; the host links the stored walks (nw_span.cpp).
 hipError_t launch_span_spec(const NwPairDesc *pairs, SpecArgs sa, uint32_t n_blocks, int passes,
                             const uint8_t *qs, const uint8_t *ds, const uint8_t *mask,
-                            const int32_t *end_h, Scoring sc, hipStream_t stream) {
+                            const int32_t *end_h, Scoring sc, hipStream_t stream, int pass_lo) {
     constexpr int kLoaders = 4;
     constexpr int32_t rows = 296;
     const size_t lds = (size_t)(rows + 1) * kCoopLine + 16 + 272 + (size_t)rows + 16;
@@ -2923,7 +2923,7 @@ hipError_t launch_span_spec(const NwPairDesc *pairs, SpecArgs sa, uint32_t n_blo
         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     if (attr != hipSuccess) return attr;
     sa.span = 0;  // every stripe stops at its own left edge
-    for (int k = 1; k <= passes; ++k) {
+    for (int k = pass_lo; k <= passes; ++k) {
         sa.pass = k;
         nw_traceback_coop_kernel<kLoaders, 2, true><<<dim3(n_blocks), dim3(64 * kLoaders), lds, stream>>>(
             pairs, 0, mask, end_h, nullptr, nullptr, sc, rows, qs, ds, sa);

@@ -416,6 +416,99 @@ int saln_nw_span_forward(saln_nw_span *src, saln_nw_span *dst, uint64_t row_lo, 
     return SALN_OK;
 }
 
+int saln_nw_spans_walk(saln_nw_span *const *spans, uint32_t n, const uint8_t *d_q,
+                       const uint8_t *d_db, saln_nw_span_cursor *exit, uint32_t *ops,
+                       uint64_t ops_cap, uint64_t *n_ops, void *stream) {
+    if (!spans || !n || !d_q || !d_db || !exit || !n_ops) return SALN_E_INVALID;
+    *n_ops = 0;
+    const saln_nw_span *f = spans[0];
+    if (f->col_lo != 0 || spans[n - 1]->col_hi != f->lq) return SALN_E_INVALID;
+    for (uint32_t r = 0; r < n; ++r) {
+        const saln_nw_span *s = spans[r];
+        if (s->ctx != f->ctx || s->lq != f->lq || s->ld != f->ld ||
+            (r + 1 < n && s->col_hi != spans[r + 1]->col_lo))
+            return SALN_E_INVALID;
+        if (!s->spec_passes) return 1;  // a span without speculative tables: walk span by span
+    }
+    HIP_TRY(hipSetDevice(f->ctx->device));
+    hipStream_t st = resolve_stream(stream, f->ctx);
+    const uint32_t T = (f->lq + 255) / 256;  // the pair's walker stripes
+    const int P = f->spec_passes;
+    SpecStripe *d_rec = nullptr, *h_rec = nullptr;
+    uint32_t *d_ops = nullptr, *h_ops = nullptr;
+    int rc = SALN_OK;
+    auto done = [&](int r) {
+        if (d_rec) dev_free(f->ctx, d_rec);
+        if (d_ops) dev_free(f->ctx, d_ops);
+        if (h_rec) (void)hipHostFree(h_rec);
+        if (h_ops) (void)hipHostFree(h_ops);
+        return r;
+    };
+    const size_t ops_words = (size_t)T * kSpecOpsCap;
+    if (dev_alloc(f->ctx, (void **)&d_rec, (T + 1) * sizeof(SpecStripe)) != hipSuccess ||
+        dev_alloc(f->ctx, (void **)&d_ops, ops_words * sizeof(uint32_t)) != hipSuccess ||
+        hipHostMalloc((void **)&h_rec, (T + 1) * sizeof(SpecStripe), 0) != hipSuccess ||
+        hipHostMalloc((void **)&h_ops, ops_words * sizeof(uint32_t), 0) != hipSuccess) {
+        set_error("spans walk: tables");
+        return done(SALN_E_HIP);
+    }
+    for (uint32_t t = 0; t <= T; ++t) {
+        h_rec[t] = SpecStripe{};
+        h_rec[t].in_k = kSpecNone;
+    }
+    // one record array for the pair's stripes (pair-wide index) shared by
+    // every span's launch: a span's rightmost stripe reads the exit of the
+    // next span's leftmost stripe from the previous pass, the pair's last
+    // stripe enters at the end cell (nw_traceback_coop_kernel kSpec)
+    if (hipMemcpyAsync(d_rec, h_rec, (T + 1) * sizeof(SpecStripe), hipMemcpyHostToDevice, st) !=
+        hipSuccess)
+        return done(SALN_E_HIP);
+    for (int k = 1; k <= P; ++k)
+        for (uint32_t r = 0; r < n; ++r) {
+            const saln_nw_span *s = spans[r];
+            SpecArgs sa{s->d_sblocks, s->d_ssp, d_rec, d_ops, nullptr, k, 0, 0, 0};
+            if (launch_span_spec(s->d_pair, sa, s->ntiles, k, d_q, d_db, s->mask_arg(), s->d_endh,
+                                 s->sc, st, k) != hipSuccess)
+                return done(SALN_E_HIP);
+        }
+    if (hipMemcpyAsync(h_rec, d_rec, T * sizeof(SpecStripe), hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipMemcpyAsync(h_ops, d_ops, ops_words * sizeof(uint32_t), hipMemcpyDeviceToHost, st) !=
+            hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess)
+        return done(SALN_E_HIP);
+    // link from the end cell's stripe leftwards (as span_walk_spec)
+    const int cf = P & 1;
+    int32_t ci = (int32_t)f->ld, cj = (int32_t)f->lq, ck = kSpecEnd;
+    uint64_t nw = 0;
+    for (int t = (int)T - 1;; --t) {
+        const SpecStripe &r = h_rec[t];
+        if (r.in_i != ci || r.in_j != cj || r.in_k != ck || r.nops > kSpecOpsCap) return done(1);
+        if (ops && nw + r.nops > ops_cap) {
+            set_error("spans walk: ops buffer too small");
+            return done(SALN_E_CAPACITY);
+        }
+        if (ops) std::memcpy(ops + nw, h_ops + (size_t)t * kSpecOpsCap, r.nops * sizeof(uint32_t));
+        nw += r.nops;
+        ci = r.out_i[cf];
+        cj = r.out_j[cf];
+        ck = r.out_k[cf];
+        if (ck >= kSpecEv || t == 0) break;
+    }
+    const uint32_t es = h_rec[T - 1].am_end;
+    // not ended at column 0, or a dead end with tied end states left (the
+    // span-by-span walk restarts in the next state): walk span by span
+    if (ck < kSpecEv || ck == kSpecNone ||
+        (ck - kSpecEv == 2 /* dead */ && (es & ~(uint32_t)(es & 4u ? 4u : es & 1u ? 1u : 2u))))
+        return done(1);
+    *n_ops = nw;
+    exit->i = ci;
+    exit->j = cj;
+    exit->kind = ck;
+    exit->end_states = es;
+    (void)rc;
+    return done(SALN_OK);
+}
+
 int saln_device_cu_count(saln_context *ctx, uint32_t *n) {
     if (!ctx || !n) return SALN_E_INVALID;
     int v = 0;

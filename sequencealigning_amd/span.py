@@ -316,6 +316,21 @@ class SpanChain:
         torch.cuda.synchronize(self.device)
         self.check()
         score, status = self.spans[-1].score()
+        # every span's speculative passes at once over one record table
+        # (saln_nw_spans_walk); span by span when they do not link
+        L = _lib.lib()
+        hs = (C.c_void_p * len(self.spans))(*[s._h.value for s in self.spans])
+        cap = self.len_q + self.len_db + 16
+        buf = (C.c_uint32 * cap)()
+        ex, n = _lib.SpanCursor(), C.c_uint64()
+        rc = L.saln_nw_spans_walk(hs, len(self.spans), C.c_void_p(self.q.data_ptr()),
+                                  C.c_void_p(self.d.data_ptr()), C.byref(ex), buf, cap,
+                                  C.byref(n), _lib.torch_stream(self.device))
+        if rc == _lib.OK:
+            ops = np.ctypeslib.as_array(buf)[:n.value].copy()
+            return result_from_walk(score, status, ex.kind - SPAN_EXIT, ex.end_states, [ops])
+        if rc != 1:
+            _lib.check(rc, "saln_nw_spans_walk")
         walkers = [lambda e, s=s: s.walk(self.q, self.d, e) for s in self.spans]
         ev, es, segs = walk_spans(walkers, self.len_q, self.len_db)
         return result_from_walk(score, status, ev, es, segs)
