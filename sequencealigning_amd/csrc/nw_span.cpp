@@ -440,18 +440,20 @@ int saln_nw_spans_walk(saln_nw_span *const *spans, uint32_t n, const uint8_t *d_
     auto done = [&](int r) {
         if (d_rec) dev_free(f->ctx, d_rec);
         if (d_ops) dev_free(f->ctx, d_ops);
-        if (h_rec) (void)hipHostFree(h_rec);
-        if (h_ops) (void)hipHostFree(h_ops);
         return r;
     };
     const size_t ops_words = (size_t)T * kSpecOpsCap;
+    // host copies in the context's pinned staging buffer (grow-only, reused)
+    const size_t rec_bytes = ((T + 1) * sizeof(SpecStripe) + 255) & ~(size_t)255;
+    void *stage = nullptr;
     if (dev_alloc(f->ctx, (void **)&d_rec, (T + 1) * sizeof(SpecStripe)) != hipSuccess ||
         dev_alloc(f->ctx, (void **)&d_ops, ops_words * sizeof(uint32_t)) != hipSuccess ||
-        hipHostMalloc((void **)&h_rec, (T + 1) * sizeof(SpecStripe), 0) != hipSuccess ||
-        hipHostMalloc((void **)&h_ops, ops_words * sizeof(uint32_t), 0) != hipSuccess) {
+        pinned_staging(f->ctx, rec_bytes + ops_words * sizeof(uint32_t), &stage) != hipSuccess) {
         set_error("spans walk: tables");
         return done(SALN_E_HIP);
     }
+    h_rec = (SpecStripe *)stage;
+    h_ops = (uint32_t *)((uint8_t *)stage + rec_bytes);
     for (uint32_t t = 0; t <= T; ++t) {
         h_rec[t] = SpecStripe{};
         h_rec[t].in_k = kSpecNone;
