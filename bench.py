@@ -64,6 +64,18 @@ ALL_LEGS = ("c5", "c1", "c3", "c3_affine", "c4", "c4_spans", "host")
 PMC_FILES = ("pmc_traffic.json", "pmc_legs.json")  # under profiles/
 
 
+# SALN_* environment variables the bench runs with (recorded in the JSON
+# line).  The engine reads no environment variable (its tuning goes through
+# saln_option_set); SALN_LIB would load a tools/ build instead of the
+# product, and any other SALN_* is a leftover of an experiment script.
+ALLOWED_ENV: tuple = ()
+
+
+def refused_env(environ=None) -> list:
+    environ = os.environ if environ is None else environ
+    return sorted(k for k in environ if k.startswith("SALN_") and k not in ALLOWED_ENV)
+
+
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
@@ -78,7 +90,15 @@ def cpu_threads() -> int:
     return max(1, min(n, 16))
 
 
-def cpu_baseline(budget_s: float = 12.0) -> dict:
+# The reference's DFS (needleman_wunsch_affine.rs:281-329) enumerates every
+# co-optimal alignment; on 150 x 150 G-iid pairs ~20 % of them need more
+# than 10^5 stack pops (round 3 capped there, which overstated the CPU
+# path ~4x) and ~1 in 2,000 more than 10^8.  The baseline caps a pair's
+# enumeration at 10^8 pops (seconds of CPU) and reports how many hit it.
+CPU_MAX_POPS = 100_000_000
+
+
+def cpu_baseline(budget_s: float = 15.0) -> dict:
     """Oracle (C port of the reference CPU path: full 3-matrix fill with
     parent sets + the reference's exhaustive DFS traceback) on a bounded
     sample of the same workload: one core for ~budget/3 (the reference's own
@@ -90,27 +110,43 @@ def cpu_baseline(budget_s: float = 12.0) -> dict:
     n = 60000
     qs, qo, ds, do = synth.iid_pairs(n, LQ, LD, seed=SEED)
     qb, db = qs.tobytes(), ds.tobytes()
-    done = cells = 0
+    done = cells = capped1 = 0
     t0 = time.perf_counter()
     while done < n and time.perf_counter() - t0 < budget_s / 3:
-        k = min(64, n - done)
-        cells += refcpu.run_pairs(qb[done * LQ:(done + k) * LQ], qo[:k + 1],
-                                  db[done * LD:(done + k) * LD], do[:k + 1], k, max_pops=100_000)
+        k = min(16, n - done)
+        c, nc = refcpu.run_pairs_capped(qb[done * LQ:(done + k) * LQ], qo[:k + 1],
+                                        db[done * LD:(done + k) * LD], do[:k + 1], k,
+                                        max_pops=CPU_MAX_POPS)
+        cells += c
+        capped1 += nc
         done += k
     dt1 = time.perf_counter() - t0
     rate1 = cells / dt1  # cells/s on one core
     T = cpu_threads()
     # pairs for ~2/3 of the budget at T x the one-core rate (sublinear scaling only shortens it)
-    n_mt = int(min(n, max(T * 64, rate1 * T * (2 * budget_s / 3) / (LQ * LD))))
+    n_mt = int(min(n, max(T * 16, rate1 * T * (2 * budget_s / 3) / (LQ * LD))))
     t0 = time.perf_counter()
-    cells_mt = refcpu.run_pairs_mt(qb[:n_mt * LQ], qo[:n_mt + 1], db[:n_mt * LD], do[:n_mt + 1],
-                                   n_mt, max_pops=100_000, threads=T)
+    cells_mt, capped_mt = refcpu.run_pairs_capped(qb[:n_mt * LQ], qo[:n_mt + 1], db[:n_mt * LD],
+                                                  do[:n_mt + 1], n_mt, max_pops=CPU_MAX_POPS,
+                                                  threads=T)
     dtm = time.perf_counter() - t0
+    # the round-3 cap on the same multi-core sample, for comparison
+    t0 = time.perf_counter()
+    cells_5, capped_5 = refcpu.run_pairs_capped(qb[:n_mt * LQ], qo[:n_mt + 1], db[:n_mt * LD],
+                                                do[:n_mt + 1], n_mt, max_pops=100_000, threads=T)
+    dt5 = time.perf_counter() - t0
     return {"value": round(cells_mt / dtm / 1e9, 6), "unit": "GCUPS", "cores": T, "kind": "port",
             "value_1core": round(rate1 / 1e9, 6),
+            "max_pops": CPU_MAX_POPS,
+            "capped_pairs": int(capped_mt), "capped_frac": round(capped_mt / max(1, n_mt), 5),
+            "capped_pairs_1core": int(capped1),
+            "at_1e5_pops": {"value": round(cells_5 / dt5 / 1e9, 6),
+                            "capped_frac": round(capped_5 / max(1, n_mt), 4)},
             "sample": f"{n_mt} of the 150x150 G-iid pairs (seed {SEED:#x}) on {T} threads in "
                       f"{dtm:.1f} s, {done} pairs on 1 thread in {dt1:.1f} s; oracle/refcpu.c "
-                      f"fill + literal DFS (<=1e5 pops/pair)"}
+                      f"fill + literal DFS, each pair's enumeration capped at {CPU_MAX_POPS:.0e} "
+                      f"stack pops ({capped_mt} of {n_mt} pairs reached it; at round 3's 1e5 "
+                      f"cap {capped_5} did)"}
 
 
 # ------------------------------------------------------------- rooflines
@@ -725,9 +761,11 @@ def main() -> None:
                     help="only start the ranks and report the world (no GPU work; tests)")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend (nccl = RCCL)")
     args = ap.parse_args()
-    if os.environ.get("SALN_LIB"):
-        sys.exit("bench.py: SALN_LIB is set (an instrumented tools/ build); the bench measures "
-                 "the product library sequencealigning_amd/libsaln.so only")
+    bad = refused_env()
+    if bad:
+        sys.exit(f"bench.py: {', '.join(bad)} set in the environment; the bench measures the "
+                 f"product library sequencealigning_amd/libsaln.so with its default options "
+                 f"(allowed SALN_* variables: {', '.join(ALLOWED_ENV) or 'none'})")
     env_world = os.environ.get("WORLD_SIZE")
     if env_world is None and args.gpus > 1:
         sys.exit(launch_ranks(args.gpus))
@@ -849,6 +887,8 @@ def main() -> None:
                                                                else "")},
             "roofline": roof,
             "status_counts": {"ok": int(statuses[0]), "ref_panic_boundary": int(statuses[2])},
+            "env": {k: os.environ[k] for k in ALLOWED_ENV if k in os.environ},
+            "options": saln._lib.non_default_options(),
         }
         if not args.score_only:
             out["verified"] = verify_c2(hr, cig[last].cpu().numpy().view(np.uint32),

@@ -42,6 +42,8 @@ typedef enum {
     SALN_REF_PANIC_SLICE = 4,    /* WFA rec_tr slice panic, wfa.rs:695-744 */
     SALN_NONCONVERGED = 5,       /* WFA score loop hit the caller's step cap (wfa.rs:28) */
     SALN_ENUM_CAP = 6,           /* NW co-optimal enumeration hit the caller's cap */
+    SALN_SPAN_UNLINKED = 7,      /* saln_nw_spans_walk only: the speculative passes did not
+                                    link; walk span by span (saln_nw_span_walk) */
 
     SALN_E_INVALID = -1,   /* bad argument */
     SALN_E_HIP = -2,       /* HIP runtime error (message: saln_last_error) */
@@ -58,7 +60,7 @@ typedef enum {
 /* Device error flags (saln_nw_plan_status, saln_nw_avsa_status). */
 #define SALN_FLAG_WAIT_TIMEOUT 1u  /* a column-stripe fill's wait for its left neighbour's
                                       boundary rows exceeded the plan's wait limit */
-#define SALN_FLAG_SPEC_UNLINKED 2u /* test builds only (SALN_SPEC_STRICT=1): a speculative
+#define SALN_FLAG_SPEC_UNLINKED 2u /* tests only (option nw.spec_strict = 1): a speculative
                                       stripe walk fell back to the sequential walker */
 
 /* ScoringScheme, needleman_wunsch_affine.rs:15-20 / :382-388.
@@ -108,6 +110,24 @@ int saln_context_destroy(saln_context *ctx);
 const char *saln_last_error(void);     /* thread-local message for the last error */
 int saln_abi_version(void);
 
+/* ---------------------------------------------------------------- options
+ * Process-wide tuning knobs (kernel geometry and A/B variants), all with the
+ * product's defaults.  No reference counterpart: the reference has no tuning
+ * (its constants are compile-time, needleman_wunsch_affine.rs:15-20).  The
+ * engine reads nothing from the process environment; these calls are the only
+ * way to change what it runs.  Every option gives the same results; most are
+ * read when a plan is created.  Names: "nw.pk_steady", "nw.wide_min_pairs",
+ * "nw.tb_chunks", "nw.fill_lds_min", "nw.rows_k", "nw.stripe_pk", "nw.spec",
+ * "nw.spec_passes", "nw.spec_strict", "nw.avsa_narrow", "nw.nib_codes",
+ * "nw.narrow_walk", "wfa2.seq_lds", "wfa2.w1", "wfa2.w2", "host.timing".
+ * SALN_E_INVALID for an unknown name or a value out of range. */
+int saln_option_set(const char *name, int64_t value);
+int saln_option_get(const char *name, int64_t *value, int64_t *default_value);
+/* Name of option `index` (0, 1, ...; SALN_E_INVALID past the last). */
+int saln_option_name(uint32_t index, const char **name);
+/* Every option back to its default. */
+int saln_options_reset(void);
+
 /* ------------------------------------------------------- NW: per pair (drop-in)
  * Replaces `pub fn n_w_align(seq1: &Record, seq2: &Record, _verbose: bool,
  * mode: Mode) -> Result<()>` (needleman_wunsch_affine.rs:424-437).
@@ -129,6 +149,36 @@ int saln_nw_align(saln_context *ctx, const uint8_t *q, uint64_t len_q, const uin
 int saln_nw_render(saln_context *ctx, const uint8_t *q, uint64_t len_q, const uint8_t *d,
                    uint64_t len_db, int32_t mode, uint64_t max_blocks, char *out, uint64_t cap,
                    uint64_t *out_len, uint64_t *n_blocks, int32_t *status);
+
+/* The same text for a batch, each pair computed once (the drop-in CLI and
+ * hosts that print per pair).  Replaces the pair loop main.rs:61-74 with the
+ * text every n_w_align call prints: one plan for all pairs (same CSR / pair
+ * conventions as saln_nw_align_batch; NULL pair lists = all-vs-all, db outer),
+ * the reference DFS per pair on host threads.  The text stays in the
+ * returned handle until saln_nw_text_free.  stop_at_panic = 1: pairs after
+ * the first one whose traceback panics (REF_PANIC_BOUNDARY) are not rendered
+ * - the reference aborts there (exit 101) - so saln_nw_text_count is that
+ * pair's index + 1.  mode != GLOBAL: every pair SALN_NOT_IMPLEMENTED with no
+ * text (main.rs:68-74 prints the error and goes on). */
+typedef struct saln_nw_text saln_nw_text;
+int saln_nw_render_batch(saln_context *ctx, const uint8_t *q_seq, const uint64_t *q_off,
+                         uint64_t n_q, const uint8_t *db_seq, const uint64_t *db_off,
+                         uint64_t n_db, const uint32_t *pair_q, const uint32_t *pair_db,
+                         uint64_t n_pairs, int32_t mode, uint64_t max_blocks, int stop_at_panic,
+                         saln_nw_text **out);
+/* One pair in one call: saln_nw_render_batch of (q, d). */
+int saln_nw_render_text(saln_context *ctx, const uint8_t *q, uint64_t len_q, const uint8_t *d,
+                        uint64_t len_db, int32_t mode, uint64_t max_blocks, saln_nw_text **out);
+uint64_t saln_nw_text_count(const saln_nw_text *t);
+/* Pair `pair` (< count): its text (valid until free; not NUL-terminated), the
+ * blocks printed, the render status (SALN_OK, SALN_REF_PANIC_BOUNDARY after
+ * the text, SALN_ENUM_CAP, SALN_NOT_IMPLEMENTED), its saln_nw_result, and
+ * its wall time (its DFS plus its share of the batch's device work).  Any
+ * output pointer may be NULL. */
+int saln_nw_text_get(const saln_nw_text *t, uint64_t pair, const char **text, uint64_t *len,
+                     uint64_t *n_blocks, int32_t *status, saln_nw_result *result,
+                     uint64_t *elapsed_ns);
+void saln_nw_text_free(saln_nw_text *t);
 
 /* Dense parent mask for parity checks: (len_db+1) x (len_q+1) bytes,
  * row-major over db.  Byte bits: 0-2 = {M,I,D} equal to max(M,I,D) at the
@@ -326,8 +376,10 @@ int saln_nw_span_forward(saln_nw_span *src, saln_nw_span *dst, uint64_t row_lo, 
 /* The walk over all n spans of a pair on ONE device at once: every span's
  * speculative stripe passes run together over a shared record table, linked
  * on the host from the end cell to the walk's end.  Returns SALN_OK with the
- * run words in walk order (from the end cell) and the final exit, 1 when the
- * passes do not link (walk span by span with saln_nw_span_walk), or an error. */
+ * pair's CIGAR in `ops` (forward order, runs of one op merged across the
+ * spans' seams: the words saln_nw_align gives when the walk printed) and the
+ * final exit, SALN_SPAN_UNLINKED when the passes do not link (walk span by
+ * span with saln_nw_span_walk), or an error. */
 int saln_nw_spans_walk(saln_nw_span *const *spans, uint32_t n, const uint8_t *d_q,
                        const uint8_t *d_db, saln_nw_span_cursor *exit, uint32_t *ops,
                        uint64_t ops_cap, uint64_t *n_ops, void *stream);

@@ -184,6 +184,12 @@ static int parents_of(const ref_nw_mats *m, int state, size_t x, size_t y, int *
 
 int ref_nw_traceback_dfs(const uint8_t *q, const uint8_t *d, const ref_nw_mats *m, char *out,
                          size_t out_cap, size_t *out_len, uint64_t max_pops, uint64_t *n_blocks) {
+    return ref_nw_traceback_dfs_blocks(q, d, m, out, out_cap, out_len, max_pops, 0, n_blocks);
+}
+
+int ref_nw_traceback_dfs_blocks(const uint8_t *q, const uint8_t *d, const ref_nw_mats *m,
+                                char *out, size_t out_cap, size_t *out_len, uint64_t max_pops,
+                                uint64_t max_blocks, uint64_t *n_blocks) {
     const size_t W = m->lq + 1;
     const size_t ex = m->ld, ey = m->lq, ek = ex * W + ey;
     sink s = {out, out_cap, 0};
@@ -211,6 +217,12 @@ int ref_nw_traceback_dfs(const uint8_t *q, const uint8_t *d, const ref_nw_mats *
             break;
         }
         if (e.x == 0 && e.y == 0) { /* :283-286 */
+            if (max_blocks && blocks >= max_blocks) { /* caller's block cap (not the reference's) */
+                free(e.s1);
+                free(e.s2);
+                rc = 3;
+                break;
+            }
             print_block(&s, &e);
             ++blocks;
         }
@@ -382,9 +394,10 @@ int ref_nw_dag_summary(const uint8_t *q, const uint8_t *d, const ref_nw_mats *m,
     return 0;
 }
 
-uint64_t ref_nw_run_pairs(const uint8_t *qs, const uint64_t *q_off, const uint8_t *ds,
-                          const uint64_t *d_off, uint64_t n_pairs, uint64_t max_pops) {
-    uint64_t cells = 0;
+uint64_t ref_nw_run_pairs_capped(const uint8_t *qs, const uint64_t *q_off, const uint8_t *ds,
+                                 const uint64_t *d_off, uint64_t n_pairs, uint64_t max_pops,
+                                 uint64_t max_blocks, uint64_t *capped) {
+    uint64_t cells = 0, nc = 0;
     for (uint64_t p = 0; p < n_pairs; ++p) {
         const uint8_t *q = qs + q_off[p], *d = ds + d_off[p];
         const size_t lq = q_off[p + 1] - q_off[p], ld = d_off[p + 1] - d_off[p];
@@ -392,11 +405,19 @@ uint64_t ref_nw_run_pairs(const uint8_t *qs, const uint64_t *q_off, const uint8_
         if (ref_nw_fill(q, lq, d, ld, &m) != 0) break;
         size_t olen = 0;
         uint64_t nb = 0;
-        ref_nw_traceback_dfs(q, d, &m, NULL, 0, &olen, max_pops, &nb);
+        /* rc 2: the DFS stopped at max_pops (the reference enumerates on) */
+        if (ref_nw_traceback_dfs_blocks(q, d, &m, NULL, 0, &olen, max_pops, max_blocks, &nb) == 2)
+            ++nc;
         ref_nw_free(&m);
         cells += (uint64_t)lq * ld;
     }
+    if (capped) *capped = nc;
     return cells;
+}
+
+uint64_t ref_nw_run_pairs(const uint8_t *qs, const uint64_t *q_off, const uint8_t *ds,
+                          const uint64_t *d_off, uint64_t n_pairs, uint64_t max_pops) {
+    return ref_nw_run_pairs_capped(qs, q_off, ds, d_off, n_pairs, max_pops, 0, NULL);
 }
 
 /* ---- FASTA parser, parse.rs:52-99 ---- */

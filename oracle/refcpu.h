@@ -62,6 +62,11 @@ void ref_nw_dense_mask(const ref_nw_mats *m, uint8_t *out);
 int ref_nw_traceback_dfs(const uint8_t *q, const uint8_t *d, const ref_nw_mats *m,
                          char *out, size_t out_cap, size_t *out_len,
                          uint64_t max_pops, uint64_t *n_blocks);
+/* The same DFS stopping before the (max_blocks+1)-th printed block (rc 3;
+ * 0 = no cap): the text of `saln --max-blocks N`. */
+int ref_nw_traceback_dfs_blocks(const uint8_t *q, const uint8_t *d, const ref_nw_mats *m,
+                                char *out, size_t out_cap, size_t *out_len, uint64_t max_pops,
+                                uint64_t max_blocks, uint64_t *n_blocks);
 
 /* Score = max(M,I,D)[ld][lq] (:247-250). end_states: bit0 M, bit1 I, bit2 D. */
 int32_t ref_nw_score(const ref_nw_mats *m, uint8_t *end_states);
@@ -79,7 +84,16 @@ int ref_nw_dag_summary(const uint8_t *q, const uint8_t *d, const ref_nw_mats *m,
  * Sequences are CSR (seq + offsets, n+1).  Returns cells processed. */
 uint64_t ref_nw_run_pairs(const uint8_t *qs, const uint64_t *q_off, const uint8_t *ds,
                           const uint64_t *d_off, uint64_t n_pairs, uint64_t max_pops);
-/* refmt.c: ref_nw_run_pairs over contiguous slices of the pairs on threads */
+/* ref_nw_run_pairs, also counting the pairs whose DFS stopped at max_pops
+ * (*capped, may be NULL) */
+uint64_t ref_nw_run_pairs_capped(const uint8_t *qs, const uint64_t *q_off, const uint8_t *ds,
+                                 const uint64_t *d_off, uint64_t n_pairs, uint64_t max_pops,
+                                 uint64_t max_blocks, uint64_t *capped);
+/* refmt.c: ref_nw_run_pairs over contiguous slices of the pairs on threads
+ * (_capped: with the count of capped pairs) */
+uint64_t ref_nw_run_pairs_mt_capped(const uint8_t *qs, const uint64_t *q_off, const uint8_t *ds,
+                                    const uint64_t *d_off, uint64_t n_pairs, uint64_t max_pops,
+                                    uint64_t max_blocks, int threads, uint64_t *capped);
 uint64_t ref_nw_run_pairs_mt(const uint8_t *qs, const uint64_t *q_off, const uint8_t *ds,
                              const uint64_t *d_off, uint64_t n_pairs, uint64_t max_pops,
                              int threads);

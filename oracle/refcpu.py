@@ -56,6 +56,17 @@ def lib():
         L.ref_nw_run_pairs_mt.argtypes = [u8p, C.POINTER(C.c_uint64), u8p, C.POINTER(C.c_uint64),
                                           C.c_uint64, C.c_uint64, C.c_int]
         L.ref_nw_run_pairs_mt.restype = C.c_uint64
+        L.ref_nw_run_pairs_capped.argtypes = [u8p, C.POINTER(C.c_uint64), u8p,
+                                              C.POINTER(C.c_uint64), C.c_uint64, C.c_uint64,
+                                              C.c_uint64, C.POINTER(C.c_uint64)]
+        L.ref_nw_run_pairs_capped.restype = C.c_uint64
+        L.ref_nw_run_pairs_mt_capped.argtypes = [u8p, C.POINTER(C.c_uint64), u8p,
+                                                 C.POINTER(C.c_uint64), C.c_uint64, C.c_uint64,
+                                                 C.c_uint64, C.c_int, C.POINTER(C.c_uint64)]
+        L.ref_nw_traceback_dfs_blocks.argtypes = [u8p, u8p, C.POINTER(_Mats), C.c_char_p,
+                                                  C.c_size_t, C.POINTER(C.c_size_t), C.c_uint64,
+                                                  C.c_uint64, C.POINTER(C.c_uint64)]
+        L.ref_nw_run_pairs_mt_capped.restype = C.c_uint64
         L.ref_nw_check_pairs_mt.argtypes = [u8p, C.POINTER(C.c_uint64), u8p,
                                             C.POINTER(C.c_uint64), C.c_uint64,
                                             C.POINTER(C.c_uint64), C.POINTER(C.c_int32), u8p, u8p,
@@ -101,7 +112,7 @@ class NwOracle:
     I: np.ndarray
     D: np.ndarray
     stdout: str | None       # literal DFS output (None when not requested)
-    dfs_rc: int | None       # 0 finished, 1 panic, 2 pop cap
+    dfs_rc: int | None       # 0 finished, 1 panic, 2 pop cap, 3 block cap (max_blocks)
     dfs_blocks: int | None
     n_blocks: int            # memoised DFS: blocks printed before the first panic
     panics: bool
@@ -109,7 +120,7 @@ class NwOracle:
 
 
 def nw(query: bytes, db: bytes, *, literal_dfs: bool = True, max_pops: int = 2_000_000,
-       out_cap: int = 1 << 22) -> NwOracle:
+       out_cap: int = 1 << 22, max_blocks: int = 0) -> NwOracle:
     L = lib()
     q, d = _u8(query), _u8(db)
     m = _Mats()
@@ -129,8 +140,8 @@ def nw(query: bytes, db: bytes, *, literal_dfs: bool = True, max_pops: int = 2_0
             out = C.create_string_buffer(out_cap)
             olen = C.c_size_t(0)
             nb = C.c_uint64(0)
-            rc = L.ref_nw_traceback_dfs(q, d, C.byref(m), out, out_cap, C.byref(olen), max_pops,
-                                        C.byref(nb))
+            rc = L.ref_nw_traceback_dfs_blocks(q, d, C.byref(m), out, out_cap, C.byref(olen),
+                                               max_pops, max_blocks, C.byref(nb))
             text = out.raw[:min(olen.value, out_cap)].decode("latin-1")
             blocks = nb.value
         nbk = C.c_uint64(0)
@@ -187,6 +198,25 @@ def run_pairs(qs: bytes, q_off: np.ndarray, ds: bytes, d_off: np.ndarray, n_pair
     do = np.ascontiguousarray(d_off, np.uint64)
     return L.ref_nw_run_pairs(_u8(qs), qo.ctypes.data_as(C.POINTER(C.c_uint64)), _u8(ds),
                               do.ctypes.data_as(C.POINTER(C.c_uint64)), n_pairs, max_pops)
+
+
+def run_pairs_capped(qs: bytes, q_off: np.ndarray, ds: bytes, d_off: np.ndarray, n_pairs: int,
+                     max_pops: int = 100_000, threads: int = 1,
+                     max_blocks: int = 0) -> tuple[int, int]:
+    """(cells, pairs whose DFS stopped at max_pops) of run_pairs / run_pairs_mt
+    (max_blocks > 0: each DFS also stops before its (max_blocks+1)-th block)."""
+    L = lib()
+    qo = np.ascontiguousarray(q_off, np.uint64)
+    do = np.ascontiguousarray(d_off, np.uint64)
+    nc = C.c_uint64(0)
+    P = lambda a: a.ctypes.data_as(C.POINTER(C.c_uint64))  # noqa: E731
+    if threads <= 1:
+        cells = L.ref_nw_run_pairs_capped(_u8(qs), P(qo), _u8(ds), P(do), n_pairs, max_pops,
+                                          max_blocks, C.byref(nc))
+    else:
+        cells = L.ref_nw_run_pairs_mt_capped(_u8(qs), P(qo), _u8(ds), P(do), n_pairs, max_pops,
+                                             max_blocks, threads, C.byref(nc))
+    return int(cells), int(nc.value)
 
 
 def run_pairs_mt(qs: bytes, q_off: np.ndarray, ds: bytes, d_off: np.ndarray, n_pairs: int,

@@ -10,14 +10,16 @@ interface: ``parse_fasta``/``Record``/``Mode`` (src/parse.rs), the
 from .records import (AlignerError, AlignmentError, Algo, CharError, FastaError, Mode, Record,
                       Records, parse_fasta, parse_fasta_bytes)
 from .nw import (NwAlignment, NwAllVsAll, NwPlan, alignment_rows, cigar_ops_string, dense_mask, n_w_align,
-                 nw_align_batch, nw_score_all_vs_all, pack_csr, render)
+                 nw_align_batch, nw_score_all_vs_all, pack_csr, render, render_batch)
 from . import wfa
 from .wfa import WfaAlignment, WfaPlan, wfa_align, wfa_align_batch
 from . import wfa_affine
+from ._lib import get_option, option_names, options, set_option
 
 __all__ = [
     "AlignerError", "AlignmentError", "Algo", "CharError", "FastaError", "Mode", "Record",
     "Records", "parse_fasta", "parse_fasta_bytes", "NwAlignment", "NwPlan", "alignment_rows",
-    "cigar_ops_string", "dense_mask", "n_w_align", "NwAllVsAll", "nw_score_all_vs_all", "nw_align_batch", "pack_csr", "render",
+    "cigar_ops_string", "dense_mask", "n_w_align", "NwAllVsAll", "nw_score_all_vs_all", "nw_align_batch", "pack_csr", "render", "render_batch",
     "wfa", "WfaAlignment", "WfaPlan", "wfa_align", "wfa_align_batch", "wfa_affine",
+    "get_option", "option_names", "options", "set_option",
 ]

@@ -24,6 +24,7 @@ REF_PANIC_TRIM = 3
 REF_PANIC_SLICE = 4
 NONCONVERGED = 5
 ENUM_CAP = 6
+SPAN_UNLINKED = 7
 E_INVALID = -1
 E_HIP = -2
 E_NO_DEVICE = -3
@@ -38,7 +39,7 @@ FLAG_SPEC_UNLINKED = 2  # SALN_FLAG_SPEC_UNLINKED
 STATUS_NAMES = {
     OK: "OK", NOT_IMPLEMENTED: "NOT_IMPLEMENTED", REF_PANIC_BOUNDARY: "REF_PANIC_BOUNDARY",
     REF_PANIC_TRIM: "REF_PANIC_TRIM", REF_PANIC_SLICE: "REF_PANIC_SLICE",
-    NONCONVERGED: "NONCONVERGED", ENUM_CAP: "ENUM_CAP", E_INVALID: "E_INVALID", E_HIP: "E_HIP",
+    NONCONVERGED: "NONCONVERGED", ENUM_CAP: "ENUM_CAP", SPAN_UNLINKED: "SPAN_UNLINKED", E_INVALID: "E_INVALID", E_HIP: "E_HIP",
     E_NO_DEVICE: "E_NO_DEVICE", E_CAPACITY: "E_CAPACITY", E_IO: "E_IO", E_FASTA: "E_FASTA",
     E_FASTA_CHARS: "E_FASTA_CHARS", E_DEVICE_WAIT: "E_DEVICE_WAIT",
 }
@@ -99,6 +100,9 @@ EXPORTS = [
     "saln_wfa_affine_plan_destroy",
     "saln_parse_fasta", "saln_parse_fasta_buffer", "saln_records_count", "saln_records_get",
     "saln_records_free",
+    "saln_option_set", "saln_option_get", "saln_option_name", "saln_options_reset",
+    "saln_nw_render_batch", "saln_nw_render_text", "saln_nw_text_count", "saln_nw_text_get",
+    "saln_nw_text_free",
 ]
 
 _lib = None
@@ -223,6 +227,20 @@ def lib() -> C.CDLL:
         L.saln_records_get.argtypes = [vp, C.c_uint64, C.POINTER(vp), u64p, C.POINTER(vp), u64p]
         L.saln_records_free.argtypes = [vp]
         L.saln_records_free.restype = None
+        L.saln_nw_render_batch.argtypes = [vp, vp, vp, C.c_uint64, vp, vp, C.c_uint64, vp, vp,
+                                           C.c_uint64, C.c_int32, C.c_uint64, C.c_int,
+                                           C.POINTER(vp)]
+        L.saln_nw_render_text.argtypes = [vp, vp, C.c_uint64, vp, C.c_uint64, C.c_int32,
+                                          C.c_uint64, C.POINTER(vp)]
+        L.saln_nw_text_count.argtypes = [vp]
+        L.saln_nw_text_count.restype = C.c_uint64
+        L.saln_nw_text_get.argtypes = [vp, C.c_uint64, C.POINTER(vp), u64p, u64p, i32p,
+                                       C.POINTER(NwResult), u64p]
+        L.saln_nw_text_free.argtypes = [vp]
+        L.saln_nw_text_free.restype = None
+        L.saln_option_set.argtypes = [C.c_char_p, C.c_int64]
+        L.saln_option_get.argtypes = [C.c_char_p, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]
+        L.saln_option_name.argtypes = [C.c_uint32, C.POINTER(C.c_char_p)]
         _lib = L
         return L
 
@@ -272,3 +290,58 @@ def scoring_arg(scoring) -> C.POINTER(NwScoring) | None:
         return C.pointer(scoring)
     m, x, o, e = scoring
     return C.pointer(NwScoring(m, x, o, e))
+
+
+# ------------------------------------------------------------------ options
+def set_option(name: str, value: int) -> None:
+    """saln_option_set: one of the engine's tuning knobs (include/saln.h)."""
+    check(lib().saln_option_set(name.encode(), int(value)), f"saln_option_set({name})")
+
+
+def get_option(name: str) -> tuple[int, int]:
+    """(current value, default) of an option."""
+    v, d = C.c_int64(), C.c_int64()
+    check(lib().saln_option_get(name.encode(), C.byref(v), C.byref(d)), f"saln_option_get({name})")
+    return v.value, d.value
+
+
+def option_names() -> list[str]:
+    out, i = [], 0
+    while True:
+        nm = C.c_char_p()
+        if lib().saln_option_name(i, C.byref(nm)) != OK:
+            return out
+        out.append(nm.value.decode())
+        i += 1
+
+
+def non_default_options() -> dict[str, int]:
+    """The options whose value differs from the default (bench.py records them)."""
+    out = {}
+    for nm in option_names():
+        v, d = get_option(nm)
+        if v != d:
+            out[nm] = v
+    return out
+
+
+class options:
+    """Context manager: set options for a block, restore the previous values.
+
+        with options(**{"nw.nib_codes": 0}): ...
+    """
+
+    def __init__(self, **kw):
+        self.kw = kw
+        self.prev = {}
+
+    def __enter__(self):
+        for k, v in self.kw.items():
+            self.prev[k] = get_option(k)[0]
+            set_option(k, v)
+        return self
+
+    def __exit__(self, *exc):
+        for k, v in self.prev.items():
+            set_option(k, v)
+        return False

@@ -3,6 +3,7 @@
 // thin wrapper: upload -> plan -> saln_nw_execute (GPU) -> download.
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -55,8 +56,8 @@ static int run_batch(saln_context *ctx, const uint8_t *q_seq, const uint64_t *q_
                      std::vector<PairMask> *masks_out) {
     StageClock clk;
     PlanGuard g;
-    int rc = saln_nw_plan_create(ctx, q_off, n_q, db_off, n_db, pair_q, pair_db, n_pairs, mode,
-                                 scoring, &g.p);
+    int rc = plan_create(ctx, q_off, n_q, db_off, n_db, pair_q, pair_db, n_pairs, mode, scoring,
+                         masks_out != nullptr, &g.p);
     if (rc == SALN_NOT_IMPLEMENTED) {
         for (uint64_t k = 0; k < n_pairs; ++k) {
             std::memset(&results[k], 0, sizeof(saln_nw_result));
@@ -65,7 +66,6 @@ static int run_batch(saln_context *ctx, const uint8_t *q_seq, const uint64_t *q_
         return rc;
     }
     if (rc != SALN_OK) return rc;
-    if (masks_out) plan_set_full_codes(g.p, true);
     clk.mark("plan");
     std::vector<uint64_t> coff(n_pairs + 1);
     saln_nw_cigar_offsets(g.p, coff.data());
@@ -92,6 +92,8 @@ static int run_batch(saln_context *ctx, const uint8_t *q_seq, const uint64_t *q_
     for (uint64_t k = 0; k < n_pairs; ++k) doff[k + 1] = doff[k] + results[k].cigar_len;
     const uint32_t *hc = nullptr;
     DevBuf dso(ctx), ddo(ctx), dcd(ctx);
+    // the context's pinned staging: held until the scatter below has read it
+    std::unique_lock<std::mutex> stage_lk(ctx->staging_mu, std::defer_lock);
     if (cigar && doff[n_pairs]) {
         TRY_HIP(dso.alloc((n_pairs + 1) * 8));
         TRY_HIP(ddo.alloc((n_pairs + 1) * 8));
@@ -102,6 +104,7 @@ static int run_batch(saln_context *ctx, const uint8_t *q_seq, const uint64_t *q_
                                      (const uint64_t *)ddo.p, (const uint32_t *)dc.p,
                                      (uint32_t *)dcd.p, n_pairs, ctx->stream));
         void *st = nullptr;
+        stage_lk.lock();
         TRY_HIP(pinned_staging(ctx, doff[n_pairs] * 4, &st));
         TRY_HIP(hipMemcpyAsync(st, dcd.p, doff[n_pairs] * 4, hipMemcpyDeviceToHost, ctx->stream));
         TRY_HIP(hipStreamSynchronize(ctx->stream));
@@ -141,7 +144,151 @@ static int run_batch(saln_context *ctx, const uint8_t *q_seq, const uint64_t *q_
     return SALN_OK;
 }
 
+// Rendered reference text of a batch (saln_nw_render_batch).
+struct saln_nw_text {
+    std::vector<std::string> text;
+    std::vector<uint64_t> blocks, ns;
+    std::vector<int32_t> status;
+    std::vector<saln_nw_result> res;
+    uint64_t count = 0;  // pairs rendered
+};
+
 extern "C" {
+
+// The pair loop main.rs:61-74 with the text n_w_align prints
+// (needleman_wunsch_affine.rs:281-286, :390-411) for every pair, computed
+// once: one full-code plan for the batch (fill + first walk on the GPU), one
+// download of the part of the mask the rendered pairs need, then the
+// reference DFS per pair on host threads.
+int saln_nw_render_batch(saln_context *ctx, const uint8_t *q_seq, const uint64_t *q_off,
+                         uint64_t n_q, const uint8_t *db_seq, const uint64_t *db_off,
+                         uint64_t n_db, const uint32_t *pair_q, const uint32_t *pair_db,
+                         uint64_t n_pairs, int32_t mode, uint64_t max_blocks, int stop_at_panic,
+                         saln_nw_text **out) {
+    if (!ctx || !q_off || !db_off || !out) return SALN_E_INVALID;
+    *out = nullptr;
+    const auto t0 = std::chrono::steady_clock::now();
+    auto *t = new saln_nw_text;
+    t->text.resize(n_pairs);
+    t->blocks.assign(n_pairs, 0);
+    t->ns.assign(n_pairs, 0);
+    t->status.assign(n_pairs, SALN_OK);
+    t->res.resize(n_pairs);
+    if (mode != SALN_MODE_GLOBAL) {  // needleman_wunsch_affine.rs:433-434: every pair errs
+        for (uint64_t k = 0; k < n_pairs; ++k) {
+            std::memset(&t->res[k], 0, sizeof(saln_nw_result));
+            t->res[k].status = t->status[k] = SALN_NOT_IMPLEMENTED;
+        }
+        t->count = n_pairs;
+        *out = t;
+        return SALN_OK;
+    }
+    PlanGuard g;
+    int rc = plan_create(ctx, q_off, n_q, db_off, n_db, pair_q, pair_db, n_pairs, mode, nullptr,
+                         true, &g.p);
+    if (rc != SALN_OK) {
+        delete t;
+        return rc;
+    }
+    std::vector<uint8_t> host;
+    {
+        DevBuf dq(ctx), dd(ctx), dr(ctx);
+        const uint64_t qbytes = q_off[n_q], dbytes = db_off[n_db];
+        auto fail = [&](hipError_t e, const char *what) {
+            set_error(std::string(what) + ": " + hipGetErrorString(e));
+            delete t;
+            return SALN_E_HIP;
+        };
+        hipError_t e;
+        if ((e = dq.alloc(qbytes)) != hipSuccess || (e = dd.alloc(dbytes)) != hipSuccess ||
+            (e = dr.alloc(n_pairs * sizeof(saln_nw_result))) != hipSuccess)
+            return fail(e, "render batch: device buffers");
+        if ((qbytes && (e = hipMemcpy(dq.p, q_seq, qbytes, hipMemcpyHostToDevice)) != hipSuccess) ||
+            (dbytes && (e = hipMemcpy(dd.p, db_seq, dbytes, hipMemcpyHostToDevice)) != hipSuccess))
+            return fail(e, "render batch: upload");
+        rc = saln_nw_execute(g.p, (const uint8_t *)dq.p, (const uint8_t *)dd.p,
+                             (saln_nw_result *)dr.p, nullptr, nullptr);
+        if (rc == SALN_OK && (e = hipDeviceSynchronize()) != hipSuccess) return fail(e, "execute");
+        if (rc == SALN_OK) rc = plan_check_error(g.p);
+        if (rc != SALN_OK) {
+            delete t;
+            return rc;
+        }
+        if (n_pairs && (e = hipMemcpy(t->res.data(), dr.p, n_pairs * sizeof(saln_nw_result),
+                                      hipMemcpyDeviceToHost)) != hipSuccess)
+            return fail(e, "render batch: results");
+    }
+    // with stop_at_panic, pairs after the first panicking one are never
+    // rendered: the reference aborts there (exit 101)
+    uint64_t n = n_pairs;
+    if (stop_at_panic)
+        for (uint64_t k = 0; k < n_pairs; ++k)
+            if (t->res[k].status == SALN_REF_PANIC_BOUNDARY) {
+                n = k + 1;
+                break;
+            }
+    if ((rc = plan_download_masks(g.p, n, &host)) != SALN_OK) {
+        delete t;
+        return rc;
+    }
+    const double dev_ns =
+        (double)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0)
+            .count();
+    // per-pair DFS on host threads (its cost varies by orders of magnitude
+    // with the number of co-optimal paths: pairs are handed out one by one)
+    std::atomic<uint64_t> next{0};
+    auto work = [&]() {
+        for (;;) {
+            const uint64_t k = next.fetch_add(1);
+            if (k >= n) return;
+            const auto a = std::chrono::steady_clock::now();
+            const uint64_t qi = pair_q ? pair_q[k] : k % n_q, di = pair_db ? pair_db[k] : k / n_q;
+            const HostMask hm = plan_host_mask(g.p, host.data(), k);
+            const DfsOutcome o = render_blocks(hm, q_seq + q_off[qi], db_seq + db_off[di],
+                                               max_blocks, &t->text[k]);
+            t->blocks[k] = o.blocks;
+            t->status[k] = o.status;
+            t->ns[k] = (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+                           std::chrono::steady_clock::now() - a).count();
+        }
+    };
+    const uint64_t nt = std::min<uint64_t>(std::max(1u, std::min(16u, std::thread::hardware_concurrency())),
+                                           n / 64 + 1);
+    std::vector<std::thread> th;
+    for (uint64_t i = 1; i < nt; ++i) th.emplace_back(work);
+    work();
+    for (auto &x : th) x.join();
+    // each pair's share of the batch's device work, added to its own DFS time
+    for (uint64_t k = 0; k < n; ++k) t->ns[k] += (uint64_t)(dev_ns / (double)std::max<uint64_t>(1, n_pairs));
+    t->count = n;
+    *out = t;
+    return SALN_OK;
+}
+
+int saln_nw_render_text(saln_context *ctx, const uint8_t *q, uint64_t len_q, const uint8_t *d,
+                        uint64_t len_db, int32_t mode, uint64_t max_blocks, saln_nw_text **out) {
+    if (!ctx || (len_q && !q) || (len_db && !d) || !out) return SALN_E_INVALID;
+    const uint64_t qo[2] = {0, len_q}, dof[2] = {0, len_db};
+    const uint32_t z = 0;
+    return saln_nw_render_batch(ctx, q, qo, 1, d, dof, 1, &z, &z, 1, mode, max_blocks, 0, out);
+}
+
+uint64_t saln_nw_text_count(const saln_nw_text *t) { return t ? t->count : 0; }
+
+int saln_nw_text_get(const saln_nw_text *t, uint64_t pair, const char **text, uint64_t *len,
+                     uint64_t *n_blocks, int32_t *status, saln_nw_result *result,
+                     uint64_t *elapsed_ns) {
+    if (!t || pair >= t->count) return SALN_E_INVALID;
+    if (text) *text = t->text[pair].data();
+    if (len) *len = t->text[pair].size();
+    if (n_blocks) *n_blocks = t->blocks[pair];
+    if (status) *status = t->status[pair];
+    if (result) *result = t->res[pair];
+    if (elapsed_ns) *elapsed_ns = t->ns[pair];
+    return SALN_OK;
+}
+
+void saln_nw_text_free(saln_nw_text *t) { delete t; }
 
 int saln_nw_align_batch(saln_context *ctx, const uint8_t *q_seq, const uint64_t *q_off,
                         uint64_t n_q, const uint8_t *db_seq, const uint64_t *db_off,

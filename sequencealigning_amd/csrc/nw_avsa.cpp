@@ -99,11 +99,8 @@ int saln_nw_avsa_create(saln_context *ctx, const uint64_t *q_off, uint64_t n_q,
     std::vector<uint32_t> fbq;
     // 8 x 19 groups for queries of <= 152 columns: the per-step overhead over
     // 19 columns and 7 steps of skew instead of 10 and 15 (C5 slice 6,738 ->
-    // 7,858 GCUPS); SALN_AVSA_V4=0 keeps the 16 x 10 geometry
-    const bool avsa_narrow = [] {
-        const char *e = std::getenv("SALN_AVSA_V4");
-        return !e || std::atoi(e) != 0;
-    }();
+    // 7,858 GCUPS); option nw.avsa_narrow = 0 keeps the 16 x 10 geometry
+    const bool avsa_narrow = opt(Opt::AvsaNarrow) != 0;
     for (uint64_t q = 0; q < n_q; ++q) {
         const uint64_t lq = q_off[q + 1] - q_off[q];
         if (lq > 0x7FFFFFFFull) {

@@ -135,6 +135,13 @@ struct Geom {
     uint32_t G, K;
     SALN_HD uint32_t KD() const { return (K + 3) / 4; }
     SALN_HD uint32_t LB() const { return KD() * 4; }
+    // 4-bit walk codes (nw_fill_pk_kernel kCodesNib): ceil(K/4) 16-bit
+    // column-group halves per pair, two per dword, plus the row's db char
+    SALN_HD uint32_t LBn() const { return 4 * ((K + 3) / 4 / 2 + 1); }
+    SALN_HD uint32_t nib_char_byte() const {
+        const uint32_t ng = (K + 3) / 4;
+        return ng % 2 ? 4 * (ng / 2) + 2 : 4 * (ng / 2);
+    }
     SALN_HD uint32_t W() const { return G * K; }
     SALN_HD uint32_t n_chunks(uint32_t len_q) const { return (len_q + W() - 1) / W(); }
     SALN_HD uint32_t n_blocks(uint32_t len_q) const { return n_chunks(len_q) * G; }

@@ -68,7 +68,8 @@ struct saln_nw_plan {
     int stripe_rows = 0;     // else: row fill with this many columns per lane (0 = skewed fill)
     uint32_t stripe_sub = kStripeSubMax;  // boundary columns per 256-column chunk
     int stripe_layout() const { return stripe_pk ? 1 : stripe_rows ? 2 : 0; }
-    bool full_codes = false;  // walk codes (default) or every parent set
+    bool full_codes = false;  // walk codes (default) or every parent set (decided at creation)
+    bool nib[kNumVariants] = {};  // variant stores 4-bit walk codes (Geom::LBn segments)
     bool score_only = false;  // no parent codes / traceback (saln_nw_plan_set_score_only)
     int buf = 0;                           // workspace of the next execute (async mode)
     bool tb_pending[2] = {false, false};
@@ -180,6 +181,19 @@ int saln_nw_plan_create(saln_context *ctx, const uint64_t *q_off, uint64_t n_q,
                         const uint64_t *db_off, uint64_t n_db, const uint32_t *pair_q,
                         const uint32_t *pair_db, uint64_t n_pairs, int32_t mode,
                         const saln_nw_scoring *scoring, saln_nw_plan **out) {
+    return saln::plan_create(ctx, q_off, n_q, db_off, n_db, pair_q, pair_db, n_pairs, mode,
+                             scoring, false, out);
+}
+
+}  // extern "C"
+
+// Plan creation.  full_codes: the fills store every parent set (host DFS,
+// dense mask) instead of walk codes; it fixes the mask layout (4-bit walk
+// codes for the short-query packed variants, bytes otherwise).
+int saln::plan_create(saln_context *ctx, const uint64_t *q_off, uint64_t n_q,
+                      const uint64_t *db_off, uint64_t n_db, const uint32_t *pair_q,
+                      const uint32_t *pair_db, uint64_t n_pairs, int32_t mode,
+                      const saln_nw_scoring *scoring, bool full_codes, saln_nw_plan **out) {
     if (!ctx || !q_off || !db_off || !out) return SALN_E_INVALID;
     *out = nullptr;
     if (mode != SALN_MODE_GLOBAL) {
@@ -197,6 +211,13 @@ int saln_nw_plan_create(saln_context *ctx, const uint64_t *q_off, uint64_t n_q,
     auto *p = new saln_nw_plan;
     p->ctx = ctx;
     p->sc = scoring_or_default(scoring);
+    p->full_codes = full_codes;
+    // 4-bit walk codes (option nw.nib_codes): variant 7 may keep bytes, the
+    // 8 x 19 variant (option nw.narrow_walk, queries of <= 152 columns) has
+    // only 4-bit codes; full-code plans keep byte codes and the 16 x 10 groups
+    const bool nib_on = !full_codes && opt(Opt::NibCodes) != 0;
+    const bool narrow = nib_on && opt(Opt::NarrowWalk) != 0;
+    for (int v = 0; v < kNumVariants; ++v) p->nib[v] = nib_on && variant_nib(v);
     p->n_pairs = n_pairs;
     p->cigar_off.resize(n_pairs + 1);
     std::vector<NwPairDesc> descs(n_pairs);
@@ -228,7 +249,7 @@ int saln_nw_plan_create(saln_context *ctx, const uint64_t *q_off, uint64_t n_q,
             memo_lq = lq;
             memo_ld = ld;
             memo_fit = scores_fit_i32(p->sc, lq, ld);
-            memo_var = memo_fit ? choose_variant((uint32_t)lq, (uint32_t)ld, p->sc) : 0;
+            memo_var = memo_fit ? choose_variant((uint32_t)lq, (uint32_t)ld, p->sc, narrow) : 0;
         }
         if (!memo_fit) {
             delete p;
@@ -252,10 +273,7 @@ int saln_nw_plan_create(saln_context *ctx, const uint64_t *q_off, uint64_t n_q,
         // throughput choice (two pairs per wave), the column stripes the
         // latency choice (four waves per pair, pipelined): a plan with few
         // such pairs keeps them on stripes.
-        static const uint64_t v8_min = [] {
-            const char *e = std::getenv("SALN_V8_MIN_PAIRS");  // experiment switch
-            return e ? (uint64_t)std::atoll(e) : (uint64_t)kWidePackedMinPairs;
-        }();
+        const uint64_t v8_min = (uint64_t)opt(Opt::WideMinPairs);
         uint64_t wide = 0;
         for (const NwPairDesc &d : descs)
             wide += d.variant == (uint32_t)kWidePackedVariant && d.len_q > 512;
@@ -353,16 +371,9 @@ int saln_nw_plan_create(saln_context *ctx, const uint64_t *q_off, uint64_t n_q,
     // them to the pack's longest db / widest query would cost over 25 % more
     // than storing them apart.
     uint64_t moff = 0;
-    // SALN_PK_SKEW=1 (experiment): packed fills write skewed per-wave regions.
-    // C2 fill 0.97 -> 0.92 ms, but the walker's pack loses its adjacent
-    // segments (0.25 -> 0.31 ms): no net gain, the interleaved rows stay
-    const bool pk_skew = [] {
-        const char *e = std::getenv("SALN_PK_SKEW");
-        return e && std::atoi(e) != 0;
-    }();
     for (int v = 0; v < kNumVariants; ++v) {
         const Geom g = variant_geom(v);
-        const uint64_t lb = g.LB();
+        const uint64_t lb = p->nib[v] ? g.LBn() : g.LB();
         for (uint32_t a = p->var_first[v], e = a + p->var_count[v]; a < e; a += 64) {
             const uint32_t np = std::min<uint32_t>(64, e - a);
             uint64_t rows = 0, nbm = 0, own = 0;
@@ -385,31 +396,6 @@ int saln_nw_plan_create(saln_context *ctx, const uint64_t *q_off, uint64_t n_q,
                     d.mask_bs = pk ? 0u : (uint32_t)lb;
                     d.mask_cs = ((uint64_t)d.len_db + (pk ? 2 * g.G : g.G) - 1) * g.W();
                     moff += g.n_chunks(d.len_q) * d.mask_cs;
-                }
-            } else if (pk_skew && variant_packed(v) && v != 4) {
-                // packed fills: one region per fill wave (its 128 / G lane
-                // groups' 2 pairs each), skewed like the stripes: line t holds
-                // the segments every lane of the wave stores at step t (lane l
-                // at row t - l + 1, block l), [block][pair slot], so a store
-                // instruction writes one contiguous line instead of 64
-                // scattered segments.  Segment (i, b) of slot s is at
-                // (i - 1 + b) * rs + b * P * LB + s * LB: rs = line, bs = rs + P * LB.
-                const uint32_t P = 128 / g.G;  // pairs per fill wave
-                const uint64_t line = (uint64_t)g.G * P * lb;
-                for (uint32_t w0 = 0; w0 < np; w0 += P) {
-                    const uint32_t nw = std::min<uint32_t>(P, np - w0);
-                    uint64_t ldw = 0;
-                    for (uint32_t s = 0; s < nw; ++s)
-                        ldw = std::max<uint64_t>(ldw, p->h_pairs[a + w0 + s].len_db);
-                    const uint64_t lines = ldw + g.G - 1;
-                    for (uint32_t s = 0; s < nw; ++s) {
-                        NwPairDesc &d = p->h_pairs[a + w0 + s];
-                        d.mask_off = moff + s * lb;
-                        d.mask_rs = line;
-                        d.mask_bs = (uint32_t)(line + P * lb);
-                        d.mask_cs = lines * line;
-                    }
-                    moff += (lines * line + 255) & ~255ull;
                 }
             } else if (4 * packed <= 5 * own + 4096) {
                 for (uint32_t s = 0; s < np; ++s) {
@@ -436,8 +422,7 @@ int saln_nw_plan_create(saln_context *ctx, const uint64_t *q_off, uint64_t n_q,
         // sub-batches for fill/traceback overlap inside one execute
         // (SALN_TB_CHUNKS, default 1); boundaries kept even so packed groups
         // stay paired
-        uint32_t nsub = 1;
-        if (const char *e = std::getenv("SALN_TB_CHUNKS")) nsub = std::max(1, std::atoi(e));
+        const uint32_t nsub = (uint32_t)opt(Opt::TbChunks);
         const uint32_t step = ((p->n_fill + nsub - 1) / nsub + 1) & ~1u;
         p->sub.push_back(0);
         for (uint32_t b = step; b < p->n_fill; b += step) p->sub.push_back(b);
@@ -514,14 +499,12 @@ int saln_nw_plan_create(saln_context *ctx, const uint64_t *q_off, uint64_t n_q,
         // Speculative stripe walks: a few long column-stripe pairs walk all
         // their 256-column stripes at once (nw_traceback_coop_kernel kSpec)
         // instead of one stripe after another (C4: walk 3.8 ms).  Off with
-        // SALN_SPEC=0; SALN_SPEC_PASSES walk passes (default 3).
-        const char *env = std::getenv("SALN_SPEC");
-        const char *pe = std::getenv("SALN_SPEC_PASSES");
-        const int passes = pe ? std::atoi(pe) : 3;
+        // option nw.spec = 0; nw.spec_passes walk passes (default 3).
+        const int passes = (int)opt(Opt::SpecPasses);
         const uint32_t nv = p->var_count[kStripeVariant];
         std::vector<SpecPair> sp;
         std::vector<uint2> blocks;
-        if ((!env || std::atoi(env) != 0) && passes > 0 && nv && nv <= kSpecMaxPairs &&
+        if (opt(Opt::Spec) != 0 && passes > 0 && nv && nv <= kSpecMaxPairs &&
             p->sub.size() == 2) {
             for (uint32_t r = p->var_first[kStripeVariant]; r < p->var_first[kStripeVariant] + nv; ++r) {
                 const NwPairDesc &d = p->h_pairs[r];
@@ -535,8 +518,7 @@ int saln_nw_plan_create(saln_context *ctx, const uint64_t *q_off, uint64_t n_q,
             p->spec_pairs = (uint32_t)sp.size();
             p->spec_blocks = (uint32_t)blocks.size();
             p->spec_passes = passes;
-            const char *st = std::getenv("SALN_SPEC_STRICT");
-            p->spec_strict = st && std::atoi(st) != 0;
+            p->spec_strict = opt(Opt::SpecStrict) != 0;
             if ((e = dev_alloc(p->ctx, (void **)&p->d_spec_blocks, blocks.size() * sizeof(uint2))) != hipSuccess ||
                 (e = hipMemcpy(p->d_spec_blocks, blocks.data(), blocks.size() * sizeof(uint2),
                                hipMemcpyHostToDevice)) != hipSuccess ||
@@ -554,6 +536,8 @@ int saln_nw_plan_create(saln_context *ctx, const uint64_t *q_off, uint64_t n_q,
     *out = p;
     return SALN_OK;
 }
+
+extern "C" {
 
 int saln_nw_plan_info(const saln_nw_plan *p, uint64_t *mask_bytes, uint64_t *cigar_words,
                       uint64_t *cells) {
@@ -654,8 +638,8 @@ int saln_nw_execute(saln_nw_plan *p, const uint8_t *d_q, const uint8_t *d_db,
             } else if (a < b)
                 HIP_TRY(launch_fill(v, p->d_pairs, a, b - a, d_q, d_db, mask, p->d_scratch, endh,
                                     d_results, d_cigar, p->sc,
-                                    p->score_only ? 2 : p->full_codes ? 1 : 0, p->var_maxld[v],
-                                    s));
+                                    p->score_only ? 2 : p->full_codes ? 1 : p->nib[v] ? 3 : 0,
+                                    p->var_maxld[v], s));
         }
         if (ev && k + 1 == nsub) HIP_TRY(hipEventRecord(ev[1], s));
         HIP_TRY(hipEventRecord(p->sync_ev[k], s));
@@ -678,7 +662,7 @@ int saln_nw_execute(saln_nw_plan *p, const uint8_t *d_q, const uint8_t *d_db,
             else if (a < b)
                 HIP_TRY(launch_traceback(v, p->d_pairs, a, b - a, d_q, d_db, mask, endh, p->d_ops,
                                          d_results, d_cigar, p->sc, p->stripe_layout(), t,
-                                         spec ? p->d_spec_done : nullptr));
+                                         spec ? p->d_spec_done : nullptr, p->nib[v]));
         }
     }
     // pairs with an empty side (boundary-only walk) ride on the traceback stream
@@ -794,12 +778,6 @@ int saln_nw_plan::resolve_events() {
 // ----------------------------------------------------------- host traceback
 namespace saln {
 
-int plan_set_full_codes(saln_nw_plan *p, bool full) {
-    if (!p) return SALN_E_INVALID;
-    p->full_codes = full;
-    return SALN_OK;
-}
-
 int plan_pair_mask(const saln_nw_plan *p, uint64_t pair_id, PairMask *pm) {
     if (!p || pair_id >= p->n_pairs) return SALN_E_INVALID;
     const NwPairDesc &d = p->h_pairs[p->plan_index[pair_id]];
@@ -822,17 +800,6 @@ int plan_pair_mask(const saln_nw_plan *p, uint64_t pair_id, PairMask *pm) {
         return SALN_OK;
     }
     const uint64_t lb = pm->g.LB();
-    if (d.mask_bs > d.mask_rs) {  // skewed packed regions: block b's rows are rs-pitched
-        const uint64_t nb = pm->g.n_blocks(d.len_q);
-        pm->rs = nb * lb;
-        pm->cs = (uint64_t)pm->g.G * lb;
-        pm->m.assign((uint64_t)d.len_db * nb * lb, 0);
-        HIP_TRY(hipSetDevice(p->ctx->device));
-        for (uint64_t b = 0; b < nb; ++b)
-            HIP_TRY(hipMemcpy2D(pm->m.data() + b * lb, nb * lb, p->d_mask + d.mask_off + b * d.mask_bs,
-                                d.mask_rs, lb, d.len_db, hipMemcpyDeviceToHost));
-        return SALN_OK;
-    }
     // every row holds rs / bs blocks (the pack's width); copy them all as
     // LB-byte rows of one bs-pitched 2-D region
     const uint64_t nb = d.mask_rs / d.mask_bs;
@@ -843,6 +810,44 @@ int plan_pair_mask(const saln_nw_plan *p, uint64_t pair_id, PairMask *pm) {
     HIP_TRY(hipMemcpy2D(pm->m.data(), lb, p->d_mask + d.mask_off, d.mask_bs, lb,
                         (uint64_t)d.len_db * nb, hipMemcpyDeviceToHost));
     return SALN_OK;
+}
+
+int plan_download_masks(const saln_nw_plan *p, uint64_t n_first, std::vector<uint8_t> *host) {
+    if (!p || n_first > p->n_pairs) return SALN_E_INVALID;
+    if (!p->full_codes) {
+        set_error("plan_download_masks: plan stores walk codes only");
+        return SALN_E_INVALID;
+    }
+    // the workspace prefix that holds pairs 0 .. n_first-1 (results order):
+    // up to the last byte of each pair's end cell (the largest offset of its
+    // cells in every layout, nw_common.hpp Geom::cell)
+    uint64_t end = 0;
+    for (uint64_t k = 0; k < n_first; ++k) {
+        const NwPairDesc &d = p->h_pairs[p->plan_index[k]];
+        if (d.len_q == 0 || d.len_db == 0) continue;
+        const Geom g = variant_geom((int)d.variant);
+        end = std::max<uint64_t>(end, d.mask_off + g.cell(d.len_db, d.len_q, d.mask_rs, d.mask_bs,
+                                                          d.mask_cs) + 1);
+    }
+    host->resize(end);
+    if (!end) return SALN_OK;
+    HIP_TRY(hipSetDevice(p->ctx->device));
+    HIP_TRY(hipMemcpy(host->data(), p->d_mask, end, hipMemcpyDeviceToHost));
+    return SALN_OK;
+}
+
+HostMask plan_host_mask(const saln_nw_plan *p, const uint8_t *host, uint64_t pair_id) {
+    const NwPairDesc &d = p->h_pairs[p->plan_index[pair_id]];
+    HostMask hm;
+    hm.m = host + d.mask_off;
+    hm.g = variant_geom((int)d.variant);
+    hm.rs = d.mask_rs;
+    hm.bs = d.mask_bs;
+    hm.cs = d.mask_cs;
+    hm.lq = d.len_q;
+    hm.ld = d.len_db;
+    hm.sc = p->sc;
+    return hm;
 }
 
 void HostMask::to_dense(uint8_t *out) const {

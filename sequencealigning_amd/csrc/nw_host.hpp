@@ -13,6 +13,7 @@
 #include <vector>
 
 #include "nw_common.hpp"
+#include "saln_options.hpp"
 #include "saln.h"
 
 struct saln_context {
@@ -26,7 +27,10 @@ struct saln_context {
     std::multimap<size_t, void *> cache;
     std::unordered_map<void *, size_t> live;
     size_t cached = 0;
-    // pinned host staging for the host-path downloads (grow-only)
+    // pinned host staging for the host-path downloads (grow-only); staging_mu
+    // is held by a user of the buffer from its first copy to its last host
+    // read (pinned_staging may free and reallocate it when it grows)
+    std::mutex staging_mu;
     void *pinned = nullptr;
     size_t pinned_bytes = 0;
 };
@@ -43,12 +47,9 @@ inline hipStream_t resolve_stream(void *stream, const saln_context *ctx) {
 
 namespace saln {
 
-// SALN_HOST_TIMING=1: stage times of the host-side paths on stderr
+// option host.timing = 1: stage times of the host-side paths on stderr
 struct StageClock {
-    bool on = [] {
-        const char *e = std::getenv("SALN_HOST_TIMING");
-        return e && e[0] == '1';
-    }();
+    bool on = opt(Opt::HostTiming) != 0;
     std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
     void mark(const char *what) {
         if (!on) return;
@@ -67,13 +68,13 @@ constexpr size_t kDevCacheMax = size_t(32) << 30;
 hipError_t dev_alloc(saln_context *ctx, void **p, size_t n);
 void dev_free(saln_context *ctx, void *p);
 void dev_cache_clear(saln_context *ctx);
-hipError_t pinned_staging(saln_context *ctx, size_t n, void **p);
+hipError_t pinned_staging(saln_context *ctx, size_t n, void **p);  // caller holds ctx->staging_mu
 
 // kernels (nw_kernels.hip)
 hipError_t launch_fill(int variant, const NwPairDesc *pairs, uint32_t first, uint32_t count,
                        const uint8_t *qs, const uint8_t *ds, uint8_t *mask, int2 *scratch,
                        int32_t *end_h, saln_nw_result *results, uint32_t *cigar, Scoring sc,
-                       int codes /* 0 walk, 1 full, 2 none */, uint32_t ld_max,
+                       int codes /* 0 walk, 1 full, 2 none, 3 4-bit walk */, uint32_t ld_max,
                        hipStream_t stream);
 hipError_t launch_fill_stripes(const NwPairDesc *pairs, const uint2 *work, uint32_t n_work,
                                const uint8_t *qs, const uint8_t *ds, uint8_t *mask,
@@ -104,7 +105,11 @@ hipError_t launch_traceback(int variant, const NwPairDesc *pairs, uint32_t first
                             const uint8_t *ds, const uint8_t *mask, const int32_t *end_h,
                             uint32_t *ops, saln_nw_result *results, uint32_t *cigar, Scoring sc,
                             int stripe_layout, hipStream_t stream,
-                            const uint32_t *spec_done = nullptr);
+                            const uint32_t *spec_done = nullptr, bool nib = false);
+// variants whose walk codes may be 4-bit (kCodesNib): the short-query packed
+// fills 7 (16 x 10) and 4 (8 x 19, 4-bit only)
+inline bool variant_nib(int v) { return v == 7 || v == 4; }
+constexpr int kNarrowVariant = 4;  // 8 x 19 groups, queries of <= 152 columns
 // speculative stripe walks of the plan's long column-stripe pairs: `passes`
 // walk passes, the link (accept or leave to the cooperative walker, `done`)
 // and the CIGAR copy; strict_err (SALN_SPEC_STRICT=1, tests): bit 1 set when a
@@ -146,7 +151,7 @@ hipError_t launch_avsa_scatter(const saln_nw_result *res, const uint32_t *q_ids,
                                hipStream_t stream);
 Geom variant_geom(int v);
 bool variant_packed(int v);
-int choose_variant(uint32_t len_q, uint32_t len_db, const Scoring &sc);
+int choose_variant(uint32_t len_q, uint32_t len_db, const Scoring &sc, bool narrow = false);
 
 void set_error(const std::string &msg);
 Scoring scoring_or_default(const saln_nw_scoring *s);
@@ -203,13 +208,22 @@ struct HostMask {
 // fill hit its dependency-wait bound since the last check.
 int plan_check_error(saln_nw_plan *plan);
 
-// Full parent codes (every parent set, needed by the host DFS and the dense
-// export) instead of the walk codes a plan stores by default.
-int plan_set_full_codes(saln_nw_plan *plan, bool full);
+// saln_nw_plan_create with the code format fixed at creation: full_codes =
+// every parent set (needed by the host DFS and the dense export) instead of
+// the walk codes a plan stores by default.
+int plan_create(saln_context *ctx, const uint64_t *q_off, uint64_t n_q, const uint64_t *db_off,
+                uint64_t n_db, const uint32_t *pair_q, const uint32_t *pair_db, uint64_t n_pairs,
+                int32_t mode, const saln_nw_scoring *scoring, bool full_codes, saln_nw_plan **out);
 
 // Copies one pair's parent codes from a plan's workspace after execute
 // (compact: bs = LB); pair_id is the results index.
 int plan_pair_mask(const saln_nw_plan *plan, uint64_t pair_id, PairMask *mask);
+
+// Host copy of the part of a full-code plan's mask workspace that holds
+// pairs 0 .. n_first-1 (results order) after an execute, and a pair's view
+// on it (render batches: one download instead of a copy per pair).
+int plan_download_masks(const saln_nw_plan *plan, uint64_t n_first, std::vector<uint8_t> *host);
+HostMask plan_host_mask(const saln_nw_plan *plan, const uint8_t *host, uint64_t pair_id);
 
 // Reference DFS (needleman_wunsch_affine.rs:246-329) over the parent codes.
 struct DfsOutcome {

@@ -24,6 +24,7 @@
 #include <utility>
 
 #include "nw_common.hpp"
+#include "saln_options.hpp"
 #include "saln.h"
 
 namespace saln {
@@ -249,18 +250,24 @@ constexpr uint32_t kOpsPerWord = 10;                     // 3-bit ops per op-str
 #ifndef SALN_WALK_NW
 #define SALN_WALK_NW 0
 #endif
-template <int K>
+// kNib: 4-bit walk codes (Geom::LBn-byte segments) and the pair's query
+// staged in LDS after the windows: QC 16-byte chunks per lane, [chunk][lane]
+// (the LDS-DMA order), enough for a variant of `cols` query columns at any
+// 16-byte misalignment.
+template <int K, bool kNib = false, uint32_t kCols = 0>
 struct WalkGeo {
-    static constexpr uint32_t LB = (K + 3) / 4 * 4;
+    static constexpr uint32_t LB = kNib ? 4 * ((K + 3) / 4 / 2 + 1) : (K + 3) / 4 * 4;
     static constexpr uint32_t NW = SALN_WALK_NW ? SALN_WALK_NW : 2;
-    static constexpr uint32_t W = SALN_WALK_W ? SALN_WALK_W : (K < 16 ? 4 : 8);
+    static constexpr uint32_t W = SALN_WALK_W ? SALN_WALK_W : (K < 16 || kNib ? 4 : 8);
     static constexpr uint32_t SB = LB == 12 ? 12 : 16;        // DMA bytes per lane
     static constexpr uint32_t kSlotBytes = 64 * 16;          // one slot of a wave
     static constexpr uint32_t kWinBytes = W * kSlotBytes;    // one window of a wave
-    static constexpr uint32_t kWaveLds = NW * kWinBytes;
+    static constexpr uint32_t QC = kNib ? (15 + kCols + 15) / 16 : 0;
+    static constexpr uint32_t kWaveLds = NW * kWinBytes + QC * kSlotBytes;
     static constexpr uint32_t kVmcnt = NW * (W - 1);
     static_assert(LB <= 16, "LDS window slots hold 16 bytes per lane");
     static_assert((NW == 2 || NW == 3) && W >= 2 && W <= 8, "8 valid bits per window");
+    static_assert(!kNib || kCols > 0, "4-bit walk: the variant's query width");
 };
 
 typedef __attribute__((address_space(3))) uint8_t lds_u8;
@@ -325,11 +332,23 @@ __device__ __forceinline__ void unroll_each(F &&f, std::integer_sequence<uint32_
 //   the phase (one subtract per phase) and the block offsets held by window
 //   0 / 1 (a crossing recomputes only the one it hands to block B-2);
 // - the op stream is a 64-bit accumulator (stored 30 bits = ten ops at a time).
-template <int G, int K>
+// kNib (round 4): 4-bit codes (nw_fill_pk_kernel kCodesNib).  The nibble of
+// column col is read at the bit nib_bit(col) of dword col / 8; the lookup
+// offsets become M 0 (argI, argD), I 1 (I-open), D 2 (D-open) instead of the
+// byte's 1 / 3 / 5, so the same kNextLut decides; the end cell's state set
+// comes from the end value's low bits; '=' / 'X' compare the query byte
+// (LDS) with the row's db char in the segment.
+template <int G, int K, bool kNib = false>
 __device__ void walk_pack_lds(const NwPairDesc &p, int32_t hend, const uint8_t *__restrict__ mask,
                               uint32_t *__restrict__ ops_all, saln_nw_result *__restrict__ results,
-                              uint32_t *__restrict__ cigar, Scoring sc, lds_u8 *win) {
-    using WG = WalkGeo<K>;
+                              uint32_t *__restrict__ cigar, Scoring sc, lds_u8 *win,
+                              const uint8_t *__restrict__ qs) {
+    using WG = WalkGeo<K, kNib, G * K>;
+    uint32_t es_nib = 0;
+    if constexpr (kNib) {
+        es_nib = (uint32_t)hend & 7u;
+        hend >>= 3;
+    }
     constexpr Geom geo{G, K};
     constexpr uint32_t kW = WG::W, NW = WG::NW;
     constexpr uint32_t kWin = WG::kWinBytes, kSlot = WG::kSlotBytes;
@@ -365,6 +384,32 @@ __device__ void walk_pack_lds(const NwPairDesc &p, int32_t hend, const uint8_t *
     for (uint32_t b = 0; b < NW; ++b)  // blocks B, B-1, .. (clamped to block 0)
         set_ow((B + NW - b) % NW, boff(B >= b ? B - b : 0));
     const uint32_t wbase = lds_off(win) + (threadIdx.x & 63u) * 16u;
+    // kNib: the query's 16-byte chunks (aligned; a chunk holding one of the
+    // query's bytes never crosses into an unmapped page) into LDS, ahead of
+    // every window DMA, so the counted waits below also cover them
+    const uint32_t qa = (uint32_t)(p.q_off & 15u);
+    lds_u8 *const qlds = win + NW * kWin;
+    if constexpr (kNib) {
+        const uint8_t *qg = qs + (p.q_off - qa);
+        const uint32_t qlast = (qa + p.len_q - 1u) / 16u;
+#pragma unroll
+        for (uint32_t c = 0; c < WG::QC; ++c)
+            __builtin_amdgcn_global_load_lds(qg + 16u * (c < qlast ? c : qlast),
+                                             (__attribute__((address_space(3))) void *)(qlds + c * kSlot),
+                                             16, 0, 0);
+    }
+    // query byte j (1-based) of this lane's pair
+    auto qbyte = [&](uint32_t j) __attribute__((always_inline)) {
+        const uint32_t o = qa + j - 1u;
+        return (uint32_t)qlds[(o >> 4) * kSlot + (threadIdx.x & 63u) * 16u + (o & 15u)];
+    };
+    // db char byte of a 4-bit segment (Geom::nib_char_byte)
+    constexpr uint32_t kNG = (K + 3) / 4, kCB = kNG % 2 ? 4 * (kNG / 2) + 2 : 4 * (kNG / 2);
+    // bit of column c's nibble in its dword (dword c / 8)
+    auto nib_bit = [](uint32_t c) __attribute__((always_inline)) {
+        return ((c & 4u) << 2) | ((c & 1u) << 3) | (c & 2u) << 1;
+    };
+    const uint32_t fend = ~es_nib & 7u;  // kNib: the end cell's raw (absent) M, I, D bits
     uint32_t wl = wbase + wc * kWin;  // my slot 0 in the current window
     // the phase's row pointer (row ti at a phase start), W rows ahead for the refills
     // (row counts on after the lane's walk ends; rows below 1 load row 1)
@@ -423,11 +468,27 @@ __device__ void walk_pack_lds(const NwPairDesc &p, int32_t hend, const uint8_t *
     auto iopen = [](uint32_t d) __attribute__((always_inline)) {
         return __builtin_amdgcn_ubfe((~d & 0x10101010u) * 0x00204081u, 25, 4);
     };
+    // kNib: a 16-bit group half holds the I-open bits (nibble bit 2) of its
+    // columns 0..3 at bits 2, 10, 6, 14; the multiply by 0x285 gathers them in
+    // column order into bits 11..14
+    auto iopen_n = [](uint32_t h) __attribute__((always_inline)) {
+        return __builtin_amdgcn_ubfe((~h & 0x4444u) * 0x285u, 11, 4);
+    };
+    auto iopen_n8 = [&](uint32_t d) __attribute__((always_inline)) {
+        return iopen_n(d) | (iopen_n(d >> 16) << 4);
+    };
     auto iopen_mask = [&](const u32x4 &v) __attribute__((always_inline)) {
-        uint32_t pm = iopen(v.x) | (iopen(v.y) << 4);
-        if constexpr (WG::LB > 8) pm |= iopen(v.z) << 8;
-        if constexpr (WG::LB > 12) pm |= iopen(v.w) << 12;
-        return pm;
+        if constexpr (kNib) {
+            uint32_t pm = iopen_n8(v.x);
+            if constexpr (K > 8) pm |= iopen_n8(v.y) << 8;
+            if constexpr (K > 16) pm |= iopen_n8(v.z) << 16;
+            return pm;
+        } else {
+            uint32_t pm = iopen(v.x) | (iopen(v.y) << 4);
+            if constexpr (WG::LB > 8) pm |= iopen(v.z) << 8;
+            if constexpr (WG::LB > 12) pm |= iopen(v.w) << 12;
+            return pm;
+        }
     };
     constexpr uint32_t kOnes3 = 0x09249249u;  // op I (1) in each of nine 3-bit slots
     auto phase = [&](auto slot_c) __attribute__((always_inline)) {
@@ -440,13 +501,22 @@ __device__ void walk_pack_lds(const NwPairDesc &p, int32_t hend, const uint8_t *
                 if (sh >= 30) flush();  // at most 30 bits per iteration follow
                 const u32x4 seg = window_seg<WG::kVmcnt>(wl + S * kSlot);
                 if (sidx != 16u) {  // a cell step in state M, D or at the end cell
-                    const uint32_t dw = pick(seg, col >> 2), b8 = (col & 3u) * 8u;
-                    const uint32_t f3 = __builtin_amdgcn_ubfe(dw, b8 + lsh, 3);
+                    uint32_t f3, eqb;
+                    if constexpr (kNib) {
+                        const uint32_t dw = pick(seg, col >> 3);
+                        f3 = sidx == 48u ? fend : __builtin_amdgcn_ubfe(dw, nib_bit(col) + lsh, 3);
+                        const uint32_t dch = __builtin_amdgcn_ubfe(pick(seg, kCB >> 2), (kCB & 3u) * 8u, 8);
+                        eqb = qbyte(tj) == dch ? 1u : 0u;
+                    } else {
+                        const uint32_t dw = pick(seg, col >> 2), b8 = (col & 3u) * 8u;
+                        f3 = __builtin_amdgcn_ubfe(dw, b8 + lsh, 3);
+                        eqb = __builtin_amdgcn_ubfe(dw, b8 + 7u, 1);
+                    }
                     const uint32_t nx = (uint32_t)(kNextLut >> (f3 * 2u + sidx)) & 3u;
-                    acc |= (uint64_t)(nx | (__builtin_amdgcn_ubfe(dw, b8 + 7u, 1) << 2)) << sh;
+                    acc |= (uint64_t)(nx | (eqb << 2)) << sh;
                     sh += 3;
                     sidx = nx * 16u;
-                    lsh = 2u * nx + 1u;
+                    lsh = kNib ? nx : 2u * nx + 1u;
                     const bool up = nx != kStI, left = nx != kStD;
                     ti -= up ? 1u : 0u;
                     tj -= left ? 1u : 0u;
@@ -474,13 +544,18 @@ __device__ void walk_pack_lds(const NwPairDesc &p, int32_t hend, const uint8_t *
                 const uint32_t pm = iopen_mask(seg) & ((2u << col) - 1u) & (~0u << lo);
                 if (pm) {  // opens at c1: ops I x (col - c1), then M, diagonal from c1
                     const uint32_t c1 = 31u - (uint32_t)__builtin_clz(pm), n = col - c1;
-                    const uint32_t eqb =
-                        __builtin_amdgcn_ubfe(pick(seg, c1 >> 2), (c1 & 3u) * 8u + 7u, 1);
+                    uint32_t eqb;
+                    if constexpr (kNib)
+                        eqb = qbyte(tj - n) ==
+                                      __builtin_amdgcn_ubfe(pick(seg, kCB >> 2), (kCB & 3u) * 8u, 8)
+                                  ? 1u : 0u;
+                    else
+                        eqb = __builtin_amdgcn_ubfe(pick(seg, c1 >> 2), (c1 & 3u) * 8u + 7u, 1);
                     acc |= (uint64_t)((kOnes3 & ((1u << (3u * n)) - 1u)) | (eqb << (3u * n + 2u)))
                            << sh;
                     sh += 3u * (n + 1u);
                     sidx = 0;
-                    lsh = 1;
+                    lsh = kNib ? 0u : 1u;
                     ti -= 1;
                     tj -= n + 1u;
                     const bool done = ti == 0 || tj == 0;
@@ -534,10 +609,13 @@ __device__ void walk_pack_lds(const NwPairDesc &p, int32_t hend, const uint8_t *
         else ev = kEvDead;
     }
     // the reference's end states: the last row's codes are stored unfiltered
-    const uint32_t es = (m[geo.cell(p.len_db, p.len_q, rs, bs, cs)] ^ 0x7Fu) & 7u;
+    // (kNib: carried by the end value)
+    const uint32_t es = kNib ? es_nib : (m[geo.cell(p.len_db, p.len_q, rs, bs, cs)] ^ 0x7Fu) & 7u;
     uint32_t nops = 0;
     bool retried = false;
-    if (ev == kEvDead) {
+    // (4-bit codes are written by the packed fills only: sentinel-free pairs,
+    // no dead end state)
+    if (!kNib && ev == kEvDead) {
         // the first end state is sentinel-rooted (i32 lanes pairs only): the
         // DFS goes on with the next tied end states (walk_first, byte loads)
         const uint32_t rest = end_states_after(es, first_end_state(es));
@@ -583,14 +661,18 @@ __device__ void walk_pack_lds(const NwPairDesc &p, int32_t hend, const uint8_t *
 }
 
 // Per-variant traceback for filled pairs whose segments fit an LDS slot.
-template <int G, int K>
+// kNib: 4-bit codes; two waves per workgroup (the query staging doubles the
+// LDS of a wave).
+template <int G, int K, bool kNib = false>
+constexpr uint32_t tb_lds_threads() { return kNib ? 128u : 256u; }
+template <int G, int K, bool kNib>
 __global__ __launch_bounds__(256) void nw_traceback_lds_kernel(
     const NwPairDesc *__restrict__ pairs, uint32_t first, uint32_t n,
     const uint8_t *__restrict__ mask, const int32_t *__restrict__ end_h,
     uint32_t *__restrict__ ops, saln_nw_result *__restrict__ results,
-    uint32_t *__restrict__ cigar, Scoring sc) {
-    constexpr uint32_t kWave = WalkGeo<K>::kWaveLds;
-    __shared__ __attribute__((aligned(16))) uint8_t win_all[4 * kWave];
+    uint32_t *__restrict__ cigar, Scoring sc, const uint8_t *__restrict__ qs) {
+    constexpr uint32_t kWave = WalkGeo<K, kNib, G * K>::kWaveLds;
+    __shared__ __attribute__((aligned(16))) uint8_t win_all[tb_lds_threads<G, K, kNib>() / 64u * kWave];
     const uint32_t idx = first + blockIdx.x * blockDim.x + threadIdx.x;
     if (idx >= first + n) return;
     // The walk is a latency-bound chain; when it shares a SIMD with the
@@ -599,7 +681,7 @@ __global__ __launch_bounds__(256) void nw_traceback_lds_kernel(
     __builtin_amdgcn_s_setprio(3);
     const NwPairDesc p = pairs[idx];
     lds_u8 *win = (lds_u8 *)(win_all + (threadIdx.x / 64u) * kWave);
-    walk_pack_lds<G, K>(p, end_h[idx], mask, ops, results, cigar, sc, win);
+    walk_pack_lds<G, K, kNib>(p, end_h[idx], mask, ops, results, cigar, sc, win, qs);
 }
 
 // One walker per pair.  Pairs with an empty side have no mask and take the
@@ -1235,12 +1317,25 @@ template <int K>
 struct PkMask {
     uint32_t w[(K + 3) / 4];
 };
+// One pair's 4-bit walk-code segment of K columns (Geom::LBn bytes).
+template <int K>
+struct NibSeg {
+    uint32_t w[(K + 3) / 4 / 2 + 1];
+};
 
 // kCodes: kCodesWalk stores walk codes only (argM/argI/argD, I-open, D-open,
 // eq) - the
 // bits the device walker reads; the extend bits (3, 5) are left 0.  Full
 // codes (every parent set) are kept for the dense-mask / render paths.
-enum { kCodesWalk = 0, kCodesFull = 1, kCodesNone = 2 };
+// kCodesNib (round 4): 4-bit walk codes, two cells per byte - bit 0 argI,
+// 1 argD, 2 I-open, 3 D-open, each set when the parent is ABSENT - plus the
+// row's db char in the segment; no eq bit (the walker compares the query
+// byte, staged in LDS, with that char) and no argM: the end cell's state set
+// travels in the low 3 bits of the end value (value << 3 | set).  Layout of a
+// segment (Geom::LBn): the 4-column groups g = c / 4 as 16-bit halves, two
+// per dword, in each half the nibble of column c at bit 8 (c & 1) +
+// 4 ((c >> 1) & 1); then the db char at byte Geom::nib_char_byte.
+enum { kCodesWalk = 0, kCodesFull = 1, kCodesNone = 2, kCodesNib = 3 };
 
 // Where the packed fill gets its pairs and puts the end values.
 // PlanSrc: the plan's sorted descriptor table; the scaled end value goes to
@@ -1402,8 +1497,10 @@ __global__ __launch_bounds__(256) void nw_fill_pk_kernel(Src src, uint32_t count
     // nothing for it (no walker reads past column len_q; 16 x 10 groups on
     // 150-column queries: one store of 16 saved).  Full codes keep every
     // segment defined.
-    const int ldAs = (kCodes == kCodesWalk && col0 >= lqA) ? 0 : ldA;
-    const int ldBs = (kCodes == kCodesWalk && col0 >= lqB) ? 0 : ldB;
+    constexpr bool kWalkCodes = kCodes == kCodesWalk || kCodes == kCodesNib;
+    static_assert(kCodes != kCodesNib || KS == K, "4-bit codes: one segment per lane");
+    const int ldAs = (kWalkCodes && col0 >= lqA) ? 0 : ldA;
+    const int ldBs = (kWalkCodes && col0 >= lqB) ? 0 : ldB;
     // Previous-row H: step t reads Hin (row r-1) and writes Hout (row r); a
     // two-step unroll swaps two arrays (no register rotation).
     uint32_t HpB[K];
@@ -1465,6 +1562,11 @@ __global__ __launch_bounds__(256) void nw_fill_pk_kernel(Src src, uint32_t count
             // code words of column pairs: bytes [A_2c, B_2c, A_2c+1, B_2c+1]
             uint32_t cw[(K + 1) / 2];
             uint32_t prv[8];  // sign sources of the previous (even) column
+            // 4-bit codes: column-group words, the group's first column pair
+            // (low nibbles), the previous column's four sources, and the end
+            // cells' state sets
+            uint32_t nw[(K + 3) / 4], nlo = 0, nprv[4];
+            uint32_t esA = 0, esB = 0;
             // argM (bit 0) is only ever read at a pair's end cell: the wave
             // computes it on the steps where one of its lanes holds one.
             auto columns = [&](auto with_argm) __attribute__((always_inline)) {
@@ -1479,7 +1581,50 @@ __global__ __launch_bounds__(256) void nw_fill_pk_kernel(Src src, uint32_t count
                 const uint32_t I = F, D = Dn[k];
                 const uint32_t H = umax2(M, umax2(I, D));
                 const uint32_t tO = M + kOpen;
-                if constexpr (kCodes != kCodesNone) {
+                if constexpr (kCodes == kCodesNib) {
+                    // the four walk decisions as signs (set = parent absent):
+                    // argI, argD (ties against the flag-free H), I-open, D-open
+                    const uint32_t Hc = H & 0xFFFEFFFEu;
+                    const uint32_t tOr = tO | 0x00010001u;
+                    auto psub = [](uint32_t a, uint32_t b) { return as_u(as_s2(a) - as_s2(b)); };
+                    uint32_t s4[4];
+                    s4[0] = psub(I, Hc);
+                    s4[1] = psub(D, Hc);
+                    s4[2] = psub(tOr, I);
+                    s4[3] = psub(tOr, D);
+                    if constexpr (kM) {  // the end cells' state sets (present bits M, I, D)
+                        const uint32_t pM = ~psub(M, Hc), pI = ~s4[0], pD = ~s4[1];
+                        const uint32_t eA = ((pM >> 15) & 1u) | ((pI >> 14) & 2u) | ((pD >> 13) & 4u);
+                        const uint32_t eB = (pM >> 31) | ((pI >> 30) & 2u) | ((pD >> 29) & 4u);
+                        esA = k == kA ? eA : esA;
+                        esB = k == kB ? eB : esB;
+                    }
+                    if (k % 2 == 0 && k < K - 1) {
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) nprv[u] = s4[u];
+                    } else {
+                        // sign bytes [A_k-1, B_k-1, A_k, B_k] per source (a lone
+                        // last column: [A_k, B_k, 0, 0]); a group's first column
+                        // pair goes to the low nibbles, its second to the high
+                        uint32_t pw[4];
+#pragma unroll
+                        for (int u = 0; u < 4; ++u)
+                            pw[u] = k % 2 ? col_pair_signs(s4[u], nprv[u]) : col_pair_signs(0u, s4[u]);
+                        const int cp = k / 2, g = cp / 2;
+                        if (cp % 2 == 0) {
+                            uint32_t lo = bfi(0x01010101u, pw[0], pw[1]);
+                            lo = bfi(0x03030303u, lo, pw[2]);
+                            lo = bfi(0x07070707u, lo, pw[3]);
+                            if (cp == (K - 1) / 2) nw[g] = lo;
+                            else nlo = lo;
+                        } else {
+                            uint32_t x = bfi(0x10101010u, pw[0], pw[1]);
+                            x = bfi(0x30303030u, x, pw[2]);
+                            x = bfi(0x70707070u, x, pw[3]);
+                            nw[g] = bfi(0x0F0F0F0Fu, nlo, x);
+                        }
+                    }
+                } else if constexpr (kCodes != kCodesNone) {
                 // Sign set <=> parent absent.  Same-cell differences of biased
                 // halves are the unbiased differences, taken with v_pk_sub
                 // (no borrow between halves); extend/open ties are decided on
@@ -1521,9 +1666,9 @@ __global__ __launch_bounds__(256) void nw_fill_pk_kernel(Src src, uint32_t count
                 Hout[k] = H;
             }
             };
-            if constexpr (kCodes == kCodesWalk && kSteady) {
+            if constexpr (kWalkCodes && kSteady) {
                 columns(std::false_type{});
-            } else if constexpr (kCodes == kCodesWalk) {
+            } else if constexpr (kWalkCodes) {
                 const bool endcell = t == tEA || t == tEB;
                 if (__builtin_amdgcn_ballot_w64(endcell))
                     columns(std::true_type{});
@@ -1535,7 +1680,28 @@ __global__ __launch_bounds__(256) void nw_fill_pk_kernel(Src src, uint32_t count
             hd = inH;
             pubF = F;
             pubH = Hout[K - 1];
-            if constexpr (kCodes != kCodesNone) {
+            if constexpr (kCodes == kCodesNib) {
+                // group words [A_c0|A_c2, B_c0|B_c2, A_c1|A_c3, B_c1|B_c3]
+                // -> per-pair halves, two groups per dword; the db chars
+                // (dch = A << 5 | B << 21) rotated to bytes 0 / 2
+                constexpr int NG = (K + 3) / 4, ND = NG / 2 + 1;
+                const uint32_t rot = __builtin_amdgcn_alignbit(dch, dch, 5);
+                NibSeg<K> na, nb;
+#pragma unroll
+                for (int d = 0; d < NG / 2; ++d) {
+                    na.w[d] = __builtin_amdgcn_perm(nw[2 * d + 1], nw[2 * d], 0x06040200u);
+                    nb.w[d] = __builtin_amdgcn_perm(nw[2 * d + 1], nw[2 * d], 0x07050301u);
+                }
+                if constexpr (NG % 2) {
+                    na.w[ND - 1] = __builtin_amdgcn_perm(rot, nw[NG - 1], 0x0C040200u);
+                    nb.w[ND - 1] = __builtin_amdgcn_perm(rot, nw[NG - 1], 0x0C060301u);
+                } else {
+                    na.w[ND - 1] = rot & 0xFFu;
+                    nb.w[ND - 1] = __builtin_amdgcn_ubfe(rot, 16, 8);
+                }
+                if (kSteady ? ldAs != 0 : r <= ldAs) *reinterpret_cast<NibSeg<K> *>(mA) = na;
+                if (kSteady ? ldBs != 0 : r <= ldBs) *reinterpret_cast<NibSeg<K> *>(mB) = nb;
+            } else if constexpr (kCodes != kCodesNone) {
                 // column-pair words [A A' ..] -> per-pair words of 4 columns,
                 // per segment of KS columns
 #pragma unroll
@@ -1565,14 +1731,16 @@ __global__ __launch_bounds__(256) void nw_fill_pk_kernel(Src src, uint32_t count
 #pragma unroll
                 for (int k = 0; k < K; ++k)
                     if (k == kA) e = (int32_t)(Hout[k] & 0xFFFFu) - 32768;
-                src.end(ia, pa, e + base - alpha * ldA - beta * lqA);
+                const int32_t hv = e + base - alpha * ldA - beta * lqA;
+                src.end(ia, pa, kCodes == kCodesNib ? (int32_t)(((uint32_t)hv << 3) | esA) : hv);
             }
             if (!kSteady && t == tEB) {
                 int32_t e = 0;
 #pragma unroll
                 for (int k = 0; k < K; ++k)
                     if (k == kB) e = (int32_t)(Hout[k] >> 16) - 32768;
-                src.end(ib, pb, e + base - alpha * ldB - beta * lqB);
+                const int32_t hv = e + base - alpha * ldB - beta * lqB;
+                src.end(ib, pb, kCodes == kCodesNib ? (int32_t)(((uint32_t)hv << 3) | esB) : hv);
             }
         } else if (&Hout != &Hin) {
 #pragma unroll
@@ -2559,15 +2727,9 @@ constexpr bool kPacked[kNumVariants] = {false, false, false, false, true, true, 
 // halve the occupancy.)
 constexpr uint32_t kFillG[kNumVariants] = {16, 16, 64, 64, 8, 16, 32, 16, 64};
 
-// The packed fill's steady-state steps (nw_fill_pk_kernel kSteady);
-// SALN_PK_STEADY=0 turns them off (A/B switch, same results)
-static bool pk_steady() {
-    static const bool on = [] {
-        const char *e = std::getenv("SALN_PK_STEADY");
-        return !(e && e[0] == '0');
-    }();
-    return on;
-}
+// The packed fill's steady-state steps (nw_fill_pk_kernel kSteady); option
+// nw.pk_steady = 0 turns them off (A/B switch, same results)
+static bool pk_steady() { return opt(Opt::PkSteady) != 0; }
 
 // Dynamic LDS cap of the packed fill's staged db rows: two workgroups per CU.
 constexpr size_t kPackedLdsMax = 80 * 1024;
@@ -2604,10 +2766,7 @@ static hipError_t fill_pk(dim3 grid, hipStream_t s, const NwPairDesc *pairs, uin
                           uint32_t count, const uint8_t *qs, const uint8_t *ds, uint8_t *mask,
                           int32_t *end_h, saln_nw_result *, uint32_t *, Scoring sc, int codes,
                           uint32_t ld_max, bool rebase) {
-    static const size_t pad = [] {  // experiment switch: LDS floor per workgroup (occupancy)
-        const char *e = std::getenv("SALN_FILL_LDS_MIN");
-        return e ? (size_t)std::atol(e) : (size_t)0;
-    }();
+    const size_t pad = (size_t)opt(Opt::FillLdsMin);  // LDS floor per workgroup (occupancy A/B)
     const size_t lds = std::max((size_t)(256 / G) * (ld_max + 2 * G) * (rebase ? 2 : 4), pad);
     if (lds > kPackedLdsMax) return hipErrorInvalidValue;  // choose_variant keeps ld below this
     const PlanSrc src{pairs, first, end_h};
@@ -2626,6 +2785,11 @@ static hipError_t fill_pk(dim3 grid, hipStream_t s, const NwPairDesc *pairs, uin
     auto by_codes = [&](auto rebase_c) {
         if (codes == kCodesFull) return go(std::integral_constant<int, kCodesFull>{}, rebase_c);
         if (codes == kCodesNone) return go(std::integral_constant<int, kCodesNone>{}, rebase_c);
+        if (codes == kCodesNib) {  // the short-query variants (7: 16 x 10, 4: 8 x 19)
+            if constexpr (G * K <= 160) return go(std::integral_constant<int, kCodesNib>{}, rebase_c);
+            return hipErrorInvalidValue;
+        }
+        if constexpr (K > 16) return hipErrorInvalidValue;  // byte codes: 16-byte walker slots
         return go(std::integral_constant<int, kCodesWalk>{}, rebase_c);
     };
     return rebase ? by_codes(std::true_type{}) : by_codes(std::false_type{});
@@ -2774,7 +2938,7 @@ hipError_t launch_fill(int variant, const NwPairDesc *pairs, uint32_t first, uin
         case 1: fill_i32<16, 16>(grid, stream, pairs, first, count, qs, ds, mask, scratch, end_h, res, cig, sc, codes, ld_max); break;
         case 2: fill_i32<64, 8>(grid, stream, pairs, first, count, qs, ds, mask, scratch, end_h, res, cig, sc, codes, ld_max); break;
         case 3: return hipErrorInvalidValue;  // stripes: launch_fill_stripes
-        case 4: return hipErrorInvalidValue;  // 8 x 19 groups: the all-vs-all only (nw_avsa.cpp)
+        case 4: e = fill_pk<8, 19>(grid, stream, pairs, first, count, qs, ds, mask, end_h, res, cig, sc, codes, ld_max, rebase); break;
         case 5: e = fill_pk<16, 16>(grid, stream, pairs, first, count, qs, ds, mask, end_h, res, cig, sc, codes, ld_max, rebase); break;
         case 7: e = fill_pk<16, 10>(grid, stream, pairs, first, count, qs, ds, mask, end_h, res, cig, sc, codes, ld_max, rebase); break;
         case 8: e = fill_pk<64, 16>(grid, stream, pairs, first, count, qs, ds, mask, end_h, res, cig, sc, codes, ld_max, rebase); break;
@@ -2784,12 +2948,13 @@ hipError_t launch_fill(int variant, const NwPairDesc *pairs, uint32_t first, uin
     return hipGetLastError();
 }
 
-template <int G, int K>
-static void tb_lds(dim3 grid, hipStream_t s, const NwPairDesc *pairs, uint32_t first, uint32_t n,
+template <int G, int K, bool kNib = false>
+static void tb_lds(hipStream_t s, const NwPairDesc *pairs, uint32_t first, uint32_t n,
                    const uint8_t *mask, const int32_t *end_h, uint32_t *ops, saln_nw_result *res,
-                   uint32_t *cig, Scoring sc) {
-    nw_traceback_lds_kernel<G, K><<<grid, dim3(256), 0, s>>>(pairs, first, n, mask, end_h, ops,
-                                                              res, cig, sc);
+                   uint32_t *cig, Scoring sc, const uint8_t *qs) {
+    constexpr uint32_t nt = tb_lds_threads<G, K, kNib>();
+    nw_traceback_lds_kernel<G, K, kNib><<<dim3((n + nt - 1) / nt), dim3(nt), 0, s>>>(
+        pairs, first, n, mask, end_h, ops, res, cig, sc, qs);
 }
 
 // Traceback of plan range [first, first+n).  variant >= 0: all pairs of that
@@ -2799,13 +2964,14 @@ hipError_t launch_traceback(int variant, const NwPairDesc *pairs, uint32_t first
                             const uint8_t *qs, const uint8_t *ds, const uint8_t *mask,
                             const int32_t *end_h, uint32_t *ops, saln_nw_result *results,
                             uint32_t *cigar, Scoring sc, int stripe_layout, hipStream_t stream,
-                            const uint32_t *spec_done) {
+                            const uint32_t *spec_done, bool nib) {
     if (n == 0) return hipSuccess;
     const dim3 grid((n + 255) / 256);
+    if (nib && variant != 4 && variant != 7) return hipErrorInvalidValue;
     switch (variant) {
-        case 0: tb_lds<16, 10>(grid, stream, pairs, first, n, mask, end_h, ops, results, cigar, sc); break;
-        case 1: tb_lds<16, 16>(grid, stream, pairs, first, n, mask, end_h, ops, results, cigar, sc); break;
-        case 2: tb_lds<64, 8>(grid, stream, pairs, first, n, mask, end_h, ops, results, cigar, sc); break;
+        case 0: tb_lds<16, 10>(stream, pairs, first, n, mask, end_h, ops, results, cigar, sc, qs); break;
+        case 1: tb_lds<16, 16>(stream, pairs, first, n, mask, end_h, ops, results, cigar, sc, qs); break;
+        case 2: tb_lds<64, 8>(stream, pairs, first, n, mask, end_h, ops, results, cigar, sc, qs); break;
         case 3: {  // column-stripe pairs: one cooperative wave per pair
             // a few pairs: the whole 160 KB (fewer window reloads); batches:
             // 48 KB windows, three waves per CU
@@ -2833,11 +2999,17 @@ hipError_t launch_traceback(int variant, const NwPairDesc *pairs, uint32_t first
             if (e != hipSuccess) return e;
             break;
         }
-        case 4: return hipErrorInvalidValue;  // no plan fills variant 4
-        case 5: tb_lds<16, 16>(grid, stream, pairs, first, n, mask, end_h, ops, results, cigar, sc); break;
-        case 6: tb_lds<32, 16>(grid, stream, pairs, first, n, mask, end_h, ops, results, cigar, sc); break;
-        case 7: tb_lds<16, 10>(grid, stream, pairs, first, n, mask, end_h, ops, results, cigar, sc); break;
-        case 8: tb_lds<64, 16>(grid, stream, pairs, first, n, mask, end_h, ops, results, cigar, sc); break;
+        case 4:  // 8 x 19 groups: 4-bit codes only (byte segments would not fit a slot)
+            if (!nib) return hipErrorInvalidValue;
+            tb_lds<8, 19, true>(stream, pairs, first, n, mask, end_h, ops, results, cigar, sc, qs);
+            break;
+        case 5: tb_lds<16, 16>(stream, pairs, first, n, mask, end_h, ops, results, cigar, sc, qs); break;
+        case 6: tb_lds<32, 16>(stream, pairs, first, n, mask, end_h, ops, results, cigar, sc, qs); break;
+        case 7:
+            if (nib) tb_lds<16, 10, true>(stream, pairs, first, n, mask, end_h, ops, results, cigar, sc, qs);
+            else tb_lds<16, 10>(stream, pairs, first, n, mask, end_h, ops, results, cigar, sc, qs);
+            break;
+        case 8: tb_lds<64, 16>(stream, pairs, first, n, mask, end_h, ops, results, cigar, sc, qs); break;
         default: {  // empty-side pairs
             GeomTable gt;
             for (int v = 0; v < kNumVariants; ++v) gt.g[v] = kVariants[v];
@@ -2934,14 +3106,15 @@ hipError_t launch_span_spec(const NwPairDesc *pairs, SpecArgs sa, uint32_t n_blo
 // Returns once rows r0 .. r1 of a boundary column are published (the row
 // fill's 8-byte (H~, I~) elements, preset to kColEmpty), so that work queued
 // behind it (an RCCL send of those rows) reads them.  Bounded like the fill's
-// own waits: err[1] polls, then err[0] bit 0.
+// own waits: each row's wait gets err[1] polls (the count restarts per row),
+// then err[0] bit 0.
 __global__ __launch_bounds__(64) void nw_span_watch_kernel(const int2 *__restrict__ col,
                                                            uint32_t r0, uint32_t r1,
                                                            uint32_t *__restrict__ err) {
     const uint32_t lim = err[1];
-    uint32_t spins = 0;
     bool failed = false;
     for (uint32_t r = r0 + threadIdx.x; r <= r1 && !failed; r += 64) {
+        uint32_t spins = 0;
         for (;;) {
             const uint64_t v = __hip_atomic_load((const uint64_t *)(col + r), __ATOMIC_RELAXED,
                                                  __HIP_MEMORY_SCOPE_AGENT);
@@ -2959,17 +3132,19 @@ __global__ __launch_bounds__(64) void nw_span_watch_kernel(const int2 *__restric
 // One device, two spans: forwards rows r0 .. r1 of src's outbox into dst's
 // inbox as they are published, 64 rows per round (one wave; each row one
 // 8-byte sc1 load once published and one sc1 store, the form of the fill's
-// own publication), so dst's first stripe sees them row by row.
+// own publication), so dst's first stripe sees them row by row.  Each row's
+// wait gets err[1] polls (the count restarts per row, as in the fill), so the
+// limit bounds one wait, not the upstream span's whole fill.
 __global__ __launch_bounds__(64) void nw_span_relay_kernel(const int2 *__restrict__ src,
                                                            int2 *__restrict__ dst, uint32_t r0,
                                                            uint32_t r1, uint32_t *__restrict__ err) {
     const uint32_t lim = err[1];
-    uint32_t spins = 0;
     bool failed = false;
     for (uint32_t base = r0; base <= r1 && !failed; base += 64) {
         const uint32_t r = base + threadIdx.x;
         if (r <= r1) {
             uint64_t v;
+            uint32_t spins = 0;
             for (;;) {
                 v = __hip_atomic_load((const uint64_t *)(src + r), __ATOMIC_RELAXED,
                                       __HIP_MEMORY_SCOPE_AGENT);
@@ -3074,24 +3249,21 @@ Geom variant_geom(int v) { return kVariants[v]; }
 // so one long pair (C4, 391 waves alone on their SIMDs) fills slower (45.4 vs
 // 40.1 ms) although the step is cheaper; once the stripe waves fill the chip
 // it wins (400 x 5 kbp pairs: 8.0 vs 9.2 ms end to end).  Chosen per plan
-// from the stripe-wave count; SALN_STRIPE_PK=0 / 1 forces it.
+// from the stripe-wave count; option nw.stripe_pk = 0 / 1 forces it.
 // Row-fill columns per lane: K = 1 (64-column stripes) while every stripe
 // wave of the plan has a SIMD to itself (a shorter row step: C1 0.197 ->
 // 0.188 ms, 5 kbp 0.75 -> 0.70 ms), else K = 2 (C4: 1,564 K = 1 waves share
-// SIMDs, 19.5 vs 14.5 ms).  SALN_ROWS_K = 1, 2 or 4
-// forces it.
+// SIMDs, 19.5 vs 14.5 ms).  Option nw.rows_k = 1, 2 or 4 forces it (read per
+// plan).
 int stripe_rows_k(uint64_t waves_k1) {
-    if (const char *e = std::getenv("SALN_ROWS_K")) {  // read per plan
-        const int v = std::atoi(e);
-        return v == 1 || v == 4 ? v : 2;
-    }
+    if (const int64_t v = opt(Opt::RowsK)) return v == 1 || v == 4 ? (int)v : 2;
     return waves_k1 <= 1024 ? 1 : 2;
 }
 
 bool stripe_packed(const Scoring &sc, uint64_t n_waves, bool wide) {
-    const char *e = std::getenv("SALN_STRIPE_PK");
-    if (e && e[0] == '0') return false;
-    if (!(e && e[0] == '1') && (n_waves < kStripePkMinWaves || !wide)) return false;
+    const int64_t force = opt(Opt::StripePk);  // -1 auto
+    if (force == 0) return false;
+    if (force != 1 && (n_waves < kStripePkMinWaves || !wide)) return false;
     const int64_t pen = 2ll * (sc.match - sc.mismatch);
     if (pen < 2 || pen > 32 || sc.gap_extend > 0 || sc.gap_open > 0) return false;
     const int64_t m = std::abs(sc.match), ge = std::abs(sc.gap_extend), go = std::abs(sc.gap_open);
@@ -3140,10 +3312,16 @@ static bool packed_ok_rebase(uint32_t lq, uint32_t ld, const Scoring &sc, uint32
     return bound < 30000;
 }
 
-int choose_variant(uint32_t len_q, uint32_t len_db, const Scoring &sc) {
+int choose_variant(uint32_t len_q, uint32_t len_db, const Scoring &sc, bool narrow) {
     // the packed fills carry V' = 2V + p (no alive flag): sentinel-free pairs only
     const bool free = sentinel_free(sc, len_q, len_db);
     if (!free) return len_q <= 160 ? 0 : len_q <= 256 ? 1 : len_q <= 512 ? 2 : 3;
+    // 8 x 19 groups (4-bit walk codes): queries of <= 152 columns, one
+    // int16 frame or the rebasing one (launch_fill decides from the widest)
+    if (narrow && len_q <= 152) {
+        const Geom g = kVariants[4];
+        if (packed_ok(g.W(), len_db, sc) || packed_ok_rebase(len_q, len_db, sc, g.G, g.W())) return 4;
+    }
     if (packed_ok(len_q, len_db, sc)) {
         if (len_q <= 160) return 7;
         if (len_q <= 256) return 5;

@@ -86,7 +86,8 @@ struct saln_nw_span {
 // from their right neighbour's previous exit); the stored walks form the
 // sequential walk when, from the rightmost stripe leftwards, each stripe's
 // stored entry is where the walk left the stripe after it.  Returns SALN_OK,
-// an error, or 1 when they do not link (the caller walks sequentially).
+// an error, or SALN_SPAN_UNLINKED when they do not link (the caller walks
+// sequentially).
 static int span_walk_spec(saln_nw_span *s, const uint8_t *d_q, const uint8_t *d_db,
                           const saln_nw_span_cursor *entry, saln_nw_span_cursor *exit,
                           uint32_t *ops, uint64_t ops_cap, uint64_t *n_ops, hipStream_t st) {
@@ -120,7 +121,7 @@ static int span_walk_spec(saln_nw_span *s, const uint8_t *d_q, const uint8_t *d_
     uint64_t nw = 0;
     for (int t = (int)n - 1;; --t) {
         const SpecStripe &r = s->h_srec[t];
-        if (r.in_i != ci || r.in_j != cj || r.in_k != ck || r.nops > kSpecOpsCap) return 1;
+        if (r.in_i != ci || r.in_j != cj || r.in_k != ck || r.nops > kSpecOpsCap) return SALN_SPAN_UNLINKED;
         if (ops && nw + r.nops > ops_cap) {
             set_error("span walk: ops buffer too small (saln_nw_span_info ops_cap)");
             return SALN_E_CAPACITY;
@@ -132,7 +133,7 @@ static int span_walk_spec(saln_nw_span *s, const uint8_t *d_q, const uint8_t *d_
         ck = r.out_k[cf];
         if (ck >= kSpecEv || t == 0) break;  // ended, or left the span
     }
-    if (ck == kSpecNone) return 1;
+    if (ck == kSpecNone) return SALN_SPAN_UNLINKED;
     *n_ops = nw;
     exit->i = ci;
     exit->j = cj;
@@ -242,13 +243,11 @@ int saln_nw_span_create(saln_context *ctx, uint64_t len_q, uint64_t len_db, uint
         (e = dev_alloc(ctx, (void **)&s->d_rec, 2 * sizeof(SpecStripe))) != hipSuccess ||
         (e = dev_alloc(ctx, (void **)&s->d_ops, (s->ops_cap + 8) * sizeof(uint32_t))) != hipSuccess)
         return fail(e, "tables");
-    // speculative walk passes (SALN_SPEC=0 off, SALN_SPEC_PASSES, default 3)
+    // speculative walk passes (options nw.spec, nw.spec_passes, default 3)
     // for spans of at least two walker stripes
     {
-        const char *env = std::getenv("SALN_SPEC");
-        const char *pe = std::getenv("SALN_SPEC_PASSES");
-        const int passes = pe ? std::atoi(pe) : 3;
-        if ((!env || std::atoi(env) != 0) && passes > 0 && s->ntiles >= 2) {
+        const int passes = (int)opt(Opt::SpecPasses);
+        if (opt(Opt::Spec) != 0 && passes > 0 && s->ntiles >= 2) {
             s->spec_passes = passes;
             std::vector<uint2> blocks;
             for (uint32_t t = 0; t < s->ntiles; ++t) blocks.push_back(make_uint2(0u, s->t0 + t));
@@ -335,7 +334,7 @@ int saln_nw_span_walk(saln_nw_span *s, const uint8_t *d_q, const uint8_t *d_db,
     hipStream_t st = resolve_stream(stream, s->ctx);
     if (s->spec_passes) {
         const int rc = span_walk_spec(s, d_q, d_db, entry, exit, ops, ops_cap, n_ops, st);
-        if (rc != 1) return rc;  // 1: the passes did not link, walk sequentially
+        if (rc != SALN_SPAN_UNLINKED) return rc;  // not linked: walk sequentially
     }
     SpecStripe rec[2];
     std::memset(rec, 0, sizeof rec);
@@ -428,7 +427,7 @@ int saln_nw_spans_walk(saln_nw_span *const *spans, uint32_t n, const uint8_t *d_
         if (s->ctx != f->ctx || s->lq != f->lq || s->ld != f->ld ||
             (r + 1 < n && s->col_hi != spans[r + 1]->col_lo))
             return SALN_E_INVALID;
-        if (!s->spec_passes) return 1;  // a span without speculative tables: walk span by span
+        if (!s->spec_passes) return SALN_SPAN_UNLINKED;  // no speculative tables: span by span
     }
     HIP_TRY(hipSetDevice(f->ctx->device));
     hipStream_t st = resolve_stream(stream, f->ctx);
@@ -436,8 +435,12 @@ int saln_nw_spans_walk(saln_nw_span *const *spans, uint32_t n, const uint8_t *d_
     const int P = f->spec_passes;
     SpecStripe *d_rec = nullptr, *h_rec = nullptr;
     uint32_t *d_ops = nullptr, *h_ops = nullptr;
-    int rc = SALN_OK;
+    // the context's pinned staging is shared with the host-buffer entry
+    // points: held from the first copy to the end of the host-side link
+    std::unique_lock<std::mutex> stage_lk(f->ctx->staging_mu);
+    bool queued = false;  // async work on st may still use d_rec / d_ops
     auto done = [&](int r) {
+        if (queued) (void)hipStreamSynchronize(st);  // no block goes back while in use
         if (d_rec) dev_free(f->ctx, d_rec);
         if (d_ops) dev_free(f->ctx, d_ops);
         return r;
@@ -462,6 +465,7 @@ int saln_nw_spans_walk(saln_nw_span *const *spans, uint32_t n, const uint8_t *d_
     // every span's launch: a span's rightmost stripe reads the exit of the
     // next span's leftmost stripe from the previous pass, the pair's last
     // stripe enters at the end cell (nw_traceback_coop_kernel kSpec)
+    queued = true;
     if (hipMemcpyAsync(d_rec, h_rec, (T + 1) * sizeof(SpecStripe), hipMemcpyHostToDevice, st) !=
         hipSuccess)
         return done(SALN_E_HIP);
@@ -478,36 +482,47 @@ int saln_nw_spans_walk(saln_nw_span *const *spans, uint32_t n, const uint8_t *d_
             hipSuccess ||
         hipStreamSynchronize(st) != hipSuccess)
         return done(SALN_E_HIP);
-    // link from the end cell's stripe leftwards (as span_walk_spec)
+    queued = false;
+    // link from the end cell's stripe leftwards (as span_walk_spec): the
+    // stripes' run words in walk order, runs of one op merged at the seams
     const int cf = P & 1;
     int32_t ci = (int32_t)f->ld, cj = (int32_t)f->lq, ck = kSpecEnd;
-    uint64_t nw = 0;
+    std::vector<uint32_t> walk;
+    walk.reserve(1024);
     for (int t = (int)T - 1;; --t) {
         const SpecStripe &r = h_rec[t];
-        if (r.in_i != ci || r.in_j != cj || r.in_k != ck || r.nops > kSpecOpsCap) return done(1);
-        if (ops && nw + r.nops > ops_cap) {
-            set_error("spans walk: ops buffer too small");
-            return done(SALN_E_CAPACITY);
+        if (r.in_i != ci || r.in_j != cj || r.in_k != ck || r.nops > kSpecOpsCap) return done(SALN_SPAN_UNLINKED);
+        const uint32_t *w = h_ops + (size_t)t * kSpecOpsCap;
+        for (uint32_t k = 0; k < r.nops; ++k) {
+            if ((w[k] >> 4) == 0) continue;  // empty run
+            if (!walk.empty() && (walk.back() & 15u) == (w[k] & 15u))
+                walk.back() += w[k] & ~15u;
+            else
+                walk.push_back(w[k]);
         }
-        if (ops) std::memcpy(ops + nw, h_ops + (size_t)t * kSpecOpsCap, r.nops * sizeof(uint32_t));
-        nw += r.nops;
         ci = r.out_i[cf];
         cj = r.out_j[cf];
         ck = r.out_k[cf];
         if (ck >= kSpecEv || t == 0) break;
     }
+    const uint64_t nw = walk.size();
     const uint32_t es = h_rec[T - 1].am_end;
     // not ended at column 0, or a dead end with tied end states left (the
     // span-by-span walk restarts in the next state): walk span by span
     if (ck < kSpecEv || ck == kSpecNone ||
         (ck - kSpecEv == 2 /* dead */ && (es & ~(uint32_t)(es & 4u ? 4u : es & 1u ? 1u : 2u))))
-        return done(1);
+        return done(SALN_SPAN_UNLINKED);
+    if (ops && nw > ops_cap) {
+        set_error("spans walk: CIGAR buffer too small");
+        return done(SALN_E_CAPACITY);
+    }
+    if (ops)  // forward order: the CIGAR
+        for (uint64_t k = 0; k < nw; ++k) ops[k] = walk[nw - 1 - k];
     *n_ops = nw;
     exit->i = ci;
     exit->j = cj;
     exit->kind = ck;
     exit->end_states = es;
-    (void)rc;
     return done(SALN_OK);
 }
 

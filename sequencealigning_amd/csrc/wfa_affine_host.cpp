@@ -19,6 +19,7 @@
 #include "nw_host.hpp"
 #include "saln.h"
 #include "wfa_affine.hpp"
+#include "saln_options.hpp"
 
 using namespace saln;
 
@@ -39,7 +40,6 @@ namespace {
 // pass's ring is the 64 KB LDS limit of a workgroup; a wavefront wider than it
 // (|k| > W/2 diagonals: penalties above ~e * W / 2) leaves score -2
 constexpr int32_t kW1 = 1024, kW2 = 2048, kW1Wide = 512, kW2Wide = 1024;
-constexpr uint64_t kSeqLds = 24u << 10;  // LDS for a pair's staged sequences
 
 #define TRY(expr)                                                                          \
     do {                                                                                   \
@@ -144,18 +144,10 @@ int saln_wfa_affine_plan_create(saln_context *ctx, const uint64_t *q_off, uint64
     }
     // Each pass stages the pair's sequences in LDS when they fit next to its
     // rings within kSeqLds / the 64 KB workgroup limit (else reads HBM).
-    static const uint64_t seq_lds = [] {  // experiment switch: LDS for staged sequences
-        const char *e = std::getenv("SALN_WFA2_SEQLDS");
-        return e ? (uint64_t)std::atol(e) : kSeqLds;
-    }();
-    static const int32_t w1 = [] {  // experiment switch: first-pass ring width
-        const char *e = std::getenv("SALN_WFA2_W1");
-        return e ? (int32_t)std::atoi(e) : 0;
-    }();
-    static const int32_t w2 = [] {  // experiment switch: second-pass ring width
-        const char *e = std::getenv("SALN_WFA2_W2");
-        return e ? (int32_t)std::atoi(e) : 0;
-    }();
+    // tuning options (saln_option_set): staged-sequence LDS, ring widths (0 auto)
+    const uint64_t seq_lds = (uint64_t)opt(Opt::Wfa2SeqLds);
+    const int32_t w1 = (int32_t)opt(Opt::Wfa2W1);
+    const int32_t w2 = (int32_t)opt(Opt::Wfa2W2);
     auto pass = [&](int32_t W) {
         WfaAffParams q = p->prm;
         q.W = W;

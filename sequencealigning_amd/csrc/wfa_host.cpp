@@ -39,7 +39,9 @@ struct DevBuf {
 };
 
 constexpr uint32_t kDefaultSteps = 64, kDefaultWidth = 64;
-constexpr uint64_t kArenaBudget = 32ull << 30;  // bytes of tensor history per launch (288 GB HBM)
+// bytes of tensor history per launch: sized for 288 GB of HBM, capped by the
+// free memory at plan time (WfaScratch::arena)
+constexpr uint64_t kArenaBudget = 32ull << 30;
 // Batch runs start every pair with this step cap (a small arena, many lanes
 // per launch); the pairs that reach it are re-run with the caller's cap.
 // Essentially every realistic pair ends far earlier (REF_PANIC_TRIM at s = 20,
@@ -63,18 +65,35 @@ struct WfaScratch {
 
     hipError_t arena(uint64_t S_, uint64_t W_, uint64_t n_pairs, WfaArena *out) {
         const uint64_t per_lane = S_ * 3 * 4 * 4 + S_ * 3 * W_ * 8 + S_;
-        uint64_t nl_ = std::max<uint64_t>(256, std::min<uint64_t>(n_pairs, kArenaBudget / per_lane));
+        // at most kArenaBudget, and at most half of the device memory free
+        // now (the arena held so far counts as free: it is replaced)
+        uint64_t budget = kArenaBudget;
+        size_t fr = 0, tot = 0;
+        if (hipMemGetInfo(&fr, &tot) == hipSuccess) {
+            const uint64_t held = S * 3 * 4 * 4 * nl + S * 3 * W * 8 * nl + S * nl;
+            budget = std::min<uint64_t>(budget, (fr + held) / 2);
+        } else {
+            (void)hipGetLastError();
+        }
+        uint64_t nl_ = std::max<uint64_t>(256, std::min<uint64_t>(n_pairs, budget / per_lane));
         nl_ = std::min<uint64_t>(nl_, n_pairs);
         if (S_ * nl_ > S * nl || S_ * W_ * nl_ > S * W * nl) {
-            for (DevBuf *b : {&hdr, &off, &meta, &tsome}) {
-                if (b->p) (void)hipFree(b->p);
-                b->p = nullptr;
+            for (;;) {  // out of memory: halve the lanes per launch (down to 256)
+                for (DevBuf *b : {&hdr, &off, &meta, &tsome}) {
+                    if (b->p) (void)hipFree(b->p);
+                    b->p = nullptr;
+                }
+                S = W = nl = 0;
+                hipError_t e;
+                if ((e = hdr.alloc(S_ * 3 * 4 * nl_ * sizeof(int32_t))) == hipSuccess &&
+                    (e = off.alloc(S_ * 3 * W_ * nl_ * sizeof(int32_t))) == hipSuccess &&
+                    (e = meta.alloc(S_ * 3 * W_ * nl_ * sizeof(uint32_t))) == hipSuccess &&
+                    (e = tsome.alloc(S_ * nl_)) == hipSuccess)
+                    break;
+                if (e != hipErrorOutOfMemory || nl_ <= 256) return e;
+                (void)hipGetLastError();
+                nl_ = std::max<uint64_t>(256, nl_ / 2);
             }
-            hipError_t e;
-            if ((e = hdr.alloc(S_ * 3 * 4 * nl_ * sizeof(int32_t))) != hipSuccess) return e;
-            if ((e = off.alloc(S_ * 3 * W_ * nl_ * sizeof(int32_t))) != hipSuccess) return e;
-            if ((e = meta.alloc(S_ * 3 * W_ * nl_ * sizeof(uint32_t))) != hipSuccess) return e;
-            if ((e = tsome.alloc(S_ * nl_)) != hipSuccess) return e;
             S = S_;
             W = W_;
             nl = nl_;

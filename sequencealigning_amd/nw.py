@@ -91,25 +91,59 @@ def n_w_align(seq1, seq2, verbose: bool = False, mode: Mode = Mode.Global, *, sc
 
 def render(seq1, seq2, mode: Mode = Mode.Global, max_blocks: int = 0, *,
            device: int = 0) -> tuple[str, int, int]:
-    """Reference stdout for one pair (timing line excluded): (text, blocks, status)."""
+    """Reference stdout for one pair (timing line excluded): (text, blocks,
+    status); one library call (saln_nw_render_text)."""
     q, d = _bytes(seq1), _bytes(seq2)
     L = _lib.lib()
-    ctx = _lib.context(device)
     qb = C.create_string_buffer(q, len(q)) if q else None
     db = C.create_string_buffer(d, len(d)) if d else None
-    n = C.c_uint64()
-    nb = C.c_uint64()
-    st = C.c_int32()
-    rc = L.saln_nw_render(ctx, qb, len(q), db, len(d), int(mode), max_blocks, None, 0,
-                          C.byref(n), C.byref(nb), C.byref(st))
-    if rc == _lib.NOT_IMPLEMENTED:
+    h = C.c_void_p()
+    _lib.check(L.saln_nw_render_text(_lib.context(device), qb, len(q), db, len(d), int(mode),
+                                     max_blocks, C.byref(h)), "saln_nw_render_text")
+    try:
+        text, blocks, status, _ = _text_get(h, 0)
+    finally:
+        L.saln_nw_text_free(h)
+    if status == _lib.NOT_IMPLEMENTED:
         raise AlignmentError("not implemented")
-    _lib.check(rc, "saln_nw_render")
-    buf = C.create_string_buffer(n.value + 1)
-    rc = L.saln_nw_render(ctx, qb, len(q), db, len(d), int(mode), max_blocks, buf, n.value + 1,
-                          C.byref(n), C.byref(nb), C.byref(st))
-    _lib.check(rc, "saln_nw_render")
-    return buf.raw[:n.value].decode("latin-1"), nb.value, st.value
+    return text, blocks, status
+
+
+def _text_get(h, k: int):
+    ptr, n, nb, st, ns = C.c_void_p(), C.c_uint64(), C.c_uint64(), C.c_int32(), C.c_uint64()
+    _lib.check(_lib.lib().saln_nw_text_get(h, k, C.byref(ptr), C.byref(n), C.byref(nb),
+                                           C.byref(st), None, C.byref(ns)), "saln_nw_text_get")
+    text = C.string_at(ptr.value, n.value).decode("latin-1") if n.value else ""
+    return text, nb.value, st.value, ns.value
+
+
+def render_batch(queries, dbs, pairs=None, *, mode: Mode = Mode.Global, max_blocks: int = 0,
+                 stop_at_panic: bool = False, device: int = 0) -> list[tuple[str, int, int]]:
+    """The reference's stdout per pair of a batch (saln_nw_render_batch: one
+    plan, every pair computed once): [(text, blocks, status)] in pair order
+    (pairs=None: all-vs-all, db outer / query inner, main.rs:61-62).  With
+    stop_at_panic the list ends at the first pair whose traceback panics (the
+    reference aborts there)."""
+    qs, qo = pack_csr(queries)
+    ds, do = pack_csr(dbs)
+    if pairs is None:
+        pq = pd = None
+        n = len(queries) * len(dbs)
+    else:
+        pa = np.asarray(pairs, np.uint32).reshape(-1, 2)
+        pq, pd = np.ascontiguousarray(pa[:, 0]), np.ascontiguousarray(pa[:, 1])
+        n = len(pa)
+    L = _lib.lib()
+    h = C.c_void_p()
+    ptr = lambda a: a.ctypes.data_as(C.c_void_p) if a is not None and a.size else None  # noqa: E731
+    _lib.check(L.saln_nw_render_batch(_lib.context(device), ptr(qs), ptr(qo), len(queries),
+                                      ptr(ds), ptr(do), len(dbs), ptr(pq), ptr(pd), n, int(mode),
+                                      max_blocks, 1 if stop_at_panic else 0, C.byref(h)),
+               "saln_nw_render_batch")
+    try:
+        return [_text_get(h, k)[:3] for k in range(L.saln_nw_text_count(h))]
+    finally:
+        L.saln_nw_text_free(h)
 
 
 def dense_mask(seq1, seq2, scoring=None, *, device: int = 0) -> np.ndarray:

@@ -112,6 +112,37 @@ def walk_spans(walkers, len_q: int, len_db: int):
         entry = (len_db, len_q, st, 0)
 
 
+class CigarWords:
+    """A CIGAR as the library's words ((len << 4) | op, forward order), read as
+    the list of (len, op) tuples NwAlignment.cigar holds, decoded on first
+    use: a 100 kbp pair has ~10^4 runs, and building their tuples costs more
+    than the device walk."""
+
+    def __init__(self, words):
+        self.words = np.asarray(words, np.uint32)
+        self._list = None
+
+    def _decoded(self):
+        if self._list is None:
+            self._list = [(int(w) >> 4, _lib.CIGAR_OPS[int(w) & 15]) for w in self.words.tolist()]
+        return self._list
+
+    def __iter__(self):
+        return iter(self._decoded())
+
+    def __len__(self):
+        return len(self.words)
+
+    def __getitem__(self, k):
+        return self._decoded()[k]
+
+    def __eq__(self, other):
+        return list(self) == list(other)
+
+    def __repr__(self):
+        return f"CigarWords({len(self.words)} runs)"
+
+
 def result_from_walk(score: int, status: int, ev: int, es: int, segs) -> NwAlignment:
     """NwAlignment like saln_nw_align's (make_result, nw_kernels.hip): the
     CIGAR only when the walk printed (ended at the origin)."""
@@ -326,10 +357,12 @@ class SpanChain:
         rc = L.saln_nw_spans_walk(hs, len(self.spans), C.c_void_p(self.q.data_ptr()),
                                   C.c_void_p(self.d.data_ptr()), C.byref(ex), buf, cap,
                                   C.byref(n), _lib.torch_stream(self.device))
-        if rc == _lib.OK:
-            ops = np.ctypeslib.as_array(buf)[:n.value].copy()
-            return result_from_walk(score, status, ex.kind - SPAN_EXIT, ex.end_states, [ops])
-        if rc != 1:
+        if rc == _lib.OK:  # the CIGAR, merged at the seams in the library
+            ev = ex.kind - SPAN_EXIT
+            words = np.ctypeslib.as_array(buf)[:n.value].copy()
+            return NwAlignment(int(score), int(status), int(ex.end_states), ev == EV_ORIGIN,
+                               CigarWords(words if ev == EV_ORIGIN else words[:0]))
+        if rc != _lib.SPAN_UNLINKED:
             _lib.check(rc, "saln_nw_spans_walk")
         walkers = [lambda e, s=s: s.walk(self.q, self.d, e) for s in self.spans]
         ev, es, segs = walk_spans(walkers, self.len_q, self.len_db)

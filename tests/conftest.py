@@ -26,3 +26,17 @@ def saln():
     from sequencealigning_amd import _lib
     _lib.lib()
     return s
+
+
+@pytest.fixture
+def saln_opt():
+    """Sets engine options (saln_option_set) for one test; every option is
+    back at its default afterwards."""
+    from sequencealigning_amd import _lib
+    _lib.lib()
+
+    def set_(name, value):
+        _lib.set_option(name, int(value))
+
+    yield set_
+    _lib.lib().saln_options_reset()

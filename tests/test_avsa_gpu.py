@@ -87,16 +87,16 @@ def test_avsa_full_configs4_sample(saln, oracle):
     av.close()
 
 
-def test_avsa_narrow_groups_equal_wide(saln, monkeypatch):
-    """Queries of <= 152 columns run in 8 x 19 lane groups (SALN_AVSA_V4,
+def test_avsa_narrow_groups_equal_wide(saln, saln_opt):
+    """Queries of <= 152 columns run in 8 x 19 lane groups (option nw.avsa_narrow,
     default on, dbs up to 600 rows); the 16 x 10 groups give the same score
     and status for every pair of a C5-shaped slice with ragged lengths and a
     db long enough to rebase the int16 frame."""
     rng = np.random.default_rng(11)
     queries = [rand_seq(rng, int(n)) for n in rng.integers(120, 153, 96)]
     dbs = [rand_seq(rng, int(n)) for n in rng.integers(100, 200, 60)] + [rand_seq(rng, 590)]
-    monkeypatch.setenv("SALN_AVSA_V4", "1")
+    saln_opt("nw.avsa_narrow", 1)
     a = saln.nw_score_all_vs_all(queries, dbs)
-    monkeypatch.setenv("SALN_AVSA_V4", "0")
+    saln_opt("nw.avsa_narrow", 0)
     b = saln.nw_score_all_vs_all(queries, dbs)
     assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])

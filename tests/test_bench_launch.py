@@ -37,3 +37,17 @@ def test_bench_refuses_instrumented_library():
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--legs", "none"],
                        capture_output=True, text=True, env=_env(SALN_LIB="/tmp/x.so"), timeout=120)
     assert r.returncode != 0 and "SALN_LIB" in r.stderr
+
+
+def test_bench_refuses_leftover_experiment_variables():
+    """Any SALN_* variable outside bench.py's allow-list (empty: the engine
+    reads none; its tuning goes through saln_option_set) stops the bench
+    before it touches the GPU, naming the variable."""
+    for var in ("SALN_PK_STEADY", "SALN_ROWS_K", "SALN_ANYTHING"):
+        r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--legs", "none"],
+                           capture_output=True, text=True, env=_env(**{var: "0"}), timeout=120)
+        assert r.returncode != 0 and var in r.stderr, (var, r.stderr[-500:])
+    sys.path.insert(0, ROOT)
+    import bench
+    assert bench.refused_env({"SALN_X": "1", "PATH": "/bin", "XSALN_Y": "2"}) == ["SALN_X"]
+    assert bench.refused_env({k: "1" for k in bench.ALLOWED_ENV}) == []

@@ -305,13 +305,13 @@ def test_wide_packed_variant(saln, oracle):
                 assert (saln.cigar_ops_string(cig[k]) if res["printed"][k] else None) == o.first_ops, (n, k)
 
 
-def test_packed_stripe_fill(saln, oracle, monkeypatch):
-    """The packed column-stripe fill, forced (SALN_STRIPE_PK=1: int16 halves,
+def test_packed_stripe_fill(saln, oracle, saln_opt):
+    """The packed column-stripe fill, forced (option nw.stripe_pk = 1: int16 halves,
     128 virtual lanes, per-row frames) and its mask layout: stripe pairs alone
     (full parent mask, first alignment) and in a batch through the cooperative
     walker equal the oracle."""
     from sequencealigning_amd import synth
-    monkeypatch.setenv("SALN_STRIPE_PK", "1")
+    saln_opt("nw.stripe_pk", 1)
     rng = np.random.default_rng(999)
     for lq, ld in [(513, 70), (1025, 40), (700, 900), (1300, 1280)]:
         _compare(saln, oracle, rand_seq(rng, lq), rand_seq(rng, ld), text=False)
@@ -328,12 +328,11 @@ def test_packed_stripe_fill(saln, oracle, monkeypatch):
         assert (saln.cigar_ops_string(cig[k]) if res["printed"][k] else None) == o.first_ops, k
 
 
-def test_packed_stripes_auto_selected(saln, oracle, monkeypatch):
+def test_packed_stripes_auto_selected(saln, oracle, saln_opt):
     """A plan with >= 1,024 stripe waves (kStripePkMinWaves) of wide
     (>= 3,000-column) queries takes the packed stripe fill and layout by
     itself; a sample of its pairs equals the oracle, and every score equals
     the forced row-fill run's."""
-    monkeypatch.delenv("SALN_STRIPE_PK", raising=False)
     rng = np.random.default_rng(2024)
     n = 90  # 3,100-column queries: 13 chunks each, 1,170 waves
     qs = [rand_seq(rng, 3100) for _ in range(n)]
@@ -345,7 +344,7 @@ def test_packed_stripes_auto_selected(saln, oracle, monkeypatch):
         assert (int(res["score"][k]), int(res["end_states"][k]), int(res["status"][k]) == 2) == \
             (o.score, o.end_states, o.panics), k
         assert (saln.cigar_ops_string(cig[k]) if res["printed"][k] else None) == o.first_ops, k
-    monkeypatch.setenv("SALN_STRIPE_PK", "0")
+    saln_opt("nw.stripe_pk", 0)
     res0, cig0 = saln.nw_align_batch(qs, ds, pairs=pairs)
     assert res0["score"].tolist() == res["score"].tolist()
     assert res0["status"].tolist() == res["status"].tolist()
@@ -436,7 +435,7 @@ def test_very_long_pair_linear_oracle(saln, oracle, shape):
 
 
 @pytest.mark.parametrize("passes", ["3", "1", "2"])
-def test_speculative_stripe_walks_equal_sequential(saln, monkeypatch, passes):
+def test_speculative_stripe_walks_equal_sequential(saln, saln_opt, passes):
     """The speculative stripe walks of long column-stripe pairs (every
     256-column stripe walks at once, nw_traceback_coop_kernel kSpec) give the
     sequential walker's results exactly: accepted when linked (default 3
@@ -459,10 +458,10 @@ def test_speculative_stripe_walks_equal_sequential(saln, monkeypatch, passes):
                                        pairs=[(k, k) for k in range(len(cases))])
         return single, res, cig
 
-    monkeypatch.setenv("SALN_SPEC", "0")
+    saln_opt("nw.spec", 0)
     seq = run()
-    monkeypatch.setenv("SALN_SPEC", "1")
-    monkeypatch.setenv("SALN_SPEC_PASSES", passes)
+    saln_opt("nw.spec", 1)
+    saln_opt("nw.spec_passes", int(passes))
     spec = run()
     for a, b in zip(seq[0], spec[0]):
         assert (a.score, a.end_states, a.panics, a.printed) == (b.score, b.end_states, b.panics, b.printed)
@@ -471,14 +470,12 @@ def test_speculative_stripe_walks_equal_sequential(saln, monkeypatch, passes):
     assert seq[2] == spec[2]
 
 
-def test_speculative_stripe_walks_link(saln, monkeypatch):
-    """On mutated long pairs the three default passes link (SALN_SPEC_STRICT=1
+def test_speculative_stripe_walks_link(saln, saln_opt):
+    """On mutated long pairs the three default passes link (option nw.spec_strict = 1
     turns a pair left to the cooperative walker into an error), so the
     speculative path, not the fallback, produced these results."""
     from sequencealigning_amd import synth
-    monkeypatch.setenv("SALN_SPEC", "1")
-    monkeypatch.delenv("SALN_SPEC_PASSES", raising=False)
-    monkeypatch.setenv("SALN_SPEC_STRICT", "1")
+    saln_opt("nw.spec_strict", 1)
     q = synth.random_bases(0x5EED0009, 40_000).tobytes()
     d = synth.mutate(q, 0.05, seed=9)
     r = saln.n_w_align(q, d)
@@ -487,19 +484,19 @@ def test_speculative_stripe_walks_link(saln, monkeypatch):
 
 
 @pytest.mark.parametrize("k", ["1", "2", "4"])
-def test_row_fill_lane_widths_agree(saln, monkeypatch, k):
-    """The row fill's 64-, 128- and 256-column stripes (SALN_ROWS_K; a plan
+def test_row_fill_lane_widths_agree(saln, saln_opt, k):
+    """The row fill's 64-, 128- and 256-column stripes (option nw.rows_k; a plan
     picks 1 or 2 itself) give identical results and CIGARs: a mutated
     12 kbp pair, a rectangular one and a batch of three."""
     from sequencealigning_amd import synth
     q = synth.random_bases(0x5EED000B, 12_000).tobytes()
     cases = [(q, synth.mutate(q, 0.05, seed=11)), (q[:7_000], synth.mutate(q, 0.1, seed=12)[:3_000])]
-    monkeypatch.setenv("SALN_ROWS_K", "2")
+    saln_opt("nw.rows_k", 2)
     ref = [saln.n_w_align(a, b) for a, b in cases]
     ref_b = saln.nw_align_batch([c[0] for c in cases] + [q[:2_500]],
                                 [c[1] for c in cases] + [q[100:2_700]],
                                 pairs=[(0, 0), (1, 1), (2, 2)])
-    monkeypatch.setenv("SALN_ROWS_K", k)
+    saln_opt("nw.rows_k", int(k))
     got = [saln.n_w_align(a, b) for a, b in cases]
     got_b = saln.nw_align_batch([c[0] for c in cases] + [q[:2_500]],
                                 [c[1] for c in cases] + [q[100:2_700]],

@@ -81,12 +81,12 @@ def test_span_chain_matches_oracle(pipelined, cu_split):
 
 
 @pytest.mark.parametrize("spec", ["1", "0"])
-def test_span_chain_long_pairs_match_plan(spec, monkeypatch):
+def test_span_chain_long_pairs_match_plan(spec, saln_opt):
     """20-30 kbp pairs over 3-8 spans (pipelined, 2,048-row bands) give the
     single-GPU plan's result word for word, with the speculative span walks
-    and with the sequential walker alone (SALN_SPEC=0); a mask-free oracle
+    and with the sequential walker alone (option nw.spec = 0); a mask-free oracle
     pins the score."""
-    monkeypatch.setenv("SALN_SPEC", spec)
+    saln_opt("nw.spec", int(spec))
     import sequencealigning_amd as saln
     from nw_check import rand_seq
     from oracle import refcpu
@@ -120,6 +120,40 @@ def test_span_injected_timeout_raises():
     sp.set_wait_limit(1 << 24)
     assert sp.status() == 0  # read and clear
     sp.close()
+
+
+def test_span_relay_wait_limit_bounds_each_row():
+    """The single-device relay (saln_nw_span_forward) under a small nonzero
+    wait limit: its source rows arrive in 64-row batches ~1 ms apart for ~60
+    ms, so the relay spends far more polls in total than the limit allows
+    one wait, but no single row waits long.  The limit bounds each row's
+    wait: every row is forwarded, no timeout is flagged."""
+    import time
+
+    import torch
+
+    from sequencealigning_amd import _lib
+    from sequencealigning_amd.span import NwSpan
+    R = 64 * 60
+    a = NwSpan(512, R, 0, 256, device=0)
+    b = NwSpan(512, R, 256, 512, device=0)
+    a.reset()
+    b.reset()
+    torch.cuda.synchronize()
+    a.set_wait_limit(8192)  # ~10 ms of polling per wait, << the ~60 ms the rows take
+    side = torch.cuda.Stream()
+    _lib.check(_lib.lib().saln_nw_span_forward(a._h, b._h, 1, R, side.cuda_stream),
+               "saln_nw_span_forward")
+    vals = torch.arange(1, R + 1, dtype=torch.int64, device="cuda") * 3 + 7
+    for lo in range(1, R + 1, 64):
+        time.sleep(0.001)
+        a.outbox[lo:lo + 64].copy_(vals[lo - 1:lo + 63])
+    side.synchronize()
+    torch.cuda.synchronize()
+    assert a.status() == 0  # no wait gave up
+    assert torch.equal(b.inbox[1:R + 1], vals)
+    a.close()
+    b.close()
 
 
 def _relay_worker(rank, world, port, q, d, out):

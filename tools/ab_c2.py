@@ -22,10 +22,15 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--pairs", type=int, default=100_000)
     ap.add_argument("--tag", default="")
+    ap.add_argument("--opt", action="append", default=[],
+                    help="engine option name=value (saln_option_set), repeatable")
     a = ap.parse_args()
     import torch
     import sequencealigning_amd as saln
     from sequencealigning_amd import _lib, synth
+    for kv in a.opt:
+        k, v = kv.split("=")
+        _lib.set_option(k, int(v))
     n, L = a.pairs, 150
     qs, qo, ds, do = synth.iid_pairs(n, L, L, seed=0x5EED0002)
     plan = saln.NwPlan(qo, do, pairs=np.stack([np.arange(n)] * 2, 1))
@@ -44,7 +49,7 @@ def main():
     plan.check()
     f, fn = plan.kernel_time("nw_fill")
     tb, tn = plan.kernel_time("nw_traceback")
-    print(json.dumps({"tag": a.tag, "lib": os.path.basename(_lib.LIB_PATH),
+    print(json.dumps({"tag": a.tag, "lib": os.path.basename(_lib.LIB_PATH), "opts": a.opt,
                       "gcups": round(plan.cells / dt / 1e9, 1), "ms_per_step": round(dt * 1e3, 4),
                       "fill_ms": round(f / fn, 4), "traceback_ms": round(tb / tn, 4)}))
 
