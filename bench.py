@@ -27,9 +27,11 @@ and `cpu_baseline`:
   c4_spans  the same pair as 8 column spans (SURVEY.md §8(f) row 3's layout,
       all on this GPU: the band hand-off's cost; 1/8 of the mask per span) (N = 1);
   host_path: configs[1] through the host-buffer C ABI (PCIe-inclusive; never
-      the value) (N = 1).
+      the value) (N = 1);
+  cli       the drop-in CLI end to end on a 316 x 316-record FASTA of 150 bp
+      (batched render, reference text per pair; process wall time) (N = 1).
 
-    python bench.py --gpus N --steps K --warmup W [--legs c5,c1,c3,c3_affine,c4,c4_spans,host|none]
+    python bench.py --gpus N --steps K --warmup W [--legs c5,c1,c3,c3_affine,c4,c4_spans,host,cli|none]
 
 With --gpus N > 1 and no WORLD_SIZE in the environment this process starts
 the N ranks itself (torch.distributed.run on 127.0.0.1, as a child process;
@@ -60,7 +62,7 @@ VALU_PEAK_TOPS = 1024 * 32 * 2.4e9 / 1e12  # 78.6 T lane-ops/s
 VALU_PK_TOPS = 1024 * 16 * 2.4e9 / 1e12
 N_PAIRS, LQ, LD = 100_000, 150, 150
 SEED = 0x5EED0002
-ALL_LEGS = ("c5", "c1", "c3", "c3_affine", "c4", "c4_spans", "host")
+ALL_LEGS = ("c5", "c1", "c3", "c3_affine", "c4", "c4_spans", "host", "cli")
 PMC_FILES = ("pmc_traffic.json", "pmc_legs.json")  # under profiles/
 
 
@@ -702,6 +704,80 @@ def leg_host(saln):
             "ms": round(dt * 1e3, 2)}
 
 
+def leg_cli(saln, n: int = 316, cpu: bool = True, max_blocks: int = 1) -> dict:
+    """The drop-in CLI end to end (`saln -q Q.fa -d D.fa -a needleman-wunsch`,
+    main.rs:19-80): n x n FASTA records of 150 bp G-iid (seed 0x5EED0002;
+    ~configs[1]'s 10^5 pairs), every pair computed once in render batches
+    (saln_nw_render_batch), each pair's reference text printed
+    (--max-blocks 1: the first block, so the stdout stays bounded; --no-abort:
+    every pair, where the reference would stop at the first panic;
+    --no-timing: no nondeterministic lines).  Wall time of the process,
+    FASTA parse and context creation included.  The first n pairs of stdout
+    are checked against the oracle's literal DFS text; the CPU baseline is
+    the oracle's fill + DFS (same block cap) on a sample of the pairs."""
+    import subprocess
+    import tempfile
+
+    from sequencealigning_amd import synth
+    cli = os.path.join(ROOT, "sequencealigning_amd", "saln")
+    qs, qo, ds, do = synth.iid_pairs(n, LQ, LD, seed=SEED)
+    q = [qs[int(qo[k]):int(qo[k + 1])].tobytes() for k in range(n)]
+    d = [ds[int(do[k]):int(do[k + 1])].tobytes() for k in range(n)]
+    with tempfile.TemporaryDirectory() as tdir:
+        qf, df, of = (os.path.join(tdir, x) for x in ("q.fa", "d.fa", "out.txt"))
+        for path, recs, tag in ((qf, q, "q"), (df, d, "d")):
+            with open(path, "wb") as fh:
+                for k, r in enumerate(recs):
+                    fh.write(b">%s%d\n%s\n" % (tag.encode(), k, r))
+        cmd = [cli, "-q", qf, "-d", df, "-a", "needleman-wunsch", "--no-timing", "--no-abort",
+               "--max-blocks", str(max_blocks)]
+        walls = []
+        for _ in range(2):  # the first run also pages in the library
+            with open(of, "wb") as out:
+                t0 = time.perf_counter()
+                r = subprocess.run(cmd, stdout=out, stderr=subprocess.PIPE, timeout=600)
+                walls.append(time.perf_counter() - t0)
+            if r.returncode != 0:
+                raise RuntimeError(f"saln exited {r.returncode}: {r.stderr[-500:]!r}")
+        with open(of, "rb") as fh:
+            head = fh.read(4 << 20).decode("latin-1")
+        out_bytes = os.path.getsize(of)
+    from oracle import refcpu  # untimed checker / cpu baseline only
+    want = "".join(refcpu.nw(a, d[0], max_blocks=max_blocks, max_pops=CPU_MAX_POPS).stdout
+                   for a in q)
+    cells = n * n * LQ * LD
+    res = {"workload": f"saln CLI (-a needleman-wunsch --no-timing --no-abort --max-blocks "
+                       f"{max_blocks}) on {n} x {n} FASTA records of 150 bp G-iid "
+                       f"({n * n} pairs, seed {SEED:#x})",
+           "value": round(cells / walls[-1] / 1e9, 2), "unit": "GCUPS (process wall time)",
+           "wall_s": round(walls[-1], 3), "wall_s_first": round(walls[0], 3),
+           "stdout_bytes": out_bytes,
+           "verified": {"pairs": n, "match": head.startswith(want),
+                        "checker": "oracle/refcpu.c literal DFS text, first db record x every "
+                                   "query (untimed)"}}
+    if cpu:
+        T = cpu_threads()
+        qb, db_ = qs.tobytes(), ds.tobytes()
+        # pairs (q_k, d_j) of the file, a seeded sample, on T threads
+        m = 4096
+        rng = np.random.default_rng(SEED)
+        qi, di = rng.integers(0, n, m), rng.integers(0, n, m)
+        sq = b"".join(q[i] for i in qi)
+        sd = b"".join(d[j] for j in di)
+        off = np.arange(m + 1, dtype=np.uint64) * LQ
+        t0 = time.perf_counter()
+        c, capped = refcpu.run_pairs_capped(sq, off, sd, off, m, max_pops=CPU_MAX_POPS,
+                                            threads=T, max_blocks=max_blocks)
+        dt = time.perf_counter() - t0
+        res["cpu_baseline"] = {"value": round(c / dt / 1e9, 5), "unit": "GCUPS", "cores": T,
+                               "kind": "port", "capped_pairs": int(capped),
+                               "sample": f"{m} seeded pairs of the file, oracle/refcpu.c fill + "
+                                         f"literal DFS stopped before block {max_blocks + 1} "
+                                         f"(<= {CPU_MAX_POPS:.0e} pops) on {T} threads, "
+                                         f"{dt:.1f} s (text not printed)"}
+    return res
+
+
 # --------------------------------------------------------------- launcher
 def launch_ranks(n: int) -> int:
     """Start n ranks of this command (torch.distributed.run, one process per
@@ -918,6 +994,8 @@ def main() -> None:
                 r = leg_c4_spans(torch, saln)
             elif leg == "host":
                 r = leg_host(saln)
+            elif leg == "cli":
+                r = leg_cli(saln, cpu=cpu)
             else:
                 raise ValueError(f"unknown leg {leg}")
         except Exception as e:  # a failing extra leg must not hide the headline line

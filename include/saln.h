@@ -240,6 +240,10 @@ int saln_nw_plan_set_async(saln_nw_plan *plan, int enable);
  * (end_states = printed = cigar_len = 0, flags bit 3 set). */
 int saln_nw_plan_set_score_only(saln_nw_plan *plan, int enable);
 int saln_nw_plan_sync(saln_nw_plan *plan, void *stream, int keep_latest);
+/* The stream a pipelined plan's tracebacks run on (NULL: the context's
+ * second stream), e.g. a CU-masked stream so that the walk of execute n and
+ * the fill of execute n+1 use disjoint CUs (tools/cu_pipeline.py). */
+int saln_nw_plan_set_tb_stream(saln_nw_plan *plan, void *stream);
 /* Device-side status of the plan's executes.  Waits (host-blocking) for every
  * execute issued since the previous call, then returns the device error
  * flags they raised (SALN_FLAG_*) in *flags (may be NULL) and clears them:
@@ -386,6 +390,16 @@ int saln_nw_spans_walk(saln_nw_span *const *spans, uint32_t n, const uint8_t *d_
 int saln_device_cu_count(saln_context *ctx, uint32_t *n);
 int saln_stream_create_cu_range(saln_context *ctx, uint32_t cu_lo, uint32_t cu_hi, void **stream);
 int saln_stream_destroy(saln_context *ctx, void *stream);
+/* A stream on an arbitrary CU mask (bit c of word c / 32 = CU c in the
+ * runtime's mask order, hipExtStreamCreateWithCUMask). */
+int saln_stream_create_cu_mask(saln_context *ctx, const uint32_t *mask, uint32_t n_words,
+                               void **stream);
+/* Diagnostic: launches n_blocks one-wave workgroups on `stream` (e.g. a
+ * CU-masked one) and returns, per workgroup, the HW_ID register of its wave
+ * (gfx9 layout: CU 11:8, SH 12, SE 15:13) and its XCC_ID (host arrays of
+ * n_blocks).  tools/cu_map.py derives the mask bit -> (XCD, SE, CU) order. */
+int saln_device_cu_probe(saln_context *ctx, void *stream, uint32_t n_blocks, uint32_t *hw_id,
+                         uint32_t *xcc_id);
 
 /* ----------------------------------------------------------------------- WFA
  * Replaces `pub fn wfa_align(seq1: &Record, seq2: &Record, mode: Mode)`

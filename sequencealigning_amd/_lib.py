@@ -94,6 +94,7 @@ EXPORTS = [
     "saln_nw_span_walk", "saln_nw_span_score", "saln_nw_span_status",
     "saln_nw_span_set_wait_limit", "saln_nw_span_destroy", "saln_nw_span_forward", "saln_nw_spans_walk",
     "saln_device_cu_count", "saln_stream_create_cu_range", "saln_stream_destroy",
+    "saln_device_cu_probe", "saln_nw_plan_set_tb_stream", "saln_stream_create_cu_mask",
     "saln_wfa_align_batch", "saln_wfa_render", "saln_wfa_plan_create", "saln_wfa_execute",
     "saln_wfa_plan_destroy",
     "saln_wfa_affine_batch", "saln_wfa_affine_plan_create", "saln_wfa_affine_execute",
@@ -201,6 +202,9 @@ def lib() -> C.CDLL:
         L.saln_device_cu_count.argtypes = [vp, u32p]
         L.saln_stream_create_cu_range.argtypes = [vp, C.c_uint32, C.c_uint32, C.POINTER(vp)]
         L.saln_stream_destroy.argtypes = [vp, vp]
+        L.saln_device_cu_probe.argtypes = [vp, vp, C.c_uint32, u32p, u32p]
+        L.saln_stream_create_cu_mask.argtypes = [vp, u32p, C.c_uint32, C.POINTER(vp)]
+        L.saln_nw_plan_set_tb_stream.argtypes = [vp, vp]
         L.saln_wfa_plan_create.argtypes = [vp, vp, C.c_uint64, vp, C.c_uint64, vp, vp,
                                            C.c_uint64, C.c_int32, C.c_uint32, C.c_uint32,
                                            C.POINTER(vp)]

@@ -72,6 +72,7 @@ struct saln_nw_plan {
     bool nib[kNumVariants] = {};  // variant stores 4-bit walk codes (Geom::LBn segments)
     bool score_only = false;  // no parent codes / traceback (saln_nw_plan_set_score_only)
     int buf = 0;                           // workspace of the next execute (async mode)
+    hipStream_t tb_stream = nullptr;       // traceback stream of async executes (NULL: ctx's)
     bool tb_pending[2] = {false, false};
     int last_buf = 0;
     uint64_t mask_bytes = 0;
@@ -587,7 +588,7 @@ int saln_nw_execute(saln_nw_plan *p, const uint8_t *d_q, const uint8_t *d_db,
     // the traceback stream: the second one only when a traceback can overlap a
     // fill (async plans, sub-batches); otherwise the same stream, so no
     // cross-stream hand-off sits between the fill and the walk
-    hipStream_t t = (p->async_tb || nsub > 1) ? p->ctx->tb_stream : s;
+    hipStream_t t = (p->async_tb || nsub > 1) ? (p->tb_stream ? p->tb_stream : p->ctx->tb_stream) : s;
     const int cur = p->async_tb ? p->buf : 0;
     uint8_t *mask = cur ? p->d_mask2 : p->d_mask;
     int32_t *endh = cur ? p->d_endh2 : p->d_endh;
@@ -702,6 +703,12 @@ int saln_nw_plan_set_async(saln_nw_plan *p, int enable) {
     }
     p->async_tb = enable != 0;
     p->buf = 0;
+    return SALN_OK;
+}
+
+int saln_nw_plan_set_tb_stream(saln_nw_plan *p, void *stream) {
+    if (!p) return SALN_E_INVALID;
+    p->tb_stream = (hipStream_t)stream;
     return SALN_OK;
 }
 

@@ -127,6 +127,7 @@ hipError_t launch_span_walk(const NwPairDesc *pairs, SpecArgs sa, const uint8_t 
                             Scoring sc, hipStream_t stream);
 hipError_t launch_span_watch(const int2 *col, uint32_t r0, uint32_t r1, uint32_t *err,
                              hipStream_t stream);
+hipError_t launch_cu_probe(uint32_t n_blocks, uint32_t *hw, uint32_t *xcc, hipStream_t stream);
 hipError_t launch_span_relay(const int2 *src, int2 *dst, uint32_t r0, uint32_t r1, uint32_t *err,
                              hipStream_t stream);
 hipError_t launch_span_spec(const NwPairDesc *pairs, SpecArgs sa, uint32_t n_blocks, int passes,

@@ -336,19 +336,14 @@ __device__ __forceinline__ void unroll_each(F &&f, std::integer_sequence<uint32_
 // column col is read at the bit nib_bit(col) of dword col / 8; the lookup
 // offsets become M 0 (argI, argD), I 1 (I-open), D 2 (D-open) instead of the
 // byte's 1 / 3 / 5, so the same kNextLut decides; the end cell's state set
-// comes from the end value's low bits; '=' / 'X' compare the query byte
-// (LDS) with the row's db char in the segment.
+// is its nibble's argI, argD and (last row) argM-in-D-open bits; '=' / 'X'
+// compare the query byte (LDS) with the row's db char in the segment.
 template <int G, int K, bool kNib = false>
 __device__ void walk_pack_lds(const NwPairDesc &p, int32_t hend, const uint8_t *__restrict__ mask,
                               uint32_t *__restrict__ ops_all, saln_nw_result *__restrict__ results,
                               uint32_t *__restrict__ cigar, Scoring sc, lds_u8 *win,
                               const uint8_t *__restrict__ qs) {
     using WG = WalkGeo<K, kNib, G * K>;
-    uint32_t es_nib = 0;
-    if constexpr (kNib) {
-        es_nib = (uint32_t)hend & 7u;
-        hend >>= 3;
-    }
     constexpr Geom geo{G, K};
     constexpr uint32_t kW = WG::W, NW = WG::NW;
     constexpr uint32_t kWin = WG::kWinBytes, kSlot = WG::kSlotBytes;
@@ -409,7 +404,10 @@ __device__ void walk_pack_lds(const NwPairDesc &p, int32_t hend, const uint8_t *
     auto nib_bit = [](uint32_t c) __attribute__((always_inline)) {
         return ((c & 4u) << 2) | ((c & 1u) << 3) | (c & 2u) << 1;
     };
-    const uint32_t fend = ~es_nib & 7u;  // kNib: the end cell's raw (absent) M, I, D bits
+    // kNib: the end cell's raw (absent) M, I, D bits from its nibble
+    auto end_bits = [](uint32_t n4) __attribute__((always_inline)) {
+        return ((n4 >> 3) & 1u) | ((n4 & 3u) << 1);
+    };
     uint32_t wl = wbase + wc * kWin;  // my slot 0 in the current window
     // the phase's row pointer (row ti at a phase start), W rows ahead for the refills
     // (row counts on after the lane's walk ends; rows below 1 load row 1)
@@ -504,7 +502,8 @@ __device__ void walk_pack_lds(const NwPairDesc &p, int32_t hend, const uint8_t *
                     uint32_t f3, eqb;
                     if constexpr (kNib) {
                         const uint32_t dw = pick(seg, col >> 3);
-                        f3 = sidx == 48u ? fend : __builtin_amdgcn_ubfe(dw, nib_bit(col) + lsh, 3);
+                        f3 = sidx == 48u ? end_bits(__builtin_amdgcn_ubfe(dw, nib_bit(col), 4))
+                                         : __builtin_amdgcn_ubfe(dw, nib_bit(col) + lsh, 3);
                         const uint32_t dch = __builtin_amdgcn_ubfe(pick(seg, kCB >> 2), (kCB & 3u) * 8u, 8);
                         eqb = qbyte(tj) == dch ? 1u : 0u;
                     } else {
@@ -609,8 +608,16 @@ __device__ void walk_pack_lds(const NwPairDesc &p, int32_t hend, const uint8_t *
         else ev = kEvDead;
     }
     // the reference's end states: the last row's codes are stored unfiltered
-    // (kNib: carried by the end value)
-    const uint32_t es = kNib ? es_nib : (m[geo.cell(p.len_db, p.len_q, rs, bs, cs)] ^ 0x7Fu) & 7u;
+    // (kNib: the end cell's nibble, argM in its D-open bit)
+    uint32_t es;
+    if constexpr (kNib) {
+        const uint32_t c = (p.len_q - 1) % K, b = (p.len_q - 1) / K;
+        const uint32_t w = *reinterpret_cast<const uint32_t *>(
+            m + (uint64_t)(p.len_db - 1) * rs + boff(b) + 4u * (c >> 3));
+        es = ~end_bits(__builtin_amdgcn_ubfe(w, nib_bit(c), 4)) & 7u;
+    } else {
+        es = (m[geo.cell(p.len_db, p.len_q, rs, bs, cs)] ^ 0x7Fu) & 7u;
+    }
     uint32_t nops = 0;
     bool retried = false;
     // (4-bit codes are written by the packed fills only: sentinel-free pairs,
@@ -1317,6 +1324,24 @@ template <int K>
 struct PkMask {
     uint32_t w[(K + 3) / 4];
 };
+// h[k] for a lane-varying k < K: a select tree over the bits of k (one
+// condition per level, ceil(log2 K) of them) instead of K compares, which
+// would each hold a lane mask (SGPR pressure, spills for K = 19).
+template <int K>
+__device__ __forceinline__ uint32_t pick_col(const uint32_t (&h)[K], int k) {
+    uint32_t v[K];
+#pragma unroll
+    for (int i = 0; i < K; ++i) v[i] = h[i];
+    int n = K;
+#pragma unroll
+    for (int bit = 0; (1 << bit) < K; ++bit) {
+        const bool b = (k >> bit) & 1;
+#pragma unroll
+        for (int i = 0; 2 * i < n; ++i) v[i] = 2 * i + 1 < n ? (b ? v[2 * i + 1] : v[2 * i]) : v[2 * i];
+        n = (n + 1) / 2;
+    }
+    return v[0];
+}
 // One pair's 4-bit walk-code segment of K columns (Geom::LBn bytes).
 template <int K>
 struct NibSeg {
@@ -1330,8 +1355,10 @@ struct NibSeg {
 // kCodesNib (round 4): 4-bit walk codes, two cells per byte - bit 0 argI,
 // 1 argD, 2 I-open, 3 D-open, each set when the parent is ABSENT - plus the
 // row's db char in the segment; no eq bit (the walker compares the query
-// byte, staged in LDS, with that char) and no argM: the end cell's state set
-// travels in the low 3 bits of the end value (value << 3 | set).  Layout of a
+// byte, staged in LDS, with that char).  The end cell's state set needs
+// argM: in a pair's last row the walker reads only I-open (a cell there is
+// entered from its right neighbour or is the end cell), so the end cell's
+// lane stores argM in the D-open bit of that row.  Layout of a
 // segment (Geom::LBn): the 4-column groups g = c / 4 as 16-bit halves, two
 // per dword, in each half the nibble of column c at bit 8 (c & 1) +
 // 4 ((c >> 1) & 1); then the db char at byte Geom::nib_char_byte.
@@ -1403,8 +1430,12 @@ __host__ __device__ inline int32_t rebase_center(const Scoring &sc, int32_t W) {
 
 // (Built for one wave per SIMD: at 124 VGPRs it runs 4; built for 5, 96
 // VGPRs, it spills 26 registers: C2 fill 0.97 -> 1.57 ms, round 1.)
+// The 8 x 19 fill with 4-bit codes needs ~183 VGPRs in its generic steps
+// (the steady loop ~126): built for 3 waves per SIMD instead of 2.
+template <int G, int K, int kCodes>
+constexpr int pk_min_waves() { return kCodes == 3 /* kCodesNib */ && G == 8 ? 3 : 1; }
 template <int G, int K, int kCodes, typename Src, int KS, bool kRebase = false>
-__global__ __launch_bounds__(256) void nw_fill_pk_kernel(Src src, uint32_t count,
+__global__ __launch_bounds__(256, (pk_min_waves<G, K, kCodes>())) void nw_fill_pk_kernel(Src src, uint32_t count,
                                                          const uint8_t *__restrict__ qs,
                                                          const uint8_t *__restrict__ ds,
                                                          uint8_t *__restrict__ mask, Scoring sc,
@@ -1563,10 +1594,11 @@ __global__ __launch_bounds__(256) void nw_fill_pk_kernel(Src src, uint32_t count
             uint32_t cw[(K + 1) / 2];
             uint32_t prv[8];  // sign sources of the previous (even) column
             // 4-bit codes: column-group words, the group's first column pair
-            // (low nibbles), the previous column's four sources, and the end
-            // cells' state sets
+            // (low nibbles), the previous column's four sources
             uint32_t nw[(K + 3) / 4], nlo = 0, nprv[4];
-            uint32_t esA = 0, esB = 0;
+            // kNib end-cell steps: the half (A low, B high) whose last row
+            // this lane computes now takes argM in its D-open bit
+            const uint32_t endsel = (t == tEA ? 0x0000FFFFu : 0u) | (t == tEB ? 0xFFFF0000u : 0u);
             // argM (bit 0) is only ever read at a pair's end cell: the wave
             // computes it on the steps where one of its lanes holds one.
             auto columns = [&](auto with_argm) __attribute__((always_inline)) {
@@ -1592,13 +1624,7 @@ __global__ __launch_bounds__(256) void nw_fill_pk_kernel(Src src, uint32_t count
                     s4[1] = psub(D, Hc);
                     s4[2] = psub(tOr, I);
                     s4[3] = psub(tOr, D);
-                    if constexpr (kM) {  // the end cells' state sets (present bits M, I, D)
-                        const uint32_t pM = ~psub(M, Hc), pI = ~s4[0], pD = ~s4[1];
-                        const uint32_t eA = ((pM >> 15) & 1u) | ((pI >> 14) & 2u) | ((pD >> 13) & 4u);
-                        const uint32_t eB = (pM >> 31) | ((pI >> 30) & 2u) | ((pD >> 29) & 4u);
-                        esA = k == kA ? eA : esA;
-                        esB = k == kB ? eB : esB;
-                    }
+                    if constexpr (kM) s4[3] = bfi(endsel, psub(M, Hc), s4[3]);
                     if (k % 2 == 0 && k < K - 1) {
 #pragma unroll
                         for (int u = 0; u < 4; ++u) nprv[u] = s4[u];
@@ -1727,20 +1753,12 @@ __global__ __launch_bounds__(256) void nw_fill_pk_kernel(Src src, uint32_t count
                 }
             }
             if (!kSteady && t == tEA) {
-                int32_t e = 0;
-#pragma unroll
-                for (int k = 0; k < K; ++k)
-                    if (k == kA) e = (int32_t)(Hout[k] & 0xFFFFu) - 32768;
-                const int32_t hv = e + base - alpha * ldA - beta * lqA;
-                src.end(ia, pa, kCodes == kCodesNib ? (int32_t)(((uint32_t)hv << 3) | esA) : hv);
+                const int32_t e = (int32_t)(pick_col<K>(Hout, kA) & 0xFFFFu) - 32768;
+                src.end(ia, pa, e + base - alpha * ldA - beta * lqA);
             }
             if (!kSteady && t == tEB) {
-                int32_t e = 0;
-#pragma unroll
-                for (int k = 0; k < K; ++k)
-                    if (k == kB) e = (int32_t)(Hout[k] >> 16) - 32768;
-                const int32_t hv = e + base - alpha * ldB - beta * lqB;
-                src.end(ib, pb, kCodes == kCodesNib ? (int32_t)(((uint32_t)hv << 3) | esB) : hv);
+                const int32_t e = (int32_t)(pick_col<K>(Hout, kB) >> 16) - 32768;
+                src.end(ib, pb, e + base - alpha * ldB - beta * lqB);
             }
         } else if (&Hout != &Hin) {
 #pragma unroll
@@ -2787,10 +2805,10 @@ static hipError_t fill_pk(dim3 grid, hipStream_t s, const NwPairDesc *pairs, uin
         if (codes == kCodesNone) return go(std::integral_constant<int, kCodesNone>{}, rebase_c);
         if (codes == kCodesNib) {  // the short-query variants (7: 16 x 10, 4: 8 x 19)
             if constexpr (G * K <= 160) return go(std::integral_constant<int, kCodesNib>{}, rebase_c);
-            return hipErrorInvalidValue;
+            else return hipErrorInvalidValue;
         }
         if constexpr (K > 16) return hipErrorInvalidValue;  // byte codes: 16-byte walker slots
-        return go(std::integral_constant<int, kCodesWalk>{}, rebase_c);
+        else return go(std::integral_constant<int, kCodesWalk>{}, rebase_c);
     };
     return rebase ? by_codes(std::true_type{}) : by_codes(std::false_type{});
 }
@@ -3162,6 +3180,27 @@ __global__ __launch_bounds__(64) void nw_span_relay_kernel(const int2 *__restric
         failed = __builtin_amdgcn_ballot_w64(failed) != 0;
     }
     if (failed && threadIdx.x == 0) atomicOr(err, 1u);
+}
+
+// Diagnostic (saln_device_cu_probe): where the waves of a launch run.  One
+// wave per workgroup records its HW_ID (gfx9 layout: wave 3:0, SIMD 5:4,
+// CU 11:8, SH 12, SE 15:13) and XCC_ID registers; vector stores only.
+__global__ __launch_bounds__(64) void nw_cu_probe_kernel(uint32_t *__restrict__ hw,
+                                                         uint32_t *__restrict__ xcc) {
+    const uint32_t h = __builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_REG_HW_ID
+    const uint32_t x = __builtin_amdgcn_s_getreg((31 << 11) | 20);  // HW_REG_XCC_ID
+    // keep the wave resident a while so a launch spreads over the CUs it may use
+    for (int k = 0; k < 64; ++k) __builtin_amdgcn_s_sleep(8);
+    if (threadIdx.x == 0) {
+        hw[blockIdx.x] = h;
+        xcc[blockIdx.x] = x;
+    }
+}
+
+hipError_t launch_cu_probe(uint32_t n_blocks, uint32_t *hw, uint32_t *xcc, hipStream_t stream) {
+    if (!n_blocks) return hipSuccess;
+    nw_cu_probe_kernel<<<dim3(n_blocks), dim3(64), 0, stream>>>(hw, xcc);
+    return hipGetLastError();
 }
 
 hipError_t launch_span_relay(const int2 *src, int2 *dst, uint32_t r0, uint32_t r1, uint32_t *err,

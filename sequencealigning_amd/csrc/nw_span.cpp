@@ -549,6 +549,34 @@ int saln_stream_create_cu_range(saln_context *ctx, uint32_t cu_lo, uint32_t cu_h
     return SALN_OK;
 }
 
+int saln_device_cu_probe(saln_context *ctx, void *stream, uint32_t n_blocks, uint32_t *hw_id,
+                         uint32_t *xcc_id) {
+    if (!ctx || !hw_id || !xcc_id || !n_blocks) return SALN_E_INVALID;
+    HIP_TRY(hipSetDevice(ctx->device));
+    uint32_t *d = nullptr;
+    HIP_TRY(dev_alloc(ctx, (void **)&d, 2ull * n_blocks * sizeof(uint32_t)));
+    hipStream_t st = resolve_stream(stream, ctx);
+    hipError_t e = launch_cu_probe(n_blocks, d, d + n_blocks, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e == hipSuccess) e = hipMemcpy(hw_id, d, n_blocks * sizeof(uint32_t), hipMemcpyDeviceToHost);
+    if (e == hipSuccess)
+        e = hipMemcpy(xcc_id, d + n_blocks, n_blocks * sizeof(uint32_t), hipMemcpyDeviceToHost);
+    (void)hipStreamSynchronize(st);
+    dev_free(ctx, d);
+    HIP_TRY(e);
+    return SALN_OK;
+}
+
+int saln_stream_create_cu_mask(saln_context *ctx, const uint32_t *mask, uint32_t n_words,
+                               void **stream) {
+    if (!ctx || !mask || !n_words || !stream) return SALN_E_INVALID;
+    HIP_TRY(hipSetDevice(ctx->device));
+    hipStream_t s = nullptr;
+    HIP_TRY(hipExtStreamCreateWithCUMask(&s, n_words, mask));
+    *stream = s;
+    return SALN_OK;
+}
+
 int saln_stream_destroy(saln_context *ctx, void *stream) {
     if (!ctx || !stream) return SALN_E_INVALID;
     HIP_TRY(hipSetDevice(ctx->device));

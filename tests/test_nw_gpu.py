@@ -161,6 +161,58 @@ def test_c2_scale_properties(saln, oracle):
     plan.close()
 
 
+@pytest.mark.parametrize("nib,narrow", [(0, 0), (1, 0), (1, 1)])
+def test_walk_code_formats_match_oracle(saln, oracle, saln_opt, nib, narrow):
+    """The three walk-code layouts of the short-query packed fills give the
+    oracle's results: byte codes (nw.nib_codes = 0, round 3), 4-bit codes in
+    16 x 10 groups (the default) and 4-bit codes in 8 x 19 groups
+    (nw.narrow_walk = 1: queries of <= 152 columns).  20,000 configs[1]
+    pairs (score, end states, panic, printed, CIGAR word for word) and a
+    ragged batch: 1..160-column queries, dbs up to 1,200 rows (the rebasing
+    int16 frame), identical and two-letter pairs."""
+    import torch
+    from sequencealigning_amd import synth
+    saln_opt("nw.nib_codes", nib)
+    saln_opt("nw.narrow_walk", narrow)
+    n, L = 20_000, 150
+    qs, qo, ds, do = synth.iid_pairs(n, L, L, seed=0x5EED0002)
+    plan = saln.NwPlan(qo, do, pairs=np.stack([np.arange(n), np.arange(n)], 1))
+    dq, dd = torch.from_numpy(qs).cuda(), torch.from_numpy(ds).cuda()
+    res_t = torch.zeros(n * 4, dtype=torch.int32, device="cuda")
+    cig_t = torch.zeros(max(1, plan.cigar_words), dtype=torch.int32, device="cuda")
+    plan.execute(dq, dd, res_t, cig_t)
+    torch.cuda.synchronize()
+    plan.check()
+    res = res_t.cpu().numpy().view(saln._lib.RESULT_DTYPE)
+    cig = cig_t.cpu().numpy().view(np.uint32)
+    want = oracle.check_pairs(qs, qo, ds, do)
+    assert np.array_equal(res["score"], want.score)
+    assert np.array_equal(res["end_states"], want.end_states)
+    assert np.array_equal(res["status"] == saln._lib.REF_PANIC_BOUNDARY, want.panics)
+    assert np.array_equal(res["printed"].astype(bool), want.cig_len >= 0)
+    for k in range(n):
+        if res["printed"][k]:
+            o0 = int(plan.cigar_off[k])
+            assert np.array_equal(cig[o0:o0 + int(res["cigar_len"][k])], want.cigar_words(k)), k
+    plan.close()
+    rng = np.random.default_rng(4040 + 2 * nib + narrow)
+    queries, dbs = [], []
+    for lq, ld in [(1, 1), (1, 40), (9, 3), (19, 19), (20, 150), (38, 900), (151, 151),
+                   (152, 152), (152, 1200), (153, 160), (160, 400), (140, 1200), (75, 5)]:
+        queries.append(rand_seq(rng, lq))
+        dbs.append(rand_seq(rng, ld))
+    base = rand_seq(rng, 152)
+    queries += [base, bytes(rng.choice([65, 67], 150).astype(np.uint8))]
+    dbs += [base, bytes(rng.choice([65, 67], 147).astype(np.uint8))]
+    m = len(queries)
+    res, cg = saln.nw_align_batch(queries, dbs, pairs=[(k, k) for k in range(m)])
+    for k in range(m):
+        o = oracle.nw(queries[k], dbs[k], literal_dfs=False)
+        assert (int(res["score"][k]), int(res["end_states"][k]), int(res["status"][k]) == 2) == \
+            (o.score, o.end_states, o.panics), (k, len(queries[k]), len(dbs[k]))
+        assert (saln.cigar_ops_string(cg[k]) if res["printed"][k] else None) == o.first_ops, k
+
+
 def test_pipelined_plan_matches_sync(saln):
     """saln_nw_plan_set_async: tracebacks overlap the next fill through two
     mask workspaces; five pipelined executes (ragged lengths, several

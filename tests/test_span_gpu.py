@@ -124,10 +124,11 @@ def test_span_injected_timeout_raises():
 
 def test_span_relay_wait_limit_bounds_each_row():
     """The single-device relay (saln_nw_span_forward) under a small nonzero
-    wait limit: its source rows arrive in 64-row batches ~1 ms apart for ~60
-    ms, so the relay spends far more polls in total than the limit allows
-    one wait, but no single row waits long.  The limit bounds each row's
-    wait: every row is forwarded, no timeout is flagged."""
+    wait limit: its source rows arrive in 64-row batches ~5 ms apart for
+    ~0.3 s, so the relay polls far longer in total than the limit allows one
+    wait (2^17 polls: ~13-130 ms at 0.1-1 us a poll), but no single row waits
+    long.  The limit bounds each row's wait: every row is
+    forwarded, no timeout is flagged."""
     import time
 
     import torch
@@ -140,15 +141,22 @@ def test_span_relay_wait_limit_bounds_each_row():
     a.reset()
     b.reset()
     torch.cuda.synchronize()
-    a.set_wait_limit(8192)  # ~10 ms of polling per wait, << the ~60 ms the rows take
+    a.set_wait_limit(1 << 17)
+    vals = torch.arange(1, R + 1, dtype=torch.int64, device="cuda") * 3 + 7
+    torch.cuda.synchronize()
     side = torch.cuda.Stream()
     _lib.check(_lib.lib().saln_nw_span_forward(a._h, b._h, 1, R, side.cuda_stream),
                "saln_nw_span_forward")
-    vals = torch.arange(1, R + 1, dtype=torch.int64, device="cuda") * 3 + 7
-    for lo in range(1, R + 1, 64):
-        time.sleep(0.001)
-        a.outbox[lo:lo + 64].copy_(vals[lo - 1:lo + 63])
+    # the writes go on a stream of their own (the null stream could wait for
+    # the relay), and nothing here synchronizes the device before they are in
+    writer = torch.cuda.Stream()
+    t0 = time.perf_counter()
+    with torch.cuda.stream(writer):
+        for lo in range(1, R + 1, 64):
+            time.sleep(0.005)
+            a.outbox[lo:lo + 64].copy_(vals[lo - 1:lo + 63])
     side.synchronize()
+    assert time.perf_counter() - t0 > 0.25  # the relay polled for the whole run
     torch.cuda.synchronize()
     assert a.status() == 0  # no wait gave up
     assert torch.equal(b.inbox[1:R + 1], vals)

@@ -1,0 +1,57 @@
+#!/bin/bash
+# Round-4 GPU steps.  STAGES (space-separated, default "smoke tests bench"):
+#   ab       A/B of the walk-code formats on the configs[1] step (tools/ab_c2.py;
+#            AB= "tag:opts,..." overrides; REPS alternations)
+#   cumap    tools/cu_map.py -> $O/cu_map.json
+#   pipe     tools/cu_pipeline.py over walk-CU counts / layouts (PIPE_CASES)
+#   pipetrace  rocprofv3 --kernel-trace of one pipeline case (PIPE_TRACE args)
+#   smoke    __graft_entry__.smoke()
+#   tests    pytest -m gpu (TESTS= narrows it)
+#   bench    bench.py --steps 20 --warmup 3 (BENCH_ARGS= extra args)
+#   prof     rocprofv3 --kernel-trace --stats of the headline command
+#   proflegs the same over tools/prof_legs.py
+#   pmc      PMC passes (tools/pmc.sh) of the headline workload -> pmc_traffic.json
+#   pmclegs  PMC passes over tools/prof_legs.py -> pmc_legs.json
+# Every GPU step has its own time limit; the script stops at the first failure.
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+export TMPDIR=/tmp
+O=gpurun_out/r04
+mkdir -p $O
+step() { local name=$1 lim=$2; shift 2; echo "[$(date +%T)] $name"; timeout -k 10 $lim "$@" > $O/$name.log 2>&1 || { echo "$name failed rc=$?"; tail -40 $O/$name.log; exit 1; }; }
+for st in ${STAGES:-smoke tests bench}; do
+  case $st in
+    ab)
+      for i in ${REPS:-1 2 3}; do
+        for spec in ${AB:-byte:nw.nib_codes=0 nib16x10: nib8x19:nw.narrow_walk=1}; do
+          tag=${spec%%:*}; opts=${spec#*:}; args=""
+          for o in ${opts//,/ }; do args="$args --opt $o"; done
+          step ab_${tag}_$i 120 python tools/ab_c2.py --tag $tag $args
+          tail -1 $O/ab_${tag}_$i.log
+        done
+      done ;;
+    cumap) step cumap 300 python tools/cu_map.py --out $O/cu_map.json
+           tail -1 $O/cumap.log | cut -c1-1500 ;;
+    pipe)
+      for c in ${PIPE_CASES:-"-1" "0" "32 contiguous" "32 balanced" "64 balanced" "16 balanced" "48 balanced"}; do
+        set -- $c
+        step pipe_$1_${2:-x} 120 python tools/cu_pipeline.py --walk-cus $1 --layout ${2:-balanced} --map $O/cu_map.json
+        tail -1 $O/pipe_$1_${2:-x}.log
+      done ;;
+    pipetrace) step pipetrace 300 rocprofv3 --kernel-trace -d $O/pipetrace -o run --output-format csv -- python3 tools/cu_pipeline.py ${PIPE_TRACE:---walk-cus 32 --layout balanced --steps 10 --warmup 2} --map $O/cu_map.json
+               python3 tools/trace_overlap.py $O/pipetrace --out $O/pipe_overlap.json || exit 1 ;;
+    smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    tests) step tests 1100 python -u -m pytest ${TESTS:-tests} -m gpu -x -q --timeout 300 --timeout-method thread
+           tail -3 $O/tests.log ;;
+    bench) step bench 900 python bench.py --steps 20 --warmup 3 $BENCH_ARGS
+           tail -1 $O/bench.log | cut -c1-1500 ;;
+    prof)  step prof_c2 600 rocprofv3 --kernel-trace --stats -d $O/prof_c2 -o run --output-format csv -- python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline --legs none ;;
+    proflegs) step prof_legs 900 rocprofv3 --kernel-trace --stats -d $O/prof_legs -o run --output-format csv -- python3 tools/prof_legs.py --legs ${PROF_LEGS:-c1,c3,c3_affine,c4,c5} ;;
+    pmc)   PMC_SETS=${PMC_SETS:-"FETCH_SIZE;WRITE_SIZE;SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU;SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU"} step pmc 900 bash tools/pmc.sh
+           python3 tools/pmc_traffic.py gpurun_out/pmc $O/pmc_traffic.json r04 nw > /dev/null || exit 1 ;;
+    pmclegs) PMC_SCRIPT=tools/prof_legs.py PMC_SETS=${PMC_SETS:-"FETCH_SIZE;WRITE_SIZE;SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU"} step pmc_legs 1100 bash tools/pmc.sh --legs ${PROF_LEGS:-c1,c3,c3_affine,c4,c5}
+           python3 tools/pmc_traffic.py gpurun_out/pmc $O/pmc_legs.json r04 legs > /dev/null || exit 1 ;;
+    *) echo "unknown stage $st"; exit 2 ;;
+  esac
+done
+echo done
