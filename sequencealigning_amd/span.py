@@ -404,7 +404,9 @@ def nw_align_long_spans(q: bytes, d: bytes, n_spans: int, *, scoring=None, devic
 
 
 class _DeviceSpanEngine:
-    """ShardedLongPair's per-rank engine on this rank's GPU."""
+    """ShardedLongPair's per-rank engine on this rank's GPU.  Three streams of
+    its own: the fill, the inbox copies of the band relay, and the watches
+    with what reads the outbox behind them (sends, D2H copies)."""
 
     def __init__(self, q: bytes, d: bytes, col_lo: int, col_hi: int, scoring, device: int):
         import torch
@@ -414,25 +416,59 @@ class _DeviceSpanEngine:
         self.d = torch.frombuffer(bytearray(d), dtype=torch.uint8).to(dev)
         self.span = NwSpan(len(q), len(d), col_lo, col_hi, scoring=scoring, device=device)
         self.side = torch.cuda.Stream(device=dev)
+        self.fill_s = torch.cuda.Stream(device=dev)
+        self.in_s = torch.cuda.Stream(device=dev)
 
-    # relay transport: whole inbox in, then the fill
-    def fill(self, inbox_host=None) -> None:
+    def reset(self) -> None:
+        """Presets the boundary columns; every later stream of the pair
+        (fill, inbox copies, watches) is ordered after it."""
         import torch
-        main = torch.cuda.current_stream(self.device)
-        self.span.reset(main)
+        self.span.reset(self.fill_s)
         ev = torch.cuda.Event()
-        ev.record(main)
-        self.side.wait_event(ev)  # the watches poll the outbox after its reset
-        if inbox_host is not None:
-            self.span.inbox[1:len(inbox_host) + 1].copy_(torch.from_numpy(inbox_host))
-        self.span.fill(self.q, self.d, main)
+        ev.record(self.fill_s)
+        self.side.wait_event(ev)
+        self.in_s.wait_event(ev)
+        # RCCL receives into the inbox are ordered after the current stream
+        torch.cuda.current_stream(self.device).wait_event(ev)
+
+    def launch_fill(self) -> None:
+        self.span.fill(self.q, self.d, self.fill_s)
+
+    # band relay (gloo): the fill starts first and polls its inbox row by row
+    def start_fill(self) -> None:
+        self.reset()
+        self.launch_fill()
+
+    def put_inbox(self, a: int, b: int, rows: np.ndarray) -> None:
+        """Inbox rows a .. b from host memory (H2D on the inbox stream, beside
+        the running fill)."""
+        import torch
+        src = torch.from_numpy(np.ascontiguousarray(rows, np.int64)).pin_memory()
+        with torch.cuda.stream(self.in_s):
+            self.span.inbox[a:b + 1].copy_(src, non_blocking=True)
+        self.in_s.synchronize()  # `src` lives until the copy is done
 
     def outbox_rows(self, a: int, b: int) -> np.ndarray:
+        """Outbox rows a .. b once the fill has published them (watch, then D2H)."""
         import torch
         with torch.cuda.stream(self.side):
             self.span.watch(a, b, self.side)
             out = self.span.outbox[a:b + 1].to("cpu", non_blocking=False)
         return out.numpy()
+
+    # RCCL transport: views and the side stream the sends are queued on
+    def inbox_view(self, a: int, b: int):
+        return self.span.inbox[a:b + 1]
+
+    def watch_outbox(self, a: int, b: int):
+        """Queues the watch of rows a .. b on the side stream; returns their
+        outbox view (for a send queued after it, inside side_stream())."""
+        self.span.watch(a, b, self.side)
+        return self.span.outbox[a:b + 1]
+
+    def side_stream(self):
+        import torch
+        return torch.cuda.stream(self.side)
 
     def finish(self) -> None:
         import torch
@@ -471,12 +507,19 @@ class ShardedLongPair:
     CIGAR: saln_nw_align's for the same pair) and None elsewhere.
 
     ``engine`` (tests) replaces the device span: engine(q, d, col_lo, col_hi)
-    with ``fill(inbox or None)``, ``outbox_rows(a, b)`` (int64 rows a..b),
-    ``finish()``, ``walk(entry) -> (exit, ops)``, ``score()`` and
-    ``close()``; it runs on the relay transport."""
+    with ``start_fill()``, ``put_inbox(a, b, rows)``, ``outbox_rows(a, b)``
+    (int64 rows a..b), ``finish()``, ``walk(entry) -> (exit, ops)``,
+    ``score()`` and ``close()``; it runs on the band relay (gloo).  The RCCL
+    path drives the engine through ``reset()``, ``inbox_view(a, b)``,
+    ``launch_fill()``, ``watch_outbox(a, b)``, ``side_stream()`` and
+    ``finish()`` (``nccl=True`` with an engine: tests of its enqueue order).
+
+    Both transports move the boundary in bands of ``band_rows`` rows while the
+    fills run: rank r receives band k, then sends its own band k, so a band
+    only waits for the bands before it (no cycle between the ranks)."""
 
     def __init__(self, q: bytes, d: bytes, *, scoring=None, device: int | None = None,
-                 band_rows: int = 4096, engine=None):
+                 band_rows: int = 4096, engine=None, nccl: bool | None = None):
         import torch
         import torch.distributed as dist
         self.world, self.rank = dist.get_world_size(), dist.get_rank()
@@ -485,7 +528,7 @@ class ShardedLongPair:
         self.bands = _bands(self.len_db, band_rows)
         lo, hi = self.cols[self.rank]
         backend = dist.get_backend()
-        self.nccl = engine is None and backend == "nccl"
+        self.nccl = (engine is None and backend == "nccl") if nccl is None else nccl
         if engine is None:
             dev = torch.cuda.current_device() if device is None else device
             self.engine = _DeviceSpanEngine(q, d, lo, hi, scoring, dev)
@@ -502,46 +545,43 @@ class ShardedLongPair:
         self.right = self.edges[self.rank] if self.rank + 1 < self.world else None
 
     def _fill_nccl(self) -> None:
-        import torch
+        """RCCL: every band's receive is posted first (queued behind the reset
+        only), then the fill that polls them, then per band a watch and the
+        send queued behind it on the side stream.  Each kernel is queued after
+        the work it waits for, so streams sharing a hardware queue can only
+        serialise the pipeline, never deadlock it."""
         import torch.distributed as dist
-        eng, sp = self.engine, self.engine.span
-        main = torch.cuda.current_stream(eng.device)
-        sp.reset(main)
+        eng = self.engine
+        eng.reset()
         works = []
-        # receives first (queued behind the reset only), then the fill that
-        # polls them, then the watches and sends that wait for the fill
         if self.left is not None:
             for a, b in self.bands:
-                works.append(dist.irecv(sp.inbox[a:b + 1], src=self.rank - 1, group=self.left))
-        ev = torch.cuda.Event()
-        ev.record(main)
-        sp.fill(eng.q, eng.d, main)
+                works.append(dist.irecv(eng.inbox_view(a, b), src=self.rank - 1, group=self.left))
+        eng.launch_fill()
         if self.right is not None:
-            eng.side.wait_event(ev)
-            with torch.cuda.stream(eng.side):
+            with eng.side_stream():
                 for a, b in self.bands:
-                    sp.watch(a, b, eng.side)
-                    works.append(dist.isend(sp.outbox[a:b + 1], dst=self.rank + 1,
-                                            group=self.right))
+                    buf = eng.watch_outbox(a, b)
+                    works.append(dist.isend(buf, dst=self.rank + 1, group=self.right))
         for w in works:
             w.wait()
-        main.wait_stream(eng.side)
         eng.finish()
 
     def _fill_relay(self) -> None:
+        """gloo: the same band pipeline through host memory.  The fill starts
+        at once and polls its inbox; per band, receive it from the left and
+        copy it in (H2D), then wait for the own outbox band (watch), copy it
+        out (D2H) and send it to the right."""
         import torch
         import torch.distributed as dist
         eng = self.engine
-        inbox = None
-        if self.left is not None:
-            inbox = np.zeros(self.len_db, np.int64)
-            for a, b in self.bands:
+        eng.start_fill()
+        for a, b in self.bands:
+            if self.left is not None:
                 t = torch.empty(b - a + 1, dtype=torch.int64)
                 dist.recv(t, src=self.rank - 1, group=self.left)
-                inbox[a - 1:b] = t.numpy()
-        eng.fill(inbox)
-        if self.right is not None:
-            for a, b in self.bands:
+                eng.put_inbox(a, b, t.numpy())
+            if self.right is not None:
                 t = torch.from_numpy(np.ascontiguousarray(eng.outbox_rows(a, b), np.int64))
                 dist.send(t, dst=self.rank + 1, group=self.right)
         eng.finish()

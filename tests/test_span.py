@@ -36,6 +36,31 @@ class _CpuSpanEngine:
         self.lq, self.ld, self.lo, self.hi = len(q), len(d), lo, hi
         self.m, self.x, self.go, self.ge = scoring
         self.out = None
+        self.inbox = None
+        self.have = 0  # inbox rows delivered (band relay)
+
+    # band relay: the fill "runs" row by row as far as its inbox allows; a
+    # request for outbox rows past the delivered inbox is a protocol error
+    def start_fill(self):
+        self.inbox = np.zeros(self.ld, np.int64)
+        self.have = 0 if self.lo > 0 else self.ld
+        self.out = None
+
+    def put_inbox(self, a, b, rows):
+        assert a == self.have + 1, ("bands out of order", a, self.have)
+        self.inbox[a - 1:b] = rows
+        self.have = b
+
+    def outbox_rows(self, a, b):
+        assert self.have >= b, ("outbox rows requested before their inbox rows", b, self.have)
+        if self.out is None and self.have == self.ld:
+            self.fill(self.inbox if self.lo > 0 else None)
+        if self.out is None:  # partial: rows 1 .. b from the rows delivered so far
+            part = _CpuSpanEngine(bytes(self.q.astype(np.uint8)), bytes(self.d[:b].astype(np.uint8)),
+                                  self.lo, self.hi, (self.m, self.x, self.go, self.ge))
+            part.fill(self.inbox[:b] if self.lo > 0 else None)
+            return part.out[a - 1:b]
+        return self.out[a - 1:b]
 
     def d_row0(self, j):
         return (j + 1) * self.ge + self.go
@@ -79,11 +104,10 @@ class _CpuSpanEngine:
         ir = np.maximum(M[1:, -1] + go2, I[1:, -1]) + ge2
         self.out = (hr & 0xFFFFFFFF) | (ir << 32)
 
-    def outbox_rows(self, a, b):
-        return self.out[a - 1:b]
-
     def finish(self):
-        pass
+        if self.out is None:
+            assert self.have == self.ld
+            self.fill(self.inbox if self.lo > 0 else None)
 
     def close(self):
         pass
@@ -286,3 +310,82 @@ def test_span_columns_and_merge():
     # dead-end order of the end states: D, M, I
     assert S.first_end_state(7) == S.SPAN_D and S.end_states_after(7, S.SPAN_D) == 3
     assert S.end_states_after(3, S.SPAN_M) == 2 and S.end_states_after(2, S.SPAN_I) == 0
+
+
+class _Recorder:
+    """Recording fake of the RCCL path: engine calls and dist.irecv / isend
+    go into one log, in the order ShardedLongPair._fill_nccl issues them."""
+
+    def __init__(self, log):
+        self.log = log
+
+    def reset(self):
+        self.log.append(("reset",))
+
+    def inbox_view(self, a, b):
+        return ("inbox", a, b)
+
+    def launch_fill(self):
+        self.log.append(("fill",))
+
+    def watch_outbox(self, a, b):
+        self.log.append(("watch", a, b))
+        return ("outbox", a, b)
+
+    def side_stream(self):
+        log = self.log
+
+        class _Ctx:
+            def __enter__(self):
+                log.append(("side+",))
+
+            def __exit__(self, *e):
+                log.append(("side-",))
+        return _Ctx()
+
+    def finish(self):
+        self.log.append(("finish",))
+
+
+def test_nccl_band_pipeline_enqueue_order(monkeypatch):
+    """ShardedLongPair's RCCL path at world 3 (each rank driven in turn with a
+    recording engine and recording irecv / isend): every band's receive is
+    posted before the fill, the fill before any watch, each send right after
+    the watch of its band and inside the side stream, and the end rank posts
+    no sends / the first no receives."""
+    import torch.distributed as dist
+
+    from sequencealigning_amd import span as S
+
+    class _Work:
+        def wait(self):
+            pass
+    world, ld, band = 3, 1000, 256
+    bands = S._bands(ld, band)
+    assert bands[0] == (1, 256) and bands[-1] == (769, 1000)
+    for rank in range(world):
+        log = []
+        monkeypatch.setattr(dist, "irecv", lambda t, src, group: log.append(("irecv", t, src)) or _Work())
+        monkeypatch.setattr(dist, "isend", lambda t, dst, group: log.append(("isend", t, dst)) or _Work())
+        sp = object.__new__(S.ShardedLongPair)
+        sp.world, sp.rank, sp.bands, sp.nccl = world, rank, bands, True
+        sp.left = "L" if rank > 0 else None
+        sp.right = "R" if rank + 1 < world else None
+        sp.engine = _Recorder(log)
+        sp._fill_nccl()
+        kinds = [e[0] for e in log]
+        assert kinds[0] == "reset" and kinds[-1] == "finish"
+        fill = kinds.index("fill")
+        recvs = [i for i, k in enumerate(kinds) if k == "irecv"]
+        assert len(recvs) == (len(bands) if rank > 0 else 0)
+        assert all(i < fill for i in recvs)
+        assert [log[i][1] for i in recvs] == ([("inbox", a, b) for a, b in bands] if rank else [])
+        assert all(log[i][2] == rank - 1 for i in recvs)
+        sends = [i for i, k in enumerate(kinds) if k == "isend"]
+        assert len(sends) == (len(bands) if rank + 1 < world else 0)
+        for (a, b), i in zip(bands, sends):
+            assert log[i - 1] == ("watch", a, b) and log[i][1] == ("outbox", a, b) and i > fill
+            assert log[i][2] == rank + 1
+        if sends:
+            side_on, side_off = kinds.index("side+"), kinds.index("side-")
+            assert side_on < sends[0] and sends[-1] < side_off and fill < side_on
