@@ -25,7 +25,7 @@ const OptDesc kDesc[kN] = {
     {"nw.spec_strict", 0, 0, 1},
     {"nw.avsa_narrow", 1, 0, 1},
     {"nw.nib_codes", 1, 0, 1},
-    {"nw.narrow_walk", 0, 0, 1},
+    {"nw.narrow_walk", 1, 0, 1},
     {"wfa2.seq_lds", 24 * 1024, 0, 64 * 1024},
     {"wfa2.w1", 0, 0, 4096},
     {"wfa2.w2", 0, 0, 4096},

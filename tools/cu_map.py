@@ -44,23 +44,32 @@ def main():
     for c in range(ncu):
         h = C.c_void_p()
         _lib.check(L.saln_stream_create_cu_range(ctx, c, c + 1, C.byref(h)), "cu_range")
-        w = probe(L, ctx, h, 8)
+        w = probe(L, ctx, h, 64)  # 64 waves: more than one per XCD if the bit allows it
         L.saln_stream_destroy(ctx, h)
         places = {(x["xcd"], x["se"], x["sh"], x["cu"]) for x in w}
         bits.append({"bit": c, "places": sorted(places)})
-    whole = probe(L, ctx, None, 2048)
+    whole = probe(L, ctx, None, 4096)
     xcds_whole = sorted({x["xcd"] for x in whole})
+    cus_whole = len({(x["xcd"], x["se"], x["sh"], x["cu"]) for x in whole})
 
-    def cover(sel):
-        pl = [p for c in sel for p in bits[c]["places"]]
-        return {"xcds": len({p[0] for p in pl}), "xcd_se": len({(p[0], p[1]) for p in pl})}
+    def measured(lo, hi, n=2048):
+        h = C.c_void_p()
+        _lib.check(L.saln_stream_create_cu_range(ctx, lo, hi, C.byref(h)), "cu_range")
+        w = probe(L, ctx, h, n)
+        L.saln_stream_destroy(ctx, h)
+        pl = {(x["xcd"], x["se"], x["sh"], x["cu"]) for x in w}
+        return {"cus": len(pl), "xcds": len({p[0] for p in pl}),
+                "xcd_se": len({(p[0], p[1]) for p in pl}),
+                "per_xcd": [sum(1 for p in pl if p[0] == x) for x in range(8)]}
 
-    ranges = {f"[0,{k})": cover(range(k)) for k in (8, 16, 32, 48, 64, 128)}
-    ranges.update({f"[{ncu - k},{ncu})": cover(range(ncu - k, ncu)) for k in (16, 32, 64)})
+    ranges = {f"[0,{k})": measured(0, k) for k in (1, 8, 16, 32, 48, 64, 128)}
+    ranges.update({f"[{ncu - k},{ncu})": measured(ncu - k, ncu) for k in (16, 32, 64)})
+    ranges["[0,256) unmasked probe"] = {"cus": cus_whole}
     doc = {"cu_count": ncu, "xcds_unmasked": xcds_whole, "bits": bits, "ranges": ranges,
            "single_place_bits": sum(len(b["places"]) == 1 for b in bits)}
     print(json.dumps({"cu_count": ncu, "xcds_unmasked": xcds_whole, "ranges": ranges,
-                      "first_bits": [(b["bit"], b["places"]) for b in bits[:20]]}))
+                      "places_per_bit": sorted({len(b["places"]) for b in bits}),
+                      "first_bits": [(b["bit"], b["places"]) for b in bits[:4]]}))
     if a.out:
         with open(a.out, "w") as f:
             json.dump(doc, f, indent=1)
