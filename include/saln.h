@@ -444,6 +444,25 @@ int saln_wfa_render(saln_context *ctx, const uint8_t *q, uint64_t len_q, const u
                     uint64_t len_db, int32_t mode, uint32_t max_steps, uint32_t max_width,
                     char *out, uint64_t cap, uint64_t *out_len, saln_wfa_result *result);
 
+/* The same text for every pair of a batch (pair conventions as
+ * saln_wfa_align_batch), each pair computed once: one GPU run of the batch
+ * with its step logs and alignment rows, then host rendering.  Replaces the
+ * size-probe + render pair of saln_wfa_render calls per pair that the pair
+ * loop main.rs:61-74 would otherwise make.  Rows are sized for the batch's
+ * longest pair; a batch whose rows exceed 16 GB is refused (split it). */
+typedef struct saln_wfa_text saln_wfa_text;
+int saln_wfa_render_batch(saln_context *ctx, const uint8_t *q_seq, const uint64_t *q_off,
+                          uint64_t n_q, const uint8_t *db_seq, const uint64_t *db_off,
+                          uint64_t n_db, const uint32_t *pair_q, const uint32_t *pair_db,
+                          uint64_t n_pairs, int32_t mode, uint32_t max_steps, uint32_t max_width,
+                          saln_wfa_text **out);
+uint64_t saln_wfa_text_count(const saln_wfa_text *t);
+/* text points into the handle (not NUL-terminated; len bytes), valid until
+ * saln_wfa_text_free. */
+int saln_wfa_text_get(const saln_wfa_text *t, uint64_t pair, const char **text, uint64_t *len,
+                      saln_wfa_result *result);
+void saln_wfa_text_free(saln_wfa_text *t);
+
 /* Device-resident WFA batch (configs[2] / C3 measurement): plan once from host
  * offsets and a pair list (NULL = all-vs-all, reference order), then execute
  * on device sequences (same CSR layout) into device results[n_pairs].  No

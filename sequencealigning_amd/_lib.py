@@ -104,6 +104,7 @@ EXPORTS = [
     "saln_option_set", "saln_option_get", "saln_option_name", "saln_options_reset",
     "saln_nw_render_batch", "saln_nw_render_text", "saln_nw_text_count", "saln_nw_text_get",
     "saln_nw_text_free",
+    "saln_wfa_render_batch", "saln_wfa_text_count", "saln_wfa_text_get", "saln_wfa_text_free",
 ]
 
 _lib = None
@@ -242,6 +243,15 @@ def lib() -> C.CDLL:
                                        C.POINTER(NwResult), u64p]
         L.saln_nw_text_free.argtypes = [vp]
         L.saln_nw_text_free.restype = None
+        L.saln_wfa_render_batch.argtypes = [vp, vp, vp, C.c_uint64, vp, vp, C.c_uint64, vp, vp,
+                                            C.c_uint64, C.c_int32, C.c_uint32, C.c_uint32,
+                                            C.POINTER(vp)]
+        L.saln_wfa_text_count.argtypes = [vp]
+        L.saln_wfa_text_count.restype = C.c_uint64
+        L.saln_wfa_text_get.argtypes = [vp, C.c_uint64, C.POINTER(vp), u64p,
+                                        C.POINTER(WfaResult)]
+        L.saln_wfa_text_free.argtypes = [vp]
+        L.saln_wfa_text_free.restype = None
         L.saln_option_set.argtypes = [C.c_char_p, C.c_int64]
         L.saln_option_get.argtypes = [C.c_char_p, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]
         L.saln_option_name.argtypes = [C.c_uint32, C.POINTER(C.c_char_p)]

@@ -13,6 +13,7 @@
 // where the reference would not terminate; a reference panic (boundary index panic of the
 // NW traceback) aborts with exit code 101 after the blocks printed before it,
 // like the reference, unless --no-abort is given.
+#include <algorithm>
 #include <chrono>
 #include <cstdint>
 #include <cstdio>
@@ -253,33 +254,63 @@ int main(int argc, char **argv) {
         std::fprintf(stderr, "saln: %s\n", saln_last_error());
         return 1;
     }
-    std::string text;
+    // Both engines run the pair loop main.rs:61-74 in chunks of pairs in the
+    // reference's order (db outer, query inner); each chunk is one batched
+    // render call (every pair computed once on the GPU), then printed pair by
+    // pair.
+    std::vector<uint8_t> qs, ds;
+    std::vector<uint64_t> qo{0}, dof{0};
+    for (const Rec &q : query) {
+        qs.insert(qs.end(), q.seq.begin(), q.seq.end());
+        qo.push_back(qs.size());
+    }
+    for (const Rec &d : db) {
+        ds.insert(ds.end(), d.seq.begin(), d.seq.end());
+        dof.push_back(ds.size());
+    }
+    const uint64_t nq = query.size(), nd = db.size(), total = nq * nd;
+    std::vector<uint32_t> pq, pd;
     if (a.algo == 2) {  // Algo::Wfa => wfa_align(q, d, mode)  (main.rs:66)
-        for (const Rec &d : db) {
-            for (const Rec &q : query) {
+        // A chunk's alignment rows are sized for its longest pair
+        // (2 * (len_q + len_db) + 64 bytes per row, two rows per pair); keep
+        // them under kWfaRowBytes.
+        constexpr uint64_t kWfaPairs = 1u << 16, kWfaRowBytes = 1ull << 30;
+        for (uint64_t p0 = 0; p0 < total;) {
+            pq.clear();
+            pd.clear();
+            uint64_t cap = 64;
+            for (uint64_t p = p0; p < total && pq.size() < kWfaPairs; ++p) {
+                const uint64_t qi = p % nq, di = p / nq;
+                const uint64_t c =
+                    std::max<uint64_t>(cap, 2 * (query[qi].seq.size() + db[di].seq.size()) + 64);
+                if (!pq.empty() && (pq.size() + 1) * 2 * c > kWfaRowBytes) break;
+                cap = c;
+                pq.push_back((uint32_t)qi);
+                pd.push_back((uint32_t)di);
+            }
+            saln_wfa_text *t = nullptr;
+            int rc = saln_wfa_render_batch(ctx, qs.data(), qo.data(), nq, ds.data(), dof.data(),
+                                           nd, pq.data(), pd.data(), pq.size(), a.mode,
+                                           a.wfa_steps, 0, &t);
+            if (rc != SALN_OK) {
+                std::fprintf(stderr, "saln: %s\n", saln_last_error());
+                saln_context_destroy(ctx);
+                return 1;
+            }
+            for (uint64_t k = 0; k < pq.size(); ++k) {
+                const Rec &q = query[pq[k]], &d = db[pd[k]];
+                const char *txt = nullptr;
                 uint64_t len = 0;
                 saln_wfa_result r;
-                int rc = saln_wfa_render(ctx, q.seq.data(), q.seq.size(), d.seq.data(),
-                                         d.seq.size(), a.mode, a.wfa_steps, 0, nullptr, 0, &len, &r);
-                if (rc == SALN_OK && r.status == SALN_NOT_IMPLEMENTED) {
+                saln_wfa_text_get(t, k, &txt, &len, &r);
+                if (r.status == SALN_NOT_IMPLEMENTED) {
                     std::fprintf(stderr,
                                  "An error occured during alignment of %s and %s\nError in "
                                  "alignment: not implemented\n",
                                  as_str(q.name).c_str(), as_str(d.name).c_str());
                     continue;
                 }
-                if (rc == SALN_OK) {
-                    text.assign(len, '\0');
-                    rc = saln_wfa_render(ctx, q.seq.data(), q.seq.size(), d.seq.data(),
-                                         d.seq.size(), a.mode, a.wfa_steps, 0, text.data(), len,
-                                         &len, &r);
-                }
-                if (rc != SALN_OK) {
-                    std::fprintf(stderr, "saln: %s\n", saln_last_error());
-                    saln_context_destroy(ctx);
-                    return 1;
-                }
-                std::fwrite(text.data(), 1, text.size(), stdout);
+                std::fwrite(txt, 1, len, stdout);
                 if (r.status == SALN_REF_PANIC_TRIM || r.status == SALN_REF_PANIC_SLICE) {
                     std::fflush(stdout);
                     const char *where = r.status == SALN_REF_PANIC_TRIM
@@ -291,6 +322,7 @@ int main(int argc, char **argv) {
                                      "`RUST_BACKTRACE=1` environment variable to display a "
                                      "backtrace\n",
                                      where);
+                        saln_wfa_text_free(t);
                         saln_context_destroy(ctx);
                         return 101;
                     }
@@ -306,30 +338,18 @@ int main(int argc, char **argv) {
                                  "reference would not terminate)\n",
                                  as_str(q.name).c_str(), as_str(d.name).c_str(), a.wfa_steps);
             }
+            saln_wfa_text_free(t);
+            p0 += pq.size();
         }
         saln_context_destroy(ctx);
         return 0;
     }
-    // Needleman-Wunsch: the pair loop main.rs:61-74 in chunks of pairs in the
-    // reference's order (db outer, query inner); each chunk is one
-    // saln_nw_render_batch (one plan, fill + walk on the GPU, every pair
-    // computed once), then printed pair by pair.  A chunk holds up to
-    // kChunkPairs pairs or ~kChunkCells cells (its full-code mask and the
-    // host copy of it stay bounded).
+    // Needleman-Wunsch: each chunk is one saln_nw_render_batch (one plan,
+    // fill + walk on the GPU).  A chunk holds up to kChunkPairs pairs or
+    // ~kChunkCells cells (its full-code mask and the host copy of it stay
+    // bounded).
     constexpr uint64_t kChunkPairs = 1u << 16;
     constexpr uint64_t kChunkCells = 2ull << 30;
-    std::vector<uint8_t> qs, ds;
-    std::vector<uint64_t> qo{0}, dof{0};
-    for (const Rec &q : query) {
-        qs.insert(qs.end(), q.seq.begin(), q.seq.end());
-        qo.push_back(qs.size());
-    }
-    for (const Rec &d : db) {
-        ds.insert(ds.end(), d.seq.begin(), d.seq.end());
-        dof.push_back(ds.size());
-    }
-    const uint64_t nq = query.size(), nd = db.size(), total = nq * nd;
-    std::vector<uint32_t> pq, pd;
     for (uint64_t p0 = 0; p0 < total;) {
         pq.clear();
         pd.clear();

@@ -7,11 +7,13 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <climits>
 #include <cstdio>
 #include <cstring>
 #include <memory>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "nw_host.hpp"
@@ -243,7 +245,105 @@ void appendf(std::string *s, const char *fmt, long long v) {
     *s += b;
 }
 
+// The text wfa_align prints for one pair (wfa.rs; lines cited inline) from
+// its result, its per-step lo/hi log, its rec_tr event log and its alignment
+// rows (a1/a2, acap bytes each, reversed as the reference pushes them).
+void render_pair(const saln_wfa_result &r, const int32_t *lohi, const uint8_t *ev, uint32_t nev,
+                 const uint8_t *a1, const uint8_t *a2, uint32_t acap, long long diag,
+                 std::string *out) {
+    std::string &t = *out;
+    if (r.status != SALN_NOT_IMPLEMENTED) {
+        // `lo: {}, hi: {}` of every WaveFrontTensor::new that had sources (:251)
+        for (uint32_t s = 0; s < r.steps; ++s) {
+            const int32_t lo = lohi[2 * s], hi = lohi[2 * s + 1];
+            if (lo == INT32_MIN) continue;
+            appendf(&t, "lo: %lld, ", lo);
+            appendf(&t, "hi: %lld\n", hi);
+        }
+    }
+    if (r.status == SALN_OK || r.status == SALN_REF_PANIC_SLICE) {
+        appendf(&t, "converged with score %lld: \n", r.score);       // :38
+        appendf(&t, "huhu, diag: %lld\n", diag);  // :650
+        t += "Element {\n";                                            // Debug :103-116
+        t += std::string("\tstate: ") + state_name(r.conv_state) + "\n";
+        appendf(&t, "\toffset: %lld\n", r.conv_offset);
+        if (!r.conv_np) {
+            t += "\tparents: []\n";
+        } else {
+            t += "\tparents: [\n";
+            for (int k = 0; k < r.conv_np; ++k)
+                t += std::string("    ") + state_name(r.conv_parents[k]) + ",\n";
+            t += "]\n";
+        }
+        t += "}\n";
+        appendf(&t, "\nscore: %lld\n", r.score);
+        // rec_tr events (:654-853): every attempt prints `well shit` or
+        // `yeah, score: N`; an attempt that moves prints its action and the
+        // walk restarts at the lower score; `open` without a move is the
+        // last attempt, so `huh` follows it.
+        enum { WELL = 0, YEAH = 1, MISMATCH = 2, EXTEND = 3, OPEN = 4, RET = 5, HUH = 6 };
+        static const uint64_t nds[3] = {4, 6, 8};
+        uint64_t score = (uint64_t)r.score;
+        int attempt = 0;
+        for (uint32_t k = 0; k < nev;) {
+            const uint8_t e = ev[k++];
+            if (e == RET) { t += "ret\n"; break; }
+            if (e == HUH) { t += "huh\n"; break; }
+            if (e == WELL) { t += "well shit\n"; ++attempt; continue; }
+            if (e != YEAH || attempt >= 3) break;
+            const uint64_t ns = score - nds[attempt];
+            appendf(&t, "yeah, score: %lld\n", (long long)ns);
+            const uint8_t nx = k < nev ? ev[k] : (uint8_t)HUH;
+            if (nx == MISMATCH || nx == EXTEND) {
+                t += nx == MISMATCH ? "mismatch\n" : "extend\n";
+                ++k;
+                score = ns;
+                attempt = 0;
+            } else if (nx == OPEN) {
+                t += "open\n";
+                ++k;
+                if (k < nev && ev[k] == HUH) {
+                    ++attempt;
+                } else {
+                    score = ns;
+                    attempt = 0;
+                }
+            } else {
+                ++attempt;
+            }
+        }
+        if (r.status == SALN_OK) {
+            // Display (:950-980) + println, then Debug (`{:#?}`)
+            const uint32_t n1 = std::min(r.aln_len1, acap), n2 = std::min(r.aln_len2, acap);
+            for (uint32_t k = n1; k > 0; --k) t += (char)a1[k - 1];
+            t += "\n";
+            for (uint32_t k = std::min(n1, n2); k > 0; --k) t += a1[k - 1] != a2[k - 1] ? " " : "|";
+            for (uint32_t k = n2; k > 0; --k) t += (char)a2[k - 1];
+            t += "\n\n";
+            t += "Alignment {\n";
+            const uint8_t *rows[2] = {a1, a2};
+            const uint32_t lens[2] = {n1, n2};
+            const char *names[2] = {"seq1", "seq2"};
+            for (int w = 0; w < 2; ++w) {
+                if (!lens[w]) {
+                    t += std::string("    ") + names[w] + ": [],\n";
+                    continue;
+                }
+                t += std::string("    ") + names[w] + ": [\n";
+                for (uint32_t k = 0; k < lens[w]; ++k) appendf(&t, "        %lld,\n", rows[w][k]);
+                t += "    ],\n";
+            }
+            t += "}\n";
+        }
+    }
+}
+
 }  // namespace
+
+struct saln_wfa_text {
+    std::vector<std::string> text;
+    std::vector<saln_wfa_result> res;
+};
 
 struct saln_wfa_plan {
     saln_context *ctx = nullptr;
@@ -281,93 +381,8 @@ int saln_wfa_render(saln_context *ctx, const uint8_t *q, uint64_t len_q, const u
     if (rc != SALN_OK) return rc;
     if (result) *result = r;
     std::string t;
-    if (r.status != SALN_NOT_IMPLEMENTED) {
-        // `lo: {}, hi: {}` of every WaveFrontTensor::new that had sources (:251)
-        for (uint32_t s = 0; s < r.steps; ++s) {
-            const int32_t lo = logs.lohi[2 * s], hi = logs.lohi[2 * s + 1];
-            if (lo == INT32_MIN) continue;
-            appendf(&t, "lo: %lld, ", lo);
-            appendf(&t, "hi: %lld\n", hi);
-        }
-    }
-    if (r.status == SALN_OK || r.status == SALN_REF_PANIC_SLICE) {
-        appendf(&t, "converged with score %lld: \n", r.score);       // :38
-        appendf(&t, "huhu, diag: %lld\n", (long long)len_q - (long long)len_db);  // :650
-        t += "Element {\n";                                            // Debug :103-116
-        t += std::string("\tstate: ") + state_name(r.conv_state) + "\n";
-        appendf(&t, "\toffset: %lld\n", r.conv_offset);
-        if (!r.conv_np) {
-            t += "\tparents: []\n";
-        } else {
-            t += "\tparents: [\n";
-            for (int k = 0; k < r.conv_np; ++k)
-                t += std::string("    ") + state_name(r.conv_parents[k]) + ",\n";
-            t += "]\n";
-        }
-        t += "}\n";
-        appendf(&t, "\nscore: %lld\n", r.score);
-        // rec_tr events (:654-853): every attempt prints `well shit` or
-        // `yeah, score: N`; an attempt that moves prints its action and the
-        // walk restarts at the lower score; `open` without a move is the
-        // last attempt, so `huh` follows it.
-        enum { WELL = 0, YEAH = 1, MISMATCH = 2, EXTEND = 3, OPEN = 4, RET = 5, HUH = 6 };
-        static const uint64_t nds[3] = {4, 6, 8};
-        const uint8_t *ev = logs.ev.data();
-        const uint32_t nev = logs.ev_cap;
-        uint64_t score = (uint64_t)r.score;
-        int attempt = 0;
-        for (uint32_t k = 0; k < nev;) {
-            const uint8_t e = ev[k++];
-            if (e == RET) { t += "ret\n"; break; }
-            if (e == HUH) { t += "huh\n"; break; }
-            if (e == WELL) { t += "well shit\n"; ++attempt; continue; }
-            if (e != YEAH || attempt >= 3) break;
-            const uint64_t ns = score - nds[attempt];
-            appendf(&t, "yeah, score: %lld\n", (long long)ns);
-            const uint8_t nx = k < nev ? ev[k] : (uint8_t)HUH;
-            if (nx == MISMATCH || nx == EXTEND) {
-                t += nx == MISMATCH ? "mismatch\n" : "extend\n";
-                ++k;
-                score = ns;
-                attempt = 0;
-            } else if (nx == OPEN) {
-                t += "open\n";
-                ++k;
-                if (k < nev && ev[k] == HUH) {
-                    ++attempt;
-                } else {
-                    score = ns;
-                    attempt = 0;
-                }
-            } else {
-                ++attempt;
-            }
-        }
-        if (r.status == SALN_OK) {
-            // Display (:950-980) + println, then Debug (`{:#?}`)
-            const uint8_t *a1 = aln.data(), *a2 = aln.data() + acap;
-            const uint32_t n1 = std::min(r.aln_len1, acap), n2 = std::min(r.aln_len2, acap);
-            for (uint32_t k = n1; k > 0; --k) t += (char)a1[k - 1];
-            t += "\n";
-            for (uint32_t k = std::min(n1, n2); k > 0; --k) t += a1[k - 1] != a2[k - 1] ? " " : "|";
-            for (uint32_t k = n2; k > 0; --k) t += (char)a2[k - 1];
-            t += "\n\n";
-            t += "Alignment {\n";
-            const uint8_t *rows[2] = {a1, a2};
-            const uint32_t lens[2] = {n1, n2};
-            const char *names[2] = {"seq1", "seq2"};
-            for (int w = 0; w < 2; ++w) {
-                if (!lens[w]) {
-                    t += std::string("    ") + names[w] + ": [],\n";
-                    continue;
-                }
-                t += std::string("    ") + names[w] + ": [\n";
-                for (uint32_t k = 0; k < lens[w]; ++k) appendf(&t, "        %lld,\n", rows[w][k]);
-                t += "    ],\n";
-            }
-            t += "}\n";
-        }
-    }
+    render_pair(r, logs.lohi.data(), logs.ev.data(), logs.ev_cap, aln.data(), aln.data() + acap,
+                acap, (long long)len_q - (long long)len_db, &t);
     if (out_len) *out_len = t.size();
     if (out) {
         std::memcpy(out, t.data(), std::min<uint64_t>(t.size(), cap));
@@ -375,6 +390,82 @@ int saln_wfa_render(saln_context *ctx, const uint8_t *q, uint64_t len_q, const u
     }
     return SALN_OK;
 }
+
+// wfa_align's text for every pair of a batch, each pair computed once: one
+// run_wfa over the batch with logs and alignment rows, then the per-pair
+// rendering on host threads.
+int saln_wfa_render_batch(saln_context *ctx, const uint8_t *q_seq, const uint64_t *q_off,
+                          uint64_t n_q, const uint8_t *db_seq, const uint64_t *db_off,
+                          uint64_t n_db, const uint32_t *pair_q, const uint32_t *pair_db,
+                          uint64_t n_pairs, int32_t mode, uint32_t max_steps, uint32_t max_width,
+                          saln_wfa_text **out) {
+    if (!ctx || !q_off || !db_off || !out) return SALN_E_INVALID;
+    *out = nullptr;
+    if (!max_steps) max_steps = kDefaultSteps;
+    auto t = std::make_unique<saln_wfa_text>();
+    t->text.resize(n_pairs);
+    t->res.resize(n_pairs);
+    if (!n_pairs) {
+        *out = t.release();
+        return SALN_OK;
+    }
+    // one row capacity for the batch: the largest 2 * (len_q + len_db) + 64
+    uint64_t acap = 64;
+    std::vector<int64_t> diag(n_pairs);
+    for (uint64_t k = 0; k < n_pairs; ++k) {
+        const uint64_t qi = pair_q ? pair_q[k] : k % std::max<uint64_t>(n_q, 1);
+        const uint64_t di = pair_db ? pair_db[k] : k / std::max<uint64_t>(n_q, 1);
+        if (qi >= n_q || di >= n_db) {
+            set_error("pair index out of range");
+            return SALN_E_INVALID;
+        }
+        const uint64_t lq = q_off[qi + 1] - q_off[qi], ld = db_off[di + 1] - db_off[di];
+        acap = std::max<uint64_t>(acap, 2 * (lq + ld) + 64);
+        diag[k] = (int64_t)lq - (int64_t)ld;
+    }
+    if (acap > 0x7FFFFFFF || n_pairs * 2 * acap > (1ull << 34)) {
+        set_error("saln_wfa_render_batch: alignment rows exceed 16 GB; split the batch");
+        return SALN_E_INVALID;
+    }
+    std::vector<uint8_t> aln(n_pairs * 2 * acap);
+    std::vector<uint64_t> aoff(n_pairs);
+    for (uint64_t k = 0; k < n_pairs; ++k) aoff[k] = k * 2 * acap;
+    Logs logs;
+    int rc = run_wfa(ctx, q_seq, q_off, n_q, db_seq, db_off, n_db, pair_q, pair_db, n_pairs, mode,
+                     max_steps, max_width, t->res.data(), aln.data(), aoff.data(), (uint32_t)acap,
+                     &logs);
+    if (rc != SALN_OK) return rc;
+    const unsigned nth = (unsigned)std::min<uint64_t>(
+        std::max(1u, std::min(16u, std::thread::hardware_concurrency())), (n_pairs + 63) / 64);
+    std::atomic<uint64_t> next{0};
+    auto work = [&] {
+        for (uint64_t k; (k = next.fetch_add(1)) < n_pairs;) {
+            const uint8_t *a = aln.data() + aoff[k];
+            render_pair(t->res[k], logs.lohi.data() + k * 2 * max_steps,
+                        logs.ev.data() + k * logs.ev_cap, logs.ev_cap, a, a + acap,
+                        (uint32_t)acap, diag[k], &t->text[k]);
+        }
+    };
+    std::vector<std::thread> th;
+    for (unsigned i = 1; i < nth; ++i) th.emplace_back(work);
+    work();
+    for (auto &x : th) x.join();
+    *out = t.release();
+    return SALN_OK;
+}
+
+uint64_t saln_wfa_text_count(const saln_wfa_text *t) { return t ? t->text.size() : 0; }
+
+int saln_wfa_text_get(const saln_wfa_text *t, uint64_t pair, const char **text, uint64_t *len,
+                      saln_wfa_result *result) {
+    if (!t || pair >= t->text.size()) return SALN_E_INVALID;
+    if (text) *text = t->text[pair].data();
+    if (len) *len = t->text[pair].size();
+    if (result) *result = t->res[pair];
+    return SALN_OK;
+}
+
+void saln_wfa_text_free(saln_wfa_text *t) { delete t; }
 
 int saln_wfa_plan_create(saln_context *ctx, const uint64_t *q_off, uint64_t n_q,
                          const uint64_t *db_off, uint64_t n_db, const uint32_t *pair_q,

@@ -49,6 +49,40 @@ def render(seq1, seq2, mode: Mode = Mode.Global, *, max_steps: int = 64, max_wid
     return buf.raw[:n.value].decode("latin-1"), res.status
 
 
+def render_batch(queries, dbs, pairs=None, mode: Mode = Mode.Global, *, max_steps: int = 64,
+                 max_width: int = 64, device: int = 0) -> list[tuple[str, int]]:
+    """The reference's stdout per pair of a batch (saln_wfa_render_batch: one
+    GPU run, every pair computed once): [(text, status)] in pair order
+    (pairs=None: all-vs-all, db outer / query inner, main.rs:61-62)."""
+    qs, qo = pack_csr(queries)
+    ds, do = pack_csr(dbs)
+    if pairs is None:
+        pq = pd = None
+        n = len(queries) * len(dbs)
+    else:
+        pa = np.asarray(pairs, np.uint32).reshape(-1, 2)
+        pq, pd = np.ascontiguousarray(pa[:, 0]), np.ascontiguousarray(pa[:, 1])
+        n = len(pa)
+    L = _lib.lib()
+    h = C.c_void_p()
+    ptr = lambda a: a.ctypes.data_as(C.c_void_p) if a is not None and a.size else None  # noqa: E731
+    _lib.check(L.saln_wfa_render_batch(_lib.context(device), ptr(qs), ptr(qo), len(queries),
+                                       ptr(ds), ptr(do), len(dbs), ptr(pq), ptr(pd), n,
+                                       int(mode), max_steps, max_width, C.byref(h)),
+               "saln_wfa_render_batch")
+    try:
+        out = []
+        for k in range(L.saln_wfa_text_count(h)):
+            tp, tn, res = C.c_void_p(), C.c_uint64(), _lib.WfaResult()
+            _lib.check(L.saln_wfa_text_get(h, k, C.byref(tp), C.byref(tn), C.byref(res)),
+                       "saln_wfa_text_get")
+            out.append((C.string_at(tp.value, tn.value).decode("latin-1") if tn.value else "",
+                        res.status))
+        return out
+    finally:
+        L.saln_wfa_text_free(h)
+
+
 def wfa_align(seq1, seq2, mode: Mode = Mode.Global, *, max_steps: int = 64, max_width: int = 64,
               device: int = 0) -> WfaAlignment:
     """wfa.rs:23 — seq1 = query, seq2 = db."""

@@ -114,3 +114,27 @@ def test_device_plan_matches_batch(saln):
     plan.close()
     for f in ("score", "status", "steps", "conv_offset", "conv_state", "conv_np"):
         assert np.array_equal(got[f], ref[f]), f
+
+
+def test_render_batch_matches_oracle(saln, oracle):
+    """saln_wfa_render_batch (one GPU run of the batch, every pair computed
+    once) gives the oracle's stdout and status for every pair of an
+    all-vs-all batch with empty, short, converging, trim-panicking and
+    non-converging pairs, in db-outer / query-inner order."""
+    rng = np.random.default_rng(15)
+    queries = [b"", b"A", b"AC", b"GATTACA"] + [rand_seq(rng, int(n)) for n in (9, 25, 60)]
+    queries.append(synth.random_bases(21, 400).tobytes())
+    dbs = [b"", b"AG", b"GCATTAC"] + [synth.mutate(q, 0.1, seed=k) or b"T"
+                                      for k, q in enumerate(queries[4:])]
+    got = saln.wfa.render_batch(queries, dbs, max_steps=64)
+    assert len(got) == len(queries) * len(dbs)
+    statuses = set()
+    for k, (text, st) in enumerate(got):
+        q, d = queries[k % len(queries)], dbs[k // len(queries)]
+        o = oracle.wfa(q, d, max_steps=64)
+        assert (st, text) == (o.status, o.stdout), (k, q[:20], d[:20])
+        statuses.add(st)
+    assert {0, 3} <= statuses, statuses
+    sub = saln.wfa.render_batch(queries, dbs, pairs=[(3, 2), (0, 0), (7, 6)], max_steps=64)
+    assert [t for t, _ in sub] == [got[2 * len(queries) + 3][0], got[0][0],
+                                   got[6 * len(queries) + 7][0]]
