@@ -388,10 +388,15 @@ int saln_nw_spans_walk(saln_nw_span *const *spans, uint32_t n, const uint8_t *d_
                        const uint8_t *d_db, saln_nw_span_cursor *exit, uint32_t *ops,
                        uint64_t ops_cap, uint64_t *n_ops, void *stream);
 int saln_device_cu_count(saln_context *ctx, uint32_t *n);
+/* A stream on mask bits [cu_lo, cu_hi).  Bit c is a CU of XCD c mod n_xcd
+ * (measured, profiles/r04_cu_map.json), so a range of 8k bits is k CUs per
+ * XCD.  Ranges shorter than the XCD count are refused (SALN_E_INVALID): an
+ * XCD left without a bit runs unmasked. */
 int saln_stream_create_cu_range(saln_context *ctx, uint32_t cu_lo, uint32_t cu_hi, void **stream);
 int saln_stream_destroy(saln_context *ctx, void *stream);
 /* A stream on an arbitrary CU mask (bit c of word c / 32 = CU c in the
- * runtime's mask order, hipExtStreamCreateWithCUMask). */
+ * runtime's mask order, hipExtStreamCreateWithCUMask; an XCD with no bit set
+ * runs unmasked, see saln_stream_create_cu_range). */
 int saln_stream_create_cu_mask(saln_context *ctx, const uint32_t *mask, uint32_t n_words,
                                void **stream);
 /* Diagnostic: launches n_blocks one-wave workgroups on `stream` (e.g. a

@@ -35,6 +35,7 @@ struct Args {
     bool timing = true, abort_on_panic = true;
     uint32_t wfa_steps = 64;  // cap on WFA score steps (the reference loops without one)
     uint64_t max_blocks = 0;
+    bool stage_times = false;
 };
 
 const char *kUsage =
@@ -54,6 +55,7 @@ const char *kUsage =
     "      --no-abort                 report reference panics and continue\n"
     "      --wfa-steps <N>            cap on WFA score steps [default: 64]\n"
     "      --max-blocks <N>           cap on printed alignments per pair [default: 0 = none]\n"
+    "      --stage-times              stage times of this run on stderr\n"
     "  -h, --help                     Print help\n";
 
 [[noreturn]] void usage_error(const std::string &msg) {
@@ -109,6 +111,8 @@ Args parse_args(int argc, char **argv) {
             a.abort_on_panic = false;
         } else if (is("--wfa-steps", "--wfa-steps")) {
             a.wfa_steps = (uint32_t)std::strtoul(need("--wfa-steps <N>").c_str(), nullptr, 10);
+        } else if (s == "--stage-times") {
+            a.stage_times = true;
         } else if (is("--max-blocks", "--max-blocks")) {
             a.max_blocks = std::strtoull(need("--max-blocks <N>").c_str(), nullptr, 10);
         } else {
@@ -240,9 +244,19 @@ std::string as_str(const std::vector<uint8_t> &v) { return std::string(v.begin()
 
 int main(int argc, char **argv) {
     const Args a = parse_args(argc, argv);
+    auto t_mark = std::chrono::steady_clock::now();
+    auto mark = [&](const char *what) {
+        if (!a.stage_times) return;
+        const auto n = std::chrono::steady_clock::now();
+        std::fprintf(stderr, "[saln cli] %-16s %8.3f ms\n", what,
+                     std::chrono::duration<double, std::milli>(n - t_mark).count());
+        t_mark = n;
+    };
+    if (a.stage_times) saln_option_set("host.timing", 1);
     std::vector<Rec> db, query;
     if (!load(a.db, "DB", &db)) return 0;
     if (!load(a.query, "Query", &query)) return 0;
+    mark("load fasta");
     if (a.algo == 0) {
         std::fprintf(stderr,
                      "saln: -a a-star (the reference's A* aligner) is not part of this engine; "
@@ -254,6 +268,7 @@ int main(int argc, char **argv) {
         std::fprintf(stderr, "saln: %s\n", saln_last_error());
         return 1;
     }
+    mark("context");
     // Both engines run the pair loop main.rs:61-74 in chunks of pairs in the
     // reference's order (db outer, query inner); each chunk is one batched
     // render call (every pair computed once on the GPU), then printed pair by
@@ -363,9 +378,11 @@ int main(int argc, char **argv) {
             pd.push_back((uint32_t)di);
         }
         saln_nw_text *t = nullptr;
+        mark("chunk plan");
         int rc = saln_nw_render_batch(ctx, qs.data(), qo.data(), nq, ds.data(), dof.data(), nd,
                                       pq.data(), pd.data(), pq.size(), a.mode, a.max_blocks,
                                       a.abort_on_panic ? 1 : 0, &t);
+        mark("render batch");
         if (rc != SALN_OK) {
             std::fprintf(stderr, "saln: %s\n", saln_last_error());
             saln_context_destroy(ctx);
@@ -408,9 +425,11 @@ int main(int argc, char **argv) {
                              as_str(d.name).c_str());
             if (a.timing) std::printf("%s\n", duration_debug(ns).c_str());
         }
+        mark("print");
         saln_nw_text_free(t);
         p0 += pq.size();
     }
     saln_context_destroy(ctx);
+    mark("exit");
     return 0;
 }

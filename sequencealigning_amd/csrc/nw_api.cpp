@@ -3,11 +3,13 @@
 // thin wrapper: upload -> plan -> saln_nw_execute (GPU) -> download.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -190,7 +192,7 @@ int saln_nw_render_batch(saln_context *ctx, const uint8_t *q_seq, const uint64_t
         delete t;
         return rc;
     }
-    std::vector<uint8_t> host;
+    StageClock clock;
     {
         DevBuf dq(ctx), dd(ctx), dr(ctx);
         const uint64_t qbytes = q_off[n_q], dbytes = db_off[n_db];
@@ -206,9 +208,11 @@ int saln_nw_render_batch(saln_context *ctx, const uint8_t *q_seq, const uint64_t
         if ((qbytes && (e = hipMemcpy(dq.p, q_seq, qbytes, hipMemcpyHostToDevice)) != hipSuccess) ||
             (dbytes && (e = hipMemcpy(dd.p, db_seq, dbytes, hipMemcpyHostToDevice)) != hipSuccess))
             return fail(e, "render batch: upload");
+        clock.mark("render: plan + upload");
         rc = saln_nw_execute(g.p, (const uint8_t *)dq.p, (const uint8_t *)dd.p,
                              (saln_nw_result *)dr.p, nullptr, nullptr);
         if (rc == SALN_OK && (e = hipDeviceSynchronize()) != hipSuccess) return fail(e, "execute");
+        clock.mark("render: execute");
         if (rc == SALN_OK) rc = plan_check_error(g.p);
         if (rc != SALN_OK) {
             delete t;
@@ -227,23 +231,63 @@ int saln_nw_render_batch(saln_context *ctx, const uint8_t *q_seq, const uint64_t
                 n = k + 1;
                 break;
             }
-    if ((rc = plan_download_masks(g.p, n, &host)) != SALN_OK) {
+    // The pairs' mask bytes stream into pinned host memory in slices (one
+    // thread issuing the copies) while the DFS threads render the pairs in
+    // the order their bytes arrive: the download and the host work overlap.
+    const uint8_t *d_mask = nullptr;
+    if ((rc = plan_mask_source(g.p, &d_mask)) != SALN_OK) {
         delete t;
         return rc;
     }
+    std::vector<uint64_t> order(n), endb(n);
+    uint64_t total = 0;
+    for (uint64_t k = 0; k < n; ++k) {
+        order[k] = k;
+        endb[k] = plan_mask_end(g.p, k);
+        total = std::max(total, endb[k]);
+    }
+    std::sort(order.begin(), order.end(), [&](uint64_t x, uint64_t y) { return endb[x] < endb[y]; });
+    std::lock_guard<std::mutex> lk(ctx->staging_mu);
+    uint8_t *host = nullptr;
+    if (total) {
+        const hipError_t e = pinned_staging(ctx, total, (void **)&host);
+        if (e != hipSuccess) {
+            set_error(std::string("render batch: pinned staging: ") + hipGetErrorString(e));
+            delete t;
+            return SALN_E_HIP;
+        }
+    }
+    clock.mark("render: results");
     const double dev_ns =
         (double)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0)
             .count();
+    constexpr uint64_t kSlice = 32ull << 20;
+    std::atomic<uint64_t> have{0};
+    std::atomic<int> dl_err{0};
+    std::thread dl([&] {
+        hipError_t e = hipSetDevice(ctx->device);
+        for (uint64_t off = 0; e == hipSuccess && off < total; off += kSlice) {
+            const uint64_t len = std::min(kSlice, total - off);
+            e = hipMemcpy(host + off, d_mask + off, len, hipMemcpyDeviceToHost);
+            if (e == hipSuccess) have.store(off + len, std::memory_order_release);
+        }
+        if (e != hipSuccess) dl_err.store((int)e, std::memory_order_release);  // (errors are per thread)
+    });
     // per-pair DFS on host threads (its cost varies by orders of magnitude
     // with the number of co-optimal paths: pairs are handed out one by one)
     std::atomic<uint64_t> next{0};
     auto work = [&]() {
         for (;;) {
-            const uint64_t k = next.fetch_add(1);
-            if (k >= n) return;
+            const uint64_t i = next.fetch_add(1);
+            if (i >= n) return;
+            const uint64_t k = order[i];
+            while (have.load(std::memory_order_acquire) < endb[k]) {
+                if (dl_err.load(std::memory_order_acquire)) return;
+                std::this_thread::yield();
+            }
             const auto a = std::chrono::steady_clock::now();
             const uint64_t qi = pair_q ? pair_q[k] : k % n_q, di = pair_db ? pair_db[k] : k / n_q;
-            const HostMask hm = plan_host_mask(g.p, host.data(), k);
+            const HostMask hm = plan_host_mask(g.p, host, k);
             const DfsOutcome o = render_blocks(hm, q_seq + q_off[qi], db_seq + db_off[di],
                                                max_blocks, &t->text[k]);
             t->blocks[k] = o.blocks;
@@ -258,6 +302,13 @@ int saln_nw_render_batch(saln_context *ctx, const uint8_t *q_seq, const uint64_t
     for (uint64_t i = 1; i < nt; ++i) th.emplace_back(work);
     work();
     for (auto &x : th) x.join();
+    dl.join();
+    if (const int e = dl_err.load()) {
+        set_error(std::string("render batch: mask download: ") + hipGetErrorString((hipError_t)e));
+        delete t;
+        return SALN_E_HIP;
+    }
+    clock.mark("render: masks + dfs");
     // each pair's share of the batch's device work, added to its own DFS time
     for (uint64_t k = 0; k < n; ++k) t->ns[k] += (uint64_t)(dev_ns / (double)std::max<uint64_t>(1, n_pairs));
     t->count = n;

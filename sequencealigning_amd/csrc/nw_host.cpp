@@ -819,28 +819,23 @@ int plan_pair_mask(const saln_nw_plan *p, uint64_t pair_id, PairMask *pm) {
     return SALN_OK;
 }
 
-int plan_download_masks(const saln_nw_plan *p, uint64_t n_first, std::vector<uint8_t> *host) {
-    if (!p || n_first > p->n_pairs) return SALN_E_INVALID;
+int plan_mask_source(const saln_nw_plan *p, const uint8_t **d_mask) {
+    if (!p || !d_mask) return SALN_E_INVALID;
     if (!p->full_codes) {
-        set_error("plan_download_masks: plan stores walk codes only");
+        set_error("plan_mask_source: plan stores walk codes only");
         return SALN_E_INVALID;
     }
-    // the workspace prefix that holds pairs 0 .. n_first-1 (results order):
-    // up to the last byte of each pair's end cell (the largest offset of its
-    // cells in every layout, nw_common.hpp Geom::cell)
-    uint64_t end = 0;
-    for (uint64_t k = 0; k < n_first; ++k) {
-        const NwPairDesc &d = p->h_pairs[p->plan_index[k]];
-        if (d.len_q == 0 || d.len_db == 0) continue;
-        const Geom g = variant_geom((int)d.variant);
-        end = std::max<uint64_t>(end, d.mask_off + g.cell(d.len_db, d.len_q, d.mask_rs, d.mask_bs,
-                                                          d.mask_cs) + 1);
-    }
-    host->resize(end);
-    if (!end) return SALN_OK;
-    HIP_TRY(hipSetDevice(p->ctx->device));
-    HIP_TRY(hipMemcpy(host->data(), p->d_mask, end, hipMemcpyDeviceToHost));
+    *d_mask = p->d_mask;
     return SALN_OK;
+}
+
+// one past the largest offset of the pair's cells in every layout
+// (nw_common.hpp Geom::cell): its end cell
+uint64_t plan_mask_end(const saln_nw_plan *p, uint64_t pair_id) {
+    const NwPairDesc &d = p->h_pairs[p->plan_index[pair_id]];
+    if (d.len_q == 0 || d.len_db == 0) return 0;
+    const Geom g = variant_geom((int)d.variant);
+    return d.mask_off + g.cell(d.len_db, d.len_q, d.mask_rs, d.mask_bs, d.mask_cs) + 1;
 }
 
 HostMask plan_host_mask(const saln_nw_plan *p, const uint8_t *host, uint64_t pair_id) {

@@ -220,10 +220,12 @@ int plan_create(saln_context *ctx, const uint64_t *q_off, uint64_t n_q, const ui
 // (compact: bs = LB); pair_id is the results index.
 int plan_pair_mask(const saln_nw_plan *plan, uint64_t pair_id, PairMask *mask);
 
-// Host copy of the part of a full-code plan's mask workspace that holds
-// pairs 0 .. n_first-1 (results order) after an execute, and a pair's view
-// on it (render batches: one download instead of a copy per pair).
-int plan_download_masks(const saln_nw_plan *plan, uint64_t n_first, std::vector<uint8_t> *host);
+// A full-code plan's mask workspace for host reads (render batches: one
+// streamed download instead of a copy per pair): the device base, the end of
+// pair pair_id's bytes in it (results index; 0 for an empty pair), and a
+// pair's view on a host copy of the workspace prefix that holds it.
+int plan_mask_source(const saln_nw_plan *plan, const uint8_t **d_mask);
+uint64_t plan_mask_end(const saln_nw_plan *plan, uint64_t pair_id);
 HostMask plan_host_mask(const saln_nw_plan *plan, const uint8_t *host, uint64_t pair_id);
 
 // Reference DFS (needleman_wunsch_affine.rs:246-329) over the parent codes.

@@ -534,15 +534,31 @@ int saln_device_cu_count(saln_context *ctx, uint32_t *n) {
     return SALN_OK;
 }
 
+// CU mask bit c selects a CU of XCD c mod n_xcd (measured on MI355X with
+// saln_device_cu_probe, tools/cu_map.py -> profiles/r04_cu_map.json: every
+// contiguous range of 8k bits holds k CUs of each XCD, spread over its shader
+// engines), so a contiguous range is XCD-balanced by construction.  An XCD
+// whose bits are all clear is NOT idle: the mask is applied per XCD and an
+// empty per-XCD mask runs that XCD unmasked (one bit gave 225 CUs).  Ranges
+// that leave an XCD without a bit are refused for that reason.
 int saln_stream_create_cu_range(saln_context *ctx, uint32_t cu_lo, uint32_t cu_hi, void **stream) {
     if (!ctx || !stream || cu_lo >= cu_hi) return SALN_E_INVALID;
     uint32_t n = 0;
     const int rc = saln_device_cu_count(ctx, &n);
     if (rc != SALN_OK) return rc;
     if (cu_hi > n) return SALN_E_INVALID;
+    HIP_TRY(hipSetDevice(ctx->device));
+    int n_xcd = 1;
+    if (hipDeviceGetAttribute(&n_xcd, hipDeviceAttributeNumberOfXccs, ctx->device) != hipSuccess ||
+        n_xcd < 1)
+        n_xcd = 1;
+    if (cu_hi - cu_lo < (uint32_t)n_xcd) {
+        set_error("saln_stream_create_cu_range: a range of fewer than " + std::to_string(n_xcd) +
+                  " CUs leaves an XCD without a mask bit, and that XCD would run unmasked");
+        return SALN_E_INVALID;
+    }
     std::vector<uint32_t> mask((n + 31) / 32, 0u);
     for (uint32_t c = cu_lo; c < cu_hi; ++c) mask[c / 32] |= 1u << (c % 32);
-    HIP_TRY(hipSetDevice(ctx->device));
     hipStream_t s = nullptr;
     HIP_TRY(hipExtStreamCreateWithCUMask(&s, (uint32_t)mask.size(), mask.data()));
     *stream = s;

@@ -267,7 +267,7 @@ class SpanChain:
     inbox complete before its fill starts)."""
 
     def __init__(self, q: bytes, d: bytes, n_spans: int, *, scoring=None, device: int = 0,
-                 band_rows: int = 2048, cu_split: bool = True):
+                 band_rows: int = 2048, cu_split: bool = True, edge_masks: str = "shared"):
         import torch
         self.q_bytes, self.d_bytes = bytes(q), bytes(d)
         self.len_q, self.len_db = len(q), len(d)
@@ -293,12 +293,26 @@ class SpanChain:
             _lib.check(L.saln_device_cu_count(ctx, C.byref(n)), "saln_device_cu_count")
             if n.value >= n_spans:
                 for lo, hi in [(n.value * r // n_spans, n.value * (r + 1) // n_spans)
-                               for r in range(n_spans)] + [(0, n.value)] * (n_spans - 1):
+                               for r in range(n_spans)]:
                     h = C.c_void_p()
                     _lib.check(L.saln_stream_create_cu_range(ctx, lo, hi, C.byref(h)),
                                "saln_stream_create_cu_range")
-                    (self.cu_streams if len(self.cu_streams) < n_spans
-                     else self.edge_streams).append(h)
+                    self.cu_streams.append(h)
+                # edge r: every CU ("shared": one mask for all edges), or every
+                # CU but bit n-1-r ("unique": no two edge streams with equal masks)
+                nw = (n.value + 31) // 32
+                for r in range(n_spans - 1):
+                    words = [0xFFFFFFFF] * nw
+                    if n.value % 32:
+                        words[-1] = (1 << (n.value % 32)) - 1
+                    if edge_masks == "unique":
+                        b = n.value - 1 - r
+                        words[b // 32] &= ~(1 << (b % 32)) & 0xFFFFFFFF
+                    arr = (C.c_uint32 * nw)(*words)
+                    h = C.c_void_p()
+                    _lib.check(L.saln_stream_create_cu_mask(ctx, arr, nw, C.byref(h)),
+                               "saln_stream_create_cu_mask")
+                    self.edge_streams.append(h)
 
     def fill(self, pipelined: bool = True) -> None:
         import torch

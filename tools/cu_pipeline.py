@@ -32,6 +32,8 @@ def balanced_bits(cu_map, w):
         x, se = b["places"][0][0], b["places"][0][1]
         groups.setdefault((x, se), []).append(b["bit"])
     keys = sorted(groups)
+    if not keys or w > sum(len(v) for v in groups.values()):
+        raise SystemExit("cu map has too few single-place bits (re-run tools/cu_map.py)")
     out, r = [], 0
     while len(out) < w:
         for k in keys:

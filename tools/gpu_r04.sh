@@ -5,6 +5,9 @@
 #   cumap    tools/cu_map.py -> $O/cu_map.json
 #   pipe     tools/cu_pipeline.py over walk-CU counts / layouts (PIPE_CASES)
 #   pipetrace  rocprofv3 --kernel-trace of one pipeline case (PIPE_TRACE args)
+#   rowfloor tools/micro/row_pk_floor (C4 row-step floor: i32 K=2 vs i16x2 frames)
+#   spans    tools/spans_sweep.py over SPAN_CASES (spans:band_rows:edge_masks)
+#   clileg   bench.py's cli leg alone (with its stage breakdown)
 #   smoke    __graft_entry__.smoke()
 #   tests    pytest -m gpu (TESTS= narrows it)
 #   bench    bench.py --steps 20 --warmup 3 (BENCH_ARGS= extra args)
@@ -40,6 +43,13 @@ for st in ${STAGES:-smoke tests bench}; do
       done ;;
     pipetrace) step pipetrace 300 rocprofv3 --kernel-trace -d $O/pipetrace -o run --output-format csv -- python3 tools/cu_pipeline.py ${PIPE_TRACE:---walk-cus 32 --layout balanced --steps 10 --warmup 2} --map $O/cu_map.json
                python3 tools/trace_overlap.py $O/pipetrace --out $O/pipe_overlap.json || exit 1 ;;
+    rowfloor) step rowfloor 120 tools/micro/row_pk_floor 782 100000 5
+              step rowfloor2 120 tools/micro/row_pk_floor 1564 50000 5
+              cat $O/rowfloor.log $O/rowfloor2.log ;;
+    spans) step spans 600 python tools/spans_sweep.py ${SPAN_CASES:-4:1024:shared,4:1024:unique,8:1024:shared,8:1024:unique,2:1024:shared}
+           cut -c1-400 $O/spans.log ;;
+    clileg) step clileg 600 python bench.py --steps 2 --warmup 1 --legs cli
+            tail -1 $O/clileg.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(json.dumps(d['configs']['cli']))" ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     tests) step tests 1100 python -u -m pytest ${TESTS:-tests} -m gpu -x -q --timeout 300 --timeout-method thread
            tail -3 $O/tests.log ;;

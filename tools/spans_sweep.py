@@ -11,8 +11,9 @@ import torch  # noqa: E402
 import bench  # noqa: E402
 import sequencealigning_amd as saln  # noqa: E402
 
-cases = [(int(a), int(b)) for a, b in (x.split(":") for x in
-                                       (sys.argv[1] if len(sys.argv) > 1 else "1:4096,8:4096").split(","))]
-for n, b in cases:
-    r = bench.leg_c4_spans(torch, saln, n_spans=n, reps=3, band_rows=b)
-    print(os.environ.get("GPU_MAX_HW_QUEUES"), n, b, json.dumps(r), flush=True)
+# cases "spans:band_rows[:edge_masks]" (edge_masks shared | unique, span.py SpanChain)
+cases = [x.split(":") for x in (sys.argv[1] if len(sys.argv) > 1 else "1:4096,8:4096").split(",")]
+for c in cases:
+    n, b, em = int(c[0]), int(c[1]), (c[2] if len(c) > 2 else "shared")
+    r = bench.leg_c4_spans(torch, saln, n_spans=n, reps=3, band_rows=b, edge_masks=em)
+    print(os.environ.get("GPU_MAX_HW_QUEUES"), n, b, em, json.dumps(r), flush=True)
