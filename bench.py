@@ -479,7 +479,8 @@ def leg_c4(torch, saln, reps=3, cpu=True):
     return out
 
 
-def leg_c4_spans(torch, saln, n_spans=8, reps=3, band_rows=1024, edge_masks="shared"):
+def leg_c4_spans(torch, saln, n_spans=8, reps=3, band_rows=1024, edge_masks="shared",
+                 cu_ranges=None):
     """configs[3]'s pair split by query columns into `n_spans` spans
     (span.py SpanChain): the spans' fills run
     concurrently on this GPU, each on its own slice of the CUs, and a relay
@@ -494,7 +495,7 @@ def leg_c4_spans(torch, saln, n_spans=8, reps=3, band_rows=1024, edge_masks="sha
     from sequencealigning_amd.span import SpanChain
     q = synth.random_bases(0x5EED0003, 100_000).tobytes()
     d = synth.mutate(q, 0.05, seed=100_000)
-    ch = SpanChain(q, d, n_spans, band_rows=band_rows, edge_masks=edge_masks)
+    ch = SpanChain(q, d, n_spans, band_rows=band_rows, edge_masks=edge_masks, cu_ranges=cu_ranges)
     fills, walks, r = [], [], None
     for k in range(1 + reps):
         torch.cuda.synchronize()

@@ -10,6 +10,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
+#include <new>
 #include <string>
 #include <thread>
 #include <vector>
@@ -231,9 +232,9 @@ int saln_nw_render_batch(saln_context *ctx, const uint8_t *q_seq, const uint64_t
                 n = k + 1;
                 break;
             }
-    // The pairs' mask bytes stream into pinned host memory in slices (one
-    // thread issuing the copies) while the DFS threads render the pairs in
-    // the order their bytes arrive: the download and the host work overlap.
+    // The pairs' mask bytes stream into the context's host buffer in slices
+    // (one thread issuing the copies) while the DFS threads render the pairs
+    // in the order their bytes arrive: the download and the host work overlap.
     const uint8_t *d_mask = nullptr;
     if ((rc = plan_mask_source(g.p, &d_mask)) != SALN_OK) {
         delete t;
@@ -248,15 +249,17 @@ int saln_nw_render_batch(saln_context *ctx, const uint8_t *q_seq, const uint64_t
     }
     std::sort(order.begin(), order.end(), [&](uint64_t x, uint64_t y) { return endb[x] < endb[y]; });
     std::lock_guard<std::mutex> lk(ctx->staging_mu);
-    uint8_t *host = nullptr;
-    if (total) {
-        const hipError_t e = pinned_staging(ctx, total, (void **)&host);
-        if (e != hipSuccess) {
-            set_error(std::string("render batch: pinned staging: ") + hipGetErrorString(e));
+    if (total > ctx->host_mask_bytes) {
+        ctx->host_mask.reset();
+        ctx->host_mask.reset(new (std::nothrow) uint8_t[total]);
+        ctx->host_mask_bytes = ctx->host_mask ? total : 0;
+        if (!ctx->host_mask) {
+            set_error("render batch: host mask buffer allocation failed");
             delete t;
             return SALN_E_HIP;
         }
     }
+    uint8_t *host = ctx->host_mask.get();
     clock.mark("render: results");
     const double dev_ns =
         (double)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0)

@@ -267,7 +267,8 @@ class SpanChain:
     inbox complete before its fill starts)."""
 
     def __init__(self, q: bytes, d: bytes, n_spans: int, *, scoring=None, device: int = 0,
-                 band_rows: int = 2048, cu_split: bool = True, edge_masks: str = "shared"):
+                 band_rows: int = 2048, cu_split: bool = True, edge_masks: str = "shared",
+                 cu_ranges=None):
         import torch
         self.q_bytes, self.d_bytes = bytes(q), bytes(d)
         self.len_q, self.len_db = len(q), len(d)
@@ -292,8 +293,10 @@ class SpanChain:
             n = C.c_uint32()
             _lib.check(L.saln_device_cu_count(ctx, C.byref(n)), "saln_device_cu_count")
             if n.value >= n_spans:
-                for lo, hi in [(n.value * r // n_spans, n.value * (r + 1) // n_spans)
-                               for r in range(n_spans)]:
+                # cu_ranges (experiments): span r's mask bits, default an equal
+                # contiguous share (bit c is a CU of XCD c mod 8: balanced)
+                for lo, hi in cu_ranges or [(n.value * r // n_spans, n.value * (r + 1) // n_spans)
+                                            for r in range(n_spans)]:
                     h = C.c_void_p()
                     _lib.check(L.saln_stream_create_cu_range(ctx, lo, hi, C.byref(h)),
                                "saln_stream_create_cu_range")

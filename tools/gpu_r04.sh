@@ -7,6 +7,8 @@
 #   pipetrace  rocprofv3 --kernel-trace of one pipeline case (PIPE_TRACE args)
 #   rowfloor tools/micro/row_pk_floor (C4 row-step floor: i32 K=2 vs i16x2 frames)
 #   spans    tools/spans_sweep.py over SPAN_CASES (spans:band_rows:edge_masks)
+#   abpipe   bench headline sequential vs --pipeline, REPS alternations
+#   spanq    span counts under GPU_MAX_HW_QUEUES=4 and 16
 #   clileg   bench.py's cli leg alone (with its stage breakdown)
 #   smoke    __graft_entry__.smoke()
 #   tests    pytest -m gpu (TESTS= narrows it)
@@ -48,6 +50,18 @@ for st in ${STAGES:-smoke tests bench}; do
               cat $O/rowfloor.log $O/rowfloor2.log ;;
     spans) step spans 600 python tools/spans_sweep.py ${SPAN_CASES:-4:1024:shared,4:1024:unique,8:1024:shared,8:1024:unique,2:1024:shared}
            cut -c1-400 $O/spans.log ;;
+    abpipe)
+      for i in ${REPS:-1 2 3}; do
+        step abpipe_seq_$i 300 python bench.py --steps 20 --warmup 3 --legs none --no-cpu-baseline
+        tail -1 $O/abpipe_seq_$i.log | cut -c1-200
+        step abpipe_pipe_$i 300 python bench.py --steps 20 --warmup 3 --legs none --no-cpu-baseline --pipeline
+        tail -1 $O/abpipe_pipe_$i.log | cut -c1-200
+      done ;;
+    spanq)
+      GPU_MAX_HW_QUEUES=4 step spanq4 600 python tools/spans_sweep.py ${SPANQ4:-3:1024,4:1024,5:1024,6:1024,4:1024:shared:32,4:1024:shared:48}
+      cut -c1-260 $O/spanq4.log
+      GPU_MAX_HW_QUEUES=16 step spanq16 600 python tools/spans_sweep.py ${SPANQ16:-4:1024,8:1024}
+      cut -c1-260 $O/spanq16.log ;;
     clileg) step clileg 600 python bench.py --steps 2 --warmup 1 --legs cli
             tail -1 $O/clileg.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(json.dumps(d['configs']['cli']))" ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;

@@ -11,9 +11,14 @@ import torch  # noqa: E402
 import bench  # noqa: E402
 import sequencealigning_amd as saln  # noqa: E402
 
-# cases "spans:band_rows[:edge_masks]" (edge_masks shared | unique, span.py SpanChain)
+# cases "spans:band_rows[:edge_masks[:width]]" (edge_masks shared | unique, span.py
+# SpanChain; width: CUs per span's mask, span r on bits [r*width, (r+1)*width),
+# default 256 / spans)
 cases = [x.split(":") for x in (sys.argv[1] if len(sys.argv) > 1 else "1:4096,8:4096").split(",")]
 for c in cases:
     n, b, em = int(c[0]), int(c[1]), (c[2] if len(c) > 2 else "shared")
-    r = bench.leg_c4_spans(torch, saln, n_spans=n, reps=3, band_rows=b, edge_masks=em)
-    print(os.environ.get("GPU_MAX_HW_QUEUES"), n, b, em, json.dumps(r), flush=True)
+    w = int(c[3]) if len(c) > 3 else 0
+    rng = [(r * w, (r + 1) * w) for r in range(n)] if w else None
+    r = bench.leg_c4_spans(torch, saln, n_spans=n, reps=3, band_rows=b, edge_masks=em,
+                           cu_ranges=rng)
+    print(os.environ.get("GPU_MAX_HW_QUEUES"), n, b, em, w or None, json.dumps(r), flush=True)
