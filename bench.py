@@ -839,9 +839,10 @@ def main() -> None:
                          "'auto' (all at N = 1, c5 at N > 1)")
     ap.add_argument("--score-only", action="store_true",
                     help="score + panic status only (no parent codes / traceback; the C5 mode)")
-    ap.add_argument("--pipeline", action="store_true",
-                    help="overlap step k's traceback with step k+1's fill on a second stream "
-                         "(measured slower on MI355X: the walk slows the VALU-bound fill)")
+    ap.add_argument("--no-pipeline", dest="pipeline", action="store_false",
+                    help="sequential steps: each step's traceback before the next step's fill "
+                         "(default: step k's traceback on the engine's second stream beside "
+                         "step k+1's fill; 2,298-2,337 vs 2,168-2,185 GCUPS on one box, r04)")
     ap.add_argument("--selftest-launch", action="store_true",
                     help="only start the ranks and report the world (no GPU work; tests)")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend (nccl = RCCL)")
@@ -884,9 +885,9 @@ def main() -> None:
     plan = saln.NwPlan(qo, do, pairs=np.stack([np.arange(n), np.arange(n)], 1), device=local)
     dq = torch.from_numpy(qs).to(f"cuda:{local}")
     dd = torch.from_numpy(ds).to(f"cuda:{local}")
-    # --pipeline: the traceback of step k runs on the engine's second stream
-    # while step k+1 fills; results/cigar/mask are double-buffered and every
-    # step's results are complete (and gathered) inside the timed region.
+    # pipelined (default): the traceback of step k runs on the engine's second
+    # stream while step k+1 fills; results/cigar/mask are double-buffered and
+    # every step's results are complete (and gathered) inside the timed region.
     pipelined = args.pipeline and not args.score_only
     plan.set_score_only(args.score_only)
     plan.set_async(pipelined)
@@ -953,6 +954,11 @@ def main() -> None:
                                        "this command (tools/pmc.sh), not measured in this run",
                         traceback_avg_ms=round(tb_ms / max(1, tb_n), 4),
                         execute_avg_ms=round(ex_ms / max(1, ex_n), 4), pipelined=pipelined,
+                        step_frac=round(cells_rank / (dt / args.steps) / 1e9 / HBM_PEAK_GBS, 4),
+                        note=("pipelined: each fill co-runs with the previous step's traceback, "
+                              "so kernel_avg_ms is the fill's co-run duration (longer than "
+                              "alone); step_frac = algorithmic bytes per step / ms_per_step / "
+                              "peak") if pipelined else None,
                         valu=valu_roof(fill_kernel, fill_avg_s) if not args.score_only else None)
         roof["frac"] = round(roof["frac"], 4)
         out = {

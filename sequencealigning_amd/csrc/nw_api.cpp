@@ -2,6 +2,7 @@
 // host batch, reference-text rendering and dense-mask export.  Each one is a
 // thin wrapper: upload -> plan -> saln_nw_execute (GPU) -> download.
 #include <hip/hip_runtime.h>
+#include <sys/mman.h>
 
 #include <algorithm>
 #include <atomic>
@@ -249,17 +250,23 @@ int saln_nw_render_batch(saln_context *ctx, const uint8_t *q_seq, const uint64_t
     }
     std::sort(order.begin(), order.end(), [&](uint64_t x, uint64_t y) { return endb[x] < endb[y]; });
     std::lock_guard<std::mutex> lk(ctx->staging_mu);
-    if (total > ctx->host_mask_bytes) {
-        ctx->host_mask.reset();
-        ctx->host_mask.reset(new (std::nothrow) uint8_t[total]);
-        ctx->host_mask_bytes = ctx->host_mask ? total : 0;
-        if (!ctx->host_mask) {
+    if (total > ctx->host_mask.n) {
+        std::free(ctx->host_mask.p);
+        ctx->host_mask.p = nullptr;
+        ctx->host_mask.n = 0;
+        constexpr size_t kHuge = size_t(2) << 20;
+        const size_t want = (total + kHuge - 1) / kHuge * kHuge;
+        void *hp = nullptr;
+        if (posix_memalign(&hp, kHuge, want) != 0 || !hp) {
             set_error("render batch: host mask buffer allocation failed");
             delete t;
             return SALN_E_HIP;
         }
+        (void)madvise(hp, want, MADV_HUGEPAGE);  // advisory: 4 KB pages if THP is off
+        ctx->host_mask.p = (uint8_t *)hp;
+        ctx->host_mask.n = want;
     }
-    uint8_t *host = ctx->host_mask.get();
+    uint8_t *host = ctx->host_mask.p;
     clock.mark("render: results");
     const double dev_ns =
         (double)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0)

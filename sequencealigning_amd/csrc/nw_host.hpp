@@ -35,11 +35,15 @@ struct saln_context {
     void *pinned = nullptr;
     size_t pinned_bytes = 0;
     // pageable host copy of render batches' mask workspaces (grow-only,
-    // uninitialised; under staging_mu): pinning a GB-sized buffer costs more
-    // than the copy it speeds up (measured: 333 ms to pin, 234 ms to unpin
-    // 1.1 GB, against ~0.1 s for the pageable copy)
-    std::unique_ptr<uint8_t[]> host_mask;
-    size_t host_mask_bytes = 0;
+    // uninitialised, 2 MB-aligned with transparent huge pages requested: the
+    // first copy into 1.1 GB of 4 KB pages spent ~0.17 s in page faults; under
+    // staging_mu): pinning a GB-sized buffer costs more than the copy it
+    // speeds up (measured: 333 ms to pin, 234 ms to unpin 1.1 GB)
+    struct HostBuf {
+        uint8_t *p = nullptr;
+        size_t n = 0;
+        ~HostBuf() { std::free(p); }
+    } host_mask;
 };
 
 // A C-ABI stream argument: NULL = the context's own (non-blocking) stream;

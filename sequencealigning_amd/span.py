@@ -301,8 +301,10 @@ class SpanChain:
                     _lib.check(L.saln_stream_create_cu_range(ctx, lo, hi, C.byref(h)),
                                "saln_stream_create_cu_range")
                     self.cu_streams.append(h)
-                # edge r: every CU ("shared": one mask for all edges), or every
-                # CU but bit n-1-r ("unique": no two edge streams with equal masks)
+                # edge r: every CU ("shared": one mask for all edges), every CU
+                # but bit n-1-r ("unique": no two edge streams with equal
+                # masks), or the last 8 bits ("reserved", experiments: give the
+                # spans cu_ranges below them)
                 nw = (n.value + 31) // 32
                 for r in range(n_spans - 1):
                     words = [0xFFFFFFFF] * nw
@@ -311,6 +313,10 @@ class SpanChain:
                     if edge_masks == "unique":
                         b = n.value - 1 - r
                         words[b // 32] &= ~(1 << (b % 32)) & 0xFFFFFFFF
+                    elif edge_masks == "reserved":  # the last octet (one CU per XCD)
+                        words = [0] * nw
+                        for b in range(n.value - 8, n.value):
+                            words[b // 32] |= 1 << (b % 32)
                     arr = (C.c_uint32 * nw)(*words)
                     h = C.c_void_p()
                     _lib.check(L.saln_stream_create_cu_mask(ctx, arr, nw, C.byref(h)),

@@ -7,7 +7,7 @@
 #   pipetrace  rocprofv3 --kernel-trace of one pipeline case (PIPE_TRACE args)
 #   rowfloor tools/micro/row_pk_floor (C4 row-step floor: i32 K=2 vs i16x2 frames)
 #   spans    tools/spans_sweep.py over SPAN_CASES (spans:band_rows:edge_masks)
-#   abpipe   bench headline sequential vs --pipeline, REPS alternations
+#   abpipe   bench headline --no-pipeline vs pipelined (default), REPS alternations
 #   spanq    span counts under GPU_MAX_HW_QUEUES=4 and 16
 #   clileg   bench.py's cli leg alone (with its stage breakdown)
 #   smoke    __graft_entry__.smoke()
@@ -52,9 +52,9 @@ for st in ${STAGES:-smoke tests bench}; do
            cut -c1-400 $O/spans.log ;;
     abpipe)
       for i in ${REPS:-1 2 3}; do
-        step abpipe_seq_$i 300 python bench.py --steps 20 --warmup 3 --legs none --no-cpu-baseline
+        step abpipe_seq_$i 300 python bench.py --steps 20 --warmup 3 --legs none --no-cpu-baseline --no-pipeline
         tail -1 $O/abpipe_seq_$i.log | cut -c1-200
-        step abpipe_pipe_$i 300 python bench.py --steps 20 --warmup 3 --legs none --no-cpu-baseline --pipeline
+        step abpipe_pipe_$i 300 python bench.py --steps 20 --warmup 3 --legs none --no-cpu-baseline
         tail -1 $O/abpipe_pipe_$i.log | cut -c1-200
       done ;;
     spanq)
@@ -62,6 +62,20 @@ for st in ${STAGES:-smoke tests bench}; do
       cut -c1-260 $O/spanq4.log
       GPU_MAX_HW_QUEUES=16 step spanq16 600 python tools/spans_sweep.py ${SPANQ16:-4:1024,8:1024}
       cut -c1-260 $O/spanq16.log ;;
+    spanx)
+      step spanx 900 python tools/spans_sweep.py ${SPANX:-7:1024,9:1024,10:1024,12:1024,16:1024,4:1024:reserved:62,8:1024:reserved:31}
+      cut -c1-300 $O/spanx.log ;;
+    spantrace)
+      for n in ${SPAN_TRACE_N:-4 8}; do
+        step spantrace_$n 300 rocprofv3 --kernel-trace -d $O/spantrace_$n -o run --output-format csv -- python3 tools/span_trace.py --spans $n
+        python3 tools/span_trace.py --report $O/spantrace_$n --spans $n > $O/spantrace_$n.json || exit 1
+        cut -c1-1500 $O/spantrace_$n.json
+      done ;;
+    spansolo)
+      for n in ${SPAN_SOLO_N:-2 4 8}; do
+        step spansolo_$n 300 python3 tools/span_trace.py --spans $n --solo
+        tail -1 $O/spansolo_$n.log
+      done ;;
     clileg) step clileg 600 python bench.py --steps 2 --warmup 1 --legs cli
             tail -1 $O/clileg.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(json.dumps(d['configs']['cli']))" ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
