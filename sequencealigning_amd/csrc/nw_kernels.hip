@@ -1882,19 +1882,37 @@ __device__ __forceinline__ int32_t wave_prefix_max(int32_t v, Fill &&fill) {
     return v;
 }
 
-template <int K, int kCodes, bool kMinPen>
-__global__ __launch_bounds__(64) void nw_fill_rows_kernel(
+// Workgroups of 1-4 waves (option nw.rows_wpg, default 1: four-wave groups
+// ran C4 in 21.2 ms against 14.2), one stripe per wave (wave v of the launch =
+// blockIdx.x * waves-per-group + the wave's index in the group; n_waves of
+// them).
+// kLone: every wave reserves the whole register file of its SIMD (an AGPR
+// clobber puts the allocation past 256 VGPR+AGPR per lane: one wave per SIMD,
+// MI355X_MICROARCH.md's occupancy table), so no two stripes share a SIMD.
+// The dispatcher otherwise stacks them: 196 one-wave groups on a 64-CU mask
+// landed on 128 SIMDs (tools/cu_occupancy.py), and a stripe that shares its
+// SIMD slows the whole row chain (a span of the 4-span chain alone: 19.8 ms
+// against 12.1 for the 8-span one's).  Used when the launch's stripes fit the
+// SIMDs; waves past them wait for a SIMD, and since workgroups dispatch in
+// order the resident stripes are always the leftmost unfinished ones.
+template <int K, int kCodes, bool kMinPen, bool kLone>
+__global__ __launch_bounds__(256) void nw_fill_rows_kernel(
     const NwPairDesc *__restrict__ pairs, const uint2 *__restrict__ work,
     const uint8_t *__restrict__ qs, const uint8_t *__restrict__ ds, uint8_t *__restrict__ mask,
     int2 *__restrict__ scratch, uint32_t *__restrict__ err, int32_t *__restrict__ end_h,
-    Scoring sc) {
+    Scoring sc, uint32_t n_waves) {
     static_assert(K == 1 || K == 2 || K == 4, "4 cells per code word");
     constexpr int S = 4 / K;   // stripes per 256-column chunk (work item)
     constexpr int W = 64 * K;  // stripe width (4 / K rows per code word)
+    if constexpr (kLone) asm volatile("" : : : "a255");
     const int lane = (int)(threadIdx.x & 63u);
-    const uint2 wk = work[blockIdx.x / S];
+    // (readfirstlane: the slot is wave-uniform, so everything derived from it
+    // stays in SGPRs: the publication base is an asm "s" operand)
+    const uint32_t v = __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
+    if (v >= n_waves) return;  // (whole wave: no group barrier in this kernel)
+    const uint2 wk = work[v / S];
     const NwPairDesc p = pairs[wk.x];
-    const uint32_t g = wk.y * S + blockIdx.x % S;  // stripe index
+    const uint32_t g = wk.y * S + v % S;  // stripe index
     const uint32_t lq = p.len_q, ld = p.len_db;
     const uint32_t c0 = g * W;  // the stripe's columns c0+1 .. c0+W
     if (c0 >= lq) return;
@@ -3217,6 +3235,23 @@ hipError_t launch_span_watch(const int2 *col, uint32_t r0, uint32_t r1, uint32_t
     return hipGetLastError();
 }
 
+// row-fill stripes per workgroup (option nw.rows_wpg)
+static uint32_t rows_wpg() { return (uint32_t)opt(Opt::RowsWpg); }
+
+// one stripe per SIMD (kLone) when a launch's stripes fit the device's SIMDs
+// (option nw.rows_lone)
+static bool rows_lone(uint32_t n_waves) {
+    if (!opt(Opt::RowsLone)) return false;
+    static const uint32_t simds = [] {
+        int dev = 0, cus = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            return 0u;
+        return 4u * (uint32_t)cus;
+    }();
+    return n_waves <= simds;
+}
+
 hipError_t launch_fill_stripes(const NwPairDesc *pairs, const uint2 *work, uint32_t n_work,
                                const uint8_t *qs, const uint8_t *ds, uint8_t *mask,
                                int2 *scratch, uint32_t *prog, uint32_t *err, int32_t *end_h,
@@ -3226,11 +3261,17 @@ hipError_t launch_fill_stripes(const NwPairDesc *pairs, const uint2 *work, uint3
     const bool pk = layout == 1;
     if (layout == 2) {  // row-synchronous stripes of 64 * rows_k columns
         const int32_t pm = 4 * (sc.match - sc.mismatch);
+        const uint32_t wpg = rows_wpg();  // waves (stripes) per workgroup
         auto go = [&](auto k_c, auto codes_c, auto minpen_c) {
             constexpr int kK = decltype(k_c)::value;
-            nw_fill_rows_kernel<kK, decltype(codes_c)::value, decltype(minpen_c)::value>
-                <<<dim3(n_work * (4 / kK)), block, 0, stream>>>(pairs, work, qs, ds, mask, scratch,
-                                                               err, end_h, sc);
+            const uint32_t nw = n_work * (4 / kK);
+            const dim3 g((nw + wpg - 1) / wpg), b(64 * wpg);
+            if (rows_lone(nw))
+                nw_fill_rows_kernel<kK, decltype(codes_c)::value, decltype(minpen_c)::value, true>
+                    <<<g, b, 0, stream>>>(pairs, work, qs, ds, mask, scratch, err, end_h, sc, nw);
+            else
+                nw_fill_rows_kernel<kK, decltype(codes_c)::value, decltype(minpen_c)::value, false>
+                    <<<g, b, 0, stream>>>(pairs, work, qs, ds, mask, scratch, err, end_h, sc, nw);
         };
         auto by_k = [&](auto codes_c, auto minpen_c) {
             if (rows_k == 4) go(std::integral_constant<int, 4>{}, codes_c, minpen_c);

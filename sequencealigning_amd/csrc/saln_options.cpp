@@ -26,6 +26,8 @@ const OptDesc kDesc[kN] = {
     {"nw.avsa_narrow", 1, 0, 1},
     {"nw.nib_codes", 1, 0, 1},
     {"nw.narrow_walk", 1, 0, 1},
+    {"nw.rows_wpg", 1, 1, 4},
+    {"nw.rows_lone", 1, 0, 1},
     {"wfa2.seq_lds", 24 * 1024, 0, 64 * 1024},
     {"wfa2.w1", 0, 0, 4096},
     {"wfa2.w2", 0, 0, 4096},

@@ -24,6 +24,8 @@ enum class Opt : int {
     AvsaNarrow,         // "nw.avsa_narrow": 8 x 19 lane groups for the score-only all-vs-all
     NibCodes,           // "nw.nib_codes": 4-bit walk codes for the short-query packed fills
     NarrowWalk,         // "nw.narrow_walk": 8 x 19 lane groups for queries of <= 152 columns
+    RowsWpg,            // "nw.rows_wpg": row-fill stripes (waves) per workgroup, 1-4
+    RowsLone,           // "nw.rows_lone": a row fill that fits the SIMDs gets one stripe per SIMD
     Wfa2SeqLds,         // "wfa2.seq_lds": LDS bytes for staged sequences (corrected WFA)
     Wfa2W1,             // "wfa2.w1": first-pass ring width (0 auto)
     Wfa2W2,             // "wfa2.w2": second-pass ring width (0 auto)

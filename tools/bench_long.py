@@ -2,7 +2,7 @@
 configs[3] (100 kbp x 100 kbp), G-mut(5%), through a device-resident plan.
 Reports fill / traceback / execute times and GCUPS (cells / execute time).
 
-    python tools/bench_long.py [--len 100000] [--reps 3] [--score-only]
+    python tools/bench_long.py [--len 100000] [--reps 3] [--score-only] [--opt name=value]
 """
 import argparse
 import json
@@ -21,9 +21,13 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--score-only", action="store_true")
     ap.add_argument("--ldb", type=int, default=0, help="db length (default: the mutated query)")
+    ap.add_argument("--opt", action="append", default=[], help="engine option name=value (A/Bs)")
     a = ap.parse_args()
     import torch
     import sequencealigning_amd as saln
+    for o in a.opt:
+        k, v = o.split("=")
+        saln.set_option(k, int(v))
     from sequencealigning_amd import synth
     L = a.len
     q = synth.random_bases(0x5EED0000 + (3 if L > 10_000 else 0), L).tobytes()

@@ -45,9 +45,11 @@ for st in ${STAGES:-smoke tests bench}; do
       done ;;
     pipetrace) step pipetrace 300 rocprofv3 --kernel-trace -d $O/pipetrace -o run --output-format csv -- python3 tools/cu_pipeline.py ${PIPE_TRACE:---walk-cus 32 --layout balanced --steps 10 --warmup 2} --map $O/cu_map.json
                python3 tools/trace_overlap.py $O/pipetrace --out $O/pipe_overlap.json || exit 1 ;;
-    rowfloor) step rowfloor 120 tools/micro/row_pk_floor 782 100000 5
-              step rowfloor2 120 tools/micro/row_pk_floor 1564 50000 5
-              cat $O/rowfloor.log $O/rowfloor2.log ;;
+    rowfloor) step rowfloor 120 tools/micro/row_pk_floor 782 100000 5 1
+              step rowfloor4 120 tools/micro/row_pk_floor 782 100000 5 4
+              step rowfloor2 120 tools/micro/row_pk_floor 1564 50000 5 1
+              step rowfloor24 120 tools/micro/row_pk_floor 1024 50000 5 4
+              cat $O/rowfloor.log $O/rowfloor4.log $O/rowfloor2.log $O/rowfloor24.log ;;
     spans) step spans 600 python tools/spans_sweep.py ${SPAN_CASES:-4:1024:shared,4:1024:unique,8:1024:shared,8:1024:unique,2:1024:shared}
            cut -c1-400 $O/spans.log ;;
     abpipe)
@@ -75,6 +77,38 @@ for st in ${STAGES:-smoke tests bench}; do
       for n in ${SPAN_SOLO_N:-2 4 8}; do
         step spansolo_$n 300 python3 tools/span_trace.py --spans $n --solo
         tail -1 $O/spansolo_$n.log
+      done ;;
+    cuocc) step cuocc 120 python tools/cu_occupancy.py
+           cat $O/cuocc.log | grep mask_cus ;;
+    abwpg)
+      for i in ${REPS:-1 2}; do
+        for w in 1 4; do
+          step abwpg_c4_${w}_$i 200 python tools/bench_long.py --len 100000 --reps 3 --opt nw.rows_wpg=$w
+          echo "wpg=$w $(tail -1 $O/abwpg_c4_${w}_$i.log | cut -c1-300)"
+          step abwpg_c4so_${w}_$i 200 python tools/bench_long.py --len 100000 --reps 3 --score-only --opt nw.rows_wpg=$w
+          echo "wpg=$w so $(tail -1 $O/abwpg_c4so_${w}_$i.log | cut -c1-300)"
+        done
+      done
+      for w in 1 4; do
+        step abwpg_spans_$w 600 python tools/spans_sweep.py 2:1024,4:1024,8:1024 nw.rows_wpg=$w
+        grep -v amdgpu.ids $O/abwpg_spans_$w.log | cut -c1-330 | sed "s/^/wpg=$w /"
+      done
+      step abwpg_c1 200 python tools/bench_long.py --len 1000 --reps 20
+      tail -1 $O/abwpg_c1.log | cut -c1-300 ;;
+    ablone)
+      for i in ${REPS:-1 2}; do
+        for w in 0 1; do
+          step ablone_c4_${w}_$i 200 python tools/bench_long.py --len 100000 --reps 3 --opt nw.rows_lone=$w
+          echo "lone=$w $(tail -1 $O/ablone_c4_${w}_$i.log | cut -c1-300)"
+          step ablone_c4so_${w}_$i 200 python tools/bench_long.py --len 100000 --reps 3 --score-only --opt nw.rows_lone=$w
+          echo "lone=$w so $(tail -1 $O/ablone_c4so_${w}_$i.log | cut -c1-300)"
+        done
+      done
+      for w in 0 1; do
+        step ablone_spans_$w 600 python tools/spans_sweep.py 2:1024,4:1024,8:1024 nw.rows_lone=$w
+        grep -v amdgpu.ids $O/ablone_spans_$w.log | cut -c1-330 | sed "s/^/lone=$w /"
+        step ablone_c1_$w 200 python tools/bench_long.py --len 1000 --reps 20 --opt nw.rows_lone=$w
+        echo "lone=$w c1 $(tail -1 $O/ablone_c1_$w.log | cut -c1-300)"
       done ;;
     clileg) step clileg 600 python bench.py --steps 2 --warmup 1 --legs cli
             tail -1 $O/clileg.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(json.dumps(d['configs']['cli']))" ;;

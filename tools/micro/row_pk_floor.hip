@@ -12,7 +12,7 @@
 //   D~(r+1, c) = max(M~ + O, D~) + Ds,  H~ = max(M~, I~, D~).
 // Checked against a host i32 computation on every wave's last row and
 // published column.  Build: hipcc -O3 --offload-arch=gfx950 row_pk_floor.hip
-// -o row_pk_floor; run: ./row_pk_floor [waves] [rows] [reps]
+// -o row_pk_floor; run: ./row_pk_floor [waves] [rows] [reps] [waves per workgroup]
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -46,6 +46,7 @@ struct Args {
     int2 *pub;            // [waves][rows + 72]: (H~(r, 128), I~ leaving); pad slots
     int32_t *last;        // [waves][128]: H~(rows, c)
     int rows;
+    int waves;
 };
 
 // db chars of rows r .. r+3 from one scalar dword load (rows 4-aligned)
@@ -55,8 +56,9 @@ __device__ __forceinline__ uint32_t dword4(const uint8_t *d, int r) {
 }
 
 // ---------------------------------------------------------------- i32, K = 2
-__global__ __launch_bounds__(64) void rows_i32(Args a) {
-    const int lane = threadIdx.x, wv = blockIdx.x;
+__global__ __launch_bounds__(256) void rows_i32(Args a) {
+    const int lane = threadIdx.x & 63, wv = blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
+    if (wv >= a.waves) return;
     const int R = a.rows;
     const int2 *bd = a.bound + (size_t)wv * (R + 1 + 2 * kG);
     int2 *pub = a.pub + (size_t)wv * (R + 72);
@@ -113,8 +115,9 @@ __global__ __launch_bounds__(64) void rows_i32(Args a) {
 }
 
 // ------------------------------------------------- i16 x 2, per-row frames
-__global__ __launch_bounds__(64) void rows_pk(Args a) {
-    const int lane = threadIdx.x, wv = blockIdx.x;
+__global__ __launch_bounds__(256) void rows_pk(Args a) {
+    const int lane = threadIdx.x & 63, wv = blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
+    if (wv >= a.waves) return;
     const int R = a.rows;
     const int2 *bd = a.bound + (size_t)wv * (R + 1 + 2 * kG);
     int2 *pub = a.pub + (size_t)wv * (R + 72);
@@ -194,8 +197,9 @@ template <int kCtrl>
 __device__ __forceinline__ uint32_t dppz(uint32_t v) {
     return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, kCtrl, 0xf, 0xf, true);
 }
-__global__ __launch_bounds__(64) void rows_pkz(Args a) {
-    const int lane = threadIdx.x, wv = blockIdx.x;
+__global__ __launch_bounds__(256) void rows_pkz(Args a) {
+    const int lane = threadIdx.x & 63, wv = blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
+    if (wv >= a.waves) return;
     const int R = a.rows;
     const int2 *bd = a.bound + (size_t)wv * (R + 1 + 2 * kG);
     int2 *pub = a.pub + (size_t)wv * (R + 72);
@@ -283,7 +287,8 @@ int main(int argc, char **argv) {
     const int waves = argc > 1 ? atoi(argv[1]) : 782;
     const int R = argc > 2 ? atoi(argv[2]) : 100000;
     const int reps = argc > 3 ? atoi(argv[3]) : 5;
-    if (waves < 1 || R < 8 || R % 8) { fprintf(stderr, "waves >= 1, rows >= 8, rows %% 8 == 0\n"); return 2; }
+    const int wpb = argc > 4 ? atoi(argv[4]) : 1;  // waves per workgroup (1..4)
+    if (waves < 1 || R < 8 || R % 8 || wpb < 1 || wpb > 4) { fprintf(stderr, "waves >= 1, rows >= 8, rows %% 8 == 0\n"); return 2; }
     srand(7);
     const char al[4] = {'A', 'C', 'G', 'T'};
     std::vector<uint8_t> q((size_t)waves * W), d(R);
@@ -320,7 +325,7 @@ int main(int argc, char **argv) {
     CK(hipMemcpy(dbd, bd.data(), bd.size() * sizeof(int2), hipMemcpyHostToDevice));
     CK(hipMemcpy(dh0, h0.data(), h0.size() * 4, hipMemcpyHostToDevice));
     CK(hipMemcpy(dd1, d1.data(), d1.size() * 4, hipMemcpyHostToDevice));
-    Args a{dq, dd, dbd, dh0, dd1, dpub, dlast, R};
+    Args a{dq, dd, dbd, dh0, dd1, dpub, dlast, R, waves};
     // host check of waves 0 and waves-1
     const int chk[2] = {0, waves - 1};
     std::vector<std::vector<int32_t>> want_last(2);
@@ -332,16 +337,17 @@ int main(int argc, char **argv) {
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
-    printf("{\"waves\": %d, \"rows\": %d, \"max_rel\": %d", waves, R, maxrel);
+    printf("{\"waves\": %d, \"waves_per_block\": %d, \"rows\": %d, \"max_rel\": %d", waves, wpb, R, maxrel);
     for (int v = 0; v < 3; ++v) {
         const char *name = v == 2 ? "pkz" : v ? "pk" : "i32";
         float best = 1e30f;
         for (int it = 0; it < reps + 1; ++it) {
             CK(hipMemset(dlast, 0, (size_t)waves * W * 4));
             CK(hipEventRecord(e0));
-            if (v == 2) rows_pkz<<<waves, 64>>>(a);
-            else if (v) rows_pk<<<waves, 64>>>(a);
-            else rows_i32<<<waves, 64>>>(a);
+            const int nb = (waves + wpb - 1) / wpb;
+            if (v == 2) rows_pkz<<<nb, 64 * wpb>>>(a);
+            else if (v) rows_pk<<<nb, 64 * wpb>>>(a);
+            else rows_i32<<<nb, 64 * wpb>>>(a);
             CK(hipEventRecord(e1));
             CK(hipEventSynchronize(e1));
             float ms = 0;

@@ -14,6 +14,9 @@ import sequencealigning_amd as saln  # noqa: E402
 # cases "spans:band_rows[:edge_masks[:width]]" (edge_masks shared | unique, span.py
 # SpanChain; width: CUs per span's mask, span r on bits [r*width, (r+1)*width),
 # default 256 / spans)
+for o in [x for x in sys.argv[2:] if "=" in x]:  # engine options name=value (A/Bs)
+    k, v = o.split("=")
+    saln.set_option(k, int(v))
 cases = [x.split(":") for x in (sys.argv[1] if len(sys.argv) > 1 else "1:4096,8:4096").split(",")]
 for c in cases:
     n, b, em = int(c[0]), int(c[1]), (c[2] if len(c) > 2 else "shared")
