@@ -408,7 +408,7 @@ def leg_c1(torch, saln, reps=50, cpu=True):
     gi = synth.random_bases(0x5EED0000 ^ 0x77, 1000).tobytes()
     g, ops = _single_pair(torch, saln, q, d, reps)
     g_iid, ops_iid = _single_pair(torch, saln, q, gi, reps)
-    kern = "nw_fill_rows_kernel<1, 0, true>"
+    kern = "nw_fill_rows_kernel<1, 0, true, true>"  # kLone: 16 stripes, one per SIMD
     fill_s = g["fill_ms"] / 1e3
     out = {"workload": "configs[0]: one 1 kbp x 1 kbp pair, score + first-printed traceback "
                        "(G-mut 5 %; iid beside it)",
@@ -453,7 +453,7 @@ def leg_c4(torch, saln, reps=3, cpu=True):
     d = synth.mutate(q, 0.05, seed=100_000)
     g, ops = _single_pair(torch, saln, q, d, reps)
     torch.cuda.empty_cache()
-    kern = "nw_fill_rows_kernel<2, 0, true>"
+    kern = "nw_fill_rows_kernel<2, 0, true, true>"  # kLone: 782 stripes, one per SIMD
     fill_s = g["fill_ms"] / 1e3
     out = {"workload": "configs[3]: one 100 kbp x 100 kbp pair, G-mut 5 %, fill + 1 B/cell mask "
                        "+ first-printed traceback", "gpu": g, "executes": 1 + reps,
@@ -939,6 +939,18 @@ def main() -> None:
     ex_ms, ex_n = plan.kernel_time("nw_execute")
     cells_rank = plan.cells
     total_cells = cells_rank * world * args.steps
+    # outside the timed region: the fill alone (sequential executes), so the
+    # line carries the kernel's own duration beside its co-run one
+    fill_alone_s = None
+    if pipelined and rank == 0:
+        plan.set_async(False)
+        plan.set_timing(True)
+        for _ in range(5):
+            plan.execute(dq, dd, res[0], cig[0])
+        torch.cuda.synchronize(local)
+        plan.check()
+        fa_ms, fa_n = plan.kernel_time("nw_fill")
+        fill_alone_s = fa_ms / max(1, fa_n) / 1e3
     gcups = total_cells / dt / 1e9
     fill_avg_s = fill_ms / max(1, fill_n) / 1e3
     out = None
@@ -955,10 +967,17 @@ def main() -> None:
                         traceback_avg_ms=round(tb_ms / max(1, tb_n), 4),
                         execute_avg_ms=round(ex_ms / max(1, ex_n), 4), pipelined=pipelined,
                         step_frac=round(cells_rank / (dt / args.steps) / 1e9 / HBM_PEAK_GBS, 4),
+                        kernel_avg_ms_alone=(round(fill_alone_s * 1e3, 4) if fill_alone_s
+                                             else None),
+                        frac_alone=(round(cells_rank / fill_alone_s / 1e9 / HBM_PEAK_GBS, 4)
+                                    if fill_alone_s else None),
                         note=("pipelined: each fill co-runs with the previous step's traceback, "
-                              "so kernel_avg_ms is the fill's co-run duration (longer than "
-                              "alone); step_frac = algorithmic bytes per step / ms_per_step / "
-                              "peak") if pipelined else None,
+                              "so kernel_avg_ms is the fill's co-run duration; "
+                              "kernel_avg_ms_alone / frac_alone: 5 sequential executes after "
+                              "the timed region; step_frac = algorithmic bytes per step / "
+                              "ms_per_step / peak; algorithmic bytes = 1 B/cell (the parent "
+                              "set, SURVEY 8(d)): the fill stores 4-bit walk codes, so its "
+                              "written bytes (traffic) are below it") if pipelined else None,
                         valu=valu_roof(fill_kernel, fill_avg_s) if not args.score_only else None)
         roof["frac"] = round(roof["frac"], 4)
         out = {
