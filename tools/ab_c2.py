@@ -22,6 +22,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--pairs", type=int, default=100_000)
     ap.add_argument("--tag", default="")
+    ap.add_argument("--pipeline", action="store_true",
+                    help="the bench's default loop: step k's walk beside step k+1's fill")
     ap.add_argument("--opt", action="append", default=[],
                     help="engine option name=value (saln_option_set), repeatable")
     a = ap.parse_args()
@@ -35,21 +37,28 @@ def main():
     qs, qo, ds, do = synth.iid_pairs(n, L, L, seed=0x5EED0002)
     plan = saln.NwPlan(qo, do, pairs=np.stack([np.arange(n)] * 2, 1))
     dq, dd = torch.from_numpy(qs).cuda(), torch.from_numpy(ds).cuda()
-    res = torch.zeros(n * 4, dtype=torch.int32, device="cuda")
-    cig = torch.zeros(max(1, plan.cigar_words), dtype=torch.int32, device="cuda")
-    for _ in range(a.warmup):
-        plan.execute(dq, dd, res, cig)
-    torch.cuda.synchronize()
+    nb = 2 if a.pipeline else 1
+    plan.set_async(a.pipeline)
+    res = [torch.zeros(n * 4, dtype=torch.int32, device="cuda") for _ in range(nb)]
+    cig = [torch.zeros(max(1, plan.cigar_words), dtype=torch.int32, device="cuda")
+           for _ in range(nb)]
+
+    def run(k):
+        for i in range(k):
+            plan.execute(dq, dd, res[i % nb], cig[i % nb])
+        if a.pipeline:
+            plan.sync()
+        torch.cuda.synchronize()
+    run(a.warmup)
     plan.set_timing(True)
     t0 = time.perf_counter()
-    for _ in range(a.steps):
-        plan.execute(dq, dd, res, cig)
-    torch.cuda.synchronize()
+    run(a.steps)
     dt = (time.perf_counter() - t0) / a.steps
     plan.check()
     f, fn = plan.kernel_time("nw_fill")
     tb, tn = plan.kernel_time("nw_traceback")
     print(json.dumps({"tag": a.tag, "lib": os.path.basename(_lib.LIB_PATH), "opts": a.opt,
+                      "pipeline": a.pipeline,
                       "gcups": round(plan.cells / dt / 1e9, 1), "ms_per_step": round(dt * 1e3, 4),
                       "fill_ms": round(f / fn, 4), "traceback_ms": round(tb / tn, 4)}))
 

@@ -31,7 +31,7 @@ for st in ${STAGES:-smoke tests bench}; do
         for spec in ${AB:-byte:nw.nib_codes=0 nib16x10: nib8x19:nw.narrow_walk=1}; do
           tag=${spec%%:*}; opts=${spec#*:}; args=""
           for o in ${opts//,/ }; do args="$args --opt $o"; done
-          step ab_${tag}_$i 120 python tools/ab_c2.py --tag $tag $args
+          step ab_${tag}_$i 120 python tools/ab_c2.py --tag $tag $args $AB_ARGS
           tail -1 $O/ab_${tag}_$i.log
         done
       done ;;
