@@ -677,15 +677,20 @@ __global__ __launch_bounds__(256) void nw_traceback_lds_kernel(
     const NwPairDesc *__restrict__ pairs, uint32_t first, uint32_t n,
     const uint8_t *__restrict__ mask, const int32_t *__restrict__ end_h,
     uint32_t *__restrict__ ops, saln_nw_result *__restrict__ results,
-    uint32_t *__restrict__ cigar, Scoring sc, const uint8_t *__restrict__ qs) {
+    uint32_t *__restrict__ cigar, Scoring sc, const uint8_t *__restrict__ qs, uint32_t prio) {
     constexpr uint32_t kWave = WalkGeo<K, kNib, G * K>::kWaveLds;
     __shared__ __attribute__((aligned(16))) uint8_t win_all[tb_lds_threads<G, K, kNib>() / 64u * kWave];
     const uint32_t idx = first + blockIdx.x * blockDim.x + threadIdx.x;
     if (idx >= first + n) return;
-    // The walk is a latency-bound chain; when it shares a SIMD with the
-    // VALU-bound fill of the next batch (pipelined plans) it must not queue
-    // behind the fill's instructions.
-    __builtin_amdgcn_s_setprio(3);
+    // The walk is a latency-bound chain that shares SIMDs with the VALU-bound
+    // fill of the next batch in pipelined plans; its issue priority (option
+    // nw.walk_prio) decides who waits when both are ready.
+    switch (prio) {  // (s_setprio takes an immediate; prio is uniform)
+        case 0: __builtin_amdgcn_s_setprio(0); break;
+        case 1: __builtin_amdgcn_s_setprio(1); break;
+        case 2: __builtin_amdgcn_s_setprio(2); break;
+        default: __builtin_amdgcn_s_setprio(3); break;
+    }
     const NwPairDesc p = pairs[idx];
     lds_u8 *win = (lds_u8 *)(win_all + (threadIdx.x / 64u) * kWave);
     walk_pack_lds<G, K, kNib>(p, end_h[idx], mask, ops, results, cigar, sc, win, qs);
@@ -2990,7 +2995,7 @@ static void tb_lds(hipStream_t s, const NwPairDesc *pairs, uint32_t first, uint3
                    uint32_t *cig, Scoring sc, const uint8_t *qs) {
     constexpr uint32_t nt = tb_lds_threads<G, K, kNib>();
     nw_traceback_lds_kernel<G, K, kNib><<<dim3((n + nt - 1) / nt), dim3(nt), 0, s>>>(
-        pairs, first, n, mask, end_h, ops, res, cig, sc, qs);
+        pairs, first, n, mask, end_h, ops, res, cig, sc, qs, (uint32_t)opt(Opt::WalkPrio));
 }
 
 // Traceback of plan range [first, first+n).  variant >= 0: all pairs of that
