@@ -110,6 +110,15 @@ for st in ${STAGES:-smoke tests bench}; do
         step ablone_c1_$w 200 python tools/bench_long.py --len 1000 --reps 20 --opt nw.rows_lone=$w
         echo "lone=$w c1 $(tail -1 $O/ablone_c1_$w.log | cut -c1-300)"
       done ;;
+    ablone8)
+      for i in 1 2; do
+        for w in 0 1; do
+          step ablone8_${w}_$i 600 python tools/spans_sweep.py 8:1024,8:1024 nw.rows_lone=$w
+          grep -v amdgpu.ids $O/ablone8_${w}_$i.log | python3 -c "import sys,json; [print('lone=$w', l.split()[1], json.loads(l[l.index('{'):])['fill_ms'], json.loads(l[l.index('{'):])['walk_ms']) for l in sys.stdin if '{' in l]"
+        done
+      done
+      step spanleg 600 python bench.py --steps 2 --warmup 1 --legs c4,c4_spans --no-cpu-baseline
+      tail -1 $O/spanleg.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); v=d['configs']['c4_spans']; print(v['fill_ms'], v['walk_ms'])" ;;
     clileg) step clileg 600 python bench.py --steps 2 --warmup 1 --legs cli
             tail -1 $O/clileg.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(json.dumps(d['configs']['cli']))" ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
