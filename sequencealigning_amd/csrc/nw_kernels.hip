@@ -634,33 +634,57 @@ __device__ void walk_pack_lds(const NwPairDesc &p, int32_t hend, const uint8_t *
             retried = true;
         }
     }
-    // CIGAR: the op stream read back in forward order (last recorded op first)
+    // CIGAR: the op stream read back in forward order (last recorded op
+    // first), a run at a time: each word's ten 3-bit ops become 2-bit classes
+    // (0 '=', 1 I, 2 D, 3 X) with a few mask operations, the class changes
+    // between neighbouring slots are a bit mask, and the loop visits the runs
+    // (clz of the changes below the current slot) instead of the ops; the next
+    // word's load is issued a word ahead.
     if (ev == kEvOrigin && !retried) {
         const uint32_t nrec = wi * kOpsPerWord + sh / 3;
         if (sh) counted_store(ops + wi, (uint32_t)(acc & kMask30));
         if (sh > 30) counted_store(ops + wi + 1, (uint32_t)(acc >> 30));
         asm volatile("s_waitcnt vmcnt(0)" : : : "memory");
-        uint32_t run_op = 0, run_len = 0;
-        for (int32_t w = (int32_t)((nrec - 1u) / kOpsPerWord); w >= 0; --w) {
-            const uint32_t word = ops[w];
-            const uint32_t top = (uint32_t)w == (nrec - 1u) / kOpsPerWord
-                                     ? (nrec - 1u) % kOpsPerWord : kOpsPerWord - 1;
-            for (int32_t k = (int32_t)top; k >= 0; --k) {
-                const uint32_t c = (word >> (3 * k)) & 7u;
-                const uint32_t op = (c & 3u) == kStI   ? SALN_CIGAR_I
-                                    : (c & 3u) == kStD ? SALN_CIGAR_D
-                                    : (c & 4u)         ? SALN_CIGAR_EQ : SALN_CIGAR_X;
-                if (run_len && op != run_op) {
-                    if (out) out[nops] = (run_len << 4) | run_op;
-                    ++nops;
+        constexpr uint32_t kSlots = 0x09249249u;  // bit 0 of each 3-bit slot
+        constexpr uint32_t kOpOf = (SALN_CIGAR_X << 12) | (SALN_CIGAR_D << 8) |
+                                   (SALN_CIGAR_I << 4) | SALN_CIGAR_EQ;  // by class
+        static_assert(SALN_CIGAR_X < 16 && SALN_CIGAR_EQ < 16, "4-bit CIGAR ops");
+        uint32_t run_cls = 4u, run_len = 0;
+        int32_t w = (int32_t)((nrec - 1u) / kOpsPerWord);
+        uint32_t word = ops[w], nxt = w > 0 ? ops[w - 1] : 0u;
+        uint32_t top = (nrec - 1u) % kOpsPerWord;
+        for (; w >= 0; --w, top = kOpsPerWord - 1) {
+            const uint32_t cur = word;
+            word = nxt;
+            nxt = w >= 2 ? ops[w - 2] : 0u;
+            const uint32_t s0 = cur & kSlots, s1 = (cur >> 1) & kSlots, e = (cur >> 2) & kSlots;
+            const uint32_t xm = ~(s0 | s1 | e) & kSlots;  // M without the '=' bit: X
+            const uint32_t c0 = s0 | xm, c1 = s1 | xm;    // class bits 0, 1 per slot
+            // slot k (k < top) starts a new run below slot k+1
+            const uint32_t chg = ((c0 ^ (c0 >> 3)) | (c1 ^ (c1 >> 3))) & kSlots &
+                                 ((1u << (3u * top)) - 1u);
+            int32_t pos = (int32_t)top;  // the highest slot not yet counted
+            for (;;) {
+                const uint32_t below = chg & ((1u << (3u * (uint32_t)pos)) - 1u);
+                const int32_t b = below ? (31 - __builtin_clz(below)) / 3 : -1;  // next run's top slot
+                const uint32_t cls = ((c0 >> (3u * (uint32_t)pos)) & 1u) |
+                                     (((c1 >> (3u * (uint32_t)pos)) & 1u) << 1);
+                const uint32_t len = (uint32_t)(pos - b);
+                if (cls != run_cls) {
+                    if (run_len) {
+                        if (out) out[nops] = (run_len << 4) | ((kOpOf >> (4u * run_cls)) & 15u);
+                        ++nops;
+                    }
+                    run_cls = cls;
                     run_len = 0;
                 }
-                run_op = op;
-                ++run_len;
+                run_len += len;
+                if (b < 0) break;
+                pos = b;
             }
         }
         if (run_len) {
-            if (out) out[nops] = (run_len << 4) | run_op;
+            if (out) out[nops] = (run_len << 4) | ((kOpOf >> (4u * run_cls)) & 15u);
             ++nops;
         }
     }

@@ -119,6 +119,15 @@ for st in ${STAGES:-smoke tests bench}; do
       done
       step spanleg 600 python bench.py --steps 2 --warmup 1 --legs c4,c4_spans --no-cpu-baseline
       tail -1 $O/spanleg.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); v=d['configs']['c4_spans']; print(v['fill_ms'], v['walk_ms'])" ;;
+    abbase)  # SALN_LIB=libsaln_base.so (an earlier tree) against the in-tree library
+      for i in ${REPS:-1 2 3}; do
+        for pp in "" "--pipeline"; do
+          SALN_LIB=$PWD/sequencealigning_amd/libsaln_base.so step abbase_b_$i 120 python tools/ab_c2.py --tag base $pp
+          tail -1 $O/abbase_b_$i.log
+          step abbase_n_$i 120 python tools/ab_c2.py --tag new $pp
+          tail -1 $O/abbase_n_$i.log
+        done
+      done ;;
     clileg) step clileg 600 python bench.py --steps 2 --warmup 1 --legs cli
             tail -1 $O/clileg.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(json.dumps(d['configs']['cli']))" ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
