@@ -40,12 +40,15 @@ struct saln_nw_avsa {
     uint32_t *d_fb_qids = nullptr;
     uint32_t n_fb = 0;
     saln_nw_result *d_fb_res = nullptr;
+    uint64_t q_bytes = 0, d_bytes = 0;  // sequence bytes (the ACGT check)
+    uint32_t *d_generic = nullptr;      // 1: a byte outside A, C, G, T (no profiles)
 
     ~saln_nw_avsa() {
         if (fb) saln_nw_plan_destroy(fb);
         for (auto &c : classes) (void)hipFree(c.d_qids);
         for (void *ptr : {(void *)d_qoff, (void *)d_doff, (void *)d_dids, (void *)d_zero_q,
-                          (void *)d_zero_d, (void *)d_fb_qids, (void *)d_fb_res})
+                          (void *)d_zero_d, (void *)d_fb_qids, (void *)d_fb_res,
+                          (void *)d_generic})
             if (ptr) (void)hipFree(ptr);
     }
 };
@@ -121,6 +124,9 @@ int saln_nw_avsa_create(saln_context *ctx, const uint64_t *q_off, uint64_t n_q,
         (variant_packed(v) ? cls[v] : fbq).push_back((uint32_t)q);
     }
     a->cells = sum_q * sum_d;
+    a->q_bytes = q_off[n_q];
+    a->d_bytes = db_off[n_db];
+    HIP_TRY(hipMalloc(&a->d_generic, sizeof(uint32_t)));
     std::vector<uint64_t> qo(q_off, q_off + n_q + 1), dof(db_off, db_off + n_db + 1);
     HIP_TRY(upload(&a->d_qoff, qo));
     HIP_TRY(upload(&a->d_doff, dof));
@@ -173,11 +179,41 @@ int saln_nw_avsa_execute(saln_nw_avsa *a, const uint8_t *d_q_seq, const uint8_t 
     hipStream_t s = resolve_stream(stream, a->ctx);
     int2 *out = reinterpret_cast<int2 *>(d_out);
     const uint32_t nqt = (uint32_t)a->n_q;
+    // the 8 x 19 class runs with query profiles when every byte is A, C, G
+    // or T: checked here on the device, read by the kernel (no host sync)
+    const bool prof = opt(Opt::AvsaProfile) != 0 && a->n_dn >= 2 &&
+                      std::any_of(a->classes.begin(), a->classes.end(),
+                                  [](const saln_nw_avsa::Class &c) { return c.variant == 4; });
+    if (prof) {
+        HIP_TRY(hipMemsetAsync(a->d_generic, 0, sizeof(uint32_t), s));
+        HIP_TRY(launch_acgt_check(d_q_seq, a->q_bytes, a->d_generic, s));
+        HIP_TRY(launch_acgt_check(d_db_seq, a->d_bytes, a->d_generic, s));
+    }
     for (const auto &c : a->classes) {
         // pairs per launch: the dispatch packet's grid size is a 32-bit count
         // of work-items, so the chunk depends on the class's pairs per block
         const uint64_t kChunk = avsa_chunk_pairs(c.variant);
-        const uint64_t total = (uint64_t)c.nq * a->n_dn;
+        uint64_t total = (uint64_t)c.nq * a->n_dn;
+        if (prof && c.variant == 4) {
+            // whole db pairs through the profile kernel, an odd last db record
+            // through the plain one
+            const uint64_t tp = (uint64_t)c.nq * (a->n_dn & ~1u);
+            hipError_t e = hipSuccess;
+            for (uint64_t base = 0; base < tp && e == hipSuccess; base += kChunk) {
+                const uint32_t n = (uint32_t)std::min<uint64_t>(kChunk, tp - base);
+                e = launch_avsa_prof(a->d_qoff, a->d_doff, c.d_qids, c.nq, a->d_dids, nqt, base, n,
+                                     d_q_seq, d_db_seq, out, a->sc, a->ld_max, a->d_generic, s);
+            }
+            if (e == hipSuccess) {
+                if (a->n_dn & 1u)
+                    HIP_TRY(launch_avsa(c.variant, a->d_qoff, a->d_doff, c.d_qids, c.nq,
+                                        a->d_dids + (a->n_dn - 1), nqt, 0, c.nq, d_q_seq, d_db_seq,
+                                        out, a->sc, a->ld_max, s));
+                continue;
+            }
+            if (e != hipErrorInvalidValue) HIP_TRY(e);  // not applicable: the plain path
+            (void)hipGetLastError();
+        }
         for (uint64_t base = 0; base < total; base += kChunk) {
             const uint32_t n = (uint32_t)std::min<uint64_t>(kChunk, total - base);
             HIP_TRY(launch_avsa(c.variant, a->d_qoff, a->d_doff, c.d_qids, c.nq, a->d_dids, nqt,

@@ -149,6 +149,12 @@ hipError_t launch_span_spec(const NwPairDesc *pairs, SpecArgs sa, uint32_t n_blo
 // launch of a packed class may take (0: not a packed variant)
 uint64_t avsa_chunk_pairs(int variant);
 uint64_t avsa_launch_blocks(int variant, uint64_t count);  // workgroups of one launch
+hipError_t launch_avsa_prof(const uint64_t *q_off, const uint64_t *d_off, const uint32_t *q_ids,
+                            uint32_t nq, const uint32_t *d_ids, uint32_t nq_total, uint64_t base,
+                            uint32_t count, const uint8_t *qs, const uint8_t *ds, int2 *out,
+                            Scoring sc, uint32_t ld_max, const uint32_t *generic,
+                            hipStream_t stream);
+hipError_t launch_acgt_check(const uint8_t *seq, uint64_t n, uint32_t *flag, hipStream_t stream);
 hipError_t launch_avsa(int variant, const uint64_t *q_off, const uint64_t *d_off,
                        const uint32_t *q_ids, uint32_t nq, const uint32_t *d_ids,
                        uint32_t nq_total, uint64_t base, uint32_t count, const uint8_t *qs,

@@ -1434,6 +1434,25 @@ struct AvsaSrc {
     }
 };
 
+// The same index space paired for a shared query profile (round 4): pair k is
+// (class query (k/2) % nq, db record 2*((k/2)/nq) + k%2), so the two pairs of
+// a lane group (2g, 2g+1) hold one query against two neighbouring db records
+// (the db list is sorted by length: the halves stay balanced).  nd_pairs
+// counts whole db pairs; an odd last db record goes through AvsaSrc.
+struct AvsaSrcP : AvsaSrc {
+    __device__ __forceinline__ NwPairDesc pair(uint32_t i) const {
+        const uint64_t k = base + i, j = k >> 1;
+        const uint32_t qi = q_ids[j % nq], di = d_ids[2 * (j / nq) + (k & 1)];
+        NwPairDesc p{};
+        p.q_off = q_off[qi];
+        p.db_off = d_off[di];
+        p.len_q = (uint32_t)(q_off[qi + 1] - p.q_off);
+        p.len_db = (uint32_t)(d_off[di + 1] - p.db_off);
+        p.mask_off = (uint64_t)di * nq_total + qi;
+        return p;
+    }
+};
+
 // KS: mask block width (the layout's K, the walker's geometry): a lane's K
 // columns are stored as K/KS segments of KS codes.  KS < K lets a narrower
 // lane group (G*K = the same width, fewer lanes: less pipeline skew, per-step
@@ -1463,12 +1482,18 @@ __host__ __device__ inline int32_t rebase_center(const Scoring &sc, int32_t W) {
 // (the steady loop ~126): built for 3 waves per SIMD instead of 2.
 template <int G, int K, int kCodes>
 constexpr int pk_min_waves() { return kCodes == 3 /* kCodesNib */ && G == 8 ? 3 : 1; }
-template <int G, int K, int kCodes, typename Src, int KS, bool kRebase = false>
-__global__ __launch_bounds__(256, (pk_min_waves<G, K, kCodes>())) void nw_fill_pk_kernel(Src src, uint32_t count,
-                                                         const uint8_t *__restrict__ qs,
-                                                         const uint8_t *__restrict__ ds,
-                                                         uint8_t *__restrict__ mask, Scoring sc,
-                                                         uint32_t ld_max, bool sc_steady) {
+// kProf (score-only all-vs-all, AvsaSrcP): both halves hold one query, so a
+// column's penalty for the row's two db chars is one v_perm of a per-column
+// profile (the penalty against A, C, T, G in bytes 0-3; code = (char >> 1) & 3)
+// with a per-step selector from the row word, instead of an xor and a packed
+// min (and the wait state after the min).  Valid while every query and db
+// byte is one of A, C, G, T (the launch checks the sequences on the device).
+template <int G, int K, int kCodes, typename Src, int KS, bool kRebase = false, bool kProf = false>
+__device__ __forceinline__ void fill_pk_body(Src src, uint32_t count, const uint8_t *__restrict__ qs,
+                                             const uint8_t *__restrict__ ds,
+                                             uint8_t *__restrict__ mask, Scoring sc,
+                                             uint32_t ld_max, bool sc_steady) {
+    static_assert(!kProf || (kCodes == kCodesNone && !kRebase), "profiles: score-only, one frame");
     constexpr int GPB = 256 / G;
     constexpr Geom geo{G, K};
     extern __shared__ uint32_t drow[];  // [GPB][G + ld_max + G] packed db chars (dch) per row
@@ -1501,12 +1526,19 @@ __global__ __launch_bounds__(256, (pk_min_waves<G, K, kCodes>())) void nw_fill_p
     // loop-carried state is kept as plain dwords (2 x i16) so the compiler
     // does not split it into halves
     uint32_t qc[K], Hp[K], Dn[K];
+    const uint32_t pen1 = 2 * (sc.match - sc.mismatch);  // kProf: the mismatch byte
 #pragma unroll
     for (int k = 0; k < K; ++k) {
         const int j = col0 + k + 1;
-        const uint32_t ca = j <= lqA ? (uint32_t)qA[j - 1] << 5 : 0xE000u;
-        const uint32_t cb = j <= lqB ? (uint32_t)qB[j - 1] << 5 : 0xE000u;
-        qc[k] = ca | (cb << 16);
+        if constexpr (kProf) {  // penalty against A, C, T, G (codes 0-3); padding: all mismatch
+            const uint32_t qch = j <= lqA ? (uint32_t)qA[j - 1] : 0u;
+            qc[k] = (qch == 'A' ? 0u : pen1) | (qch == 'C' ? 0u : pen1 << 8) |
+                    (qch == 'T' ? 0u : pen1 << 16) | (qch == 'G' ? 0u : pen1 << 24);
+        } else {
+            const uint32_t ca = j <= lqA ? (uint32_t)qA[j - 1] << 5 : 0xE000u;
+            const uint32_t cb = j <= lqB ? (uint32_t)qB[j - 1] << 5 : 0xE000u;
+            qc[k] = ca | (cb << 16);
+        }
         const int32_t h0 = hs_row0(sc, (uint32_t)j) + beta * j - ctr;     // H~(0, j)
         const int32_t d1 = ds_row1(sc, (uint32_t)j) + alpha + beta * j - ctr;  // D~(1, j)
         Hp[k] = pkb(h0, h0);
@@ -1630,6 +1662,9 @@ __global__ __launch_bounds__(256, (pk_min_waves<G, K, kCodes>())) void nw_fill_p
             const uint32_t endsel = (t == tEA ? 0x0000FFFFu : 0u) | (t == tEB ? 0xFFFF0000u : 0u);
             // argM (bit 0) is only ever read at a pair's end cell: the wave
             // computes it on the steps where one of its lanes holds one.
+            // kProf: bytes 0 / 2 select the profile byte of the A / B db char
+            // (dch = A << 5 | B << 21), bytes 1 / 3 zero
+            const uint32_t psel = kProf ? (((dch >> 6) & 0x00030003u) | 0x0C000C00u) : 0u;
             auto columns = [&](auto with_argm) __attribute__((always_inline)) {
             constexpr bool kM = decltype(with_argm)::value;
             uint32_t diag = hd;  // H~(r-1, c-1) of column k
@@ -1637,7 +1672,8 @@ __global__ __launch_bounds__(256, (pk_min_waves<G, K, kCodes>())) void nw_fill_p
             for (int k = 0; k < K; ++k) {
                 const uint32_t hdk = diag;
                 diag = Hin[k];
-                const uint32_t pen = umin2(qc[k] ^ dch, kPen);
+                const uint32_t pen = kProf ? __builtin_amdgcn_perm(0u, qc[k], psel)
+                                           : umin2(qc[k] ^ dch, kPen);
                 const uint32_t M = hdk - pen;
                 const uint32_t I = F, D = Dn[k];
                 const uint32_t H = umax2(M, umax2(I, D));
@@ -1829,6 +1865,39 @@ __global__ __launch_bounds__(256, (pk_min_waves<G, K, kCodes>())) void nw_fill_p
         step(t + 1, HpB, Hp, G0, 0u);
     }
     if (t < T) step(t, Hp, HpB, G0, 0u);
+}
+
+template <int G, int K, int kCodes, typename Src, int KS, bool kRebase = false>
+__global__ __launch_bounds__(256, (pk_min_waves<G, K, kCodes>())) void nw_fill_pk_kernel(
+    Src src, uint32_t count, const uint8_t *__restrict__ qs, const uint8_t *__restrict__ ds,
+    uint8_t *__restrict__ mask, Scoring sc, uint32_t ld_max, bool sc_steady) {
+    fill_pk_body<G, K, kCodes, Src, KS, kRebase>(src, count, qs, ds, mask, sc, ld_max, sc_steady);
+}
+
+// Score-only all-vs-all with query profiles; *generic (set by
+// nw_acgt_check_kernel earlier on the stream) selects the xor path when a
+// sequence byte is not one of A, C, G, T.
+template <int G, int K>
+__global__ __launch_bounds__(256) void nw_fill_avsa_prof_kernel(
+    AvsaSrcP src, uint32_t count, const uint8_t *__restrict__ qs, const uint8_t *__restrict__ ds,
+    Scoring sc, uint32_t ld_max, bool sc_steady, const uint32_t *__restrict__ generic) {
+    if (__builtin_amdgcn_readfirstlane(*generic))
+        fill_pk_body<G, K, kCodesNone, AvsaSrcP, K, false, false>(src, count, qs, ds, nullptr, sc,
+                                                                  ld_max, sc_steady);
+    else
+        fill_pk_body<G, K, kCodesNone, AvsaSrcP, K, false, true>(src, count, qs, ds, nullptr, sc,
+                                                                 ld_max, sc_steady);
+}
+
+// flag |= 1 when a byte of seq[0, n) is not A, C, G or T
+__global__ __launch_bounds__(256) void nw_acgt_check_kernel(const uint8_t *__restrict__ seq,
+                                                            uint64_t n, uint32_t *__restrict__ flag) {
+    bool bad = false;
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
+        const uint8_t c = seq[i];
+        bad |= c != 'A' && c != 'C' && c != 'G' && c != 'T';
+    }
+    if (__builtin_amdgcn_ballot_w64(bad) && (threadIdx.x & 63u) == 0) atomicOr(flag, 1u);
 }
 
 // Column-stripe fill (declared with the stripe protocol above), i32 lanes.
@@ -2917,6 +2986,43 @@ static hipError_t avsa_pk(const AvsaSrc &src, uint32_t count, const uint8_t *qs,
         return hipSuccess;
     };
     return rebase ? go(std::true_type{}) : go(std::false_type{});
+}
+
+// The 8 x 19 class with query profiles (AvsaSrcP: count even, pairs
+// [base, base + count) of its index space over whole db pairs).  Returns
+// hipErrorInvalidValue where the profile kernel does not apply (a db too long
+// for one int16 frame): the caller runs launch_avsa instead.
+hipError_t launch_avsa_prof(const uint64_t *q_off, const uint64_t *d_off, const uint32_t *q_ids,
+                            uint32_t nq, const uint32_t *d_ids, uint32_t nq_total, uint64_t base,
+                            uint32_t count, const uint8_t *qs, const uint8_t *ds, int2 *out,
+                            Scoring sc, uint32_t ld_max, const uint32_t *generic,
+                            hipStream_t stream) {
+    constexpr int G = 8, K = 19;
+    if (!count) return hipSuccess;
+    if ((count | base) & 1u || !packed_ok(G * K, ld_max, sc)) return hipErrorInvalidValue;
+    AvsaSrcP src;
+    static_cast<AvsaSrc &>(src) = AvsaSrc{q_off, d_off, q_ids, d_ids, nq, nq_total, base, out};
+    const uint64_t blocks = avsa_blocks(G, count);
+    if (blocks * 256 > 0xFFFFFFFFull) return hipErrorInvalidConfiguration;
+    const size_t lds = (size_t)(256 / G) * (ld_max + 2 * G) * 4;
+    if (lds > kPackedLdsMax) return hipErrorInvalidValue;
+    const auto kern = nw_fill_avsa_prof_kernel<G, K>;
+    if (lds > 65536) {
+        const hipError_t e = hipFuncSetAttribute((const void *)kern,
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                 (int)kPackedLdsMax);
+        if (e != hipSuccess) return e;
+    }
+    kern<<<dim3((uint32_t)blocks), dim3(256), lds, stream>>>(src, count, qs, ds, sc, ld_max,
+                                                              pk_steady(), generic);
+    return hipGetLastError();
+}
+
+hipError_t launch_acgt_check(const uint8_t *seq, uint64_t n, uint32_t *flag, hipStream_t stream) {
+    if (!n) return hipSuccess;
+    const uint64_t blocks = std::min<uint64_t>((n + 255) / 256, 2048);
+    nw_acgt_check_kernel<<<dim3((uint32_t)blocks), dim3(256), 0, stream>>>(seq, n, flag);
+    return hipGetLastError();
 }
 
 // Score-only all-vs-all over one packed query class (variant 4-7): pairs

@@ -100,3 +100,25 @@ def test_avsa_narrow_groups_equal_wide(saln, saln_opt):
     saln_opt("nw.avsa_narrow", 0)
     b = saln.nw_score_all_vs_all(queries, dbs)
     assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
+
+
+@pytest.mark.parametrize("nd,alphabet", [(401, b"ACGT"), (400, b"ACGT"), (201, b"ACGTN")])
+def test_avsa_query_profiles_equal_generic(saln, saln_opt, oracle, nd, alphabet):
+    """The 8 x 19 class with query profiles (nw.avsa_profile, AvsaSrcP: a
+    group's two halves share the query; penalties from a per-column v_perm)
+    equals the generic xor path on every pair: an odd db count (the last db
+    record through AvsaSrc), and an N in the data (the device check selects
+    the generic body inside the profile kernel).  A sample against the oracle."""
+    rng = np.random.default_rng(nd)
+    nq = 97
+    queries = [rand_seq(rng, int(n), alphabet) for n in rng.integers(100, 153, nq)]
+    dbs = [rand_seq(rng, int(n), alphabet) for n in rng.integers(100, 161, nd)]
+    s1, t1 = saln.nw_score_all_vs_all(queries, dbs)
+    saln_opt("nw.avsa_profile", 0)
+    s0, t0 = saln.nw_score_all_vs_all(queries, dbs)
+    assert np.array_equal(s1, s0) and np.array_equal(t1, t0)
+    for k in range(40):
+        qi, di = int(rng.integers(nq)), int(rng.integers(nd))
+        o = oracle.nw(queries[qi], dbs[di], literal_dfs=False)
+        assert s1[di, qi] == o.score, (qi, di)
+        assert (t1[di, qi] == saln._lib.REF_PANIC_BOUNDARY) == o.panics, (qi, di)

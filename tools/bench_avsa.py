@@ -22,9 +22,14 @@ def main():
     ap.add_argument("--ndb", type=int, default=100_000)
     ap.add_argument("--len", type=int, default=150)
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--opt", action="append", default=[], help="engine option name=value (A/Bs)")
+    ap.add_argument("--check", action="store_true", help="compare every result with nw.avsa_profile=0")
     a = ap.parse_args()
     import torch
     import sequencealigning_amd as saln
+    for o in a.opt:
+        k, v = o.split("=")
+        saln.set_option(k, int(v))
     from sequencealigning_amd import synth
     seed = 0x5EED0004
     L = a.len
@@ -46,6 +51,13 @@ def main():
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / a.reps
     pairs = a.nq * a.ndb
+    same = None
+    if a.check:  # the same plan's results with the profile path off
+        ref = torch.empty_like(out)
+        with saln.options(**{"nw.avsa_profile": 0}):
+            av.execute(dq, dd, ref)
+        torch.cuda.synchronize()
+        same = bool(torch.equal(out, ref))
     h = out[: 2 * min(pairs, 1 << 20)].cpu().numpy().reshape(-1, 2)
     full_cells = 10_000 * 100_000 * L * L
     gcups = av.cells / dt / 1e9
@@ -54,7 +66,8 @@ def main():
                       "fallback_pairs": av.fallback_pairs, "plan_s": round(setup, 3),
                       "ms": round(dt * 1e3, 3), "gcups": round(gcups, 1), "pairs_per_s": round(pairs / dt, 1),
                       "full_c5_s_at_this_rate_1gpu": round(full_cells / (gcups * 1e9), 1),
-                      "panic_frac_sample": round(float((h[:, 1] == 2).mean()), 4)}))
+                      "panic_frac_sample": round(float((h[:, 1] == 2).mean()), 4),
+                      "opts": a.opt, "equal_without_profile": same}))
     av.close()
 
 

@@ -128,6 +128,15 @@ for st in ${STAGES:-smoke tests bench}; do
           tail -1 $O/abbase_n_$i.log
         done
       done ;;
+    abprof)
+      step abprof_chk 200 python tools/bench_avsa.py --nq 1000 --ndb 100000 --reps 2 --check
+      tail -1 $O/abprof_chk.log | cut -c1-400
+      for i in ${REPS:-1 2}; do
+        for w in 0 1; do
+          step abprof_${w}_$i 200 python tools/bench_avsa.py --nq 1000 --ndb 100000 --reps 3 --opt nw.avsa_profile=$w
+          echo "prof=$w $(tail -1 $O/abprof_${w}_$i.log | cut -c1-300)"
+        done
+      done ;;
     clileg) step clileg 600 python bench.py --steps 2 --warmup 1 --legs cli
             tail -1 $O/clileg.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(json.dumps(d['configs']['cli']))" ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
