@@ -113,6 +113,7 @@ def test_avsa_query_profiles_equal_generic(saln, saln_opt, oracle, nd, alphabet)
     nq = 97
     queries = [rand_seq(rng, int(n), alphabet) for n in rng.integers(100, 153, nq)]
     dbs = [rand_seq(rng, int(n), alphabet) for n in rng.integers(100, 161, nd)]
+    saln_opt("nw.avsa_profile", 1)
     s1, t1 = saln.nw_score_all_vs_all(queries, dbs)
     saln_opt("nw.avsa_profile", 0)
     s0, t0 = saln.nw_score_all_vs_all(queries, dbs)

@@ -52,7 +52,7 @@ def main():
     dt = (time.perf_counter() - t0) / a.reps
     pairs = a.nq * a.ndb
     same = None
-    if a.check:  # the same plan's results with the profile path off
+    if a.check:  # the same plan's results with the profile path off (run with nw.avsa_profile=1)
         ref = torch.empty_like(out)
         with saln.options(**{"nw.avsa_profile": 0}):
             av.execute(dq, dd, ref)

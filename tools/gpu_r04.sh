@@ -129,7 +129,7 @@ for st in ${STAGES:-smoke tests bench}; do
         done
       done ;;
     abprof)
-      step abprof_chk 200 python tools/bench_avsa.py --nq 1000 --ndb 100000 --reps 2 --check
+      step abprof_chk 200 python tools/bench_avsa.py --nq 1000 --ndb 100000 --reps 2 --check --opt nw.avsa_profile=1
       tail -1 $O/abprof_chk.log | cut -c1-400
       for i in ${REPS:-1 2}; do
         for w in 0 1; do
