@@ -299,7 +299,7 @@ def leg_c5(world, rank, local, dist, torch, nq=10_000, ndb=100_000, L=150, cpu=T
     av.check()
     out = None
     if rank == 0:
-        kern = "nw_fill_pk_kernel<8, 19, 2, saln::AvsaSrc, 19"
+        kern = "nw_fill_avsa_prof_kernel<8, 19>"  # query profiles (nw.avsa_profile)
         ins = valu_per_execute(kern, "c5")
         if ins is not None and world > 1:
             ins *= (hi - lo) / ndb  # this rank's share of the profiled (N = 1) launch

@@ -292,3 +292,25 @@ def test_span_chain_custom_scoring_matches_plan(scoring):
         for n in (2, 5):
             r = nw_align_long_spans(q, d, n, scoring=scoring, band_rows=512)
             _same(r, saln.n_w_align(q, d, scoring=scoring))
+
+
+def test_cu_range_streams_cover_every_xcd():
+    """saln_stream_create_cu_range refuses a range that leaves an XCD without a
+    mask bit (that XCD would run unmasked), and a range of 8k bits places its
+    waves on k CUs of every XCD (bit c -> XCD c mod 8, profiles/r04_cu_map.json)."""
+    import ctypes as C
+
+    from sequencealigning_amd import _lib
+    L, ctx = _lib.lib(), _lib.context(0)
+    h = C.c_void_p()
+    assert L.saln_stream_create_cu_range(ctx, 0, 4, C.byref(h)) == _lib.E_INVALID
+    assert L.saln_stream_create_cu_range(ctx, 8, 24, C.byref(h)) == _lib.OK
+    n = 256
+    hw, xc = (C.c_uint32 * n)(), (C.c_uint32 * n)()
+    try:
+        assert L.saln_device_cu_probe(ctx, h, n, hw, xc) == _lib.OK
+    finally:
+        L.saln_stream_destroy(ctx, h)
+    places = {(xc[k] & 0xF, (hw[k] >> 13) & 7, (hw[k] >> 12) & 1, (hw[k] >> 8) & 0xF) for k in range(n)}
+    per_xcd = [sum(1 for p in places if p[0] == x) for x in range(8)]
+    assert per_xcd == [2] * 8, per_xcd
