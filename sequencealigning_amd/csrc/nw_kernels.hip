@@ -1963,7 +1963,10 @@ __device__ __forceinline__ uint32_t stripe_code_word(const uint32_t (&s)[8][4]) 
 // to kColEmpty); stripe g+1 polls kRowsBlk-row blocks (nw_fill_stripe_kernel).
 constexpr int32_t kNegInf = INT32_MIN;
 constexpr uint32_t kRowsOff = 0;  // boundary row r at element r of the column
-constexpr uint32_t kRowsGrp = 8;  // rows per boundary group (round 2: 4 was slower)
+#ifndef SALN_ROWS_GRP
+#define SALN_ROWS_GRP 8  // experiment builds: 4
+#endif
+constexpr uint32_t kRowsGrp = SALN_ROWS_GRP;  // rows per boundary group (round 2: 4 was slower)
 
 // inclusive prefix max over the wave's 64 lanes (lane order).  `fill`:
 // independent work placed inside the chain, where each dependent DPP step

@@ -137,6 +137,18 @@ for st in ${STAGES:-smoke tests bench}; do
           echo "prof=$w $(tail -1 $O/abprof_${w}_$i.log | cut -c1-300)"
         done
       done ;;
+    abg4)  # 4-row boundary groups (libsaln_g4.so) against 8 on C4 / C1 / spans
+      for i in 1 2; do
+        for v in g8 g4; do
+          lib=""; [[ $v == g4 ]] && lib="SALN_LIB=$PWD/sequencealigning_amd/libsaln_g4.so"
+          step abg4_c4_${v}_$i 200 env $lib python tools/bench_long.py --len 100000 --reps 3
+          echo "$v c4 $(tail -1 $O/abg4_c4_${v}_$i.log | cut -c150-330)"
+          step abg4_so_${v}_$i 200 env $lib python tools/bench_long.py --len 100000 --reps 3 --score-only
+          echo "$v so $(tail -1 $O/abg4_so_${v}_$i.log | cut -c150-330)"
+          step abg4_c1_${v}_$i 200 env $lib python tools/bench_long.py --len 1000 --reps 20
+          echo "$v c1 $(tail -1 $O/abg4_c1_${v}_$i.log | cut -c130-300)"
+        done
+      done ;;
     clileg) step clileg 600 python bench.py --steps 2 --warmup 1 --legs cli
             tail -1 $O/clileg.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(json.dumps(d['configs']['cli']))" ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
