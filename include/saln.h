@@ -454,8 +454,8 @@ int saln_wfa_render(saln_context *ctx, const uint8_t *q, uint64_t len_q, const u
  * saln_wfa_align_batch), each pair computed once: one GPU run of the batch
  * with its step logs and alignment rows, then host rendering.  Replaces the
  * size-probe + render pair of saln_wfa_render calls per pair that the pair
- * loop main.rs:61-74 would otherwise make.  Rows are sized for the batch's
- * longest pair; a batch whose rows exceed 16 GB is refused (split it). */
+ * loop main.rs:61-74 would otherwise make.  Large batches run in chunks of
+ * at most ~1 GB of alignment rows and step logs each. */
 typedef struct saln_wfa_text saln_wfa_text;
 int saln_wfa_render_batch(saln_context *ctx, const uint8_t *q_seq, const uint64_t *q_off,
                           uint64_t n_q, const uint8_t *db_seq, const uint64_t *db_off,

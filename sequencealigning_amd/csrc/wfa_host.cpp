@@ -409,9 +409,8 @@ int saln_wfa_render_batch(saln_context *ctx, const uint8_t *q_seq, const uint64_
         *out = t.release();
         return SALN_OK;
     }
-    // one row capacity for the batch: the largest 2 * (len_q + len_db) + 64
-    uint64_t acap = 64;
-    std::vector<int64_t> diag(n_pairs);
+    std::vector<uint32_t> pq(n_pairs), pd(n_pairs);
+    std::vector<uint64_t> acap_k(n_pairs);
     for (uint64_t k = 0; k < n_pairs; ++k) {
         const uint64_t qi = pair_q ? pair_q[k] : k % std::max<uint64_t>(n_q, 1);
         const uint64_t di = pair_db ? pair_db[k] : k / std::max<uint64_t>(n_q, 1);
@@ -419,37 +418,56 @@ int saln_wfa_render_batch(saln_context *ctx, const uint8_t *q_seq, const uint64_
             set_error("pair index out of range");
             return SALN_E_INVALID;
         }
-        const uint64_t lq = q_off[qi + 1] - q_off[qi], ld = db_off[di + 1] - db_off[di];
-        acap = std::max<uint64_t>(acap, 2 * (lq + ld) + 64);
-        diag[k] = (int64_t)lq - (int64_t)ld;
-    }
-    if (acap > 0x7FFFFFFF || n_pairs * 2 * acap > (1ull << 34)) {
-        set_error("saln_wfa_render_batch: alignment rows exceed 16 GB; split the batch");
-        return SALN_E_INVALID;
-    }
-    std::vector<uint8_t> aln(n_pairs * 2 * acap);
-    std::vector<uint64_t> aoff(n_pairs);
-    for (uint64_t k = 0; k < n_pairs; ++k) aoff[k] = k * 2 * acap;
-    Logs logs;
-    int rc = run_wfa(ctx, q_seq, q_off, n_q, db_seq, db_off, n_db, pair_q, pair_db, n_pairs, mode,
-                     max_steps, max_width, t->res.data(), aln.data(), aoff.data(), (uint32_t)acap,
-                     &logs);
-    if (rc != SALN_OK) return rc;
-    const unsigned nth = (unsigned)std::min<uint64_t>(
-        std::max(1u, std::min(16u, std::thread::hardware_concurrency())), (n_pairs + 63) / 64);
-    std::atomic<uint64_t> next{0};
-    auto work = [&] {
-        for (uint64_t k; (k = next.fetch_add(1)) < n_pairs;) {
-            const uint8_t *a = aln.data() + aoff[k];
-            render_pair(t->res[k], logs.lohi.data() + k * 2 * max_steps,
-                        logs.ev.data() + k * logs.ev_cap, logs.ev_cap, a, a + acap,
-                        (uint32_t)acap, diag[k], &t->text[k]);
+        pq[k] = (uint32_t)qi;
+        pd[k] = (uint32_t)di;
+        acap_k[k] = 2 * ((q_off[qi + 1] - q_off[qi]) + (db_off[di + 1] - db_off[di])) + 64;
+        if (acap_k[k] > 0x7FFFFFFF) {
+            set_error("saln_wfa_render_batch: sequence too long");
+            return SALN_E_INVALID;
         }
-    };
-    std::vector<std::thread> th;
-    for (unsigned i = 1; i < nth; ++i) th.emplace_back(work);
-    work();
-    for (auto &x : th) x.join();
+    }
+    // chunks whose host/device buffers (alignment rows sized for the chunk's
+    // longest pair, the per-step lo/hi log and the rec_tr events) stay under
+    // kChunkBytes; each chunk is one GPU run
+    constexpr uint64_t kChunkBytes = 1ull << 30;
+    const uint64_t per_log = 2ull * max_steps * sizeof(int32_t) + ev_cap_for(max_steps);
+    const unsigned hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    for (uint64_t c0 = 0; c0 < n_pairs;) {
+        uint64_t acap = 64, c1 = c0;
+        while (c1 < n_pairs) {
+            const uint64_t cap = std::max(acap, acap_k[c1]);
+            if (c1 > c0 && (c1 + 1 - c0) * (2 * cap + per_log) > kChunkBytes) break;
+            acap = cap;
+            ++c1;
+        }
+        const uint64_t n = c1 - c0;
+        std::vector<uint8_t> aln(n * 2 * acap);
+        std::vector<uint64_t> aoff(n);
+        for (uint64_t k = 0; k < n; ++k) aoff[k] = k * 2 * acap;
+        Logs logs;
+        int rc = run_wfa(ctx, q_seq, q_off, n_q, db_seq, db_off, n_db, pq.data() + c0,
+                         pd.data() + c0, n, mode, max_steps, max_width, t->res.data() + c0,
+                         aln.data(), aoff.data(), (uint32_t)acap, &logs);
+        if (rc != SALN_OK) return rc;
+        const unsigned nth = (unsigned)std::min<uint64_t>(hw, (n + 63) / 64);
+        std::atomic<uint64_t> next{0};
+        auto work = [&] {
+            for (uint64_t k; (k = next.fetch_add(1)) < n;) {
+                const uint64_t g = c0 + k;
+                const uint8_t *al = aln.data() + aoff[k];
+                const long long diag = (long long)(q_off[pq[g] + 1] - q_off[pq[g]]) -
+                                       (long long)(db_off[pd[g] + 1] - db_off[pd[g]]);
+                render_pair(t->res[g], logs.lohi.data() + k * 2 * max_steps,
+                            logs.ev.data() + k * logs.ev_cap, logs.ev_cap, al, al + acap,
+                            (uint32_t)acap, diag, &t->text[g]);
+            }
+        };
+        std::vector<std::thread> th;
+        for (unsigned i = 1; i < nth; ++i) th.emplace_back(work);
+        work();
+        for (auto &x : th) x.join();
+        c0 = c1;
+    }
     *out = t.release();
     return SALN_OK;
 }
