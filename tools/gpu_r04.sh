@@ -122,7 +122,7 @@ for st in ${STAGES:-smoke tests bench}; do
     abbase)  # SALN_LIB=libsaln_base.so (an earlier tree) against the in-tree library
       for i in ${REPS:-1 2 3}; do
         for pp in "" "--pipeline"; do
-          SALN_LIB=$PWD/sequencealigning_amd/libsaln_base.so step abbase_b_$i 120 python tools/ab_c2.py --tag base $pp
+          SALN_LIB=$PWD/sequencealigning_amd/${ABLIB:-libsaln_base.so} step abbase_b_$i 120 python tools/ab_c2.py --tag ${ABLIB:-base} $pp
           tail -1 $O/abbase_b_$i.log
           step abbase_n_$i 120 python tools/ab_c2.py --tag new $pp
           tail -1 $O/abbase_n_$i.log
