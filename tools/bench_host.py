@@ -21,8 +21,12 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--pairs", type=int, default=100_000)
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--opt", action="append", default=[], help="engine option name=value")
     a = ap.parse_args()
     import sequencealigning_amd as saln
+    for o in a.opt:
+        k, v = o.split("=")
+        saln.set_option(k, int(v))
     from sequencealigning_amd import _lib, synth
     qs, qo, ds, do = synth.iid_pairs(a.pairs, 150, 150, seed=0x5EED0002)
     pq = np.arange(a.pairs, dtype=np.uint32)

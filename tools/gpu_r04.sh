@@ -149,6 +149,8 @@ for st in ${STAGES:-smoke tests bench}; do
           echo "$v c1 $(tail -1 $O/abg4_c1_${v}_$i.log | cut -c130-300)"
         done
       done ;;
+    hostt) step hostt 200 python tools/bench_host.py --reps 3 --opt host.timing=1
+           grep -v amdgpu.ids $O/hostt.log | tail -24 ;;
     clileg) step clileg 600 python bench.py --steps 2 --warmup 1 --legs cli
             tail -1 $O/clileg.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(json.dumps(d['configs']['cli']))" ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
