@@ -59,6 +59,26 @@ static int run_batch(saln_context *ctx, const uint8_t *q_seq, const uint64_t *q_
                      uint32_t *cigar, const uint64_t *cigar_off,
                      std::vector<PairMask> *masks_out) {
     StageClock clk;
+    if (!q_off || !db_off || (n_q && !q_seq && q_off[n_q]) || (n_db && !db_seq && db_off[n_db]))
+        return SALN_E_INVALID;
+    // the sequences' upload runs on a helper thread while this one plans (the
+    // plan is host work: descriptors, order, layout), joined before execute
+    DevBuf dq(ctx), dd(ctx), dr(ctx), dc(ctx);
+    const uint64_t qbytes = q_off[n_q], dbytes = db_off[n_db];
+    TRY_HIP(dq.alloc(qbytes));
+    TRY_HIP(dd.alloc(dbytes));
+    hipError_t up_err = hipSuccess;
+    const bool upload = mode == SALN_MODE_GLOBAL;  // other modes: every pair "not implemented"
+    std::thread up([&] {
+        if (!upload) return;
+        up_err = hipSetDevice(ctx->device);
+        if (up_err == hipSuccess && qbytes) up_err = hipMemcpy(dq.p, q_seq, qbytes, hipMemcpyHostToDevice);
+        if (up_err == hipSuccess && dbytes) up_err = hipMemcpy(dd.p, db_seq, dbytes, hipMemcpyHostToDevice);
+    });
+    struct Joiner {
+        std::thread &t;
+        ~Joiner() { if (t.joinable()) t.join(); }
+    } joiner{up};
     PlanGuard g;
     int rc = plan_create(ctx, q_off, n_q, db_off, n_db, pair_q, pair_db, n_pairs, mode, scoring,
                          masks_out != nullptr, &g.p);
@@ -70,18 +90,14 @@ static int run_batch(saln_context *ctx, const uint8_t *q_seq, const uint64_t *q_
         return rc;
     }
     if (rc != SALN_OK) return rc;
-    clk.mark("plan");
+    clk.mark("plan (upload beside it)");
     std::vector<uint64_t> coff(n_pairs + 1);
     saln_nw_cigar_offsets(g.p, coff.data());
     uint64_t cig_words = coff[n_pairs];
-    DevBuf dq(ctx), dd(ctx), dr(ctx), dc(ctx);
-    const uint64_t qbytes = q_off[n_q], dbytes = db_off[n_db];
-    TRY_HIP(dq.alloc(qbytes));
-    TRY_HIP(dd.alloc(dbytes));
     TRY_HIP(dr.alloc(n_pairs * sizeof(saln_nw_result)));
     TRY_HIP(dc.alloc(cig_words * 4));
-    if (qbytes) TRY_HIP(hipMemcpy(dq.p, q_seq, qbytes, hipMemcpyHostToDevice));
-    if (dbytes) TRY_HIP(hipMemcpy(dd.p, db_seq, dbytes, hipMemcpyHostToDevice));
+    up.join();
+    TRY_HIP(up_err);
     clk.mark("alloc+h2d");
     rc = saln_nw_execute(g.p, (const uint8_t *)dq.p, (const uint8_t *)dd.p,
                          (saln_nw_result *)dr.p, (uint32_t *)dc.p, nullptr);
