@@ -151,6 +151,14 @@ for st in ${STAGES:-smoke tests bench}; do
       done ;;
     hostt) step hostt 200 python tools/bench_host.py --reps 3 --opt host.timing=1
            grep -v amdgpu.ids $O/hostt.log | tail -24 ;;
+    abwalk)  # walker variants (sequential steps: the walk's own time)
+      for i in 1 2; do
+        for v in base noeq new; do
+          lib=""; [[ $v != new ]] && lib="SALN_LIB=$PWD/sequencealigning_amd/libsaln_$v.so"
+          step abwalk_${v}_$i 120 env $lib python tools/ab_c2.py --tag $v
+          tail -1 $O/abwalk_${v}_$i.log | cut -c1-220
+        done
+      done ;;
     clileg) step clileg 600 python bench.py --steps 2 --warmup 1 --legs cli
             tail -1 $O/clileg.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(json.dumps(d['configs']['cli']))" ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
