@@ -497,10 +497,6 @@ __device__ void walk_pack_lds(const NwPairDesc &p, int32_t hend, const uint8_t *
             ensure(slot_c);
             for (;;) {
                 if (sh >= 30) flush();  // at most 30 bits per iteration follow
-                // kNib: the cell's query byte is read before the segment, so its
-                // LDS latency runs beside the segment read's (window_seg waits
-                // for both) instead of after it
-                const uint32_t qcur = kNib ? qbyte(tj) : 0u;
                 const u32x4 seg = window_seg<WG::kVmcnt>(wl + S * kSlot);
                 if (sidx != 16u) {  // a cell step in state M, D or at the end cell
                     uint32_t f3, eqb;
@@ -509,7 +505,7 @@ __device__ void walk_pack_lds(const NwPairDesc &p, int32_t hend, const uint8_t *
                         f3 = sidx == 48u ? end_bits(__builtin_amdgcn_ubfe(dw, nib_bit(col), 4))
                                          : __builtin_amdgcn_ubfe(dw, nib_bit(col) + lsh, 3);
                         const uint32_t dch = __builtin_amdgcn_ubfe(pick(seg, kCB >> 2), (kCB & 3u) * 8u, 8);
-                        eqb = qcur == dch ? 1u : 0u;
+                        eqb = qbyte(tj) == dch ? 1u : 0u;
                     } else {
                         const uint32_t dw = pick(seg, col >> 2), b8 = (col & 3u) * 8u;
                         f3 = __builtin_amdgcn_ubfe(dw, b8 + lsh, 3);
