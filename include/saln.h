@@ -120,7 +120,8 @@ int saln_abi_version(void);
  * "nw.tb_chunks", "nw.fill_lds_min", "nw.rows_k", "nw.stripe_pk", "nw.spec",
  * "nw.spec_passes", "nw.spec_strict", "nw.avsa_narrow", "nw.nib_codes",
  * "nw.narrow_walk", "nw.rows_wpg",
- * "nw.rows_lone", "nw.walk_prio", "nw.avsa_profile", "wfa2.seq_lds", "wfa2.w1", "wfa2.w2", "host.timing".
+ * "nw.rows_lone", "nw.walk_prio", "nw.avsa_profile", "nw.pk_tab", "wfa2.seq_lds", "wfa2.w1",
+ * "wfa2.w2", "host.timing".
  * SALN_E_INVALID for an unknown name or a value out of range. */
 int saln_option_set(const char *name, int64_t value);
 int saln_option_get(const char *name, int64_t *value, int64_t *default_value);

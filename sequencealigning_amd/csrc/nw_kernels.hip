@@ -19,6 +19,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdlib>
 #include <type_traits>
 #include <utility>
@@ -1488,12 +1489,31 @@ constexpr int pk_min_waves() { return kCodes == 3 /* kCodesNib */ && G == 8 ? 3 
 // with a per-step selector from the row word, instead of an xor and a packed
 // min (and the wait state after the min).  Valid while every query and db
 // byte is one of A, C, G, T (the launch checks the sequences on the device).
-template <int G, int K, int kCodes, typename Src, int KS, bool kRebase = false, bool kProf = false>
+// kTab (4-bit walk codes, one frame; round 4): alpha = beta = -2*gap_extend,
+// so neither gap extension adds anything (D~(r+1,c) = max(M~ + 2*gap_open,
+// D~), no per-column add) and the diagonal step is M~ = H~(r-1,c-1) + bonus,
+// bonus = 2*match - 4*gap_extend on a match and 2*mismatch - 4*gap_extend
+// otherwise (both in [0, 255]: pk_tab_ok), one v_perm of a constant table
+// selected by (q code ^ d code) in each half's low byte; the row word holds
+// the db codes with 0x0C (v_perm's zero byte) in each half's high byte.
+// Codes are (char >> 1) & 3 for A, C, T, G; a wave with any other byte in its
+// pairs stores the launch's epoch in g_tab_slots[epoch % 1024] and returns
+// before its first step; the fallback launch behind it (kTabMode 2: the
+// generic 4-bit-code body) runs only when that slot holds its epoch, and then
+// only in the waves that found such a byte.  Every value stays within the packed bound: X~ = X' + 2|ge|(r + c)
+// lies in [-(4|go| + ...), rows (2|m| + 2|ge|) + 2|ge| lq] (X' is at least
+// its all-gap path, at most its all-match one).
+__device__ uint32_t g_tab_slots[1024];
+
+template <int G, int K, int kCodes, typename Src, int KS, bool kRebase = false, bool kProf = false,
+          int kTabMode = 0>
 __device__ __forceinline__ void fill_pk_body(Src src, uint32_t count, const uint8_t *__restrict__ qs,
                                              const uint8_t *__restrict__ ds,
                                              uint8_t *__restrict__ mask, Scoring sc,
-                                             uint32_t ld_max, bool sc_steady) {
+                                             uint32_t ld_max, bool sc_steady, uint32_t epoch = 0) {
+    constexpr bool kTab = kTabMode == 1;  // table body; kTabMode 2: the generic body of its bail-outs
     static_assert(!kProf || (kCodes == kCodesNone && !kRebase), "profiles: score-only, one frame");
+    static_assert(!kTab || (kCodes == kCodesNib && !kRebase && !kProf), "tables: 4-bit codes, one frame");
     constexpr int GPB = 256 / G;
     constexpr Geom geo{G, K};
     extern __shared__ uint32_t drow[];  // [GPB][G + ld_max + G] packed db chars (dch) per row
@@ -1513,11 +1533,18 @@ __device__ __forceinline__ void fill_pk_body(Src src, uint32_t count, const uint
     const uint8_t *__restrict__ dB = ds + pb.db_off;
     const int ldM = ldA > ldB ? ldA : ldB;
     const int32_t beta = -2 * sc.gap_extend;
-    const int32_t alpha = -2 * sc.match - beta;
+    const int32_t alpha = kTab ? beta : -2 * sc.match - beta;
     const uint32_t kPen = cst2(2 * (sc.match - sc.mismatch));  // 0 < pen <= 32
     const uint32_t kOpen = cst2(2 * sc.gap_open);
     const uint32_t kDstep = cst2(2 * sc.gap_extend + alpha);
-    const int32_t drift = 2 * sc.gap_extend + alpha;  // column-0 X~ per row (kRebase)
+    const int32_t drift = kTab ? 0 : 2 * sc.gap_extend + alpha;  // column-0 X~ per row
+    // kTab: the diagonal bonus by (q code ^ d code) and the chars of codes 0-3
+    const uint32_t cm = (uint32_t)(2 * sc.match + alpha + beta) & 0xFFu;
+    const uint32_t cmm = (uint32_t)(2 * sc.mismatch + alpha + beta) & 0xFFu;
+    const uint32_t kBonus = cm | cmm * 0x01010100u;
+    constexpr uint32_t kAcgt = 'A' | 'C' << 8 | 'T' << 16 | 'G' << 24;
+    auto acgt = [](uint32_t c) { return c == 'A' || c == 'C' || c == 'G' || c == 'T'; };
+    bool bad = false;  // kTabMode: a byte other than A, C, G, T in this lane's share
     const uint32_t kRebaseAdd = cst2(-drift * kRebaseSteps);
     const int32_t ctr = kRebase ? rebase_center(sc, G * K) : 0;  // frame centring (kRebase)
     const bool gstart = lane == 0;
@@ -1534,9 +1561,15 @@ __device__ __forceinline__ void fill_pk_body(Src src, uint32_t count, const uint
             const uint32_t qch = j <= lqA ? (uint32_t)qA[j - 1] : 0u;
             qc[k] = (qch == 'A' ? 0u : pen1) | (qch == 'C' ? 0u : pen1 << 8) |
                     (qch == 'T' ? 0u : pen1 << 16) | (qch == 'G' ? 0u : pen1 << 24);
+        } else if constexpr (kTab) {  // codes in bytes 0 / 2 (padding: code 0)
+            const uint32_t ca = j <= lqA ? (uint32_t)qA[j - 1] : 'A';
+            const uint32_t cb = j <= lqB ? (uint32_t)qB[j - 1] : 'A';
+            bad |= !acgt(ca) || !acgt(cb);
+            qc[k] = ((ca >> 1) & 3u) | ((cb >> 1) & 3u) << 16;
         } else {
             const uint32_t ca = j <= lqA ? (uint32_t)qA[j - 1] << 5 : 0xE000u;
             const uint32_t cb = j <= lqB ? (uint32_t)qB[j - 1] << 5 : 0xE000u;
+            if constexpr (kTabMode == 2) bad |= (j <= lqA && !acgt(ca >> 5)) || (j <= lqB && !acgt(cb >> 5));
             qc[k] = ca | (cb << 16);
         }
         const int32_t h0 = hs_row0(sc, (uint32_t)j) + beta * j - ctr;     // H~(0, j)
@@ -1561,13 +1594,26 @@ __device__ __forceinline__ void fill_pk_body(Src src, uint32_t count, const uint
     for (int i = lane; i < ldM; i += G) {
         const uint32_t ca = i < ldA ? (uint32_t)dA[i] : 0u;
         const uint32_t cb = i < ldB ? (uint32_t)dB[i] : 0u;
-        if constexpr (kRebase)
+        if constexpr (kRebase) {
             myrow16[i] = (uint16_t)(ca | (cb << 8));
-        else
+        } else if constexpr (kTab) {
+            bad |= (i < ldA && !acgt(ca)) || (i < ldB && !acgt(cb));
+            myrow[i] = ((ca >> 1) & 3u) | ((cb >> 1) & 3u) << 16 | 0x0C000C00u;
+        } else {
+            if constexpr (kTabMode == 2) bad |= (i < ldA && !acgt(ca)) || (i < ldB && !acgt(cb));
             myrow[i] = (ca << 5) | (cb << 21);
+        }
     }
     asm volatile("s_waitcnt lgkmcnt(0)" : : : "memory");
     __builtin_amdgcn_wave_barrier();
+    if constexpr (kTabMode == 1) {
+        if (__builtin_amdgcn_ballot_w64(bad)) {  // the wave is left to the fallback launch
+            g_tab_slots[epoch & 1023u] = epoch;
+            return;
+        }
+    } else if constexpr (kTabMode == 2) {
+        if (!__builtin_amdgcn_ballot_w64(bad)) return;  // done by the table launch
+    }
     // end-cell owners
     const int lA = (lqA - 1) / K, kA = (lqA - 1) % K;
     const int lB = hasB ? (lqB - 1) / K : -1, kB = hasB ? (lqB - 1) % K : 0;
@@ -1673,8 +1719,9 @@ __device__ __forceinline__ void fill_pk_body(Src src, uint32_t count, const uint
                 const uint32_t hdk = diag;
                 diag = Hin[k];
                 const uint32_t pen = kProf ? __builtin_amdgcn_perm(0u, qc[k], psel)
-                                           : umin2(qc[k] ^ dch, kPen);
-                const uint32_t M = hdk - pen;
+                                     : kTab  ? __builtin_amdgcn_perm(0u, kBonus, qc[k] ^ dch)
+                                             : umin2(qc[k] ^ dch, kPen);
+                const uint32_t M = kTab ? hdk + pen : hdk - pen;
                 const uint32_t I = F, D = Dn[k];
                 const uint32_t H = umax2(M, umax2(I, D));
                 const uint32_t tO = M + kOpen;
@@ -1753,7 +1800,7 @@ __device__ __forceinline__ void fill_pk_body(Src src, uint32_t count, const uint
                 }
                 }
                 F = umax2(tO, I);
-                Dn[k] = umax2(tO, D) + kDstep;
+                Dn[k] = kTab ? umax2(tO, D) : umax2(tO, D) + kDstep;
                 Hout[k] = H;
             }
             };
@@ -1776,7 +1823,8 @@ __device__ __forceinline__ void fill_pk_body(Src src, uint32_t count, const uint
                 // -> per-pair halves, two groups per dword; the db chars
                 // (dch = A << 5 | B << 21) rotated to bytes 0 / 2
                 constexpr int NG = (K + 3) / 4, ND = NG / 2 + 1;
-                const uint32_t rot = __builtin_amdgcn_alignbit(dch, dch, 5);
+                const uint32_t rot = kTab ? __builtin_amdgcn_perm(0u, kAcgt, dch)
+                                          : __builtin_amdgcn_alignbit(dch, dch, 5);
                 NibSeg<K> na, nb;
 #pragma unroll
                 for (int d = 0; d < NG / 2; ++d) {
@@ -1872,6 +1920,26 @@ __global__ __launch_bounds__(256, (pk_min_waves<G, K, kCodes>())) void nw_fill_p
     Src src, uint32_t count, const uint8_t *__restrict__ qs, const uint8_t *__restrict__ ds,
     uint8_t *__restrict__ mask, Scoring sc, uint32_t ld_max, bool sc_steady) {
     fill_pk_body<G, K, kCodes, Src, KS, kRebase>(src, count, qs, ds, mask, sc, ld_max, sc_steady);
+}
+
+// 4-bit walk codes with table penalties (kTabMode 1, nw.pk_tab), and the
+// launch behind it for the waves whose pairs hold a byte other than A, C, G, T
+// (kTabMode 2; its waves return at once unless the table launch of `epoch`
+// left work).  Two kernels, not one with both bodies: together they spill.
+template <int G, int K, typename Src>
+__global__ __launch_bounds__(256, (pk_min_waves<G, K, kCodesNib>())) void nw_fill_pk_tab_kernel(
+    Src src, uint32_t count, const uint8_t *__restrict__ qs, const uint8_t *__restrict__ ds,
+    uint8_t *__restrict__ mask, Scoring sc, uint32_t ld_max, bool sc_steady, uint32_t epoch) {
+    fill_pk_body<G, K, kCodesNib, Src, K, false, false, 1>(src, count, qs, ds, mask, sc, ld_max,
+                                                            sc_steady, epoch);
+}
+template <int G, int K, typename Src>
+__global__ __launch_bounds__(256, (pk_min_waves<G, K, kCodesNib>())) void nw_fill_pk_tabfb_kernel(
+    Src src, uint32_t count, const uint8_t *__restrict__ qs, const uint8_t *__restrict__ ds,
+    uint8_t *__restrict__ mask, Scoring sc, uint32_t ld_max, bool sc_steady, uint32_t epoch) {
+    if (__builtin_amdgcn_readfirstlane(g_tab_slots[epoch & 1023u]) != epoch) return;
+    fill_pk_body<G, K, kCodesNib, Src, K, false, false, 2>(src, count, qs, ds, mask, sc, ld_max,
+                                                            sc_steady, epoch);
 }
 
 // Score-only all-vs-all with query profiles; *generic (set by
@@ -2898,6 +2966,13 @@ static void fill_i32(dim3 grid, hipStream_t s, const NwPairDesc *pairs, uint32_t
     else by_pen(std::integral_constant<int, kCodesWalk>{});
 }
 
+// The table-penalty fill's bonuses fit a byte (fill_pk_body, kTab) and its
+// frame's floor, a few opens below zero, stays far inside int16.
+static bool pk_tab_ok(const Scoring &sc) {
+    const int64_t cm = 2ll * sc.match - 4ll * sc.gap_extend, cmm = 2ll * sc.mismatch - 4ll * sc.gap_extend;
+    return cmm >= 0 && cm <= 255 && cmm < cm && -(int64_t)sc.gap_open <= 2000;
+}
+
 template <int G, int K, int KS = K>
 static hipError_t fill_pk(dim3 grid, hipStream_t s, const NwPairDesc *pairs, uint32_t first,
                           uint32_t count, const uint8_t *qs, const uint8_t *ds, uint8_t *mask,
@@ -2910,6 +2985,25 @@ static hipError_t fill_pk(dim3 grid, hipStream_t s, const NwPairDesc *pairs, uin
     auto go = [&](auto codes_c, auto rebase_c) -> hipError_t {
         const auto kern = nw_fill_pk_kernel<G, K, decltype(codes_c)::value, PlanSrc, KS,
                                             decltype(rebase_c)::value>;
+        if constexpr (decltype(codes_c)::value == kCodesNib && !decltype(rebase_c)::value && KS == K) {
+            if (opt(Opt::PkTab) && pk_tab_ok(sc)) {
+                static std::atomic<uint32_t> epochs{0};
+                const uint32_t ep = epochs.fetch_add(1, std::memory_order_relaxed) + 1;
+                if (lds > 65536) {
+                    for (const void *f : {(const void *)nw_fill_pk_tab_kernel<G, K, PlanSrc>,
+                                          (const void *)nw_fill_pk_tabfb_kernel<G, K, PlanSrc>}) {
+                        const hipError_t e = hipFuncSetAttribute(
+                            f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kPackedLdsMax);
+                        if (e != hipSuccess) return e;
+                    }
+                }
+                nw_fill_pk_tab_kernel<G, K, PlanSrc><<<grid, dim3(256), lds, s>>>(
+                    src, count, qs, ds, mask, sc, ld_max, pk_steady(), ep);
+                nw_fill_pk_tabfb_kernel<G, K, PlanSrc><<<grid, dim3(256), lds, s>>>(
+                    src, count, qs, ds, mask, sc, ld_max, pk_steady(), ep);
+                return hipSuccess;
+            }
+        }
         if (lds > 65536) {
             const hipError_t e = hipFuncSetAttribute((const void *)kern,
                                                      hipFuncAttributeMaxDynamicSharedMemorySize,

@@ -28,6 +28,7 @@ enum class Opt : int {
     RowsLone,           // "nw.rows_lone": a row fill that fits the SIMDs gets one stripe per SIMD
     WalkPrio,           // "nw.walk_prio": issue priority (s_setprio) of the LDS walker's waves
     AvsaProfile,        // "nw.avsa_profile": query-profile penalties in the 8 x 19 all-vs-all fill
+    PkTab,              // "nw.pk_tab": table penalties + extension-free frame in the 4-bit-code fills
     Wfa2SeqLds,         // "wfa2.seq_lds": LDS bytes for staged sequences (corrected WFA)
     Wfa2W1,             // "wfa2.w1": first-pass ring width (0 auto)
     Wfa2W2,             // "wfa2.w2": second-pass ring width (0 auto)

@@ -213,6 +213,60 @@ def test_walk_code_formats_match_oracle(saln, oracle, saln_opt, nib, narrow):
         assert (saln.cigar_ops_string(cg[k]) if res["printed"][k] else None) == o.first_ops, k
 
 
+def _run_plan(saln, qs, qo, ds, do, scoring=None):
+    import torch
+    n = len(qo) - 1
+    plan = saln.NwPlan(qo, do, pairs=np.stack([np.arange(n), np.arange(n)], 1), scoring=scoring)
+    dq, dd = torch.from_numpy(qs).cuda(), torch.from_numpy(ds).cuda()
+    res_t = torch.zeros(n * 4, dtype=torch.int32, device="cuda")
+    cig_t = torch.zeros(max(1, plan.cigar_words), dtype=torch.int32, device="cuda")
+    plan.execute(dq, dd, res_t, cig_t)
+    torch.cuda.synchronize()
+    plan.check()
+    res = res_t.cpu().numpy().view(saln._lib.RESULT_DTYPE).copy()
+    cig = cig_t.cpu().numpy().view(np.uint32).copy()
+    off = np.array(plan.cigar_off, copy=True)
+    plan.close()
+    return res, cig, off
+
+
+@pytest.mark.parametrize("case", ["acgt", "with_n", "scheme"])
+def test_table_fill_equals_generic(saln, oracle, saln_opt, case):
+    """nw.pk_tab = 1 (the 4-bit-code fill with table penalties in the
+    extension-free frame, and its fallback launch for the waves whose pairs
+    hold a byte other than A, C, G, T) equals nw.pk_tab = 0 on 20,000
+    configs[1]-shaped pairs: every result field and every CIGAR word.  "acgt"
+    is also checked against the oracle pair by pair; "with_n" puts an N into
+    1 % of the queries and 1 % of the dbs (those waves take the fallback
+    launch, the rest of the launch the table body); "scheme" uses
+    {2, -3, -5, -2} (bonuses 12 / 2)."""
+    from sequencealigning_amd import synth
+    n, L = 20_000, 150
+    qs, qo, ds, do = synth.iid_pairs(n, L, L, seed=0x7AB0 + len(case))
+    qs, ds = qs.copy(), ds.copy()
+    scoring = (2, -3, -5, -2) if case == "scheme" else None
+    if case == "with_n":
+        rng = np.random.default_rng(77)
+        for buf, off in ((qs, qo), (ds, do)):
+            for k in rng.choice(n, n // 100, replace=False):
+                buf[int(off[k]) + int(rng.integers(L))] = ord("N")
+    saln_opt("nw.pk_tab", 1)
+    r1, c1, o1 = _run_plan(saln, qs, qo, ds, do, scoring)
+    saln_opt("nw.pk_tab", 0)
+    r0, c0, o0 = _run_plan(saln, qs, qo, ds, do, scoring)
+    assert np.array_equal(r1, r0)
+    assert np.array_equal(o1, o0) and np.array_equal(c1, c0)
+    if case == "acgt":
+        want = oracle.check_pairs(qs, qo, ds, do)
+        assert np.array_equal(r1["score"], want.score)
+        assert np.array_equal(r1["end_states"], want.end_states)
+        assert np.array_equal(r1["status"] == saln._lib.REF_PANIC_BOUNDARY, want.panics)
+        for k in range(0, n, 7):
+            if r1["printed"][k]:
+                got = c1[int(o1[k]):int(o1[k]) + int(r1["cigar_len"][k])]
+                assert np.array_equal(got, want.cigar_words(k)), k
+
+
 def test_pipelined_plan_matches_sync(saln):
     """saln_nw_plan_set_async: tracebacks overlap the next fill through two
     mask workspaces; five pipelined executes (ragged lengths, several

@@ -159,6 +159,15 @@ for st in ${STAGES:-smoke tests bench}; do
           tail -1 $O/abwalk_${v}_$i.log | cut -c1-220
         done
       done ;;
+    abtab)  # table-penalty fill (nw.pk_tab) against the default: sequential and pipelined steps
+      for i in 1 2; do
+        for w in 0 1; do
+          step abtab_${w}_$i 120 python tools/ab_c2.py --tag tab$w --opt nw.pk_tab=$w
+          tail -1 $O/abtab_${w}_$i.log | cut -c1-220
+          step abtabp_${w}_$i 120 python tools/ab_c2.py --pipeline --tag tab$w --opt nw.pk_tab=$w
+          tail -1 $O/abtabp_${w}_$i.log | cut -c1-220
+        done
+      done ;;
     clileg) step clileg 600 python bench.py --steps 2 --warmup 1 --legs cli
             tail -1 $O/clileg.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(json.dumps(d['configs']['cli']))" ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
