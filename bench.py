@@ -958,7 +958,9 @@ def main() -> None:
         last = (args.steps - 1) % nbuf if args.steps else 0
         hr = res[last].cpu().numpy()
         statuses = np.bincount(hr[1::4] & 0xFF, minlength=3)
-        fill_kernel = "nw_fill_pk_kernel<8, 19, 3,"  # 8 x 19 groups, 4-bit walk codes
+        # 8 x 19 groups, 4-bit walk codes (table penalties unless nw.pk_tab = 0)
+        fill_kernel = ("nw_fill_pk_tab_kernel<8, 19," if saln._lib.get_option("nw.pk_tab")[0]
+                       else "nw_fill_pk_kernel<8, 19, 3,")
         roof = roof_hbm(cells_rank, fill_avg_s, "nw_fill",
                         pmc(fill_kernel) if not args.score_only else None,
                         traffic_unit="bytes/launch (PMC FETCH_SIZE*2 + WRITE_SIZE)",

@@ -30,7 +30,7 @@ const OptDesc kDesc[kN] = {
     {"nw.rows_lone", 1, 0, 1},
     {"nw.walk_prio", 3, 0, 3},
     {"nw.avsa_profile", 1, 0, 1},
-    {"nw.pk_tab", 0, 0, 1},
+    {"nw.pk_tab", 1, 0, 1},
     {"wfa2.seq_lds", 24 * 1024, 0, 64 * 1024},
     {"wfa2.w1", 0, 0, 4096},
     {"wfa2.w2", 0, 0, 4096},

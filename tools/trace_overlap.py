@@ -18,7 +18,7 @@ def main():
     f = sorted(glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True))[-1]
     rows = list(csv.DictReader(open(f)))
     ks = [(int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]) for r in rows]
-    fills = sorted((s, e) for s, e, n in ks if "nw_fill_pk_kernel" in n)
+    fills = sorted((s, e) for s, e, n in ks if "nw_fill_pk_kernel" in n or "nw_fill_pk_tab_kernel" in n)
     walks = sorted((s, e) for s, e, n in ks if "nw_traceback_lds_kernel" in n)
     fr = []
     for s, e in walks:
