@@ -278,7 +278,7 @@ def leg_c5(world, rank, local, dist, torch, nq=10_000, ndb=100_000, L=150, cpu=T
     C2), G-iid (seed 0x5EED0004), score-only all-vs-all with
     the db sharded over the ranks and the records gathered to rank 0
     (dist.ShardedAllVsAll).  Total work is fixed as N grows (strong)."""
-    from sequencealigning_amd import synth
+    from sequencealigning_amd import _lib, synth
     from sequencealigning_amd.dist import ShardedAllVsAll, shard_db
     seed = 0x5EED0004
     qs = synth.random_bases(seed, nq * L)
@@ -299,7 +299,9 @@ def leg_c5(world, rank, local, dist, torch, nq=10_000, ndb=100_000, L=150, cpu=T
     av.check()
     out = None
     if rank == 0:
-        kern = "nw_fill_avsa_prof_kernel<8, 19>"  # query profiles (nw.avsa_profile)
+        # query profiles (nw.avsa_profile), bonuses in the extension-free frame (nw.pk_tab)
+        kern = "nw_fill_avsa_prof_kernel<8, 19, %s>" % (
+            "true" if _lib.get_option("nw.pk_tab")[0] else "false")
         ins = valu_per_execute(kern, "c5")
         if ins is not None and world > 1:
             ins *= (hi - lo) / ndb  # this rank's share of the profiled (N = 1) launch

@@ -1512,6 +1512,10 @@ __device__ __forceinline__ void fill_pk_body(Src src, uint32_t count, const uint
                                              uint8_t *__restrict__ mask, Scoring sc,
                                              uint32_t ld_max, bool sc_steady, uint32_t epoch = 0) {
     constexpr bool kTab = kTabMode == 1;  // table body; kTabMode 2: the generic body of its bail-outs
+    // the extension-free frame (alpha = beta = -2*gap_extend, M~ = H~ + bonus):
+    // the table body, and kTabMode 3 = query profiles holding bonuses
+    constexpr bool kFree = kTabMode == 1 || kTabMode == 3;
+    static_assert(kTabMode != 3 || kProf, "kTabMode 3: query profiles");
     static_assert(!kProf || (kCodes == kCodesNone && !kRebase), "profiles: score-only, one frame");
     static_assert(!kTab || (kCodes == kCodesNib && !kRebase && !kProf), "tables: 4-bit codes, one frame");
     constexpr int GPB = 256 / G;
@@ -1533,11 +1537,11 @@ __device__ __forceinline__ void fill_pk_body(Src src, uint32_t count, const uint
     const uint8_t *__restrict__ dB = ds + pb.db_off;
     const int ldM = ldA > ldB ? ldA : ldB;
     const int32_t beta = -2 * sc.gap_extend;
-    const int32_t alpha = kTab ? beta : -2 * sc.match - beta;
+    const int32_t alpha = kFree ? beta : -2 * sc.match - beta;
     const uint32_t kPen = cst2(2 * (sc.match - sc.mismatch));  // 0 < pen <= 32
     const uint32_t kOpen = cst2(2 * sc.gap_open);
     const uint32_t kDstep = cst2(2 * sc.gap_extend + alpha);
-    const int32_t drift = kTab ? 0 : 2 * sc.gap_extend + alpha;  // column-0 X~ per row
+    const int32_t drift = kFree ? 0 : 2 * sc.gap_extend + alpha;  // column-0 X~ per row
     // kTab: the diagonal bonus by (q code ^ d code) and the chars of codes 0-3
     const uint32_t cm = (uint32_t)(2 * sc.match + alpha + beta) & 0xFFu;
     const uint32_t cmm = (uint32_t)(2 * sc.mismatch + alpha + beta) & 0xFFu;
@@ -1557,7 +1561,11 @@ __device__ __forceinline__ void fill_pk_body(Src src, uint32_t count, const uint
 #pragma unroll
     for (int k = 0; k < K; ++k) {
         const int j = col0 + k + 1;
-        if constexpr (kProf) {  // penalty against A, C, T, G (codes 0-3); padding: all mismatch
+        if constexpr (kProf && kFree) {  // bonus against A, C, T, G; padding: all mismatch
+            const uint32_t qch = j <= lqA ? (uint32_t)qA[j - 1] : 0u;
+            qc[k] = (qch == 'A' ? cm : cmm) | (qch == 'C' ? cm : cmm) << 8 |
+                    (qch == 'T' ? cm : cmm) << 16 | (qch == 'G' ? cm : cmm) << 24;
+        } else if constexpr (kProf) {  // penalty against A, C, T, G (codes 0-3); padding: all mismatch
             const uint32_t qch = j <= lqA ? (uint32_t)qA[j - 1] : 0u;
             qc[k] = (qch == 'A' ? 0u : pen1) | (qch == 'C' ? 0u : pen1 << 8) |
                     (qch == 'T' ? 0u : pen1 << 16) | (qch == 'G' ? 0u : pen1 << 24);
@@ -1721,7 +1729,7 @@ __device__ __forceinline__ void fill_pk_body(Src src, uint32_t count, const uint
                 const uint32_t pen = kProf ? __builtin_amdgcn_perm(0u, qc[k], psel)
                                      : kTab  ? __builtin_amdgcn_perm(0u, kBonus, qc[k] ^ dch)
                                              : umin2(qc[k] ^ dch, kPen);
-                const uint32_t M = kTab ? hdk + pen : hdk - pen;
+                const uint32_t M = kFree ? hdk + pen : hdk - pen;
                 const uint32_t I = F, D = Dn[k];
                 const uint32_t H = umax2(M, umax2(I, D));
                 const uint32_t tO = M + kOpen;
@@ -1800,7 +1808,7 @@ __device__ __forceinline__ void fill_pk_body(Src src, uint32_t count, const uint
                 }
                 }
                 F = umax2(tO, I);
-                Dn[k] = kTab ? umax2(tO, D) : umax2(tO, D) + kDstep;
+                Dn[k] = kFree ? umax2(tO, D) : umax2(tO, D) + kDstep;
                 Hout[k] = H;
             }
             };
@@ -1945,7 +1953,8 @@ __global__ __launch_bounds__(256, (pk_min_waves<G, K, kCodesNib>())) void nw_fil
 // Score-only all-vs-all with query profiles; *generic (set by
 // nw_acgt_check_kernel earlier on the stream) selects the xor path when a
 // sequence byte is not one of A, C, G, T.
-template <int G, int K>
+// kFree: profiles of bonuses in the extension-free frame (nw.pk_tab, pk_tab_ok).
+template <int G, int K, bool kFree>
 __global__ __launch_bounds__(256) void nw_fill_avsa_prof_kernel(
     AvsaSrcP src, uint32_t count, const uint8_t *__restrict__ qs, const uint8_t *__restrict__ ds,
     Scoring sc, uint32_t ld_max, bool sc_steady, const uint32_t *__restrict__ generic) {
@@ -1953,8 +1962,8 @@ __global__ __launch_bounds__(256) void nw_fill_avsa_prof_kernel(
         fill_pk_body<G, K, kCodesNone, AvsaSrcP, K, false, false>(src, count, qs, ds, nullptr, sc,
                                                                   ld_max, sc_steady);
     else
-        fill_pk_body<G, K, kCodesNone, AvsaSrcP, K, false, true>(src, count, qs, ds, nullptr, sc,
-                                                                 ld_max, sc_steady);
+        fill_pk_body<G, K, kCodesNone, AvsaSrcP, K, false, true, kFree ? 3 : 0>(
+            src, count, qs, ds, nullptr, sc, ld_max, sc_steady);
 }
 
 // flag |= 1 when a byte of seq[0, n) is not A, C, G or T
@@ -3103,7 +3112,8 @@ hipError_t launch_avsa_prof(const uint64_t *q_off, const uint64_t *d_off, const 
     if (blocks * 256 > 0xFFFFFFFFull) return hipErrorInvalidConfiguration;
     const size_t lds = (size_t)(256 / G) * (ld_max + 2 * G) * 4;
     if (lds > kPackedLdsMax) return hipErrorInvalidValue;
-    const auto kern = nw_fill_avsa_prof_kernel<G, K>;
+    const auto kern = opt(Opt::PkTab) && pk_tab_ok(sc) ? nw_fill_avsa_prof_kernel<G, K, true>
+                                                       : nw_fill_avsa_prof_kernel<G, K, false>;
     if (lds > 65536) {
         const hipError_t e = hipFuncSetAttribute((const void *)kern,
                                                  hipFuncAttributeMaxDynamicSharedMemorySize,

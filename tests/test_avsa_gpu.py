@@ -105,8 +105,9 @@ def test_avsa_narrow_groups_equal_wide(saln, saln_opt):
 @pytest.mark.parametrize("nd,alphabet", [(401, b"ACGT"), (400, b"ACGT"), (201, b"ACGTN")])
 def test_avsa_query_profiles_equal_generic(saln, saln_opt, oracle, nd, alphabet):
     """The 8 x 19 class with query profiles (nw.avsa_profile, AvsaSrcP: a
-    group's two halves share the query; penalties from a per-column v_perm)
-    equals the generic xor path on every pair: an odd db count (the last db
+    group's two halves share the query; bonuses in the extension-free frame
+    (nw.pk_tab = 1, the default) or penalties (nw.pk_tab = 0) from a
+    per-column v_perm) equals the generic xor path on every pair: an odd db count (the last db
     record through AvsaSrc), and an N in the data (the device check selects
     the generic body inside the profile kernel).  A sample against the oracle."""
     rng = np.random.default_rng(nd)
@@ -115,9 +116,12 @@ def test_avsa_query_profiles_equal_generic(saln, saln_opt, oracle, nd, alphabet)
     dbs = [rand_seq(rng, int(n), alphabet) for n in rng.integers(100, 161, nd)]
     saln_opt("nw.avsa_profile", 1)
     s1, t1 = saln.nw_score_all_vs_all(queries, dbs)
+    saln_opt("nw.pk_tab", 0)  # profiles of penalties in the original frame
+    s2, t2 = saln.nw_score_all_vs_all(queries, dbs)
     saln_opt("nw.avsa_profile", 0)
     s0, t0 = saln.nw_score_all_vs_all(queries, dbs)
     assert np.array_equal(s1, s0) and np.array_equal(t1, t0)
+    assert np.array_equal(s2, s0) and np.array_equal(t2, t0)
     for k in range(40):
         qi, di = int(rng.integers(nq)), int(rng.integers(nd))
         o = oracle.nw(queries[qi], dbs[di], literal_dfs=False)

@@ -159,6 +159,15 @@ for st in ${STAGES:-smoke tests bench}; do
           tail -1 $O/abwalk_${v}_$i.log | cut -c1-220
         done
       done ;;
+    abfree)  # C5 query profiles: bonuses in the extension-free frame (nw.pk_tab) against penalties
+      step abfree_chk 200 python tools/bench_avsa.py --nq 1000 --ndb 100000 --reps 2 --check --opt nw.pk_tab=1
+      tail -1 $O/abfree_chk.log | cut -c1-400
+      for i in ${REPS:-1 2}; do
+        for w in 0 1; do
+          step abfree_${w}_$i 200 python tools/bench_avsa.py --nq 1000 --ndb 100000 --reps 3 --opt nw.pk_tab=$w
+          echo "tab=$w $(tail -1 $O/abfree_${w}_$i.log | cut -c1-300)"
+        done
+      done ;;
     abtab)  # table-penalty fill (nw.pk_tab) against the default: sequential and pipelined steps
       for i in 1 2; do
         for w in 0 1; do
