@@ -267,6 +267,46 @@ def test_table_fill_equals_generic(saln, oracle, saln_opt, case):
                 assert np.array_equal(got, want.cigar_words(k)), k
 
 
+def test_table_fill_concurrent_plans(saln, saln_opt):
+    """Two plans whose data hold N bytes execute at the same time on two
+    streams, three times each: every table launch has its own epoch slot, so
+    each fallback launch runs exactly its own launch's bail-outs.  Results
+    equal each plan run alone."""
+    import torch
+    from sequencealigning_amd import synth
+    saln_opt("nw.pk_tab", 1)
+    n, L = 8_000, 150
+    data, plans, alone = [], [], []
+    for seed in (0xC0, 0xC1):
+        qs, qo, ds, do = synth.iid_pairs(n, L, L, seed=seed)
+        qs = qs.copy()
+        rng = np.random.default_rng(seed)
+        for k in rng.choice(n, n // 50, replace=False):
+            qs[int(qo[k]) + int(rng.integers(L))] = ord("N")
+        data.append((qs, qo, ds, do))
+        alone.append(_run_plan(saln, qs, qo, ds, do))
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    bufs = []
+    for (qs, qo, ds, do) in data:
+        plan = saln.NwPlan(qo, do, pairs=np.stack([np.arange(n), np.arange(n)], 1))
+        dq, dd = torch.from_numpy(qs).cuda(), torch.from_numpy(ds).cuda()
+        res_t = torch.zeros(n * 4, dtype=torch.int32, device="cuda")
+        cig_t = torch.zeros(max(1, plan.cigar_words), dtype=torch.int32, device="cuda")
+        plans.append(plan)
+        bufs.append((dq, dd, res_t, cig_t))
+    torch.cuda.synchronize()
+    for _ in range(3):
+        for plan, (dq, dd, res_t, cig_t), st in zip(plans, bufs, streams):
+            plan.execute(dq, dd, res_t, cig_t, stream=st.cuda_stream)
+    torch.cuda.synchronize()
+    for plan, (dq, dd, res_t, cig_t), (r0, c0, _) in zip(plans, bufs, alone):
+        plan.check()
+        res = res_t.cpu().numpy().view(saln._lib.RESULT_DTYPE)
+        assert np.array_equal(res, r0)
+        assert np.array_equal(cig_t.cpu().numpy().view(np.uint32), c0)
+        plan.close()
+
+
 def test_pipelined_plan_matches_sync(saln):
     """saln_nw_plan_set_async: tracebacks overlap the next fill through two
     mask workspaces; five pipelined executes (ragged lengths, several
