@@ -1504,6 +1504,21 @@ constexpr int pk_min_waves() { return kCodes == 3 /* kCodesNib */ && G == 8 ? 3 
 // lies in [-(4|go| + ...), rows (2|m| + 2|ge|) + 2|ge| lq] (X' is at least
 // its all-gap path, at most its all-match one).
 __device__ uint32_t g_tab_slots[1024];
+constexpr int32_t kFreeBias = 4096;
+#ifndef SALN_FREE_MAX3
+#define SALN_FREE_MAX3 1  // experiment builds: 0 (two packed u16 maxima)
+#endif
+constexpr bool kFreeMax3 = SALN_FREE_MAX3;
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+// max of three words of two biased halves read as positive normal f16 (one
+// v_pk_maximum3_f16); exact only inside the extension-free frame's window
+__device__ __forceinline__ uint32_t hmax3(uint32_t a, uint32_t b, uint32_t c) {
+    return __builtin_bit_cast(
+        uint32_t, __builtin_elementwise_maximum(__builtin_bit_cast(f16x2, a),
+                                                __builtin_elementwise_maximum(
+                                                    __builtin_bit_cast(f16x2, b),
+                                                    __builtin_bit_cast(f16x2, c))));
+}
 
 template <int G, int K, int kCodes, typename Src, int KS, bool kRebase = false, bool kProf = false,
           int kTabMode = 0>
@@ -1516,6 +1531,14 @@ __device__ __forceinline__ void fill_pk_body(Src src, uint32_t count, const uint
     // the table body, and kTabMode 3 = query profiles holding bonuses
     constexpr bool kFree = kTabMode == 1 || kTabMode == 3;
     static_assert(kTabMode != 3 || kProf, "kTabMode 3: query profiles");
+    // The extension-free frame's values lie in a narrow window above about
+    // -(6|go| + 6|ge|) (pk_free_ok): biased by kFreeBias they are the bit
+    // patterns of positive normal halves, [0x0400, 0x7BFF], whose order is
+    // their integer order, so H = max(M, I, D) is one v_pk_maximum3_f16.
+    constexpr int32_t kBias = kFree ? kFreeBias : 32768;
+    auto pkx = [](int32_t lo, int32_t hi) {
+        return ((uint32_t)(lo + kBias) & 0xFFFFu) | ((uint32_t)(hi + kBias) << 16);
+    };
     static_assert(!kProf || (kCodes == kCodesNone && !kRebase), "profiles: score-only, one frame");
     static_assert(!kTab || (kCodes == kCodesNib && !kRebase && !kProf), "tables: 4-bit codes, one frame");
     constexpr int GPB = 256 / G;
@@ -1582,10 +1605,10 @@ __device__ __forceinline__ void fill_pk_body(Src src, uint32_t count, const uint
         }
         const int32_t h0 = hs_row0(sc, (uint32_t)j) + beta * j - ctr;     // H~(0, j)
         const int32_t d1 = ds_row1(sc, (uint32_t)j) + alpha + beta * j - ctr;  // D~(1, j)
-        Hp[k] = pkb(h0, h0);
-        Dn[k] = pkb(d1, d1);
+        Hp[k] = pkx(h0, h0);
+        Dn[k] = pkx(d1, d1);
     }
-    uint32_t hd = pkb(hs_row0(sc, (uint32_t)col0) + beta * col0 - ctr,
+    uint32_t hd = pkx(hs_row0(sc, (uint32_t)col0) + beta * col0 - ctr,
                       hs_row0(sc, (uint32_t)col0) + beta * col0 - ctr);  // H~(r-1, col0)
     uint32_t pubF = 0, pubH = 0;
     // db chars of both pairs, staged once per group in LDS as the packed
@@ -1697,8 +1720,8 @@ __device__ __forceinline__ void fill_pk_body(Src src, uint32_t count, const uint
         } else {
             const int32_t bF = is_col1(sc, (uint32_t)rb) + alpha * rb + beta - base;
             const int32_t bH = hs_col0(sc, (uint32_t)rb) + alpha * rb - base;
-            gF = pkb(bF, bF);
-            gH = pkb(bH, bH);
+            gF = pkx(bF, bF);
+            gH = pkx(bH, bH);
         }
         const uint32_t inF = gshift<G>(gF, pubF, gstart);
         const uint32_t inH = gshift<G>(gH, pubH, gstart);
@@ -1731,7 +1754,7 @@ __device__ __forceinline__ void fill_pk_body(Src src, uint32_t count, const uint
                                              : umin2(qc[k] ^ dch, kPen);
                 const uint32_t M = kFree ? hdk + pen : hdk - pen;
                 const uint32_t I = F, D = Dn[k];
-                const uint32_t H = umax2(M, umax2(I, D));
+                const uint32_t H = kFree && kFreeMax3 ? hmax3(M, I, D) : umax2(M, umax2(I, D));
                 const uint32_t tO = M + kOpen;
                 if constexpr (kCodes == kCodesNib) {
                     // the four walk decisions as signs (set = parent absent):
@@ -1874,11 +1897,11 @@ __device__ __forceinline__ void fill_pk_body(Src src, uint32_t count, const uint
                 }
             }
             if (!kSteady && t == tEA) {
-                const int32_t e = (int32_t)(pick_col<K>(Hout, kA) & 0xFFFFu) - 32768;
+                const int32_t e = (int32_t)(pick_col<K>(Hout, kA) & 0xFFFFu) - kBias;
                 src.end(ia, pa, e + base - alpha * ldA - beta * lqA);
             }
             if (!kSteady && t == tEB) {
-                const int32_t e = (int32_t)(pick_col<K>(Hout, kB) >> 16) - 32768;
+                const int32_t e = (int32_t)(pick_col<K>(Hout, kB) >> 16) - kBias;
                 src.end(ib, pb, e + base - alpha * ldB - beta * lqB);
             }
         } else if (&Hout != &Hin) {
@@ -1905,8 +1928,8 @@ __device__ __forceinline__ void fill_pk_body(Src src, uint32_t count, const uint
             const int32_t rb = tS0 + 1;
             const int32_t bF = is_col1(sc, (uint32_t)rb) + alpha * rb + beta;
             const int32_t bH = hs_col0(sc, (uint32_t)rb) + alpha * rb;
-            sF = pkb(bF, bF);
-            sH = pkb(bH, bH);
+            sF = pkx(bF, bF);
+            sH = pkx(bH, bH);
         }
         uint32_t d0 = kRebase ? 0u : rowp[t];
         for (; t < tS1; t += 2) {
@@ -2981,6 +3004,18 @@ static bool pk_tab_ok(const Scoring &sc) {
     const int64_t cm = 2ll * sc.match - 4ll * sc.gap_extend, cmm = 2ll * sc.mismatch - 4ll * sc.gap_extend;
     return cmm >= 0 && cm <= 255 && cmm < cm && -(int64_t)sc.gap_open <= 2000;
 }
+// ... and its values, biased by kFreeBias, stay positive normal halves for
+// W-column lanes groups over `rows` rows: X~ = X' + 2|ge|(r + c) is at least
+// the all-gap path's 4go + 4ge less an open and a mismatch for M / I / D, at
+// most rows (2|m| + 2|ge|) + 2|ge| W plus the boundary flag.
+static bool pk_free_ok(const Scoring &sc, uint32_t W, uint32_t rows) {
+    if (!pk_tab_ok(sc)) return false;
+    const int64_t m = std::abs(sc.match), mm = std::abs(sc.mismatch), ge = std::abs(sc.gap_extend),
+                  go = std::abs(sc.gap_open);
+    const int64_t lo = 6 * go + 6 * ge + 2 * mm + 64;
+    const int64_t hi = (int64_t)rows * (2 * m + 2 * ge) + 2 * ge * (int64_t)W + 2 * go + 64;
+    return lo <= kFreeBias - 0x400 && hi <= 0x7BFF - kFreeBias;
+}
 
 template <int G, int K, int KS = K>
 static hipError_t fill_pk(dim3 grid, hipStream_t s, const NwPairDesc *pairs, uint32_t first,
@@ -2995,7 +3030,7 @@ static hipError_t fill_pk(dim3 grid, hipStream_t s, const NwPairDesc *pairs, uin
         const auto kern = nw_fill_pk_kernel<G, K, decltype(codes_c)::value, PlanSrc, KS,
                                             decltype(rebase_c)::value>;
         if constexpr (decltype(codes_c)::value == kCodesNib && !decltype(rebase_c)::value && KS == K) {
-            if (opt(Opt::PkTab) && pk_tab_ok(sc)) {
+            if (opt(Opt::PkTab) && pk_free_ok(sc, G * K, ld_max)) {
                 static std::atomic<uint32_t> epochs{0};
                 const uint32_t ep = epochs.fetch_add(1, std::memory_order_relaxed) + 1;
                 if (lds > 65536) {
@@ -3112,7 +3147,7 @@ hipError_t launch_avsa_prof(const uint64_t *q_off, const uint64_t *d_off, const 
     if (blocks * 256 > 0xFFFFFFFFull) return hipErrorInvalidConfiguration;
     const size_t lds = (size_t)(256 / G) * (ld_max + 2 * G) * 4;
     if (lds > kPackedLdsMax) return hipErrorInvalidValue;
-    const auto kern = opt(Opt::PkTab) && pk_tab_ok(sc) ? nw_fill_avsa_prof_kernel<G, K, true>
+    const auto kern = opt(Opt::PkTab) && pk_free_ok(sc, G * K, ld_max) ? nw_fill_avsa_prof_kernel<G, K, true>
                                                        : nw_fill_avsa_prof_kernel<G, K, false>;
     if (lds > 65536) {
         const hipError_t e = hipFuncSetAttribute((const void *)kern,

@@ -168,6 +168,18 @@ for st in ${STAGES:-smoke tests bench}; do
           echo "tab=$w $(tail -1 $O/abfree_${w}_$i.log | cut -c1-300)"
         done
       done ;;
+    abmax3)  # H as one v_pk_maximum3_f16 in the extension-free frame vs two u16 maxima (libsaln_nomax3.so)
+      for i in 1 2; do
+        for v in nomax3 new; do
+          lib=""; [[ $v != new ]] && lib="SALN_LIB=$PWD/sequencealigning_amd/libsaln_$v.so"
+          step abm3_${v}_$i 120 env $lib python tools/ab_c2.py --tag $v
+          tail -1 $O/abm3_${v}_$i.log | cut -c1-220
+          step abm3p_${v}_$i 120 env $lib python tools/ab_c2.py --pipeline --tag $v
+          tail -1 $O/abm3p_${v}_$i.log | cut -c1-220
+          step abm3a_${v}_$i 200 env $lib python tools/bench_avsa.py --nq 1000 --ndb 100000 --reps 3
+          echo "$v $(tail -1 $O/abm3a_${v}_$i.log | cut -c1-260)"
+        done
+      done ;;
     abtab)  # table-penalty fill (nw.pk_tab) against the default: sequential and pipelined steps
       for i in 1 2; do
         for w in 0 1; do
