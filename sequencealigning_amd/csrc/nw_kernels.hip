@@ -469,9 +469,10 @@ __device__ void walk_pack_lds(const NwPairDesc &p, int32_t hend, const uint8_t *
     };
     // kNib: a 16-bit group half holds the I-open bits (nibble bit 2) of its
     // columns 0..3 at bits 2, 10, 6, 14; the multiply by 0x285 gathers them in
-    // column order into bits 11..14
+    // column order into bits 11..14 (a 24-bit multiply: full rate, where the
+    // 32-bit one is quarter rate)
     auto iopen_n = [](uint32_t h) __attribute__((always_inline)) {
-        return __builtin_amdgcn_ubfe((~h & 0x4444u) * 0x285u, 11, 4);
+        return __builtin_amdgcn_ubfe((uint32_t)__umul24(~h & 0x4444u, 0x285u), 11, 4);
     };
     auto iopen_n8 = [&](uint32_t d) __attribute__((always_inline)) {
         return iopen_n(d) | (iopen_n(d >> 16) << 4);

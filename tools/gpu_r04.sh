@@ -180,6 +180,16 @@ for st in ${STAGES:-smoke tests bench}; do
           echo "$v $(tail -1 $O/abm3a_${v}_$i.log | cut -c1-260)"
         done
       done ;;
+    abmul)  # walker I-open gather with a 24-bit multiply (new) vs the 32-bit one (libsaln_base.so)
+      for i in 1 2 3; do
+        for v in base new; do
+          lib=""; [[ $v != new ]] && lib="SALN_LIB=$PWD/sequencealigning_amd/libsaln_$v.so"
+          step abmul_${v}_$i 120 env $lib python tools/ab_c2.py --tag $v
+          tail -1 $O/abmul_${v}_$i.log | cut -c1-220
+          step abmulp_${v}_$i 120 env $lib python tools/ab_c2.py --pipeline --tag $v
+          tail -1 $O/abmulp_${v}_$i.log | cut -c1-220
+        done
+      done ;;
     abtab)  # table-penalty fill (nw.pk_tab) against the default: sequential and pipelined steps
       for i in 1 2; do
         for w in 0 1; do
