@@ -184,7 +184,10 @@ int saln_nw_avsa_execute(saln_nw_avsa *a, const uint8_t *d_q_seq, const uint8_t 
     const bool prof = opt(Opt::AvsaProfile) != 0 && a->n_dn >= 2 &&
                       std::any_of(a->classes.begin(), a->classes.end(),
                                   [](const saln_nw_avsa::Class &c) { return c.variant == 4; });
-    if (prof) {
+    // the other classes take table penalties under the same check (nw.pk_tab)
+    const bool checked = prof || opt(Opt::PkTab) != 0;
+    const uint32_t *generic = checked ? a->d_generic : nullptr;
+    if (checked) {
         HIP_TRY(hipMemsetAsync(a->d_generic, 0, sizeof(uint32_t), s));
         HIP_TRY(launch_acgt_check(d_q_seq, a->q_bytes, a->d_generic, s));
         HIP_TRY(launch_acgt_check(d_db_seq, a->d_bytes, a->d_generic, s));
@@ -208,7 +211,7 @@ int saln_nw_avsa_execute(saln_nw_avsa *a, const uint8_t *d_q_seq, const uint8_t 
                 if (a->n_dn & 1u)
                     HIP_TRY(launch_avsa(c.variant, a->d_qoff, a->d_doff, c.d_qids, c.nq,
                                         a->d_dids + (a->n_dn - 1), nqt, 0, c.nq, d_q_seq, d_db_seq,
-                                        out, a->sc, a->ld_max, s));
+                                        out, a->sc, a->ld_max, s, generic));
                 continue;
             }
             if (e != hipErrorInvalidValue) HIP_TRY(e);  // not applicable: the plain path
@@ -217,7 +220,7 @@ int saln_nw_avsa_execute(saln_nw_avsa *a, const uint8_t *d_q_seq, const uint8_t 
         for (uint64_t base = 0; base < total; base += kChunk) {
             const uint32_t n = (uint32_t)std::min<uint64_t>(kChunk, total - base);
             HIP_TRY(launch_avsa(c.variant, a->d_qoff, a->d_doff, c.d_qids, c.nq, a->d_dids, nqt,
-                                base, n, d_q_seq, d_db_seq, out, a->sc, a->ld_max, s));
+                                base, n, d_q_seq, d_db_seq, out, a->sc, a->ld_max, s, generic));
         }
     }
     // empty db records x every query; empty queries x non-empty db records

@@ -159,7 +159,7 @@ hipError_t launch_avsa(int variant, const uint64_t *q_off, const uint64_t *d_off
                        const uint32_t *q_ids, uint32_t nq, const uint32_t *d_ids,
                        uint32_t nq_total, uint64_t base, uint32_t count, const uint8_t *qs,
                        const uint8_t *ds, int2 *out, Scoring sc, uint32_t ld_max,
-                       hipStream_t stream);
+                       hipStream_t stream, const uint32_t *generic = nullptr);
 hipError_t launch_avsa_boundary(const uint64_t *q_off, const uint64_t *d_off,
                                 const uint32_t *q_ids, uint32_t nq, const uint32_t *d_ids,
                                 uint64_t n, uint32_t nq_total, int2 *out, Scoring sc,

@@ -1541,7 +1541,8 @@ __device__ __forceinline__ void fill_pk_body(Src src, uint32_t count, const uint
         return ((uint32_t)(lo + kBias) & 0xFFFFu) | ((uint32_t)(hi + kBias) << 16);
     };
     static_assert(!kProf || (kCodes == kCodesNone && !kRebase), "profiles: score-only, one frame");
-    static_assert(!kTab || (kCodes == kCodesNib && !kRebase && !kProf), "tables: 4-bit codes, one frame");
+    static_assert(!kTab || ((kCodes == kCodesNib || kCodes == kCodesNone) && !kRebase && !kProf),
+                  "tables: 4-bit codes or score-only, one frame");
     constexpr int GPB = 256 / G;
     constexpr Geom geo{G, K};
     extern __shared__ uint32_t drow[];  // [GPB][G + ld_max + G] packed db chars (dch) per row
@@ -1972,6 +1973,21 @@ __global__ __launch_bounds__(256, (pk_min_waves<G, K, kCodesNib>())) void nw_fil
     if (__builtin_amdgcn_readfirstlane(g_tab_slots[epoch & 1023u]) != epoch) return;
     fill_pk_body<G, K, kCodesNib, Src, K, false, false, 2>(src, count, qs, ds, mask, sc, ld_max,
                                                             sc_steady, epoch);
+}
+
+// Score-only all-vs-all of the other query classes with table penalties in
+// the extension-free frame (nw.pk_tab); *generic (nw_acgt_check_kernel earlier
+// on the stream) selects the xor body when a byte is not A, C, G or T.
+template <int G, int K>
+__global__ __launch_bounds__(256, (pk_min_waves<G, K, kCodesNone>())) void nw_fill_avsa_tab_kernel(
+    AvsaSrc src, uint32_t count, const uint8_t *__restrict__ qs, const uint8_t *__restrict__ ds,
+    Scoring sc, uint32_t ld_max, bool sc_steady, const uint32_t *__restrict__ generic) {
+    if (__builtin_amdgcn_readfirstlane(*generic))
+        fill_pk_body<G, K, kCodesNone, AvsaSrc, K, false, false, 0>(src, count, qs, ds, nullptr, sc,
+                                                                    ld_max, sc_steady);
+    else
+        fill_pk_body<G, K, kCodesNone, AvsaSrc, K, false, false, 1>(src, count, qs, ds, nullptr, sc,
+                                                                    ld_max, sc_steady);
 }
 
 // Score-only all-vs-all with query profiles; *generic (set by
@@ -3108,7 +3124,7 @@ uint64_t avsa_launch_blocks(int variant, uint64_t count) {
 
 template <int G, int K>
 static hipError_t avsa_pk(const AvsaSrc &src, uint32_t count, const uint8_t *qs, const uint8_t *ds,
-                          Scoring sc, uint32_t ld_max, hipStream_t s) {
+                          Scoring sc, uint32_t ld_max, hipStream_t s, const uint32_t *generic) {
     constexpr uint32_t gpb = 256 / G;
     const uint64_t blocks = avsa_blocks(G, count);
     if (blocks * 256 > 0xFFFFFFFFull) return hipErrorInvalidConfiguration;  // 32-bit grid
@@ -3117,6 +3133,19 @@ static hipError_t avsa_pk(const AvsaSrc &src, uint32_t count, const uint8_t *qs,
     const size_t lds = (size_t)gpb * (ld_max + 2 * G) * (rebase ? 2 : 4);
     if (lds > kPackedLdsMax) return hipErrorInvalidValue;
     auto go = [&](auto rebase_c) -> hipError_t {
+        if constexpr (!decltype(rebase_c)::value) {
+            if (generic && opt(Opt::PkTab) && pk_free_ok(sc, G * K, ld_max)) {
+                const auto kern = nw_fill_avsa_tab_kernel<G, K>;
+                if (lds > 65536) {
+                    const hipError_t e = hipFuncSetAttribute(
+                        (const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                        (int)kPackedLdsMax);
+                    if (e != hipSuccess) return e;
+                }
+                kern<<<grid, dim3(256), lds, s>>>(src, count, qs, ds, sc, ld_max, pk_steady(), generic);
+                return hipSuccess;
+            }
+        }
         const auto kern = nw_fill_pk_kernel<G, K, kCodesNone, AvsaSrc, K, decltype(rebase_c)::value>;
         if (lds > 65536) {
             const hipError_t e = hipFuncSetAttribute((const void *)kern,
@@ -3174,16 +3203,16 @@ hipError_t launch_avsa(int variant, const uint64_t *q_off, const uint64_t *d_off
                        const uint32_t *q_ids, uint32_t nq, const uint32_t *d_ids,
                        uint32_t nq_total, uint64_t base, uint32_t count, const uint8_t *qs,
                        const uint8_t *ds, int2 *out, Scoring sc, uint32_t ld_max,
-                       hipStream_t stream) {
+                       hipStream_t stream, const uint32_t *generic) {
     if (!count) return hipSuccess;
     const AvsaSrc src{q_off, d_off, q_ids, d_ids, nq, nq_total, base, out};
     hipError_t e;
     switch (variant) {
-        case 4: e = avsa_pk<8, 19>(src, count, qs, ds, sc, ld_max, stream); break;
-        case 5: e = avsa_pk<16, 16>(src, count, qs, ds, sc, ld_max, stream); break;
-        case 6: e = avsa_pk<32, 16>(src, count, qs, ds, sc, ld_max, stream); break;
-        case 7: e = avsa_pk<16, 10>(src, count, qs, ds, sc, ld_max, stream); break;
-        case 8: e = avsa_pk<64, 16>(src, count, qs, ds, sc, ld_max, stream); break;
+        case 4: e = avsa_pk<8, 19>(src, count, qs, ds, sc, ld_max, stream, generic); break;
+        case 5: e = avsa_pk<16, 16>(src, count, qs, ds, sc, ld_max, stream, generic); break;
+        case 6: e = avsa_pk<32, 16>(src, count, qs, ds, sc, ld_max, stream, generic); break;
+        case 7: e = avsa_pk<16, 10>(src, count, qs, ds, sc, ld_max, stream, generic); break;
+        case 8: e = avsa_pk<64, 16>(src, count, qs, ds, sc, ld_max, stream, generic); break;
         default: return hipErrorInvalidValue;
     }
     if (e != hipSuccess) return e;

@@ -127,3 +127,26 @@ def test_avsa_query_profiles_equal_generic(saln, saln_opt, oracle, nd, alphabet)
         o = oracle.nw(queries[qi], dbs[di], literal_dfs=False)
         assert s1[di, qi] == o.score, (qi, di)
         assert (t1[di, qi] == saln._lib.REF_PANIC_BOUNDARY) == o.panics, (qi, di)
+
+
+@pytest.mark.parametrize("lo,hi,alphabet", [(153, 256, b"ACGT"), (257, 512, b"ACGT"),
+                                            (100, 600, b"ACGT"), (153, 256, b"ACGTN")])
+def test_avsa_table_classes_equal_generic(saln, saln_opt, oracle, lo, hi, alphabet):
+    """The query classes without profiles (16 x 16, 32 x 16, 16 x 10 / 8 x 19
+    odd records) take table penalties in the extension-free frame under
+    nw.pk_tab = 1 when every byte is A, C, G or T (the device check; with an
+    N they keep the xor body): equal to nw.pk_tab = 0 on every pair, and a
+    sample against the oracle."""
+    rng = np.random.default_rng(lo * 7 + hi + len(alphabet))
+    queries = [rand_seq(rng, int(n), alphabet) for n in rng.integers(lo, hi + 1, 61)]
+    dbs = [rand_seq(rng, int(n), alphabet) for n in rng.integers(lo, hi + 1, 37)]
+    saln_opt("nw.pk_tab", 1)
+    s1, t1 = saln.nw_score_all_vs_all(queries, dbs)
+    saln_opt("nw.pk_tab", 0)
+    s0, t0 = saln.nw_score_all_vs_all(queries, dbs)
+    assert np.array_equal(s1, s0) and np.array_equal(t1, t0)
+    for _ in range(12):
+        qi, di = int(rng.integers(len(queries))), int(rng.integers(len(dbs)))
+        o = oracle.nw(queries[qi], dbs[di], literal_dfs=False)
+        assert s1[di, qi] == o.score, (qi, di)
+        assert (t1[di, qi] == saln._lib.REF_PANIC_BOUNDARY) == o.panics, (qi, di)

@@ -190,6 +190,15 @@ for st in ${STAGES:-smoke tests bench}; do
           tail -1 $O/abmulp_${v}_$i.log | cut -c1-220
         done
       done ;;
+    abgen)  # all-vs-all classes without profiles (250 / 400 bp): table penalties (nw.pk_tab) vs xor
+      for i in 1 2; do
+        for L in 250 400; do
+          for w in 0 1; do
+            step abgen_${L}_${w}_$i 200 python tools/bench_avsa.py --nq 500 --ndb 50000 --len $L --reps 3 --opt nw.pk_tab=$w
+            echo "len=$L tab=$w $(tail -1 $O/abgen_${L}_${w}_$i.log | cut -c1-240)"
+          done
+        done
+      done ;;
     abtab)  # table-penalty fill (nw.pk_tab) against the default: sequential and pipelined steps
       for i in 1 2; do
         for w in 0 1; do
