@@ -1978,13 +1978,16 @@ __global__ __launch_bounds__(256, (pk_min_waves<G, K, kCodesNib>())) void nw_fil
 // Score-only all-vs-all of the other query classes with table penalties in
 // the extension-free frame (nw.pk_tab); *generic (nw_acgt_check_kernel earlier
 // on the stream) selects the xor body when a byte is not A, C, G or T.
-template <int G, int K>
+// kRebaseGeneric: dbs too long for the original frame's single int16 window
+// (the extension-free frame has no drift, so its table body needs no
+// rebasing); the xor body then rebases.
+template <int G, int K, bool kRebaseGeneric>
 __global__ __launch_bounds__(256, (pk_min_waves<G, K, kCodesNone>())) void nw_fill_avsa_tab_kernel(
     AvsaSrc src, uint32_t count, const uint8_t *__restrict__ qs, const uint8_t *__restrict__ ds,
     Scoring sc, uint32_t ld_max, bool sc_steady, const uint32_t *__restrict__ generic) {
     if (__builtin_amdgcn_readfirstlane(*generic))
-        fill_pk_body<G, K, kCodesNone, AvsaSrc, K, false, false, 0>(src, count, qs, ds, nullptr, sc,
-                                                                    ld_max, sc_steady);
+        fill_pk_body<G, K, kCodesNone, AvsaSrc, K, kRebaseGeneric, false, 0>(
+            src, count, qs, ds, nullptr, sc, ld_max, sc_steady);
     else
         fill_pk_body<G, K, kCodesNone, AvsaSrc, K, false, false, 1>(src, count, qs, ds, nullptr, sc,
                                                                     ld_max, sc_steady);
@@ -3132,19 +3135,21 @@ static hipError_t avsa_pk(const AvsaSrc &src, uint32_t count, const uint8_t *qs,
     const bool rebase = !packed_ok(G * K, ld_max, sc);
     const size_t lds = (size_t)gpb * (ld_max + 2 * G) * (rebase ? 2 : 4);
     if (lds > kPackedLdsMax) return hipErrorInvalidValue;
+    // the table body stages 32-bit row words, the rebasing xor body 16-bit ones
+    const size_t lds_tab = (size_t)gpb * (ld_max + 2 * G) * 4;
+    const bool tab = generic && opt(Opt::PkTab) && pk_free_ok(sc, G * K, ld_max) &&
+                     lds_tab <= kPackedLdsMax;
     auto go = [&](auto rebase_c) -> hipError_t {
-        if constexpr (!decltype(rebase_c)::value) {
-            if (generic && opt(Opt::PkTab) && pk_free_ok(sc, G * K, ld_max)) {
-                const auto kern = nw_fill_avsa_tab_kernel<G, K>;
-                if (lds > 65536) {
-                    const hipError_t e = hipFuncSetAttribute(
-                        (const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
-                        (int)kPackedLdsMax);
-                    if (e != hipSuccess) return e;
-                }
-                kern<<<grid, dim3(256), lds, s>>>(src, count, qs, ds, sc, ld_max, pk_steady(), generic);
-                return hipSuccess;
+        if (tab) {
+            const auto kern = nw_fill_avsa_tab_kernel<G, K, decltype(rebase_c)::value>;
+            if (lds_tab > 65536) {
+                const hipError_t e = hipFuncSetAttribute(
+                    (const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                    (int)kPackedLdsMax);
+                if (e != hipSuccess) return e;
             }
+            kern<<<grid, dim3(256), lds_tab, s>>>(src, count, qs, ds, sc, ld_max, pk_steady(), generic);
+            return hipSuccess;
         }
         const auto kern = nw_fill_pk_kernel<G, K, kCodesNone, AvsaSrc, K, decltype(rebase_c)::value>;
         if (lds > 65536) {
