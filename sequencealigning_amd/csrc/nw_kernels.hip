@@ -1628,6 +1628,7 @@ __device__ __forceinline__ void fill_pk_body(Src src, uint32_t count, const uint
         const uint32_t ca = i < ldA ? (uint32_t)dA[i] : 0u;
         const uint32_t cb = i < ldB ? (uint32_t)dB[i] : 0u;
         if constexpr (kRebase) {
+            if constexpr (kTabMode == 2) bad |= (i < ldA && !acgt(ca)) || (i < ldB && !acgt(cb));
             myrow16[i] = (uint16_t)(ca | (cb << 8));
         } else if constexpr (kTab) {
             bad |= (i < ldA && !acgt(ca)) || (i < ldB && !acgt(cb));
@@ -1966,13 +1967,15 @@ __global__ __launch_bounds__(256, (pk_min_waves<G, K, kCodesNib>())) void nw_fil
     fill_pk_body<G, K, kCodesNib, Src, K, false, false, 1>(src, count, qs, ds, mask, sc, ld_max,
                                                             sc_steady, epoch);
 }
-template <int G, int K, typename Src>
+// (kRebaseGeneric: the fallback of a launch whose dbs need the rebasing frame;
+// the extension-free table body has no drift and needs none)
+template <int G, int K, typename Src, bool kRebaseGeneric>
 __global__ __launch_bounds__(256, (pk_min_waves<G, K, kCodesNib>())) void nw_fill_pk_tabfb_kernel(
     Src src, uint32_t count, const uint8_t *__restrict__ qs, const uint8_t *__restrict__ ds,
     uint8_t *__restrict__ mask, Scoring sc, uint32_t ld_max, bool sc_steady, uint32_t epoch) {
     if (__builtin_amdgcn_readfirstlane(g_tab_slots[epoch & 1023u]) != epoch) return;
-    fill_pk_body<G, K, kCodesNib, Src, K, false, false, 2>(src, count, qs, ds, mask, sc, ld_max,
-                                                            sc_steady, epoch);
+    fill_pk_body<G, K, kCodesNib, Src, K, kRebaseGeneric, false, 2>(src, count, qs, ds, mask, sc,
+                                                                     ld_max, sc_steady, epoch);
 }
 
 // Score-only all-vs-all of the other query classes with table penalties in
@@ -2990,6 +2993,7 @@ static bool pk_steady() { return opt(Opt::PkSteady) != 0; }
 
 // Dynamic LDS cap of the packed fill's staged db rows: two workgroups per CU.
 constexpr size_t kPackedLdsMax = 80 * 1024;
+constexpr size_t kLdsPerCu = 160 * 1024;  // MI355X_MICROARCH.md
 static bool packed_ok(uint32_t lq, uint32_t ld, const Scoring &sc);
 
 template <int G, int K>
@@ -3049,21 +3053,26 @@ static hipError_t fill_pk(dim3 grid, hipStream_t s, const NwPairDesc *pairs, uin
     auto go = [&](auto codes_c, auto rebase_c) -> hipError_t {
         const auto kern = nw_fill_pk_kernel<G, K, decltype(codes_c)::value, PlanSrc, KS,
                                             decltype(rebase_c)::value>;
-        if constexpr (decltype(codes_c)::value == kCodesNib && !decltype(rebase_c)::value && KS == K) {
-            if (opt(Opt::PkTab) && pk_free_ok(sc, G * K, ld_max)) {
+        if constexpr (decltype(codes_c)::value == kCodesNib && KS == K) {
+            // (the table body stages 32-bit row words; a rebasing fallback 16-bit ones)
+            // (and keeps four workgroups per CU where the rebasing fill had them)
+            const size_t lds_tab = std::max((size_t)(256 / G) * (ld_max + 2 * G) * 4, pad);
+            if (opt(Opt::PkTab) && pk_free_ok(sc, G * K, ld_max) &&
+                lds_tab <= std::max(lds, kLdsPerCu / 4)) {
+                constexpr bool kRb = decltype(rebase_c)::value;
                 static std::atomic<uint32_t> epochs{0};
                 const uint32_t ep = epochs.fetch_add(1, std::memory_order_relaxed) + 1;
-                if (lds > 65536) {
+                if (lds_tab > 65536) {
                     for (const void *f : {(const void *)nw_fill_pk_tab_kernel<G, K, PlanSrc>,
-                                          (const void *)nw_fill_pk_tabfb_kernel<G, K, PlanSrc>}) {
+                                          (const void *)nw_fill_pk_tabfb_kernel<G, K, PlanSrc, kRb>}) {
                         const hipError_t e = hipFuncSetAttribute(
                             f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kPackedLdsMax);
                         if (e != hipSuccess) return e;
                     }
                 }
-                nw_fill_pk_tab_kernel<G, K, PlanSrc><<<grid, dim3(256), lds, s>>>(
+                nw_fill_pk_tab_kernel<G, K, PlanSrc><<<grid, dim3(256), lds_tab, s>>>(
                     src, count, qs, ds, mask, sc, ld_max, pk_steady(), ep);
-                nw_fill_pk_tabfb_kernel<G, K, PlanSrc><<<grid, dim3(256), lds, s>>>(
+                nw_fill_pk_tabfb_kernel<G, K, PlanSrc, kRb><<<grid, dim3(256), lds_tab, s>>>(
                     src, count, qs, ds, mask, sc, ld_max, pk_steady(), ep);
                 return hipSuccess;
             }
@@ -3138,7 +3147,7 @@ static hipError_t avsa_pk(const AvsaSrc &src, uint32_t count, const uint8_t *qs,
     // the table body stages 32-bit row words, the rebasing xor body 16-bit ones
     const size_t lds_tab = (size_t)gpb * (ld_max + 2 * G) * 4;
     const bool tab = generic && opt(Opt::PkTab) && pk_free_ok(sc, G * K, ld_max) &&
-                     lds_tab <= kPackedLdsMax;
+                     lds_tab <= std::max(lds, kLdsPerCu / 4);
     auto go = [&](auto rebase_c) -> hipError_t {
         if (tab) {
             const auto kern = nw_fill_avsa_tab_kernel<G, K, decltype(rebase_c)::value>;

@@ -230,7 +230,7 @@ def _run_plan(saln, qs, qo, ds, do, scoring=None):
     return res, cig, off
 
 
-@pytest.mark.parametrize("case", ["acgt", "with_n", "scheme"])
+@pytest.mark.parametrize("case", ["acgt", "with_n", "scheme", "long_db", "long_db_n"])
 def test_table_fill_equals_generic(saln, oracle, saln_opt, case):
     """nw.pk_tab = 1 (the 4-bit-code fill with table penalties in the
     extension-free frame, and its fallback launch for the waves whose pairs
@@ -239,13 +239,20 @@ def test_table_fill_equals_generic(saln, oracle, saln_opt, case):
     is also checked against the oracle pair by pair; "with_n" puts an N into
     1 % of the queries and 1 % of the dbs (those waves take the fallback
     launch, the rest of the launch the table body); "scheme" uses
-    {2, -3, -5, -2} (bonuses 12 / 2)."""
+    {2, -3, -5, -2} (bonuses 12 / 2).  "long_db" / "long_db_n": 150 x 500
+    pairs in 16 x 10 groups, whose dbs need the rebasing frame in the original
+    frame but not in the extension-free one (the fallback launch then
+    rebases)."""
     from sequencealigning_amd import synth
     n, L = 20_000, 150
-    qs, qo, ds, do = synth.iid_pairs(n, L, L, seed=0x7AB0 + len(case))
+    LD = L
+    if case.startswith("long_db"):
+        n, LD = 4_000, 500
+        saln_opt("nw.narrow_walk", 0)
+    qs, qo, ds, do = synth.iid_pairs(n, L, LD, seed=0x7AB0 + len(case))
     qs, ds = qs.copy(), ds.copy()
     scoring = (2, -3, -5, -2) if case == "scheme" else None
-    if case == "with_n":
+    if case in ("with_n", "long_db_n"):
         rng = np.random.default_rng(77)
         for buf, off in ((qs, qo), (ds, do)):
             for k in rng.choice(n, n // 100, replace=False):
@@ -256,7 +263,7 @@ def test_table_fill_equals_generic(saln, oracle, saln_opt, case):
     r0, c0, o0 = _run_plan(saln, qs, qo, ds, do, scoring)
     assert np.array_equal(r1, r0)
     assert np.array_equal(o1, o0) and np.array_equal(c1, c0)
-    if case == "acgt":
+    if case in ("acgt", "long_db"):
         want = oracle.check_pairs(qs, qo, ds, do)
         assert np.array_equal(r1["score"], want.score)
         assert np.array_equal(r1["end_states"], want.end_states)
