@@ -111,24 +111,33 @@ const char *saln_last_error(void);     /* thread-local message for the last erro
 int saln_abi_version(void);
 
 /* ---------------------------------------------------------------- options
- * Process-wide tuning knobs (kernel geometry and A/B variants), all with the
- * product's defaults.  No reference counterpart: the reference has no tuning
- * (its constants are compile-time, needleman_wunsch_affine.rs:15-20).  The
- * engine reads nothing from the process environment; these calls are the only
- * way to change what it runs.  Every option gives the same results; most are
- * read when a plan is created.  Names: "nw.pk_steady", "nw.wide_min_pairs",
- * "nw.tb_chunks", "nw.fill_lds_min", "nw.rows_k", "nw.stripe_pk", "nw.spec",
- * "nw.spec_passes", "nw.spec_strict", "nw.avsa_narrow", "nw.nib_codes",
- * "nw.narrow_walk", "nw.rows_wpg",
- * "nw.rows_lone", "nw.walk_prio", "nw.avsa_profile", "nw.pk_tab", "wfa2.seq_lds", "wfa2.w1",
- * "wfa2.w2", "host.timing".
- * SALN_E_INVALID for an unknown name or a value out of range. */
+ * Tuning knobs (kernel geometry and A/B variants), all with the product's
+ * defaults.  No reference counterpart: the reference has no tuning (its
+ * constants are compile-time, needleman_wunsch_affine.rs:15-20).  The engine
+ * reads nothing from the process environment; these calls are the only way
+ * to change what it runs.  Every option gives the same results.  Names:
+ * "nw.wide_min_pairs", "nw.rows_k", "nw.stripe_pk", "nw.spec",
+ * "nw.spec_passes", "nw.spec_strict", "nw.avsa_narrow", "nw.rows_lone",
+ * "nw.rows_xcd", "nw.avsa_profile", "nw.pk_tab", "nw.fuse_walk",
+ * "wfa2.seq_lds", "wfa2.w1", "wfa2.w2", "host.timing".
+ * Two levels, no other shared state:
+ *  - saln_option_*: the process registry, the default of every context;
+ *  - saln_context_option_*: overrides of one context (its own thread's
+ *    choices; another context is not affected).
+ * A plan, all-vs-all handle, span or host-buffer call takes its context's
+ * effective values when it is created (or called); a later change does not
+ * reach it.  SALN_E_INVALID for an unknown name or a value out of range. */
 int saln_option_set(const char *name, int64_t value);
 int saln_option_get(const char *name, int64_t *value, int64_t *default_value);
 /* Name of option `index` (0, 1, ...; SALN_E_INVALID past the last). */
 int saln_option_name(uint32_t index, const char **name);
-/* Every option back to its default. */
+/* Every option of the registry back to its default. */
 int saln_options_reset(void);
+/* One context's override; _get returns the context's effective value; _clear
+ * drops one override (name) or all of them (name NULL). */
+int saln_context_option_set(saln_context *ctx, const char *name, int64_t value);
+int saln_context_option_get(saln_context *ctx, const char *name, int64_t *value);
+int saln_context_option_clear(saln_context *ctx, const char *name);
 
 /* ------------------------------------------------------- NW: per pair (drop-in)
  * Replaces `pub fn n_w_align(seq1: &Record, seq2: &Record, _verbose: bool,

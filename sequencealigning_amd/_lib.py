@@ -102,6 +102,7 @@ EXPORTS = [
     "saln_parse_fasta", "saln_parse_fasta_buffer", "saln_records_count", "saln_records_get",
     "saln_records_free",
     "saln_option_set", "saln_option_get", "saln_option_name", "saln_options_reset",
+    "saln_context_option_set", "saln_context_option_get", "saln_context_option_clear",
     "saln_nw_render_batch", "saln_nw_render_text", "saln_nw_text_count", "saln_nw_text_get",
     "saln_nw_text_free",
     "saln_wfa_render_batch", "saln_wfa_text_count", "saln_wfa_text_get", "saln_wfa_text_free",
@@ -255,6 +256,9 @@ def lib() -> C.CDLL:
         L.saln_option_set.argtypes = [C.c_char_p, C.c_int64]
         L.saln_option_get.argtypes = [C.c_char_p, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]
         L.saln_option_name.argtypes = [C.c_uint32, C.POINTER(C.c_char_p)]
+        L.saln_context_option_set.argtypes = [vp, C.c_char_p, C.c_int64]
+        L.saln_context_option_get.argtypes = [vp, C.c_char_p, C.POINTER(C.c_int64)]
+        L.saln_context_option_clear.argtypes = [vp, C.c_char_p]
         _lib = L
         return L
 
@@ -339,10 +343,38 @@ def non_default_options() -> dict[str, int]:
     return out
 
 
+def set_context_option(ctx, name: str, value: int) -> None:
+    """saln_context_option_set: an override of one context (include/saln.h)."""
+    check(lib().saln_context_option_set(ctx, name.encode(), int(value)),
+          f"saln_context_option_set({name})")
+
+
+def get_context_option(ctx, name: str) -> int:
+    """A context's effective value of an option."""
+    v = C.c_int64()
+    check(lib().saln_context_option_get(ctx, name.encode(), C.byref(v)),
+          f"saln_context_option_get({name})")
+    return v.value
+
+
+def clear_context_option(ctx, name: str | None = None) -> None:
+    """Drop one override of a context (name) or all of them (None)."""
+    check(lib().saln_context_option_clear(ctx, name.encode() if name else None),
+          "saln_context_option_clear")
+
+
+def new_context(device: int = 0) -> C.c_void_p:
+    """A context of its own (not the per-process one of context()); the
+    caller destroys it with lib().saln_context_destroy."""
+    ctx = C.c_void_p()
+    check(lib().saln_context_create(device, C.byref(ctx)), "saln_context_create")
+    return ctx
+
+
 class options:
     """Context manager: set options for a block, restore the previous values.
 
-        with options(**{"nw.nib_codes": 0}): ...
+        with options(**{"nw.pk_tab": 0}): ...
     """
 
     def __init__(self, **kw):

@@ -58,7 +58,8 @@ static int run_batch(saln_context *ctx, const uint8_t *q_seq, const uint64_t *q_
                      int32_t mode, const saln_nw_scoring *scoring, saln_nw_result *results,
                      uint32_t *cigar, const uint64_t *cigar_off,
                      std::vector<PairMask> *masks_out) {
-    StageClock clk;
+    if (!ctx) return SALN_E_INVALID;
+    StageClock clk(ctx->opts.effective());
     if (!q_off || !db_off || (n_q && !q_seq && q_off[n_q]) || (n_db && !db_seq && db_off[n_db]))
         return SALN_E_INVALID;
     // the sequences' upload runs on a helper thread while this one plans (the
@@ -210,7 +211,7 @@ int saln_nw_render_batch(saln_context *ctx, const uint8_t *q_seq, const uint64_t
         delete t;
         return rc;
     }
-    StageClock clock;
+    StageClock clock(ctx->opts.effective());
     {
         DevBuf dq(ctx), dd(ctx), dr(ctx);
         const uint64_t qbytes = q_off[n_q], dbytes = db_off[n_db];

@@ -27,6 +27,7 @@ struct saln_nw_avsa {
         uint32_t *d_qids = nullptr;
     };
     saln_context *ctx = nullptr;
+    Options opts{};  // the context's effective options at creation
     Scoring sc{};
     uint64_t n_q = 0, n_db = 0, cells = 0;
     uint64_t *d_qoff = nullptr, *d_doff = nullptr;
@@ -80,6 +81,7 @@ int saln_nw_avsa_create(saln_context *ctx, const uint64_t *q_off, uint64_t n_q,
     HIP_TRY(hipSetDevice(ctx->device));
     auto a = std::make_unique<saln_nw_avsa>();
     a->ctx = ctx;
+    a->opts = ctx->opts.effective();
     a->sc = scoring_or_default(scoring);
     a->n_q = n_q;
     a->n_db = n_db;
@@ -103,7 +105,7 @@ int saln_nw_avsa_create(saln_context *ctx, const uint64_t *q_off, uint64_t n_q,
     // 8 x 19 groups for queries of <= 152 columns: the per-step overhead over
     // 19 columns and 7 steps of skew instead of 10 and 15 (C5 slice 6,738 ->
     // 7,858 GCUPS); option nw.avsa_narrow = 0 keeps the 16 x 10 geometry
-    const bool avsa_narrow = opt(Opt::AvsaNarrow) != 0;
+    const bool avsa_narrow = a->opts[Opt::AvsaNarrow] != 0;
     for (uint64_t q = 0; q < n_q; ++q) {
         const uint64_t lq = q_off[q + 1] - q_off[q];
         if (lq > 0x7FFFFFFFull) {
@@ -181,11 +183,11 @@ int saln_nw_avsa_execute(saln_nw_avsa *a, const uint8_t *d_q_seq, const uint8_t 
     const uint32_t nqt = (uint32_t)a->n_q;
     // the 8 x 19 class runs with query profiles when every byte is A, C, G
     // or T: checked here on the device, read by the kernel (no host sync)
-    const bool prof = opt(Opt::AvsaProfile) != 0 && a->n_dn >= 2 &&
+    const bool prof = a->opts[Opt::AvsaProfile] != 0 && a->n_dn >= 2 &&
                       std::any_of(a->classes.begin(), a->classes.end(),
                                   [](const saln_nw_avsa::Class &c) { return c.variant == 4; });
     // the other classes take table penalties under the same check (nw.pk_tab)
-    const bool checked = prof || opt(Opt::PkTab) != 0;
+    const bool checked = prof || a->opts[Opt::PkTab] != 0;
     const uint32_t *generic = checked ? a->d_generic : nullptr;
     if (checked) {
         HIP_TRY(hipMemsetAsync(a->d_generic, 0, sizeof(uint32_t), s));
@@ -205,13 +207,14 @@ int saln_nw_avsa_execute(saln_nw_avsa *a, const uint8_t *d_q_seq, const uint8_t 
             for (uint64_t base = 0; base < tp && e == hipSuccess; base += kChunk) {
                 const uint32_t n = (uint32_t)std::min<uint64_t>(kChunk, tp - base);
                 e = launch_avsa_prof(a->d_qoff, a->d_doff, c.d_qids, c.nq, a->d_dids, nqt, base, n,
-                                     d_q_seq, d_db_seq, out, a->sc, a->ld_max, a->d_generic, s);
+                                     d_q_seq, d_db_seq, out, a->sc, a->ld_max, a->d_generic, s,
+                                     a->opts);
             }
             if (e == hipSuccess) {
                 if (a->n_dn & 1u)
                     HIP_TRY(launch_avsa(c.variant, a->d_qoff, a->d_doff, c.d_qids, c.nq,
                                         a->d_dids + (a->n_dn - 1), nqt, 0, c.nq, d_q_seq, d_db_seq,
-                                        out, a->sc, a->ld_max, s, generic));
+                                        out, a->sc, a->ld_max, s, a->opts, generic));
                 continue;
             }
             if (e != hipErrorInvalidValue) HIP_TRY(e);  // not applicable: the plain path
@@ -220,7 +223,8 @@ int saln_nw_avsa_execute(saln_nw_avsa *a, const uint8_t *d_q_seq, const uint8_t 
         for (uint64_t base = 0; base < total; base += kChunk) {
             const uint32_t n = (uint32_t)std::min<uint64_t>(kChunk, total - base);
             HIP_TRY(launch_avsa(c.variant, a->d_qoff, a->d_doff, c.d_qids, c.nq, a->d_dids, nqt,
-                                base, n, d_q_seq, d_db_seq, out, a->sc, a->ld_max, s, generic));
+                                base, n, d_q_seq, d_db_seq, out, a->sc, a->ld_max, s, a->opts,
+                                generic));
         }
     }
     // empty db records x every query; empty queries x non-empty db records

@@ -52,6 +52,7 @@ using namespace saln;
 
 struct saln_nw_plan {
     saln_context *ctx = nullptr;
+    Options opts{};  // the context's effective options at creation
     Scoring sc{};
     uint64_t n_pairs = 0;
     std::vector<NwPairDesc> h_pairs;  // plan order
@@ -88,7 +89,24 @@ struct saln_nw_plan {
     uint32_t wait_limit = kWaitLimitDefault;
     bool unchecked[2] = {false, false};  // executes on workspace b since the last status
     uint64_t n_prog = 0;
-    uint32_t *d_ops = nullptr;  // traceback op-stream scratch (one traceback at a time)
+    uint32_t *d_ops = nullptr;  // traceback op-stream scratch of workspace 0
+    uint32_t *d_ops2 = nullptr;  // ... of workspace 1 (async: its walks may overlap workspace 0's)
+    uint64_t ops_words = 0;
+    // per workspace: the table fills' bail word (16 bytes), then the fused
+    // fill + walk's per-pack arrival words (8 bytes) and walk-left flags of
+    // the 8 x 19 variant (nw_fill_walk_kernel); zeroed once, self-clearing
+    uint8_t *d_fuse[2] = {nullptr, nullptr};
+    uint32_t fuse_packs = 0;
+    uint32_t epoch = 0;  // table launches of this plan (the bail word's values)
+    bool fused[kNumVariants] = {};  // the last execute's fill walked the variant itself
+    uint64_t fuse_bytes() const { return 16 + (uint64_t)fuse_packs * 12; }
+    uint32_t *bail(int b) const { return reinterpret_cast<uint32_t *>(d_fuse[b]); }
+    unsigned long long *arrive(int b) const {
+        return reinterpret_cast<unsigned long long *>(d_fuse[b] + 16);
+    }
+    uint32_t *walk_left(int b) const {
+        return reinterpret_cast<uint32_t *>(d_fuse[b] + 16 + (uint64_t)fuse_packs * 8);
+    }
     // speculative stripe walks (a few long column-stripe pairs): block map,
     // pairs, stripe records, run words, per-pair done flags (plan order)
     uint32_t spec_pairs = 0, spec_blocks = 0;
@@ -110,10 +128,9 @@ struct saln_nw_plan {
     std::map<std::string, std::pair<double, uint64_t>> ktime;
     int resolve_events();
     // the two events after the sub-batch events mark "traceback of workspace b done"
-    hipEvent_t tb_done(int b) const { return sync_ev[sync_ev.size() - 2 + b]; }
-    // fill/traceback pipelining: plan-order boundaries of the sub-batches of
-    // [0, n_fill) and one sync event per sub-batch (+1 for the final join)
-    std::vector<uint32_t> sub;
+    hipEvent_t tb_done(int b) const { return sync_ev[1 + b]; }
+    // fill -> traceback stream hand-off (async) and "traceback of workspace b
+    // done" (two events)
     std::vector<hipEvent_t> sync_ev;
 };
 
@@ -167,7 +184,8 @@ int saln_nw_plan_destroy(saln_nw_plan *p) {
     (void)hipDeviceSynchronize();  // the blocks go back to the context cache
     for (void *b : {(void *)p->d_pairs, (void *)p->d_mask, (void *)p->d_mask2, (void *)p->d_endh2,
                     (void *)p->d_scratch, (void *)p->d_work, (void *)p->d_prog, (void *)p->d_err,
-                    (void *)p->d_ops, (void *)p->d_endh, (void *)p->d_spec_blocks,
+                    (void *)p->d_ops, (void *)p->d_ops2, (void *)p->d_fuse[0], (void *)p->d_fuse[1],
+                    (void *)p->d_endh, (void *)p->d_spec_blocks,
                     (void *)p->d_spec_pairs, (void *)p->d_spec_stripes, (void *)p->d_spec_ops,
                     (void *)p->d_spec_done})
         dev_free(p->ctx, b);
@@ -208,16 +226,18 @@ int saln::plan_create(saln_context *ctx, const uint64_t *q_off, uint64_t n_q,
     }
     if (n_pairs > 0xFFFFFFFFull) return SALN_E_INVALID;
     HIP_TRY(hipSetDevice(ctx->device));
-    StageClock clk;
+    const Options opts = ctx->opts.effective();
+    StageClock clk(opts);
     auto *p = new saln_nw_plan;
     p->ctx = ctx;
+    p->opts = opts;
     p->sc = scoring_or_default(scoring);
     p->full_codes = full_codes;
-    // 4-bit walk codes (option nw.nib_codes): variant 7 may keep bytes, the
-    // 8 x 19 variant (option nw.narrow_walk, queries of <= 152 columns) has
-    // only 4-bit codes; full-code plans keep byte codes and the 16 x 10 groups
-    const bool nib_on = !full_codes && opt(Opt::NibCodes) != 0;
-    const bool narrow = nib_on && opt(Opt::NarrowWalk) != 0;
+    // 4-bit walk codes for the short-query packed variants: 8 x 19 groups for
+    // queries of <= 152 columns, 16 x 10 up to 160; full-code plans keep byte
+    // codes and the 16 x 10 groups
+    const bool nib_on = !full_codes;
+    const bool narrow = nib_on;
     for (int v = 0; v < kNumVariants; ++v) p->nib[v] = nib_on && variant_nib(v);
     p->n_pairs = n_pairs;
     p->cigar_off.resize(n_pairs + 1);
@@ -274,7 +294,7 @@ int saln::plan_create(saln_context *ctx, const uint64_t *q_off, uint64_t n_q,
         // throughput choice (two pairs per wave), the column stripes the
         // latency choice (four waves per pair, pipelined): a plan with few
         // such pairs keeps them on stripes.
-        const uint64_t v8_min = (uint64_t)opt(Opt::WideMinPairs);
+        const uint64_t v8_min = (uint64_t)opts[Opt::WideMinPairs];
         uint64_t wide = 0;
         for (const NwPairDesc &d : descs)
             wide += d.variant == (uint32_t)kWidePackedVariant && d.len_q > 512;
@@ -347,8 +367,8 @@ int saln::plan_create(saln_context *ctx, const uint64_t *q_off, uint64_t n_q,
         // 400 x 5 kbp^2 953 vs 1,204 (one box, round 2)
         const bool wide = p->var_count[kStripeVariant] &&
                           cols / p->var_count[kStripeVariant] >= 3000;
-        p->stripe_pk = waves > 0 && free_all && stripe_packed(p->sc, waves, wide);
-        p->stripe_rows = p->stripe_pk ? 0 : stripe_rows_k(waves_k1);
+        p->stripe_pk = waves > 0 && free_all && stripe_packed(p->sc, waves, wide, opts);
+        p->stripe_rows = p->stripe_pk ? 0 : stripe_rows_k(waves_k1, opts);
         // boundary columns per 256-column chunk: the row fill's 4 / K stripes,
         // else one; the scratch offsets above reserved kStripeSubMax
         p->stripe_sub = p->stripe_rows ? 4u / (uint32_t)p->stripe_rows : 1u;
@@ -420,15 +440,7 @@ int saln::plan_create(saln_context *ctx, const uint64_t *q_off, uint64_t n_q,
         }
     }
     {
-        // sub-batches for fill/traceback overlap inside one execute
-        // (SALN_TB_CHUNKS, default 1); boundaries kept even so packed groups
-        // stay paired
-        const uint32_t nsub = (uint32_t)opt(Opt::TbChunks);
-        const uint32_t step = ((p->n_fill + nsub - 1) / nsub + 1) & ~1u;
-        p->sub.push_back(0);
-        for (uint32_t b = step; b < p->n_fill; b += step) p->sub.push_back(b);
-        p->sub.push_back(p->n_fill);
-        p->sync_ev.resize(p->sub.size() + 1);
+        p->sync_ev.resize(3);
         for (auto &e : p->sync_ev) {
             if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
                 e = nullptr;
@@ -494,19 +506,26 @@ int saln::plan_create(saln_context *ctx, const uint64_t *q_off, uint64_t n_q,
     clk.mark("plan: mask+work");
     if (soff && (e = dev_alloc(p->ctx, (void **)&p->d_scratch, soff * sizeof(int2))) != hipSuccess)
         return fail(e, "hipMalloc(scratch)");
+    p->ops_words = ooff;
     if (ooff && (e = dev_alloc(p->ctx, (void **)&p->d_ops, ooff * sizeof(uint32_t))) != hipSuccess)
         return fail(e, "hipMalloc(op stream)");
+    if (p->nib[kNarrowVariant] && p->var_count[kNarrowVariant])
+        p->fuse_packs = n_packs(p->var_count[kNarrowVariant]);
+    if ((p->var_count[kNarrowVariant] && p->nib[kNarrowVariant]) || (p->var_count[7] && p->nib[7])) {
+        if ((e = dev_alloc(p->ctx, (void **)&p->d_fuse[0], p->fuse_bytes())) != hipSuccess ||
+            (e = hipMemset(p->d_fuse[0], 0, p->fuse_bytes())) != hipSuccess)
+            return fail(e, "fused fill + walk words");
+    }
     {
         // Speculative stripe walks: a few long column-stripe pairs walk all
         // their 256-column stripes at once (nw_traceback_coop_kernel kSpec)
         // instead of one stripe after another (C4: walk 3.8 ms).  Off with
         // option nw.spec = 0; nw.spec_passes walk passes (default 3).
-        const int passes = (int)opt(Opt::SpecPasses);
+        const int passes = (int)opts[Opt::SpecPasses];
         const uint32_t nv = p->var_count[kStripeVariant];
         std::vector<SpecPair> sp;
         std::vector<uint2> blocks;
-        if (opt(Opt::Spec) != 0 && passes > 0 && nv && nv <= kSpecMaxPairs &&
-            p->sub.size() == 2) {
+        if (opts[Opt::Spec] != 0 && passes > 0 && nv && nv <= kSpecMaxPairs) {
             for (uint32_t r = p->var_first[kStripeVariant]; r < p->var_first[kStripeVariant] + nv; ++r) {
                 const NwPairDesc &d = p->h_pairs[r];
                 const uint32_t S = (d.len_q + 255) / 256;
@@ -519,7 +538,7 @@ int saln::plan_create(saln_context *ctx, const uint64_t *q_off, uint64_t n_q,
             p->spec_pairs = (uint32_t)sp.size();
             p->spec_blocks = (uint32_t)blocks.size();
             p->spec_passes = passes;
-            p->spec_strict = opt(Opt::SpecStrict) != 0;
+            p->spec_strict = opts[Opt::SpecStrict] != 0;
             if ((e = dev_alloc(p->ctx, (void **)&p->d_spec_blocks, blocks.size() * sizeof(uint2))) != hipSuccess ||
                 (e = hipMemcpy(p->d_spec_blocks, blocks.data(), blocks.size() * sizeof(uint2),
                                hipMemcpyHostToDevice)) != hipSuccess ||
@@ -584,31 +603,31 @@ int saln_nw_execute(saln_nw_plan *p, const uint8_t *d_q, const uint8_t *d_db,
     if (p->n_pairs == 0) return SALN_OK;
     HIP_TRY(hipSetDevice(p->ctx->device));
     hipStream_t s = resolve_stream(stream, p->ctx);
-    const size_t nsub = p->sub.size() - 1;  // >= 1 (an empty sub-batch if n_fill == 0)
-    // the traceback stream: the second one only when a traceback can overlap a
-    // fill (async plans, sub-batches); otherwise the same stream, so no
+    // the traceback stream: the second one only in async plans (the walk of
+    // execute n beside the fill of n+1); otherwise the same stream, so no
     // cross-stream hand-off sits between the fill and the walk
-    hipStream_t t = (p->async_tb || nsub > 1) ? (p->tb_stream ? p->tb_stream : p->ctx->tb_stream) : s;
+    hipStream_t t = p->async_tb ? (p->tb_stream ? p->tb_stream : p->ctx->tb_stream) : s;
     const int cur = p->async_tb ? p->buf : 0;
     uint8_t *mask = cur ? p->d_mask2 : p->d_mask;
     int32_t *endh = cur ? p->d_endh2 : p->d_endh;
+    uint32_t *ops = cur ? p->d_ops2 : p->d_ops;
     // this workspace may still be read by the traceback of execute n-2
     if (p->tb_pending[cur]) HIP_TRY(hipStreamWaitEvent(s, p->tb_done(cur), 0));
     // boundary columns preset to kColEmpty: a row is published once its value
     // replaces the preset (nw_fill_rows_kernel).  Issued ahead of the timing
     // events, so "nw_fill" times the fill kernels alone.
-    for (size_t k = 0; k + 1 < p->sub.size(); ++k) {
-        const uint32_t a = std::max(p->sub[k], p->var_first[kStripeVariant]);
-        const uint32_t b = std::min(p->sub[k + 1], p->var_first[kStripeVariant] +
-                                                       p->var_count[kStripeVariant]);
-        if (a >= b || p->work_first[b] <= p->work_first[a]) continue;
-        const NwPairDesc &la = p->h_pairs[b - 1];
-        const uint64_t c0 = p->h_pairs[a].scratch_off;
-        const uint64_t c1 = la.scratch_off + (uint64_t)p->stripe_sub *
-                                                 variant_geom(kStripeVariant).n_chunks(la.len_q) *
-                                                 scratch_col(la.len_db);
-        HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)(p->d_scratch + c0), (int)0x80000000u,
-                                  2 * (c1 - c0), s));
+    {
+        const uint32_t a = p->var_first[kStripeVariant];
+        const uint32_t b = a + p->var_count[kStripeVariant];
+        if (a < b && p->work_first[b] > p->work_first[a]) {
+            const NwPairDesc &la = p->h_pairs[b - 1];
+            const uint64_t c0 = p->h_pairs[a].scratch_off;
+            const uint64_t c1 = la.scratch_off + (uint64_t)p->stripe_sub *
+                                                     variant_geom(kStripeVariant).n_chunks(la.len_q) *
+                                                     scratch_col(la.len_db);
+            HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)(p->d_scratch + c0), (int)0x80000000u,
+                                      2 * (c1 - c0), s));
+        }
     }
     hipEvent_t *ev = nullptr;
     if (p->timing) {
@@ -620,51 +639,59 @@ int saln_nw_execute(saln_nw_plan *p, const uint8_t *d_q, const uint8_t *d_db,
         ev = p->ev_pool[p->ev_used++].data();
         HIP_TRY(hipEventRecord(ev[0], s));
     }
-    // Sub-batch k: fill on `s`, then its traceback on `t`; with two streams
-    // the (latency-bound) traceback overlaps the next fill.
-    for (size_t k = 0; k < nsub; ++k) {
-        const uint32_t lo = p->sub[k], hi = p->sub[k + 1];
-        for (int v = 0; v < kNumVariants; ++v) {
-            const uint32_t a = std::max(lo, p->var_first[v]);
-            const uint32_t b = std::min(hi, p->var_first[v] + p->var_count[v]);
-            if (a < b && v == kStripeVariant) {
-                const uint32_t w0 = p->work_first[a], w1 = p->work_first[b];
-                if (w1 > w0) {
-                    HIP_TRY(launch_fill_stripes(p->d_pairs, p->d_work + w0, w1 - w0, d_q, d_db,
-                                                mask, p->d_scratch, p->d_prog, p->d_err, endh,
-                                                p->sc,
-                                                p->score_only ? 2 : p->full_codes ? 1 : 0,
-                                                p->stripe_layout(), p->stripe_rows, s));
-                }
-            } else if (a < b)
-                HIP_TRY(launch_fill(v, p->d_pairs, a, b - a, d_q, d_db, mask, p->d_scratch, endh,
-                                    d_results, d_cigar, p->sc,
-                                    p->score_only ? 2 : p->full_codes ? 1 : p->nib[v] ? 3 : 0,
-                                    p->var_maxld[v], s));
+    // fills on `s`, then the walks on `t` (async: beside the next fill).  The
+    // 8 x 19 table fill walks its packs in the same launch (nw.fuse_walk);
+    // its walker launch then only takes the packs the fill left to it.
+    FillExtras fx;
+    fx.o = &p->opts;
+    fx.bail = p->d_fuse[cur] ? p->bail(cur) : nullptr;
+    fx.ops = ops;
+    for (int v = 0; v < kNumVariants; ++v) {
+        const uint32_t a = p->var_first[v], b = a + p->var_count[v];
+        p->fused[v] = false;
+        if (a >= b) continue;
+        if (v == kStripeVariant) {
+            const uint32_t w0 = p->work_first[a], w1 = p->work_first[b];
+            if (w1 > w0)
+                HIP_TRY(launch_fill_stripes(p->d_pairs, p->d_work + w0, w1 - w0, d_q, d_db, mask,
+                                            p->d_scratch, p->d_prog, p->d_err, endh, p->sc,
+                                            p->score_only ? 2 : p->full_codes ? 1 : 0,
+                                            p->stripe_layout(), p->stripe_rows, s, p->opts));
+            continue;
         }
-        if (ev && k + 1 == nsub) HIP_TRY(hipEventRecord(ev[1], s));
-        HIP_TRY(hipEventRecord(p->sync_ev[k], s));
-        if (t != s) HIP_TRY(hipStreamWaitEvent(t, p->sync_ev[k], 0));
-        if (ev && k == 0) HIP_TRY(hipEventRecord(ev[2], t));
-        for (int v = 0; v < kNumVariants; ++v) {
-            const uint32_t a = std::max(lo, p->var_first[v]);
-            const uint32_t b = std::min(hi, p->var_first[v] + p->var_count[v]);
-            const bool spec = v == kStripeVariant && p->spec_pairs && !p->score_only;
-            if (a < b && spec)
-                HIP_TRY(launch_traceback_spec(
-                    p->d_pairs,
-                    SpecArgs{p->d_spec_blocks, p->d_spec_pairs, p->d_spec_stripes, p->d_spec_ops,
-                             p->d_spec_done, 0},
-                    p->spec_blocks, p->spec_pairs, p->d_spec_done, p->spec_passes, d_q, d_db, mask,
-                    endh, d_results, d_cigar, p->sc, p->stripe_layout(),
-                    p->spec_strict ? p->d_err : nullptr, t));
-            if (a < b && p->score_only)
-                HIP_TRY(launch_score_results(p->d_pairs, a, b - a, endh, d_results, p->sc, t));
-            else if (a < b)
-                HIP_TRY(launch_traceback(v, p->d_pairs, a, b - a, d_q, d_db, mask, endh, p->d_ops,
-                                         d_results, d_cigar, p->sc, p->stripe_layout(), t,
-                                         spec ? p->d_spec_done : nullptr, p->nib[v]));
-        }
+        const bool fuse = v == kNarrowVariant && !p->score_only && p->fuse_packs;
+        fx.epoch = ++p->epoch;
+        fx.arrive = fuse ? p->arrive(cur) : nullptr;
+        fx.walk_left = fuse ? p->walk_left(cur) : nullptr;
+        HIP_TRY(launch_fill(v, p->d_pairs, a, b - a, d_q, d_db, mask, p->d_scratch, endh,
+                            d_results, d_cigar, p->sc,
+                            p->score_only ? 2 : p->full_codes ? 1 : p->nib[v] ? 3 : 0,
+                            p->var_maxld[v], s, fx));
+        p->fused[v] = fx.fused;
+    }
+    if (ev) HIP_TRY(hipEventRecord(ev[1], s));
+    HIP_TRY(hipEventRecord(p->sync_ev[0], s));
+    if (t != s) HIP_TRY(hipStreamWaitEvent(t, p->sync_ev[0], 0));
+    if (ev) HIP_TRY(hipEventRecord(ev[2], t));
+    for (int v = 0; v < kNumVariants; ++v) {
+        const uint32_t a = p->var_first[v], b = a + p->var_count[v];
+        if (a >= b) continue;
+        const bool spec = v == kStripeVariant && p->spec_pairs && !p->score_only;
+        if (spec)
+            HIP_TRY(launch_traceback_spec(
+                p->d_pairs,
+                SpecArgs{p->d_spec_blocks, p->d_spec_pairs, p->d_spec_stripes, p->d_spec_ops,
+                         p->d_spec_done, 0},
+                p->spec_blocks, p->spec_pairs, p->d_spec_done, p->spec_passes, d_q, d_db, mask,
+                endh, d_results, d_cigar, p->sc, p->stripe_layout(),
+                p->spec_strict ? p->d_err : nullptr, t));
+        if (p->score_only)
+            HIP_TRY(launch_score_results(p->d_pairs, a, b - a, endh, d_results, p->sc, t));
+        else
+            HIP_TRY(launch_traceback(v, p->d_pairs, a, b - a, d_q, d_db, mask, endh, ops,
+                                     d_results, d_cigar, p->sc, p->stripe_layout(), t,
+                                     spec ? p->d_spec_done : nullptr, p->nib[v],
+                                     p->fused[v] ? p->walk_left(cur) : nullptr));
     }
     // pairs with an empty side (boundary-only walk) ride on the traceback stream
     if (p->n_pairs > p->n_fill && p->score_only)
@@ -672,7 +699,7 @@ int saln_nw_execute(saln_nw_plan *p, const uint8_t *d_q, const uint8_t *d_db,
                                      endh, d_results, p->sc, t));
     else if (p->n_pairs > p->n_fill)
         HIP_TRY(launch_traceback(-1, p->d_pairs, p->n_fill, (uint32_t)(p->n_pairs - p->n_fill),
-                                 d_q, d_db, mask, endh, p->d_ops, d_results, d_cigar, p->sc,
+                                 d_q, d_db, mask, endh, ops, d_results, d_cigar, p->sc,
                                  p->stripe_layout(), t));
     if (ev) HIP_TRY(hipEventRecord(ev[3], t));
     HIP_TRY(hipEventRecord(p->tb_done(cur), t));
@@ -700,6 +727,12 @@ int saln_nw_plan_set_async(saln_nw_plan *p, int enable) {
     if (enable && !p->d_mask2 && p->mask_bytes) {
         HIP_TRY(dev_alloc(p->ctx, (void **)&p->d_mask2, p->mask_bytes + 64));
         HIP_TRY(dev_alloc(p->ctx, (void **)&p->d_endh2, p->n_pairs * sizeof(int32_t)));
+        if (p->ops_words)
+            HIP_TRY(dev_alloc(p->ctx, (void **)&p->d_ops2, p->ops_words * sizeof(uint32_t)));
+        if (p->d_fuse[0]) {
+            HIP_TRY(dev_alloc(p->ctx, (void **)&p->d_fuse[1], p->fuse_bytes()));
+            HIP_TRY(hipMemset(p->d_fuse[1], 0, p->fuse_bytes()));
+        }
     }
     p->async_tb = enable != 0;
     p->buf = 0;

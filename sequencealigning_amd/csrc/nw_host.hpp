@@ -19,6 +19,7 @@
 
 struct saln_context {
     int device = 0;
+    saln::OptOverrides opts;  // saln_context_option_set (on top of the process registry)
     hipStream_t stream = nullptr;
     hipStream_t tb_stream = nullptr;  // traceback stream (pipelined NW plans)
     // Device blocks released by plans / host-path calls, kept for reuse
@@ -60,7 +61,8 @@ namespace saln {
 
 // option host.timing = 1: stage times of the host-side paths on stderr
 struct StageClock {
-    bool on = opt(Opt::HostTiming) != 0;
+    bool on;
+    explicit StageClock(const Options &o) : on(o[Opt::HostTiming] != 0) {}
     std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
     void mark(const char *what) {
         if (!on) return;
@@ -82,17 +84,35 @@ void dev_cache_clear(saln_context *ctx);
 hipError_t pinned_staging(saln_context *ctx, size_t n, void **p);  // caller holds ctx->staging_mu
 
 // kernels (nw_kernels.hip)
+// What a packed fill launch needs besides the pairs: the plan's options, the
+// workspace's bail word and the launch's epoch (4-bit-code table fills: the
+// fallback launch runs only when a wave of its table launch left pairs to it),
+// and for the fused fill + walk of the 8 x 19 variant (nw_fill_walk_kernel)
+// the workspace's per-pack arrival and walk-left words and the walk outputs.
+// fused: set when the launch walked (or marked) every pair itself.
+struct FillExtras {
+    const Options *o = nullptr;
+    uint32_t *bail = nullptr;
+    uint32_t epoch = 0;
+    unsigned long long *arrive = nullptr;  // non-null: fuse the walk when the table fill runs
+    uint32_t *walk_left = nullptr;
+    uint32_t *ops = nullptr;
+    bool fused = false;
+};
 hipError_t launch_fill(int variant, const NwPairDesc *pairs, uint32_t first, uint32_t count,
                        const uint8_t *qs, const uint8_t *ds, uint8_t *mask, int2 *scratch,
                        int32_t *end_h, saln_nw_result *results, uint32_t *cigar, Scoring sc,
                        int codes /* 0 walk, 1 full, 2 none, 3 4-bit walk */, uint32_t ld_max,
-                       hipStream_t stream);
+                       hipStream_t stream, FillExtras &fx);
+// mask packs (64 pairs) of a variant range: the fused kernel's per-pack words
+inline uint32_t n_packs(uint32_t count) { return (count + 63) / 64; }
 hipError_t launch_fill_stripes(const NwPairDesc *pairs, const uint2 *work, uint32_t n_work,
                                const uint8_t *qs, const uint8_t *ds, uint8_t *mask,
                                int2 *scratch, uint32_t *prog, uint32_t *err, int32_t *end_h,
                                Scoring sc, int codes /* 0 walk, 1 full, 2 none */,
                                int layout /* 0 skewed, 1 packed, 2 row-major tiles */,
-                               int rows_k /* layout 2: columns per lane */, hipStream_t stream);
+                               int rows_k /* layout 2: columns per lane */, hipStream_t stream,
+                               const Options &o);
 hipError_t launch_cigar_compact(const saln_nw_result *res, const uint64_t *src_off,
                                 const uint64_t *dst_off, const uint32_t *src, uint32_t *dst,
                                 uint64_t n, hipStream_t stream);
@@ -102,10 +122,10 @@ constexpr int kStripeVariant = 3;
 constexpr uint32_t kStripeSubMax = 4;
 // row fill (nw_fill_rows_kernel) columns per lane, 0 = the skewed stripe fill;
 // waves_k1: the plan's stripe waves at one column per lane
-int stripe_rows_k(uint64_t waves_k1);
+int stripe_rows_k(uint64_t waves_k1, const Options &o);
 // column stripes run the packed (int16 halves) fill for this scoring and
 // this many stripe waves in the plan (decided once per plan: it sets the layout)
-bool stripe_packed(const Scoring &sc, uint64_t n_waves, bool wide);
+bool stripe_packed(const Scoring &sc, uint64_t n_waves, bool wide, const Options &o);
 constexpr int kWidePackedVariant = 8;        // packed, 64-lane groups, up to 1,024 columns
 constexpr uint64_t kWidePackedMinPairs = 1536;  // fewer such pairs: column stripes (measured crossover 1,024-2,048)
 hipError_t launch_score_results(const NwPairDesc *pairs, uint32_t first, uint32_t n,
@@ -116,7 +136,8 @@ hipError_t launch_traceback(int variant, const NwPairDesc *pairs, uint32_t first
                             const uint8_t *ds, const uint8_t *mask, const int32_t *end_h,
                             uint32_t *ops, saln_nw_result *results, uint32_t *cigar, Scoring sc,
                             int stripe_layout, hipStream_t stream,
-                            const uint32_t *spec_done = nullptr, bool nib = false);
+                            const uint32_t *spec_done = nullptr, bool nib = false,
+                            const uint32_t *walk_left = nullptr);
 // variants whose walk codes may be 4-bit (kCodesNib): the short-query packed
 // fills 7 (16 x 10) and 4 (8 x 19, 4-bit only)
 inline bool variant_nib(int v) { return v == 7 || v == 4; }
@@ -153,13 +174,13 @@ hipError_t launch_avsa_prof(const uint64_t *q_off, const uint64_t *d_off, const 
                             uint32_t nq, const uint32_t *d_ids, uint32_t nq_total, uint64_t base,
                             uint32_t count, const uint8_t *qs, const uint8_t *ds, int2 *out,
                             Scoring sc, uint32_t ld_max, const uint32_t *generic,
-                            hipStream_t stream);
+                            hipStream_t stream, const Options &o);
 hipError_t launch_acgt_check(const uint8_t *seq, uint64_t n, uint32_t *flag, hipStream_t stream);
 hipError_t launch_avsa(int variant, const uint64_t *q_off, const uint64_t *d_off,
                        const uint32_t *q_ids, uint32_t nq, const uint32_t *d_ids,
                        uint32_t nq_total, uint64_t base, uint32_t count, const uint8_t *qs,
                        const uint8_t *ds, int2 *out, Scoring sc, uint32_t ld_max,
-                       hipStream_t stream, const uint32_t *generic = nullptr);
+                       hipStream_t stream, const Options &o, const uint32_t *generic = nullptr);
 hipError_t launch_avsa_boundary(const uint64_t *q_off, const uint64_t *d_off,
                                 const uint32_t *q_ids, uint32_t nq, const uint32_t *d_ids,
                                 uint64_t n, uint32_t nq_total, int2 *out, Scoring sc,

@@ -25,11 +25,12 @@
 #include <utility>
 
 #include "nw_common.hpp"
+#include "nw_host.hpp"
 #include "saln_options.hpp"
 #include "saln.h"
 
 namespace saln {
-bool stripe_packed(const Scoring &sc, uint64_t n_waves, bool wide);
+bool stripe_packed(const Scoring &sc, uint64_t n_waves, bool wide, const Options &o);
 }
 
 namespace saln {
@@ -244,31 +245,30 @@ constexpr uint32_t kOpsPerWord = 10;                     // 3-bit ops per op-str
 // latency: round 3 measured (NW x W) 2 x 4 0.26 ms, 2 x 8 0.28, 3 x 4 0.30,
 // 3 x 6 0.30 (tools/exp_ab_c2.sh, one box), so the default is the leanest.
 // NW = 3 keeps block B-2 resident too (no synchronous reload when a path
-// crosses two blocks within W rows); SALN_WALK_NW / SALN_WALK_W select it.
-#ifndef SALN_WALK_W
-#define SALN_WALK_W 0  // experiment switches: force the window depth / count
-#endif
-#ifndef SALN_WALK_NW
-#define SALN_WALK_NW 0
-#endif
+// crosses two blocks within W rows) and was slower.
 // kNib: 4-bit walk codes (Geom::LBn-byte segments) and the pair's query
 // staged in LDS after the windows: QC 16-byte chunks per lane, [chunk][lane]
 // (the LDS-DMA order), enough for a variant of `cols` query columns at any
-// 16-byte misalignment.
-template <int K, bool kNib = false, uint32_t kCols = 0>
+// 16-byte misalignment.  kQCodes (the fused fill + walk, nw_fill_walk_kernel):
+// the query as 2-bit codes ((c >> 1) & 3; A, C, G, T only) instead, QD
+// dwords of 16 columns per lane, [dword][lane]: 2.5 KB for 152 columns
+// against 11 KB of bytes, so the fused kernel keeps three waves per SIMD.
+template <int K, bool kNib = false, uint32_t kCols = 0, bool kQCodes = false>
 struct WalkGeo {
     static constexpr uint32_t LB = kNib ? 4 * ((K + 3) / 4 / 2 + 1) : (K + 3) / 4 * 4;
-    static constexpr uint32_t NW = SALN_WALK_NW ? SALN_WALK_NW : 2;
-    static constexpr uint32_t W = SALN_WALK_W ? SALN_WALK_W : (K < 16 || kNib ? 4 : 8);
+    static constexpr uint32_t NW = 2;
+    static constexpr uint32_t W = K < 16 || kNib ? 4 : 8;
     static constexpr uint32_t SB = LB == 12 ? 12 : 16;        // DMA bytes per lane
     static constexpr uint32_t kSlotBytes = 64 * 16;          // one slot of a wave
     static constexpr uint32_t kWinBytes = W * kSlotBytes;    // one window of a wave
-    static constexpr uint32_t QC = kNib ? (15 + kCols + 15) / 16 : 0;
-    static constexpr uint32_t kWaveLds = NW * kWinBytes + QC * kSlotBytes;
+    static constexpr uint32_t QC = kNib && !kQCodes ? (15 + kCols + 15) / 16 : 0;
+    static constexpr uint32_t QD = kQCodes ? (kCols + 15) / 16 : 0;
+    static constexpr uint32_t kWaveLds = NW * kWinBytes + QC * kSlotBytes + QD * 256;
     static constexpr uint32_t kVmcnt = NW * (W - 1);
     static_assert(LB <= 16, "LDS window slots hold 16 bytes per lane");
     static_assert((NW == 2 || NW == 3) && W >= 2 && W <= 8, "8 valid bits per window");
     static_assert(!kNib || kCols > 0, "4-bit walk: the variant's query width");
+    static_assert(!kQCodes || kNib, "query codes: 4-bit walk codes");
 };
 
 typedef __attribute__((address_space(3))) uint8_t lds_u8;
@@ -339,12 +339,12 @@ __device__ __forceinline__ void unroll_each(F &&f, std::integer_sequence<uint32_
 // byte's 1 / 3 / 5, so the same kNextLut decides; the end cell's state set
 // is its nibble's argI, argD and (last row) argM-in-D-open bits; '=' / 'X'
 // compare the query byte (LDS) with the row's db char in the segment.
-template <int G, int K, bool kNib = false>
+template <int G, int K, bool kNib = false, bool kQCodes = false>
 __device__ void walk_pack_lds(const NwPairDesc &p, int32_t hend, const uint8_t *__restrict__ mask,
                               uint32_t *__restrict__ ops_all, saln_nw_result *__restrict__ results,
                               uint32_t *__restrict__ cigar, Scoring sc, lds_u8 *win,
                               const uint8_t *__restrict__ qs) {
-    using WG = WalkGeo<K, kNib, G * K>;
+    using WG = WalkGeo<K, kNib, G * K, kQCodes>;
     constexpr Geom geo{G, K};
     constexpr uint32_t kW = WG::W, NW = WG::NW;
     constexpr uint32_t kWin = WG::kWinBytes, kSlot = WG::kSlotBytes;
@@ -385,7 +385,30 @@ __device__ void walk_pack_lds(const NwPairDesc &p, int32_t hend, const uint8_t *
     // every window DMA, so the counted waits below also cover them
     const uint32_t qa = (uint32_t)(p.q_off & 15u);
     lds_u8 *const qlds = win + NW * kWin;
-    if constexpr (kNib) {
+    if constexpr (kQCodes) {
+        // the query's bytes (dword loads from its 4-byte-aligned start; only
+        // dwords holding query bytes) as 2-bit codes, 16 columns per dword:
+        // y = the codes in bytes 0-3, y * 0x41041 gathers them into bits 18..25
+        const uint32_t qa4 = (uint32_t)(p.q_off & 3u);
+        const uint32_t *qw = reinterpret_cast<const uint32_t *>(qs + (p.q_off - qa4));
+        const uint32_t nsrc = (qa4 + p.len_q + 3u) / 4u;
+        constexpr uint32_t NS = 4 * WG::QD + 1;
+        uint32_t src[NS];
+#pragma unroll
+        for (uint32_t i = 0; i < NS; ++i) src[i] = i < nsrc ? qw[i] : 0u;
+#pragma unroll
+        for (uint32_t d = 0; d < WG::QD; ++d) {
+            uint32_t code = 0;
+#pragma unroll
+            for (uint32_t k = 0; k < 4; ++k) {
+                const uint32_t x = __builtin_amdgcn_alignbyte(src[4 * d + k + 1], src[4 * d + k], qa4);
+                const uint32_t y = (x >> 1) & 0x03030303u;
+                code |= ((y * 0x00041041u) >> 18 & 0xFFu) << (8u * k);
+            }
+            *reinterpret_cast<__attribute__((address_space(3))) uint32_t *>(
+                qlds + d * 256u + (threadIdx.x & 63u) * 4u) = code;
+        }
+    } else if constexpr (kNib) {
         const uint8_t *qg = qs + (p.q_off - qa);
         const uint32_t qlast = (qa + p.len_q - 1u) / 16u;
 #pragma unroll
@@ -394,10 +417,17 @@ __device__ void walk_pack_lds(const NwPairDesc &p, int32_t hend, const uint8_t *
                                              (__attribute__((address_space(3))) void *)(qlds + c * kSlot),
                                              16, 0, 0);
     }
-    // query byte j (1-based) of this lane's pair
-    auto qbyte = [&](uint32_t j) __attribute__((always_inline)) {
-        const uint32_t o = qa + j - 1u;
-        return (uint32_t)qlds[(o >> 4) * kSlot + (threadIdx.x & 63u) * 16u + (o & 15u)];
+    // query column j (1-based) of this lane's pair equals the db char dch
+    auto qeq = [&](uint32_t j, uint32_t dch) __attribute__((always_inline)) {
+        if constexpr (kQCodes) {
+            const uint32_t o = j - 1u;
+            const uint32_t w = *reinterpret_cast<const __attribute__((address_space(3))) uint32_t *>(
+                qlds + (o >> 4) * 256u + (threadIdx.x & 63u) * 4u);
+            return ((w >> (2u * (o & 15u))) & 3u) == ((dch >> 1) & 3u);
+        } else {
+            const uint32_t o = qa + j - 1u;
+            return (uint32_t)qlds[(o >> 4) * kSlot + (threadIdx.x & 63u) * 16u + (o & 15u)] == dch;
+        }
     };
     // db char byte of a 4-bit segment (Geom::nib_char_byte)
     constexpr uint32_t kNG = (K + 3) / 4, kCB = kNG % 2 ? 4 * (kNG / 2) + 2 : 4 * (kNG / 2);
@@ -507,7 +537,7 @@ __device__ void walk_pack_lds(const NwPairDesc &p, int32_t hend, const uint8_t *
                         f3 = sidx == 48u ? end_bits(__builtin_amdgcn_ubfe(dw, nib_bit(col), 4))
                                          : __builtin_amdgcn_ubfe(dw, nib_bit(col) + lsh, 3);
                         const uint32_t dch = __builtin_amdgcn_ubfe(pick(seg, kCB >> 2), (kCB & 3u) * 8u, 8);
-                        eqb = qbyte(tj) == dch ? 1u : 0u;
+                        eqb = qeq(tj, dch) ? 1u : 0u;
                     } else {
                         const uint32_t dw = pick(seg, col >> 2), b8 = (col & 3u) * 8u;
                         f3 = __builtin_amdgcn_ubfe(dw, b8 + lsh, 3);
@@ -547,8 +577,7 @@ __device__ void walk_pack_lds(const NwPairDesc &p, int32_t hend, const uint8_t *
                     const uint32_t c1 = 31u - (uint32_t)__builtin_clz(pm), n = col - c1;
                     uint32_t eqb;
                     if constexpr (kNib)
-                        eqb = qbyte(tj - n) ==
-                                      __builtin_amdgcn_ubfe(pick(seg, kCB >> 2), (kCB & 3u) * 8u, 8)
+                        eqb = qeq(tj - n, __builtin_amdgcn_ubfe(pick(seg, kCB >> 2), (kCB & 3u) * 8u, 8))
                                   ? 1u : 0u;
                     else
                         eqb = __builtin_amdgcn_ubfe(pick(seg, c1 >> 2), (c1 & 3u) * 8u + 7u, 1);
@@ -698,25 +727,30 @@ __device__ void walk_pack_lds(const NwPairDesc &p, int32_t hend, const uint8_t *
 // LDS of a wave).
 template <int G, int K, bool kNib = false>
 constexpr uint32_t tb_lds_threads() { return kNib ? 128u : 256u; }
+// walk_left (fused fill + walk plans): only the packs (64 pairs, one wave)
+// whose fill launch left them here are walked; the flag is cleared for the
+// next execute.
 template <int G, int K, bool kNib>
 __global__ __launch_bounds__(256) void nw_traceback_lds_kernel(
     const NwPairDesc *__restrict__ pairs, uint32_t first, uint32_t n,
     const uint8_t *__restrict__ mask, const int32_t *__restrict__ end_h,
     uint32_t *__restrict__ ops, saln_nw_result *__restrict__ results,
-    uint32_t *__restrict__ cigar, Scoring sc, const uint8_t *__restrict__ qs, uint32_t prio) {
+    uint32_t *__restrict__ cigar, Scoring sc, const uint8_t *__restrict__ qs,
+    uint32_t *__restrict__ walk_left) {
     constexpr uint32_t kWave = WalkGeo<K, kNib, G * K>::kWaveLds;
     __shared__ __attribute__((aligned(16))) uint8_t win_all[tb_lds_threads<G, K, kNib>() / 64u * kWave];
-    const uint32_t idx = first + blockIdx.x * blockDim.x + threadIdx.x;
-    if (idx >= first + n) return;
-    // The walk is a latency-bound chain that shares SIMDs with the VALU-bound
-    // fill of the next batch in pipelined plans; its issue priority (option
-    // nw.walk_prio) decides who waits when both are ready.
-    switch (prio) {  // (s_setprio takes an immediate; prio is uniform)
-        case 0: __builtin_amdgcn_s_setprio(0); break;
-        case 1: __builtin_amdgcn_s_setprio(1); break;
-        case 2: __builtin_amdgcn_s_setprio(2); break;
-        default: __builtin_amdgcn_s_setprio(3); break;
+    const uint32_t rel = blockIdx.x * blockDim.x + threadIdx.x;
+    if (rel >= n) return;
+    if (walk_left) {  // (lane 0 of a wave holds the pack's first pair: rel < n)
+        const uint32_t pack = rel / 64u;
+        if (!__builtin_amdgcn_readfirstlane(walk_left[pack])) return;
+        if ((threadIdx.x & 63u) == 0) walk_left[pack] = 0;
     }
+    const uint32_t idx = first + rel;
+    // The walk is a latency-bound chain that shares SIMDs with the VALU-bound
+    // fill of the next batch in pipelined plans: it issues at the highest
+    // priority (round 4: 3 / 1 / 0 gave 0.94 / 0.94 / 0.96 ms per step).
+    __builtin_amdgcn_s_setprio(3);
     const NwPairDesc p = pairs[idx];
     lds_u8 *win = (lds_u8 *)(win_all + (threadIdx.x / 64u) * kWave);
     walk_pack_lds<G, K, kNib>(p, end_h[idx], mask, ops, results, cigar, sc, win, qs);
@@ -1498,18 +1532,14 @@ constexpr int pk_min_waves() { return kCodes == 3 /* kCodesNib */ && G == 8 ? 3 
 // selected by (q code ^ d code) in each half's low byte; the row word holds
 // the db codes with 0x0C (v_perm's zero byte) in each half's high byte.
 // Codes are (char >> 1) & 3 for A, C, T, G; a wave with any other byte in its
-// pairs stores the launch's epoch in g_tab_slots[epoch % 1024] and returns
-// before its first step; the fallback launch behind it (kTabMode 2: the
-// generic 4-bit-code body) runs only when that slot holds its epoch, and then
-// only in the waves that found such a byte.  Every value stays within the packed bound: X~ = X' + 2|ge|(r + c)
-// lies in [-(4|go| + ...), rows (2|m| + 2|ge|) + 2|ge| lq] (X' is at least
-// its all-gap path, at most its all-match one).
-__device__ uint32_t g_tab_slots[1024];
+// pairs returns before its first step (fill_pk_body returns 1) and its
+// kernel marks the launch in its plan's bail word; the fallback launch behind
+// it (kTabMode 2: the generic 4-bit-code body) runs only when the word holds
+// its launch, and then only in the waves that found such a byte.  Every value
+// stays within the packed bound: X~ = X' + 2|ge|(r + c) lies in
+// [-(4|go| + ...), rows (2|m| + 2|ge|) + 2|ge| lq] (X' is at least its
+// all-gap path, at most its all-match one).
 constexpr int32_t kFreeBias = 4096;
-#ifndef SALN_FREE_MAX3
-#define SALN_FREE_MAX3 1  // experiment builds: 0 (two packed u16 maxima)
-#endif
-constexpr bool kFreeMax3 = SALN_FREE_MAX3;
 typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
 // max of three words of two biased halves read as positive normal f16 (one
 // v_pk_maximum3_f16); exact only inside the extension-free frame's window
@@ -1521,12 +1551,16 @@ __device__ __forceinline__ uint32_t hmax3(uint32_t a, uint32_t b, uint32_t c) {
                                                     __builtin_bit_cast(f16x2, c))));
 }
 
+// Returns (per lane; wave-uniform over the lanes that hold pairs): 0 filled
+// (or no pair), 1 the table body left the wave's pairs to the fallback launch
+// (a byte other than A, C, G, T), 2 the fallback body found nothing to do.
+// kThreads: the workgroup's threads (256; 64 for the fused fill + walk).
 template <int G, int K, int kCodes, typename Src, int KS, bool kRebase = false, bool kProf = false,
-          int kTabMode = 0>
-__device__ __forceinline__ void fill_pk_body(Src src, uint32_t count, const uint8_t *__restrict__ qs,
-                                             const uint8_t *__restrict__ ds,
-                                             uint8_t *__restrict__ mask, Scoring sc,
-                                             uint32_t ld_max, bool sc_steady, uint32_t epoch = 0) {
+          int kTabMode = 0, int kThreads = 256>
+__device__ __forceinline__ int fill_pk_body(Src src, uint32_t count, const uint8_t *__restrict__ qs,
+                                            const uint8_t *__restrict__ ds,
+                                            uint8_t *__restrict__ mask, Scoring sc,
+                                            uint32_t ld_max, bool sc_steady) {
     constexpr bool kTab = kTabMode == 1;  // table body; kTabMode 2: the generic body of its bail-outs
     // the extension-free frame (alpha = beta = -2*gap_extend, M~ = H~ + bonus):
     // the table body, and kTabMode 3 = query profiles holding bonuses
@@ -1543,13 +1577,13 @@ __device__ __forceinline__ void fill_pk_body(Src src, uint32_t count, const uint
     static_assert(!kProf || (kCodes == kCodesNone && !kRebase), "profiles: score-only, one frame");
     static_assert(!kTab || ((kCodes == kCodesNib || kCodes == kCodesNone) && !kRebase && !kProf),
                   "tables: 4-bit codes or score-only, one frame");
-    constexpr int GPB = 256 / G;
+    constexpr int GPB = kThreads / G;
     constexpr Geom geo{G, K};
     extern __shared__ uint32_t drow[];  // [GPB][G + ld_max + G] packed db chars (dch) per row
     const int lane = threadIdx.x % G;
     const uint32_t gi = pack_block(blocks_per_pack(2 * GPB)) * GPB + threadIdx.x / G;
     const uint32_t ia = 2 * gi, ib = 2 * gi + 1;
-    if (ia >= count) return;  // whole group
+    if (ia >= count) return 0;  // whole group
     const bool hasB = ib < count;
     const NwPairDesc pa = src.pair(ia);
     NwPairDesc pb = pa;
@@ -1641,12 +1675,9 @@ __device__ __forceinline__ void fill_pk_body(Src src, uint32_t count, const uint
     asm volatile("s_waitcnt lgkmcnt(0)" : : : "memory");
     __builtin_amdgcn_wave_barrier();
     if constexpr (kTabMode == 1) {
-        if (__builtin_amdgcn_ballot_w64(bad)) {  // the wave is left to the fallback launch
-            g_tab_slots[epoch & 1023u] = epoch;
-            return;
-        }
+        if (__builtin_amdgcn_ballot_w64(bad)) return 1;  // the wave is left to the fallback launch
     } else if constexpr (kTabMode == 2) {
-        if (!__builtin_amdgcn_ballot_w64(bad)) return;  // done by the table launch
+        if (!__builtin_amdgcn_ballot_w64(bad)) return 2;  // done by the table launch
     }
     // end-cell owners
     const int lA = (lqA - 1) / K, kA = (lqA - 1) % K;
@@ -1757,7 +1788,7 @@ __device__ __forceinline__ void fill_pk_body(Src src, uint32_t count, const uint
                                              : umin2(qc[k] ^ dch, kPen);
                 const uint32_t M = kFree ? hdk + pen : hdk - pen;
                 const uint32_t I = F, D = Dn[k];
-                const uint32_t H = kFree && kFreeMax3 ? hmax3(M, I, D) : umax2(M, umax2(I, D));
+                const uint32_t H = kFree ? hmax3(M, I, D) : umax2(M, umax2(I, D));
                 const uint32_t tO = M + kOpen;
                 if constexpr (kCodes == kCodesNib) {
                     // the four walk decisions as signs (set = parent absent):
@@ -1947,6 +1978,7 @@ __device__ __forceinline__ void fill_pk_body(Src src, uint32_t count, const uint
         step(t + 1, HpB, Hp, G0, 0u);
     }
     if (t < T) step(t, Hp, HpB, G0, 0u);
+    return 0;
 }
 
 template <int G, int K, int kCodes, typename Src, int KS, bool kRebase = false>
@@ -1958,25 +1990,135 @@ __global__ __launch_bounds__(256, (pk_min_waves<G, K, kCodes>())) void nw_fill_p
 
 // 4-bit walk codes with table penalties (kTabMode 1, nw.pk_tab), and the
 // launch behind it for the waves whose pairs hold a byte other than A, C, G, T
-// (kTabMode 2; its waves return at once unless the table launch of `epoch`
-// left work).  Two kernels, not one with both bodies: together they spill.
+// (kTabMode 2).  A bailing wave stores the launch's epoch in its plan's bail
+// word (one per mask workspace; the plan numbers its launches, and the
+// launches of one workspace run in stream order); the fallback launch runs
+// only when that word holds its epoch.  Two kernels, not one with both
+// bodies: together they spill.
 template <int G, int K, typename Src>
 __global__ __launch_bounds__(256, (pk_min_waves<G, K, kCodesNib>())) void nw_fill_pk_tab_kernel(
     Src src, uint32_t count, const uint8_t *__restrict__ qs, const uint8_t *__restrict__ ds,
-    uint8_t *__restrict__ mask, Scoring sc, uint32_t ld_max, bool sc_steady, uint32_t epoch) {
-    fill_pk_body<G, K, kCodesNib, Src, K, false, false, 1>(src, count, qs, ds, mask, sc, ld_max,
-                                                            sc_steady, epoch);
+    uint8_t *__restrict__ mask, Scoring sc, uint32_t ld_max, uint32_t *__restrict__ bail,
+    uint32_t epoch) {
+    const int st = fill_pk_body<G, K, kCodesNib, Src, K, false, false, 1>(src, count, qs, ds, mask,
+                                                                           sc, ld_max, true);
+    if (__builtin_amdgcn_ballot_w64(st == 1) && (threadIdx.x & 63u) == 0) *bail = epoch;
 }
 // (kRebaseGeneric: the fallback of a launch whose dbs need the rebasing frame;
 // the extension-free table body has no drift and needs none)
 template <int G, int K, typename Src, bool kRebaseGeneric>
 __global__ __launch_bounds__(256, (pk_min_waves<G, K, kCodesNib>())) void nw_fill_pk_tabfb_kernel(
     Src src, uint32_t count, const uint8_t *__restrict__ qs, const uint8_t *__restrict__ ds,
-    uint8_t *__restrict__ mask, Scoring sc, uint32_t ld_max, bool sc_steady, uint32_t epoch) {
-    if (__builtin_amdgcn_readfirstlane(g_tab_slots[epoch & 1023u]) != epoch) return;
+    uint8_t *__restrict__ mask, Scoring sc, uint32_t ld_max, const uint32_t *__restrict__ bail,
+    uint32_t epoch) {
+    if (__builtin_amdgcn_readfirstlane(*bail) != epoch) return;
     fill_pk_body<G, K, kCodesNib, Src, K, kRebaseGeneric, false, 2>(src, count, qs, ds, mask, sc,
-                                                                     ld_max, sc_steady, epoch);
+                                                                     ld_max, true);
 }
+
+// ------------------------------------------------- fused fill + walk (C2)
+// The 8 x 19 table fill of configs[1]-shaped plans with the walk of each mask
+// pack (64 pairs) run by the pack's last finishing wave, inside the fill
+// launch (round 5).  One-wave workgroups of 16 pairs; the four of a pack sit
+// on one XCD (pack_block).  A wave that finished its fill waits for its mask
+// and end-value stores (vmcnt(0): in the XCD's L2) and adds 1 << (8 * its
+// XCC_ID) to the pack's 64-bit arrival word; the wave whose add completes the
+// count walks the pack's 64 pairs (one lane each, walk_pack_lds) if every
+// wave of the pack finished on its own XCD - the stores are then in the L2
+// its loads read (the end values with sc1 loads, which bypass this CU's L1:
+// a neighbouring pack's walk on this CU may have cached their line; the mask
+// lines of a pack are its own, 256-byte aligned) - and otherwise leaves the
+// pack to the walker launch behind (walk_left; the launch boundary makes
+// every store visible).  The last arrival also clears the word for the next
+// execute.  Packs completed by the fallback launch (a byte other than A, C,
+// G, T) are left to the walker launch as well.  No separate walker pass over
+// the mask, and no co-resident walker
+// kernel taking the fill's registers and issue slots (round 4: the fill ran
+// 0.88-0.92 ms beside it against 0.686 alone).
+struct FuseArgs {
+    const NwPairDesc *pairs;         // plan table (pairs[first + i])
+    uint32_t *bail;                  // the workspace's bail word (kMode 1 writes, 2 reads)
+    uint32_t epoch;
+    unsigned long long *arrive;      // per pack: arrivals by XCD (bytes)
+    uint32_t *walk_left;             // per pack: 1 = the walker launch walks it
+    uint32_t *ops;
+    saln_nw_result *results;
+    uint32_t *cigar;
+    uint32_t defer;                  // 1 (nw.fuse_walk = 2, tests): every pack left to the walker launch
+};
+constexpr uint32_t kFuseThreads = 64;  // one wave per workgroup
+
+constexpr int kFuseG = 8, kFuseK = 19;  // the 8 x 19 variant (4)
+template <int kMode, bool kRebaseGeneric>
+__global__ __launch_bounds__(kFuseThreads, 3) void nw_fill_walk_kernel(
+    PlanSrc src, uint32_t count, const uint8_t *__restrict__ qs, const uint8_t *__restrict__ ds,
+    uint8_t *__restrict__ mask, Scoring sc, uint32_t ld_max, FuseArgs fa) {
+    static_assert(kMode == 1 || kMode == 2, "table launch or its fallback");
+    constexpr int G = kFuseG, K = kFuseK;
+    constexpr uint32_t kPairsPerWave = 2 * kFuseThreads / G;  // 16
+    constexpr uint32_t kWavesPerPack = 64 / kPairsPerWave;    // 4
+    if constexpr (kMode == 2)
+        if (__builtin_amdgcn_readfirstlane(*fa.bail) != fa.epoch) return;
+    const int st = fill_pk_body<G, K, kCodesNib, PlanSrc, K, kMode == 2 && kRebaseGeneric, false,
+                                kMode, (int)kFuseThreads>(src, count, qs, ds, mask, sc, ld_max, true);
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t lb = pack_block(kWavesPerPack);  // the wave's 16 pairs: lb * 16 ..
+    if (lb * kPairsPerWave >= count) return;
+    if (__builtin_amdgcn_ballot_w64(st == 1)) {  // (kMode 1) left to the fallback launch
+        if (lane == 0) *fa.bail = fa.epoch;
+        return;
+    }
+    if (__builtin_amdgcn_ballot_w64(st == 2)) return;  // (kMode 2) filled by the table launch
+    asm volatile("s_waitcnt vmcnt(0)" : : : "memory");  // my mask and end stores are in L2
+    const uint32_t pack = lb / kWavesPerPack;
+    const uint32_t np = min(64u, count - 64u * pack);
+    const uint32_t nwv = (np + kPairsPerWave - 1) / kPairsPerWave;
+    const uint32_t xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20) & 7u;  // HW_REG_XCC_ID
+    const unsigned long long mine = 1ull << (8u * xcc);
+    unsigned long long old = 0;
+    if (lane == 0) old = atomicAdd(&fa.arrive[pack], mine);
+    const uint32_t olo = __builtin_amdgcn_readlane((uint32_t)old, 0);
+    const uint32_t ohi = __builtin_amdgcn_readlane((uint32_t)(old >> 32), 0);
+    const unsigned long long tot = ((unsigned long long)ohi << 32 | olo) + mine;
+    const uint32_t sum = ((uint32_t)tot & 0xFFu) + ((uint32_t)tot >> 8 & 0xFFu) +
+                         ((uint32_t)tot >> 16 & 0xFFu) + ((uint32_t)tot >> 24) +
+                         ((uint32_t)(tot >> 32) & 0xFFu) + ((uint32_t)(tot >> 40) & 0xFFu) +
+                         ((uint32_t)(tot >> 48) & 0xFFu) + (uint32_t)(tot >> 56);
+    if (sum != nwv) return;  // not the pack's last wave
+    if (lane == 0)  // (every wave of the pack has added)
+        __hip_atomic_store(&fa.arrive[pack], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // the fallback launch's packs hold a byte other than A, C, G, T, which the
+    // walk's 2-bit query codes cannot tell from G: the walker launch takes them
+    if (kMode == 2 || fa.defer || tot != (unsigned long long)nwv << (8u * xcc)) {
+        if (lane == 0) fa.walk_left[pack] = 1u;
+        return;
+    }
+    __builtin_amdgcn_s_setprio(3);  // a latency-bound chain beside the fills of the other waves
+    asm volatile("s_waitcnt lgkmcnt(0)" : : : "memory");  // the fill's LDS reads are done
+    const uint32_t i = 64u * pack + lane;
+    if (i >= count) return;
+    const NwPairDesc p = fa.pairs[src.first + i];
+    const int32_t hend = __hip_atomic_load(src.end_h + src.first + i, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+    extern __shared__ uint32_t drow[];
+    walk_pack_lds<kFuseG, kFuseK, true, true>(p, hend, mask, fa.ops, fa.results, fa.cigar, sc,
+                                              (lds_u8 *)drow, qs);
+}
+
+// (explicit instantiations: the launches sit in a generic lambda of fill_pk,
+// and hipcc emitted no host stubs for them there)
+template __global__ void nw_fill_walk_kernel<1, false>(PlanSrc, uint32_t, const uint8_t *,
+                                                       const uint8_t *, uint8_t *, Scoring,
+                                                       uint32_t, FuseArgs);
+template __global__ void nw_fill_walk_kernel<1, true>(PlanSrc, uint32_t, const uint8_t *,
+                                                      const uint8_t *, uint8_t *, Scoring, uint32_t,
+                                                      FuseArgs);
+template __global__ void nw_fill_walk_kernel<2, false>(PlanSrc, uint32_t, const uint8_t *,
+                                                       const uint8_t *, uint8_t *, Scoring,
+                                                       uint32_t, FuseArgs);
+template __global__ void nw_fill_walk_kernel<2, true>(PlanSrc, uint32_t, const uint8_t *,
+                                                      const uint8_t *, uint8_t *, Scoring, uint32_t,
+                                                      FuseArgs);
 
 // Score-only all-vs-all of the other query classes with table penalties in
 // the extension-free frame (nw.pk_tab); *generic (nw_acgt_check_kernel earlier
@@ -2086,10 +2228,7 @@ __device__ __forceinline__ uint32_t stripe_code_word(const uint32_t (&s)[8][4]) 
 // to kColEmpty); stripe g+1 polls kRowsBlk-row blocks (nw_fill_stripe_kernel).
 constexpr int32_t kNegInf = INT32_MIN;
 constexpr uint32_t kRowsOff = 0;  // boundary row r at element r of the column
-#ifndef SALN_ROWS_GRP
-#define SALN_ROWS_GRP 8  // experiment builds: 4
-#endif
-constexpr uint32_t kRowsGrp = SALN_ROWS_GRP;  // rows per boundary group (round 2: 4 was slower)
+constexpr uint32_t kRowsGrp = 8;  // rows per boundary group (4: slower, rounds 2 and 4)
 
 // inclusive prefix max over the wave's 64 lanes (lane order).  `fill`:
 // independent work placed inside the chain, where each dependent DPP step
@@ -2106,34 +2245,51 @@ __device__ __forceinline__ int32_t wave_prefix_max(int32_t v, Fill &&fill) {
     return v;
 }
 
-// Workgroups of 1-4 waves (option nw.rows_wpg, default 1: four-wave groups
-// ran C4 in 21.2 ms against 14.2), one stripe per wave (wave v of the launch =
-// blockIdx.x * waves-per-group + the wave's index in the group; n_waves of
-// them).
-// kLone: every wave reserves the whole register file of its SIMD (an AGPR
-// clobber puts the allocation past 256 VGPR+AGPR per lane: one wave per SIMD,
-// MI355X_MICROARCH.md's occupancy table), so no two stripes share a SIMD.
-// The dispatcher otherwise stacks them: 196 one-wave groups on a 64-CU mask
-// landed on 128 SIMDs (tools/cu_occupancy.py), and a stripe that shares its
-// SIMD slows the whole row chain (a span of the 4-span chain alone: 19.8 ms
-// against 12.1 for the 8-span one's).  Used when the launch's stripes fit the
-// SIMDs; waves past them wait for a SIMD, and since workgroups dispatch in
-// order the resident stripes are always the leftmost unfinished ones.
-template <int K, int kCodes, bool kMinPen, bool kLone>
-__global__ __launch_bounds__(256) void nw_fill_rows_kernel(
+// One-wave workgroups, one stripe each (n_waves of them; round 4: four-wave
+// groups ran C4 in 21.2 ms against 14.2).  Placement (kPlace):
+// 0  wave v = workgroup v; the dispatcher may stack stripes on a SIMD.
+// 1  (kPlaceLone) every wave reserves the whole register file of its SIMD (an
+//    AGPR clobber puts the allocation past 256 VGPR+AGPR per lane: one wave
+//    per SIMD, MI355X_MICROARCH.md's occupancy table), so no two stripes
+//    share a SIMD.  The dispatcher otherwise stacks them: 196 one-wave groups
+//    on a 64-CU mask landed on 128 SIMDs (tools/cu_occupancy.py), and a stripe
+//    that shares its SIMD slows the whole row chain (a span of the 4-span
+//    chain alone: 19.8 ms against 12.1 for the 8-span one's).  Used when the
+//    launch's stripes fit the SIMDs; waves past them wait for a SIMD, and
+//    since workgroups dispatch in order the resident stripes are always the
+//    leftmost unfinished ones.
+// 2  (kPlaceXcd) lone, and XCD-local neighbours: workgroups are dispatched
+//    round-robin over the 8 XCDs (workgroup b -> XCD b % 8), so wave v =
+//    (b % 8) * xcd_run + b / 8 puts runs of xcd_run consecutive stripes on
+//    one XCD and only 7 hand-offs cross XCDs.  Valid only when every stripe of
+//    the launch is resident at once (a stripe's left neighbour may have a
+//    later workgroup id): the host takes it for launches on the context's
+//    unmasked streams whose stripes fit the device's SIMDs.  A stripe whose
+//    consumer is in its own run publishes with plain stores, which keep the
+//    line in the XCD's L2 where the consumer's sc1 load finds it (the hand-off
+//    rules in DESIGN.md §3); the last stripe of a run publishes sc1
+//    (write-through, visible to the next XCD).
+constexpr int kPlaceShared = 0, kPlaceLone = 1, kPlaceXcd = 2;
+template <int K, int kCodes, bool kMinPen, int kPlace>
+__global__ __launch_bounds__(64) void nw_fill_rows_kernel(
     const NwPairDesc *__restrict__ pairs, const uint2 *__restrict__ work,
     const uint8_t *__restrict__ qs, const uint8_t *__restrict__ ds, uint8_t *__restrict__ mask,
     int2 *__restrict__ scratch, uint32_t *__restrict__ err, int32_t *__restrict__ end_h,
-    Scoring sc, uint32_t n_waves) {
+    Scoring sc, uint32_t n_waves, uint32_t xcd_run) {
     static_assert(K == 1 || K == 2 || K == 4, "4 cells per code word");
     constexpr int S = 4 / K;   // stripes per 256-column chunk (work item)
     constexpr int W = 64 * K;  // stripe width (4 / K rows per code word)
-    if constexpr (kLone) asm volatile("" : : : "a255");
+    if constexpr (kPlace != kPlaceShared) asm volatile("" : : : "a255");
     const int lane = (int)(threadIdx.x & 63u);
     // (readfirstlane: the slot is wave-uniform, so everything derived from it
     // stays in SGPRs: the publication base is an asm "s" operand)
-    const uint32_t v = __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
+    const uint32_t v = __builtin_amdgcn_readfirstlane(
+        kPlace == kPlaceXcd ? (blockIdx.x & 7u) * xcd_run + (blockIdx.x >> 3) : blockIdx.x);
     if (v >= n_waves) return;  // (whole wave: no group barrier in this kernel)
+    // plain publication: my consumer (stripe v + 1, when it is one) runs on my XCD
+    // (the launch's last stripe publishes sc1: a span's outbox is read by a
+    // relay kernel, a copy or RCCL, none of them in this XCD's L2)
+    const bool plain_pub = kPlace == kPlaceXcd && (v + 1) % xcd_run != 0 && v + 1 < n_waves;
     const uint2 wk = work[v / S];
     const NwPairDesc p = pairs[wk.x];
     const uint32_t g = wk.y * S + v % S;  // stripe index
@@ -2193,7 +2349,7 @@ __global__ __launch_bounds__(256) void nw_fill_rows_kernel(
     // sets for the end states); every other row stores walk codes without
     // argM, tied against H'' & ~1 with no per-row test
     auto row = [&](uint32_t r, uint32_t dch, int32_t bH, int32_t bI, auto u_c, auto q_c,
-                   auto m_c, auto &&fill, auto vb_c) __attribute__((always_inline)) {
+                   auto m_c, auto &&fill, auto vb_c, auto plain_c) __attribute__((always_inline)) {
         constexpr int u = decltype(u_c)::value;
         constexpr int q = decltype(q_c)::value;  // row in its boundary group
         constexpr bool kM = decltype(m_c)::value;
@@ -2265,8 +2421,12 @@ __global__ __launch_bounds__(256) void nw_fill_rows_kernel(
             const uint32_t vo = pub_voff;  // (asm operands take locals, not captures)
             const int2 *pb = pub_base;
             // (a 64-bit store has no data hazard with the VALU around it)
-            asm volatile("global_store_dwordx2 %0, %1, %2 offset:%3 sc1"
-                         : : "v"(vo), "v"(val), "s"(pb), "i"(8 * q) : "memory");
+            if constexpr (decltype(plain_c)::value)
+                asm volatile("global_store_dwordx2 %0, %1, %2 offset:%3"
+                             : : "v"(vo), "v"(val), "s"(pb), "i"(8 * q) : "memory");
+            else
+                asm volatile("global_store_dwordx2 %0, %1, %2 offset:%3 sc1"
+                             : : "v"(vo), "v"(val), "s"(pb), "i"(8 * q) : "memory");
         }
     };
     // store the code word of rows r0 .. r0+(4/K)-1 (n of them valid)
@@ -2303,7 +2463,7 @@ __global__ __launch_bounds__(256) void nw_fill_rows_kernel(
     // be exact - a load still in flight after its wait would land in
     // registers the compiler has reused.  Rows not yet published are
     // re-polled with ordinary (compiler-waited) loads.
-    auto rows = [&](auto F) __attribute__((always_inline)) {
+    auto rows = [&](auto F, auto PL) __attribute__((always_inline)) {
         constexpr bool kFirst = decltype(F)::value;
         const std::integral_constant<bool, !kFirst> VB;  // boundary rows kept in cH_v
         constexpr uint32_t kG = kRowsGrp;  // rows per boundary group
@@ -2392,23 +2552,23 @@ __global__ __launch_bounds__(256) void nw_fill_rows_kernel(
             dnidx = min(dnidx + 1, last_dw);
             dnxt = dw[dnidx];
             if constexpr (K == 4) {
-                row(r, (w & 0xFFu) << 8, bh[o], bi[o], u0, q0, m_c, nofill, VB); put(r, 1, m_c);
-                row(r + 1, ((w >> 8) & 0xFFu) << 8, bh[o + 1], bi[o + 1], u0, q1, m_c, nofill, VB); put(r + 1, 1, m_c);
-                row(r + 2, ((w >> 16) & 0xFFu) << 8, bh[o + 2], bi[o + 2], u0, q2, m_c, nofill, VB); put(r + 2, 1, m_c);
-                row(r + 3, (w >> 24) << 8, bh[o + 3], bi[o + 3], u0, q3, m_c, nofill, VB); put(r + 3, 1, m_c);
+                row(r, (w & 0xFFu) << 8, bh[o], bi[o], u0, q0, m_c, nofill, VB, PL); put(r, 1, m_c);
+                row(r + 1, ((w >> 8) & 0xFFu) << 8, bh[o + 1], bi[o + 1], u0, q1, m_c, nofill, VB, PL); put(r + 1, 1, m_c);
+                row(r + 2, ((w >> 16) & 0xFFu) << 8, bh[o + 2], bi[o + 2], u0, q2, m_c, nofill, VB, PL); put(r + 2, 1, m_c);
+                row(r + 3, (w >> 24) << 8, bh[o + 3], bi[o + 3], u0, q3, m_c, nofill, VB, PL); put(r + 3, 1, m_c);
             } else if constexpr (K == 2) {
                 // rows r, r+1's code word is built inside row r+2's prefix chain
-                row(r, (w & 0xFFu) << 8, bh[o], bi[o], u0, q0, m_c, fill0, VB);
-                row(r + 1, ((w >> 8) & 0xFFu) << 8, bh[o + 1], bi[o + 1], u1, q1, m_c, nofill, VB);
+                row(r, (w & 0xFFu) << 8, bh[o], bi[o], u0, q0, m_c, fill0, VB, PL);
+                row(r + 1, ((w >> 8) & 0xFFu) << 8, bh[o + 1], bi[o + 1], u1, q1, m_c, nofill, VB, PL);
                 row(r + 2, ((w >> 16) & 0xFFu) << 8, bh[o + 2], bi[o + 2], u0, q2, m_c,
-                    [&]() __attribute__((always_inline)) { put(r, 2, m_c); }, VB);
-                row(r + 3, (w >> 24) << 8, bh[o + 3], bi[o + 3], u1, q3, m_c, nofill, VB);
+                    [&]() __attribute__((always_inline)) { put(r, 2, m_c); }, VB, PL);
+                row(r + 3, (w >> 24) << 8, bh[o + 3], bi[o + 3], u1, q3, m_c, nofill, VB, PL);
                 if constexpr (kFlush) put(r + 2, 2, m_c);
             } else {
-                row(r, (w & 0xFFu) << 8, bh[o], bi[o], u0, q0, m_c, fill0, VB);
-                row(r + 1, ((w >> 8) & 0xFFu) << 8, bh[o + 1], bi[o + 1], u1, q1, m_c, nofill, VB);
-                row(r + 2, ((w >> 16) & 0xFFu) << 8, bh[o + 2], bi[o + 2], u2, q2, m_c, nofill, VB);
-                row(r + 3, (w >> 24) << 8, bh[o + 3], bi[o + 3], u3, q3, m_c, nofill, VB);
+                row(r, (w & 0xFFu) << 8, bh[o], bi[o], u0, q0, m_c, fill0, VB, PL);
+                row(r + 1, ((w >> 8) & 0xFFu) << 8, bh[o + 1], bi[o + 1], u1, q1, m_c, nofill, VB, PL);
+                row(r + 2, ((w >> 16) & 0xFFu) << 8, bh[o + 2], bi[o + 2], u2, q2, m_c, nofill, VB, PL);
+                row(r + 3, (w >> 24) << 8, bh[o + 3], bi[o + 3], u3, q3, m_c, nofill, VB, PL);
                 if constexpr (kFlush) put(r, 4, m_c);
             }
         };
@@ -2421,18 +2581,18 @@ __global__ __launch_bounds__(256) void nw_fill_rows_kernel(
             const uint32_t w = doff ? (dcur >> doff) | (dnxt << (32u - doff)) : dcur;
             const uint32_t n = ld - r + 1;
             if constexpr (K == 4) {
-                row(r, (w & 0xFFu) << 8, bh[o], bi[o], u0, q0, m_c, nofill, VB); put(r, 1, m_c);
-                if (n > 1) { row(r + 1, ((w >> 8) & 0xFFu) << 8, bh[o + 1], bi[o + 1], u0, q1, m_c, nofill, VB); put(r + 1, 1, m_c); }
-                if (n > 2) { row(r + 2, ((w >> 16) & 0xFFu) << 8, bh[o + 2], bi[o + 2], u0, q2, m_c, nofill, VB); put(r + 2, 1, m_c); }
+                row(r, (w & 0xFFu) << 8, bh[o], bi[o], u0, q0, m_c, nofill, VB, PL); put(r, 1, m_c);
+                if (n > 1) { row(r + 1, ((w >> 8) & 0xFFu) << 8, bh[o + 1], bi[o + 1], u0, q1, m_c, nofill, VB, PL); put(r + 1, 1, m_c); }
+                if (n > 2) { row(r + 2, ((w >> 16) & 0xFFu) << 8, bh[o + 2], bi[o + 2], u0, q2, m_c, nofill, VB, PL); put(r + 2, 1, m_c); }
             } else if constexpr (K == 2) {
-                row(r, (w & 0xFFu) << 8, bh[o], bi[o], u0, q0, m_c, nofill, VB);
-                if (n > 1) row(r + 1, ((w >> 8) & 0xFFu) << 8, bh[o + 1], bi[o + 1], u1, q1, m_c, nofill, VB);
+                row(r, (w & 0xFFu) << 8, bh[o], bi[o], u0, q0, m_c, nofill, VB, PL);
+                if (n > 1) row(r + 1, ((w >> 8) & 0xFFu) << 8, bh[o + 1], bi[o + 1], u1, q1, m_c, nofill, VB, PL);
                 put(r, min(n, 2u), m_c);
-                if (n > 2) { row(r + 2, ((w >> 16) & 0xFFu) << 8, bh[o + 2], bi[o + 2], u0, q2, m_c, nofill, VB); put(r + 2, 1, m_c); }
+                if (n > 2) { row(r + 2, ((w >> 16) & 0xFFu) << 8, bh[o + 2], bi[o + 2], u0, q2, m_c, nofill, VB, PL); put(r + 2, 1, m_c); }
             } else {
-                row(r, (w & 0xFFu) << 8, bh[o], bi[o], u0, q0, m_c, nofill, VB);
-                if (n > 1) row(r + 1, ((w >> 8) & 0xFFu) << 8, bh[o + 1], bi[o + 1], u1, q1, m_c, nofill, VB);
-                if (n > 2) row(r + 2, ((w >> 16) & 0xFFu) << 8, bh[o + 2], bi[o + 2], u2, q2, m_c, nofill, VB);
+                row(r, (w & 0xFFu) << 8, bh[o], bi[o], u0, q0, m_c, nofill, VB, PL);
+                if (n > 1) row(r + 1, ((w >> 8) & 0xFFu) << 8, bh[o + 1], bi[o + 1], u1, q1, m_c, nofill, VB, PL);
+                if (n > 2) row(r + 2, ((w >> 16) & 0xFFu) << 8, bh[o + 2], bi[o + 2], u2, q2, m_c, nofill, VB, PL);
                 put(r, n, m_c);
             }
         };
@@ -2476,8 +2636,18 @@ __global__ __launch_bounds__(256) void nw_fill_rows_kernel(
             quad(r, o0, M1, nofill, std::true_type{});
         }
     };
-    if (g == 0) rows(std::true_type{});
-    else rows(std::false_type{});
+    if constexpr (kPlace == kPlaceXcd) {
+        if (plain_pub) {
+            if (g == 0) rows(std::true_type{}, std::true_type{});
+            else rows(std::false_type{}, std::true_type{});
+        } else {
+            if (g == 0) rows(std::true_type{}, std::false_type{});
+            else rows(std::false_type{}, std::false_type{});
+        }
+    } else {
+        if (g == 0) rows(std::true_type{}, std::false_type{});
+        else rows(std::false_type{}, std::false_type{});
+    }
     if (end_lane) {
         int32_t e = 0;
 #pragma unroll
@@ -2987,9 +3157,6 @@ constexpr bool kPacked[kNumVariants] = {false, false, false, false, true, true, 
 // halve the occupancy.)
 constexpr uint32_t kFillG[kNumVariants] = {16, 16, 64, 64, 8, 16, 32, 16, 64};
 
-// The packed fill's steady-state steps (nw_fill_pk_kernel kSteady); option
-// nw.pk_steady = 0 turns them off (A/B switch, same results)
-static bool pk_steady() { return opt(Opt::PkSteady) != 0; }
 
 // Dynamic LDS cap of the packed fill's staged db rows: two workgroups per CU.
 constexpr size_t kPackedLdsMax = 80 * 1024;
@@ -3044,57 +3211,79 @@ static bool pk_free_ok(const Scoring &sc, uint32_t W, uint32_t rows) {
 template <int G, int K, int KS = K>
 static hipError_t fill_pk(dim3 grid, hipStream_t s, const NwPairDesc *pairs, uint32_t first,
                           uint32_t count, const uint8_t *qs, const uint8_t *ds, uint8_t *mask,
-                          int32_t *end_h, saln_nw_result *, uint32_t *, Scoring sc, int codes,
-                          uint32_t ld_max, bool rebase) {
-    const size_t pad = (size_t)opt(Opt::FillLdsMin);  // LDS floor per workgroup (occupancy A/B)
-    const size_t lds = std::max((size_t)(256 / G) * (ld_max + 2 * G) * (rebase ? 2 : 4), pad);
+                          int32_t *end_h, saln_nw_result *results, uint32_t *cigar, Scoring sc,
+                          int codes, uint32_t ld_max, bool rebase, FillExtras &fx) {
+    const Options &o = *fx.o;
+    const size_t lds = (size_t)(256 / G) * (ld_max + 2 * G) * (rebase ? 2 : 4);
     if (lds > kPackedLdsMax) return hipErrorInvalidValue;  // choose_variant keeps ld below this
     const PlanSrc src{pairs, first, end_h};
+    auto big_lds = [](std::initializer_list<const void *> fs, size_t n) -> hipError_t {
+        if (n <= 65536) return hipSuccess;
+        for (const void *f : fs) {
+            const hipError_t e =
+                hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kPackedLdsMax);
+            if (e != hipSuccess) return e;
+        }
+        return hipSuccess;
+    };
     auto go = [&](auto codes_c, auto rebase_c) -> hipError_t {
         const auto kern = nw_fill_pk_kernel<G, K, decltype(codes_c)::value, PlanSrc, KS,
                                             decltype(rebase_c)::value>;
         if constexpr (decltype(codes_c)::value == kCodesNib && KS == K) {
             // (the table body stages 32-bit row words; a rebasing fallback 16-bit ones)
             // (and keeps four workgroups per CU where the rebasing fill had them)
-            const size_t lds_tab = std::max((size_t)(256 / G) * (ld_max + 2 * G) * 4, pad);
-            if (opt(Opt::PkTab) && pk_free_ok(sc, G * K, ld_max) &&
+            const size_t lds_tab = (size_t)(256 / G) * (ld_max + 2 * G) * 4;
+            if (o[Opt::PkTab] && fx.bail && pk_free_ok(sc, G * K, ld_max) &&
                 lds_tab <= std::max(lds, kLdsPerCu / 4)) {
                 constexpr bool kRb = decltype(rebase_c)::value;
-                static std::atomic<uint32_t> epochs{0};
-                const uint32_t ep = epochs.fetch_add(1, std::memory_order_relaxed) + 1;
-                if (lds_tab > 65536) {
-                    for (const void *f : {(const void *)nw_fill_pk_tab_kernel<G, K, PlanSrc>,
-                                          (const void *)nw_fill_pk_tabfb_kernel<G, K, PlanSrc, kRb>}) {
-                        const hipError_t e = hipFuncSetAttribute(
-                            f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kPackedLdsMax);
+                if constexpr (G == 8 && K == 19) {
+                    if (fx.arrive && o[Opt::FuseWalk]) {  // fill + walk in one launch
+                        constexpr uint32_t gpb = kFuseThreads / G, sup = 8 * blocks_per_pack(2 * gpb);
+                        const uint32_t groups = (count + 1) / 2;
+                        const dim3 fg(((groups + gpb - 1) / gpb + sup - 1) / sup * sup);
+                        const size_t lf = std::max<size_t>((size_t)gpb * (ld_max + 2 * G) * 4,
+                                                           WalkGeo<K, true, G * K, true>::kWaveLds);
+                        const hipError_t e = big_lds({(const void *)nw_fill_walk_kernel<1, kRb>,
+                                                      (const void *)nw_fill_walk_kernel<2, kRb>}, lf);
                         if (e != hipSuccess) return e;
+                        const FuseArgs fa{pairs, fx.bail, fx.epoch, fx.arrive, fx.walk_left, fx.ops,
+                                          results, cigar, o[Opt::FuseWalk] == 2 ? 1u : 0u};
+                        nw_fill_walk_kernel<1, kRb><<<fg, dim3(kFuseThreads), lf, s>>>(
+                            src, count, qs, ds, mask, sc, ld_max, fa);
+                        nw_fill_walk_kernel<2, kRb><<<fg, dim3(kFuseThreads), lf, s>>>(
+                            src, count, qs, ds, mask, sc, ld_max, fa);
+                        fx.fused = true;
+                        return hipSuccess;
                     }
                 }
+                const hipError_t e = big_lds({(const void *)nw_fill_pk_tab_kernel<G, K, PlanSrc>,
+                                              (const void *)nw_fill_pk_tabfb_kernel<G, K, PlanSrc, kRb>},
+                                             lds_tab);
+                if (e != hipSuccess) return e;
                 nw_fill_pk_tab_kernel<G, K, PlanSrc><<<grid, dim3(256), lds_tab, s>>>(
-                    src, count, qs, ds, mask, sc, ld_max, pk_steady(), ep);
+                    src, count, qs, ds, mask, sc, ld_max, fx.bail, fx.epoch);
                 nw_fill_pk_tabfb_kernel<G, K, PlanSrc, kRb><<<grid, dim3(256), lds_tab, s>>>(
-                    src, count, qs, ds, mask, sc, ld_max, pk_steady(), ep);
+                    src, count, qs, ds, mask, sc, ld_max, fx.bail, fx.epoch);
                 return hipSuccess;
             }
         }
-        if (lds > 65536) {
-            const hipError_t e = hipFuncSetAttribute((const void *)kern,
-                                                     hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                     (int)kPackedLdsMax);
-            if (e != hipSuccess) return e;
-        }
-        kern<<<grid, dim3(256), lds, s>>>(src, count, qs, ds, mask, sc, ld_max, pk_steady());
+        const hipError_t e = big_lds({(const void *)kern}, lds);
+        if (e != hipSuccess) return e;
+        kern<<<grid, dim3(256), lds, s>>>(src, count, qs, ds, mask, sc, ld_max, true);
         return hipSuccess;
     };
     auto by_codes = [&](auto rebase_c) {
         if (codes == kCodesFull) return go(std::integral_constant<int, kCodesFull>{}, rebase_c);
         if (codes == kCodesNone) return go(std::integral_constant<int, kCodesNone>{}, rebase_c);
-        if (codes == kCodesNib) {  // the short-query variants (7: 16 x 10, 4: 8 x 19)
-            if constexpr (G * K <= 160) return go(std::integral_constant<int, kCodesNib>{}, rebase_c);
-            else return hipErrorInvalidValue;
+        // the short-query variants (7: 16 x 10, 4: 8 x 19) store 4-bit walk
+        // codes, the wider ones bytes
+        if constexpr (G * K <= 160) {
+            if (codes == kCodesNib) return go(std::integral_constant<int, kCodesNib>{}, rebase_c);
+            return hipErrorInvalidValue;
+        } else {
+            if (codes == kCodesWalk) return go(std::integral_constant<int, kCodesWalk>{}, rebase_c);
+            return hipErrorInvalidValue;
         }
-        if constexpr (K > 16) return hipErrorInvalidValue;  // byte codes: 16-byte walker slots
-        else return go(std::integral_constant<int, kCodesWalk>{}, rebase_c);
     };
     return rebase ? by_codes(std::true_type{}) : by_codes(std::false_type{});
 }
@@ -3136,7 +3325,8 @@ uint64_t avsa_launch_blocks(int variant, uint64_t count) {
 
 template <int G, int K>
 static hipError_t avsa_pk(const AvsaSrc &src, uint32_t count, const uint8_t *qs, const uint8_t *ds,
-                          Scoring sc, uint32_t ld_max, hipStream_t s, const uint32_t *generic) {
+                          Scoring sc, uint32_t ld_max, hipStream_t s, const uint32_t *generic,
+                          const Options &o) {
     constexpr uint32_t gpb = 256 / G;
     const uint64_t blocks = avsa_blocks(G, count);
     if (blocks * 256 > 0xFFFFFFFFull) return hipErrorInvalidConfiguration;  // 32-bit grid
@@ -3146,7 +3336,7 @@ static hipError_t avsa_pk(const AvsaSrc &src, uint32_t count, const uint8_t *qs,
     if (lds > kPackedLdsMax) return hipErrorInvalidValue;
     // the table body stages 32-bit row words, the rebasing xor body 16-bit ones
     const size_t lds_tab = (size_t)gpb * (ld_max + 2 * G) * 4;
-    const bool tab = generic && opt(Opt::PkTab) && pk_free_ok(sc, G * K, ld_max) &&
+    const bool tab = generic && o[Opt::PkTab] && pk_free_ok(sc, G * K, ld_max) &&
                      lds_tab <= std::max(lds, kLdsPerCu / 4);
     auto go = [&](auto rebase_c) -> hipError_t {
         if (tab) {
@@ -3157,7 +3347,7 @@ static hipError_t avsa_pk(const AvsaSrc &src, uint32_t count, const uint8_t *qs,
                     (int)kPackedLdsMax);
                 if (e != hipSuccess) return e;
             }
-            kern<<<grid, dim3(256), lds_tab, s>>>(src, count, qs, ds, sc, ld_max, pk_steady(), generic);
+            kern<<<grid, dim3(256), lds_tab, s>>>(src, count, qs, ds, sc, ld_max, true, generic);
             return hipSuccess;
         }
         const auto kern = nw_fill_pk_kernel<G, K, kCodesNone, AvsaSrc, K, decltype(rebase_c)::value>;
@@ -3167,7 +3357,7 @@ static hipError_t avsa_pk(const AvsaSrc &src, uint32_t count, const uint8_t *qs,
                                                      (int)kPackedLdsMax);
             if (e != hipSuccess) return e;
         }
-        kern<<<grid, dim3(256), lds, s>>>(src, count, qs, ds, nullptr, sc, ld_max, pk_steady());
+        kern<<<grid, dim3(256), lds, s>>>(src, count, qs, ds, nullptr, sc, ld_max, true);
         return hipSuccess;
     };
     return rebase ? go(std::true_type{}) : go(std::false_type{});
@@ -3181,7 +3371,7 @@ hipError_t launch_avsa_prof(const uint64_t *q_off, const uint64_t *d_off, const 
                             uint32_t nq, const uint32_t *d_ids, uint32_t nq_total, uint64_t base,
                             uint32_t count, const uint8_t *qs, const uint8_t *ds, int2 *out,
                             Scoring sc, uint32_t ld_max, const uint32_t *generic,
-                            hipStream_t stream) {
+                            hipStream_t stream, const Options &o) {
     constexpr int G = 8, K = 19;
     if (!count) return hipSuccess;
     if ((count | base) & 1u || !packed_ok(G * K, ld_max, sc)) return hipErrorInvalidValue;
@@ -3191,7 +3381,7 @@ hipError_t launch_avsa_prof(const uint64_t *q_off, const uint64_t *d_off, const 
     if (blocks * 256 > 0xFFFFFFFFull) return hipErrorInvalidConfiguration;
     const size_t lds = (size_t)(256 / G) * (ld_max + 2 * G) * 4;
     if (lds > kPackedLdsMax) return hipErrorInvalidValue;
-    const auto kern = opt(Opt::PkTab) && pk_free_ok(sc, G * K, ld_max) ? nw_fill_avsa_prof_kernel<G, K, true>
+    const auto kern = o[Opt::PkTab] && pk_free_ok(sc, G * K, ld_max) ? nw_fill_avsa_prof_kernel<G, K, true>
                                                        : nw_fill_avsa_prof_kernel<G, K, false>;
     if (lds > 65536) {
         const hipError_t e = hipFuncSetAttribute((const void *)kern,
@@ -3200,7 +3390,7 @@ hipError_t launch_avsa_prof(const uint64_t *q_off, const uint64_t *d_off, const 
         if (e != hipSuccess) return e;
     }
     kern<<<dim3((uint32_t)blocks), dim3(256), lds, stream>>>(src, count, qs, ds, sc, ld_max,
-                                                              pk_steady(), generic);
+                                                              true, generic);
     return hipGetLastError();
 }
 
@@ -3217,16 +3407,16 @@ hipError_t launch_avsa(int variant, const uint64_t *q_off, const uint64_t *d_off
                        const uint32_t *q_ids, uint32_t nq, const uint32_t *d_ids,
                        uint32_t nq_total, uint64_t base, uint32_t count, const uint8_t *qs,
                        const uint8_t *ds, int2 *out, Scoring sc, uint32_t ld_max,
-                       hipStream_t stream, const uint32_t *generic) {
+                       hipStream_t stream, const Options &o, const uint32_t *generic) {
     if (!count) return hipSuccess;
     const AvsaSrc src{q_off, d_off, q_ids, d_ids, nq, nq_total, base, out};
     hipError_t e;
     switch (variant) {
-        case 4: e = avsa_pk<8, 19>(src, count, qs, ds, sc, ld_max, stream, generic); break;
-        case 5: e = avsa_pk<16, 16>(src, count, qs, ds, sc, ld_max, stream, generic); break;
-        case 6: e = avsa_pk<32, 16>(src, count, qs, ds, sc, ld_max, stream, generic); break;
-        case 7: e = avsa_pk<16, 10>(src, count, qs, ds, sc, ld_max, stream, generic); break;
-        case 8: e = avsa_pk<64, 16>(src, count, qs, ds, sc, ld_max, stream, generic); break;
+        case 4: e = avsa_pk<8, 19>(src, count, qs, ds, sc, ld_max, stream, generic, o); break;
+        case 5: e = avsa_pk<16, 16>(src, count, qs, ds, sc, ld_max, stream, generic, o); break;
+        case 6: e = avsa_pk<32, 16>(src, count, qs, ds, sc, ld_max, stream, generic, o); break;
+        case 7: e = avsa_pk<16, 10>(src, count, qs, ds, sc, ld_max, stream, generic, o); break;
+        case 8: e = avsa_pk<64, 16>(src, count, qs, ds, sc, ld_max, stream, generic, o); break;
         default: return hipErrorInvalidValue;
     }
     if (e != hipSuccess) return e;
@@ -3281,7 +3471,8 @@ hipError_t launch_avsa_scatter(const saln_nw_result *res, const uint32_t *q_ids,
 hipError_t launch_fill(int variant, const NwPairDesc *pairs, uint32_t first, uint32_t count,
                        const uint8_t *qs, const uint8_t *ds, uint8_t *mask, int2 *scratch,
                        int32_t *end_h, saln_nw_result *res, uint32_t *cig, Scoring sc,
-                       int codes, uint32_t ld_max, hipStream_t stream) {
+                       int codes, uint32_t ld_max, hipStream_t stream, FillExtras &fx) {
+    fx.fused = false;
     if (count == 0) return hipSuccess;
     const uint32_t gpb = 256 / kFillG[variant];  // lane groups per block
     const uint32_t groups = kPacked[variant] ? (count + 1) / 2 : count;
@@ -3295,11 +3486,11 @@ hipError_t launch_fill(int variant, const NwPairDesc *pairs, uint32_t first, uin
         case 1: fill_i32<16, 16>(grid, stream, pairs, first, count, qs, ds, mask, scratch, end_h, res, cig, sc, codes, ld_max); break;
         case 2: fill_i32<64, 8>(grid, stream, pairs, first, count, qs, ds, mask, scratch, end_h, res, cig, sc, codes, ld_max); break;
         case 3: return hipErrorInvalidValue;  // stripes: launch_fill_stripes
-        case 4: e = fill_pk<8, 19>(grid, stream, pairs, first, count, qs, ds, mask, end_h, res, cig, sc, codes, ld_max, rebase); break;
-        case 5: e = fill_pk<16, 16>(grid, stream, pairs, first, count, qs, ds, mask, end_h, res, cig, sc, codes, ld_max, rebase); break;
-        case 7: e = fill_pk<16, 10>(grid, stream, pairs, first, count, qs, ds, mask, end_h, res, cig, sc, codes, ld_max, rebase); break;
-        case 8: e = fill_pk<64, 16>(grid, stream, pairs, first, count, qs, ds, mask, end_h, res, cig, sc, codes, ld_max, rebase); break;
-        default: e = fill_pk<32, 16>(grid, stream, pairs, first, count, qs, ds, mask, end_h, res, cig, sc, codes, ld_max, rebase); break;
+        case 4: e = fill_pk<8, 19>(grid, stream, pairs, first, count, qs, ds, mask, end_h, res, cig, sc, codes, ld_max, rebase, fx); break;
+        case 5: e = fill_pk<16, 16>(grid, stream, pairs, first, count, qs, ds, mask, end_h, res, cig, sc, codes, ld_max, rebase, fx); break;
+        case 7: e = fill_pk<16, 10>(grid, stream, pairs, first, count, qs, ds, mask, end_h, res, cig, sc, codes, ld_max, rebase, fx); break;
+        case 8: e = fill_pk<64, 16>(grid, stream, pairs, first, count, qs, ds, mask, end_h, res, cig, sc, codes, ld_max, rebase, fx); break;
+        default: e = fill_pk<32, 16>(grid, stream, pairs, first, count, qs, ds, mask, end_h, res, cig, sc, codes, ld_max, rebase, fx); break;
     }
     if (e != hipSuccess) return e;
     return hipGetLastError();
@@ -3308,10 +3499,10 @@ hipError_t launch_fill(int variant, const NwPairDesc *pairs, uint32_t first, uin
 template <int G, int K, bool kNib = false>
 static void tb_lds(hipStream_t s, const NwPairDesc *pairs, uint32_t first, uint32_t n,
                    const uint8_t *mask, const int32_t *end_h, uint32_t *ops, saln_nw_result *res,
-                   uint32_t *cig, Scoring sc, const uint8_t *qs) {
+                   uint32_t *cig, Scoring sc, const uint8_t *qs, uint32_t *walk_left = nullptr) {
     constexpr uint32_t nt = tb_lds_threads<G, K, kNib>();
     nw_traceback_lds_kernel<G, K, kNib><<<dim3((n + nt - 1) / nt), dim3(nt), 0, s>>>(
-        pairs, first, n, mask, end_h, ops, res, cig, sc, qs, (uint32_t)opt(Opt::WalkPrio));
+        pairs, first, n, mask, end_h, ops, res, cig, sc, qs, walk_left);
 }
 
 // Traceback of plan range [first, first+n).  variant >= 0: all pairs of that
@@ -3321,7 +3512,7 @@ hipError_t launch_traceback(int variant, const NwPairDesc *pairs, uint32_t first
                             const uint8_t *qs, const uint8_t *ds, const uint8_t *mask,
                             const int32_t *end_h, uint32_t *ops, saln_nw_result *results,
                             uint32_t *cigar, Scoring sc, int stripe_layout, hipStream_t stream,
-                            const uint32_t *spec_done, bool nib) {
+                            const uint32_t *spec_done, bool nib, const uint32_t *walk_left) {
     if (n == 0) return hipSuccess;
     const dim3 grid((n + 255) / 256);
     if (nib && variant != 4 && variant != 7) return hipErrorInvalidValue;
@@ -3358,7 +3549,8 @@ hipError_t launch_traceback(int variant, const NwPairDesc *pairs, uint32_t first
         }
         case 4:  // 8 x 19 groups: 4-bit codes only (byte segments would not fit a slot)
             if (!nib) return hipErrorInvalidValue;
-            tb_lds<8, 19, true>(stream, pairs, first, n, mask, end_h, ops, results, cigar, sc, qs);
+            tb_lds<8, 19, true>(stream, pairs, first, n, mask, end_h, ops, results, cigar, sc, qs,
+                                const_cast<uint32_t *>(walk_left));
             break;
         case 5: tb_lds<16, 16>(stream, pairs, first, n, mask, end_h, ops, results, cigar, sc, qs); break;
         case 6: tb_lds<32, 16>(stream, pairs, first, n, mask, end_h, ops, results, cigar, sc, qs); break;
@@ -3556,13 +3748,10 @@ hipError_t launch_span_watch(const int2 *col, uint32_t r0, uint32_t r1, uint32_t
     return hipGetLastError();
 }
 
-// row-fill stripes per workgroup (option nw.rows_wpg)
-static uint32_t rows_wpg() { return (uint32_t)opt(Opt::RowsWpg); }
-
-// one stripe per SIMD (kLone) when a launch's stripes fit the device's SIMDs
-// (option nw.rows_lone)
-static bool rows_lone(uint32_t n_waves) {
-    if (!opt(Opt::RowsLone)) return false;
+// one stripe per SIMD (kPlaceLone) when a launch's stripes fit the device's
+// SIMDs (option nw.rows_lone); XCD-local neighbours (kPlaceXcd) on top when
+// the caller's stream may use every CU (option nw.rows_xcd)
+static uint32_t device_simds() {
     static const uint32_t simds = [] {
         int dev = 0, cus = 0;
         if (hipGetDevice(&dev) != hipSuccess ||
@@ -3570,29 +3759,54 @@ static bool rows_lone(uint32_t n_waves) {
             return 0u;
         return 4u * (uint32_t)cus;
     }();
-    return n_waves <= simds;
+    return simds;
+}
+
+// The stream may run on every CU of the device (no CU mask narrower than it):
+// only then is every stripe of a launch that fits the SIMDs resident at once.
+static bool stream_all_cus(hipStream_t s) {
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        return false;
+    uint32_t m[32] = {};
+    const uint32_t nw = std::min<uint32_t>(32, ((uint32_t)cus + 31) / 32);
+    if (hipExtStreamGetCUMask(s, nw, m) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    for (uint32_t c = 0; c < (uint32_t)cus; ++c)
+        if (!(m[c / 32] >> (c % 32) & 1u)) return false;
+    return true;
 }
 
 hipError_t launch_fill_stripes(const NwPairDesc *pairs, const uint2 *work, uint32_t n_work,
                                const uint8_t *qs, const uint8_t *ds, uint8_t *mask,
                                int2 *scratch, uint32_t *prog, uint32_t *err, int32_t *end_h,
-                               Scoring sc, int codes, int layout, int rows_k, hipStream_t stream) {
+                               Scoring sc, int codes, int layout, int rows_k, hipStream_t stream,
+                               const Options &o) {
     if (!n_work) return hipSuccess;
     const dim3 grid(n_work), block(64);
     const bool pk = layout == 1;
     if (layout == 2) {  // row-synchronous stripes of 64 * rows_k columns
         const int32_t pm = 4 * (sc.match - sc.mismatch);
-        const uint32_t wpg = rows_wpg();  // waves (stripes) per workgroup
         auto go = [&](auto k_c, auto codes_c, auto minpen_c) {
             constexpr int kK = decltype(k_c)::value;
+            constexpr int kC = decltype(codes_c)::value;
+            constexpr bool kP = decltype(minpen_c)::value;
             const uint32_t nw = n_work * (4 / kK);
-            const dim3 g((nw + wpg - 1) / wpg), b(64 * wpg);
-            if (rows_lone(nw))
-                nw_fill_rows_kernel<kK, decltype(codes_c)::value, decltype(minpen_c)::value, true>
-                    <<<g, b, 0, stream>>>(pairs, work, qs, ds, mask, scratch, err, end_h, sc, nw);
-            else
-                nw_fill_rows_kernel<kK, decltype(codes_c)::value, decltype(minpen_c)::value, false>
-                    <<<g, b, 0, stream>>>(pairs, work, qs, ds, mask, scratch, err, end_h, sc, nw);
+            const bool lone = o[Opt::RowsLone] && nw <= device_simds();
+            if (lone && o[Opt::RowsXcd] && nw >= 16 && stream_all_cus(stream)) {
+                const uint32_t run = (nw + 7) / 8;
+                nw_fill_rows_kernel<kK, kC, kP, kPlaceXcd><<<dim3(8 * run), block, 0, stream>>>(
+                    pairs, work, qs, ds, mask, scratch, err, end_h, sc, nw, run);
+            } else if (lone) {
+                nw_fill_rows_kernel<kK, kC, kP, kPlaceLone><<<dim3(nw), block, 0, stream>>>(
+                    pairs, work, qs, ds, mask, scratch, err, end_h, sc, nw, 0);
+            } else {
+                nw_fill_rows_kernel<kK, kC, kP, kPlaceShared><<<dim3(nw), block, 0, stream>>>(
+                    pairs, work, qs, ds, mask, scratch, err, end_h, sc, nw, 0);
+            }
         };
         auto by_k = [&](auto codes_c, auto minpen_c) {
             if (rows_k == 4) go(std::integral_constant<int, 4>{}, codes_c, minpen_c);
@@ -3656,13 +3870,13 @@ Geom variant_geom(int v) { return kVariants[v]; }
 // 0.188 ms, 5 kbp 0.75 -> 0.70 ms), else K = 2 (C4: 1,564 K = 1 waves share
 // SIMDs, 19.5 vs 14.5 ms).  Option nw.rows_k = 1, 2 or 4 forces it (read per
 // plan).
-int stripe_rows_k(uint64_t waves_k1) {
-    if (const int64_t v = opt(Opt::RowsK)) return v == 1 || v == 4 ? (int)v : 2;
+int stripe_rows_k(uint64_t waves_k1, const Options &o) {
+    if (const int64_t v = o[Opt::RowsK]) return v == 1 || v == 4 ? (int)v : 2;
     return waves_k1 <= 1024 ? 1 : 2;
 }
 
-bool stripe_packed(const Scoring &sc, uint64_t n_waves, bool wide) {
-    const int64_t force = opt(Opt::StripePk);  // -1 auto
+bool stripe_packed(const Scoring &sc, uint64_t n_waves, bool wide, const Options &o) {
+    const int64_t force = o[Opt::StripePk];  // -1 auto
     if (force == 0) return false;
     if (force != 1 && (n_waves < kStripePkMinWaves || !wide)) return false;
     const int64_t pen = 2ll * (sc.match - sc.mismatch);

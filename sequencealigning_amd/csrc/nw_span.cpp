@@ -33,6 +33,7 @@ using namespace saln;
 
 struct saln_nw_span {
     saln_context *ctx = nullptr;
+    Options opts{};  // the context's effective options at creation
     Scoring sc{};
     uint32_t lq = 0, ld = 0, col_lo = 0, col_hi = 0;
     int K = 2;                  // row-fill columns per lane (stripe width 64 K)
@@ -144,8 +145,8 @@ static int span_walk_spec(saln_nw_span *s, const uint8_t *d_q, const uint8_t *d_
 
 // Row-fill columns per lane of a span: K = 1 while every 64-column stripe of
 // the span has a SIMD to itself (stripe_rows_k)
-static int span_k(uint64_t col_lo, uint64_t col_hi, uint64_t device_cols) {
-    return stripe_rows_k((std::max(col_hi - col_lo, device_cols) + 63) / 64);
+static int span_k(uint64_t col_lo, uint64_t col_hi, uint64_t device_cols, const Options &o) {
+    return stripe_rows_k((std::max(col_hi - col_lo, device_cols) + 63) / 64, o);
 }
 
 extern "C" {
@@ -156,7 +157,8 @@ uint64_t saln_nw_span_boundary_elems(uint64_t len_db) {
 
 uint64_t saln_nw_span_boundary_cols(uint64_t col_lo, uint64_t col_hi, uint64_t device_cols) {
     if (col_hi <= col_lo) return 0;
-    const uint64_t W = 64u * (uint64_t)span_k(col_lo, col_hi, device_cols);
+    // (no context: the process registry's nw.rows_k)
+    const uint64_t W = 64u * (uint64_t)span_k(col_lo, col_hi, device_cols, opt_registry());
     return (col_hi + W - 1) / W - col_lo / W + 1;
 }
 
@@ -184,12 +186,13 @@ int saln_nw_span_create(saln_context *ctx, uint64_t len_q, uint64_t len_db, uint
     HIP_TRY(hipSetDevice(ctx->device));
     auto *s = new saln_nw_span;
     s->ctx = ctx;
+    s->opts = ctx->opts.effective();
     s->sc = sc;
     s->lq = (uint32_t)len_q;
     s->ld = (uint32_t)len_db;
     s->col_lo = (uint32_t)col_lo;
     s->col_hi = (uint32_t)col_hi;
-    s->K = span_k(col_lo, col_hi, device_cols);
+    s->K = span_k(col_lo, col_hi, device_cols, s->opts);
     const uint32_t W = 64u * (uint32_t)s->K;
     s->g0 = s->col_lo / W;
     s->nst = (s->col_hi + W - 1) / W - s->g0;
@@ -246,8 +249,8 @@ int saln_nw_span_create(saln_context *ctx, uint64_t len_q, uint64_t len_db, uint
     // speculative walk passes (options nw.spec, nw.spec_passes, default 3)
     // for spans of at least two walker stripes
     {
-        const int passes = (int)opt(Opt::SpecPasses);
-        if (opt(Opt::Spec) != 0 && passes > 0 && s->ntiles >= 2) {
+        const int passes = (int)s->opts[Opt::SpecPasses];
+        if (s->opts[Opt::Spec] != 0 && passes > 0 && s->ntiles >= 2) {
             s->spec_passes = passes;
             std::vector<uint2> blocks;
             for (uint32_t t = 0; t < s->ntiles; ++t) blocks.push_back(make_uint2(0u, s->t0 + t));
@@ -301,7 +304,7 @@ int saln_nw_span_fill(saln_nw_span *s, const uint8_t *d_q, const uint8_t *d_db, 
     HIP_TRY(launch_fill_stripes(s->d_pair, s->d_work, s->n_work, d_q, d_db, s->mask_arg(),
                                 s->scratch_arg(), nullptr, s->d_err, s->d_endh, s->sc,
                                 0 /* walk codes */, 2 /* row-major tiles */, s->K,
-                                resolve_stream(stream, s->ctx)));
+                                resolve_stream(stream, s->ctx), s->opts));
     return SALN_OK;
 }
 

@@ -145,9 +145,10 @@ int saln_wfa_affine_plan_create(saln_context *ctx, const uint64_t *q_off, uint64
     // Each pass stages the pair's sequences in LDS when they fit next to its
     // rings within kSeqLds / the 64 KB workgroup limit (else reads HBM).
     // tuning options (saln_option_set): staged-sequence LDS, ring widths (0 auto)
-    const uint64_t seq_lds = (uint64_t)opt(Opt::Wfa2SeqLds);
-    const int32_t w1 = (int32_t)opt(Opt::Wfa2W1);
-    const int32_t w2 = (int32_t)opt(Opt::Wfa2W2);
+    const Options opts = ctx->opts.effective();
+    const uint64_t seq_lds = (uint64_t)opts[Opt::Wfa2SeqLds];
+    const int32_t w1 = (int32_t)opts[Opt::Wfa2W1];
+    const int32_t w2 = (int32_t)opts[Opt::Wfa2W2];
     auto pass = [&](int32_t W) {
         WfaAffParams q = p->prm;
         q.W = W;

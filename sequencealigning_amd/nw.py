@@ -170,9 +170,10 @@ def pack_csr(seqs) -> tuple[np.ndarray, np.ndarray]:
 
 
 def nw_align_batch(queries, dbs, pairs=None, mode: Mode = Mode.Global, *, scoring=None,
-                   device: int = 0, with_cigar: bool = True):
+                   device: int = 0, with_cigar: bool = True, ctx=None):
     """Batched n_w_align.  pairs: None (all-vs-all, db outer / query inner like
-    main.rs:61-62) or an (n, 2) array of (query index, db index).
+    main.rs:61-62) or an (n, 2) array of (query index, db index).  ctx: a
+    context of the caller's (_lib.new_context) instead of the per-process one.
     Returns (results structured array, list of CIGARs or None)."""
     qs, qo = pack_csr(queries)
     ds, do = pack_csr(dbs)
@@ -199,7 +200,7 @@ def nw_align_batch(queries, dbs, pairs=None, mode: Mode = Mode.Global, *, scorin
     cig = np.zeros(max(1, int(coff[-1])), np.uint32) if with_cigar else None
     vp = lambda a: a.ctypes.data_as(C.c_void_p) if a is not None else None  # noqa: E731
     rc = _lib.lib().saln_nw_align_batch(
-        _lib.context(device), vp(qs), vp(qo), len(qo) - 1, vp(ds), vp(do), len(do) - 1, vp(pq),
+        ctx if ctx is not None else _lib.context(device), vp(qs), vp(qo), len(qo) - 1, vp(ds), vp(do), len(do) - 1, vp(pq),
         vp(pd), n_pairs, int(mode), _lib.scoring_arg(scoring), vp(res), vp(cig), vp(coff))
     if rc == _lib.NOT_IMPLEMENTED:
         raise AlignmentError("not implemented")
@@ -217,7 +218,7 @@ class NwPlan:
     multi-GPU driver."""
 
     def __init__(self, q_off: np.ndarray, db_off: np.ndarray, pairs=None, *, scoring=None,
-                 device: int = 0):
+                 device: int = 0, ctx=None):
         self._L = _lib.lib()
         self.device = device
         self.q_off = np.ascontiguousarray(q_off, np.uint64)
@@ -233,7 +234,8 @@ class NwPlan:
             pd = np.ascontiguousarray(pairs[:, 1])
         self._h = C.c_void_p()
         vp = lambda a: a.ctypes.data_as(C.c_void_p) if a is not None else None  # noqa: E731
-        _lib.check(self._L.saln_nw_plan_create(_lib.context(device), vp(self.q_off), n_q,
+        ctx = ctx if ctx is not None else _lib.context(device)
+        _lib.check(self._L.saln_nw_plan_create(ctx, vp(self.q_off), n_q,
                                                vp(self.db_off), n_db, vp(pq), vp(pd),
                                                self.n_pairs, int(Mode.Global),
                                                _lib.scoring_arg(scoring), C.byref(self._h)),

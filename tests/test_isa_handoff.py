@@ -45,21 +45,22 @@ def rows_kernels():
     funcs = isa_check.load_functions(OBJ)
     out = {}
     for name, insns in funcs.items():
-        m = re.search(r"nw_fill_rows_kernelILi(\d)ELi(\d)ELb(\d)E", name)
+        m = re.search(r"nw_fill_rows_kernelILi(\d)ELi(\d)ELb(\d)ELi(\d)E", name)
         if m:
-            out[tuple(int(m.group(i)) for i in range(1, 4))] = insns
+            out[tuple(int(m.group(i)) for i in range(1, 5))] = insns
     return out
 
 
-# (K, codes, minpen): every instantiation
-KEYS = [(k, c, p) for k in (1, 2, 4) for c in (0, 1, 2) for p in (0, 1)]
+# (K, codes, minpen, placement): every instantiation (placement 2, XCD-local
+# neighbours, holds a plain-publication and an sc1-publication body)
+KEYS = [(k, c, p, pl) for k in (1, 2, 4) for c in (0, 1, 2) for p in (0, 1) for pl in (0, 1, 2)]
 
 
 def test_all_row_fill_instantiations_present(rows_kernels):
     assert set(rows_kernels) == set(KEYS)
 
 
-@pytest.mark.parametrize("key", KEYS, ids=lambda k: f"K{k[0]}_codes{k[1]}_minpen{k[2]}")
+@pytest.mark.parametrize("key", KEYS, ids=lambda k: f"K{k[0]}_codes{k[1]}_minpen{k[2]}_place{k[3]}")
 def test_prefetch_counted_wait_exact(rows_kernels, key):
     import isa_check
     insns = rows_kernels[key]

@@ -161,19 +161,22 @@ def test_c2_scale_properties(saln, oracle):
     plan.close()
 
 
-@pytest.mark.parametrize("nib,narrow", [(0, 0), (1, 0), (1, 1)])
-def test_walk_code_formats_match_oracle(saln, oracle, saln_opt, nib, narrow):
-    """The three walk-code layouts of the short-query packed fills give the
-    oracle's results: byte codes (nw.nib_codes = 0, round 3), 4-bit codes in
-    16 x 10 groups (the default) and 4-bit codes in 8 x 19 groups
-    (nw.narrow_walk = 1: queries of <= 152 columns).  20,000 configs[1]
-    pairs (score, end states, panic, printed, CIGAR word for word) and a
-    ragged batch: 1..160-column queries, dbs up to 1,200 rows (the rebasing
-    int16 frame), identical and two-letter pairs."""
+@pytest.mark.parametrize("tab,fuse", [(1, 1), (1, 2), (1, 0), (0, 0)])
+def test_walk_code_formats_match_oracle(saln, oracle, saln_opt, tab, fuse):
+    """The 4-bit walk codes of the short-query packed fills (8 x 19 groups for
+    queries of <= 152 columns, 16 x 10 up to 160) give the oracle's results
+    through every fill / walk route: the table fill walking its packs in the
+    same launch (nw.fuse_walk = 1, the default), the same fill leaving every
+    pack to the walker launch (2: the route of a pack whose waves ran on
+    several XCDs), the table fill with the separate walker (0), and the
+    generic fill (nw.pk_tab = 0).  20,000 configs[1] pairs (score, end
+    states, panic, printed, CIGAR word for word) and a ragged batch: 1..160-
+    column queries, dbs up to 1,200 rows (the rebasing int16 frame),
+    identical and two-letter pairs."""
     import torch
     from sequencealigning_amd import synth
-    saln_opt("nw.nib_codes", nib)
-    saln_opt("nw.narrow_walk", narrow)
+    saln_opt("nw.pk_tab", tab)
+    saln_opt("nw.fuse_walk", fuse)
     n, L = 20_000, 150
     qs, qo, ds, do = synth.iid_pairs(n, L, L, seed=0x5EED0002)
     plan = saln.NwPlan(qo, do, pairs=np.stack([np.arange(n), np.arange(n)], 1))
@@ -195,7 +198,7 @@ def test_walk_code_formats_match_oracle(saln, oracle, saln_opt, nib, narrow):
             o0 = int(plan.cigar_off[k])
             assert np.array_equal(cig[o0:o0 + int(res["cigar_len"][k])], want.cigar_words(k)), k
     plan.close()
-    rng = np.random.default_rng(4040 + 2 * nib + narrow)
+    rng = np.random.default_rng(4040 + 3 * tab + fuse)
     queries, dbs = [], []
     for lq, ld in [(1, 1), (1, 40), (9, 3), (19, 19), (20, 150), (38, 900), (151, 151),
                    (152, 152), (152, 1200), (153, 160), (160, 400), (140, 1200), (75, 5)]:
@@ -240,16 +243,22 @@ def test_table_fill_equals_generic(saln, oracle, saln_opt, case):
     1 % of the queries and 1 % of the dbs (those waves take the fallback
     launch, the rest of the launch the table body); "scheme" uses
     {2, -3, -5, -2} (bonuses 12 / 2).  "long_db" / "long_db_n": 150 x 500
-    pairs in 16 x 10 groups, whose dbs need the rebasing frame in the original
-    frame but not in the extension-free one (the fallback launch then
-    rebases)."""
+    pairs (8 x 19 groups, the fused fill + walk) and 155 x 500 pairs (16 x 10
+    groups), whose dbs need the rebasing frame in the original frame but not
+    in the extension-free one (the fallback launch then rebases)."""
     from sequencealigning_amd import synth
     n, L = 20_000, 150
     LD = L
     if case.startswith("long_db"):
         n, LD = 4_000, 500
-        saln_opt("nw.narrow_walk", 0)
     qs, qo, ds, do = synth.iid_pairs(n, L, LD, seed=0x7AB0 + len(case))
+    if case.startswith("long_db"):  # the same db against a 155-column query (16 x 10)
+        qs2, qo2, _, _ = synth.iid_pairs(n, 155, LD, seed=0x7AB1 + len(case))
+        qs = np.concatenate([qs, qs2])
+        qo = np.concatenate([qo, qo2[1:] + qo[-1]])
+        ds = np.concatenate([ds, ds])
+        do = np.concatenate([do, do[1:] + do[-1]])
+        n *= 2
     qs, ds = qs.copy(), ds.copy()
     scoring = (2, -3, -5, -2) if case == "scheme" else None
     if case in ("with_n", "long_db_n"):
@@ -274,17 +283,20 @@ def test_table_fill_equals_generic(saln, oracle, saln_opt, case):
                 assert np.array_equal(got, want.cigar_words(k)), k
 
 
-def test_table_fill_concurrent_plans(saln, saln_opt):
+@pytest.mark.parametrize("lens", [(150, 150), (150, 156)])
+def test_table_fill_concurrent_plans(saln, saln_opt, lens):
     """Two plans whose data hold N bytes execute at the same time on two
-    streams, three times each: every table launch has its own epoch slot, so
-    each fallback launch runs exactly its own launch's bail-outs.  Results
-    equal each plan run alone."""
+    streams, three times each: each plan's table launches mark their
+    bail-outs in the plan's own bail word (a process-wide slot
+    ring shared by the instantiations), so each fallback launch runs exactly
+    its own launch's bail-outs.  (150, 156): the fused 8 x 19 fill + walk
+    beside the 16 x 10 table fill.  Results equal each plan run alone."""
     import torch
     from sequencealigning_amd import synth
     saln_opt("nw.pk_tab", 1)
-    n, L = 8_000, 150
+    n = 8_000
     data, plans, alone = [], [], []
-    for seed in (0xC0, 0xC1):
+    for seed, L in zip((0xC0, 0xC1), lens):
         qs, qo, ds, do = synth.iid_pairs(n, L, L, seed=seed)
         qs = qs.copy()
         rng = np.random.default_rng(seed)
@@ -753,3 +765,61 @@ def test_long_gaps_lds_walker(saln, oracle):
         assert int(res["end_states"][k]) == o.end_states, k
         assert (int(res["status"][k]) == 2) == o.panics, k
         assert (expand(cig[k]) if res["printed"][k] else None) == o.first_ops, k
+
+
+def test_context_options_two_threads(saln, oracle):
+    """Per-context options (saln_context_option_set): two
+    contexts on two host threads run batches at the same time with
+    different kernel choices - the fused 8 x 19 table fill + walk (pk_tab 1,
+    fuse_walk 1) and the generic fill with the separate walker (pk_tab 0) -
+    and both equal the oracle; the process registry and the per-process
+    context keep their defaults."""
+    import threading
+
+    from sequencealigning_amd import _lib
+    L = _lib.lib()
+    rng = np.random.default_rng(91)
+    n = 3_000
+    qs = [rand_seq(rng, 150) for _ in range(n)]
+    ds = [rand_seq(rng, int(rng.integers(120, 170))) for _ in range(n)]
+    want = [oracle.nw(qs[k], ds[k], literal_dfs=False) for k in range(0, n, 10)]
+    ctxs = [_lib.new_context(0), _lib.new_context(0)]
+    try:
+        _lib.set_context_option(ctxs[0], "nw.pk_tab", 1)
+        _lib.set_context_option(ctxs[0], "nw.fuse_walk", 1)
+        _lib.set_context_option(ctxs[1], "nw.pk_tab", 0)
+        assert _lib.get_context_option(ctxs[1], "nw.pk_tab") == 0
+        assert _lib.get_option("nw.pk_tab")[0] == 1
+        assert _lib.get_context_option(_lib.context(0), "nw.pk_tab") == 1
+        out = [None, None]
+        errs = []
+
+        def run(i):
+            try:
+                rs = []
+                for _ in range(3):  # overlapping repeats
+                    rs.append(saln.nw_align_batch(qs, ds, pairs=[(k, k) for k in range(n)],
+                                                  ctx=ctxs[i]))
+                out[i] = rs
+            except Exception as e:  # pragma: no cover - surfaced below
+                errs.append(e)
+
+        th = [threading.Thread(target=run, args=(i,)) for i in range(2)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        assert not errs, errs
+        for i in range(2):
+            for res, cg in out[i]:
+                for j, k in enumerate(range(0, n, 10)):
+                    o = want[j]
+                    assert (int(res["score"][k]), int(res["end_states"][k]),
+                            int(res["status"][k]) == 2) == (o.score, o.end_states, o.panics), (i, k)
+                    assert (saln.cigar_ops_string(cg[k]) if res["printed"][k] else None) == \
+                        o.first_ops, (i, k)
+        _lib.clear_context_option(ctxs[1])
+        assert _lib.get_context_option(ctxs[1], "nw.pk_tab") == 1
+    finally:
+        for c in ctxs:
+            L.saln_context_destroy(c)

@@ -314,3 +314,38 @@ def test_cu_range_streams_cover_every_xcd():
     places = {(xc[k] & 0xF, (hw[k] >> 13) & 7, (hw[k] >> 12) & 1, (hw[k] >> 8) & 0xF) for k in range(n)}
     per_xcd = [sum(1 for p in places if p[0] == x) for x in range(8)]
     assert per_xcd == [2] * 8, per_xcd
+
+
+def test_workgroup_dispatch_round_robin_over_xcds():
+    """The row fill's XCD-local placement (nw_fill_rows_kernel kPlaceXcd)
+    assumes workgroup b of a launch on an unmasked stream runs on XCD b % 8:
+    wave v = (b % 8) * run + b / 8 then keeps runs of consecutive stripes on
+    one XCD.  The probe records each one-wave workgroup's XCC_ID."""
+    import ctypes as C
+
+    from sequencealigning_amd import _lib
+    L, ctx = _lib.lib(), _lib.context(0)
+    n = 1024
+    hw, xc = (C.c_uint32 * n)(), (C.c_uint32 * n)()
+    assert L.saln_device_cu_probe(ctx, None, n, hw, xc) == _lib.OK
+    ids = [xc[b] & 0xF for b in range(n)]
+    assert len(set(ids[:8])) == 8, ids[:8]
+    assert all(ids[b] == ids[b % 8] for b in range(n)), \
+        [(b, ids[b], ids[b % 8]) for b in range(n) if ids[b] != ids[b % 8]][:8]
+
+
+@pytest.mark.parametrize("lq,ld", [(20000, 20000), (9000, 30000)])
+def test_row_fill_xcd_placement_equal(saln_opt, lq, ld):
+    """nw.rows_xcd = 1 (stripes in XCD runs, plain publication inside a run)
+    gives the same scores, statuses and CIGARs as the dispatch-order placement."""
+    from nw_check import rand_seq
+
+    import sequencealigning_amd as saln
+    rng = np.random.default_rng(lq + ld)
+    q = rand_seq(rng, lq)
+    d = _mut(rng, q, 0.05)[:ld] if ld <= lq else _mut(rng, q, 0.05) + rand_seq(rng, ld - lq)
+    saln_opt("nw.rows_xcd", 0)
+    a = saln.n_w_align(q, d)
+    saln_opt("nw.rows_xcd", 1)
+    b = saln.n_w_align(q, d)
+    _same(a, b)
