@@ -254,10 +254,52 @@ def timed(fn, world, dist, torch, local):
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
+    timed.local_s = dt  # this rank's own wall time (rank_diag)
     t = torch.tensor([dt], dtype=torch.float64, device=f"cuda:{local}")
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+def rank_diag(dist, torch, world: int, device, compute_s: float, gather_s: float,
+              gather_bytes: int, wall_s: float | None = None) -> list[dict]:
+    """Per-rank diagnosis of a multi-GPU line: every rank's
+    compute time, gather time and the bytes its gather moved, all-gathered
+    so rank 0 can print them beside the value; a scaling curve then shows
+    where its time went (compute imbalance or the RCCL gather)."""
+    t = torch.tensor([compute_s, gather_s, float(gather_bytes),
+                      -1.0 if wall_s is None else wall_s], dtype=torch.float64, device=device)
+    if world > 1:
+        out = [torch.zeros_like(t) for _ in range(world)]
+        dist.all_gather(out, t)
+    else:
+        out = [t]
+    rows = []
+    for r, x in enumerate(out):
+        v = x.cpu().tolist()
+        row = {"rank": r, "compute_ms": round(v[0] * 1e3, 3), "gather_ms": round(v[1] * 1e3, 3),
+               "gather_bytes": int(v[2])}
+        if v[3] >= 0:
+            row["wall_ms"] = round(v[3] * 1e3, 3)
+        rows.append(row)
+    return rows
+
+
+def gather_probe(dist, torch, world: int, fn, reps: int = 3) -> float:
+    """Seconds per call of one gather (fn), untimed by the line: barrier and
+    synchronize around each call, min over reps."""
+    best = float("inf")
+    for _ in range(reps):
+        if world > 1:
+            dist.barrier()
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        fn()
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
+        best = min(best, time.perf_counter() - t0)
+    return best
 
 
 def event_time(torch, fn, reps: int) -> float:
@@ -297,6 +339,11 @@ def leg_c5(world, rank, local, dist, torch, nq=10_000, ndb=100_000, L=150, cpu=T
     # on torch's stream, the stream the engine launches on)
     fill_s = event_time(torch, lambda: av.execute(gather=False, check=False), 1)
     av.check()
+    diag = None
+    if world > 1:
+        g_s = gather_probe(dist, torch, world, av.gather)
+        diag = rank_diag(dist, torch, world, f"cuda:{local}", fill_s, g_s,
+                         av.cap * 4 * (world if rank == av.dst else 1), wall_s=timed.local_s)
     out = None
     if rank == 0:
         # query profiles (nw.avsa_profile), bonuses in the extension-free frame (nw.pk_tab)
@@ -315,6 +362,12 @@ def leg_c5(world, rank, local, dist, torch, nq=10_000, ndb=100_000, L=150, cpu=T
                "roofline": valu_roof(kern, fill_s, ins, note="score-only: no mask, HBM traffic "
                                      "~0 B/cell; the packed fill's VALU issue is the bound",
                                      gcups_fill=round(av.cells_local / fill_s / 1e9, 1))}
+        if diag is not None:
+            out["rank_diag"] = {"per_execute": diag,
+                                "note": "compute_ms: the rank's block (one execute without the "
+                                        "gather, hipEvents); gather_ms: one dist.gather of the "
+                                        "{score, status} records to rank 0 (RCCL); gather_bytes: "
+                                        "received at rank 0, sent elsewhere"}
         if cpu:
             # checker: a seeded sample of the gathered records against the oracle
             from oracle import refcpu  # checker only
@@ -816,17 +869,29 @@ def launch_selftest(backend: str) -> None:
     import torch.distributed as dist
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
+    diag = None
     if world > 1:
         dist.init_process_group(backend)
         t = torch.tensor([rank], dtype=torch.int64)
         ranks = [torch.zeros_like(t) for _ in range(world)]
         dist.all_gather(ranks, t)
         ranks = sorted(int(x.item()) for x in ranks)
+        # the multi-GPU diagnosis of the real lines on a host stand-in: a
+        # per-rank "compute" step and the gather of its records to rank 0
+        rec = torch.full((4096,), rank, dtype=torch.int32)
+        parts = [torch.empty_like(rec) for _ in range(world)] if rank == 0 else None
+        t0 = time.perf_counter()
+        _ = np.sort(np.random.default_rng(rank).random(200_000))
+        compute_s = time.perf_counter() - t0
+        gather_s = gather_probe(dist, torch, world, lambda: dist.gather(rec, parts, dst=0), 2)
+        diag = rank_diag(dist, torch, world, "cpu", compute_s, gather_s,
+                         rec.numel() * 4 * (world if rank == 0 else 1))
         dist.destroy_process_group()
     else:
         ranks = [0]
     if rank == 0:
-        print(json.dumps({"launch_selftest": True, "n_gpus": world, "ranks": ranks}), flush=True)
+        print(json.dumps({"launch_selftest": True, "n_gpus": world, "ranks": ranks,
+                          "rank_diag": diag}), flush=True)
 
 
 def main() -> None:
@@ -935,10 +1000,19 @@ def main() -> None:
             step()
         drain()
     dt = timed(run_steps, world, dist, torch, local)
+    local_dt = timed.local_s
     plan.check()  # device-side status of every timed execute (raises on a timeout)
     fill_ms, fill_n = plan.kernel_time("nw_fill")
     tb_ms, tb_n = plan.kernel_time("nw_traceback")
     ex_ms, ex_n = plan.kernel_time("nw_execute")
+    diag = None
+    if world > 1:
+        # where a rank's step time went: its executes (events, per step) and
+        # one RCCL gather of its records (probed after the timed region)
+        g_s = gather_probe(dist, torch, world, lambda: gather(0))
+        diag = rank_diag(dist, torch, world, f"cuda:{local}", ex_ms / max(1, ex_n) / 1e3, g_s,
+                         res[0].numel() * 4 * (world if rank == 0 else 1),
+                         wall_s=local_dt / max(1, args.steps))
     cells_rank = plan.cells
     total_cells = cells_rank * world * args.steps
     # outside the timed region: the fill alone (sequential executes), so the
@@ -1004,6 +1078,12 @@ def main() -> None:
             "env": {k: os.environ[k] for k in ALLOWED_ENV if k in os.environ},
             "options": saln._lib.non_default_options(),
         }
+        if diag is not None:
+            out["rank_diag"] = {"per_step": diag,
+                                "note": "compute_ms: the rank's execute (fill + walk) per step "
+                                        "from hipEvents; gather_ms: one dist.gather of its "
+                                        "records to rank 0 (RCCL), probed after the timed "
+                                        "region; wall_ms: the rank's own timed wall per step"}
         if not args.score_only:
             out["verified"] = verify_c2(hr, cig[last].cpu().numpy().view(np.uint32),
                                         plan.cigar_off, qs, qo, ds, do)

@@ -164,8 +164,12 @@ int saln_nw_render(saln_context *ctx, const uint8_t *q, uint64_t len_q, const ui
 /* The same text for a batch, each pair computed once (the drop-in CLI and
  * hosts that print per pair).  Replaces the pair loop main.rs:61-74 with the
  * text every n_w_align call prints: one plan for all pairs (same CSR / pair
- * conventions as saln_nw_align_batch; NULL pair lists = all-vs-all, db outer),
- * the reference DFS per pair on host threads.  The text stays in the
+ * conventions as saln_nw_align_batch; NULL pair lists = all-vs-all, db outer).
+ * The GPU walks each pair's first printed alignment and decides what the
+ * reference DFS meets after it; pairs whose text that settles (no block,
+ * exactly one block, or with max_blocks = 1 the first block and then the cap
+ * or the panic) are rendered from that walk, the others by the reference DFS
+ * on host threads over their parent codes.  The text stays in the
  * returned handle until saln_nw_text_free.  stop_at_panic = 1: pairs after
  * the first one whose traceback panics (REF_PANIC_BOUNDARY) are not rendered
  * - the reference aborts there (exit 101) - so saln_nw_text_count is that
@@ -181,6 +185,9 @@ int saln_nw_render_batch(saln_context *ctx, const uint8_t *q_seq, const uint64_t
 int saln_nw_render_text(saln_context *ctx, const uint8_t *q, uint64_t len_q, const uint8_t *d,
                         uint64_t len_db, int32_t mode, uint64_t max_blocks, saln_nw_text **out);
 uint64_t saln_nw_text_count(const saln_nw_text *t);
+/* Of those pairs, the ones rendered from the GPU's walk alone (no parent-code
+ * download, no host DFS). */
+uint64_t saln_nw_text_gpu_decided(const saln_nw_text *t);
 /* Pair `pair` (< count): its text (valid until free; not NUL-terminated), the
  * blocks printed, the render status (SALN_OK, SALN_REF_PANIC_BOUNDARY after
  * the text, SALN_ENUM_CAP, SALN_NOT_IMPLEMENTED), its saln_nw_result, and

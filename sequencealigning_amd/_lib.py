@@ -104,6 +104,7 @@ EXPORTS = [
     "saln_option_set", "saln_option_get", "saln_option_name", "saln_options_reset",
     "saln_context_option_set", "saln_context_option_get", "saln_context_option_clear",
     "saln_nw_render_batch", "saln_nw_render_text", "saln_nw_text_count", "saln_nw_text_get",
+    "saln_nw_text_gpu_decided",
     "saln_nw_text_free",
     "saln_wfa_render_batch", "saln_wfa_text_count", "saln_wfa_text_get", "saln_wfa_text_free",
 ]
@@ -240,6 +241,8 @@ def lib() -> C.CDLL:
                                           C.c_uint64, C.POINTER(vp)]
         L.saln_nw_text_count.argtypes = [vp]
         L.saln_nw_text_count.restype = C.c_uint64
+        L.saln_nw_text_gpu_decided.argtypes = [vp]
+        L.saln_nw_text_gpu_decided.restype = C.c_uint64
         L.saln_nw_text_get.argtypes = [vp, C.c_uint64, C.POINTER(vp), u64p, u64p, i32p,
                                        C.POINTER(NwResult), u64p]
         L.saln_nw_text_free.argtypes = [vp]

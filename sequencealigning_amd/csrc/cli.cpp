@@ -383,18 +383,32 @@ int main(int argc, char **argv) {
                                       pq.data(), pd.data(), pq.size(), a.mode, a.max_blocks,
                                       a.abort_on_panic ? 1 : 0, &t);
         mark("render batch");
-        if (rc != SALN_OK) {
-            std::fprintf(stderr, "saln: %s\n", saln_last_error());
-            saln_context_destroy(ctx);
-            return 1;
-        }
-        const uint64_t n = saln_nw_text_count(t);
+        // a chunk that fails as a whole (one pair whose scores leave the
+        // engine's int32 range, an allocation) is rendered pair by pair, so
+        // every pair before the failing one is printed first, in the
+        // reference's streaming order (main.rs:61-74)
+        const bool per_pair = rc != SALN_OK;
+        const uint64_t n = per_pair ? pq.size() : saln_nw_text_count(t);
         for (uint64_t k = 0; k < n; ++k) {
             const Rec &q = query[pq[k]], &d = db[pd[k]];
             const char *txt = nullptr;
             uint64_t len = 0, blocks = 0, ns = 0;
             int32_t status = SALN_OK;
-            saln_nw_text_get(t, k, &txt, &len, &blocks, &status, nullptr, &ns);
+            if (per_pair) {
+                if (t) saln_nw_text_free(t);
+                t = nullptr;
+                rc = saln_nw_render_text(ctx, q.seq.data(), q.seq.size(), d.seq.data(),
+                                         d.seq.size(), a.mode, a.max_blocks, &t);
+                if (rc != SALN_OK) {
+                    std::fflush(stdout);
+                    std::fprintf(stderr, "saln: %s\n", saln_last_error());
+                    saln_context_destroy(ctx);
+                    return 1;
+                }
+                saln_nw_text_get(t, 0, &txt, &len, &blocks, &status, nullptr, &ns);
+            } else {
+                saln_nw_text_get(t, k, &txt, &len, &blocks, &status, nullptr, &ns);
+            }
             if (status == SALN_NOT_IMPLEMENTED) {  // main.rs:68-74
                 std::fprintf(stderr,
                              "An error occured during alignment of %s and %s\nError in alignment: "

@@ -12,6 +12,7 @@
 #include <cstring>
 #include <mutex>
 #include <new>
+#include <numeric>
 #include <string>
 #include <thread>
 #include <vector>
@@ -172,15 +173,53 @@ struct saln_nw_text {
     std::vector<int32_t> status;
     std::vector<saln_nw_result> res;
     uint64_t count = 0;  // pairs rendered
+    uint64_t gpu_decided = 0;  // of them rendered from the GPU's walk alone (no host DFS)
 };
 
 extern "C" {
 
 // The pair loop main.rs:61-74 with the text n_w_align prints
 // (needleman_wunsch_affine.rs:281-286, :390-411) for every pair, computed
-// once: one full-code plan for the batch (fill + first walk on the GPU), one
-// download of the part of the mask the rendered pairs need, then the
-// reference DFS per pair on host threads.
+// once: one full-code plan for the batch (fill + first walk on the GPU).  The
+// GPU also decides what the reference DFS meets after each pair's first
+// printed alignment (plan_next_event).  A pair whose text that decides - no
+// block (the first event is the panic, or nothing), exactly one block, or
+// under max_blocks = 1 the first block followed by a second block (the cap)
+// or a panic - is rendered from its CIGAR: no parent codes cross PCIe for it
+// and no host DFS runs.  The other pairs (more co-optimal alignments than the
+// cap allows to skip, sentinel-rooted subtrees) run the reference DFS on host
+// threads over their parent codes, downloaded for those pairs only.
+namespace {
+
+// One block of reference text from a first printed alignment (CIGAR words,
+// forward): TraceBackInfo Display, needleman_wunsch_affine.rs:390-411.
+void block_from_cigar(const uint8_t *q, const uint8_t *d, const uint32_t *w, uint32_t n,
+                      std::string *out) {
+    std::string a, bars, c;
+    uint64_t i = 0, j = 0;  // db, query positions
+    for (uint32_t k = 0; k < n; ++k) {
+        const uint32_t len = w[k] >> 4, op = w[k] & 15u;
+        for (uint32_t x = 0; x < len; ++x) {
+            const char qc = op == SALN_CIGAR_D ? '-' : (char)q[j];
+            const char dc = op == SALN_CIGAR_I ? '-' : (char)d[i];
+            a.push_back(qc);
+            c.push_back(dc);
+            bars.push_back(qc == dc ? '|' : ' ');
+            j += op != SALN_CIGAR_D;
+            i += op != SALN_CIGAR_I;
+        }
+    }
+    out->append("alignment found\n\nseq1: ");
+    out->append(a);
+    out->append("\n      ");
+    out->append(bars);
+    out->append("\nseq2: ");
+    out->append(c);
+    out->push_back('\n');
+}
+
+}  // namespace
+
 int saln_nw_render_batch(saln_context *ctx, const uint8_t *q_seq, const uint64_t *q_off,
                          uint64_t n_q, const uint8_t *db_seq, const uint64_t *db_off,
                          uint64_t n_db, const uint32_t *pair_q, const uint32_t *pair_db,
@@ -212,35 +251,62 @@ int saln_nw_render_batch(saln_context *ctx, const uint8_t *q_seq, const uint64_t
         return rc;
     }
     StageClock clock(ctx->opts.effective());
+    auto fail = [&](hipError_t e, const char *what) {
+        set_error(std::string(what) + ": " + hipGetErrorString(e));
+        delete t;
+        return SALN_E_HIP;
+    };
+    std::vector<uint64_t> coff(n_pairs + 1), doff(n_pairs + 1, 0);
+    std::vector<uint32_t> hcig;    // every pair's first alignment, packed (doff)
+    std::vector<uint8_t> next(n_pairs, kNextHost);
     {
-        DevBuf dq(ctx), dd(ctx), dr(ctx);
+        DevBuf dq(ctx), dd(ctx), dr(ctx), dc(ctx), dnx(ctx), dso(ctx), ddo(ctx), dcd(ctx);
         const uint64_t qbytes = q_off[n_q], dbytes = db_off[n_db];
-        auto fail = [&](hipError_t e, const char *what) {
-            set_error(std::string(what) + ": " + hipGetErrorString(e));
-            delete t;
-            return SALN_E_HIP;
-        };
+        saln_nw_cigar_offsets(g.p, coff.data());
         hipError_t e;
         if ((e = dq.alloc(qbytes)) != hipSuccess || (e = dd.alloc(dbytes)) != hipSuccess ||
-            (e = dr.alloc(n_pairs * sizeof(saln_nw_result))) != hipSuccess)
+            (e = dr.alloc(n_pairs * sizeof(saln_nw_result))) != hipSuccess ||
+            (e = dc.alloc(std::max<uint64_t>(1, coff[n_pairs]) * 4)) != hipSuccess ||
+            (e = dnx.alloc(std::max<uint64_t>(1, n_pairs))) != hipSuccess)
             return fail(e, "render batch: device buffers");
         if ((qbytes && (e = hipMemcpy(dq.p, q_seq, qbytes, hipMemcpyHostToDevice)) != hipSuccess) ||
             (dbytes && (e = hipMemcpy(dd.p, db_seq, dbytes, hipMemcpyHostToDevice)) != hipSuccess))
             return fail(e, "render batch: upload");
         clock.mark("render: plan + upload");
         rc = saln_nw_execute(g.p, (const uint8_t *)dq.p, (const uint8_t *)dd.p,
-                             (saln_nw_result *)dr.p, nullptr, nullptr);
-        if (rc == SALN_OK && (e = hipDeviceSynchronize()) != hipSuccess) return fail(e, "execute");
+                             (saln_nw_result *)dr.p, (uint32_t *)dc.p, ctx->stream);
+        if (rc == SALN_OK)
+            rc = plan_next_event(g.p, (const saln_nw_result *)dr.p, (uint8_t *)dnx.p, ctx->stream);
+        if (rc == SALN_OK && (e = hipStreamSynchronize(ctx->stream)) != hipSuccess)
+            return fail(e, "execute");
         clock.mark("render: execute");
         if (rc == SALN_OK) rc = plan_check_error(g.p);
         if (rc != SALN_OK) {
             delete t;
             return rc;
         }
-        if (n_pairs && (e = hipMemcpy(t->res.data(), dr.p, n_pairs * sizeof(saln_nw_result),
-                                      hipMemcpyDeviceToHost)) != hipSuccess)
+        if (n_pairs && ((e = hipMemcpy(t->res.data(), dr.p, n_pairs * sizeof(saln_nw_result),
+                                       hipMemcpyDeviceToHost)) != hipSuccess ||
+                        (e = hipMemcpy(next.data(), dnx.p, n_pairs, hipMemcpyDeviceToHost)) != hipSuccess))
             return fail(e, "render batch: results");
+        // first alignments: packed densely on the device, one download
+        for (uint64_t k = 0; k < n_pairs; ++k) doff[k + 1] = doff[k] + t->res[k].cigar_len;
+        hcig.resize(doff[n_pairs]);
+        if (doff[n_pairs]) {
+            if ((e = dso.alloc((n_pairs + 1) * 8)) != hipSuccess ||
+                (e = ddo.alloc((n_pairs + 1) * 8)) != hipSuccess ||
+                (e = dcd.alloc(doff[n_pairs] * 4)) != hipSuccess ||
+                (e = hipMemcpy(dso.p, coff.data(), (n_pairs + 1) * 8, hipMemcpyHostToDevice)) != hipSuccess ||
+                (e = hipMemcpy(ddo.p, doff.data(), (n_pairs + 1) * 8, hipMemcpyHostToDevice)) != hipSuccess ||
+                (e = launch_cigar_compact((const saln_nw_result *)dr.p, (const uint64_t *)dso.p,
+                                          (const uint64_t *)ddo.p, (const uint32_t *)dc.p,
+                                          (uint32_t *)dcd.p, n_pairs, ctx->stream)) != hipSuccess ||
+                (e = hipStreamSynchronize(ctx->stream)) != hipSuccess ||
+                (e = hipMemcpy(hcig.data(), dcd.p, doff[n_pairs] * 4, hipMemcpyDeviceToHost)) != hipSuccess)
+                return fail(e, "render batch: alignments");
+        }
     }
+    clock.mark("render: results");
     // with stop_at_panic, pairs after the first panicking one are never
     // rendered: the reference aborts there (exit 101)
     uint64_t n = n_pairs;
@@ -250,94 +316,138 @@ int saln_nw_render_batch(saln_context *ctx, const uint8_t *q_seq, const uint64_t
                 n = k + 1;
                 break;
             }
-    // The pairs' mask bytes stream into the context's host buffer in slices
-    // (one thread issuing the copies) while the DFS threads render the pairs
-    // in the order their bytes arrive: the download and the host work overlap.
-    const uint8_t *d_mask = nullptr;
-    if ((rc = plan_mask_source(g.p, &d_mask)) != SALN_OK) {
-        delete t;
-        return rc;
-    }
-    std::vector<uint64_t> order(n), endb(n);
-    uint64_t total = 0;
-    for (uint64_t k = 0; k < n; ++k) {
-        order[k] = k;
-        endb[k] = plan_mask_end(g.p, k);
-        total = std::max(total, endb[k]);
-    }
-    std::sort(order.begin(), order.end(), [&](uint64_t x, uint64_t y) { return endb[x] < endb[y]; });
-    std::lock_guard<std::mutex> lk(ctx->staging_mu);
-    if (total > ctx->host_mask.n) {
-        std::free(ctx->host_mask.p);
-        ctx->host_mask.p = nullptr;
-        ctx->host_mask.n = 0;
-        constexpr size_t kHuge = size_t(2) << 20;
-        const size_t want = (total + kHuge - 1) / kHuge * kHuge;
-        void *hp = nullptr;
-        if (posix_memalign(&hp, kHuge, want) != 0 || !hp) {
-            set_error("render batch: host mask buffer allocation failed");
-            delete t;
-            return SALN_E_HIP;
-        }
-        (void)madvise(hp, want, MADV_HUGEPAGE);  // advisory: 4 KB pages if THP is off
-        ctx->host_mask.p = (uint8_t *)hp;
-        ctx->host_mask.n = want;
-    }
-    uint8_t *host = ctx->host_mask.p;
-    clock.mark("render: results");
     const double dev_ns =
         (double)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0)
             .count();
-    constexpr uint64_t kSlice = 32ull << 20;
-    std::atomic<uint64_t> have{0};
-    std::atomic<int> dl_err{0};
-    std::thread dl([&] {
-        hipError_t e = hipSetDevice(ctx->device);
-        for (uint64_t off = 0; e == hipSuccess && off < total; off += kSlice) {
-            const uint64_t len = std::min(kSlice, total - off);
-            e = hipMemcpy(host + off, d_mask + off, len, hipMemcpyDeviceToHost);
-            if (e == hipSuccess) have.store(off + len, std::memory_order_release);
+    // the GPU-decided pairs; the rest go to the host DFS
+    std::vector<uint64_t> host;
+    for (uint64_t k = 0; k < n; ++k) {
+        const saln_nw_result &r = t->res[k];
+        const uint64_t qi = pair_q ? pair_q[k] : k % n_q, di = pair_db ? pair_db[k] : k / n_q;
+        if (!r.printed) {  // the first DFS event is the panic, or every end state is dead
+            t->status[k] = r.status == SALN_REF_PANIC_BOUNDARY ? SALN_REF_PANIC_BOUNDARY : SALN_OK;
+            continue;
         }
-        if (e != hipSuccess) dl_err.store((int)e, std::memory_order_release);  // (errors are per thread)
-    });
-    // per-pair DFS on host threads (its cost varies by orders of magnitude
-    // with the number of co-optimal paths: pairs are handed out one by one)
-    std::atomic<uint64_t> next{0};
-    auto work = [&]() {
-        for (;;) {
-            const uint64_t i = next.fetch_add(1);
-            if (i >= n) return;
-            const uint64_t k = order[i];
-            while (have.load(std::memory_order_acquire) < endb[k]) {
-                if (dl_err.load(std::memory_order_acquire)) return;
-                std::this_thread::yield();
+        const uint8_t nx = next[k];
+        const bool one = nx == kNextNone;
+        const bool capped = max_blocks == 1 && (nx == kNextBlock || nx == kNextPanic);
+        if (!one && !capped) {
+            host.push_back(k);
+            continue;
+        }
+        const auto a = std::chrono::steady_clock::now();
+        block_from_cigar(q_seq + q_off[qi], db_seq + db_off[di], hcig.data() + doff[k],
+                         r.cigar_len, &t->text[k]);
+        t->blocks[k] = 1;
+        t->status[k] = one ? SALN_OK : nx == kNextBlock ? SALN_ENUM_CAP : SALN_REF_PANIC_BOUNDARY;
+        t->ns[k] = (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+                       std::chrono::steady_clock::now() - a).count();
+    }
+    clock.mark("render: gpu-decided");
+    if (!host.empty()) {
+        // their parent codes: the workspace prefix the last of them needs,
+        // streamed in slices while the DFS threads render the pairs in the
+        // order their bytes arrive (the download and the host work overlap)
+        const uint8_t *d_mask = nullptr;
+        if ((rc = plan_mask_source(g.p, &d_mask)) != SALN_OK) {
+            delete t;
+            return rc;
+        }
+        const uint64_t nh = host.size();
+        std::vector<uint64_t> endb(nh);
+        uint64_t total = 0;
+        for (uint64_t x = 0; x < nh; ++x) {
+            endb[x] = plan_mask_end(g.p, host[x]);
+            total = std::max(total, endb[x]);
+        }
+        std::vector<uint64_t> order(nh);
+        std::iota(order.begin(), order.end(), 0);
+        std::sort(order.begin(), order.end(), [&](uint64_t x, uint64_t y) { return endb[x] < endb[y]; });
+        // the context's host buffer is taken out under staging_mu and handed
+        // back after the DFS, so the lock is not held while the pairs render
+        saln_context::HostBuf hb;
+        {
+            std::lock_guard<std::mutex> lk(ctx->staging_mu);
+            std::swap(hb.p, ctx->host_mask.p);
+            std::swap(hb.n, ctx->host_mask.n);
+        }
+        auto give_back = [&]() {
+            std::lock_guard<std::mutex> lk(ctx->staging_mu);
+            if (hb.n > ctx->host_mask.n) {
+                std::swap(hb.p, ctx->host_mask.p);
+                std::swap(hb.n, ctx->host_mask.n);
             }
-            const auto a = std::chrono::steady_clock::now();
-            const uint64_t qi = pair_q ? pair_q[k] : k % n_q, di = pair_db ? pair_db[k] : k / n_q;
-            const HostMask hm = plan_host_mask(g.p, host, k);
-            const DfsOutcome o = render_blocks(hm, q_seq + q_off[qi], db_seq + db_off[di],
-                                               max_blocks, &t->text[k]);
-            t->blocks[k] = o.blocks;
-            t->status[k] = o.status;
-            t->ns[k] = (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
-                           std::chrono::steady_clock::now() - a).count();
+        };  // (hb frees whichever buffer it holds last)
+        if (total > hb.n) {
+            std::free(hb.p);
+            hb.p = nullptr;
+            hb.n = 0;
+            constexpr size_t kHuge = size_t(2) << 20;
+            const size_t want = (total + kHuge - 1) / kHuge * kHuge;
+            void *hp = nullptr;
+            if (posix_memalign(&hp, kHuge, want) != 0 || !hp) {
+                set_error("render batch: host mask buffer allocation failed");
+                delete t;
+                return SALN_E_HIP;
+            }
+            (void)madvise(hp, want, MADV_HUGEPAGE);  // advisory: 4 KB pages if THP is off
+            hb.p = (uint8_t *)hp;
+            hb.n = want;
         }
-    };
-    const uint64_t nt = std::min<uint64_t>(std::max(1u, std::min(16u, std::thread::hardware_concurrency())),
-                                           n / 64 + 1);
-    std::vector<std::thread> th;
-    for (uint64_t i = 1; i < nt; ++i) th.emplace_back(work);
-    work();
-    for (auto &x : th) x.join();
-    dl.join();
-    if (const int e = dl_err.load()) {
-        set_error(std::string("render batch: mask download: ") + hipGetErrorString((hipError_t)e));
-        delete t;
-        return SALN_E_HIP;
+        uint8_t *hbuf = hb.p;
+        constexpr uint64_t kSlice = 32ull << 20;
+        std::atomic<uint64_t> have{0};
+        std::atomic<int> dl_err{0};
+        std::thread dl([&] {
+            hipError_t e = hipSetDevice(ctx->device);
+            for (uint64_t off = 0; e == hipSuccess && off < total; off += kSlice) {
+                const uint64_t len = std::min(kSlice, total - off);
+                e = hipMemcpy(hbuf + off, d_mask + off, len, hipMemcpyDeviceToHost);
+                if (e == hipSuccess) have.store(off + len, std::memory_order_release);
+            }
+            if (e != hipSuccess) dl_err.store((int)e, std::memory_order_release);  // (errors are per thread)
+        });
+        // per-pair DFS on host threads (its cost varies by orders of magnitude
+        // with the number of co-optimal paths: pairs are handed out one by one)
+        std::atomic<uint64_t> nxt{0};
+        auto work = [&]() {
+            for (;;) {
+                const uint64_t x = nxt.fetch_add(1);
+                if (x >= nh) return;
+                const uint64_t k = host[order[x]];
+                while (have.load(std::memory_order_acquire) < endb[order[x]]) {
+                    if (dl_err.load(std::memory_order_acquire)) return;
+                    std::this_thread::yield();
+                }
+                const auto a = std::chrono::steady_clock::now();
+                const uint64_t qi = pair_q ? pair_q[k] : k % n_q, di = pair_db ? pair_db[k] : k / n_q;
+                const HostMask hm = plan_host_mask(g.p, hbuf, k);
+                const DfsOutcome o = render_blocks(hm, q_seq + q_off[qi], db_seq + db_off[di],
+                                                   max_blocks, &t->text[k]);
+                t->blocks[k] = o.blocks;
+                t->status[k] = o.status;
+                t->ns[k] = (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+                               std::chrono::steady_clock::now() - a).count();
+            }
+        };
+        const uint64_t nt = std::min<uint64_t>(std::max(1u, std::min(16u, std::thread::hardware_concurrency())),
+                                               nh / 64 + 1);
+        std::vector<std::thread> th;
+        for (uint64_t i = 1; i < nt; ++i) th.emplace_back(work);
+        work();
+        for (auto &x : th) x.join();
+        dl.join();
+        give_back();
+        if (const int e = dl_err.load()) {
+            set_error(std::string("render batch: mask download: ") + hipGetErrorString((hipError_t)e));
+            delete t;
+            return SALN_E_HIP;
+        }
     }
     clock.mark("render: masks + dfs");
-    // each pair's share of the batch's device work, added to its own DFS time
+    // each pair's share of the batch's device work, added to its own host time
     for (uint64_t k = 0; k < n; ++k) t->ns[k] += (uint64_t)(dev_ns / (double)std::max<uint64_t>(1, n_pairs));
+    t->gpu_decided = n - host.size();
     t->count = n;
     *out = t;
     return SALN_OK;
@@ -352,6 +462,7 @@ int saln_nw_render_text(saln_context *ctx, const uint8_t *q, uint64_t len_q, con
 }
 
 uint64_t saln_nw_text_count(const saln_nw_text *t) { return t ? t->count : 0; }
+uint64_t saln_nw_text_gpu_decided(const saln_nw_text *t) { return t ? t->gpu_decided : 0; }
 
 int saln_nw_text_get(const saln_nw_text *t, uint64_t pair, const char **text, uint64_t *len,
                      uint64_t *n_blocks, int32_t *status, saln_nw_result *result,

@@ -852,6 +852,20 @@ int plan_pair_mask(const saln_nw_plan *p, uint64_t pair_id, PairMask *pm) {
     return SALN_OK;
 }
 
+int plan_next_event(saln_nw_plan *p, const saln_nw_result *d_results, uint8_t *d_next,
+                    hipStream_t stream) {
+    if (!p || !d_results || !d_next) return SALN_E_INVALID;
+    if (!p->full_codes) {
+        set_error("plan_next_event: plan stores walk codes only");
+        return SALN_E_INVALID;
+    }
+    if (!p->n_pairs) return SALN_OK;
+    HIP_TRY(hipSetDevice(p->ctx->device));
+    HIP_TRY(launch_next_event(p->d_pairs, (uint32_t)p->n_pairs, p->d_mask, d_results, p->sc,
+                              d_next, stream));
+    return SALN_OK;
+}
+
 int plan_mask_source(const saln_nw_plan *p, const uint8_t **d_mask) {
     if (!p || !d_mask) return SALN_E_INVALID;
     if (!p->full_codes) {

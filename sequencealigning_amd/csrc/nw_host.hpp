@@ -113,6 +113,11 @@ hipError_t launch_fill_stripes(const NwPairDesc *pairs, const uint2 *work, uint3
                                int layout /* 0 skewed, 1 packed, 2 row-major tiles */,
                                int rows_k /* layout 2: columns per lane */, hipStream_t stream,
                                const Options &o);
+// render batches: the reference DFS's event after each pair's first printed
+// alignment (full-code plans; next[pair_id]: 0 none, 1 block, 2 panic, 3 host)
+hipError_t launch_next_event(const NwPairDesc *pairs, uint32_t n, const uint8_t *mask,
+                             const saln_nw_result *results, Scoring sc, uint8_t *next,
+                             hipStream_t stream);
 hipError_t launch_cigar_compact(const saln_nw_result *res, const uint64_t *src_off,
                                 const uint64_t *dst_off, const uint32_t *src, uint32_t *dst,
                                 uint64_t n, hipStream_t stream);
@@ -253,6 +258,13 @@ int plan_check_error(saln_nw_plan *plan);
 int plan_create(saln_context *ctx, const uint64_t *q_off, uint64_t n_q, const uint64_t *db_off,
                 uint64_t n_db, const uint32_t *pair_q, const uint32_t *pair_db, uint64_t n_pairs,
                 int32_t mode, const saln_nw_scoring *scoring, bool full_codes, saln_nw_plan **out);
+
+// Render batches: the reference DFS's event after each pair's first printed
+// alignment, for every pair of a full-code plan after its execute
+// (nw_next_event_kernel; d_next[results index]: kNext* of nw_kernels.hip).
+int plan_next_event(saln_nw_plan *plan, const saln_nw_result *d_results, uint8_t *d_next,
+                    hipStream_t stream);
+enum { kNextNone = 0, kNextBlock = 1, kNextPanic = 2, kNextHost = 3 };
 
 // Copies one pair's parent codes from a plan's workspace after execute
 // (compact: bs = LB); pair_id is the results index.

@@ -356,7 +356,9 @@ __device__ void walk_pack_lds(const NwPairDesc &p, int32_t hend, const uint8_t *
     uint32_t *const ops = ops_all + p.ops_off;
     // block b's segment at row 1, relative to m
     auto boff = [&](uint32_t b) __attribute__((always_inline)) {
-        return (uint64_t)(b / G) * cs + (uint64_t)((b % G) * bs);
+        // (4-bit codes: queries of <= G * K columns, one chunk, b < G)
+        if constexpr (kNib) return (uint64_t)(b * bs);
+        else return (uint64_t)(b / G) * cs + (uint64_t)((b % G) * bs);
     };
     uint64_t acc = 0;        // pending 3-bit ops (state | eq << 2), oldest lowest
     uint32_t sh = 0, wi = 0; // acc's bit count; op words stored
@@ -770,6 +772,98 @@ __global__ __launch_bounds__(256) void nw_traceback_kernel(
     const Geom geo = gt.g[p.variant];
     walk_pair(p, p.len_q && p.len_db ? end_h[idx] : hs_boundary_end(sc, p.len_q, p.len_db), qs,
               ds, mask, geo, results, cigar, sc);
+}
+
+// ------------------------------------------------ render batches: next event
+// What the reference DFS (needleman_wunsch_affine.rs:281-329) meets after the
+// first printed alignment, decided on the GPU from a full-code plan's parent
+// sets (saln_nw_render_batch: a pair whose text this decides is rendered from
+// its CIGAR, with no mask download and no host DFS).  The DFS stack holds,
+// when the first path reaches the origin, the parents each node of that path
+// did not take (pushed in the order M, I, D / extend, open and popped in
+// reverse) and, at the bottom, the tied end states after the first (:247-280);
+// the next pop is the not-taken parent of the deepest node that has one.  In a
+// sentinel-free pair every node reaches a terminal (the origin or a panic
+// node), so the next event is the first terminal of the greedy walk from that
+// parent: the origin = a second block, a panic node = the panic.  Codes:
+// 0 none (exactly one block), 1 a second block, 2 a panic after the first
+// block, 3 not decided here (sentinel-rooted subtrees: the host DFS decides).
+// Pairs with nothing printed need no next event (0).
+__global__ __launch_bounds__(256) void nw_next_event_kernel(
+    const NwPairDesc *__restrict__ pairs, uint32_t n, const uint8_t *__restrict__ mask,
+    const saln_nw_result *__restrict__ results, Scoring sc, GeomTable gt,
+    uint8_t *__restrict__ next) {
+    const uint32_t idx = blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= n) return;
+    const NwPairDesc p = pairs[idx];
+    const saln_nw_result r = results[p.pair_id];
+    uint8_t out = kNextNone;
+    if (r.printed && p.len_q && p.len_db) {
+        if (!sentinel_free(sc, p.len_q, p.len_db)) {
+            out = kNextHost;
+        } else {
+            const MaskCell mc{mask + p.mask_off, gt.g[p.variant], p.mask_rs, p.mask_bs, p.mask_cs, sc};
+            int st = first_end_state(r.end_states);
+            const uint32_t rest = end_states_after(r.end_states, st);
+            int ast = rest ? first_end_state(rest) : -1;  // the next pop: an end state ...
+            uint32_t ai = p.len_db, aj = p.len_q;
+            uint32_t i = p.len_db, j = p.len_q;
+            // ... unless a node of the first path left a parent (the deepest wins)
+            for (uint32_t guard = 0; !(i == 0 && j == 0) && guard <= p.len_q + p.len_db; ++guard) {
+                int ps[3];
+                uint32_t pi[3], pj[3];
+                int np = 0;
+                auto push = [&](int s2, uint32_t i2, uint32_t j2) {
+                    ps[np] = s2;
+                    pi[np] = i2;
+                    pj[np] = j2;
+                    ++np;
+                };
+                if (i == 0 || j == 0) break;  // (a printed first path meets no other boundary cell)
+                if (st == kStM) {
+                    const uint8_t a = mc.argmax(i - 1, j - 1);
+                    if (a & kArgM) push(kStM, i - 1, j - 1);
+                    if (a & kArgI) push(kStI, i - 1, j - 1);
+                    if (a & kArgD) push(kStD, i - 1, j - 1);
+                } else if (st == kStI) {
+                    const uint8_t b = mc.ibits(i, j);
+                    if (b & 1) push(kStI, i, j - 1);
+                    if (b & 2) push(kStM, i, j - 1);
+                } else {
+                    const uint8_t b = mc.dbits(i, j);
+                    if (b & 1) push(kStD, i - 1, j);
+                    if (b & 2) push(kStM, i - 1, j);
+                }
+                if (np == 0) break;
+                if (np >= 2) {
+                    ast = ps[np - 2];
+                    ai = pi[np - 2];
+                    aj = pj[np - 2];
+                }
+                st = ps[np - 1];
+                i = pi[np - 1];
+                j = pj[np - 1];
+            }
+            if (!(i == 0 && j == 0 && st == kStM)) {
+                out = kNextHost;  // (not the printed path: leave it to the host DFS)
+            } else if (ast >= 0) {
+                const WalkOut w = walk_greedy(mc, ast, ai, aj, nullptr, nullptr, nullptr);
+                out = w.ev == kEvOrigin ? kNextBlock : w.ev == kEvPanic ? kNextPanic : kNextHost;
+            }
+        }
+    }
+    next[p.pair_id] = out;
+}
+
+hipError_t launch_next_event(const NwPairDesc *pairs, uint32_t n, const uint8_t *mask,
+                             const saln_nw_result *results, Scoring sc, uint8_t *next,
+                             hipStream_t stream) {
+    if (!n) return hipSuccess;
+    GeomTable gt;
+    for (int v = 0; v < kNumVariants; ++v) gt.g[v] = variant_geom(v);
+    nw_next_event_kernel<<<dim3((n + 255) / 256), dim3(256), 0, stream>>>(pairs, n, mask, results,
+                                                                       sc, gt, next);
+    return hipGetLastError();
 }
 
 // ------------------------------------------- long pairs: cooperative walker
@@ -2276,7 +2370,7 @@ __global__ __launch_bounds__(64) void nw_fill_rows_kernel(
     const uint8_t *__restrict__ qs, const uint8_t *__restrict__ ds, uint8_t *__restrict__ mask,
     int2 *__restrict__ scratch, uint32_t *__restrict__ err, int32_t *__restrict__ end_h,
     Scoring sc, uint32_t n_waves, uint32_t xcd_run) {
-    static_assert(K == 1 || K == 2 || K == 4, "4 cells per code word");
+    static_assert(K == 1 || K == 2, "4 cells per code word (K = 4, 256-column stripes: slower, round 2)");
     constexpr int S = 4 / K;   // stripes per 256-column chunk (work item)
     constexpr int W = 64 * K;  // stripe width (4 / K rows per code word)
     if constexpr (kPlace != kPlaceShared) asm volatile("" : : : "a255");
@@ -2434,9 +2528,7 @@ __global__ __launch_bounds__(64) void nw_fill_rows_kernel(
         if constexpr (kCodesHere) {
             const uint32_t wv = stripe_code_word<kCodes, decltype(m_c)::value, false>(sg);
             uint8_t *a = mrow + (uint64_t)(r0 - 1) * 256;
-            if constexpr (K == 4) {
-                *reinterpret_cast<uint32_t *>(a) = wv;
-            } else if constexpr (K == 2) {
+            if constexpr (K == 2) {
                 *reinterpret_cast<uint16_t *>(a) = (uint16_t)wv;
                 if (n > 1) *reinterpret_cast<uint16_t *>(a + 256) = (uint16_t)(wv >> 16);
             } else {
@@ -2551,12 +2643,7 @@ __global__ __launch_bounds__(64) void nw_fill_rows_kernel(
             dcur = dnxt;
             dnidx = min(dnidx + 1, last_dw);
             dnxt = dw[dnidx];
-            if constexpr (K == 4) {
-                row(r, (w & 0xFFu) << 8, bh[o], bi[o], u0, q0, m_c, nofill, VB, PL); put(r, 1, m_c);
-                row(r + 1, ((w >> 8) & 0xFFu) << 8, bh[o + 1], bi[o + 1], u0, q1, m_c, nofill, VB, PL); put(r + 1, 1, m_c);
-                row(r + 2, ((w >> 16) & 0xFFu) << 8, bh[o + 2], bi[o + 2], u0, q2, m_c, nofill, VB, PL); put(r + 2, 1, m_c);
-                row(r + 3, (w >> 24) << 8, bh[o + 3], bi[o + 3], u0, q3, m_c, nofill, VB, PL); put(r + 3, 1, m_c);
-            } else if constexpr (K == 2) {
+            if constexpr (K == 2) {
                 // rows r, r+1's code word is built inside row r+2's prefix chain
                 row(r, (w & 0xFFu) << 8, bh[o], bi[o], u0, q0, m_c, fill0, VB, PL);
                 row(r + 1, ((w >> 8) & 0xFFu) << 8, bh[o + 1], bi[o + 1], u1, q1, m_c, nofill, VB, PL);
@@ -2580,11 +2667,7 @@ __global__ __launch_bounds__(64) void nw_fill_rows_kernel(
             const std::integral_constant<int, o + 2> q2;
             const uint32_t w = doff ? (dcur >> doff) | (dnxt << (32u - doff)) : dcur;
             const uint32_t n = ld - r + 1;
-            if constexpr (K == 4) {
-                row(r, (w & 0xFFu) << 8, bh[o], bi[o], u0, q0, m_c, nofill, VB, PL); put(r, 1, m_c);
-                if (n > 1) { row(r + 1, ((w >> 8) & 0xFFu) << 8, bh[o + 1], bi[o + 1], u0, q1, m_c, nofill, VB, PL); put(r + 1, 1, m_c); }
-                if (n > 2) { row(r + 2, ((w >> 16) & 0xFFu) << 8, bh[o + 2], bi[o + 2], u0, q2, m_c, nofill, VB, PL); put(r + 2, 1, m_c); }
-            } else if constexpr (K == 2) {
+            if constexpr (K == 2) {
                 row(r, (w & 0xFFu) << 8, bh[o], bi[o], u0, q0, m_c, nofill, VB, PL);
                 if (n > 1) row(r + 1, ((w >> 8) & 0xFFu) << 8, bh[o + 1], bi[o + 1], u1, q1, m_c, nofill, VB, PL);
                 put(r, min(n, 2u), m_c);
@@ -3809,8 +3892,7 @@ hipError_t launch_fill_stripes(const NwPairDesc *pairs, const uint2 *work, uint3
             }
         };
         auto by_k = [&](auto codes_c, auto minpen_c) {
-            if (rows_k == 4) go(std::integral_constant<int, 4>{}, codes_c, minpen_c);
-            else if (rows_k == 2) go(std::integral_constant<int, 2>{}, codes_c, minpen_c);
+            if (rows_k == 2) go(std::integral_constant<int, 2>{}, codes_c, minpen_c);
             else go(std::integral_constant<int, 1>{}, codes_c, minpen_c);
         };
         auto by_codes = [&](auto minpen_c) {
@@ -3871,7 +3953,7 @@ Geom variant_geom(int v) { return kVariants[v]; }
 // SIMDs, 19.5 vs 14.5 ms).  Option nw.rows_k = 1, 2 or 4 forces it (read per
 // plan).
 int stripe_rows_k(uint64_t waves_k1, const Options &o) {
-    if (const int64_t v = o[Opt::RowsK]) return v == 1 || v == 4 ? (int)v : 2;
+    if (const int64_t v = o[Opt::RowsK]) return v == 1 ? 1 : 2;
     return waves_k1 <= 1024 ? 1 : 2;
 }
 

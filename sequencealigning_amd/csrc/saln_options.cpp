@@ -14,7 +14,7 @@ namespace {
 // name, default, min, max
 const OptDesc kDesc[kNumOpts] = {
     {"nw.wide_min_pairs", 1536, 0, int64_t(1) << 40},
-    {"nw.rows_k", 0, 0, 4},
+    {"nw.rows_k", 0, 0, 2},
     {"nw.stripe_pk", -1, -1, 1},
     {"nw.spec", 1, 0, 1},
     {"nw.spec_passes", 3, 0, 16},

@@ -19,7 +19,7 @@ namespace saln {
 
 enum class Opt : int {
     WideMinPairs = 0,   // "nw.wide_min_pairs": 513-1,024-column pairs a plan needs for the 64-lane packed fill
-    RowsK,              // "nw.rows_k": row-fill columns per lane (0 auto, 1, 2, 4)
+    RowsK,              // "nw.rows_k": row-fill columns per lane (0 auto, 1, 2)
     StripePk,           // "nw.stripe_pk": packed column stripes (-1 auto, 0 off, 1 forced)
     Spec,               // "nw.spec": speculative stripe walks (1) or the sequential walker only (0)
     SpecPasses,         // "nw.spec_passes": speculative walk passes

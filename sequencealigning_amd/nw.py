@@ -118,12 +118,14 @@ def _text_get(h, k: int):
 
 
 def render_batch(queries, dbs, pairs=None, *, mode: Mode = Mode.Global, max_blocks: int = 0,
-                 stop_at_panic: bool = False, device: int = 0) -> list[tuple[str, int, int]]:
+                 stop_at_panic: bool = False, device: int = 0,
+                 stats: dict | None = None) -> list[tuple[str, int, int]]:
     """The reference's stdout per pair of a batch (saln_nw_render_batch: one
     plan, every pair computed once): [(text, blocks, status)] in pair order
     (pairs=None: all-vs-all, db outer / query inner, main.rs:61-62).  With
     stop_at_panic the list ends at the first pair whose traceback panics (the
-    reference aborts there)."""
+    reference aborts there).  stats (a dict) receives "gpu_decided": the pairs
+    rendered from the GPU's walk alone."""
     qs, qo = pack_csr(queries)
     ds, do = pack_csr(dbs)
     if pairs is None:
@@ -141,6 +143,8 @@ def render_batch(queries, dbs, pairs=None, *, mode: Mode = Mode.Global, max_bloc
                                       max_blocks, 1 if stop_at_panic else 0, C.byref(h)),
                "saln_nw_render_batch")
     try:
+        if stats is not None:
+            stats["gpu_decided"] = int(L.saln_nw_text_gpu_decided(h))
         return [_text_get(h, k)[:3] for k in range(L.saln_nw_text_count(h))]
     finally:
         L.saln_nw_text_free(h)

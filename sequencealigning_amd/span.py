@@ -464,7 +464,13 @@ class _DeviceSpanEngine:
 
     def put_inbox(self, a: int, b: int, rows: np.ndarray) -> None:
         """Inbox rows a .. b from host memory (H2D on the inbox stream, beside
-        the running fill)."""
+        the running fill).  The fill was queued first and polls these rows, so
+        the copy must not wait behind it: a pinned-host H2D copy runs on a DMA
+        engine (SDMA), not on a compute queue, so it cannot queue behind the
+        running kernel whatever hardware queue the two streams share.  Should
+        it ever be served by a blit kernel stuck behind the fill, the fill's
+        bounded polls end it with the span's wait-timeout flag, which finish()
+        turns into an error (span.check) - never a hang or a silent result."""
         import torch
         src = torch.from_numpy(np.ascontiguousarray(rows, np.int64)).pin_memory()
         with torch.cuda.stream(self.in_s):
@@ -607,7 +613,7 @@ class ShardedLongPair:
             if self.right is not None:
                 t = torch.from_numpy(np.ascontiguousarray(eng.outbox_rows(a, b), np.int64))
                 dist.send(t, dst=self.rank + 1, group=self.right)
-        eng.finish()
+        eng.finish()  # raises if a boundary wait timed out (SALN_FLAG_WAIT_TIMEOUT)
 
     def fill(self) -> None:
         if self.nccl:

@@ -24,6 +24,13 @@ def test_bench_starts_two_ranks():
     line = [l for l in r.stdout.splitlines() if l.startswith("{")][-1]
     doc = json.loads(line)
     assert doc["launch_selftest"] and doc["n_gpus"] == 2 and doc["ranks"] == [0, 1]
+    # the per-rank diagnosis the N > 1 lines carry (bench.rank_diag)
+    diag = doc["rank_diag"]
+    assert [d["rank"] for d in diag] == [0, 1]
+    for d in diag:
+        assert set(d) == {"rank", "compute_ms", "gather_ms", "gather_bytes"}
+        assert d["compute_ms"] > 0 and d["gather_ms"] > 0
+    assert diag[0]["gather_bytes"] == 2 * 4096 * 4 and diag[1]["gather_bytes"] == 4096 * 4
 
 
 def test_bench_refuses_world_mismatch():

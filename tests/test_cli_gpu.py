@@ -118,3 +118,51 @@ def test_cli_nw_batch_max_blocks_matches_oracle(tmp_path, oracle):
     want = "".join(oracle.nw(a.encode(), b.encode(), max_blocks=1, max_pops=10**8).stdout
                    for b in d for a in q)
     assert p.stdout.decode() == want
+
+
+@pytest.mark.parametrize("max_blocks", [1, 2, 0])
+def test_render_batch_gpu_decided_matches_oracle(saln, oracle, max_blocks):
+    """Render batches decide most pairs on the GPU (the first walk and the
+    DFS's next event, nw_next_event_kernel) and run the host DFS only for
+    the rest; every pair's text, block count and status equal the oracle's
+    literal DFS (stopped at max_blocks) on configs[1]-shaped i.i.d. pairs,
+    5 % mutated pairs (co-optimal gap placements), two-letter pairs (many
+    co-optimal paths), N and panicking pairs."""
+    import numpy as np
+    from nw_check import rand_seq
+
+    from sequencealigning_amd import synth
+    rng = np.random.default_rng(303 + max_blocks)
+    qs, ds = [], []
+    for k in range(120):
+        q = rand_seq(rng, int(rng.integers(100, 160)))
+        kind = k % 4
+        if kind == 0:
+            d = rand_seq(rng, int(rng.integers(100, 160)))
+        elif kind == 1:
+            d = synth.mutate(q, 0.05, seed=k)
+        elif kind == 2:
+            q = bytes(rng.choice([65, 67], len(q)).astype(np.uint8))
+            d = bytes(rng.choice([65, 67], int(rng.integers(90, 150))).astype(np.uint8))
+        else:
+            d = synth.mutate(q, 0.1, seed=k)[:int(rng.integers(60, 140))]
+        qs.append(q)
+        ds.append(d)
+    qs += [b"TA", b"NNACGTN", b"AAA", b""]
+    ds += [b"A", b"ACGGT", b"AA", b""]
+    n = len(qs)
+    st = {}
+    out = saln.render_batch(qs, ds, pairs=[(k, k) for k in range(n)], max_blocks=max_blocks,
+                            stats=st)
+    assert len(out) == n
+    for k in range(n):
+        o = oracle.nw(qs[k], ds[k], max_blocks=max_blocks, max_pops=10**8)
+        text, blocks, status = out[k]
+        assert o.dfs_rc in (0, 1, 3), (k, o.dfs_rc)
+        assert text == o.stdout, k
+        assert blocks == o.dfs_blocks, k
+        want = {0: saln._lib.OK, 1: saln._lib.REF_PANIC_BOUNDARY, 3: saln._lib.ENUM_CAP}[o.dfs_rc]
+        assert status == want, (k, status, o.dfs_rc)
+    # the GPU settles every sentinel-free pair under max_blocks = 1, and the
+    # pairs with one co-optimal alignment (or none printed) otherwise
+    assert st["gpu_decided"] >= (n - 8 if max_blocks == 1 else 1), st

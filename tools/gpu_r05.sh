@@ -37,7 +37,7 @@ for st in ${STAGES:-smoke tests bench}; do
       done ;;
     abfuse)
       for i in ${REPS:-1 2}; do
-        for f in 1 0; do
+        for f in ${FUSE:-1 0}; do
           for pl in "" "--pipeline"; do
             tag=fuse${f}${pl:+_pipe}_$i
             step $tag 180 python tools/ab_c2.py --tag $tag --opt nw.fuse_walk=$f $pl
