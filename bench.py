@@ -62,7 +62,7 @@ VALU_PEAK_TOPS = 1024 * 32 * 2.4e9 / 1e12  # 78.6 T lane-ops/s
 VALU_PK_TOPS = 1024 * 16 * 2.4e9 / 1e12
 N_PAIRS, LQ, LD = 100_000, 150, 150
 SEED = 0x5EED0002
-ALL_LEGS = ("c5", "c1", "c3", "c3_affine", "c4", "c4_spans", "host", "cli")
+ALL_LEGS = ("c5", "c1", "c3", "c3_affine", "c4", "c4_spans", "host", "cli", "cli_all")
 PMC_FILES = ("pmc_traffic.json", "pmc_legs.json")  # under profiles/
 
 
@@ -760,33 +760,50 @@ def leg_host(saln):
             "ms": round(dt * 1e3, 2)}
 
 
-def leg_cli(saln, n: int = 316, cpu: bool = True, max_blocks: int = 1) -> dict:
+def leg_cli(saln, n: int = 316, cpu: bool = True, max_blocks: int = 1, gmut: bool = False) -> dict:
     """The drop-in CLI end to end (`saln -q Q.fa -d D.fa -a needleman-wunsch`,
-    main.rs:19-80): n x n FASTA records of 150 bp G-iid (seed 0x5EED0002;
-    ~configs[1]'s 10^5 pairs), every pair computed once in render batches
-    (saln_nw_render_batch), each pair's reference text printed
-    (--max-blocks 1: the first block, so the stdout stays bounded; --no-abort:
-    every pair, where the reference would stop at the first panic;
-    --no-timing: no nondeterministic lines).  Wall time of the process,
-    FASTA parse and context creation included.  The first n pairs of stdout
-    are checked against the oracle's literal DFS text; the CPU baseline is
-    the oracle's fill + DFS (same block cap) on a sample of the pairs."""
+    main.rs:19-80) on n x n FASTA records of 150 bp, every pair computed once
+    in render batches (saln_nw_render_batch), each pair's reference text
+    printed; --no-abort: every pair, where the reference would stop at the
+    first panic; --no-timing: no nondeterministic lines.
+    - default (`cli`): G-iid records (seed 0x5EED0002; ~configs[1]'s 10^5
+      pairs), --max-blocks 1 (the first block, so the stdout stays bounded);
+    - gmut (`cli_all`): every record a G-mut(5 %) copy of one 150 bp base, so
+      each pair is ~10 % divergent with a few to thousands of co-optimal
+      alignments, and the reference's default output: every block
+      (max_blocks 0), the host DFS over the GPU's parent codes.
+    Wall time of the process, FASTA parse and context creation included.  The
+    first n pairs of stdout are checked against the oracle's literal DFS text;
+    the CPU baseline is the oracle's fill + DFS (same block cap) over every
+    pair of the file."""
     import subprocess
     import tempfile
 
     from sequencealigning_amd import synth
     cli = os.path.join(ROOT, "sequencealigning_amd", "saln")
-    qs, qo, ds, do = synth.iid_pairs(n, LQ, LD, seed=SEED)
-    q = [qs[int(qo[k]):int(qo[k + 1])].tobytes() for k in range(n)]
-    d = [ds[int(do[k]):int(do[k + 1])].tobytes() for k in range(n)]
+    if gmut:
+        rng = np.random.default_rng(SEED)
+        base = bytes(rng.choice(np.frombuffer(b"ACGT", np.uint8), LQ))
+        q = [synth.mutate(base, 0.05, seed=SEED + k) for k in range(n)]
+        d = [synth.mutate(base, 0.05, seed=SEED + n + k) for k in range(n)]
+        qs, ds = np.frombuffer(b"".join(q), np.uint8), np.frombuffer(b"".join(d), np.uint8)
+        qo = np.concatenate([[0], np.cumsum([len(x) for x in q])]).astype(np.uint64)
+        do = np.concatenate([[0], np.cumsum([len(x) for x in d])]).astype(np.uint64)
+        kind = f"G-mut(5 %) copies of one {LQ} bp base"
+    else:
+        qs, qo, ds, do = synth.iid_pairs(n, LQ, LD, seed=SEED)
+        q = [qs[int(qo[k]):int(qo[k + 1])].tobytes() for k in range(n)]
+        d = [ds[int(do[k]):int(do[k + 1])].tobytes() for k in range(n)]
+        kind = f"{LQ} bp G-iid"
     with tempfile.TemporaryDirectory() as tdir:
         qf, df, of = (os.path.join(tdir, x) for x in ("q.fa", "d.fa", "out.txt"))
         for path, recs, tag in ((qf, q, "q"), (df, d, "d")):
             with open(path, "wb") as fh:
                 for k, r in enumerate(recs):
                     fh.write(b">%s%d\n%s\n" % (tag.encode(), k, r))
-        cmd = [cli, "-q", qf, "-d", df, "-a", "needleman-wunsch", "--no-timing", "--no-abort",
-               "--max-blocks", str(max_blocks)]
+        cmd = [cli, "-q", qf, "-d", df, "-a", "needleman-wunsch", "--no-timing", "--no-abort"]
+        if max_blocks:
+            cmd += ["--max-blocks", str(max_blocks)]
         walls = []
         for _ in range(2):  # the first run also pages in the library
             with open(of, "wb") as out:
@@ -796,7 +813,7 @@ def leg_cli(saln, n: int = 316, cpu: bool = True, max_blocks: int = 1) -> dict:
             if r.returncode != 0:
                 raise RuntimeError(f"saln exited {r.returncode}: {r.stderr[-500:]!r}")
         with open(of, "rb") as fh:
-            head = fh.read(4 << 20).decode("latin-1")
+            head = fh.read(64 << 20).decode("latin-1")
         out_bytes = os.path.getsize(of)
         # one more run for its stage breakdown (stderr; not the timed value)
         with open(of, "wb") as out:
@@ -805,12 +822,13 @@ def leg_cli(saln, n: int = 316, cpu: bool = True, max_blocks: int = 1) -> dict:
         stages = [ln.split("]", 1)[1].strip() for ln in r.stderr.decode("latin-1").splitlines()
                   if ln.startswith("[saln ")]
     from oracle import refcpu  # untimed checker / cpu baseline only
-    want = "".join(refcpu.nw(a, d[0], max_blocks=max_blocks, max_pops=CPU_MAX_POPS).stdout
-                   for a in q)
-    cells = n * n * LQ * LD
-    res = {"workload": f"saln CLI (-a needleman-wunsch --no-timing --no-abort --max-blocks "
-                       f"{max_blocks}) on {n} x {n} FASTA records of 150 bp G-iid "
-                       f"({n * n} pairs, seed {SEED:#x})",
+    want = "".join(refcpu.nw(a, d[0], max_blocks=max_blocks, max_pops=CPU_MAX_POPS,
+                             out_cap=1 << 26).stdout for a in q)
+    lq, ld = np.diff(qo).astype(np.int64), np.diff(do).astype(np.int64)
+    cells = int(lq.sum() * ld.sum())
+    flags = "--no-timing --no-abort" + (f" --max-blocks {max_blocks}" if max_blocks else "")
+    res = {"workload": f"saln CLI (-a needleman-wunsch {flags}) on {n} x {n} FASTA records, "
+                       f"{kind} ({n * n} pairs, seed {SEED:#x})",
            "value": round(cells / walls[-1] / 1e9, 2), "unit": "GCUPS (process wall time)",
            "stages_ms": stages,
            "wall_s": round(walls[-1], 3), "wall_s_first": round(walls[0], 3),
@@ -820,21 +838,22 @@ def leg_cli(saln, n: int = 316, cpu: bool = True, max_blocks: int = 1) -> dict:
                                    "query (untimed)"}}
     if cpu:
         T = cpu_threads()
-        qb, db_ = qs.tobytes(), ds.tobytes()
         # every pair of the file (db outer, query inner), on T threads
         m = n * n
         qi, di = np.arange(m) % n, np.arange(m) // n
         sq = b"".join(q[i] for i in qi)
         sd = b"".join(d[j] for j in di)
-        off = np.arange(m + 1, dtype=np.uint64) * LQ
+        qoff = np.concatenate([[0], np.cumsum(lq[qi])]).astype(np.uint64)
+        doff = np.concatenate([[0], np.cumsum(ld[di])]).astype(np.uint64)
         t0 = time.perf_counter()
-        c, capped = refcpu.run_pairs_capped(sq, off, sd, off, m, max_pops=CPU_MAX_POPS,
+        c, capped = refcpu.run_pairs_capped(sq, qoff, sd, doff, m, max_pops=CPU_MAX_POPS,
                                             threads=T, max_blocks=max_blocks)
         dt = time.perf_counter() - t0
         res["cpu_baseline"] = {"value": round(c / dt / 1e9, 5), "unit": "GCUPS", "cores": T,
                                "kind": "port", "capped_pairs": int(capped),
                                "sample": f"all {m} pairs of the file, oracle/refcpu.c fill + "
-                                         f"literal DFS stopped before block {max_blocks + 1} "
+                                         f"literal DFS "
+                                         f"{'stopped before block %d' % (max_blocks + 1) if max_blocks else 'over every block'} "
                                          f"(<= {CPU_MAX_POPS:.0e} pops) on {T} threads, "
                                          f"{dt:.2f} s; in-process, no text formatting, no "
                                          f"output, no process start (the CLI's value "
@@ -1114,6 +1133,8 @@ def main() -> None:
                 r = leg_host(saln)
             elif leg == "cli":
                 r = leg_cli(saln, cpu=cpu)
+            elif leg == "cli_all":
+                r = leg_cli(saln, n=100, cpu=cpu, max_blocks=0, gmut=True)
             else:
                 raise ValueError(f"unknown leg {leg}")
         except Exception as e:  # a failing extra leg must not hide the headline line

@@ -20,7 +20,10 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
+
+#include <unistd.h>
 
 #include "saln.h"
 
@@ -253,19 +256,37 @@ int main(int argc, char **argv) {
         t_mark = n;
     };
     if (a.stage_times) saln_option_set("host.timing", 1);
-    std::vector<Rec> db, query;
-    if (!load(a.db, "DB", &db)) return 0;
-    if (!load(a.query, "Query", &query)) return 0;
-    mark("load fasta");
+    // stdout to a file or pipe: large writes (the default 4 KB buffer makes
+    // ~10^4 write calls per 45 MB of text); a terminal keeps line buffering
+    // (stderr too: --max-blocks prints a line per capped pair)
+    if (!isatty(STDOUT_FILENO)) std::setvbuf(stdout, nullptr, _IOFBF, 4u << 20);
+    if (!isatty(STDERR_FILENO)) std::setvbuf(stderr, nullptr, _IOFBF, 1u << 20);
     if (a.algo == 0) {
+        std::vector<Rec> db, query;  // the reference parses both files first
+        if (!load(a.db, "DB", &db) || !load(a.query, "Query", &query)) return 0;
         std::fprintf(stderr,
                      "saln: -a a-star (the reference's A* aligner) is not part of this engine; "
                      "use -a needleman-wunsch or -a wfa\n");
         return 2;
     }
+    // the HIP runtime starts (~0.2 s) while the FASTA files are read
     saln_context *ctx = nullptr;
-    if (saln_context_create(a.device, &ctx) != SALN_OK) {
-        std::fprintf(stderr, "saln: %s\n", saln_last_error());
+    int ctx_rc = SALN_OK;
+    std::string ctx_err;  // (saln_last_error is per thread)
+    std::thread ctx_thread([&] {
+        ctx_rc = saln_context_create(a.device, &ctx);
+        if (ctx_rc != SALN_OK) ctx_err = saln_last_error();
+    });
+    std::vector<Rec> db, query;
+    const bool loaded = load(a.db, "DB", &db) && load(a.query, "Query", &query);
+    mark("load fasta");
+    ctx_thread.join();
+    if (!loaded) {
+        if (ctx) saln_context_destroy(ctx);
+        return 0;
+    }
+    if (ctx_rc != SALN_OK) {
+        std::fprintf(stderr, "saln: %s\n", ctx_err.c_str());
         return 1;
     }
     mark("context");
@@ -362,9 +383,70 @@ int main(int argc, char **argv) {
     // Needleman-Wunsch: each chunk is one saln_nw_render_batch (one plan,
     // fill + walk on the GPU).  A chunk holds up to kChunkPairs pairs or
     // ~kChunkCells cells (its full-code mask and the host copy of it stay
-    // bounded).
+    // bounded).  A chunk's text is printed on a thread while the next chunk
+    // renders, unless the chunk ends the run (a panic under the reference's
+    // abort), which is printed before anything else happens.
     constexpr uint64_t kChunkPairs = 1u << 16;
     constexpr uint64_t kChunkCells = 2ull << 30;
+    // pair k of a rendered chunk: its text and what the reference does next;
+    // returns the process exit code when the run ends here, else -1
+    auto print_pair = [&](const Rec &q, const Rec &d, const char *txt, uint64_t len,
+                          int32_t status, uint64_t ns) -> int {
+        if (status == SALN_NOT_IMPLEMENTED) {  // main.rs:68-74
+            std::fprintf(stderr,
+                         "An error occured during alignment of %s and %s\nError in alignment: "
+                         "not implemented\n",
+                         as_str(q.name).c_str(), as_str(d.name).c_str());
+            return -1;
+        }
+        std::fwrite(txt, 1, len, stdout);
+        if (status == SALN_REF_PANIC_BOUNDARY) {
+            std::fflush(stdout);
+            if (a.abort_on_panic) {
+                std::fprintf(stderr,
+                             "thread 'main' panicked at src/needleman_wunsch_affine.rs: index "
+                             "out of bounds (traceback reached a boundary cell other than the "
+                             "origin)\nnote: run with `RUST_BACKTRACE=1` environment variable "
+                             "to display a backtrace\n");
+                return 101;
+            }
+            std::fprintf(stderr, "saln: reference panic (REF_PANIC_BOUNDARY) for %s vs %s\n",
+                         as_str(q.name).c_str(), as_str(d.name).c_str());
+            return -1;
+        }
+        if (status == SALN_ENUM_CAP)
+            std::fprintf(stderr, "saln: enumeration capped at %llu blocks for %s vs %s\n",
+                         (unsigned long long)a.max_blocks, as_str(q.name).c_str(),
+                         as_str(d.name).c_str());
+        if (a.timing) std::printf("%s\n", duration_debug(ns).c_str());
+        return -1;
+    };
+    auto print_chunk = [&](saln_nw_text *t, const std::vector<uint32_t> &cq,
+                           const std::vector<uint32_t> &cd) -> int {
+        const uint64_t n = saln_nw_text_count(t);
+        for (uint64_t k = 0; k < n; ++k) {
+            const char *txt = nullptr;
+            uint64_t len = 0, blocks = 0, ns = 0;
+            int32_t status = SALN_OK;
+            saln_nw_text_get(t, k, &txt, &len, &blocks, &status, nullptr, &ns);
+            const int e = print_pair(query[cq[k]], db[cd[k]], txt, len, status, ns);
+            if (e >= 0) return e;
+        }
+        return -1;
+    };
+    std::thread printer;
+    double print_ms = 0;  // the printer thread's time for its chunk
+    auto join_printer = [&]() {
+        if (!printer.joinable()) return;
+        printer.join();
+        if (a.stage_times) std::fprintf(stderr, "[saln cli] %-16s %8.3f ms\n", "print (beside)", print_ms);
+    };
+    auto finish = [&](int code) {
+        join_printer();
+        std::fflush(stdout);
+        if (code != 0) saln_context_destroy(ctx);
+        return code;
+    };
     for (uint64_t p0 = 0; p0 < total;) {
         pq.clear();
         pd.clear();
@@ -377,72 +459,62 @@ int main(int argc, char **argv) {
             pq.push_back((uint32_t)qi);
             pd.push_back((uint32_t)di);
         }
+        p0 += pq.size();
         saln_nw_text *t = nullptr;
         mark("chunk plan");
-        int rc = saln_nw_render_batch(ctx, qs.data(), qo.data(), nq, ds.data(), dof.data(), nd,
-                                      pq.data(), pd.data(), pq.size(), a.mode, a.max_blocks,
-                                      a.abort_on_panic ? 1 : 0, &t);
+        const int rc = saln_nw_render_batch(ctx, qs.data(), qo.data(), nq, ds.data(), dof.data(), nd,
+                                            pq.data(), pd.data(), pq.size(), a.mode, a.max_blocks,
+                                            a.abort_on_panic ? 1 : 0, &t);
         mark("render batch");
-        // a chunk that fails as a whole (one pair whose scores leave the
-        // engine's int32 range, an allocation) is rendered pair by pair, so
-        // every pair before the failing one is printed first, in the
-        // reference's streaming order (main.rs:61-74)
-        const bool per_pair = rc != SALN_OK;
-        const uint64_t n = per_pair ? pq.size() : saln_nw_text_count(t);
-        for (uint64_t k = 0; k < n; ++k) {
-            const Rec &q = query[pq[k]], &d = db[pd[k]];
-            const char *txt = nullptr;
-            uint64_t len = 0, blocks = 0, ns = 0;
-            int32_t status = SALN_OK;
-            if (per_pair) {
-                if (t) saln_nw_text_free(t);
-                t = nullptr;
-                rc = saln_nw_render_text(ctx, q.seq.data(), q.seq.size(), d.seq.data(),
-                                         d.seq.size(), a.mode, a.max_blocks, &t);
-                if (rc != SALN_OK) {
+        join_printer();  // the previous chunk's text comes first
+        if (rc != SALN_OK) {
+            // a chunk that fails as a whole (one pair whose scores leave the
+            // engine's int32 range, an allocation) is rendered pair by pair,
+            // so every pair before the failing one is printed first, in the
+            // reference's streaming order (main.rs:61-74)
+            if (t) saln_nw_text_free(t);
+            for (uint64_t k = 0; k < pq.size(); ++k) {
+                const Rec &q = query[pq[k]], &d = db[pd[k]];
+                saln_nw_text *one = nullptr;
+                if (saln_nw_render_text(ctx, q.seq.data(), q.seq.size(), d.seq.data(), d.seq.size(),
+                                        a.mode, a.max_blocks, &one) != SALN_OK) {
                     std::fflush(stdout);
                     std::fprintf(stderr, "saln: %s\n", saln_last_error());
-                    saln_context_destroy(ctx);
-                    return 1;
+                    return finish(1);
                 }
-                saln_nw_text_get(t, 0, &txt, &len, &blocks, &status, nullptr, &ns);
-            } else {
-                saln_nw_text_get(t, k, &txt, &len, &blocks, &status, nullptr, &ns);
+                const char *txt = nullptr;
+                uint64_t len = 0, blocks = 0, ns = 0;
+                int32_t status = SALN_OK;
+                saln_nw_text_get(one, 0, &txt, &len, &blocks, &status, nullptr, &ns);
+                const int e = print_pair(q, d, txt, len, status, ns);
+                saln_nw_text_free(one);
+                if (e >= 0) return finish(e);
             }
-            if (status == SALN_NOT_IMPLEMENTED) {  // main.rs:68-74
-                std::fprintf(stderr,
-                             "An error occured during alignment of %s and %s\nError in alignment: "
-                             "not implemented\n",
-                             as_str(q.name).c_str(), as_str(d.name).c_str());
-                continue;
-            }
-            std::fwrite(txt, 1, len, stdout);
-            if (status == SALN_REF_PANIC_BOUNDARY) {
-                std::fflush(stdout);
-                if (a.abort_on_panic) {
-                    std::fprintf(stderr,
-                                 "thread 'main' panicked at src/needleman_wunsch_affine.rs: index "
-                                 "out of bounds (traceback reached a boundary cell other than the "
-                                 "origin)\nnote: run with `RUST_BACKTRACE=1` environment variable "
-                                 "to display a backtrace\n");
-                    saln_nw_text_free(t);
-                    saln_context_destroy(ctx);
-                    return 101;
-                }
-                std::fprintf(stderr, "saln: reference panic (REF_PANIC_BOUNDARY) for %s vs %s\n",
-                             as_str(q.name).c_str(), as_str(d.name).c_str());
-                continue;
-            }
-            if (status == SALN_ENUM_CAP)
-                std::fprintf(stderr, "saln: enumeration capped at %llu blocks for %s vs %s\n",
-                             (unsigned long long)a.max_blocks, as_str(q.name).c_str(),
-                             as_str(d.name).c_str());
-            if (a.timing) std::printf("%s\n", duration_debug(ns).c_str());
+            mark("print");
+            continue;
         }
-        mark("print");
-        saln_nw_text_free(t);
-        p0 += pq.size();
+        bool ends = false;  // a panic the reference aborts at
+        if (a.abort_on_panic)
+            for (uint64_t k = 0, n = saln_nw_text_count(t); k < n && !ends; ++k) {
+                int32_t status = SALN_OK;
+                saln_nw_text_get(t, k, nullptr, nullptr, nullptr, &status, nullptr, nullptr);
+                ends = status == SALN_REF_PANIC_BOUNDARY;
+            }
+        if (ends || p0 >= total) {  // the last chunk: nothing to overlap
+            const int e = print_chunk(t, pq, pd);
+            saln_nw_text_free(t);
+            mark("print");
+            if (e >= 0) return finish(e);
+            continue;
+        }
+        printer = std::thread([&, t, cq = pq, cd = pd]() {
+            const auto s0 = std::chrono::steady_clock::now();
+            print_chunk(t, cq, cd);  // (no exit code: the chunk has no abort)
+            saln_nw_text_free(t);
+            print_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - s0).count();
+        });
     }
+    join_printer();
     // The context is left to the process exit: destroying it frees the GB-sized
     // device and host blocks one by one (measured 0.26 s at the end of a 10^5-pair
     // run), which the exit's teardown does anyway.

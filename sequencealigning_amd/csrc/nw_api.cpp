@@ -10,6 +10,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <mutex>
 #include <new>
 #include <numeric>
@@ -168,7 +169,13 @@ static int run_batch(saln_context *ctx, const uint8_t *q_seq, const uint64_t *q_
 
 // Rendered reference text of a batch (saln_nw_render_batch).
 struct saln_nw_text {
-    std::vector<std::string> text;
+    std::vector<std::string> text;  // the host-DFS pairs' text
+    // the GPU-decided pairs' text, back to back in pair order: pair k's at
+    // arena + aoff[k] (aoff[k] == kNoArena: in text[k])
+    static constexpr uint64_t kNoArena = ~0ull;
+    char *arena = nullptr;
+    std::vector<uint64_t> aoff, alen;
+    ~saln_nw_text() { std::free(arena); }
     std::vector<uint64_t> blocks, ns;
     std::vector<int32_t> status;
     std::vector<saln_nw_result> res;
@@ -193,29 +200,73 @@ namespace {
 
 // One block of reference text from a first printed alignment (CIGAR words,
 // forward): TraceBackInfo Display, needleman_wunsch_affine.rs:390-411.
+constexpr char kBlockHead[] = "alignment found\n\nseq1: ", kBlockMid[] = "\n      ",
+               kBlockTail[] = "\nseq2: ";
+constexpr uint64_t kBlockFixed = sizeof(kBlockHead) + sizeof(kBlockMid) + sizeof(kBlockTail) - 2;
+
+// the alignment's length (columns) from its CIGAR words
+uint64_t cigar_columns(const uint32_t *w, uint32_t n) {
+    uint64_t L = 0;
+    for (uint32_t k = 0; k < n; ++k) L += w[k] >> 4;
+    return L;
+}
+
+// One block of reference text from a first printed alignment of L columns
+// (CIGAR words, forward) into out[0, kBlockFixed + 3 L): TraceBackInfo
+// Display, needleman_wunsch_affine.rs:390-411.
 void block_from_cigar(const uint8_t *q, const uint8_t *d, const uint32_t *w, uint32_t n,
-                      std::string *out) {
-    std::string a, bars, c;
-    uint64_t i = 0, j = 0;  // db, query positions
+                      uint64_t L, char *out) {
+    constexpr size_t nh = sizeof(kBlockHead) - 1, nm = sizeof(kBlockMid) - 1,
+                     nt = sizeof(kBlockTail) - 1;
+    char *a = out;
+    std::memcpy(a, kBlockHead, nh);
+    a += nh;
+    char *bars = a + L + nm, *c = bars + L + nt;
+    std::memcpy(a + L, kBlockMid, nm);
+    std::memcpy(bars + L, kBlockTail, nt);
+    c[L] = '\n';
+    uint64_t i = 0, j = 0, x = 0;  // db, query, column positions
     for (uint32_t k = 0; k < n; ++k) {
         const uint32_t len = w[k] >> 4, op = w[k] & 15u;
-        for (uint32_t x = 0; x < len; ++x) {
-            const char qc = op == SALN_CIGAR_D ? '-' : (char)q[j];
-            const char dc = op == SALN_CIGAR_I ? '-' : (char)d[i];
-            a.push_back(qc);
-            c.push_back(dc);
-            bars.push_back(qc == dc ? '|' : ' ');
-            j += op != SALN_CIGAR_D;
-            i += op != SALN_CIGAR_I;
+        // (a bar wherever the two printed chars are equal, a '-' byte in a
+        // sequence against a gap included, as the reference's Display does)
+        if (op == SALN_CIGAR_I) {  // query chars against gaps
+            std::memcpy(a + x, q + j, len);
+            std::memset(c + x, '-', len);
+            for (uint32_t y = 0; y < len; ++y) bars[x + y] = q[j + y] == '-' ? '|' : ' ';
+            j += len;
+        } else if (op == SALN_CIGAR_D) {
+            std::memset(a + x, '-', len);
+            std::memcpy(c + x, d + i, len);
+            for (uint32_t y = 0; y < len; ++y) bars[x + y] = d[i + y] == '-' ? '|' : ' ';
+            i += len;
+        } else {
+            std::memcpy(a + x, q + j, len);
+            std::memcpy(c + x, d + i, len);
+            for (uint32_t y = 0; y < len; ++y) bars[x + y] = q[j + y] == d[i + y] ? '|' : ' ';
+            i += len;
+            j += len;
         }
+        x += len;
     }
-    out->append("alignment found\n\nseq1: ");
-    out->append(a);
-    out->append("\n      ");
-    out->append(bars);
-    out->append("\nseq2: ");
-    out->append(c);
-    out->push_back('\n');
+}
+
+// work items [0, n) on up to 16 host threads, handed out in blocks of `grain`
+void host_parallel(uint64_t n, uint64_t grain, const std::function<void(uint64_t)> &f) {
+    const uint64_t nt = std::min<uint64_t>(std::max(1u, std::min(16u, std::thread::hardware_concurrency())),
+                                           n / grain + 1);
+    std::atomic<uint64_t> next{0};
+    auto work = [&]() {
+        for (;;) {
+            const uint64_t b = next.fetch_add(grain);
+            if (b >= n) return;
+            for (uint64_t k = b; k < std::min(n, b + grain); ++k) f(k);
+        }
+    };
+    std::vector<std::thread> th;
+    for (uint64_t i = 1; i < nt; ++i) th.emplace_back(work);
+    work();
+    for (auto &x : th) x.join();
 }
 
 }  // namespace
@@ -319,11 +370,11 @@ int saln_nw_render_batch(saln_context *ctx, const uint8_t *q_seq, const uint64_t
     const double dev_ns =
         (double)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0)
             .count();
-    // the GPU-decided pairs; the rest go to the host DFS
-    std::vector<uint64_t> host;
+    // the GPU-decided pairs (rendered from their CIGARs on host threads); the
+    // rest go to the host DFS
+    std::vector<uint64_t> host, dec;
     for (uint64_t k = 0; k < n; ++k) {
         const saln_nw_result &r = t->res[k];
-        const uint64_t qi = pair_q ? pair_q[k] : k % n_q, di = pair_db ? pair_db[k] : k / n_q;
         if (!r.printed) {  // the first DFS event is the panic, or every end state is dead
             t->status[k] = r.status == SALN_REF_PANIC_BOUNDARY ? SALN_REF_PANIC_BOUNDARY : SALN_OK;
             continue;
@@ -335,14 +386,48 @@ int saln_nw_render_batch(saln_context *ctx, const uint8_t *q_seq, const uint64_t
             host.push_back(k);
             continue;
         }
-        const auto a = std::chrono::steady_clock::now();
-        block_from_cigar(q_seq + q_off[qi], db_seq + db_off[di], hcig.data() + doff[k],
-                         r.cigar_len, &t->text[k]);
         t->blocks[k] = 1;
         t->status[k] = one ? SALN_OK : nx == kNextBlock ? SALN_ENUM_CAP : SALN_REF_PANIC_BOUNDARY;
+        dec.push_back(k);
+    }
+    // their text sizes, offsets in the arena, then the text, on host threads
+    // (one arena: ~0.5 KB per configs[1] pair without an allocation each)
+    const uint64_t nd = dec.size();
+    t->aoff.assign(n_pairs, saln_nw_text::kNoArena);
+    t->alen.assign(n_pairs, 0);
+    std::vector<uint64_t> cols(nd);
+    host_parallel(nd, 1024, [&](uint64_t x) {
+        const uint64_t k = dec[x];
+        cols[x] = cigar_columns(hcig.data() + doff[k], t->res[k].cigar_len);
+    });
+    uint64_t asz = 0;
+    for (uint64_t x = 0; x < nd; ++x) {
+        const uint64_t k = dec[x];
+        t->aoff[k] = asz;
+        t->alen[k] = kBlockFixed + 3 * cols[x];
+        asz += t->alen[k];
+    }
+    if (asz) {
+        constexpr size_t kHuge = size_t(2) << 20;
+        const size_t want = (asz + kHuge - 1) / kHuge * kHuge;
+        void *hp = nullptr;
+        if (posix_memalign(&hp, kHuge, want) != 0 || !hp) {
+            set_error("render batch: text buffer allocation failed");
+            delete t;
+            return SALN_E_HIP;
+        }
+        (void)madvise(hp, want, MADV_HUGEPAGE);  // advisory: fewer first-touch faults
+        t->arena = (char *)hp;
+    }
+    host_parallel(nd, 256, [&](uint64_t x) {
+        const uint64_t k = dec[x];
+        const auto a = std::chrono::steady_clock::now();
+        const uint64_t qi = pair_q ? pair_q[k] : k % n_q, di = pair_db ? pair_db[k] : k / n_q;
+        block_from_cigar(q_seq + q_off[qi], db_seq + db_off[di], hcig.data() + doff[k],
+                         t->res[k].cigar_len, cols[x], t->arena + t->aoff[k]);
         t->ns[k] = (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
                        std::chrono::steady_clock::now() - a).count();
-    }
+    });
     clock.mark("render: gpu-decided");
     if (!host.empty()) {
         // their parent codes: the workspace prefix the last of them needs,
@@ -468,8 +553,9 @@ int saln_nw_text_get(const saln_nw_text *t, uint64_t pair, const char **text, ui
                      uint64_t *n_blocks, int32_t *status, saln_nw_result *result,
                      uint64_t *elapsed_ns) {
     if (!t || pair >= t->count) return SALN_E_INVALID;
-    if (text) *text = t->text[pair].data();
-    if (len) *len = t->text[pair].size();
+    const bool ar = !t->aoff.empty() && t->aoff[pair] != saln_nw_text::kNoArena;
+    if (text) *text = ar ? t->arena + t->aoff[pair] : t->text[pair].data();
+    if (len) *len = ar ? t->alen[pair] : t->text[pair].size();
     if (n_blocks) *n_blocks = t->blocks[pair];
     if (status) *status = t->status[pair];
     if (result) *result = t->res[pair];

@@ -92,21 +92,10 @@ struct saln_nw_plan {
     uint32_t *d_ops = nullptr;  // traceback op-stream scratch of workspace 0
     uint32_t *d_ops2 = nullptr;  // ... of workspace 1 (async: its walks may overlap workspace 0's)
     uint64_t ops_words = 0;
-    // per workspace: the table fills' bail word (16 bytes), then the fused
-    // fill + walk's per-pack arrival words (8 bytes) and walk-left flags of
-    // the 8 x 19 variant (nw_fill_walk_kernel); zeroed once, self-clearing
-    uint8_t *d_fuse[2] = {nullptr, nullptr};
-    uint32_t fuse_packs = 0;
+    // per workspace: the table fills' bail word (zeroed once; a table launch
+    // whose waves left pairs to its fallback launch stores its epoch there)
+    uint32_t *d_bail[2] = {nullptr, nullptr};
     uint32_t epoch = 0;  // table launches of this plan (the bail word's values)
-    bool fused[kNumVariants] = {};  // the last execute's fill walked the variant itself
-    uint64_t fuse_bytes() const { return 16 + (uint64_t)fuse_packs * 12; }
-    uint32_t *bail(int b) const { return reinterpret_cast<uint32_t *>(d_fuse[b]); }
-    unsigned long long *arrive(int b) const {
-        return reinterpret_cast<unsigned long long *>(d_fuse[b] + 16);
-    }
-    uint32_t *walk_left(int b) const {
-        return reinterpret_cast<uint32_t *>(d_fuse[b] + 16 + (uint64_t)fuse_packs * 8);
-    }
     // speculative stripe walks (a few long column-stripe pairs): block map,
     // pairs, stripe records, run words, per-pair done flags (plan order)
     uint32_t spec_pairs = 0, spec_blocks = 0;
@@ -184,7 +173,7 @@ int saln_nw_plan_destroy(saln_nw_plan *p) {
     (void)hipDeviceSynchronize();  // the blocks go back to the context cache
     for (void *b : {(void *)p->d_pairs, (void *)p->d_mask, (void *)p->d_mask2, (void *)p->d_endh2,
                     (void *)p->d_scratch, (void *)p->d_work, (void *)p->d_prog, (void *)p->d_err,
-                    (void *)p->d_ops, (void *)p->d_ops2, (void *)p->d_fuse[0], (void *)p->d_fuse[1],
+                    (void *)p->d_ops, (void *)p->d_ops2, (void *)p->d_bail[0], (void *)p->d_bail[1],
                     (void *)p->d_endh, (void *)p->d_spec_blocks,
                     (void *)p->d_spec_pairs, (void *)p->d_spec_stripes, (void *)p->d_spec_ops,
                     (void *)p->d_spec_done})
@@ -464,9 +453,19 @@ int saln::plan_create(saln_context *ctx, const uint64_t *q_off, uint64_t n_q,
     if (n_pairs) {
         if ((e = dev_alloc(p->ctx, (void **)&p->d_pairs, n_pairs * sizeof(NwPairDesc))) != hipSuccess)
             return fail(e, "hipMalloc(pairs)");
-        if ((e = hipMemcpy(p->d_pairs, p->h_pairs.data(), n_pairs * sizeof(NwPairDesc),
-                           hipMemcpyHostToDevice)) != hipSuccess)
-            return fail(e, "hipMemcpy(pairs)");
+        clk.mark("plan: pairs alloc");
+        // through the context's pinned staging: a pageable copy of a freshly
+        // built array pins its pages first (measured 12-17 ms for the 2.7-5.2
+        // MB of a render chunk's descriptors, against ~1 ms of memcpy here)
+        {
+            std::lock_guard<std::mutex> lk(p->ctx->staging_mu);
+            void *st = nullptr;
+            const size_t nb = n_pairs * sizeof(NwPairDesc);
+            if ((e = pinned_staging(p->ctx, nb, &st)) != hipSuccess) return fail(e, "pinned staging");
+            std::memcpy(st, p->h_pairs.data(), nb);
+            if ((e = hipMemcpy(p->d_pairs, st, nb, hipMemcpyHostToDevice)) != hipSuccess)
+                return fail(e, "hipMemcpy(pairs)");
+        }
         if ((e = dev_alloc(p->ctx, (void **)&p->d_endh, n_pairs * sizeof(int32_t))) != hipSuccess)
             return fail(e, "hipMalloc(end)");
     }
@@ -509,12 +508,10 @@ int saln::plan_create(saln_context *ctx, const uint64_t *q_off, uint64_t n_q,
     p->ops_words = ooff;
     if (ooff && (e = dev_alloc(p->ctx, (void **)&p->d_ops, ooff * sizeof(uint32_t))) != hipSuccess)
         return fail(e, "hipMalloc(op stream)");
-    if (p->nib[kNarrowVariant] && p->var_count[kNarrowVariant])
-        p->fuse_packs = n_packs(p->var_count[kNarrowVariant]);
     if ((p->var_count[kNarrowVariant] && p->nib[kNarrowVariant]) || (p->var_count[7] && p->nib[7])) {
-        if ((e = dev_alloc(p->ctx, (void **)&p->d_fuse[0], p->fuse_bytes())) != hipSuccess ||
-            (e = hipMemset(p->d_fuse[0], 0, p->fuse_bytes())) != hipSuccess)
-            return fail(e, "fused fill + walk words");
+        if ((e = dev_alloc(p->ctx, (void **)&p->d_bail[0], 16)) != hipSuccess ||
+            (e = hipMemset(p->d_bail[0], 0, 16)) != hipSuccess)
+            return fail(e, "table fill bail word");
     }
     {
         // Speculative stripe walks: a few long column-stripe pairs walk all
@@ -639,16 +636,12 @@ int saln_nw_execute(saln_nw_plan *p, const uint8_t *d_q, const uint8_t *d_db,
         ev = p->ev_pool[p->ev_used++].data();
         HIP_TRY(hipEventRecord(ev[0], s));
     }
-    // fills on `s`, then the walks on `t` (async: beside the next fill).  The
-    // 8 x 19 table fill walks its packs in the same launch (nw.fuse_walk);
-    // its walker launch then only takes the packs the fill left to it.
+    // fills on `s`, then the walks on `t` (async: beside the next fill)
     FillExtras fx;
     fx.o = &p->opts;
-    fx.bail = p->d_fuse[cur] ? p->bail(cur) : nullptr;
-    fx.ops = ops;
+    fx.bail = p->d_bail[cur];
     for (int v = 0; v < kNumVariants; ++v) {
         const uint32_t a = p->var_first[v], b = a + p->var_count[v];
-        p->fused[v] = false;
         if (a >= b) continue;
         if (v == kStripeVariant) {
             const uint32_t w0 = p->work_first[a], w1 = p->work_first[b];
@@ -659,15 +652,11 @@ int saln_nw_execute(saln_nw_plan *p, const uint8_t *d_q, const uint8_t *d_db,
                                             p->stripe_layout(), p->stripe_rows, s, p->opts));
             continue;
         }
-        const bool fuse = v == kNarrowVariant && !p->score_only && p->fuse_packs;
         fx.epoch = ++p->epoch;
-        fx.arrive = fuse ? p->arrive(cur) : nullptr;
-        fx.walk_left = fuse ? p->walk_left(cur) : nullptr;
         HIP_TRY(launch_fill(v, p->d_pairs, a, b - a, d_q, d_db, mask, p->d_scratch, endh,
                             d_results, d_cigar, p->sc,
                             p->score_only ? 2 : p->full_codes ? 1 : p->nib[v] ? 3 : 0,
                             p->var_maxld[v], s, fx));
-        p->fused[v] = fx.fused;
     }
     if (ev) HIP_TRY(hipEventRecord(ev[1], s));
     HIP_TRY(hipEventRecord(p->sync_ev[0], s));
@@ -690,8 +679,7 @@ int saln_nw_execute(saln_nw_plan *p, const uint8_t *d_q, const uint8_t *d_db,
         else
             HIP_TRY(launch_traceback(v, p->d_pairs, a, b - a, d_q, d_db, mask, endh, ops,
                                      d_results, d_cigar, p->sc, p->stripe_layout(), t,
-                                     spec ? p->d_spec_done : nullptr, p->nib[v],
-                                     p->fused[v] ? p->walk_left(cur) : nullptr));
+                                     spec ? p->d_spec_done : nullptr, p->nib[v]));
     }
     // pairs with an empty side (boundary-only walk) ride on the traceback stream
     if (p->n_pairs > p->n_fill && p->score_only)
@@ -729,9 +717,9 @@ int saln_nw_plan_set_async(saln_nw_plan *p, int enable) {
         HIP_TRY(dev_alloc(p->ctx, (void **)&p->d_endh2, p->n_pairs * sizeof(int32_t)));
         if (p->ops_words)
             HIP_TRY(dev_alloc(p->ctx, (void **)&p->d_ops2, p->ops_words * sizeof(uint32_t)));
-        if (p->d_fuse[0]) {
-            HIP_TRY(dev_alloc(p->ctx, (void **)&p->d_fuse[1], p->fuse_bytes()));
-            HIP_TRY(hipMemset(p->d_fuse[1], 0, p->fuse_bytes()));
+        if (p->d_bail[0]) {
+            HIP_TRY(dev_alloc(p->ctx, (void **)&p->d_bail[1], 16));
+            HIP_TRY(hipMemset(p->d_bail[1], 0, 16));
         }
     }
     p->async_tb = enable != 0;

@@ -86,26 +86,17 @@ hipError_t pinned_staging(saln_context *ctx, size_t n, void **p);  // caller hol
 // kernels (nw_kernels.hip)
 // What a packed fill launch needs besides the pairs: the plan's options, the
 // workspace's bail word and the launch's epoch (4-bit-code table fills: the
-// fallback launch runs only when a wave of its table launch left pairs to it),
-// and for the fused fill + walk of the 8 x 19 variant (nw_fill_walk_kernel)
-// the workspace's per-pack arrival and walk-left words and the walk outputs.
-// fused: set when the launch walked (or marked) every pair itself.
+// fallback launch runs only when a wave of its table launch left pairs to it).
 struct FillExtras {
     const Options *o = nullptr;
     uint32_t *bail = nullptr;
     uint32_t epoch = 0;
-    unsigned long long *arrive = nullptr;  // non-null: fuse the walk when the table fill runs
-    uint32_t *walk_left = nullptr;
-    uint32_t *ops = nullptr;
-    bool fused = false;
 };
 hipError_t launch_fill(int variant, const NwPairDesc *pairs, uint32_t first, uint32_t count,
                        const uint8_t *qs, const uint8_t *ds, uint8_t *mask, int2 *scratch,
                        int32_t *end_h, saln_nw_result *results, uint32_t *cigar, Scoring sc,
                        int codes /* 0 walk, 1 full, 2 none, 3 4-bit walk */, uint32_t ld_max,
-                       hipStream_t stream, FillExtras &fx);
-// mask packs (64 pairs) of a variant range: the fused kernel's per-pack words
-inline uint32_t n_packs(uint32_t count) { return (count + 63) / 64; }
+                       hipStream_t stream, const FillExtras &fx);
 hipError_t launch_fill_stripes(const NwPairDesc *pairs, const uint2 *work, uint32_t n_work,
                                const uint8_t *qs, const uint8_t *ds, uint8_t *mask,
                                int2 *scratch, uint32_t *prog, uint32_t *err, int32_t *end_h,
@@ -141,8 +132,7 @@ hipError_t launch_traceback(int variant, const NwPairDesc *pairs, uint32_t first
                             const uint8_t *ds, const uint8_t *mask, const int32_t *end_h,
                             uint32_t *ops, saln_nw_result *results, uint32_t *cigar, Scoring sc,
                             int stripe_layout, hipStream_t stream,
-                            const uint32_t *spec_done = nullptr, bool nib = false,
-                            const uint32_t *walk_left = nullptr);
+                            const uint32_t *spec_done = nullptr, bool nib = false);
 // variants whose walk codes may be 4-bit (kCodesNib): the short-query packed
 // fills 7 (16 x 10) and 4 (8 x 19, 4-bit only)
 inline bool variant_nib(int v) { return v == 7 || v == 4; }

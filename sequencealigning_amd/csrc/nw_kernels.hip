@@ -249,11 +249,8 @@ constexpr uint32_t kOpsPerWord = 10;                     // 3-bit ops per op-str
 // kNib: 4-bit walk codes (Geom::LBn-byte segments) and the pair's query
 // staged in LDS after the windows: QC 16-byte chunks per lane, [chunk][lane]
 // (the LDS-DMA order), enough for a variant of `cols` query columns at any
-// 16-byte misalignment.  kQCodes (the fused fill + walk, nw_fill_walk_kernel):
-// the query as 2-bit codes ((c >> 1) & 3; A, C, G, T only) instead, QD
-// dwords of 16 columns per lane, [dword][lane]: 2.5 KB for 152 columns
-// against 11 KB of bytes, so the fused kernel keeps three waves per SIMD.
-template <int K, bool kNib = false, uint32_t kCols = 0, bool kQCodes = false>
+// 16-byte misalignment.
+template <int K, bool kNib = false, uint32_t kCols = 0>
 struct WalkGeo {
     static constexpr uint32_t LB = kNib ? 4 * ((K + 3) / 4 / 2 + 1) : (K + 3) / 4 * 4;
     static constexpr uint32_t NW = 2;
@@ -261,14 +258,12 @@ struct WalkGeo {
     static constexpr uint32_t SB = LB == 12 ? 12 : 16;        // DMA bytes per lane
     static constexpr uint32_t kSlotBytes = 64 * 16;          // one slot of a wave
     static constexpr uint32_t kWinBytes = W * kSlotBytes;    // one window of a wave
-    static constexpr uint32_t QC = kNib && !kQCodes ? (15 + kCols + 15) / 16 : 0;
-    static constexpr uint32_t QD = kQCodes ? (kCols + 15) / 16 : 0;
-    static constexpr uint32_t kWaveLds = NW * kWinBytes + QC * kSlotBytes + QD * 256;
+    static constexpr uint32_t QC = kNib ? (15 + kCols + 15) / 16 : 0;
+    static constexpr uint32_t kWaveLds = NW * kWinBytes + QC * kSlotBytes;
     static constexpr uint32_t kVmcnt = NW * (W - 1);
     static_assert(LB <= 16, "LDS window slots hold 16 bytes per lane");
     static_assert((NW == 2 || NW == 3) && W >= 2 && W <= 8, "8 valid bits per window");
     static_assert(!kNib || kCols > 0, "4-bit walk: the variant's query width");
-    static_assert(!kQCodes || kNib, "query codes: 4-bit walk codes");
 };
 
 typedef __attribute__((address_space(3))) uint8_t lds_u8;
@@ -339,12 +334,12 @@ __device__ __forceinline__ void unroll_each(F &&f, std::integer_sequence<uint32_
 // byte's 1 / 3 / 5, so the same kNextLut decides; the end cell's state set
 // is its nibble's argI, argD and (last row) argM-in-D-open bits; '=' / 'X'
 // compare the query byte (LDS) with the row's db char in the segment.
-template <int G, int K, bool kNib = false, bool kQCodes = false>
+template <int G, int K, bool kNib = false>
 __device__ void walk_pack_lds(const NwPairDesc &p, int32_t hend, const uint8_t *__restrict__ mask,
                               uint32_t *__restrict__ ops_all, saln_nw_result *__restrict__ results,
                               uint32_t *__restrict__ cigar, Scoring sc, lds_u8 *win,
                               const uint8_t *__restrict__ qs) {
-    using WG = WalkGeo<K, kNib, G * K, kQCodes>;
+    using WG = WalkGeo<K, kNib, G * K>;
     constexpr Geom geo{G, K};
     constexpr uint32_t kW = WG::W, NW = WG::NW;
     constexpr uint32_t kWin = WG::kWinBytes, kSlot = WG::kSlotBytes;
@@ -387,30 +382,7 @@ __device__ void walk_pack_lds(const NwPairDesc &p, int32_t hend, const uint8_t *
     // every window DMA, so the counted waits below also cover them
     const uint32_t qa = (uint32_t)(p.q_off & 15u);
     lds_u8 *const qlds = win + NW * kWin;
-    if constexpr (kQCodes) {
-        // the query's bytes (dword loads from its 4-byte-aligned start; only
-        // dwords holding query bytes) as 2-bit codes, 16 columns per dword:
-        // y = the codes in bytes 0-3, y * 0x41041 gathers them into bits 18..25
-        const uint32_t qa4 = (uint32_t)(p.q_off & 3u);
-        const uint32_t *qw = reinterpret_cast<const uint32_t *>(qs + (p.q_off - qa4));
-        const uint32_t nsrc = (qa4 + p.len_q + 3u) / 4u;
-        constexpr uint32_t NS = 4 * WG::QD + 1;
-        uint32_t src[NS];
-#pragma unroll
-        for (uint32_t i = 0; i < NS; ++i) src[i] = i < nsrc ? qw[i] : 0u;
-#pragma unroll
-        for (uint32_t d = 0; d < WG::QD; ++d) {
-            uint32_t code = 0;
-#pragma unroll
-            for (uint32_t k = 0; k < 4; ++k) {
-                const uint32_t x = __builtin_amdgcn_alignbyte(src[4 * d + k + 1], src[4 * d + k], qa4);
-                const uint32_t y = (x >> 1) & 0x03030303u;
-                code |= ((y * 0x00041041u) >> 18 & 0xFFu) << (8u * k);
-            }
-            *reinterpret_cast<__attribute__((address_space(3))) uint32_t *>(
-                qlds + d * 256u + (threadIdx.x & 63u) * 4u) = code;
-        }
-    } else if constexpr (kNib) {
+    if constexpr (kNib) {
         const uint8_t *qg = qs + (p.q_off - qa);
         const uint32_t qlast = (qa + p.len_q - 1u) / 16u;
 #pragma unroll
@@ -421,15 +393,8 @@ __device__ void walk_pack_lds(const NwPairDesc &p, int32_t hend, const uint8_t *
     }
     // query column j (1-based) of this lane's pair equals the db char dch
     auto qeq = [&](uint32_t j, uint32_t dch) __attribute__((always_inline)) {
-        if constexpr (kQCodes) {
-            const uint32_t o = j - 1u;
-            const uint32_t w = *reinterpret_cast<const __attribute__((address_space(3))) uint32_t *>(
-                qlds + (o >> 4) * 256u + (threadIdx.x & 63u) * 4u);
-            return ((w >> (2u * (o & 15u))) & 3u) == ((dch >> 1) & 3u);
-        } else {
-            const uint32_t o = qa + j - 1u;
-            return (uint32_t)qlds[(o >> 4) * kSlot + (threadIdx.x & 63u) * 16u + (o & 15u)] == dch;
-        }
+        const uint32_t o = qa + j - 1u;
+        return (uint32_t)qlds[(o >> 4) * kSlot + (threadIdx.x & 63u) * 16u + (o & 15u)] == dch;
     };
     // db char byte of a 4-bit segment (Geom::nib_char_byte)
     constexpr uint32_t kNG = (K + 3) / 4, kCB = kNG % 2 ? 4 * (kNG / 2) + 2 : 4 * (kNG / 2);
@@ -729,25 +694,16 @@ __device__ void walk_pack_lds(const NwPairDesc &p, int32_t hend, const uint8_t *
 // LDS of a wave).
 template <int G, int K, bool kNib = false>
 constexpr uint32_t tb_lds_threads() { return kNib ? 128u : 256u; }
-// walk_left (fused fill + walk plans): only the packs (64 pairs, one wave)
-// whose fill launch left them here are walked; the flag is cleared for the
-// next execute.
 template <int G, int K, bool kNib>
 __global__ __launch_bounds__(256) void nw_traceback_lds_kernel(
     const NwPairDesc *__restrict__ pairs, uint32_t first, uint32_t n,
     const uint8_t *__restrict__ mask, const int32_t *__restrict__ end_h,
     uint32_t *__restrict__ ops, saln_nw_result *__restrict__ results,
-    uint32_t *__restrict__ cigar, Scoring sc, const uint8_t *__restrict__ qs,
-    uint32_t *__restrict__ walk_left) {
+    uint32_t *__restrict__ cigar, Scoring sc, const uint8_t *__restrict__ qs) {
     constexpr uint32_t kWave = WalkGeo<K, kNib, G * K>::kWaveLds;
     __shared__ __attribute__((aligned(16))) uint8_t win_all[tb_lds_threads<G, K, kNib>() / 64u * kWave];
     const uint32_t rel = blockIdx.x * blockDim.x + threadIdx.x;
     if (rel >= n) return;
-    if (walk_left) {  // (lane 0 of a wave holds the pack's first pair: rel < n)
-        const uint32_t pack = rel / 64u;
-        if (!__builtin_amdgcn_readfirstlane(walk_left[pack])) return;
-        if ((threadIdx.x & 63u) == 0) walk_left[pack] = 0;
-    }
     const uint32_t idx = first + rel;
     // The walk is a latency-bound chain that shares SIMDs with the VALU-bound
     // fill of the next batch in pipelined plans: it issues at the highest
@@ -1648,9 +1604,8 @@ __device__ __forceinline__ uint32_t hmax3(uint32_t a, uint32_t b, uint32_t c) {
 // Returns (per lane; wave-uniform over the lanes that hold pairs): 0 filled
 // (or no pair), 1 the table body left the wave's pairs to the fallback launch
 // (a byte other than A, C, G, T), 2 the fallback body found nothing to do.
-// kThreads: the workgroup's threads (256; 64 for the fused fill + walk).
 template <int G, int K, int kCodes, typename Src, int KS, bool kRebase = false, bool kProf = false,
-          int kTabMode = 0, int kThreads = 256>
+          int kTabMode = 0>
 __device__ __forceinline__ int fill_pk_body(Src src, uint32_t count, const uint8_t *__restrict__ qs,
                                             const uint8_t *__restrict__ ds,
                                             uint8_t *__restrict__ mask, Scoring sc,
@@ -1671,7 +1626,7 @@ __device__ __forceinline__ int fill_pk_body(Src src, uint32_t count, const uint8
     static_assert(!kProf || (kCodes == kCodesNone && !kRebase), "profiles: score-only, one frame");
     static_assert(!kTab || ((kCodes == kCodesNib || kCodes == kCodesNone) && !kRebase && !kProf),
                   "tables: 4-bit codes or score-only, one frame");
-    constexpr int GPB = kThreads / G;
+    constexpr int GPB = 256 / G;
     constexpr Geom geo{G, K};
     extern __shared__ uint32_t drow[];  // [GPB][G + ld_max + G] packed db chars (dch) per row
     const int lane = threadIdx.x % G;
@@ -2109,110 +2064,6 @@ __global__ __launch_bounds__(256, (pk_min_waves<G, K, kCodesNib>())) void nw_fil
     fill_pk_body<G, K, kCodesNib, Src, K, kRebaseGeneric, false, 2>(src, count, qs, ds, mask, sc,
                                                                      ld_max, true);
 }
-
-// ------------------------------------------------- fused fill + walk (C2)
-// The 8 x 19 table fill of configs[1]-shaped plans with the walk of each mask
-// pack (64 pairs) run by the pack's last finishing wave, inside the fill
-// launch (round 5).  One-wave workgroups of 16 pairs; the four of a pack sit
-// on one XCD (pack_block).  A wave that finished its fill waits for its mask
-// and end-value stores (vmcnt(0): in the XCD's L2) and adds 1 << (8 * its
-// XCC_ID) to the pack's 64-bit arrival word; the wave whose add completes the
-// count walks the pack's 64 pairs (one lane each, walk_pack_lds) if every
-// wave of the pack finished on its own XCD - the stores are then in the L2
-// its loads read (the end values with sc1 loads, which bypass this CU's L1:
-// a neighbouring pack's walk on this CU may have cached their line; the mask
-// lines of a pack are its own, 256-byte aligned) - and otherwise leaves the
-// pack to the walker launch behind (walk_left; the launch boundary makes
-// every store visible).  The last arrival also clears the word for the next
-// execute.  Packs completed by the fallback launch (a byte other than A, C,
-// G, T) are left to the walker launch as well.  No separate walker pass over
-// the mask, and no co-resident walker
-// kernel taking the fill's registers and issue slots (round 4: the fill ran
-// 0.88-0.92 ms beside it against 0.686 alone).
-struct FuseArgs {
-    const NwPairDesc *pairs;         // plan table (pairs[first + i])
-    uint32_t *bail;                  // the workspace's bail word (kMode 1 writes, 2 reads)
-    uint32_t epoch;
-    unsigned long long *arrive;      // per pack: arrivals by XCD (bytes)
-    uint32_t *walk_left;             // per pack: 1 = the walker launch walks it
-    uint32_t *ops;
-    saln_nw_result *results;
-    uint32_t *cigar;
-    uint32_t defer;                  // 1 (nw.fuse_walk = 2, tests): every pack left to the walker launch
-};
-constexpr uint32_t kFuseThreads = 64;  // one wave per workgroup
-
-constexpr int kFuseG = 8, kFuseK = 19;  // the 8 x 19 variant (4)
-template <int kMode, bool kRebaseGeneric>
-__global__ __launch_bounds__(kFuseThreads, 3) void nw_fill_walk_kernel(
-    PlanSrc src, uint32_t count, const uint8_t *__restrict__ qs, const uint8_t *__restrict__ ds,
-    uint8_t *__restrict__ mask, Scoring sc, uint32_t ld_max, FuseArgs fa) {
-    static_assert(kMode == 1 || kMode == 2, "table launch or its fallback");
-    constexpr int G = kFuseG, K = kFuseK;
-    constexpr uint32_t kPairsPerWave = 2 * kFuseThreads / G;  // 16
-    constexpr uint32_t kWavesPerPack = 64 / kPairsPerWave;    // 4
-    if constexpr (kMode == 2)
-        if (__builtin_amdgcn_readfirstlane(*fa.bail) != fa.epoch) return;
-    const int st = fill_pk_body<G, K, kCodesNib, PlanSrc, K, kMode == 2 && kRebaseGeneric, false,
-                                kMode, (int)kFuseThreads>(src, count, qs, ds, mask, sc, ld_max, true);
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t lb = pack_block(kWavesPerPack);  // the wave's 16 pairs: lb * 16 ..
-    if (lb * kPairsPerWave >= count) return;
-    if (__builtin_amdgcn_ballot_w64(st == 1)) {  // (kMode 1) left to the fallback launch
-        if (lane == 0) *fa.bail = fa.epoch;
-        return;
-    }
-    if (__builtin_amdgcn_ballot_w64(st == 2)) return;  // (kMode 2) filled by the table launch
-    asm volatile("s_waitcnt vmcnt(0)" : : : "memory");  // my mask and end stores are in L2
-    const uint32_t pack = lb / kWavesPerPack;
-    const uint32_t np = min(64u, count - 64u * pack);
-    const uint32_t nwv = (np + kPairsPerWave - 1) / kPairsPerWave;
-    const uint32_t xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20) & 7u;  // HW_REG_XCC_ID
-    const unsigned long long mine = 1ull << (8u * xcc);
-    unsigned long long old = 0;
-    if (lane == 0) old = atomicAdd(&fa.arrive[pack], mine);
-    const uint32_t olo = __builtin_amdgcn_readlane((uint32_t)old, 0);
-    const uint32_t ohi = __builtin_amdgcn_readlane((uint32_t)(old >> 32), 0);
-    const unsigned long long tot = ((unsigned long long)ohi << 32 | olo) + mine;
-    const uint32_t sum = ((uint32_t)tot & 0xFFu) + ((uint32_t)tot >> 8 & 0xFFu) +
-                         ((uint32_t)tot >> 16 & 0xFFu) + ((uint32_t)tot >> 24) +
-                         ((uint32_t)(tot >> 32) & 0xFFu) + ((uint32_t)(tot >> 40) & 0xFFu) +
-                         ((uint32_t)(tot >> 48) & 0xFFu) + (uint32_t)(tot >> 56);
-    if (sum != nwv) return;  // not the pack's last wave
-    if (lane == 0)  // (every wave of the pack has added)
-        __hip_atomic_store(&fa.arrive[pack], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    // the fallback launch's packs hold a byte other than A, C, G, T, which the
-    // walk's 2-bit query codes cannot tell from G: the walker launch takes them
-    if (kMode == 2 || fa.defer || tot != (unsigned long long)nwv << (8u * xcc)) {
-        if (lane == 0) fa.walk_left[pack] = 1u;
-        return;
-    }
-    __builtin_amdgcn_s_setprio(3);  // a latency-bound chain beside the fills of the other waves
-    asm volatile("s_waitcnt lgkmcnt(0)" : : : "memory");  // the fill's LDS reads are done
-    const uint32_t i = 64u * pack + lane;
-    if (i >= count) return;
-    const NwPairDesc p = fa.pairs[src.first + i];
-    const int32_t hend = __hip_atomic_load(src.end_h + src.first + i, __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_AGENT);
-    extern __shared__ uint32_t drow[];
-    walk_pack_lds<kFuseG, kFuseK, true, true>(p, hend, mask, fa.ops, fa.results, fa.cigar, sc,
-                                              (lds_u8 *)drow, qs);
-}
-
-// (explicit instantiations: the launches sit in a generic lambda of fill_pk,
-// and hipcc emitted no host stubs for them there)
-template __global__ void nw_fill_walk_kernel<1, false>(PlanSrc, uint32_t, const uint8_t *,
-                                                       const uint8_t *, uint8_t *, Scoring,
-                                                       uint32_t, FuseArgs);
-template __global__ void nw_fill_walk_kernel<1, true>(PlanSrc, uint32_t, const uint8_t *,
-                                                      const uint8_t *, uint8_t *, Scoring, uint32_t,
-                                                      FuseArgs);
-template __global__ void nw_fill_walk_kernel<2, false>(PlanSrc, uint32_t, const uint8_t *,
-                                                       const uint8_t *, uint8_t *, Scoring,
-                                                       uint32_t, FuseArgs);
-template __global__ void nw_fill_walk_kernel<2, true>(PlanSrc, uint32_t, const uint8_t *,
-                                                      const uint8_t *, uint8_t *, Scoring, uint32_t,
-                                                      FuseArgs);
 
 // Score-only all-vs-all of the other query classes with table penalties in
 // the extension-free frame (nw.pk_tab); *generic (nw_acgt_check_kernel earlier
@@ -3294,8 +3145,8 @@ static bool pk_free_ok(const Scoring &sc, uint32_t W, uint32_t rows) {
 template <int G, int K, int KS = K>
 static hipError_t fill_pk(dim3 grid, hipStream_t s, const NwPairDesc *pairs, uint32_t first,
                           uint32_t count, const uint8_t *qs, const uint8_t *ds, uint8_t *mask,
-                          int32_t *end_h, saln_nw_result *results, uint32_t *cigar, Scoring sc,
-                          int codes, uint32_t ld_max, bool rebase, FillExtras &fx) {
+                          int32_t *end_h, saln_nw_result *, uint32_t *, Scoring sc,
+                          int codes, uint32_t ld_max, bool rebase, const FillExtras &fx) {
     const Options &o = *fx.o;
     const size_t lds = (size_t)(256 / G) * (ld_max + 2 * G) * (rebase ? 2 : 4);
     if (lds > kPackedLdsMax) return hipErrorInvalidValue;  // choose_variant keeps ld below this
@@ -3319,26 +3170,6 @@ static hipError_t fill_pk(dim3 grid, hipStream_t s, const NwPairDesc *pairs, uin
             if (o[Opt::PkTab] && fx.bail && pk_free_ok(sc, G * K, ld_max) &&
                 lds_tab <= std::max(lds, kLdsPerCu / 4)) {
                 constexpr bool kRb = decltype(rebase_c)::value;
-                if constexpr (G == 8 && K == 19) {
-                    if (fx.arrive && o[Opt::FuseWalk]) {  // fill + walk in one launch
-                        constexpr uint32_t gpb = kFuseThreads / G, sup = 8 * blocks_per_pack(2 * gpb);
-                        const uint32_t groups = (count + 1) / 2;
-                        const dim3 fg(((groups + gpb - 1) / gpb + sup - 1) / sup * sup);
-                        const size_t lf = std::max<size_t>((size_t)gpb * (ld_max + 2 * G) * 4,
-                                                           WalkGeo<K, true, G * K, true>::kWaveLds);
-                        const hipError_t e = big_lds({(const void *)nw_fill_walk_kernel<1, kRb>,
-                                                      (const void *)nw_fill_walk_kernel<2, kRb>}, lf);
-                        if (e != hipSuccess) return e;
-                        const FuseArgs fa{pairs, fx.bail, fx.epoch, fx.arrive, fx.walk_left, fx.ops,
-                                          results, cigar, o[Opt::FuseWalk] == 2 ? 1u : 0u};
-                        nw_fill_walk_kernel<1, kRb><<<fg, dim3(kFuseThreads), lf, s>>>(
-                            src, count, qs, ds, mask, sc, ld_max, fa);
-                        nw_fill_walk_kernel<2, kRb><<<fg, dim3(kFuseThreads), lf, s>>>(
-                            src, count, qs, ds, mask, sc, ld_max, fa);
-                        fx.fused = true;
-                        return hipSuccess;
-                    }
-                }
                 const hipError_t e = big_lds({(const void *)nw_fill_pk_tab_kernel<G, K, PlanSrc>,
                                               (const void *)nw_fill_pk_tabfb_kernel<G, K, PlanSrc, kRb>},
                                              lds_tab);
@@ -3554,8 +3385,7 @@ hipError_t launch_avsa_scatter(const saln_nw_result *res, const uint32_t *q_ids,
 hipError_t launch_fill(int variant, const NwPairDesc *pairs, uint32_t first, uint32_t count,
                        const uint8_t *qs, const uint8_t *ds, uint8_t *mask, int2 *scratch,
                        int32_t *end_h, saln_nw_result *res, uint32_t *cig, Scoring sc,
-                       int codes, uint32_t ld_max, hipStream_t stream, FillExtras &fx) {
-    fx.fused = false;
+                       int codes, uint32_t ld_max, hipStream_t stream, const FillExtras &fx) {
     if (count == 0) return hipSuccess;
     const uint32_t gpb = 256 / kFillG[variant];  // lane groups per block
     const uint32_t groups = kPacked[variant] ? (count + 1) / 2 : count;
@@ -3582,10 +3412,10 @@ hipError_t launch_fill(int variant, const NwPairDesc *pairs, uint32_t first, uin
 template <int G, int K, bool kNib = false>
 static void tb_lds(hipStream_t s, const NwPairDesc *pairs, uint32_t first, uint32_t n,
                    const uint8_t *mask, const int32_t *end_h, uint32_t *ops, saln_nw_result *res,
-                   uint32_t *cig, Scoring sc, const uint8_t *qs, uint32_t *walk_left = nullptr) {
+                   uint32_t *cig, Scoring sc, const uint8_t *qs) {
     constexpr uint32_t nt = tb_lds_threads<G, K, kNib>();
     nw_traceback_lds_kernel<G, K, kNib><<<dim3((n + nt - 1) / nt), dim3(nt), 0, s>>>(
-        pairs, first, n, mask, end_h, ops, res, cig, sc, qs, walk_left);
+        pairs, first, n, mask, end_h, ops, res, cig, sc, qs);
 }
 
 // Traceback of plan range [first, first+n).  variant >= 0: all pairs of that
@@ -3595,7 +3425,7 @@ hipError_t launch_traceback(int variant, const NwPairDesc *pairs, uint32_t first
                             const uint8_t *qs, const uint8_t *ds, const uint8_t *mask,
                             const int32_t *end_h, uint32_t *ops, saln_nw_result *results,
                             uint32_t *cigar, Scoring sc, int stripe_layout, hipStream_t stream,
-                            const uint32_t *spec_done, bool nib, const uint32_t *walk_left) {
+                            const uint32_t *spec_done, bool nib) {
     if (n == 0) return hipSuccess;
     const dim3 grid((n + 255) / 256);
     if (nib && variant != 4 && variant != 7) return hipErrorInvalidValue;
@@ -3632,8 +3462,7 @@ hipError_t launch_traceback(int variant, const NwPairDesc *pairs, uint32_t first
         }
         case 4:  // 8 x 19 groups: 4-bit codes only (byte segments would not fit a slot)
             if (!nib) return hipErrorInvalidValue;
-            tb_lds<8, 19, true>(stream, pairs, first, n, mask, end_h, ops, results, cigar, sc, qs,
-                                const_cast<uint32_t *>(walk_left));
+            tb_lds<8, 19, true>(stream, pairs, first, n, mask, end_h, ops, results, cigar, sc, qs);
             break;
         case 5: tb_lds<16, 16>(stream, pairs, first, n, mask, end_h, ops, results, cigar, sc, qs); break;
         case 6: tb_lds<32, 16>(stream, pairs, first, n, mask, end_h, ops, results, cigar, sc, qs); break;

@@ -161,22 +161,18 @@ def test_c2_scale_properties(saln, oracle):
     plan.close()
 
 
-@pytest.mark.parametrize("tab,fuse", [(1, 1), (1, 2), (1, 0), (0, 0)])
-def test_walk_code_formats_match_oracle(saln, oracle, saln_opt, tab, fuse):
+@pytest.mark.parametrize("tab", [1, 0])
+def test_walk_code_formats_match_oracle(saln, oracle, saln_opt, tab):
     """The 4-bit walk codes of the short-query packed fills (8 x 19 groups for
     queries of <= 152 columns, 16 x 10 up to 160) give the oracle's results
-    through every fill / walk route: the table fill walking its packs in the
-    same launch (nw.fuse_walk = 1, the default), the same fill leaving every
-    pack to the walker launch (2: the route of a pack whose waves ran on
-    several XCDs), the table fill with the separate walker (0), and the
-    generic fill (nw.pk_tab = 0).  20,000 configs[1] pairs (score, end
+    through both fills: the table fill (nw.pk_tab = 1, the default) and the
+    generic one (nw.pk_tab = 0).  20,000 configs[1] pairs (score, end
     states, panic, printed, CIGAR word for word) and a ragged batch: 1..160-
     column queries, dbs up to 1,200 rows (the rebasing int16 frame),
     identical and two-letter pairs."""
     import torch
     from sequencealigning_amd import synth
     saln_opt("nw.pk_tab", tab)
-    saln_opt("nw.fuse_walk", fuse)
     n, L = 20_000, 150
     qs, qo, ds, do = synth.iid_pairs(n, L, L, seed=0x5EED0002)
     plan = saln.NwPlan(qo, do, pairs=np.stack([np.arange(n), np.arange(n)], 1))
@@ -198,7 +194,7 @@ def test_walk_code_formats_match_oracle(saln, oracle, saln_opt, tab, fuse):
             o0 = int(plan.cigar_off[k])
             assert np.array_equal(cig[o0:o0 + int(res["cigar_len"][k])], want.cigar_words(k)), k
     plan.close()
-    rng = np.random.default_rng(4040 + 3 * tab + fuse)
+    rng = np.random.default_rng(4040 + 3 * tab)
     queries, dbs = [], []
     for lq, ld in [(1, 1), (1, 40), (9, 3), (19, 19), (20, 150), (38, 900), (151, 151),
                    (152, 152), (152, 1200), (153, 160), (160, 400), (140, 1200), (75, 5)]:
@@ -243,7 +239,7 @@ def test_table_fill_equals_generic(saln, oracle, saln_opt, case):
     1 % of the queries and 1 % of the dbs (those waves take the fallback
     launch, the rest of the launch the table body); "scheme" uses
     {2, -3, -5, -2} (bonuses 12 / 2).  "long_db" / "long_db_n": 150 x 500
-    pairs (8 x 19 groups, the fused fill + walk) and 155 x 500 pairs (16 x 10
+    pairs (8 x 19 groups) and 155 x 500 pairs (16 x 10
     groups), whose dbs need the rebasing frame in the original frame but not
     in the extension-free one (the fallback launch then rebases)."""
     from sequencealigning_amd import synth
@@ -289,8 +285,8 @@ def test_table_fill_concurrent_plans(saln, saln_opt, lens):
     streams, three times each: each plan's table launches mark their
     bail-outs in the plan's own bail word (a process-wide slot
     ring shared by the instantiations), so each fallback launch runs exactly
-    its own launch's bail-outs.  (150, 156): the fused 8 x 19 fill + walk
-    beside the 16 x 10 table fill.  Results equal each plan run alone."""
+    its own launch's bail-outs.  (150, 156): the 8 x 19 table fill beside
+    the 16 x 10 one.  Results equal each plan run alone."""
     import torch
     from sequencealigning_amd import synth
     saln_opt("nw.pk_tab", 1)
@@ -770,9 +766,9 @@ def test_long_gaps_lds_walker(saln, oracle):
 def test_context_options_two_threads(saln, oracle):
     """Per-context options (saln_context_option_set): two
     contexts on two host threads run batches at the same time with
-    different kernel choices - the fused 8 x 19 table fill + walk (pk_tab 1,
-    fuse_walk 1) and the generic fill with the separate walker (pk_tab 0) -
-    and both equal the oracle; the process registry and the per-process
+    different kernel choices - the 8 x 19 table fill (nw.pk_tab 1) and the
+    generic 4-bit-code fill (pk_tab 0) - and both equal the oracle; the
+    process registry and the per-process
     context keep their defaults."""
     import threading
 
@@ -786,7 +782,6 @@ def test_context_options_two_threads(saln, oracle):
     ctxs = [_lib.new_context(0), _lib.new_context(0)]
     try:
         _lib.set_context_option(ctxs[0], "nw.pk_tab", 1)
-        _lib.set_context_option(ctxs[0], "nw.fuse_walk", 1)
         _lib.set_context_option(ctxs[1], "nw.pk_tab", 0)
         assert _lib.get_context_option(ctxs[1], "nw.pk_tab") == 0
         assert _lib.get_option("nw.pk_tab")[0] == 1

@@ -16,7 +16,7 @@ def test_options_table_matches_header(saln):
     hdr = open(os.path.join(ROOT, "include", "saln.h")).read()
     block = hdr[hdr.index("Tuning knobs (kernel geometry"):hdr.index("int saln_option_set")]
     assert sorted(re.findall(r'"([a-z0-9_.]+)"', block)) == sorted(names)
-    assert len(names) == len(set(names)) >= 16
+    assert len(names) == len(set(names)) >= 15
 
 
 def test_option_set_get_reset(saln):

@@ -2,8 +2,8 @@
 # Round-5 GPU steps.  STAGES (space-separated, default "smoke tests bench"):
 #   abxcd    C4 row fill, XCD-local stripe runs (nw.rows_xcd) vs dispatch order,
 #            REPS alternations of tools/bench_long.py (walk codes and score-only)
-#   abfuse   C2 step: fused fill + walk (nw.fuse_walk=1) vs the separate walker
-#            (0), sequential and pipelined, REPS alternations (tools/ab_c2.py)
+#   abwalk   C2 step with this tree's walker vs sequencealigning_amd/libsaln_prev.so
+#            (an earlier commit's build), sequential and pipelined, REPS alternations
 #   smoke    __graft_entry__.smoke()
 #   tests    pytest -m gpu (TESTS= narrows it, e.g. "tests/test_span_gpu.py -k xcd")
 #   bench    bench.py --steps 20 --warmup 3 (BENCH_ARGS= extra args)
@@ -35,12 +35,16 @@ for st in ${STAGES:-smoke tests bench}; do
           tail -1 $O/lag${x}_$ns.log
         done
       done ;;
-    abfuse)
+    abwalk)  # the walker of this tree vs the one in sequencealigning_amd/libsaln_prev.so
       for i in ${REPS:-1 2}; do
-        for f in ${FUSE:-1 0}; do
+        for lib in prev cur; do
           for pl in "" "--pipeline"; do
-            tag=fuse${f}${pl:+_pipe}_$i
-            step $tag 180 python tools/ab_c2.py --tag $tag --opt nw.fuse_walk=$f $pl
+            tag=walk_${lib}${pl:+_pipe}_$i
+            if [ $lib = prev ]; then
+              SALN_LIB=sequencealigning_amd/libsaln_prev.so step $tag 180 python tools/ab_c2.py --tag $tag $pl
+            else
+              step $tag 180 python tools/ab_c2.py --tag $tag $pl
+            fi
             tail -1 $O/$tag.log
           done
         done
