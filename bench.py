@@ -161,18 +161,27 @@ def _pmc_docs():
             continue
 
 
-def pmc(kernel: str, field: str = "hbm_bytes"):
+def pmc(kernel, field: str = "hbm_bytes"):
     """A per-launch PMC figure of `kernel` (HBM bytes, VALU wave-instructions
     with field="valu_wave_insts", their sum over the profiled run with
     "valu_wave_insts_sum") from the committed PMC summaries (profiles/
     pmc_traffic.json: the headline command; profiles/pmc_legs.json: the
     legs, tools/prof_legs.py), written by tools/pmc_traffic.py from separate
-    rocprofv3 --pmc passes (tools/pmc.sh), or None."""
-    for _, doc in _pmc_docs():
-        for name, v in doc.get("kernels", {}).items():
-            if kernel in name and field in v:
-                return v[field]
+    rocprofv3 --pmc passes (tools/pmc.sh), or None.  `kernel`: a name or a
+    tuple of names, the first one found wins."""
+    for k in ((kernel,) if isinstance(kernel, str) else kernel):
+        for _, doc in _pmc_docs():
+            for name, v in doc.get("kernels", {}).items():
+                if k in name and field in v:
+                    return v[field]
     return None
+
+
+def pmc_name(*names: str) -> str:
+    """The first of `names` (kernel instantiations a leg may run, e.g. the
+    row fill's stripe placements) that the committed PMC summaries hold,
+    else the first."""
+    return next((k for k in names if pmc(k) is not None), names[0])
 
 
 def pmc_executes(leg: str):
@@ -463,7 +472,8 @@ def leg_c1(torch, saln, reps=50, cpu=True):
     gi = synth.random_bases(0x5EED0000 ^ 0x77, 1000).tobytes()
     g, ops = _single_pair(torch, saln, q, d, reps)
     g_iid, ops_iid = _single_pair(torch, saln, q, gi, reps)
-    kern = "nw_fill_rows_kernel<1, 0, true, true>"  # kLone: 16 stripes, one per SIMD
+    # 16 stripes, one per SIMD (kPlace 2: XCD-local runs on a whole-device stream; 1: lone)
+    kern = pmc_name("nw_fill_rows_kernel<1, 0, true, 2>", "nw_fill_rows_kernel<1, 0, true, 1>")
     fill_s = g["fill_ms"] / 1e3
     out = {"workload": "configs[0]: one 1 kbp x 1 kbp pair, score + first-printed traceback "
                        "(G-mut 5 %; iid beside it)",
@@ -508,7 +518,8 @@ def leg_c4(torch, saln, reps=3, cpu=True):
     d = synth.mutate(q, 0.05, seed=100_000)
     g, ops = _single_pair(torch, saln, q, d, reps)
     torch.cuda.empty_cache()
-    kern = "nw_fill_rows_kernel<2, 0, true, true>"  # kLone: 782 stripes, one per SIMD
+    # 782 stripes, one per SIMD, XCD-local runs (nw.rows_xcd)
+    kern = pmc_name("nw_fill_rows_kernel<2, 0, true, 2>", "nw_fill_rows_kernel<2, 0, true, 1>")
     fill_s = g["fill_ms"] / 1e3
     out = {"workload": "configs[3]: one 100 kbp x 100 kbp pair, G-mut 5 %, fill + 1 B/cell mask "
                        "+ first-printed traceback", "gpu": g, "executes": 1 + reps,
@@ -591,6 +602,11 @@ def leg_c4_spans(torch, saln, n_spans=8, reps=3, band_rows=1024, edge_masks="sha
     want = saln.n_w_align(q, d)
     fill_s, walk_s = float(np.mean(fills)), float(np.mean(walks))
     cells = len(q) * len(d)
+    # the chain's span fills (128-column stripes on CU-masked streams: one
+    # stripe per SIMD of the span's CUs), one launch per span and execute
+    span_kern = pmc_name("nw_fill_rows_kernel<2, 0, true, 1>", "nw_fill_rows_kernel<2, 0, true, 0>")
+    per_launch = pmc(span_kern)
+    span_traffic = per_launch * n_spans if per_launch else None
     return {"workload": f"configs[3]'s pair as {n_spans} column spans on one GPU, each on "
                         f"1/{n_spans} of its CUs (CU-masked streams), boundary rows relayed "
                         f"span to span as they are published (one relay kernel per edge)", "value": round(cells / (fill_s + walk_s) / 1e9, 1),
@@ -604,8 +620,11 @@ def leg_c4_spans(torch, saln, n_spans=8, reps=3, band_rows=1024, edge_masks="sha
                                   want.cigar)),
             "checked": "score, status, end states and the first printed CIGAR vs n_w_align",
             "roofline": roof_hbm(cells, fill_s, "nw_fill_rows_kernel (8 spans, CU-partitioned)",
+                                 span_traffic, traffic_kernel=span_kern,
                                  note="1 B/cell of mask over the spans' concurrent fills; bound "
-                                      "by the row chain like c4 (DESIGN.md §6)"),
+                                      "by the row chain like c4 (DESIGN.md §6); traffic: the "
+                                      "spans' fill launches of one execute (PMC, "
+                                      "profiles/pmc_legs.json)"),
             "cpu_baseline": "the c4 leg's (the same pair)"}
 
 

@@ -38,6 +38,7 @@ struct Args {
     bool timing = true, abort_on_panic = true;
     uint32_t wfa_steps = 64;  // cap on WFA score steps (the reference loops without one)
     uint64_t max_blocks = 0;
+    uint64_t chunk_pairs = 1u << 14;  // pairs per render batch (the first one: a quarter)
     bool stage_times = false;
 };
 
@@ -58,6 +59,7 @@ const char *kUsage =
     "      --no-abort                 report reference panics and continue\n"
     "      --wfa-steps <N>            cap on WFA score steps [default: 64]\n"
     "      --max-blocks <N>           cap on printed alignments per pair [default: 0 = none]\n"
+    "      --chunk-pairs <N>          pairs per GPU batch [default: 16384]\n"
     "      --stage-times              stage times of this run on stderr\n"
     "  -h, --help                     Print help\n";
 
@@ -118,6 +120,8 @@ Args parse_args(int argc, char **argv) {
             a.stage_times = true;
         } else if (is("--max-blocks", "--max-blocks")) {
             a.max_blocks = std::strtoull(need("--max-blocks <N>").c_str(), nullptr, 10);
+        } else if (is("--chunk-pairs", "--chunk-pairs")) {
+            a.chunk_pairs = std::max<uint64_t>(1, std::strtoull(need("--chunk-pairs <N>").c_str(), nullptr, 10));
         } else {
             usage_error("unexpected argument '" + s + "' found");
         }
@@ -385,8 +389,10 @@ int main(int argc, char **argv) {
     // ~kChunkCells cells (its full-code mask and the host copy of it stay
     // bounded).  A chunk's text is printed on a thread while the next chunk
     // renders, unless the chunk ends the run (a panic under the reference's
-    // abort), which is printed before anything else happens.
-    constexpr uint64_t kChunkPairs = 1u << 16;
+    // abort), which is printed before anything else happens.  The first
+    // chunk is a quarter of the others, so printing starts early; the last
+    // chunk's print is the part that overlaps nothing.
+    const uint64_t kChunkPairs = a.chunk_pairs;
     constexpr uint64_t kChunkCells = 2ull << 30;
     // pair k of a rendered chunk: its text and what the reference does next;
     // returns the process exit code when the run ends here, else -1
@@ -451,7 +457,8 @@ int main(int argc, char **argv) {
         pq.clear();
         pd.clear();
         uint64_t cells = 0;
-        for (uint64_t p = p0; p < total && pq.size() < kChunkPairs; ++p) {
+        const uint64_t cap = p0 == 0 ? std::max<uint64_t>(1, kChunkPairs / 4) : kChunkPairs;
+        for (uint64_t p = p0; p < total && pq.size() < cap; ++p) {
             const uint64_t qi = p % nq, di = p / nq;
             const uint64_t c = (uint64_t)query[qi].seq.size() * db[di].seq.size();
             if (!pq.empty() && cells + c > kChunkCells) break;

@@ -7,10 +7,14 @@
 #   smoke    __graft_entry__.smoke()
 #   tests    pytest -m gpu (TESTS= narrows it, e.g. "tests/test_span_gpu.py -k xcd")
 #   bench    bench.py --steps 20 --warmup 3 (BENCH_ARGS= extra args)
-#   prof     rocprofv3 --kernel-trace --stats of the headline command
+#   prof     rocprofv3 --kernel-trace --stats of the headline command (pipelined),
+#            its fills split into co-run / alone by tools/trace_overlap.py
+#   profseq  the same with --no-pipeline (every fill alone)
 #   proflegs the same over tools/prof_legs.py
 #   pmc      PMC passes (tools/pmc.sh) of the headline workload -> pmc_traffic.json
 #   pmclegs  PMC passes over tools/prof_legs.py -> pmc_legs.json
+#   pmcxcd   PMC traffic of the c4 leg with nw.rows_xcd=0 (stripes in dispatch
+#            order) -> pmc_c4_xcd0.json
 # Every GPU step has its own time limit; the script stops at the first failure.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
@@ -56,13 +60,19 @@ for st in ${STAGES:-smoke tests bench}; do
     bench) step bench 600 python bench.py --steps 20 --warmup 3 $BENCH_ARGS
            tail -1 $O/bench.log | cut -c1-3000 ;;
     prof) step prof 600 rocprofv3 --kernel-trace --stats -d $O/prof -o run --output-format csv -- python3 bench.py --steps 20 --warmup 3 --legs none --no-cpu-baseline
-          find $O/prof -name '*kernel_stats.csv' -exec head -12 {} \; | cut -c1-220 ;;
+          find $O/prof -name '*kernel_stats.csv' -exec head -12 {} \; | cut -c1-220
+          python3 tools/trace_overlap.py $O/prof --out $O/prof_overlap.json ;;
+    profseq) step profseq 600 rocprofv3 --kernel-trace --stats -d $O/profseq -o run --output-format csv -- python3 bench.py --steps 20 --warmup 3 --legs none --no-cpu-baseline --no-pipeline
+          find $O/profseq -name '*kernel_stats.csv' -exec head -12 {} \; | cut -c1-220
+          python3 tools/trace_overlap.py $O/profseq --out $O/profseq_overlap.json ;;
     proflegs) step proflegs 900 rocprofv3 --kernel-trace --stats -d $O/proflegs -o run --output-format csv -- python3 tools/prof_legs.py
               find $O/proflegs -name '*kernel_stats.csv' -exec head -20 {} \; | cut -c1-220 ;;
     pmc)   PMC_SETS=${PMC_SETS:-"FETCH_SIZE;WRITE_SIZE;SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU;SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU"} step pmc 900 bash tools/pmc.sh
            python3 tools/pmc_traffic.py gpurun_out/pmc $O/pmc_traffic.json r05 nw > /dev/null || exit 1 ;;
-    pmclegs) PMC_SCRIPT=tools/prof_legs.py PMC_SETS=${PMC_SETS:-"FETCH_SIZE;WRITE_SIZE;SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU"} step pmc_legs 1100 bash tools/pmc.sh --legs ${PROF_LEGS:-c1,c3,c3_affine,c4,c5}
+    pmclegs) PMC_SCRIPT=tools/prof_legs.py PMC_SETS=${PMC_SETS:-"FETCH_SIZE;WRITE_SIZE;SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU"} step pmc_legs 1100 bash tools/pmc.sh --legs ${PROF_LEGS:-c1,c3,c3_affine,c4,c4_spans,c5}
            python3 tools/pmc_traffic.py gpurun_out/pmc $O/pmc_legs.json r05 legs > /dev/null || exit 1 ;;
+    pmcxcd) PMC_SCRIPT=tools/prof_legs.py PMC_SETS="FETCH_SIZE;WRITE_SIZE;SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU" step pmc_xcd0 600 bash tools/pmc.sh --legs c4 --opt nw.rows_xcd=0
+           python3 tools/pmc_traffic.py gpurun_out/pmc $O/pmc_c4_xcd0.json r05 legs > /dev/null || exit 1 ;;
     *) echo "unknown stage $st"; exit 2 ;;
   esac
 done

@@ -5,7 +5,10 @@ tools/pmc.sh).  Writes {leg: executes} (runs of the leg's workload) to
 $PMC_EXECUTES (default gpurun_out/pmc/executes.json) so tools/pmc_traffic.py
 can turn the counters' per-run sums into per-execute figures.
 
-    python tools/prof_legs.py [--legs c1,c3,c3_affine,c4,c5]
+    python tools/prof_legs.py [--legs c1,c3,c3_affine,c4,c4_spans,c5] [--opt name=value ...]
+
+--opt sets engine options (saln_option_set) for the whole run, e.g.
+nw.rows_xcd=0 for the C4 row fill's traffic without XCD-local stripes.
 """
 import argparse
 import json
@@ -19,10 +22,16 @@ sys.path.insert(0, ROOT)
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--legs", default="c1,c3,c3_affine,c4,c5")
+    ap.add_argument("--opt", action="append", default=[],
+                    help="engine option name=value (saln_option_set), repeatable")
     a = ap.parse_args()
     import torch
     import sequencealigning_amd as saln
     import bench
+    from sequencealigning_amd import _lib
+    for kv in a.opt:
+        k, v = kv.split("=")
+        _lib.set_option(k, int(v))
     ex = {}
     for leg in a.legs.split(","):
         if leg == "c5":
@@ -35,6 +44,8 @@ def main():
             r = bench.leg_c3_affine(torch, saln, cpu=False)
         elif leg == "c4":
             r = bench.leg_c4(torch, saln, cpu=False)
+        elif leg == "c4_spans":
+            r = bench.leg_c4_spans(torch, saln)
         else:
             raise SystemExit(f"unknown leg {leg}")
         ex[leg] = r["executes"]

@@ -1,7 +1,10 @@
 """Overlap of the C2 pipeline's kernels in a rocprofv3 kernel trace
-(tools/cu_pipeline.py under rocprofv3 --kernel-trace --output-format csv):
-for each walk (nw_traceback_lds_kernel) the fraction of its duration during
-which a fill (nw_fill_pk_kernel) ran.  Tools only.
+(tools/cu_pipeline.py or bench.py under rocprofv3 --kernel-trace
+--output-format csv): for each walk (nw_traceback_lds_kernel) the fraction
+of its duration during which a fill (nw_fill_pk_kernel / _tab_kernel) ran,
+and the fills split into those that overlapped a walk (co-run: the bench's
+pipelined kernel_avg_ms) and those that ran alone (kernel_avg_ms_alone:
+the bench's sequential executes after its timed region).  Tools only.
 
     python tools/trace_overlap.py <dir with *kernel_trace.csv> [--out file.json]
 """
@@ -25,11 +28,18 @@ def main():
         ov = sum(max(0, min(e, fe) - max(s, fs)) for fs, fe in fills)
         fr.append(ov / max(1, e - s))
     span = (max(e for _, e, _ in ks) - min(s for s, _, _ in ks)) / 1e6
+    corun, alone = [], []
+    for s, e in fills:
+        ov = any(min(e, we) > max(s, ws) for ws, we in walks)
+        (corun if ov else alone).append((e - s) / 1e6)
+    avg = lambda x: round(sum(x) / len(x), 4) if x else None  # noqa: E731
     doc = {"trace": os.path.relpath(f), "walks": len(walks), "fills": len(fills),
            "walk_ms_avg": round(sum(e - s for s, e in walks) / max(1, len(walks)) / 1e6, 4),
            "fill_ms_avg": round(sum(e - s for s, e in fills) / max(1, len(fills)) / 1e6, 4),
            "walk_overlap_frac_avg": round(sum(fr) / max(1, len(fr)), 3),
            "walk_overlap_frac_min": round(min(fr), 3) if fr else None,
+           "fill_corun_n": len(corun), "fill_corun_ms_avg": avg(corun),
+           "fill_alone_n": len(alone), "fill_alone_ms_avg": avg(alone),
            "trace_span_ms": round(span, 3)}
     print(json.dumps(doc))
     if out:
