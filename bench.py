@@ -152,8 +152,8 @@ def cpu_baseline(budget_s: float = 15.0) -> dict:
 
 
 # ------------------------------------------------------------- rooflines
-def _pmc_docs():
-    for f in PMC_FILES:
+def _pmc_docs(files=PMC_FILES):
+    for f in files:
         try:
             with open(os.path.join(ROOT, "profiles", f)) as fh:
                 yield f, json.load(fh)
@@ -161,16 +161,16 @@ def _pmc_docs():
             continue
 
 
-def pmc(kernel, field: str = "hbm_bytes"):
+def pmc(kernel, field: str = "hbm_bytes", files=PMC_FILES):
     """A per-launch PMC figure of `kernel` (HBM bytes, VALU wave-instructions
     with field="valu_wave_insts", their sum over the profiled run with
     "valu_wave_insts_sum") from the committed PMC summaries (profiles/
     pmc_traffic.json: the headline command; profiles/pmc_legs.json: the
     legs, tools/prof_legs.py), written by tools/pmc_traffic.py from separate
     rocprofv3 --pmc passes (tools/pmc.sh), or None.  `kernel`: a name or a
-    tuple of names, the first one found wins."""
+    tuple of names, the first one found wins; `files`: the summaries to read."""
     for k in ((kernel,) if isinstance(kernel, str) else kernel):
-        for _, doc in _pmc_docs():
+        for _, doc in _pmc_docs(files):
             for name, v in doc.get("kernels", {}).items():
                 if k in name and field in v:
                     return v[field]
@@ -602,10 +602,12 @@ def leg_c4_spans(torch, saln, n_spans=8, reps=3, band_rows=1024, edge_masks="sha
     want = saln.n_w_align(q, d)
     fill_s, walk_s = float(np.mean(fills)), float(np.mean(walks))
     cells = len(q) * len(d)
-    # the chain's span fills (128-column stripes on CU-masked streams: one
-    # stripe per SIMD of the span's CUs), one launch per span and execute
-    span_kern = pmc_name("nw_fill_rows_kernel<2, 0, true, 1>", "nw_fill_rows_kernel<2, 0, true, 0>")
-    per_launch = pmc(span_kern)
+    # the chain's span fills (128-column stripes on CU-masked streams, one
+    # per SIMD of the span's CUs, in XCD runs when they fit), one launch per
+    # span and execute; their own PMC summary (tools/prof_legs.py c4_spans:
+    # the same instantiation as the c4 leg's fill)
+    span_kern = "nw_fill_rows_kernel<2, 0, true,"
+    per_launch = pmc(span_kern, files=("pmc_c4_spans.json",))
     span_traffic = per_launch * n_spans if per_launch else None
     return {"workload": f"configs[3]'s pair as {n_spans} column spans on one GPU, each on "
                         f"1/{n_spans} of its CUs (CU-masked streams), boundary rows relayed "
@@ -624,7 +626,7 @@ def leg_c4_spans(torch, saln, n_spans=8, reps=3, band_rows=1024, edge_masks="sha
                                  note="1 B/cell of mask over the spans' concurrent fills; bound "
                                       "by the row chain like c4 (DESIGN.md §6); traffic: the "
                                       "spans' fill launches of one execute (PMC, "
-                                      "profiles/pmc_legs.json)"),
+                                      "profiles/pmc_c4_spans.json)"),
             "cpu_baseline": "the c4 leg's (the same pair)"}
 
 

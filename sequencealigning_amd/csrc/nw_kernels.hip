@@ -3674,21 +3674,30 @@ static uint32_t device_simds() {
     return simds;
 }
 
-// The stream may run on every CU of the device (no CU mask narrower than it):
-// only then is every stripe of a launch that fits the SIMDs resident at once.
-static bool stream_all_cus(hipStream_t s) {
-    int dev = 0, cus = 0;
+// XCD runs of a lone launch (kPlaceXcd: workgroup b on XCD b % 8, also on a
+// CU-masked stream - tests/test_span_gpu.py) need every run resident at
+// once: a run's first stripe waits for the previous XCD's last one, a later
+// workgroup.  The stream's mask holds per XCD (bit c: a CU of XCD c mod 8,
+// profiles/r04_cu_map.json; an XCD without a bit runs unmasked) CUs whose
+// SIMDs must cover the run, one stripe per SIMD.
+static bool xcd_fit(hipStream_t s, uint32_t run) {
+    int dev = 0, cus = 0, xcds = 0;
     if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        hipDeviceGetAttribute(&xcds, hipDeviceAttributeNumberOfXccs, dev) != hipSuccess)
         return false;
+    if (xcds != 8 || cus % 8) return false;  // the kernel's b % 8 mapping
     uint32_t m[32] = {};
     const uint32_t nw = std::min<uint32_t>(32, ((uint32_t)cus + 31) / 32);
     if (hipExtStreamGetCUMask(s, nw, m) != hipSuccess) {
         (void)hipGetLastError();
         return false;
     }
+    uint32_t per[8] = {};
     for (uint32_t c = 0; c < (uint32_t)cus; ++c)
-        if (!(m[c / 32] >> (c % 32) & 1u)) return false;
+        if (m[c / 32] >> (c % 32) & 1u) ++per[c % 8];
+    for (uint32_t x = 0; x < 8; ++x)
+        if (4u * (per[x] ? per[x] : (uint32_t)cus / 8) < run) return false;
     return true;
 }
 
@@ -3708,8 +3717,8 @@ hipError_t launch_fill_stripes(const NwPairDesc *pairs, const uint2 *work, uint3
             constexpr bool kP = decltype(minpen_c)::value;
             const uint32_t nw = n_work * (4 / kK);
             const bool lone = o[Opt::RowsLone] && nw <= device_simds();
-            if (lone && o[Opt::RowsXcd] && nw >= 16 && stream_all_cus(stream)) {
-                const uint32_t run = (nw + 7) / 8;
+            const uint32_t run = (nw + 7) / 8;
+            if (lone && o[Opt::RowsXcd] && nw >= 16 && xcd_fit(stream, run)) {
                 nw_fill_rows_kernel<kK, kC, kP, kPlaceXcd><<<dim3(8 * run), block, 0, stream>>>(
                     pairs, work, qs, ds, mask, scratch, err, end_h, sc, nw, run);
             } else if (lone) {

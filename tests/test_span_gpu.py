@@ -334,6 +334,29 @@ def test_workgroup_dispatch_round_robin_over_xcds():
         [(b, ids[b], ids[b % 8]) for b in range(n) if ids[b] != ids[b % 8]][:8]
 
 
+@pytest.mark.parametrize("lo,hi", [(0, 32), (96, 128), (0, 64)])
+def test_workgroup_dispatch_round_robin_masked_stream(lo, hi):
+    """On a CU-range stream (a span's 1/8 or 1/4 of the CUs, k CUs of every
+    XCD) workgroup b still runs on XCD b % 8, so the row fill's XCD runs also
+    hold for the spans' masked fills (xcd_fit)."""
+    import ctypes as C
+
+    from sequencealigning_amd import _lib
+    L, ctx = _lib.lib(), _lib.context(0)
+    st = C.c_void_p()
+    assert L.saln_stream_create_cu_range(ctx, lo, hi, C.byref(st)) == _lib.OK
+    try:
+        n = 1024
+        hw, xc = (C.c_uint32 * n)(), (C.c_uint32 * n)()
+        assert L.saln_device_cu_probe(ctx, st, n, hw, xc) == _lib.OK
+        ids = [xc[b] & 0xF for b in range(n)]
+        assert len(set(ids[:8])) == 8, ids[:8]
+        assert all(ids[b] == ids[b % 8] for b in range(n)), \
+            [(b, ids[b], ids[b % 8]) for b in range(n) if ids[b] != ids[b % 8]][:8]
+    finally:
+        L.saln_stream_destroy(ctx, st)
+
+
 @pytest.mark.parametrize("lq,ld", [(20000, 20000), (9000, 30000)])
 def test_row_fill_xcd_placement_equal(saln_opt, lq, ld):
     """nw.rows_xcd = 1 (stripes in XCD runs, plain publication inside a run)
