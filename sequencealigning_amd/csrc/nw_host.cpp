@@ -85,7 +85,8 @@ struct saln_nw_plan {
     // d_err[0]: device error flags since the last saln_nw_plan_status (bit 0
     // a dependency wait timed out, bit 1 an unlinked speculative walk under
     // SALN_SPEC_STRICT); d_err[1]: the wait limit the fills read
-    uint32_t *d_prog = nullptr, *d_err = nullptr;
+    uint32_t *d_prog = nullptr, *d_err = nullptr;  // d_err: kErrWords (the row fill's XCD slots after the two)
+    uint32_t fill_epoch = 0;  // stripe fills launched (the XCD slots' epochs)
     uint32_t wait_limit = kWaitLimitDefault;
     bool unchecked[2] = {false, false};  // executes on workspace b since the last status
     uint64_t n_prog = 0;
@@ -493,7 +494,7 @@ int saln::plan_create(saln_context *ctx, const uint64_t *q_off, uint64_t n_q,
                 (e = hipMemcpy(p->d_work, work.data(), work.size() * sizeof(uint2),
                                hipMemcpyHostToDevice)) != hipSuccess ||
                 (e = dev_alloc(p->ctx, (void **)&p->d_prog, p->n_prog * sizeof(uint32_t))) != hipSuccess ||
-                (e = dev_alloc(p->ctx, (void **)&p->d_err, 2 * sizeof(uint32_t))) != hipSuccess ||
+                (e = dev_alloc(p->ctx, (void **)&p->d_err, kErrWords * sizeof(uint32_t))) != hipSuccess ||
                 (e = hipMemcpy(p->d_err, std::array<uint32_t, 2>{0u, kWaitLimitDefault}.data(),
                                2 * sizeof(uint32_t), hipMemcpyHostToDevice)) != hipSuccess)
                 return fail(e, "stripe work list");
@@ -649,7 +650,8 @@ int saln_nw_execute(saln_nw_plan *p, const uint8_t *d_q, const uint8_t *d_db,
                 HIP_TRY(launch_fill_stripes(p->d_pairs, p->d_work + w0, w1 - w0, d_q, d_db, mask,
                                             p->d_scratch, p->d_prog, p->d_err, endh, p->sc,
                                             p->score_only ? 2 : p->full_codes ? 1 : 0,
-                                            p->stripe_layout(), p->stripe_rows, s, p->opts));
+                                            p->stripe_layout(), p->stripe_rows, s, p->opts,
+                                            ++p->fill_epoch));
             continue;
         }
         fx.epoch = ++p->epoch;

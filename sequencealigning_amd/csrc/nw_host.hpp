@@ -103,7 +103,12 @@ hipError_t launch_fill_stripes(const NwPairDesc *pairs, const uint2 *work, uint3
                                Scoring sc, int codes /* 0 walk, 1 full, 2 none */,
                                int layout /* 0 skewed, 1 packed, 2 row-major tiles */,
                                int rows_k /* layout 2: columns per lane */, hipStream_t stream,
-                               const Options &o);
+                               const Options &o, uint32_t epoch);
+// err buffer of a stripe fill: [device error flags, wait limit, kXcdSlots
+// slots] - the row fill's XCD runs post {epoch, XCC_ID} per wave there, so a
+// launch needs an epoch its buffer has not seen (1, 2, ...)
+constexpr uint32_t kXcdSlots = 1024;
+constexpr size_t kErrWords = 2 + kXcdSlots;
 // render batches: the reference DFS's event after each pair's first printed
 // alignment (full-code plans; next[pair_id]: 0 none, 1 block, 2 panic, 3 host)
 hipError_t launch_next_event(const NwPairDesc *pairs, uint32_t n, const uint8_t *mask,

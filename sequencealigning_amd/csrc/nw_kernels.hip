@@ -2208,19 +2208,24 @@ __device__ __forceinline__ int32_t wave_prefix_max(int32_t v, Fill &&fill) {
 //    (b % 8) * xcd_run + b / 8 puts runs of xcd_run consecutive stripes on
 //    one XCD and only 7 hand-offs cross XCDs.  Valid only when every stripe of
 //    the launch is resident at once (a stripe's left neighbour may have a
-//    later workgroup id): the host takes it for launches on the context's
-//    unmasked streams whose stripes fit the device's SIMDs.  A stripe whose
-//    consumer is in its own run publishes with plain stores, which keep the
-//    line in the XCD's L2 where the consumer's sc1 load finds it (the hand-off
-//    rules in DESIGN.md §3); the last stripe of a run publishes sc1
-//    (write-through, visible to the next XCD).
+//    later workgroup id): the host takes it when every XCD's SIMDs (of the
+//    stream's CU mask) hold its run (xcd_fit).  A stripe whose consumer runs
+//    on its own XCD publishes with plain stores, which keep the line in the
+//    XCD's L2 where the consumer's sc1 load finds it (the hand-off rules in
+//    DESIGN.md §3); every other stripe publishes sc1 (write-through, visible
+//    to any XCD).  "Its own XCD" is checked, not assumed (HIP promises no
+//    workgroup-to-XCD placement; the b % 8 round-robin is observed,
+//    MI355X_MICROARCH.md "Workgroup dispatch"): each wave posts {epoch, its
+//    XCC_ID} in its slot of the launch's err buffer with an sc1 store, and a
+//    producer reads its consumer's slot with sc1 loads before the row loop;
+//    anything but a match within the bound publishes sc1.
 constexpr int kPlaceShared = 0, kPlaceLone = 1, kPlaceXcd = 2;
 template <int K, int kCodes, bool kMinPen, int kPlace>
 __global__ __launch_bounds__(64) void nw_fill_rows_kernel(
     const NwPairDesc *__restrict__ pairs, const uint2 *__restrict__ work,
     const uint8_t *__restrict__ qs, const uint8_t *__restrict__ ds, uint8_t *__restrict__ mask,
     int2 *__restrict__ scratch, uint32_t *__restrict__ err, int32_t *__restrict__ end_h,
-    Scoring sc, uint32_t n_waves, uint32_t xcd_run) {
+    Scoring sc, uint32_t n_waves, uint32_t xcd_run, uint32_t epoch) {
     static_assert(K == 1 || K == 2, "4 cells per code word (K = 4, 256-column stripes: slower, round 2)");
     constexpr int S = 4 / K;   // stripes per 256-column chunk (work item)
     constexpr int W = 64 * K;  // stripe width (4 / K rows per code word)
@@ -2231,10 +2236,28 @@ __global__ __launch_bounds__(64) void nw_fill_rows_kernel(
     const uint32_t v = __builtin_amdgcn_readfirstlane(
         kPlace == kPlaceXcd ? (blockIdx.x & 7u) * xcd_run + (blockIdx.x >> 3) : blockIdx.x);
     if (v >= n_waves) return;  // (whole wave: no group barrier in this kernel)
-    // plain publication: my consumer (stripe v + 1, when it is one) runs on my XCD
-    // (the launch's last stripe publishes sc1: a span's outbox is read by a
-    // relay kernel, a copy or RCCL, none of them in this XCD's L2)
-    const bool plain_pub = kPlace == kPlaceXcd && (v + 1) % xcd_run != 0 && v + 1 < n_waves;
+    // plain publication: my consumer (stripe v + 1, when it is one) runs on my
+    // XCD, seen in its slot (err[2 + v + 1]: {epoch, XCC_ID}, posted by its
+    // lane 0 at its start; a stale epoch or a bounded wait that expires: sc1).
+    // The launch's last stripe publishes sc1: a span's outbox is read by a
+    // relay kernel, a copy or RCCL, none of them in this XCD's L2.
+    bool plain_pub = false;
+    if constexpr (kPlace == kPlaceXcd) {
+        uint32_t *const slots = err + 2;
+        const uint32_t xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20) & 15u;  // HW_REG_XCC_ID
+        const uint32_t me = (epoch << 4) | xcc;
+        if (lane == 0) asm volatile("global_store_dword %0, %1, off sc1" : : "v"(slots + v), "v"(me) : "memory");
+        if ((v + 1) % xcd_run != 0 && v + 1 < n_waves) {
+            uint32_t got = 0;
+            for (uint32_t k = 0; k < 4096u; ++k) {  // (the consumer is resident: microseconds)
+                asm volatile("global_load_dword %0, %1, off sc1\n\ts_waitcnt vmcnt(0)"
+                             : "=v"(got) : "v"(slots + v + 1) : "memory");
+                if ((got >> 4) == ((epoch << 4) >> 4)) break;
+                __builtin_amdgcn_s_sleep(2);
+            }
+            plain_pub = __builtin_amdgcn_readfirstlane(got) == me;
+        }
+    }
     const uint2 wk = work[v / S];
     const NwPairDesc p = pairs[wk.x];
     const uint32_t g = wk.y * S + v % S;  // stripe index
@@ -3680,7 +3703,8 @@ static uint32_t device_simds() {
 // workgroup.  The stream's mask holds per XCD (bit c: a CU of XCD c mod 8,
 // profiles/r04_cu_map.json; an XCD without a bit runs unmasked) CUs whose
 // SIMDs must cover the run, one stripe per SIMD.
-static bool xcd_fit(hipStream_t s, uint32_t run) {
+static bool xcd_fit(hipStream_t s, uint32_t run, uint32_t nw) {
+    if (nw > kXcdSlots) return false;  // one slot per wave in the err buffer
     int dev = 0, cus = 0, xcds = 0;
     if (hipGetDevice(&dev) != hipSuccess ||
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
@@ -3688,8 +3712,8 @@ static bool xcd_fit(hipStream_t s, uint32_t run) {
         return false;
     if (xcds != 8 || cus % 8) return false;  // the kernel's b % 8 mapping
     uint32_t m[32] = {};
-    const uint32_t nw = std::min<uint32_t>(32, ((uint32_t)cus + 31) / 32);
-    if (hipExtStreamGetCUMask(s, nw, m) != hipSuccess) {
+    const uint32_t words = std::min<uint32_t>(32, ((uint32_t)cus + 31) / 32);
+    if (hipExtStreamGetCUMask(s, words, m) != hipSuccess) {
         (void)hipGetLastError();
         return false;
     }
@@ -3705,7 +3729,7 @@ hipError_t launch_fill_stripes(const NwPairDesc *pairs, const uint2 *work, uint3
                                const uint8_t *qs, const uint8_t *ds, uint8_t *mask,
                                int2 *scratch, uint32_t *prog, uint32_t *err, int32_t *end_h,
                                Scoring sc, int codes, int layout, int rows_k, hipStream_t stream,
-                               const Options &o) {
+                               const Options &o, uint32_t epoch) {
     if (!n_work) return hipSuccess;
     const dim3 grid(n_work), block(64);
     const bool pk = layout == 1;
@@ -3718,15 +3742,15 @@ hipError_t launch_fill_stripes(const NwPairDesc *pairs, const uint2 *work, uint3
             const uint32_t nw = n_work * (4 / kK);
             const bool lone = o[Opt::RowsLone] && nw <= device_simds();
             const uint32_t run = (nw + 7) / 8;
-            if (lone && o[Opt::RowsXcd] && nw >= 16 && xcd_fit(stream, run)) {
+            if (lone && o[Opt::RowsXcd] && nw >= 16 && xcd_fit(stream, run, nw)) {
                 nw_fill_rows_kernel<kK, kC, kP, kPlaceXcd><<<dim3(8 * run), block, 0, stream>>>(
-                    pairs, work, qs, ds, mask, scratch, err, end_h, sc, nw, run);
+                    pairs, work, qs, ds, mask, scratch, err, end_h, sc, nw, run, epoch);
             } else if (lone) {
                 nw_fill_rows_kernel<kK, kC, kP, kPlaceLone><<<dim3(nw), block, 0, stream>>>(
-                    pairs, work, qs, ds, mask, scratch, err, end_h, sc, nw, 0);
+                    pairs, work, qs, ds, mask, scratch, err, end_h, sc, nw, 0, 0);
             } else {
                 nw_fill_rows_kernel<kK, kC, kP, kPlaceShared><<<dim3(nw), block, 0, stream>>>(
-                    pairs, work, qs, ds, mask, scratch, err, end_h, sc, nw, 0);
+                    pairs, work, qs, ds, mask, scratch, err, end_h, sc, nw, 0, 0);
             }
         };
         auto by_k = [&](auto codes_c, auto minpen_c) {

@@ -46,7 +46,8 @@ struct saln_nw_span {
     NwPairDesc *d_pair = nullptr;
     uint2 *d_work = nullptr;
     uint32_t n_work = 0;
-    uint32_t *d_err = nullptr;  // [flags, wait limit] (the fill's and the watch's waits)
+    uint32_t *d_err = nullptr;  // [flags, wait limit, XCD slots] (kErrWords; the fill's and the watch's waits)
+    uint32_t fill_epoch = 0;    // fills launched (the XCD slots' epochs)
     int32_t *d_endh = nullptr;
     uint2 *d_blocks = nullptr;
     SpecPair *d_sp = nullptr;
@@ -236,7 +237,7 @@ int saln_nw_span_create(saln_context *ctx, uint64_t len_q, uint64_t len_db, uint
         (e = hipMemcpy(s->d_pair, &d, sizeof d, hipMemcpyHostToDevice)) != hipSuccess ||
         (e = dev_alloc(ctx, (void **)&s->d_work, work.size() * sizeof(uint2))) != hipSuccess ||
         (e = hipMemcpy(s->d_work, work.data(), work.size() * sizeof(uint2), hipMemcpyHostToDevice)) != hipSuccess ||
-        (e = dev_alloc(ctx, (void **)&s->d_err, sizeof err0)) != hipSuccess ||
+        (e = dev_alloc(ctx, (void **)&s->d_err, kErrWords * sizeof(uint32_t))) != hipSuccess ||
         (e = hipMemcpy(s->d_err, err0, sizeof err0, hipMemcpyHostToDevice)) != hipSuccess ||
         (e = dev_alloc(ctx, (void **)&s->d_endh, sizeof(int32_t))) != hipSuccess ||
         (e = dev_alloc(ctx, (void **)&s->d_blocks, sizeof blk)) != hipSuccess ||
@@ -304,7 +305,7 @@ int saln_nw_span_fill(saln_nw_span *s, const uint8_t *d_q, const uint8_t *d_db, 
     HIP_TRY(launch_fill_stripes(s->d_pair, s->d_work, s->n_work, d_q, d_db, s->mask_arg(),
                                 s->scratch_arg(), nullptr, s->d_err, s->d_endh, s->sc,
                                 0 /* walk codes */, 2 /* row-major tiles */, s->K,
-                                resolve_stream(stream, s->ctx), s->opts));
+                                resolve_stream(stream, s->ctx), s->opts, ++s->fill_epoch));
     return SALN_OK;
 }
 

@@ -81,3 +81,35 @@ def test_prefetch_counted_wait_exact(rows_kernels, key):
                 counted.append(n)
     # the group prefetch (the poll loop's and the first group's loads wait vmcnt(0))
     assert counted and set(counted) == {expect}
+
+
+@pytest.mark.parametrize("key", KEYS, ids=lambda k: f"K{k[0]}_codes{k[1]}_minpen{k[2]}_place{k[3]}")
+def test_publication_forms(rows_kernels, key):
+    """The visibility rule of the boundary hand-off (DESIGN.md §3 "Hand-off
+    rules", MI355X_MICROARCH.md "Workgroup dispatch, XCD placement &
+    inter-workgroup visibility"), on the shipped ISA:
+
+    * every boundary load is a vector `global_load_dwordx2 ... sc1` (L1
+      bypassed, L2-served: never a stale L1 line, never a scalar load);
+    * the dispatch-order placements (0, 1) publish every row with
+      `global_store_dwordx2 ... sc1` (write-through: visible from any XCD);
+    * the XCD-run placement (2) also holds the plain form (the line stays in
+      the producer's L2, which its same-XCD consumer's sc1 load reads) and
+      the co-location check that selects it: one `global_store_dword ... sc1`
+      posting the wave's {epoch, XCC_ID} slot and `global_load_dword ... sc1`
+      polls of the consumer's slot, vector forms only."""
+    insns = rows_kernels[key]
+    sc1 = lambda i: i.args.rstrip().endswith("sc1")  # noqa: E731
+    x2_loads = [i for i in insns if i.op == "global_load_dwordx2"]
+    assert x2_loads and all(sc1(i) for i in x2_loads)
+    assert not any(i.op.startswith("flat_load") for i in insns)
+    pub = [i for i in insns if i.op == "global_store_dwordx2"]
+    plain = [i for i in pub if not sc1(i)]
+    slot_posts = [i for i in insns if i.op == "global_store_dword" and sc1(i)]
+    slot_polls = [i for i in insns if i.op == "global_load_dword" and sc1(i)]
+    assert any(sc1(i) for i in pub)
+    if key[3] == 2:
+        assert plain and len(slot_posts) == 1 and slot_polls
+        assert slot_posts[0].addr < min(i.addr for i in slot_polls)
+    else:
+        assert not plain and not slot_posts and not slot_polls
