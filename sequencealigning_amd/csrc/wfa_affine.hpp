@@ -25,9 +25,10 @@ struct WfaAffParams {
 
 size_t wfa_affine_lds_bytes(const WfaAffParams &prm, bool wide);
 // n_dev (optional): the pair count is read from device memory (n bounds it)
+// next: a zeroed device counter the launch's waves take pair indices from
 hipError_t launch_wfa_affine(const WfaAffPair *pairs, uint32_t n, const uint8_t *qs,
                              const uint8_t *ds, const WfaAffParams &prm, bool wide,
-                             uint32_t grid, const uint32_t *n_dev, int32_t *scores,
+                             uint32_t grid, const uint32_t *n_dev, uint32_t *next, int32_t *scores,
                              hipStream_t stream);
 hipError_t launch_wfa_affine_compact(const WfaAffPair *pairs, uint32_t n, const int32_t *scores,
                                      WfaAffPair *out, uint32_t *count, hipStream_t stream);

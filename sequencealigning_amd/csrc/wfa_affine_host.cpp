@@ -29,7 +29,7 @@ struct saln_wfa_affine_plan {
     bool wide = false;  // i32 offsets (a sequence longer than 32,000 bases)
     uint64_t n = 0;
     WfaAffPair *d_pairs = nullptr, *d_rerun = nullptr;
-    uint32_t *d_count = nullptr;
+    uint32_t *d_count = nullptr;  // [rerun pairs, pass-1 next pair, pass-2 next pair]
     WfaAffParams p1{}, p2{};  // the two passes (ring width, LDS sequence staging)
     uint32_t grid1 = 0, grid2 = 0;
 };
@@ -79,7 +79,8 @@ uint32_t grid_for(const WfaAffParams &prm, bool wide, uint64_t n, int device) {
 
 int build_pairs(const uint64_t *q_off, uint64_t n_q, const uint64_t *db_off, uint64_t n_db,
                 const uint32_t *pair_q, const uint32_t *pair_db, uint64_t n_pairs,
-                std::vector<WfaAffPair> *out, bool *wide, uint64_t *seq_need) {
+                std::vector<WfaAffPair> *out, bool *wide, uint64_t *seq_need,
+                uint64_t *code_need) {
     out->resize(n_pairs);
     uint64_t maxlen = 0;
     for (uint64_t k = 0; k < n_pairs; ++k) {
@@ -96,6 +97,10 @@ int build_pairs(const uint64_t *q_off, uint64_t n_q, const uint64_t *db_off, uin
         maxlen = std::max({maxlen, lq, ld});
         // LDS bytes to stage both sequences (wfa_affine_kernel's layout)
         *seq_need = std::max<uint64_t>(*seq_need, ((lq + 47) & ~15ull) + ld + 48);
+        // ... or as 2-bit codes (16 per word, the 16-byte-aligned base's
+        // words plus two pad words per sequence)
+        // (at any alignment of the caller's buffers)
+        *code_need = std::max<uint64_t>(*code_need, 4 * ((15 + lq + 15) / 16 + 2 + (15 + ld + 15) / 16 + 2));
         (*out)[k] = p;
     }
     *wide = maxlen > 32000;
@@ -118,10 +123,10 @@ int saln_wfa_affine_plan_create(saln_context *ctx, const uint64_t *q_off, uint64
     p->ctx = ctx;
     int rc = make_params(pen, max_score, &p->prm);
     std::vector<WfaAffPair> hp;
-    uint64_t seq_need = 0;
+    uint64_t seq_need = 0, code_need = 0;
     if (rc == SALN_OK)
         rc = build_pairs(q_off, n_q, db_off, n_db, pair_q, pair_db, n_pairs, &hp, &p->wide,
-                         &seq_need);
+                         &seq_need, &code_need);
     if (rc != SALN_OK) {
         delete p;
         return rc;
@@ -137,7 +142,7 @@ int saln_wfa_affine_plan_create(saln_context *ctx, const uint64_t *q_off, uint64
     if (n_pairs) {
         if ((e = hipMalloc(&p->d_pairs, n_pairs * sizeof(WfaAffPair))) != hipSuccess) return fail(e);
         if ((e = hipMalloc(&p->d_rerun, n_pairs * sizeof(WfaAffPair))) != hipSuccess) return fail(e);
-        if ((e = hipMalloc(&p->d_count, sizeof(uint32_t))) != hipSuccess) return fail(e);
+        if ((e = hipMalloc(&p->d_count, 3 * sizeof(uint32_t))) != hipSuccess) return fail(e);
         if ((e = hipMemcpy(p->d_pairs, hp.data(), n_pairs * sizeof(WfaAffPair),
                            hipMemcpyHostToDevice)) != hipSuccess)
             return fail(e);
@@ -155,7 +160,12 @@ int saln_wfa_affine_plan_create(saln_context *ctx, const uint64_t *q_off, uint64
         q.seqcap = 0;
         const size_t rings = wfa_affine_lds_bytes(q, p->wide);
         const uint64_t cap = std::min<uint64_t>(seq_lds, (64u << 10) - rings);
-        q.seqcap = seq_need <= cap ? (int32_t)((seq_need + 15) & ~15ull) : 0;
+        // 2-bit codes when they fit (a pair holding other bytes then reads
+        // HBM), bytes too when they take little more: the kernel tries codes
+        // first, then bytes, within seqcap
+        uint64_t want = code_need <= cap ? code_need : 0;
+        if (seq_need <= cap && seq_need <= std::max<uint64_t>(want, 8u << 10)) want = std::max(want, seq_need);
+        q.seqcap = (int32_t)((want + 15) & ~15ull);
         return q;
     };
     p->p1 = pass(w1 ? w1 : p->wide ? kW1Wide : kW1);
@@ -172,13 +182,13 @@ int saln_wfa_affine_execute(saln_wfa_affine_plan *p, const uint8_t *d_q_seq,
     if (!p->n) return SALN_OK;
     hipStream_t s = resolve_stream(stream, p->ctx);
     TRY(hipSetDevice(p->ctx->device));
+    TRY(hipMemsetAsync(p->d_count, 0, 3 * sizeof(uint32_t), s));
     TRY(launch_wfa_affine(p->d_pairs, (uint32_t)p->n, d_q_seq, d_db_seq, p->p1, p->wide, p->grid1,
-                          nullptr, d_scores, s));
-    TRY(hipMemsetAsync(p->d_count, 0, sizeof(uint32_t), s));
+                          nullptr, p->d_count + 1, d_scores, s));
     TRY(launch_wfa_affine_compact(p->d_pairs, (uint32_t)p->n, d_scores, p->d_rerun, p->d_count, s));
     // pass 2 reads its pair count from the device (no host round trip)
     TRY(launch_wfa_affine(p->d_rerun, (uint32_t)p->n, d_q_seq, d_db_seq, p->p2, p->wide, p->grid2,
-                          p->d_count, d_scores, s));
+                          p->d_count, p->d_count + 2, d_scores, s));
     return SALN_OK;
 }
 

@@ -19,12 +19,17 @@
 // of g = gcd(x, o+e, e); the wavefronts needed are the last (o+e)/g (M) and
 // e/g (I, D) steps, kept in an LDS ring per wave.
 //
-// Geometry: one wave per pair (a persistent grid walks the pairs), lanes over
+// Geometry: one wave per pair (a persistent grid takes the pairs one by one
+// from a device counter: a wave that shares its SIMD takes fewer of them -
+// round 5, with the static stride the slowest SIMD set the time), lanes over
 // the diagonals of a step in chunks of 64; the ring holds W (a power of two)
 // diagonals per wavefront at index k & (W-1), with each slot's [lo, hi]
 // range in LDS; reads outside a source's range are -inf.  Offsets are i16
-// (pairs up to 32,000 bases; i32 above).  Extension compares 4 bases at a
-// time from the sequences in global memory (L1/L2-resident per pair).
+// (pairs up to 32,000 bases; i32 above).  Extension compares the sequences
+// staged in LDS as 2-bit codes, 16 bases at a time (round 5: a 10 kbp pair's
+// two sequences take 5 KB instead of 20, so five waves fit a CU beside their
+// rings instead of three); a pair with a byte other than A, C, G, T stages
+// bytes (4 at a time) when they fit, else reads HBM.
 #include <hip/hip_runtime.h>
 
 #include <stdint.h>
@@ -70,17 +75,48 @@ __device__ __forceinline__ uint32_t load4(P p) {
     return __builtin_amdgcn_alignbyte(w[1], w[0], (uint32_t)(a & 3));
 }
 
-// Extend (v, h) along matching bases: returns the new text offset.
+// A sequence as the extension reads it: chunk(i) holds bases i, i+1, ... in
+// kStep fields of kBits bits (equal bases <=> equal fields), at(i) one base.
+// Bytes (global memory or staged in LDS): 4 bases per chunk; a chunk at i
+// needs bytes i .. i+4 readable (kNeed).
 template <typename P>
-__device__ __forceinline__ int32_t extend(P q, int32_t lq, P d, int32_t ld, int32_t v, int32_t h) {
+struct SeqBytes {
+    P p;
+    static constexpr int32_t kStep = 4, kShift = 3, kNeed = 5;
+    __device__ __forceinline__ uint32_t chunk(int32_t i) const { return load4(p + i); }
+    __device__ __forceinline__ uint32_t at(int32_t i) const { return p[i]; }
+};
+// 2-bit codes staged in LDS ((c >> 1) & 3: A 0, C 1, T 2, G 3): word w holds
+// the codes of the 16 bytes at the sequence's 16-byte-aligned base + 16 w,
+// off = the sequence's start within the first word.  A chunk is 16 bases
+// (a funnel shift of two words; the staged words are padded by two).
+struct SeqCodes {
+    lds_cu32 *w;
+    int32_t off;
+    static constexpr int32_t kStep = 16, kShift = 1, kNeed = 16;
+    __device__ __forceinline__ uint32_t chunk(int32_t i) const {
+        const uint32_t j = (uint32_t)(i + off);
+        const uint64_t pair = ((uint64_t)w[(j >> 4) + 1] << 32) | w[j >> 4];
+        return (uint32_t)(pair >> (2u * (j & 15u)));
+    }
+    __device__ __forceinline__ uint32_t at(int32_t i) const {
+        const uint32_t j = (uint32_t)(i + off);
+        return (w[j >> 4] >> (2u * (j & 15u))) & 3u;
+    }
+};
+
+// Extend (v, h) along matching bases: returns the new text offset.
+template <typename S>
+__device__ __forceinline__ int32_t extend(const S &q, int32_t lq, const S &d, int32_t ld, int32_t v,
+                                          int32_t h) {
     for (;;) {
-        if (v + 5 <= lq && h + 5 <= ld) {
-            const uint32_t x = load4(q + v) ^ load4(d + h);
-            if (x) return h + (int32_t)(__builtin_ctz(x) >> 3);
-            v += 4;
-            h += 4;
+        if (v + S::kNeed <= lq && h + S::kNeed <= ld) {
+            const uint32_t x = q.chunk(v) ^ d.chunk(h);
+            if (x) return h + (int32_t)(__builtin_ctz(x) >> S::kShift);
+            v += S::kStep;
+            h += S::kStep;
         } else {
-            while (v < lq && h < ld && q[v] == d[h]) {
+            while (v < lq && h < ld && q.at(v) == d.at(h)) {
                 ++v;
                 ++h;
             }
@@ -89,13 +125,14 @@ __device__ __forceinline__ int32_t extend(P q, int32_t lq, P d, int32_t ld, int3
     }
 }
 
-// Score of one pair (q, d in global memory or staged in LDS): the first s
-// whose M wavefront reaches (lq, ld); -1 above max_score, -2 ring too narrow.
-// kSafe0: the sequences have >= 8 readable bytes at q and d (staged in LDS,
-// or long enough), so a probe that is not taken may still load there.
-template <typename OffT, int CM, bool kSafe0, typename P>
-__device__ __forceinline__ int32_t wfa_pair(P q, int32_t lq, P d, int32_t ld, const WfaAffParams &prm,
-                            int32_t *rng, OffT *Mr, OffT *Ir, OffT *Dr) {
+// Score of one pair (q, d: SeqBytes over global memory or LDS, or SeqCodes):
+// the first s whose M wavefront reaches (lq, ld); -1 above max_score, -2
+// ring too narrow.  kSafe0: a chunk at 0 is readable in both (staged, or
+// long enough), so a probe that is not taken may still load there.
+template <typename OffT, int CM, bool kSafe0, typename S>
+__device__ __forceinline__ int32_t wfa_pair(const S &q, int32_t lq, const S &d, int32_t ld,
+                                            const WfaAffParams &prm, int32_t *rng, OffT *Mr,
+                                            OffT *Ir, OffT *Dr) {
     constexpr int32_t kNeg = OffTraits<OffT>::kNeg;
     const int32_t lane = (int32_t)threadIdx.x;
     const int32_t W = prm.W, wm = prm.W - 1;
@@ -214,11 +251,11 @@ __device__ __forceinline__ int32_t wfa_pair(P q, int32_t lq, P d, int32_t ld, co
                 const int32_t k = mLo + 64 * (4 * g + c) + lane;
                 const int32_t M = Mv[c];
                 const int32_t v = M - k;
-                const bool fast = kSafe0 && max(max(-M, v + 5 - lq), M + 5 - ld) <= 0;
+                const bool fast = kSafe0 && max(max(-M, v + S::kNeed - lq), M + S::kNeed - ld) <= 0;
                 slow[c] = M >= 0 && !fast;
                 if constexpr (kSafe0) {  // loads at a safe address when not fast
-                    const uint32_t x = load4(q + (fast ? v : 0)) ^ load4(d + (fast ? M : 0));
-                    const int32_t adv = x ? (int32_t)(__builtin_ctz(x) >> 3) : 4;
+                    const uint32_t x = q.chunk(fast ? v : 0) ^ d.chunk(fast ? M : 0);
+                    const int32_t adv = x ? (int32_t)(__builtin_ctz(x) >> S::kShift) : S::kStep;
                     Mv[c] = fast ? M + adv : M;
                     more |= (fast && !x) ? 1u << c : 0u;
                 }
@@ -258,6 +295,39 @@ __device__ __forceinline__ lds_cu8 *stage(const uint8_t *src, int32_t len, lds_c
     return dst + (a & 15);
 }
 
+// The 2-bit codes of len bytes at src into LDS words at dst (word i: the 16
+// bytes at (src & ~15) + 16 i), two zero words after them; returns whether
+// every byte of the sequence is A, C, G or T (wave-uniform).
+__device__ __forceinline__ bool stage_codes(const uint8_t *src, int32_t len, lds_cu8_raw *dst) {
+    const uintptr_t a = (uintptr_t)src, base = a & ~(uintptr_t)15;
+    const int32_t off = (int32_t)(a & 15);
+    const int32_t nblk = (off + len + 15) / 16;
+    typedef __attribute__((address_space(3))) uint32_t lds_u32;
+    lds_u32 *w = (lds_u32 *)dst;
+    bool bad = false;
+    for (int32_t i = (int32_t)threadIdx.x; i < nblk + 2; i += 64) {
+        uint32_t code = 0;
+        if (i < nblk) {
+            const uint4 v = ((const uint4 *)base)[i];
+            const uint32_t x[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const uint32_t y = (x[k] >> 1) & 0x03030303u;
+                code |= ((y * 0x00041041u) >> 18 & 0xFFu) << (8u * k);
+#pragma unroll
+                for (int b = 0; b < 4; ++b) {  // the sequence's bytes must be A, C, G, T
+                    const int32_t pos = 16 * i + 4 * k + b - off;
+                    const uint32_t c = (x[k] >> (8 * b)) & 0xFFu;
+                    const bool acgt = c == 'A' || c == 'C' || c == 'G' || c == 'T';
+                    bad |= pos >= 0 && pos < len && !acgt;
+                }
+            }
+        }
+        w[i] = code;
+    }
+    return !__builtin_amdgcn_ballot_w64(bad);
+}
+
 template <typename OffT>
 __global__ __launch_bounds__(64) void wfa_affine_kernel(const WfaAffPair *__restrict__ pairs,
                                                         uint32_t n_pairs,
@@ -265,6 +335,7 @@ __global__ __launch_bounds__(64) void wfa_affine_kernel(const WfaAffPair *__rest
                                                         const uint8_t *__restrict__ ds,
                                                         WfaAffParams prm,
                                                         const uint32_t *__restrict__ n_dev,
+                                                        uint32_t *__restrict__ next,
                                                         int32_t *__restrict__ scores) {
     if (n_dev) n_pairs = *n_dev;
     extern __shared__ __attribute__((aligned(16))) uint8_t lds_raw[];
@@ -277,7 +348,11 @@ __global__ __launch_bounds__(64) void wfa_affine_kernel(const WfaAffPair *__rest
     lds_cu8_raw *sbuf = (lds_cu8_raw *)(((uintptr_t)(Dr + prm.RI * prm.W) + 15) & ~(uintptr_t)15);
     const int32_t lane = (int32_t)threadIdx.x;
 
-    for (uint32_t pi = blockIdx.x; pi < n_pairs; pi += gridDim.x) {
+    for (;;) {
+        uint32_t got = 0;
+        if (lane == 0) got = __hip_atomic_fetch_add(next, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t pi = __builtin_amdgcn_readlane(got, 0);
+        if (pi >= n_pairs) break;
         const WfaAffPair p = pairs[pi];
         const int32_t lq = (int32_t)p.lq, ld = (int32_t)p.ld;
         const uint8_t *__restrict__ q = qs + p.q_off;
@@ -288,24 +363,42 @@ __global__ __launch_bounds__(64) void wfa_affine_kernel(const WfaAffPair *__rest
             result = len == 0 ? 0 : prm.o + prm.e * len;
             if (result > prm.max_score) result = -1;
         } else {
-            const int32_t qspan = (lq + 47) & ~15;  // staged q: +15 lead, +16 tail pad
-            if (qspan + ld + 48 <= prm.seqcap) {
+            auto run = [&](auto safe_c, const auto &Q, const auto &D) __attribute__((always_inline)) {
+                constexpr bool kS = decltype(safe_c)::value;
+                return prm.W == 512    ? wfa_pair<OffT, 8, kS>(Q, lq, D, ld, prm, rng, Mr, Ir, Dr)
+                       : prm.W == 1024 ? wfa_pair<OffT, 16, kS>(Q, lq, D, ld, prm, rng, Mr, Ir, Dr)
+                                       : wfa_pair<OffT, 32, kS>(Q, lq, D, ld, prm, rng, Mr, Ir, Dr);
+            };
+            // staged 2-bit codes, else staged bytes, else HBM
+            const int32_t qa = (int32_t)((uintptr_t)q & 15), da = (int32_t)((uintptr_t)d & 15);
+            const int32_t qwords = (qa + lq + 15) / 16 + 2, dwords = (da + ld + 15) / 16 + 2;
+            const int32_t qspan = (lq + 47) & ~15;  // staged q bytes: +15 lead, +16 tail pad
+            bool done = false;
+            result = 0;
+            if (4 * (qwords + dwords) <= prm.seqcap) {
+                __builtin_amdgcn_wave_barrier();
+                const bool okq = stage_codes(q, lq, sbuf);
+                const bool okd = stage_codes(d, ld, sbuf + 4 * qwords);
+                __builtin_amdgcn_s_waitcnt(0xC07F);
+                __builtin_amdgcn_wave_barrier();
+                if (okq && okd) {
+                    const SeqCodes Q{(lds_cu32 *)sbuf, qa};
+                    const SeqCodes D{(lds_cu32 *)(sbuf + 4 * qwords), da};
+                    result = run(std::true_type{}, Q, D);
+                    done = true;
+                }
+            }
+            if (!done && qspan + ld + 48 <= prm.seqcap) {
                 __builtin_amdgcn_wave_barrier();
                 lds_cu8 *lq8 = stage(q, lq, sbuf);
                 lds_cu8 *ld8 = stage(d, ld, sbuf + qspan);
                 __builtin_amdgcn_s_waitcnt(0xC07F);
                 __builtin_amdgcn_wave_barrier();
-                result = prm.W == 512    ? wfa_pair<OffT, 8, true>(lq8, lq, ld8, ld, prm, rng, Mr, Ir, Dr)
-                         : prm.W == 1024 ? wfa_pair<OffT, 16, true>(lq8, lq, ld8, ld, prm, rng, Mr, Ir, Dr)
-                                         : wfa_pair<OffT, 32, true>(lq8, lq, ld8, ld, prm, rng, Mr, Ir, Dr);
-            } else if (lq >= 8 && ld >= 8) {
-                result = prm.W == 512    ? wfa_pair<OffT, 8, true>(q, lq, d, ld, prm, rng, Mr, Ir, Dr)
-                         : prm.W == 1024 ? wfa_pair<OffT, 16, true>(q, lq, d, ld, prm, rng, Mr, Ir, Dr)
-                                         : wfa_pair<OffT, 32, true>(q, lq, d, ld, prm, rng, Mr, Ir, Dr);
-            } else {
-                result = prm.W == 512    ? wfa_pair<OffT, 8, false>(q, lq, d, ld, prm, rng, Mr, Ir, Dr)
-                         : prm.W == 1024 ? wfa_pair<OffT, 16, false>(q, lq, d, ld, prm, rng, Mr, Ir, Dr)
-                                         : wfa_pair<OffT, 32, false>(q, lq, d, ld, prm, rng, Mr, Ir, Dr);
+                result = run(std::true_type{}, SeqBytes<lds_cu8 *>{lq8}, SeqBytes<lds_cu8 *>{ld8});
+            } else if (!done && lq >= 8 && ld >= 8) {
+                result = run(std::true_type{}, SeqBytes<const uint8_t *>{q}, SeqBytes<const uint8_t *>{d});
+            } else if (!done) {
+                result = run(std::false_type{}, SeqBytes<const uint8_t *>{q}, SeqBytes<const uint8_t *>{d});
             }
         }
         if (lane == 0) scores[p.out] = result;
@@ -324,16 +417,16 @@ size_t wfa_affine_lds_bytes(const WfaAffParams &prm, bool wide) {
 
 hipError_t launch_wfa_affine(const WfaAffPair *pairs, uint32_t n, const uint8_t *qs,
                              const uint8_t *ds, const WfaAffParams &prm, bool wide,
-                             uint32_t grid, const uint32_t *n_dev, int32_t *scores,
+                             uint32_t grid, const uint32_t *n_dev, uint32_t *next, int32_t *scores,
                              hipStream_t stream) {
     if (!n) return hipSuccess;
     const size_t lds = wfa_affine_lds_bytes(prm, wide);
     if (wide)
         wfa_affine_kernel<int32_t><<<dim3(grid), dim3(64), lds, stream>>>(pairs, n, qs, ds, prm,
-                                                                          n_dev, scores);
+                                                                          n_dev, next, scores);
     else
         wfa_affine_kernel<int16_t><<<dim3(grid), dim3(64), lds, stream>>>(pairs, n, qs, ds, prm,
-                                                                          n_dev, scores);
+                                                                          n_dev, next, scores);
     return hipGetLastError();
 }
 
