@@ -826,7 +826,11 @@ def leg_cli(saln, n: int = 316, cpu: bool = True, max_blocks: int = 1, gmut: boo
         if max_blocks:
             cmd += ["--max-blocks", str(max_blocks)]
         walls = []
-        for _ in range(4):  # the first run also pages in the library; value: the median of 3
+        for k in range(4):  # the first run also pages in the library; value: the median of 3
+            # a fresh output file per run (the previous run's pages are freed
+            # outside the timed region, not while this one writes)
+            if k:
+                os.remove(of)
             with open(of, "wb") as out:
                 t0 = time.perf_counter()
                 r = subprocess.run(cmd, stdout=out, stderr=subprocess.PIPE, timeout=600)
