@@ -72,7 +72,7 @@ def nw_align_sharded(queries, dbs, *, scoring=None, device: int | None = None):
     import torch.distributed as dist
 
     from . import _lib
-    from .nw import nw_align_batch
+    from .nw import CigarBatch, nw_align_batch
     world, rank = dist.get_world_size(), dist.get_rank()
     dev = torch.cuda.current_device() if device is None else device
     lo, hi = shard_db([len(d) for d in dbs], world, rank)
@@ -81,21 +81,23 @@ def nw_align_sharded(queries, dbs, *, scoring=None, device: int | None = None):
     tdev = torch.device("cuda", dev) if backend == "nccl" else torch.device("cpu")
     rec = torch.from_numpy(res.view(np.int32).copy()).to(tdev)
     allrec = gather_records(rec)
-    # CIGARs: lengths, then the words, through the same gather
-    flat = [((n << 4) | {"=": 7, "X": 8, "I": 1, "D": 2}[op]) for c in cigs for n, op in c]
-    lens = torch.tensor([len(c) for c in cigs], dtype=torch.int64, device=tdev)
-    cw = torch.tensor(flat, dtype=torch.int64, device=tdev)
+    # CIGARs: lengths, then the words (the engine's length << 4 | op), through
+    # the same gather
+    lens_np = np.asarray(res["cigar_len"], np.int64)
+    flat = (np.concatenate([cigs.words(k) for k in range(len(cigs))]).astype(np.int64)
+            if len(cigs) else np.zeros(0, np.int64))
+    lens = torch.from_numpy(lens_np).to(tdev)
+    cw = torch.from_numpy(flat).to(tdev)
     all_lens = gather_records(lens)
     all_words = gather_records(cw)
     if rank != 0:
         return None, None
     out = allrec.cpu().numpy().astype(np.int32).view(_lib.RESULT_DTYPE)
-    cig, pos = [], 0
-    words = all_words.cpu().numpy()
-    for n in all_lens.cpu().numpy():
-        cig.append([(int(w) >> 4, _lib.CIGAR_OPS[int(w) & 15]) for w in words[pos:pos + n]])
-        pos += int(n)
-    return out, cig
+    n_all = all_lens.cpu().numpy().astype(np.int64)
+    off = np.zeros(len(n_all), np.int64)
+    if len(n_all) > 1:
+        off[1:] = np.cumsum(n_all)[:-1]
+    return out, CigarBatch(all_words.cpu().numpy().astype(np.uint32), off, n_all)
 
 
 def shard_counts(db_lengths, world: int) -> list[tuple[int, int]]:

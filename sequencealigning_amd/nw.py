@@ -11,6 +11,7 @@ reference's exact text.  All compute runs in libsaln's HIP kernels.
 from __future__ import annotations
 
 import ctypes as C
+from collections.abc import Sequence
 from dataclasses import dataclass
 
 import numpy as np
@@ -40,6 +41,44 @@ class NwAlignment:
 
 def _decode_cigar(words) -> list[tuple[int, str]]:
     return [(int(w) >> 4, _lib.CIGAR_OPS[int(w) & 15]) for w in words]
+
+
+class CigarBatch(Sequence):
+    """The first printed alignments of a batch, decoded on access: item k is
+    pair k's CIGAR as [(length, op), ...] (op in '=', 'X', 'I', 'D'); words(k)
+    is its raw (length << 4 | op) words.  Indexable, iterable and comparable
+    like the list it stands for, without building ~30 tuples per pair up
+    front (10^5 pairs: ~1.3 s in Python)."""
+
+    def __init__(self, words: np.ndarray, offsets: np.ndarray, lengths: np.ndarray):
+        self._w, self._o, self._n = words, offsets, lengths
+
+    def __len__(self) -> int:
+        return len(self._n)
+
+    def words(self, k: int) -> np.ndarray:
+        o = int(self._o[k])
+        return self._w[o:o + int(self._n[k])]
+
+    def __getitem__(self, k):
+        if isinstance(k, slice):
+            return [self[i] for i in range(*k.indices(len(self)))]
+        if k < 0:
+            k += len(self)
+        if not 0 <= k < len(self):
+            raise IndexError(k)
+        return _decode_cigar(self.words(k))
+
+    def __eq__(self, other) -> bool:
+        if not isinstance(other, Sequence) or isinstance(other, (str, bytes)):
+            return NotImplemented
+        return len(self) == len(other) and all(self[k] == other[k] for k in range(len(self)))
+
+    def __ne__(self, other) -> bool:
+        eq = self.__eq__(other)
+        return eq if eq is NotImplemented else not eq
+
+    __hash__ = None
 
 
 def cigar_ops_string(cigar: list[tuple[int, str]]) -> str:
@@ -178,7 +217,8 @@ def nw_align_batch(queries, dbs, pairs=None, mode: Mode = Mode.Global, *, scorin
     """Batched n_w_align.  pairs: None (all-vs-all, db outer / query inner like
     main.rs:61-62) or an (n, 2) array of (query index, db index).  ctx: a
     context of the caller's (_lib.new_context) instead of the per-process one.
-    Returns (results structured array, list of CIGARs or None)."""
+    Returns (results structured array, CIGARs or None): the CIGARs are a
+    CigarBatch, pair k's [(length, op), ...] decoded when read."""
     qs, qo = pack_csr(queries)
     ds, do = pack_csr(dbs)
     if pairs is None:
@@ -209,10 +249,7 @@ def nw_align_batch(queries, dbs, pairs=None, mode: Mode = Mode.Global, *, scorin
     if rc == _lib.NOT_IMPLEMENTED:
         raise AlignmentError("not implemented")
     _lib.check(rc, "saln_nw_align_batch")
-    cigars = None
-    if with_cigar:
-        cigars = [_decode_cigar(cig[int(coff[k]):int(coff[k]) + int(res["cigar_len"][k])])
-                  for k in range(n_pairs)]
+    cigars = CigarBatch(cig, coff[:-1], res["cigar_len"].copy()) if with_cigar else None
     return res, cigars
 
 

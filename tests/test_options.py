@@ -66,3 +66,4 @@ def test_no_experiment_macros_in_product():
     tools/, VERDICT r4 #5)."""
     src = open(os.path.join(ROOT, "sequencealigning_amd", "csrc", "nw_kernels.hip")).read()
     assert not re.findall(r"#\s*(?:ifndef|ifdef|if)\s+SALN_", src)
+
