@@ -418,10 +418,25 @@ __device__ void walk_pack_lds(const NwPairDesc &p, int32_t hend, const uint8_t *
             a, (__attribute__((address_space(3))) void *)(win + w * kWin + s * kSlot), WG::SB, 0,
             0);
     };
+    // Slot S of both windows <- the row W phases ahead: the lane's block B
+    // (window wc) while it walks, block B-1 only when the lane may cross into
+    // it within W rows (col < W + 2: a diagonal path moves a column per row; a
+    // longer I run takes ensure()'s synchronous reload).  The other lanes load
+    // their pair's first segment (one line per pack, cached): every lane
+    // issues exactly NW DMAs per phase, as the counted waits need, but a
+    // finished lane or a far block costs no HBM request (round 5: the
+    // walker's window loads were half of its co-run cost, a no-load timing
+    // probe ran the pipelined C2 step 0.82-0.84 ms against 0.90-0.91).
+    // Sets slot S's validity: wc's when walking, the other window's iff near.
+    static_assert(NW == 2, "two windows: the lane's block and the one left of it");
     auto refill = [&](auto slot_c, const uint8_t *row) __attribute__((always_inline)) {
-        dma(std::integral_constant<uint32_t, 0>{}, slot_c, row + ow0);
-        dma(std::integral_constant<uint32_t, 1>{}, slot_c, row + ow1);
-        if constexpr (NW == 3) dma(std::integral_constant<uint32_t, 2>{}, slot_c, row + ow2);
+        constexpr uint32_t S = decltype(slot_c)::value;
+        const bool near = walking && col < kW + 2u;
+        const bool own0 = walking && wc == 0u, own1 = walking && wc == 1u;
+        dma(std::integral_constant<uint32_t, 0>{}, slot_c, (own0 || near) ? row + ow0 : m);
+        dma(std::integral_constant<uint32_t, 1>{}, slot_c, (own1 || near) ? row + ow1 : m);
+        const uint32_t mine = 1u << (wc * 8u + S), other = 1u << ((wc ^ 1u) * 8u + S);
+        valid = (valid | mine | (near ? other : 0u)) & ~(near ? 0u : other);
     };
     // slot S of the current window not refreshed since a crossing: load it now
     auto ensure = [&](auto slot_c) __attribute__((always_inline)) {
@@ -580,7 +595,6 @@ __device__ void walk_pack_lds(const NwPairDesc &p, int32_t hend, const uint8_t *
         refill(slot_c, ahead);
         rp -= rs;
         --row;
-        valid |= (NW == 3 ? 0x10101u : 0x101u) << S;
     };
     // the first W rows; then exactly NW DMAs per phase, for every lane still walking
     unroll_each([&](auto slot_c) __attribute__((always_inline)) {
