@@ -826,7 +826,7 @@ def leg_cli(saln, n: int = 316, cpu: bool = True, max_blocks: int = 1, gmut: boo
         if max_blocks:
             cmd += ["--max-blocks", str(max_blocks)]
         walls = []
-        for k in range(4):  # the first run also pages in the library; value: the median of 3
+        for k in range(6):  # the first run also pages in the library; value: the median of 5
             # a fresh output file per run (the previous run's pages are freed
             # outside the timed region, not while this one writes)
             if k:
@@ -855,7 +855,7 @@ def leg_cli(saln, n: int = 316, cpu: bool = True, max_blocks: int = 1, gmut: boo
     res = {"workload": f"saln CLI (-a needleman-wunsch {flags}) on {n} x {n} FASTA records, "
                        f"{kind} ({n * n} pairs, seed {SEED:#x})",
            "value": round(cells / float(np.median(walls[1:])) / 1e9, 2),
-           "unit": "GCUPS (process wall time, median of 3 runs after a first)",
+           "unit": "GCUPS (process wall time, median of 5 runs after a first)",
            "stages_ms": stages,
            "wall_s": round(float(np.median(walls[1:])), 3), "wall_s_first": round(walls[0], 3),
            "walls_s": [round(w, 3) for w in walls],

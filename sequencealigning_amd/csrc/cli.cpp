@@ -19,6 +19,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <ctime>
 #include <string>
 #include <thread>
 #include <vector>
@@ -40,6 +41,7 @@ struct Args {
     uint64_t max_blocks = 0;
     uint64_t chunk_pairs = 1u << 14;  // pairs per render batch (the first one: a quarter)
     bool stage_times = false;
+    bool teardown = false;
 };
 
 const char *kUsage =
@@ -61,6 +63,7 @@ const char *kUsage =
     "      --max-blocks <N>           cap on printed alignments per pair [default: 0 = none]\n"
     "      --chunk-pairs <N>          pairs per GPU batch [default: 16384]\n"
     "      --stage-times              stage times of this run on stderr\n"
+    "      --teardown                 the HIP runtime's full tear-down at exit (for profilers)\n"
     "  -h, --help                     Print help\n";
 
 [[noreturn]] void usage_error(const std::string &msg) {
@@ -118,6 +121,8 @@ Args parse_args(int argc, char **argv) {
             a.wfa_steps = (uint32_t)std::strtoul(need("--wfa-steps <N>").c_str(), nullptr, 10);
         } else if (s == "--stage-times") {
             a.stage_times = true;
+        } else if (s == "--teardown") {
+            a.teardown = true;
         } else if (is("--max-blocks", "--max-blocks")) {
             a.max_blocks = std::strtoull(need("--max-blocks <N>").c_str(), nullptr, 10);
         } else if (is("--chunk-pairs", "--chunk-pairs")) {
@@ -247,6 +252,19 @@ bool load(const std::string &path, const char *which, std::vector<Rec> *out) {
 
 std::string as_str(const std::vector<uint8_t> &v) { return std::string(v.begin(), v.end()); }
 
+// The end of a finished run: the output is flushed and every GPU result has
+// been read, so the process leaves without the HIP runtime's tear-down (its
+// queues, code objects and GB-sized device and pinned blocks; after main
+// 4-108 ms against 58-114 ms on MI355X, profiles/r05_cli_exit_ab.jsonl),
+// which the kernel driver reclaims at exit anyway.  --teardown keeps the
+// normal exit (e.g. under a profiler whose exit handlers write its results).
+int leave(int code, bool teardown) {
+    std::fflush(stdout);
+    std::fflush(stderr);
+    if (teardown) return code;
+    std::_Exit(code);
+}
+
 }  // namespace
 
 int main(int argc, char **argv) {
@@ -259,6 +277,16 @@ int main(int argc, char **argv) {
                      std::chrono::duration<double, std::milli>(n - t_mark).count());
         t_mark = n;
     };
+    // wall-clock stamps, so a caller can split its own process time into
+    // start-up before main, main, and tear-down after it
+    auto clock_stamp = [&](const char *what) {
+        if (!a.stage_times) return;
+        timespec ts{};
+        clock_gettime(CLOCK_REALTIME, &ts);
+        std::fprintf(stderr, "[saln-clock] %s %lld\n", what,
+                     static_cast<long long>(ts.tv_sec) * 1000000000LL + ts.tv_nsec);
+    };
+    clock_stamp("main-entry");
     if (a.stage_times) saln_option_set("host.timing", 1);
     // stdout to a file or pipe: large writes (the default 4 KB buffer makes
     // ~10^4 write calls per 45 MB of text); a terminal keeps line buffering
@@ -451,7 +479,7 @@ int main(int argc, char **argv) {
         join_printer();
         std::fflush(stdout);
         if (code != 0) saln_context_destroy(ctx);
-        return code;
+        return code == 0 ? leave(code, a.teardown) : code;
     };
     for (uint64_t p0 = 0; p0 < total;) {
         pq.clear();
@@ -525,7 +553,7 @@ int main(int argc, char **argv) {
     // The context is left to the process exit: destroying it frees the GB-sized
     // device and host blocks one by one (measured 0.26 s at the end of a 10^5-pair
     // run), which the exit's teardown does anyway.
-    std::fflush(stdout);
     mark("exit");
-    return 0;
+    clock_stamp("main-exit");
+    return leave(0, a.teardown);
 }
