@@ -50,6 +50,7 @@ using namespace saln;
 
 
 
+
 struct saln_nw_plan {
     saln_context *ctx = nullptr;
     Options opts{};  // the context's effective options at creation
@@ -641,6 +642,12 @@ int saln_nw_execute(saln_nw_plan *p, const uint8_t *d_q, const uint8_t *d_db,
     FillExtras fx;
     fx.o = &p->opts;
     fx.bail = p->d_bail[cur];
+    // async: the table fills' fallback launches go to the walk stream, behind
+    // the hand-off, so nothing but the hand-off's packets sits between this
+    // fill and the next one on `s` (each packet there left ~5 us idle, rocprof
+    // kernel trace, round 5)
+    std::vector<std::function<hipError_t(hipStream_t)>> fallbacks;
+    if (t != s) fx.deferred = &fallbacks;
     for (int v = 0; v < kNumVariants; ++v) {
         const uint32_t a = p->var_first[v], b = a + p->var_count[v];
         if (a >= b) continue;
@@ -660,9 +667,11 @@ int saln_nw_execute(saln_nw_plan *p, const uint8_t *d_q, const uint8_t *d_db,
                             p->score_only ? 2 : p->full_codes ? 1 : p->nib[v] ? 3 : 0,
                             p->var_maxld[v], s, fx));
     }
-    if (ev) HIP_TRY(hipEventRecord(ev[1], s));
-    HIP_TRY(hipEventRecord(p->sync_ev[0], s));
-    if (t != s) HIP_TRY(hipStreamWaitEvent(t, p->sync_ev[0], 0));
+    // the fill's end (timed: its timing event doubles as the hand-off)
+    hipEvent_t filled = ev ? ev[1] : p->sync_ev[0];
+    HIP_TRY(hipEventRecord(filled, s));
+    if (t != s) HIP_TRY(hipStreamWaitEvent(t, filled, 0));
+    for (auto &fb : fallbacks) HIP_TRY(fb(t));
     if (ev) HIP_TRY(hipEventRecord(ev[2], t));
     for (int v = 0; v < kNumVariants; ++v) {
         const uint32_t a = p->var_first[v], b = a + p->var_count[v];

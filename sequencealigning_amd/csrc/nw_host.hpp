@@ -6,6 +6,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
+#include <functional>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -87,10 +88,15 @@ hipError_t pinned_staging(saln_context *ctx, size_t n, void **p);  // caller hol
 // What a packed fill launch needs besides the pairs: the plan's options, the
 // workspace's bail word and the launch's epoch (4-bit-code table fills: the
 // fallback launch runs only when a wave of its table launch left pairs to it).
+// deferred: when set, the fallback launch is appended there instead of being
+// queued behind the table launch, for the caller to queue on the stream that
+// walks the workspace once the fills are done (pipelined plans: the fill
+// stream then runs the next step's fill without it in between).
 struct FillExtras {
     const Options *o = nullptr;
     uint32_t *bail = nullptr;
     uint32_t epoch = 0;
+    std::vector<std::function<hipError_t(hipStream_t)>> *deferred = nullptr;
 };
 hipError_t launch_fill(int variant, const NwPairDesc *pairs, uint32_t first, uint32_t count,
                        const uint8_t *qs, const uint8_t *ds, uint8_t *mask, int2 *scratch,

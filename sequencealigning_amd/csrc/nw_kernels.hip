@@ -3213,8 +3213,13 @@ static hipError_t fill_pk(dim3 grid, hipStream_t s, const NwPairDesc *pairs, uin
                 if (e != hipSuccess) return e;
                 nw_fill_pk_tab_kernel<G, K, PlanSrc><<<grid, dim3(256), lds_tab, s>>>(
                     src, count, qs, ds, mask, sc, ld_max, fx.bail, fx.epoch);
-                nw_fill_pk_tabfb_kernel<G, K, PlanSrc, kRb><<<grid, dim3(256), lds_tab, s>>>(
-                    src, count, qs, ds, mask, sc, ld_max, fx.bail, fx.epoch);
+                auto fb = [=, bail = fx.bail, epoch = fx.epoch](hipStream_t fs) {
+                    nw_fill_pk_tabfb_kernel<G, K, PlanSrc, kRb><<<grid, dim3(256), lds_tab, fs>>>(
+                        src, count, qs, ds, mask, sc, ld_max, bail, epoch);
+                    return hipGetLastError();
+                };
+                if (fx.deferred) fx.deferred->push_back(fb);
+                else return fb(s);
                 return hipSuccess;
             }
         }

@@ -33,6 +33,12 @@ def main():
         ov = any(min(e, we) > max(s, ws) for ws, we in walks)
         (corun if ov else alone).append((e - s) / 1e6)
     avg = lambda x: round(sum(x) / len(x), 4) if x else None  # noqa: E731
+    # idle time of the fill stream between consecutive pipelined fills (one
+    # fill's end to the next one's start, both beside a walk): the hand-off
+    # packets between steps (fallback launch, event records and waits)
+    co = [(s, e) for s, e in fills if any(min(e, we) > max(s, ws) for ws, we in walks)]
+    gaps = sorted((b[0] - a[1]) / 1e3 for a, b in zip(co, co[1:]) if 0 <= b[0] - a[1] < 200e3)
+    med = lambda x: round(x[len(x) // 2], 2) if x else None  # noqa: E731
     doc = {"trace": os.path.relpath(f), "walks": len(walks), "fills": len(fills),
            "walk_ms_avg": round(sum(e - s for s, e in walks) / max(1, len(walks)) / 1e6, 4),
            "fill_ms_avg": round(sum(e - s for s, e in fills) / max(1, len(fills)) / 1e6, 4),
@@ -40,7 +46,8 @@ def main():
            "walk_overlap_frac_min": round(min(fr), 3) if fr else None,
            "fill_corun_n": len(corun), "fill_corun_ms_avg": avg(corun),
            "fill_alone_n": len(alone), "fill_alone_ms_avg": avg(alone),
-           "trace_span_ms": round(span, 3)}
+           "fill_gap_us_median": med(gaps), "fill_gap_us_min": round(gaps[0], 2) if gaps else None,
+           "fill_gap_n": len(gaps), "trace_span_ms": round(span, 3)}
     print(json.dumps(doc))
     if out:
         json.dump(doc, open(out, "w"), indent=1)
