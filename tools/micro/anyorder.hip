@@ -2,7 +2,8 @@
 // the same stream has finished on gfx950?  Two spin kernels of ~1 ms each on
 // one stream (a few waves, so both fit at once); the wall time of the pair is
 // ~2 ms when the second waits for the first and ~1 ms when they overlap.
-// Also times the gap an event record / cross-stream wait leaves between two
+// Also times the gap an event record / cross-stream wait / timing events
+// (recorded around a kernel, or given to hipExtLaunchKernel) leave between two
 // short kernels.
 // Build: hipcc -O2 --offload-arch=gfx950 anyorder.hip -o anyorder
 #include <hip/hip_ext.h>
@@ -58,12 +59,17 @@ int main() {
         CK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         const uint64_t shortc = 1000;  // ~10 us
         void *sargs[] = {(void *)&shortc, (void *)&out};
-        for (int mode = 0; mode < 3; ++mode) {
+        hipEvent_t te[2];
+        CK(hipEventCreate(&te[0]));
+        CK(hipEventCreate(&te[1]));
+        for (int mode = 0; mode < 5; ++mode) {
             CK(hipDeviceSynchronize());
             auto t0 = std::chrono::steady_clock::now();
             for (int k = 0; k < 200; ++k) {
-                CK(hipExtLaunchKernel((const void *)spin, dim3(8), dim3(64), sargs, 0, s, nullptr,
-                                      nullptr, 0));
+                if (mode == 4) CK(hipEventRecord(te[0], s));
+                CK(hipExtLaunchKernel((const void *)spin, dim3(8), dim3(64), sargs, 0, s,
+                                      mode == 3 ? te[0] : nullptr, mode == 3 ? te[1] : nullptr, 0));
+                if (mode == 4) CK(hipEventRecord(te[1], s));
                 if (mode == 1) CK(hipEventRecord(e, s));
                 if (mode == 2) {
                     CK(hipEventRecord(e, t));
@@ -71,11 +77,18 @@ int main() {
                 }
             }
             CK(hipStreamSynchronize(s));
-            const char *name[] = {"back to back", "event record between", "cross-stream wait between"};
+            const char *name[] = {"back to back", "event record between", "cross-stream wait between",
+                                  "start/stop events of hipExtLaunchKernel",
+                                  "timing events recorded around each"};
             std::printf("{\"test\": \"200 x 10 us kernels, %s\", \"us_per_kernel\": %.2f}\n", name[mode],
                         ms_since(t0) * 1000.0 / 200);
         }
+        float ms = 0;
+        CK(hipEventElapsedTime(&ms, te[0], te[1]));
+        std::printf("{\"test\": \"last timed kernel\", \"us\": %.2f}\n", ms * 1000.0f);
         CK(hipEventDestroy(e));
+        CK(hipEventDestroy(te[0]));
+        CK(hipEventDestroy(te[1]));
     }
     return 0;
 }
