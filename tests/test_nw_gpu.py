@@ -818,3 +818,50 @@ def test_context_options_two_threads(saln, oracle):
     finally:
         for c in ctxs:
             L.saln_context_destroy(c)
+
+
+def test_pipelined_fallback_on_walk_stream(saln):
+    """Pipelined plans queue the table fill's fallback launch (the waves whose
+    pairs hold a byte other than A, C, G, T) on the walk stream behind the
+    hand-off (round 5).  Steps alternate between inputs with ~1 % N bytes and
+    clean ones, so a bailing step is followed by a fill into the other
+    workspace while its fallback and walk run; each must equal the
+    synchronous plan byte for byte."""
+    import torch
+    from sequencealigning_amd import synth
+    n = 4000
+    qs0, qo, ds0, do = synth.iid_pairs(n, 150, 150, seed=0x5EED0041)
+    pairs = np.stack([np.arange(n)] * 2, 1)
+    rng = np.random.default_rng(41)
+    sync_plan = saln.NwPlan(qo, do, pairs=pairs)
+    pipe = saln.NwPlan(qo, do, pairs=pairs)
+    pipe.set_async(True)
+    steps = 6
+    ins, want = [], []
+    for s in range(steps):
+        qs, ds = qs0.copy(), ds0.copy()
+        if s % 2 == 0:
+            qs[rng.random(qs.size) < 0.01] = ord("N")
+            ds[rng.random(ds.size) < 0.01] = ord("N")
+        else:
+            qs = np.roll(qs, s)
+        dq, dd = torch.from_numpy(qs).cuda(), torch.from_numpy(ds).cuda()
+        r = torch.zeros(n * 4, dtype=torch.int32, device="cuda")
+        c = torch.zeros(max(1, sync_plan.cigar_words), dtype=torch.int32, device="cuda")
+        sync_plan.execute(dq, dd, r, c)
+        ins.append((dq, dd))
+        want.append((r, c))
+    got = []
+    for s in range(steps):
+        r = torch.full((n * 4,), -1, dtype=torch.int32, device="cuda")
+        c = torch.zeros(max(1, pipe.cigar_words), dtype=torch.int32, device="cuda")
+        pipe.execute(*ins[s], r, c)
+        got.append((r, c))
+    pipe.sync()
+    pipe.check()
+    torch.cuda.synchronize()
+    for s in range(steps):
+        assert torch.equal(got[s][0], want[s][0]), s
+        assert torch.equal(got[s][1], want[s][1]), s
+    sync_plan.close()
+    pipe.close()
