@@ -118,7 +118,7 @@ int saln_abi_version(void);
  * to change what it runs.  Every option gives the same results.  Names:
  * "nw.wide_min_pairs", "nw.rows_k", "nw.stripe_pk", "nw.spec",
  * "nw.spec_passes", "nw.spec_strict", "nw.avsa_narrow", "nw.rows_lone",
- * "nw.rows_xcd", "nw.avsa_profile", "nw.pk_tab",
+ * "nw.rows_xcd", "nw.avsa_profile", "nw.pk_tab", "nw.walk_waves",
  * "wfa2.seq_lds", "wfa2.w1", "wfa2.w2", "host.timing".
  * Two levels, no other shared state:
  *  - saln_option_*: the process registry, the default of every context;

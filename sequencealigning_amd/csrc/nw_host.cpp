@@ -596,6 +596,17 @@ int saln_nw_plan_kernel_time(const saln_nw_plan *p, const char *kernel, double *
     return SALN_OK;
 }
 
+// Waves of an LDS walk launch (nw.walk_waves; -1 auto).  Beside the next
+// step's fill (async plans) every lane walks two pairs in turn: half the
+// walker waves take SIMD slots from the fill, and the walk still ends inside
+// it (round 5, profiles/r05_walk_waves_ab.jsonl: C2 step 0.853-0.861 ->
+// 0.836-0.846 ms at 768 waves; 512 made the walk outlast the fill, 0.97 ms).
+// Alone, a lane per pair (the shortest walk).
+static uint32_t walk_waves(int64_t opt, uint32_t n, bool beside_fill) {
+    if (opt >= 0) return (uint32_t)opt;
+    return beside_fill ? (n + 127) / 128 : 0;
+}
+
 int saln_nw_execute(saln_nw_plan *p, const uint8_t *d_q, const uint8_t *d_db,
                     saln_nw_result *d_results, uint32_t *d_cigar, void *stream) {
     if (!p || !d_results || (!d_q && p->n_pairs) || (!d_db && p->n_pairs)) return SALN_E_INVALID;
@@ -690,7 +701,8 @@ int saln_nw_execute(saln_nw_plan *p, const uint8_t *d_q, const uint8_t *d_db,
         else
             HIP_TRY(launch_traceback(v, p->d_pairs, a, b - a, d_q, d_db, mask, endh, ops,
                                      d_results, d_cigar, p->sc, p->stripe_layout(), t,
-                                     spec ? p->d_spec_done : nullptr, p->nib[v]));
+                                     spec ? p->d_spec_done : nullptr, p->nib[v],
+                                     walk_waves(p->opts[Opt::WalkWaves], b - a, t != s)));
     }
     // pairs with an empty side (boundary-only walk) ride on the traceback stream
     if (p->n_pairs > p->n_fill && p->score_only)

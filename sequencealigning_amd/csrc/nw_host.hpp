@@ -143,7 +143,8 @@ hipError_t launch_traceback(int variant, const NwPairDesc *pairs, uint32_t first
                             const uint8_t *ds, const uint8_t *mask, const int32_t *end_h,
                             uint32_t *ops, saln_nw_result *results, uint32_t *cigar, Scoring sc,
                             int stripe_layout, hipStream_t stream,
-                            const uint32_t *spec_done = nullptr, bool nib = false);
+                            const uint32_t *spec_done = nullptr, bool nib = false,
+                            uint32_t walk_waves = 0);
 // variants whose walk codes may be 4-bit (kCodesNib): the short-query packed
 // fills 7 (16 x 10) and 4 (8 x 19, 4-bit only)
 inline bool variant_nib(int v) { return v == 7 || v == 4; }

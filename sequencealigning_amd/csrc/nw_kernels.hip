@@ -716,16 +716,20 @@ __global__ __launch_bounds__(256) void nw_traceback_lds_kernel(
     uint32_t *__restrict__ cigar, Scoring sc, const uint8_t *__restrict__ qs) {
     constexpr uint32_t kWave = WalkGeo<K, kNib, G * K>::kWaveLds;
     __shared__ __attribute__((aligned(16))) uint8_t win_all[tb_lds_threads<G, K, kNib>() / 64u * kWave];
-    const uint32_t rel = blockIdx.x * blockDim.x + threadIdx.x;
-    if (rel >= n) return;
-    const uint32_t idx = first + rel;
     // The walk is a latency-bound chain that shares SIMDs with the VALU-bound
     // fill of the next batch in pipelined plans: it issues at the highest
     // priority (round 4: 3 / 1 / 0 gave 0.94 / 0.94 / 0.96 ms per step).
     __builtin_amdgcn_s_setprio(3);
-    const NwPairDesc p = pairs[idx];
     lds_u8 *win = (lds_u8 *)(win_all + (threadIdx.x / 64u) * kWave);
-    walk_pack_lds<G, K, kNib>(p, end_h[idx], mask, ops, results, cigar, sc, win, qs);
+    // a lane per pair; a grid smaller than the pairs walks them in turns (the
+    // wave's lanes start their next pairs together, after the last of the
+    // previous ones has finished)
+    const uint32_t stride = gridDim.x * blockDim.x;
+    for (uint32_t rel = blockIdx.x * blockDim.x + threadIdx.x; rel < n; rel += stride) {
+        const uint32_t idx = first + rel;
+        const NwPairDesc p = pairs[idx];
+        walk_pack_lds<G, K, kNib>(p, end_h[idx], mask, ops, results, cigar, sc, win, qs);
+    }
 }
 
 // One walker per pair.  Pairs with an empty side have no mask and take the
@@ -3454,9 +3458,11 @@ hipError_t launch_fill(int variant, const NwPairDesc *pairs, uint32_t first, uin
 template <int G, int K, bool kNib = false>
 static void tb_lds(hipStream_t s, const NwPairDesc *pairs, uint32_t first, uint32_t n,
                    const uint8_t *mask, const int32_t *end_h, uint32_t *ops, saln_nw_result *res,
-                   uint32_t *cig, Scoring sc, const uint8_t *qs) {
+                   uint32_t *cig, Scoring sc, const uint8_t *qs, uint32_t waves = 0) {
     constexpr uint32_t nt = tb_lds_threads<G, K, kNib>();
-    nw_traceback_lds_kernel<G, K, kNib><<<dim3((n + nt - 1) / nt), dim3(nt), 0, s>>>(
+    uint32_t blocks = (n + nt - 1) / nt;
+    if (waves) blocks = std::min(blocks, std::max(1u, waves / (nt / 64u)));
+    nw_traceback_lds_kernel<G, K, kNib><<<dim3(blocks), dim3(nt), 0, s>>>(
         pairs, first, n, mask, end_h, ops, res, cig, sc, qs);
 }
 
@@ -3467,7 +3473,7 @@ hipError_t launch_traceback(int variant, const NwPairDesc *pairs, uint32_t first
                             const uint8_t *qs, const uint8_t *ds, const uint8_t *mask,
                             const int32_t *end_h, uint32_t *ops, saln_nw_result *results,
                             uint32_t *cigar, Scoring sc, int stripe_layout, hipStream_t stream,
-                            const uint32_t *spec_done, bool nib) {
+                            const uint32_t *spec_done, bool nib, uint32_t walk_waves) {
     if (n == 0) return hipSuccess;
     const dim3 grid((n + 255) / 256);
     if (nib && variant != 4 && variant != 7) return hipErrorInvalidValue;
@@ -3504,7 +3510,8 @@ hipError_t launch_traceback(int variant, const NwPairDesc *pairs, uint32_t first
         }
         case 4:  // 8 x 19 groups: 4-bit codes only (byte segments would not fit a slot)
             if (!nib) return hipErrorInvalidValue;
-            tb_lds<8, 19, true>(stream, pairs, first, n, mask, end_h, ops, results, cigar, sc, qs);
+            tb_lds<8, 19, true>(stream, pairs, first, n, mask, end_h, ops, results, cigar, sc, qs,
+                                walk_waves);
             break;
         case 5: tb_lds<16, 16>(stream, pairs, first, n, mask, end_h, ops, results, cigar, sc, qs); break;
         case 6: tb_lds<32, 16>(stream, pairs, first, n, mask, end_h, ops, results, cigar, sc, qs); break;

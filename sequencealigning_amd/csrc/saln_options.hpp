@@ -29,6 +29,7 @@ enum class Opt : int {
     RowsXcd,            // "nw.rows_xcd": XCD-local neighbours for row fills whose stripes fit the SIMDs
     AvsaProfile,        // "nw.avsa_profile": query-profile penalties in the 8 x 19 all-vs-all fill
     PkTab,              // "nw.pk_tab": table penalties + extension-free frame in the 4-bit-code fills
+    WalkWaves,          // "nw.walk_waves": waves of an LDS walk launch (-1 auto, 0 a lane per pair)
     Wfa2SeqLds,         // "wfa2.seq_lds": LDS bytes for staged sequences (corrected WFA)
     Wfa2W1,             // "wfa2.w1": first-pass ring width (0 auto)
     Wfa2W2,             // "wfa2.w2": second-pass ring width (0 auto)

@@ -865,3 +865,39 @@ def test_pipelined_fallback_on_walk_stream(saln):
         assert torch.equal(got[s][1], want[s][1]), s
     sync_plan.close()
     pipe.close()
+
+
+@pytest.mark.parametrize("waves", [1, 6, 48])
+def test_walker_grid_in_turns(saln, waves):
+    """nw.walk_waves caps the LDS walk launch; each lane then walks several
+    pairs in turn (round 5: two per lane beside the next fill by default).
+    Sequential and pipelined plans with a capped grid equal the uncapped one."""
+    import torch
+    from sequencealigning_amd import synth
+    n = 3000
+    qs, qo, ds, do = synth.iid_pairs(n, 150, 150, seed=0x5EED0042)
+    qs[::97] = ord("N")
+    pairs = np.stack([np.arange(n)] * 2, 1)
+    dq, dd = torch.from_numpy(qs).cuda(), torch.from_numpy(ds).cuda()
+
+    def run(async_, opt):
+        with saln.options(**{"nw.walk_waves": opt}):
+            plan = saln.NwPlan(qo, do, pairs=pairs)
+        plan.set_async(async_)
+        out = []
+        for _ in range(3):
+            r = torch.full((n * 4,), -1, dtype=torch.int32, device="cuda")
+            c = torch.zeros(max(1, plan.cigar_words), dtype=torch.int32, device="cuda")
+            plan.execute(dq, dd, r, c)
+            out.append((r, c))
+        plan.sync()
+        plan.check()
+        torch.cuda.synchronize()
+        plan.close()
+        return out
+
+    want = run(False, 0)
+    for async_ in (False, True):
+        for r, c in run(async_, waves):
+            assert torch.equal(r, want[0][0]), (async_, waves)
+            assert torch.equal(c, want[0][1]), (async_, waves)
