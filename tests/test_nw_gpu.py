@@ -867,15 +867,16 @@ def test_pipelined_fallback_on_walk_stream(saln):
     pipe.close()
 
 
-@pytest.mark.parametrize("waves", [1, 6, 48])
-def test_walker_grid_in_turns(saln, waves):
-    """nw.walk_waves caps the LDS walk launch; each lane then walks several
-    pairs in turn (round 5: two per lane beside the next fill by default).
+@pytest.mark.parametrize("waves,length", [(1, 150), (6, 150), (48, 150)])
+def test_walker_grid_in_turns(saln, waves, length):
+    """nw.walk_waves caps the LDS walk launch of the 8 x 19 variant; each lane
+    then walks several pairs in turn (round 5: two per lane beside the next
+    fill by default).
     Sequential and pipelined plans with a capped grid equal the uncapped one."""
     import torch
     from sequencealigning_amd import synth
     n = 3000
-    qs, qo, ds, do = synth.iid_pairs(n, 150, 150, seed=0x5EED0042)
+    qs, qo, ds, do = synth.iid_pairs(n, length, length, seed=0x5EED0042)
     qs[::97] = ord("N")
     pairs = np.stack([np.arange(n)] * 2, 1)
     dq, dd = torch.from_numpy(qs).cuda(), torch.from_numpy(ds).cuda()

@@ -21,6 +21,7 @@ def main():
     ap.add_argument("--steps", type=int, default=40)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--pairs", type=int, default=100_000)
+    ap.add_argument("--len", type=int, default=150, help="query and db length (150: configs[1])")
     ap.add_argument("--tag", default="")
     ap.add_argument("--pipeline", action="store_true",
                     help="the bench's default loop: step k's walk beside step k+1's fill")
@@ -35,7 +36,7 @@ def main():
     for kv in a.opt:
         k, v = kv.split("=")
         _lib.set_option(k, int(v))
-    n, L = a.pairs, 150
+    n, L = a.pairs, a.len
     qs, qo, ds, do = synth.iid_pairs(n, L, L, seed=0x5EED0002)
     plan = saln.NwPlan(qo, do, pairs=np.stack([np.arange(n)] * 2, 1))
     dq, dd = torch.from_numpy(qs).cuda(), torch.from_numpy(ds).cuda()
