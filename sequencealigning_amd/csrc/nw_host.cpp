@@ -496,6 +496,8 @@ int saln::plan_create(saln_context *ctx, const uint64_t *q_off, uint64_t n_q,
                                hipMemcpyHostToDevice)) != hipSuccess ||
                 (e = dev_alloc(p->ctx, (void **)&p->d_prog, p->n_prog * sizeof(uint32_t))) != hipSuccess ||
                 (e = dev_alloc(p->ctx, (void **)&p->d_err, kErrWords * sizeof(uint32_t))) != hipSuccess ||
+                // every XCD slot cleared: a recycled block must not hold a live epoch
+                (e = hipMemset(p->d_err, 0, kErrWords * sizeof(uint32_t))) != hipSuccess ||
                 (e = hipMemcpy(p->d_err, std::array<uint32_t, 2>{0u, kWaitLimitDefault}.data(),
                                2 * sizeof(uint32_t), hipMemcpyHostToDevice)) != hipSuccess)
                 return fail(e, "stripe work list");
@@ -652,7 +654,6 @@ int saln_nw_execute(saln_nw_plan *p, const uint8_t *d_q, const uint8_t *d_db,
     // fills on `s`, then the walks on `t` (async: beside the next fill)
     FillExtras fx;
     fx.o = &p->opts;
-    fx.bail = p->d_bail[cur];
     // async: the table fills' fallback launches go to the walk stream, behind
     // the hand-off, so nothing but the hand-off's packets sits between this
     // fill and the next one on `s` (each packet there left ~5 us idle, rocprof
@@ -673,6 +674,9 @@ int saln_nw_execute(saln_nw_plan *p, const uint8_t *d_q, const uint8_t *d_db,
             continue;
         }
         fx.epoch = ++p->epoch;
+        // one bail word per 4-bit-code variant: two table fills queued before
+        // either deferred fallback runs must not overwrite each other's epoch
+        fx.bail = p->d_bail[cur] ? p->d_bail[cur] + (v == 7 ? 1 : 0) : nullptr;
         HIP_TRY(launch_fill(v, p->d_pairs, a, b - a, d_q, d_db, mask, p->d_scratch, endh,
                             d_results, d_cigar, p->sc,
                             p->score_only ? 2 : p->full_codes ? 1 : p->nib[v] ? 3 : 0,

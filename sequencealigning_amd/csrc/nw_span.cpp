@@ -238,6 +238,8 @@ int saln_nw_span_create(saln_context *ctx, uint64_t len_q, uint64_t len_db, uint
         (e = dev_alloc(ctx, (void **)&s->d_work, work.size() * sizeof(uint2))) != hipSuccess ||
         (e = hipMemcpy(s->d_work, work.data(), work.size() * sizeof(uint2), hipMemcpyHostToDevice)) != hipSuccess ||
         (e = dev_alloc(ctx, (void **)&s->d_err, kErrWords * sizeof(uint32_t))) != hipSuccess ||
+        // every XCD slot cleared: a recycled block must not hold a live epoch
+        (e = hipMemset(s->d_err, 0, kErrWords * sizeof(uint32_t))) != hipSuccess ||
         (e = hipMemcpy(s->d_err, err0, sizeof err0, hipMemcpyHostToDevice)) != hipSuccess ||
         (e = dev_alloc(ctx, (void **)&s->d_endh, sizeof(int32_t))) != hipSuccess ||
         (e = dev_alloc(ctx, (void **)&s->d_blocks, sizeof blk)) != hipSuccess ||

@@ -80,6 +80,16 @@ class CigarBatch(Sequence):
 
     __hash__ = None
 
+    def tolist(self) -> list:
+        """A real list of every pair's CIGAR (for json.dumps, isinstance checks)."""
+        return [self[k] for k in range(len(self))]
+
+    def __add__(self, other) -> list:
+        return self.tolist() + list(other)
+
+    def __radd__(self, other) -> list:
+        return list(other) + self.tolist()
+
 
 def cigar_ops_string(cigar: list[tuple[int, str]]) -> str:
     """Expanded one-char-per-column op string ('=', 'X', 'I', 'D')."""

@@ -20,3 +20,20 @@ def test_cigar_batch_sequence_semantics():
     assert cb != want[:2] and cb != [want[0], want[2], want[1]]
     assert pickle.loads(pickle.dumps(cb)) == cb
     assert list(cb.words(2)) == [(2 << 4) | 1, (5 << 4) | 2]
+
+
+def test_cigar_batch_list_operations():
+    """list-only operations on a CigarBatch (concatenation,
+    json.dumps through tolist(), isinstance(list)) have a real-list path."""
+    import json
+
+    import numpy as np
+
+    from sequencealigning_amd.nw import CigarBatch
+    words = np.array([(3 << 4) | 7, (2 << 4) | 1], np.uint32)
+    cb = CigarBatch(words, np.array([0, 1], np.uint64), np.array([1, 1], np.uint32))
+    lst = cb.tolist()
+    assert isinstance(lst, list) and lst == [[(3, "=")], [(2, "I")]]
+    assert cb + [[(1, "X")]] == lst + [[(1, "X")]]
+    assert [[(1, "X")]] + cb == [[(1, "X")]] + lst
+    assert json.loads(json.dumps(cb.tolist())) == [[[3, "="]], [[2, "I"]]]

@@ -867,6 +867,72 @@ def test_pipelined_fallback_on_walk_stream(saln):
     pipe.close()
 
 
+@pytest.mark.parametrize("waves", [-1, 1, 7])
+def test_pipelined_mixed_variants_bail(saln, oracle, waves):
+    """one async plan holding both 4-bit-code variants
+    (150-column queries: 8 x 19; 156-column: 16 x 10) whose table fills both
+    bail (N bytes in each), so both fallbacks are queued on the walk stream
+    behind the two table launches.  Each variant has its own bail word; every
+    step must equal the synchronous plan.  n = 4001 pairs (not a multiple of
+    the walk grid's lanes) and explicit walk grids of 1 and 7 waves."""
+    import torch
+    from sequencealigning_amd import synth
+    n = 4001
+    lq = np.where(np.arange(n) % 2 == 0, 150, 156).astype(np.int64)
+    ld = np.full(n, 150, np.int64)
+    qo = np.concatenate([[0], np.cumsum(lq)]).astype(np.uint64)
+    do = np.concatenate([[0], np.cumsum(ld)]).astype(np.uint64)
+    qs0 = synth.random_bases(0x5EED0043, int(qo[-1]))
+    ds0 = synth.random_bases(0x5EED0044, int(do[-1]))
+    pairs = np.stack([np.arange(n)] * 2, 1)
+    rng = np.random.default_rng(43)
+    with saln.options(**{"nw.walk_waves": waves}):
+        sync_plan = saln.NwPlan(qo, do, pairs=pairs)
+        pipe = saln.NwPlan(qo, do, pairs=pairs)
+    pipe.set_async(True)
+    steps = 5
+    ins, want = [], []
+    for s in range(steps):
+        qs, ds = qs0.copy(), ds0.copy()
+        if s % 2 == 0:  # N bytes in pairs of both variants
+            qs[rng.random(qs.size) < 0.004] = ord("N")
+            ds[rng.random(ds.size) < 0.004] = ord("N")
+        else:
+            ds = np.roll(ds, s)
+        dq, dd = torch.from_numpy(qs).cuda(), torch.from_numpy(ds).cuda()
+        r = torch.zeros(n * 4, dtype=torch.int32, device="cuda")
+        c = torch.zeros(max(1, sync_plan.cigar_words), dtype=torch.int32, device="cuda")
+        sync_plan.execute(dq, dd, r, c)
+        ins.append((dq, dd))
+        want.append((r, c))
+    got = []
+    for s in range(steps):
+        r = torch.full((n * 4,), -1, dtype=torch.int32, device="cuda")
+        c = torch.zeros(max(1, pipe.cigar_words), dtype=torch.int32, device="cuda")
+        pipe.execute(*ins[s], r, c)
+        got.append((r, c))
+    pipe.sync()
+    pipe.check()
+    sync_plan.check()
+    torch.cuda.synchronize()
+    for s in range(steps):
+        assert torch.equal(got[s][0], want[s][0]), s
+        assert torch.equal(got[s][1], want[s][1]), s
+    # the N step against the oracle for every pair (both variants bailed)
+    res = want[0][0].cpu().numpy().view(saln._lib.RESULT_DTYPE)
+    cig = want[0][1].cpu().numpy().view(np.uint32)
+    ref = oracle.check_pairs(ins[0][0].cpu().numpy(), qo, ins[0][1].cpu().numpy(), do)
+    assert np.array_equal(res["score"], ref.score)
+    assert np.array_equal(res["end_states"], ref.end_states)
+    assert np.array_equal(res["printed"].astype(bool), ref.cig_len >= 0)
+    for k in range(n):
+        if res["printed"][k]:
+            o0 = int(sync_plan.cigar_off[k])
+            assert np.array_equal(cig[o0:o0 + int(res["cigar_len"][k])], ref.cigar_words(k)), k
+    sync_plan.close()
+    pipe.close()
+
+
 @pytest.mark.parametrize("waves,length", [(1, 150), (6, 150), (48, 150)])
 def test_walker_grid_in_turns(saln, waves, length):
     """nw.walk_waves caps the LDS walk launch of the 8 x 19 variant; each lane
