@@ -31,7 +31,7 @@ and `cpu_baseline`:
   cli       the drop-in CLI end to end on a 316 x 316-record FASTA of 150 bp
       (batched render, reference text per pair; process wall time) (N = 1).
 
-    python bench.py --gpus N --steps K --warmup W [--legs c5,c1,c3,c3_affine,c4,c4_spans,host,cli|none]
+    python bench.py --gpus N --steps K --warmup W [--legs c2_full,c5,c1,c3,c3_affine,c4,c4_spans,host,cli|none]
 
 With --gpus N > 1 and no WORLD_SIZE in the environment this process starts
 the N ranks itself (torch.distributed.run on 127.0.0.1, as a child process;
@@ -62,7 +62,7 @@ VALU_PEAK_TOPS = 1024 * 32 * 2.4e9 / 1e12  # 78.6 T lane-ops/s
 VALU_PK_TOPS = 1024 * 16 * 2.4e9 / 1e12
 N_PAIRS, LQ, LD = 100_000, 150, 150
 SEED = 0x5EED0002
-ALL_LEGS = ("c5", "c1", "c3", "c3_affine", "c4", "c4_spans", "host", "cli", "cli_all")
+ALL_LEGS = ("c2_full", "c5", "c1", "c3", "c3_affine", "c4", "c4_spans", "host", "cli", "cli_all")
 PMC_FILES = ("pmc_traffic.json", "pmc_legs.json")  # under profiles/
 
 
@@ -505,6 +505,71 @@ def leg_c1(torch, saln, reps=50, cpu=True):
     out["checked"] = "score, panic status and the first printed CIGAR of both pairs"
     out["speedup_vs_cpu"] = round(cpu_s * 1e3 / g["execute_ms"], 1)
     return out
+
+
+def leg_c2_full(torch, saln, n=N_PAIRS, steps=10, warmup=2):
+    """configs[1] as SURVEY 8(d) defines it: 10^5 G-iid 150x150 pairs, fill +
+    the reference's full parent sets stored (1 B/cell, the 7 parent bits of
+    needleman_wunsch_affine.rs:96-153 that the all-blocks DFS :281-329 reads;
+    saln_nw_plan_create_full) + the first printed traceback / CIGAR, pipelined
+    like the headline (the headline stores 4-bit walk codes instead)."""
+    from sequencealigning_amd import synth
+    qs, qo, ds, do = synth.iid_pairs(n, LQ, LD, seed=SEED)
+    plan = saln.NwPlan(qo, do, pairs=np.stack([np.arange(n), np.arange(n)], 1), full_codes=True)
+    dq, dd = torch.from_numpy(qs).cuda(), torch.from_numpy(ds).cuda()
+    plan.set_async(True)
+    res = [torch.zeros(n * 4, dtype=torch.int32, device="cuda") for _ in range(2)]
+    cig = [torch.zeros(max(1, plan.cigar_words), dtype=torch.int32, device="cuda")
+           for _ in range(2)]
+    for k in range(warmup):
+        plan.execute(dq, dd, res[k % 2], cig[k % 2])
+    plan.sync()
+    torch.cuda.synchronize()
+    plan.set_timing(True)
+    t0 = time.perf_counter()
+    for k in range(steps):
+        plan.execute(dq, dd, res[k % 2], cig[k % 2])
+    plan.sync()
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / steps
+    plan.check()
+    fill_ms, fill_n = plan.kernel_time("nw_fill")
+    tb_ms, tb_n = plan.kernel_time("nw_traceback")
+    last = (steps - 1) % 2
+    hr = res[last].cpu().numpy()
+    verified = verify_c2(hr, cig[last].cpu().numpy().view(np.uint32), plan.cigar_off, qs, qo, ds,
+                         do)
+    plan.set_async(False)
+    plan.set_timing(True)
+    for _ in range(5):
+        plan.execute(dq, dd, res[0], cig[0])
+    torch.cuda.synchronize()
+    plan.check()
+    fa_ms, fa_n = plan.kernel_time("nw_fill")
+    # the dense parent sets of one pair of the timed plan, against the oracle (untimed)
+    from oracle import refcpu  # checker only
+    mask_ok = all(np.array_equal(plan.dense_mask(k), refcpu.nw(
+        qs[qo[k]:qo[k + 1]].tobytes(), ds[do[k]:do[k + 1]].tobytes(),
+        literal_dfs=False).dense_mask) for k in (0, n // 2, n - 1))
+    cells = plan.cells
+    plan.close()
+    fill_s, alone_s = fill_ms / max(1, fill_n) / 1e3, fa_ms / max(1, fa_n) / 1e3
+    kern = "nw_fill_pk_kernel<16, 10, 1, PlanSrc, 10, false>"
+    return {"workload": "configs[1] as SURVEY 8(d) defines it: 10^5 independent 150x150 G-iid "
+                        "pairs, fill + full 1 B/cell parent sets (7 bits: argmax {M,I,D}, I and "
+                        "D extend/open) + first-printed traceback/CIGAR, pipelined",
+            "value": round(cells / dt / 1e9, 2), "unit": "GCUPS", "ms_per_step": round(dt * 1e3, 4),
+            "steps": steps, "cells": cells, "executes": warmup + steps + 5,
+            "roofline": roof_hbm(cells, fill_s, kern, pmc(kern),
+                                 kernel_avg_ms_alone=round(alone_s * 1e3, 4),
+                                 frac_alone=round(cells / alone_s / 1e9 / HBM_PEAK_GBS, 4),
+                                 step_frac=round(cells / dt / 1e9 / HBM_PEAK_GBS, 4),
+                                 traceback_avg_ms=round(tb_ms / max(1, tb_n), 4),
+                                 note="algorithmic bytes = 1 B/cell, here also the bytes the "
+                                      "fill stores; traffic from profiles/pmc_legs.json",
+                                 valu=valu_roof(kern, fill_s)),
+            "verified": verified, "dense_mask_equal_oracle": bool(mask_ok),
+            "cpu_baseline": "the headline's (the oracle's fill computes every parent set)"}
 
 
 def leg_c4(torch, saln, reps=3, cpu=True):
@@ -1113,7 +1178,9 @@ def main() -> None:
             "dtype": "i32-exact (i16x2 packed arithmetic)",
             "data": "synthetic (splitmix64 G-iid ACGT)",
             "config": {"workload": ("configs[1]: independent 150x150 NW-affine pairs per GPU "
-                                    "(fill + 1 B/cell parent mask + first-printed traceback/CIGAR)")
+                                    "(fill storing 4-bit walk codes (0.5 B/cell: argI, argD, "
+                                    "I-open, D-open) + first-printed traceback/CIGAR; the full "
+                                    "1 B/cell parent-set variant is leg c2_full)")
                        if not args.score_only else
                        ("score-only 150x150 NW-affine pairs per GPU (the configs[4] per-pair "
                         "mode: score + panic status, no mask)"),
@@ -1147,6 +1214,8 @@ def main() -> None:
                 r = leg_c5(world, rank, local, dist, torch, cpu=cpu)
             elif rank != 0 or world > 1:
                 continue
+            elif leg == "c2_full":
+                r = leg_c2_full(torch, saln)
             elif leg == "c1":
                 r = leg_c1(torch, saln, cpu=cpu)
             elif leg == "c3":

@@ -234,6 +234,20 @@ int saln_nw_plan_create(saln_context *ctx, const uint64_t *q_off, uint64_t n_q,
                         const uint64_t *db_off, uint64_t n_db, const uint32_t *pair_q,
                         const uint32_t *pair_db, uint64_t n_pairs, int32_t mode,
                         const saln_nw_scoring *scoring, saln_nw_plan **out);
+/* The same plan storing the reference's full parent sets: one byte per cell
+ * (7 parent bits: the {M,I,D} argmax set and the I / D extend/open parents,
+ * needleman_wunsch_affine.rs:96-153 - what the all-blocks DFS :281-329
+ * consumes), instead of the walk codes saln_nw_plan_create's fills store.
+ * Execute fills, walks and writes the first printed CIGAR as before;
+ * saln_nw_plan_dense_mask reads a pair's parent sets back. */
+int saln_nw_plan_create_full(saln_context *ctx, const uint64_t *q_off, uint64_t n_q,
+                             const uint64_t *db_off, uint64_t n_db, const uint32_t *pair_q,
+                             const uint32_t *pair_db, uint64_t n_pairs, int32_t mode,
+                             const saln_nw_scoring *scoring, saln_nw_plan **out);
+/* Pair `pair`'s parent sets from the last execute of a synchronous full plan
+ * (waits for it), as saln_nw_dense_mask lays them out: (len_db+1) x (len_q+1)
+ * bytes. */
+int saln_nw_plan_dense_mask(saln_nw_plan *plan, uint64_t pair, uint8_t *out);
 /* mask_bytes: HBM parent-mask workspace (owned by the plan);
  * cigar_words: required length of the device cigar buffer. */
 int saln_nw_plan_info(const saln_nw_plan *plan, uint64_t *mask_bytes, uint64_t *cigar_words,

@@ -83,7 +83,8 @@ WFA_RESULT_DTYPE = [("score", "<i4"), ("status", "<i4"), ("steps", "<u4"), ("aln
 EXPORTS = [
     "saln_context_create", "saln_context_destroy", "saln_last_error", "saln_abi_version",
     "saln_nw_align", "saln_nw_render", "saln_nw_dense_mask", "saln_nw_align_batch",
-    "saln_nw_plan_create", "saln_nw_plan_info", "saln_nw_cigar_offsets", "saln_nw_execute",
+    "saln_nw_plan_create", "saln_nw_plan_create_full", "saln_nw_plan_dense_mask",
+    "saln_nw_plan_info", "saln_nw_cigar_offsets", "saln_nw_execute",
     "saln_nw_plan_set_timing", "saln_nw_plan_kernel_time", "saln_nw_plan_set_async",
     "saln_nw_plan_set_score_only", "saln_nw_plan_sync", "saln_nw_plan_destroy",
     "saln_nw_plan_status", "saln_nw_plan_set_wait_limit",
@@ -164,6 +165,8 @@ def lib() -> C.CDLL:
         L.saln_nw_plan_create.argtypes = [vp, vp, C.c_uint64, vp, C.c_uint64, vp, vp,
                                           C.c_uint64, C.c_int32, C.POINTER(NwScoring),
                                           C.POINTER(vp)]
+        L.saln_nw_plan_create_full.argtypes = L.saln_nw_plan_create.argtypes
+        L.saln_nw_plan_dense_mask.argtypes = [vp, C.c_uint64, vp]
         L.saln_nw_plan_info.argtypes = [vp, u64p, u64p, u64p]
         L.saln_nw_cigar_offsets.argtypes = [vp, vp]
         L.saln_nw_execute.argtypes = [vp, vp, vp, vp, vp, vp]

@@ -195,6 +195,32 @@ int saln_nw_plan_create(saln_context *ctx, const uint64_t *q_off, uint64_t n_q,
                              scoring, false, out);
 }
 
+int saln_nw_plan_create_full(saln_context *ctx, const uint64_t *q_off, uint64_t n_q,
+                             const uint64_t *db_off, uint64_t n_db, const uint32_t *pair_q,
+                             const uint32_t *pair_db, uint64_t n_pairs, int32_t mode,
+                             const saln_nw_scoring *scoring, saln_nw_plan **out) {
+    return saln::plan_create(ctx, q_off, n_q, db_off, n_db, pair_q, pair_db, n_pairs, mode,
+                             scoring, true, out);
+}
+
+int saln_nw_plan_dense_mask(saln_nw_plan *p, uint64_t pair, uint8_t *out) {
+    if (!p || !out || pair >= p->n_pairs) return SALN_E_INVALID;
+    if (p->async_tb) {  // the mask of the last execute may sit in either workspace
+        set_error("saln_nw_plan_dense_mask: synchronous plans only");
+        return SALN_E_INVALID;
+    }
+    HIP_TRY(hipSetDevice(p->ctx->device));
+    for (int b = 0; b < 2; ++b)
+        if (p->tb_pending[b]) HIP_TRY(hipEventSynchronize(p->tb_done(b)));
+    saln::PairMask pm;
+    const int rc = saln::plan_pair_mask(p, pair, &pm);
+    if (rc != SALN_OK) return rc;
+    const NwPairDesc &d = p->h_pairs[p->plan_index[pair]];
+    const saln::HostMask hm(pm, d.len_q, d.len_db, p->sc);
+    hm.to_dense(out);
+    return SALN_OK;
+}
+
 }  // extern "C"
 
 // Plan creation.  full_codes: the fills store every parent set (host DFS,

@@ -269,8 +269,11 @@ class NwPlan:
     multi-GPU driver."""
 
     def __init__(self, q_off: np.ndarray, db_off: np.ndarray, pairs=None, *, scoring=None,
-                 device: int = 0, ctx=None):
+                 device: int = 0, ctx=None, full_codes: bool = False):
+        """full_codes: the fills store the reference's full parent sets (1 B
+        per cell, saln_nw_plan_create_full) instead of walk codes."""
         self._L = _lib.lib()
+        self.full_codes = bool(full_codes)
         self.device = device
         self.q_off = np.ascontiguousarray(q_off, np.uint64)
         self.db_off = np.ascontiguousarray(db_off, np.uint64)
@@ -286,11 +289,16 @@ class NwPlan:
         self._h = C.c_void_p()
         vp = lambda a: a.ctypes.data_as(C.c_void_p) if a is not None else None  # noqa: E731
         ctx = ctx if ctx is not None else _lib.context(device)
-        _lib.check(self._L.saln_nw_plan_create(ctx, vp(self.q_off), n_q,
-                                               vp(self.db_off), n_db, vp(pq), vp(pd),
-                                               self.n_pairs, int(Mode.Global),
-                                               _lib.scoring_arg(scoring), C.byref(self._h)),
+        create = (self._L.saln_nw_plan_create_full if self.full_codes
+                  else self._L.saln_nw_plan_create)
+        _lib.check(create(ctx, vp(self.q_off), n_q, vp(self.db_off), n_db, vp(pq), vp(pd),
+                          self.n_pairs, int(Mode.Global), _lib.scoring_arg(scoring),
+                          C.byref(self._h)),
                    "saln_nw_plan_create")
+        self._lens = (np.diff(self.q_off)[pq if pq is not None else
+                                          np.arange(self.n_pairs) % max(1, n_q)],
+                      np.diff(self.db_off)[pd if pd is not None else
+                                           np.arange(self.n_pairs) // max(1, n_q)])
         mb, cw, cells = C.c_uint64(), C.c_uint64(), C.c_uint64()
         self._L.saln_nw_plan_info(self._h, C.byref(mb), C.byref(cw), C.byref(cells))
         self.mask_bytes, self.cigar_words, self.cells = mb.value, cw.value, cells.value
@@ -305,6 +313,15 @@ class NwPlan:
             stream = _lib.torch_stream(self.device)
         _lib.check(self._L.saln_nw_execute(self._h, ptr(q_seq), ptr(db_seq), ptr(results),
                                            ptr(cigar), stream), "saln_nw_execute")
+
+    def dense_mask(self, pair: int) -> np.ndarray:
+        """Pair `pair`'s parent sets from the last execute of a synchronous
+        full-code plan: (len_db+1, len_q+1) uint8 (saln_nw_plan_dense_mask)."""
+        lq, ld = int(self._lens[0][pair]), int(self._lens[1][pair])
+        out = np.zeros((ld + 1, lq + 1), np.uint8)
+        _lib.check(self._L.saln_nw_plan_dense_mask(self._h, pair, out.ctypes.data_as(C.c_void_p)),
+                   "saln_nw_plan_dense_mask")
+        return out
 
     def status(self) -> int:
         """Wait for every execute since the last call; return and clear the

@@ -71,7 +71,7 @@ for st in ${STAGES:-smoke tests bench}; do
               find $O/proflegs -name '*kernel_stats.csv' -exec head -20 {} \; | cut -c1-220 ;;
     pmc)   PMC_SETS=${PMC_SETS:-"FETCH_SIZE;WRITE_SIZE;SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU;SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU"} step pmc 900 bash tools/pmc.sh
            python3 tools/pmc_traffic.py gpurun_out/pmc $O/pmc_traffic.json r06 nw > /dev/null || exit 1 ;;
-    pmclegs) PMC_SCRIPT=tools/prof_legs.py PMC_SETS=${PMC_SETS:-"FETCH_SIZE;WRITE_SIZE;SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU"} step pmc_legs 1100 bash tools/pmc.sh --legs ${PROF_LEGS:-c1,c3,c3_affine,c4,c5}
+    pmclegs) PMC_SCRIPT=tools/prof_legs.py PMC_SETS=${PMC_SETS:-"FETCH_SIZE;WRITE_SIZE;SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU"} step pmc_legs 1100 bash tools/pmc.sh --legs ${PROF_LEGS:-c2_full,c1,c3,c3_affine,c4,c5}
            python3 tools/pmc_traffic.py gpurun_out/pmc $O/pmc_legs.json r06 legs > /dev/null || exit 1 ;;
     pmcspans) PMC_SCRIPT=tools/prof_legs.py PMC_SETS="FETCH_SIZE;WRITE_SIZE;SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU" step pmc_spans 600 bash tools/pmc.sh --legs c4_spans
            python3 tools/pmc_traffic.py gpurun_out/pmc $O/pmc_c4_spans.json r06 legs > /dev/null || exit 1 ;;

@@ -1,11 +1,11 @@
-"""Profiling driver for bench.py's legs (c1, c3, c3_affine, c4, c5): each
+"""Profiling driver for bench.py's legs (c2_full, c1, c3, c3_affine, c4, c5): each
 leg's GPU workload exactly as the bench runs it, without its CPU baseline and
 checks; used under rocprofv3 (--kernel-trace --stats, and the --pmc passes of
 tools/pmc.sh).  Writes {leg: executes} (runs of the leg's workload) to
 $PMC_EXECUTES (default gpurun_out/pmc/executes.json) so tools/pmc_traffic.py
 can turn the counters' per-run sums into per-execute figures.
 
-    python tools/prof_legs.py [--legs c1,c3,c3_affine,c4,c4_spans,c5] [--opt name=value ...]
+    python tools/prof_legs.py [--legs c2_full,c1,c3,c3_affine,c4,c4_spans,c5] [--opt name=value ...]
 
 --opt sets engine options (saln_option_set) for the whole run, e.g.
 nw.rows_xcd=0 for the C4 row fill's traffic without XCD-local stripes.
@@ -49,7 +49,7 @@ def c4_spans_serial(torch, n_spans=8, reps=3):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--legs", default="c1,c3,c3_affine,c4,c5")
+    ap.add_argument("--legs", default="c2_full,c1,c3,c3_affine,c4,c5")
     ap.add_argument("--opt", action="append", default=[],
                     help="engine option name=value (saln_option_set), repeatable")
     a = ap.parse_args()
@@ -64,6 +64,8 @@ def main():
     for leg in a.legs.split(","):
         if leg == "c5":
             r = bench.leg_c5(1, 0, 0, None, torch, cpu=False)
+        elif leg == "c2_full":
+            r = bench.leg_c2_full(torch, saln)
         elif leg == "c1":
             r = bench.leg_c1(torch, saln, cpu=False)
         elif leg == "c3":
