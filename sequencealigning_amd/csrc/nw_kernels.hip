@@ -1628,10 +1628,24 @@ __device__ __forceinline__ int fill_pk_body(Src src, uint32_t count, const uint8
                                             const uint8_t *__restrict__ ds,
                                             uint8_t *__restrict__ mask, Scoring sc,
                                             uint32_t ld_max, bool sc_steady) {
-    constexpr bool kTab = kTabMode == 1;  // table body; kTabMode 2: the generic body of its bail-outs
+    // table body (kTabMode 1; 4: the same at scale 4, below); kTabMode 2: the
+    // generic body of its bail-outs
+    constexpr bool kTab = kTabMode == 1 || kTabMode == 4;
     // the extension-free frame (alpha = beta = -2*gap_extend, M~ = H~ + bonus):
     // the table body, and kTabMode 3 = query profiles holding bonuses
-    constexpr bool kFree = kTabMode == 1 || kTabMode == 3;
+    constexpr bool kFree = kTab || kTabMode == 3;
+    // kTabMode 4 (round 6): values carried as V = 4x + p instead of 2x + p
+    // (bit 1 always 0).  The walk tests then have a strict margin on both
+    // sides: argI present <=> (H - 2) - I < 0 (present: -2 + p_H - p_I in
+    // [-2, -1], since a tied I's flag is in H's; absent: >= 4 - 2 - 1), I-open
+    // present <=> (tO + 2) - I >= 1 (absent <= -4 + 3), so each is one full-rate
+    // 32-bit v_sub_u32 on the pair word (a low half's borrow lowers the high
+    // half by 1, which neither margin minds) instead of a quarter-rate
+    // v_pk_sub_i16, and the flag masks (H & ~1, tO | 1) become the two adds.
+    constexpr bool kS4 = kTabMode == 4;
+    constexpr int kSc = kS4 ? 4 : 2;  // value scale
+    // 2V + p (the boundary helpers, the end values) <-> kSc V + p
+    auto up = [](int32_t v2) -> int32_t { return kS4 ? (v2 >> 1) * 4 + (v2 & 1) : v2; };
     static_assert(kTabMode != 3 || kProf, "kTabMode 3: query profiles");
     // The extension-free frame's values lie in a narrow window above about
     // -(6|go| + 6|ge|) (pk_free_ok): biased by kFreeBias they are the bit
@@ -1662,15 +1676,15 @@ __device__ __forceinline__ int fill_pk_body(Src src, uint32_t count, const uint8
     const uint8_t *__restrict__ dA = ds + pa.db_off;
     const uint8_t *__restrict__ dB = ds + pb.db_off;
     const int ldM = ldA > ldB ? ldA : ldB;
-    const int32_t beta = -2 * sc.gap_extend;
+    const int32_t beta = -kSc * sc.gap_extend;
     const int32_t alpha = kFree ? beta : -2 * sc.match - beta;
     const uint32_t kPen = cst2(2 * (sc.match - sc.mismatch));  // 0 < pen <= 32
-    const uint32_t kOpen = cst2(2 * sc.gap_open);
+    const uint32_t kOpen = cst2(kSc * sc.gap_open);
     const uint32_t kDstep = cst2(2 * sc.gap_extend + alpha);
     const int32_t drift = kFree ? 0 : 2 * sc.gap_extend + alpha;  // column-0 X~ per row
     // kTab: the diagonal bonus by (q code ^ d code) and the chars of codes 0-3
-    const uint32_t cm = (uint32_t)(2 * sc.match + alpha + beta) & 0xFFu;
-    const uint32_t cmm = (uint32_t)(2 * sc.mismatch + alpha + beta) & 0xFFu;
+    const uint32_t cm = (uint32_t)(kSc * sc.match + alpha + beta) & 0xFFu;
+    const uint32_t cmm = (uint32_t)(kSc * sc.mismatch + alpha + beta) & 0xFFu;
     const uint32_t kBonus = cm | cmm * 0x01010100u;
     constexpr uint32_t kAcgt = 'A' | 'C' << 8 | 'T' << 16 | 'G' << 24;
     auto acgt = [](uint32_t c) { return c == 'A' || c == 'C' || c == 'G' || c == 'T'; };
@@ -1706,13 +1720,13 @@ __device__ __forceinline__ int fill_pk_body(Src src, uint32_t count, const uint8
             if constexpr (kTabMode == 2) bad |= (j <= lqA && !acgt(ca >> 5)) || (j <= lqB && !acgt(cb >> 5));
             qc[k] = ca | (cb << 16);
         }
-        const int32_t h0 = hs_row0(sc, (uint32_t)j) + beta * j - ctr;     // H~(0, j)
-        const int32_t d1 = ds_row1(sc, (uint32_t)j) + alpha + beta * j - ctr;  // D~(1, j)
+        const int32_t h0 = up(hs_row0(sc, (uint32_t)j)) + beta * j - ctr;     // H~(0, j)
+        const int32_t d1 = up(ds_row1(sc, (uint32_t)j)) + alpha + beta * j - ctr;  // D~(1, j)
         Hp[k] = pkx(h0, h0);
         Dn[k] = pkx(d1, d1);
     }
-    uint32_t hd = pkx(hs_row0(sc, (uint32_t)col0) + beta * col0 - ctr,
-                      hs_row0(sc, (uint32_t)col0) + beta * col0 - ctr);  // H~(r-1, col0)
+    uint32_t hd = pkx(up(hs_row0(sc, (uint32_t)col0)) + beta * col0 - ctr,
+                      up(hs_row0(sc, (uint32_t)col0)) + beta * col0 - ctr);  // H~(r-1, col0)
     uint32_t pubF = 0, pubH = 0;
     // db chars of both pairs, staged once per group in LDS as the packed
     // (A << 5 | B << 21) word of each row; a step reads its row's word from
@@ -1741,7 +1755,7 @@ __device__ __forceinline__ int fill_pk_body(Src src, uint32_t count, const uint8
     }
     asm volatile("s_waitcnt lgkmcnt(0)" : : : "memory");
     __builtin_amdgcn_wave_barrier();
-    if constexpr (kTabMode == 1) {
+    if constexpr (kTab) {
         if (__builtin_amdgcn_ballot_w64(bad)) return 1;  // the wave is left to the fallback launch
     } else if constexpr (kTabMode == 2) {
         if (!__builtin_amdgcn_ballot_w64(bad)) return 2;  // done by the table launch
@@ -1819,8 +1833,8 @@ __device__ __forceinline__ int fill_pk_body(Src src, uint32_t count, const uint8
             sF += kRowAdd;
             sH += kRowAdd;
         } else {
-            const int32_t bF = is_col1(sc, (uint32_t)rb) + alpha * rb + beta - base;
-            const int32_t bH = hs_col0(sc, (uint32_t)rb) + alpha * rb - base;
+            const int32_t bF = up(is_col1(sc, (uint32_t)rb)) + alpha * rb + beta - base;
+            const int32_t bH = up(hs_col0(sc, (uint32_t)rb)) + alpha * rb - base;
             gF = pkx(bF, bF);
             gH = pkx(bH, bH);
         }
@@ -1860,15 +1874,27 @@ __device__ __forceinline__ int fill_pk_body(Src src, uint32_t count, const uint8
                 if constexpr (kCodes == kCodesNib) {
                     // the four walk decisions as signs (set = parent absent):
                     // argI, argD (ties against the flag-free H), I-open, D-open
+                    // (kS4: argI / argD signs set = present, inverted in the merge)
+                    uint32_t s4[4];
+                    if constexpr (kS4) {
+                        const uint32_t Hm = H - 0x00020002u;
+                        const uint32_t tO2 = M + (kOpen + 0x00020002u);
+                        s4[0] = Hm - I;
+                        s4[1] = Hm - D;
+                        s4[2] = tO2 - I;
+                        s4[3] = tO2 - D;
+                        // argM: M - (H - 2) is >= 1 when present, <= -1 when absent
+                        if constexpr (kM) s4[3] = bfi(endsel, M - Hm, s4[3]);
+                    } else {
                     const uint32_t Hc = H & 0xFFFEFFFEu;
                     const uint32_t tOr = tO | 0x00010001u;
                     auto psub = [](uint32_t a, uint32_t b) { return as_u(as_s2(a) - as_s2(b)); };
-                    uint32_t s4[4];
                     s4[0] = psub(I, Hc);
                     s4[1] = psub(D, Hc);
                     s4[2] = psub(tOr, I);
                     s4[3] = psub(tOr, D);
                     if constexpr (kM) s4[3] = bfi(endsel, psub(M, Hc), s4[3]);
+                    }
                     if (k % 2 == 0 && k < K - 1) {
 #pragma unroll
                         for (int u = 0; u < 4; ++u) nprv[u] = s4[u];
@@ -1878,17 +1904,24 @@ __device__ __forceinline__ int fill_pk_body(Src src, uint32_t count, const uint8
                         // pair goes to the low nibbles, its second to the high
                         uint32_t pw[4];
 #pragma unroll
+                        // (a lone last column's missing neighbour: signs clear after
+                        // the merge, so kS4's inverted sources get set ones here)
                         for (int u = 0; u < 4; ++u)
-                            pw[u] = k % 2 ? col_pair_signs(s4[u], nprv[u]) : col_pair_signs(0u, s4[u]);
+                            pw[u] = k % 2 ? col_pair_signs(s4[u], nprv[u])
+                                          : col_pair_signs(kS4 && u < 2 ? 0x80008000u : 0u, s4[u]);
                         const int cp = k / 2, g = cp / 2;
+                        // m ? a : b, or m ? ~a : ~b (kS4: argI / argD signs inverted)
+                        auto bfi01 = [](uint32_t m, uint32_t a, uint32_t b) {
+                            return kS4 ? __builtin_amdgcn_bitop3_b32(m, a, b, 0x35) : bfi(m, a, b);
+                        };
                         if (cp % 2 == 0) {
-                            uint32_t lo = bfi(0x01010101u, pw[0], pw[1]);
+                            uint32_t lo = bfi01(0x01010101u, pw[0], pw[1]);
                             lo = bfi(0x03030303u, lo, pw[2]);
                             lo = bfi(0x07070707u, lo, pw[3]);
                             if (cp == (K - 1) / 2) nw[g] = lo;
                             else nlo = lo;
                         } else {
-                            uint32_t x = bfi(0x10101010u, pw[0], pw[1]);
+                            uint32_t x = bfi01(0x10101010u, pw[0], pw[1]);
                             x = bfi(0x30303030u, x, pw[2]);
                             x = bfi(0x70707070u, x, pw[3]);
                             nw[g] = bfi(0x0F0F0F0Fu, nlo, x);
@@ -1997,13 +2030,15 @@ __device__ __forceinline__ int fill_pk_body(Src src, uint32_t count, const uint8
                         *reinterpret_cast<PkMask<KS> *>(mB + (uint64_t)sg * pb.mask_bs) = wb[sg];
                 }
             }
+            // (end values in the 2V + p form the walkers and results read)
+            auto down = [](int32_t v) -> int32_t { return kS4 ? (v >> 2) * 2 + (v & 1) : v; };
             if (!kSteady && t == tEA) {
                 const int32_t e = (int32_t)(pick_col<K>(Hout, kA) & 0xFFFFu) - kBias;
-                src.end(ia, pa, e + base - alpha * ldA - beta * lqA);
+                src.end(ia, pa, down(e + base - alpha * ldA - beta * lqA));
             }
             if (!kSteady && t == tEB) {
                 const int32_t e = (int32_t)(pick_col<K>(Hout, kB) >> 16) - kBias;
-                src.end(ib, pb, e + base - alpha * ldB - beta * lqB);
+                src.end(ib, pb, down(e + base - alpha * ldB - beta * lqB));
             }
         } else if (&Hout != &Hin) {
 #pragma unroll
@@ -2027,8 +2062,8 @@ __device__ __forceinline__ int fill_pk_body(Src src, uint32_t count, const uint8
     if (tS1 > tS0) {
         if constexpr (!kRebase) {
             const int32_t rb = tS0 + 1;
-            const int32_t bF = is_col1(sc, (uint32_t)rb) + alpha * rb + beta;
-            const int32_t bH = hs_col0(sc, (uint32_t)rb) + alpha * rb;
+            const int32_t bF = up(is_col1(sc, (uint32_t)rb)) + alpha * rb + beta;
+            const int32_t bH = up(hs_col0(sc, (uint32_t)rb)) + alpha * rb;
             sF = pkx(bF, bF);
             sH = pkx(bH, bH);
         }
@@ -2062,13 +2097,13 @@ __global__ __launch_bounds__(256, (pk_min_waves<G, K, kCodes>())) void nw_fill_p
 // launches of one workspace run in stream order); the fallback launch runs
 // only when that word holds its epoch.  Two kernels, not one with both
 // bodies: together they spill.
-template <int G, int K, typename Src>
+template <int G, int K, typename Src, int kScale = 2>
 __global__ __launch_bounds__(256, (pk_min_waves<G, K, kCodesNib>())) void nw_fill_pk_tab_kernel(
     Src src, uint32_t count, const uint8_t *__restrict__ qs, const uint8_t *__restrict__ ds,
     uint8_t *__restrict__ mask, Scoring sc, uint32_t ld_max, uint32_t *__restrict__ bail,
     uint32_t epoch) {
-    const int st = fill_pk_body<G, K, kCodesNib, Src, K, false, false, 1>(src, count, qs, ds, mask,
-                                                                           sc, ld_max, true);
+    const int st = fill_pk_body<G, K, kCodesNib, Src, K, false, false, kScale == 4 ? 4 : 1>(
+        src, count, qs, ds, mask, sc, ld_max, true);
     if (__builtin_amdgcn_ballot_w64(st == 1) && (threadIdx.x & 63u) == 0) *bail = epoch;
 }
 // (kRebaseGeneric: the fallback of a launch whose dbs need the rebasing frame;
@@ -3174,12 +3209,16 @@ static bool pk_tab_ok(const Scoring &sc) {
 // W-column lanes groups over `rows` rows: X~ = X' + 2|ge|(r + c) is at least
 // the all-gap path's 4go + 4ge less an open and a mismatch for M / I / D, at
 // most rows (2|m| + 2|ge|) + 2|ge| W plus the boundary flag.
-static bool pk_free_ok(const Scoring &sc, uint32_t W, uint32_t rows) {
+// scale: 2 (V = 2x + p) or 4 (the scale-4 table body, kTabMode 4): every
+// bound scales with it, and its bonuses must still fit a byte.
+static bool pk_free_ok(const Scoring &sc, uint32_t W, uint32_t rows, int scale = 2) {
     if (!pk_tab_ok(sc)) return false;
     const int64_t m = std::abs(sc.match), mm = std::abs(sc.mismatch), ge = std::abs(sc.gap_extend),
                   go = std::abs(sc.gap_open);
-    const int64_t lo = 6 * go + 6 * ge + 2 * mm + 64;
-    const int64_t hi = (int64_t)rows * (2 * m + 2 * ge) + 2 * ge * (int64_t)W + 2 * go + 64;
+    const int64_t f = scale / 2;
+    if (f * (2ll * sc.match - 4ll * sc.gap_extend) > 255) return false;
+    const int64_t lo = f * (6 * go + 6 * ge + 2 * mm + 64);
+    const int64_t hi = f * ((int64_t)rows * (2 * m + 2 * ge) + 2 * ge * (int64_t)W + 2 * go + 64);
     return lo <= kFreeBias - 0x400 && hi <= 0x7BFF - kFreeBias;
 }
 
@@ -3211,12 +3250,20 @@ static hipError_t fill_pk(dim3 grid, hipStream_t s, const NwPairDesc *pairs, uin
             if (o[Opt::PkTab] && fx.bail && pk_free_ok(sc, G * K, ld_max) &&
                 lds_tab <= std::max(lds, kLdsPerCu / 4)) {
                 constexpr bool kRb = decltype(rebase_c)::value;
-                const hipError_t e = big_lds({(const void *)nw_fill_pk_tab_kernel<G, K, PlanSrc>,
-                                              (const void *)nw_fill_pk_tabfb_kernel<G, K, PlanSrc, kRb>},
+                // nw.pk_tab 1: the scale-4 body where its window holds the
+                // launch (C2: 150 rows), else the scale-2 one; 2: scale 2 only
+                const bool s4 = o[Opt::PkTab] == 1 && pk_free_ok(sc, G * K, ld_max, 4);
+                const void *tk = s4 ? (const void *)nw_fill_pk_tab_kernel<G, K, PlanSrc, 4>
+                                    : (const void *)nw_fill_pk_tab_kernel<G, K, PlanSrc, 2>;
+                const hipError_t e = big_lds({tk, (const void *)nw_fill_pk_tabfb_kernel<G, K, PlanSrc, kRb>},
                                              lds_tab);
                 if (e != hipSuccess) return e;
-                nw_fill_pk_tab_kernel<G, K, PlanSrc><<<grid, dim3(256), lds_tab, s>>>(
-                    src, count, qs, ds, mask, sc, ld_max, fx.bail, fx.epoch);
+                if (s4)
+                    nw_fill_pk_tab_kernel<G, K, PlanSrc, 4><<<grid, dim3(256), lds_tab, s>>>(
+                        src, count, qs, ds, mask, sc, ld_max, fx.bail, fx.epoch);
+                else
+                    nw_fill_pk_tab_kernel<G, K, PlanSrc, 2><<<grid, dim3(256), lds_tab, s>>>(
+                        src, count, qs, ds, mask, sc, ld_max, fx.bail, fx.epoch);
                 auto fb = [=, bail = fx.bail, epoch = fx.epoch](hipStream_t fs) {
                     nw_fill_pk_tabfb_kernel<G, K, PlanSrc, kRb><<<grid, dim3(256), lds_tab, fs>>>(
                         src, count, qs, ds, mask, sc, ld_max, bail, epoch);

@@ -161,7 +161,7 @@ def test_c2_scale_properties(saln, oracle):
     plan.close()
 
 
-@pytest.mark.parametrize("tab", [1, 0])
+@pytest.mark.parametrize("tab", [1, 2, 0])
 def test_walk_code_formats_match_oracle(saln, oracle, saln_opt, tab):
     """The 4-bit walk codes of the short-query packed fills (8 x 19 groups for
     queries of <= 152 columns, 16 x 10 up to 160) give the oracle's results
@@ -229,8 +229,9 @@ def _run_plan(saln, qs, qo, ds, do, scoring=None):
     return res, cig, off
 
 
+@pytest.mark.parametrize("tab", [1, 2])
 @pytest.mark.parametrize("case", ["acgt", "with_n", "scheme", "long_db", "long_db_n"])
-def test_table_fill_equals_generic(saln, oracle, saln_opt, case):
+def test_table_fill_equals_generic(saln, oracle, saln_opt, case, tab):
     """nw.pk_tab = 1 (the 4-bit-code fill with table penalties in the
     extension-free frame, and its fallback launch for the waves whose pairs
     hold a byte other than A, C, G, T) equals nw.pk_tab = 0 on 20,000
@@ -241,7 +242,9 @@ def test_table_fill_equals_generic(saln, oracle, saln_opt, case):
     {2, -3, -5, -2} (bonuses 12 / 2).  "long_db" / "long_db_n": 150 x 500
     pairs (8 x 19 groups) and 155 x 500 pairs (16 x 10
     groups), whose dbs need the rebasing frame in the original frame but not
-    in the extension-free one (the fallback launch then rebases)."""
+    in the extension-free one (the fallback launch then rebases).  tab = 1:
+    the scale-4 table body (round 6; values 4x + p, full-rate subtracts for
+    the walk tests), 2: the scale-2 one."""
     from sequencealigning_amd import synth
     n, L = 20_000, 150
     LD = L
@@ -262,7 +265,7 @@ def test_table_fill_equals_generic(saln, oracle, saln_opt, case):
         for buf, off in ((qs, qo), (ds, do)):
             for k in rng.choice(n, n // 100, replace=False):
                 buf[int(off[k]) + int(rng.integers(L))] = ord("N")
-    saln_opt("nw.pk_tab", 1)
+    saln_opt("nw.pk_tab", tab)
     r1, c1, o1 = _run_plan(saln, qs, qo, ds, do, scoring)
     saln_opt("nw.pk_tab", 0)
     r0, c0, o0 = _run_plan(saln, qs, qo, ds, do, scoring)

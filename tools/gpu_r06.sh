@@ -4,6 +4,8 @@
 #            REPS alternations of tools/bench_long.py (walk codes and score-only)
 #   abwalk   C2 step with this tree's walker vs sequencealigning_amd/libsaln_prev.so
 #            (an earlier commit's build), sequential and pipelined, REPS alternations
+#   abtab    C2 step, scale-4 table fill (nw.pk_tab=1) vs scale 2 (nw.pk_tab=2), REPS alternations
+#   c2full   the c2_full leg alone (full 1 B/cell parent sets)
 #   smoke    __graft_entry__.smoke()
 #   tests    pytest -m gpu (TESTS= narrows it, e.g. "tests/test_span_gpu.py -k xcd")
 #   bench    bench.py --steps 20 --warmup 3 (BENCH_ARGS= extra args)
@@ -55,6 +57,18 @@ for st in ${STAGES:-smoke tests bench}; do
           done
         done
       done ;;
+    abtab)  # C2 table fill at scale 4 (nw.pk_tab=1) vs scale 2 (nw.pk_tab=2), sequential and pipelined
+      for i in ${REPS:-1 2}; do
+        for t in 2 1; do
+          for pl in "" "--pipeline"; do
+            tag=tab${t}${pl:+_pipe}_$i
+            step $tag 180 python tools/ab_c2.py --tag $tag $pl --opt nw.pk_tab=$t
+            tail -1 $O/$tag.log
+          done
+        done
+      done ;;
+    c2full) step c2full 400 python bench.py --steps 5 --warmup 2 --legs c2_full --no-cpu-baseline
+            tail -1 $O/c2full.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(json.dumps(d['configs']['c2_full'])[:1500])" ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
            tail -3 $O/smoke.log ;;
     tests) step tests 1500 python -u -m pytest ${TESTS:-tests} -m gpu -x -v --timeout 300 --timeout-method thread
