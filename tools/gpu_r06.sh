@@ -7,7 +7,8 @@
 #   abtab    C2 step, scale-4 table fill (nw.pk_tab=1) vs scale 2 (nw.pk_tab=2), REPS alternations
 #   c2full   the c2_full leg alone (full 1 B/cell parent sets)
 #   smoke    __graft_entry__.smoke()
-#   tests    pytest -m gpu (TESTS= narrows it, e.g. "tests/test_span_gpu.py -k xcd")
+#   tests    pytest -m gpu (TESTS= narrows it to files, KEXPR= to a -k expression)
+#   chains   tools/micro/row_chains (row-fill chains per wave)
 #   bench    bench.py --steps 20 --warmup 3 (BENCH_ARGS= extra args)
 #   prof     rocprofv3 --kernel-trace --stats of the headline command (pipelined),
 #            its fills split into co-run / alone by tools/trace_overlap.py
@@ -69,9 +70,15 @@ for st in ${STAGES:-smoke tests bench}; do
       done ;;
     c2full) step c2full 400 python bench.py --steps 5 --warmup 2 --legs c2_full --no-cpu-baseline
             tail -1 $O/c2full.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(json.dumps(d['configs']['c2_full'])[:1500])" ;;
+    chains) step chains 300 tools/micro/row_chains
+            cat $O/chains.log ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
            tail -3 $O/smoke.log ;;
-    tests) step tests 1500 python -u -m pytest ${TESTS:-tests} -m gpu -x -v --timeout 300 --timeout-method thread
+    tests) if [ -n "$KEXPR" ]; then
+             step tests 1500 python -u -m pytest ${TESTS:-tests} -k "$KEXPR" -m gpu -x -v --timeout 300 --timeout-method thread
+           else
+             step tests 1500 python -u -m pytest ${TESTS:-tests} -m gpu -x -v --timeout 300 --timeout-method thread
+           fi
            tail -3 $O/tests.log ;;
     bench) step bench 600 python bench.py --steps 20 --warmup 3 $BENCH_ARGS
            tail -1 $O/bench.log | cut -c1-3000 ;;
