@@ -698,6 +698,86 @@ def leg_c4_spans(torch, saln, n_spans=8, reps=3, band_rows=1024, edge_masks="sha
 _C3_PAIRS = {}
 
 
+def leg_c4_sharded(world, rank, local, dist, torch, reps=3, band_rows=1024, engine=None,
+                   q=None, d=None):
+    """SURVEY 8(f) row 3 at N > 1: configs[3]'s pair (100 kbp x 100 kbp G-mut
+    5 %, seed 0x5EED0003) split by query columns over the ranks, one span
+    per GPU (span.ShardedLongPair: the boundary rows travel rank r -> r+1 in
+    bands over RCCL send/recv while the spans fill, then the walk crosses the
+    ranks right to left and rank 0 assembles the CIGAR; main.rs:61-62 runs
+    the pair on one core).  Every rank returns the line; rank 0's holds
+    per-rank fill / walk / wall times and a probe of the band exchange alone
+    (the whole boundary column sent r -> r+1 in bands, after the timed runs).
+    engine / q / d: a CPU span engine and a small pair (tests, gloo)."""
+    import numpy as _np
+
+    from sequencealigning_amd.span import ShardedLongPair
+    if q is None:
+        from sequencealigning_amd import synth
+        q = synth.random_bases(0x5EED0003, 100_000).tobytes()
+        d = synth.mutate(q, 0.05, seed=100_000)
+    on_gpu = engine is None
+    sync = (lambda: torch.cuda.synchronize(local)) if on_gpu else (lambda: None)
+    sp = ShardedLongPair(q, d, band_rows=band_rows, engine=engine)
+    lo, hi = sp.cols[rank]
+    fills, walks, walls = [], [], []
+    res = None
+    for it in range(1 + reps):  # the first run warms up (not timed)
+        dist.barrier()
+        sync()
+        t0 = time.perf_counter()
+        sp.fill()
+        sync()
+        t1 = time.perf_counter()
+        res = sp.walk()
+        sync()
+        t2 = time.perf_counter()
+        if it:
+            fills.append(t1 - t0)
+            walks.append(t2 - t1)
+            walls.append(t2 - t0)
+    # the band exchange alone: every band of the boundary column r -> r+1
+    tdev = torch.device("cuda", local) if on_gpu and sp.nccl else torch.device("cpu")
+    dist.barrier()
+    sync()
+    t0 = time.perf_counter()
+    for a, b in sp.bands:
+        buf = torch.zeros(b - a + 1, dtype=torch.int64, device=tdev)
+        if sp.left is not None:
+            dist.recv(buf, src=rank - 1, group=sp.left)
+        if sp.right is not None:
+            dist.send(buf, dst=rank + 1, group=sp.right)
+    sync()
+    band_s = time.perf_counter() - t0
+    sp.close()
+    mine = _np.array([rank, hi - lo, _np.median(fills) * 1e3, _np.median(walks) * 1e3,
+                      _np.median(walls) * 1e3, band_s * 1e3], _np.float64)
+    t = torch.tensor(mine, dtype=torch.float64, device=tdev)
+    parts = [torch.zeros_like(t) for _ in range(world)] if rank == 0 else None
+    dist.gather(t, parts, dst=0)
+    wall_max = torch.tensor([max(walls)], dtype=torch.float64, device=tdev)
+    dist.all_reduce(wall_max, op=dist.ReduceOp.MAX)
+    if rank != 0:
+        return {}
+    per = [dict(zip(("rank", "cols", "fill_ms", "walk_ms", "wall_ms", "band_exchange_ms"),
+                    [int(x[0]), int(x[1])] + [round(float(v), 3) for v in x[2:]]))
+           for x in (p.cpu().numpy() for p in parts)]
+    cells = len(q) * len(d)
+    med = float(_np.median([max(p["wall_ms"] for p in per)]))
+    return {"workload": f"configs[3]'s pair ({len(q)} x {len(d)}) as {world} column spans, one "
+                        f"per rank (ShardedLongPair: {band_rows}-row bands over "
+                        f"{'RCCL' if sp.nccl else 'the host relay'}, right-to-left walk, CIGAR "
+                        f"on rank 0)",
+            "value": round(cells / (med / 1e3) / 1e9, 2), "unit": "GCUPS",
+            "ms": round(med, 3), "ms_max": round(float(wall_max.item()) * 1e3, 3),
+            "n_ranks": world, "reps": reps, "per_rank": per,
+            "result": {"score": int(res.score), "status": int(res.status),
+                       "printed": int(res.printed), "cigar_runs": len(res.cigar)},
+            "note": "value: cells / the slowest rank's median fill + walk; fill_ms includes "
+                    "the waits for the left neighbour's bands; band_exchange_ms: the whole "
+                    "boundary column sent r -> r+1 band by band, alone, after the timed runs"}
+
+
 def c3_pairs(torch, n_pairs, L):
     """configs[2]'s 10^6 distinct 10 kbp G-mut(5 %) pairs, generated on the
     device once (synth.mut_pairs_torch) and shared by c3 and c3_affine."""
@@ -891,26 +971,30 @@ def leg_cli(saln, n: int = 316, cpu: bool = True, max_blocks: int = 1, gmut: boo
         if max_blocks:
             cmd += ["--max-blocks", str(max_blocks)]
         walls = []
+        # timed runs write the text to /dev/null, like the CPU baseline below
+        # (both format every byte; neither pays for a file system)
         for k in range(6):  # the first run also pages in the library; value: the median of 5
-            # a fresh output file per run (the previous run's pages are freed
-            # outside the timed region, not while this one writes)
-            if k:
-                os.remove(of)
-            with open(of, "wb") as out:
+            with open(os.devnull, "wb") as out:
                 t0 = time.perf_counter()
                 r = subprocess.run(cmd, stdout=out, stderr=subprocess.PIPE, timeout=600)
                 walls.append(time.perf_counter() - t0)
             if r.returncode != 0:
                 raise RuntimeError(f"saln exited {r.returncode}: {r.stderr[-500:]!r}")
+        # one more run into a file: the text checked below, and its stage
+        # breakdown (stderr; not the timed value)
+        with open(of, "wb") as out:
+            t0 = time.perf_counter()
+            r = subprocess.run(cmd + ["--stage-times"], stdout=out, stderr=subprocess.PIPE,
+                               timeout=600)
+            wall_file = time.perf_counter() - t0
+        if r.returncode != 0:
+            raise RuntimeError(f"saln exited {r.returncode}: {r.stderr[-500:]!r}")
+        stages = [ln.split("]", 1)[1].strip() for ln in r.stderr.decode("latin-1").splitlines()
+                  if ln.startswith("[saln ")]
         with open(of, "rb") as fh:
             head = fh.read(64 << 20).decode("latin-1")
         out_bytes = os.path.getsize(of)
-        # one more run for its stage breakdown (stderr; not the timed value)
-        with open(of, "wb") as out:
-            r = subprocess.run(cmd + ["--stage-times"], stdout=out, stderr=subprocess.PIPE,
-                               timeout=600)
-        stages = [ln.split("]", 1)[1].strip() for ln in r.stderr.decode("latin-1").splitlines()
-                  if ln.startswith("[saln ")]
+        os.remove(of)
     from oracle import refcpu  # untimed checker / cpu baseline only
     want = "".join(refcpu.nw(a, d[0], max_blocks=max_blocks, max_pops=CPU_MAX_POPS,
                              out_cap=1 << 26).stdout for a in q)
@@ -920,8 +1004,9 @@ def leg_cli(saln, n: int = 316, cpu: bool = True, max_blocks: int = 1, gmut: boo
     res = {"workload": f"saln CLI (-a needleman-wunsch {flags}) on {n} x {n} FASTA records, "
                        f"{kind} ({n * n} pairs, seed {SEED:#x})",
            "value": round(cells / float(np.median(walls[1:])) / 1e9, 2),
-           "unit": "GCUPS (process wall time, median of 5 runs after a first)",
-           "stages_ms": stages,
+           "unit": "GCUPS (process wall time, stdout to /dev/null, median of 5 runs after a "
+                   "first)",
+           "stages_ms": stages, "wall_s_to_file": round(wall_file, 3),
            "wall_s": round(float(np.median(walls[1:])), 3), "wall_s_first": round(walls[0], 3),
            "walls_s": [round(w, 3) for w in walls],
            "stdout_bytes": out_bytes,
@@ -937,21 +1022,61 @@ def leg_cli(saln, n: int = 316, cpu: bool = True, max_blocks: int = 1, gmut: boo
         sd = b"".join(d[j] for j in di)
         qoff = np.concatenate([[0], np.cumsum(lq[qi])]).astype(np.uint64)
         doff = np.concatenate([[0], np.cumsum(ld[di])]).astype(np.uint64)
+        blk = (f"stopped before block {max_blocks + 1}" if max_blocks else "over every block")
+        # text-inclusive: every pair's reference text formatted and written to
+        # /dev/null in pair order (oracle/refmt.c ref_nw_run_pairs_text_mt)
+        fd = os.open(os.devnull, os.O_WRONLY)
+        try:
+            t0 = time.perf_counter()
+            c, nbytes, capped = refcpu.run_pairs_text(sq, qoff, sd, doff, m, fd,
+                                                      max_pops=CPU_MAX_POPS, threads=T,
+                                                      max_blocks=max_blocks)
+            dt = time.perf_counter() - t0
+        finally:
+            os.close(fd)
         t0 = time.perf_counter()
-        c, capped = refcpu.run_pairs_capped(sq, qoff, sd, doff, m, max_pops=CPU_MAX_POPS,
-                                            threads=T, max_blocks=max_blocks)
-        dt = time.perf_counter() - t0
+        c2, capped2 = refcpu.run_pairs_capped(sq, qoff, sd, doff, m, max_pops=CPU_MAX_POPS,
+                                              threads=T, max_blocks=max_blocks)
+        dt2 = time.perf_counter() - t0
         res["cpu_baseline"] = {"value": round(c / dt / 1e9, 5), "unit": "GCUPS", "cores": T,
                                "kind": "port", "capped_pairs": int(capped),
+                               "text_bytes": int(nbytes), "seconds": round(dt, 3),
                                "sample": f"all {m} pairs of the file, oracle/refcpu.c fill + "
-                                         f"literal DFS "
-                                         f"{'stopped before block %d' % (max_blocks + 1) if max_blocks else 'over every block'} "
-                                         f"(<= {CPU_MAX_POPS:.0e} pops) on {T} threads, "
-                                         f"{dt:.2f} s; in-process, no text formatting, no "
-                                         f"output, no process start (the CLI's value "
-                                         f"includes all three)"}
+                                         f"literal DFS {blk} (<= {CPU_MAX_POPS:.0e} pops) on "
+                                         f"{T} threads, each pair's reference text formatted "
+                                         f"and written to /dev/null in pair order "
+                                         f"(refmt.c), {dt:.2f} s; in-process (no process "
+                                         f"start, which the CLI's value includes)",
+                               "no_text": {"value": round(c2 / dt2 / 1e9, 5),
+                                           "seconds": round(dt2, 3),
+                                           "capped_pairs": int(capped2),
+                                           "note": "the same DFS without formatting or "
+                                                   "writing any text"}}
         res["vs_cpu_baseline"] = round(res["value"] / res["cpu_baseline"]["value"], 2)
     return res
+
+
+C4_SHARDED_TIMEOUT_S = 180.0
+
+
+def _leg_watchdog(rank, out, extra, leg, seconds):
+    """A timer that, if `leg` has not finished after `seconds`, prints rank
+    0's line (the headline and the legs so far, this one marked as timed out)
+    and ends every rank's process (os._exit: no exec, no collective)."""
+    import threading
+
+    def fire():
+        if rank == 0 and out is not None:
+            o = dict(out)
+            o["configs"] = dict(extra, **{leg: {"error": f"timed out after {seconds:.0f} s"}})
+            print(json.dumps(o), flush=True)
+        sys.stderr.flush()
+        os._exit(0)
+
+    t = threading.Timer(seconds, fire)
+    t.daemon = True
+    t.start()
+    return t
 
 
 # --------------------------------------------------------------- launcher
@@ -1014,8 +1139,9 @@ def main() -> None:
     ap.add_argument("--pairs", type=int, default=N_PAIRS)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--legs", default="auto",
-                    help="comma list of extra configs (c5,c1,c3,c3_affine,c4,host), 'none', or "
-                         "'auto' (all at N = 1, c5 at N > 1)")
+                    help="comma list of extra configs (c2_full,c5,c1,c3,c3_affine,c4,c4_spans,host,"
+                         "cli,cli_all; c4_sharded at N > 1), 'none', or 'auto' (all at N = 1, "
+                         "c5 and c4_sharded at N > 1)")
     ap.add_argument("--score-only", action="store_true",
                     help="score + panic status only (no parent codes / traceback; the C5 mode)")
     ap.add_argument("--no-pipeline", dest="pipeline", action="store_false",
@@ -1053,7 +1179,7 @@ def main() -> None:
     if world > 1:
         dist.init_process_group(args.backend, device_id=torch.device("cuda", local))
     if args.legs == "auto":
-        legs = list(ALL_LEGS) if world == 1 else ["c5"]
+        legs = list(ALL_LEGS) if world == 1 else ["c5", "c4_sharded"]
     elif args.legs == "none":
         legs = []
     else:
@@ -1212,6 +1338,18 @@ def main() -> None:
         try:
             if leg == "c5":
                 r = leg_c5(world, rank, local, dist, torch, cpu=cpu)
+            elif leg == "c4_sharded":
+                if world < 2:
+                    continue  # one span per rank: a multi-GPU leg
+                # never run on >= 2 real RCCL ranks before: a watchdog ends a
+                # stuck leg with the headline line still printed by rank 0
+                wd = _leg_watchdog(rank, out, extra, leg, C4_SHARDED_TIMEOUT_S)
+                try:
+                    r = leg_c4_sharded(world, rank, local, dist, torch)
+                except Exception as e:  # the line must survive this leg
+                    r = {"error": f"{type(e).__name__}: {e}"}
+                finally:
+                    wd.cancel()
             elif rank != 0 or world > 1:
                 continue
             elif leg == "c2_full":
@@ -1231,7 +1369,7 @@ def main() -> None:
             elif leg == "cli":
                 r = leg_cli(saln, cpu=cpu)
             elif leg == "cli_all":
-                r = leg_cli(saln, n=100, cpu=cpu, max_blocks=0, gmut=True)
+                r = leg_cli(saln, n=316, cpu=cpu, max_blocks=0, gmut=True)
             else:
                 raise ValueError(f"unknown leg {leg}")
         except Exception as e:  # a failing extra leg must not hide the headline line

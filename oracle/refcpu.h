@@ -94,6 +94,11 @@ uint64_t ref_nw_run_pairs_capped(const uint8_t *qs, const uint64_t *q_off, const
 uint64_t ref_nw_run_pairs_mt_capped(const uint8_t *qs, const uint64_t *q_off, const uint8_t *ds,
                                     const uint64_t *d_off, uint64_t n_pairs, uint64_t max_pops,
                                     uint64_t max_blocks, int threads, uint64_t *capped);
+/* the same with every pair's text written to fd in pair order (refmt.c) */
+uint64_t ref_nw_run_pairs_text_mt(const uint8_t *qs, const uint64_t *q_off, const uint8_t *ds,
+                                  const uint64_t *d_off, uint64_t n_pairs, uint64_t max_pops,
+                                  uint64_t max_blocks, int threads, int fd, uint64_t chunk,
+                                  uint64_t *bytes, uint64_t *capped);
 uint64_t ref_nw_run_pairs_mt(const uint8_t *qs, const uint64_t *q_off, const uint8_t *ds,
                              const uint64_t *d_off, uint64_t n_pairs, uint64_t max_pops,
                              int threads);

@@ -67,6 +67,11 @@ def lib():
                                                   C.c_size_t, C.POINTER(C.c_size_t), C.c_uint64,
                                                   C.c_uint64, C.POINTER(C.c_uint64)]
         L.ref_nw_run_pairs_mt_capped.restype = C.c_uint64
+        L.ref_nw_run_pairs_text_mt.argtypes = [u8p, C.POINTER(C.c_uint64), u8p,
+                                               C.POINTER(C.c_uint64), C.c_uint64, C.c_uint64,
+                                               C.c_uint64, C.c_int, C.c_int, C.c_uint64,
+                                               C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
+        L.ref_nw_run_pairs_text_mt.restype = C.c_uint64
         L.ref_nw_check_pairs_mt.argtypes = [u8p, C.POINTER(C.c_uint64), u8p,
                                             C.POINTER(C.c_uint64), C.c_uint64,
                                             C.POINTER(C.c_uint64), C.POINTER(C.c_int32), u8p, u8p,
@@ -217,6 +222,22 @@ def run_pairs_capped(qs: bytes, q_off: np.ndarray, ds: bytes, d_off: np.ndarray,
         cells = L.ref_nw_run_pairs_mt_capped(_u8(qs), P(qo), _u8(ds), P(do), n_pairs, max_pops,
                                              max_blocks, threads, C.byref(nc))
     return int(cells), int(nc.value)
+
+
+def run_pairs_text(qs: bytes, q_off: np.ndarray, ds: bytes, d_off: np.ndarray, n_pairs: int,
+                   fd: int, max_pops: int = 100_000, threads: int = 1, max_blocks: int = 0,
+                   chunk: int = 4096) -> tuple[int, int, int]:
+    """(cells, text bytes, capped pairs): the pair loop with the reference's
+    text of every pair written to file descriptor `fd` in pair order
+    (refmt.c ref_nw_run_pairs_text_mt; the CLI's text-inclusive CPU baseline)."""
+    L = lib()
+    qo = np.ascontiguousarray(q_off, np.uint64)
+    do = np.ascontiguousarray(d_off, np.uint64)
+    nb, nc = C.c_uint64(0), C.c_uint64(0)
+    P = lambda a: a.ctypes.data_as(C.POINTER(C.c_uint64))  # noqa: E731
+    cells = L.ref_nw_run_pairs_text_mt(_u8(qs), P(qo), _u8(ds), P(do), n_pairs, max_pops,
+                                       max_blocks, threads, fd, chunk, C.byref(nb), C.byref(nc))
+    return int(cells), int(nb.value), int(nc.value)
 
 
 def run_pairs_mt(qs: bytes, q_off: np.ndarray, ds: bytes, d_off: np.ndarray, n_pairs: int,

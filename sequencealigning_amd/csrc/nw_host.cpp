@@ -1016,8 +1016,45 @@ DfsOutcome render_blocks(const HostMask &hm, const uint8_t *q, const uint8_t *d,
         Node n;
         uint32_t depth;
     };
+    // Every mask layout is row-separable: cell(i, j) = (i-1) RS + co[j] (the
+    // packed stripes' skew included, RS = 256), so a node's code byte is one
+    // multiply-add and a table load instead of Geom::cell's divisions.
+    const uint32_t lq = hm.lq, ld = hm.ld;
+    std::vector<uint64_t> co(lq + 1, 0);
+    for (uint32_t j = 1; j <= lq && ld; ++j) co[j] = hm.g.cell(1, j, hm.rs, hm.bs, hm.cs);
+    const uint64_t RS = hm.bs == 0 ? 256 : hm.rs;
+    auto byte = [&](uint32_t i, uint32_t j) -> uint8_t {
+        return hm.m[(uint64_t)(i - 1) * RS + co[j]] ^ 0x7F;
+    };
+    auto argmax = [&](uint32_t i, uint32_t j) -> uint8_t {
+        if (i == 0 || j == 0) return hm.argmax(i, j);
+        return byte(i, j) & 7;
+    };
+    auto kids = [&](int st, uint32_t i, uint32_t j, int *ps, uint32_t *pi, uint32_t *pj) -> int {
+        if (i == 0 || j == 0 || (st == ST_I && j == 1) || (st == ST_D && i == 1))
+            return parents(hm, st, i, j, ps, pi, pj);
+        int n = 0;
+        if (st == ST_M) {
+            const uint8_t a = argmax(i - 1, j - 1);
+            if (a & kArgM) { ps[n] = ST_M; pi[n] = i - 1; pj[n] = j - 1; ++n; }
+            if (a & kArgI) { ps[n] = ST_I; pi[n] = i - 1; pj[n] = j - 1; ++n; }
+            if (a & kArgD) { ps[n] = ST_D; pi[n] = i - 1; pj[n] = j - 1; ++n; }
+        } else if (st == ST_I) {
+            const uint8_t b = (byte(i, j - 1) >> 3) & 3;
+            if (b & 1) { ps[n] = ST_I; pi[n] = i; pj[n] = j - 1; ++n; }
+            if (b & 2) { ps[n] = ST_M; pi[n] = i; pj[n] = j - 1; ++n; }
+        } else {
+            const uint8_t b = (byte(i - 1, j) >> 5) & 3;
+            if (b & 1) { ps[n] = ST_D; pi[n] = i - 1; pj[n] = j; ++n; }
+            if (b & 2) { ps[n] = ST_M; pi[n] = i - 1; pj[n] = j; ++n; }
+        }
+        return n;
+    };
     std::vector<Item> stack;
-    std::vector<char> p1(hm.lq + hm.ld + 1), p2(hm.lq + hm.ld + 1);
+    // the path's columns stored back to front (depth k at cap - 1 - k), so a
+    // block's three lines are three contiguous copies
+    const uint32_t cap = lq + ld + 1;
+    std::vector<char> p1(cap), p2(cap), pb(cap);
     Node ends[3];
     const int ne = end_nodes(hm, ends);
     for (int k = ne - 1; k >= 0; --k) stack.push_back({ends[k], 0});  // pop order D, M, I
@@ -1031,26 +1068,30 @@ DfsOutcome render_blocks(const HostMask &hm, const uint8_t *q, const uint8_t *d,
                 return res;
             }
             if (out) {
+                const uint32_t D = it.depth, a = cap - D;
                 out->append("alignment found\n\nseq1: ");
-                for (uint32_t k = it.depth; k-- > 0;) out->push_back(p1[k]);
+                out->append(p1.data() + a, D);
                 out->append("\n      ");
-                for (uint32_t k = it.depth; k-- > 0;) out->push_back(p1[k] == p2[k] ? '|' : ' ');
+                out->append(pb.data() + a, D);
                 out->append("\nseq2: ");
-                for (uint32_t k = it.depth; k-- > 0;) out->push_back(p2[k]);
+                out->append(p2.data() + a, D);
                 out->push_back('\n');
             }
             ++res.blocks;
         }
         int ps[3];
         uint32_t pi[3], pj[3];
-        const int np = parents(hm, n.st, n.i, n.j, ps, pi, pj);
+        const int np = kids(n.st, n.i, n.j, ps, pi, pj);
         if (panics(n.st, n.i, n.j, np)) {
             res.status = SALN_REF_PANIC_BOUNDARY;
             return res;
         }
         if (np) {
-            p1[it.depth] = col_q(n.st, q, n.j);
-            p2[it.depth] = col_d(n.st, d, n.i);
+            const uint32_t x = cap - 1 - it.depth;
+            const char c1 = col_q(n.st, q, n.j), c2 = col_d(n.st, d, n.i);
+            p1[x] = c1;
+            p2[x] = c2;
+            pb[x] = c1 == c2 ? '|' : ' ';
         }
         for (int k = 0; k < np; ++k) stack.push_back({{ps[k], pi[k], pj[k]}, it.depth + 1});
     }

@@ -58,3 +58,69 @@ def test_bench_refuses_leftover_experiment_variables():
     import bench
     assert bench.refused_env({"SALN_X": "1", "PATH": "/bin", "XSALN_Y": "2"}) == ["SALN_X"]
     assert bench.refused_env({k: "1" for k in bench.ALLOWED_ENV}) == []
+
+
+def _c4_sharded_worker(rank, world, port, q, d, out):
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import torch
+    import torch.distributed as dist
+
+    import bench
+    from test_span import _CpuSpanEngine
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    r = bench.leg_c4_sharded(world, rank, 0, dist, torch, reps=2, band_rows=64,
+                             engine=_CpuSpanEngine, q=q, d=d)
+    if rank == 0:
+        out.put(r)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_c4_sharded_leg_shape_gloo():
+    """at N > 1 bench.py adds the c4_sharded leg (one long pair
+    as one column span per rank, span.ShardedLongPair).  Its line on gloo with
+    CPU span engines at world 2: per-rank fill / walk / wall / band-exchange
+    times, the spans' columns covering the query, and the assembled result
+    equal to the oracle's."""
+    import multiprocessing as mp
+    import socket
+
+    import numpy as np
+    sys.path.insert(0, ROOT)
+    from oracle import refcpu
+    rng = np.random.default_rng(606)
+    q = bytes(rng.choice(np.frombuffer(b"ACGT", np.uint8), 600))
+    d = bytearray(q[:520])
+    for k in range(0, len(d), 13):
+        d[k] = ord("ACGT"[(d[k] + 1) % 4])
+    d = bytes(d)
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    out = ctx.Queue()
+    procs = [ctx.Process(target=_c4_sharded_worker, args=(r, 2, port, q, d, out)) for r in range(2)]
+    for p in procs:
+        p.start()
+    r = out.get(timeout=300)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert r["n_ranks"] == 2 and r["unit"] == "GCUPS" and r["value"] > 0
+    assert [x["rank"] for x in r["per_rank"]] == [0, 1]
+    assert sum(x["cols"] for x in r["per_rank"]) == len(q)
+    for x in r["per_rank"]:
+        assert set(x) == {"rank", "cols", "fill_ms", "walk_ms", "wall_ms", "band_exchange_ms"}
+        assert x["fill_ms"] > 0 and x["walk_ms"] > 0 and x["band_exchange_ms"] >= 0
+    o = refcpu.nw(q, d, literal_dfs=False)
+    assert r["result"]["score"] == o.score and (r["result"]["status"] == 2) == o.panics
+
+
+def test_gpus1_legs_exclude_c4_sharded():
+    """--gpus 1 output is unchanged by the N > 1 leg: it is not an N = 1 leg."""
+    sys.path.insert(0, ROOT)
+    import bench
+    assert "c4_sharded" not in bench.ALL_LEGS
