@@ -63,7 +63,7 @@ VALU_PK_TOPS = 1024 * 16 * 2.4e9 / 1e12
 N_PAIRS, LQ, LD = 100_000, 150, 150
 SEED = 0x5EED0002
 ALL_LEGS = ("c2_full", "c5", "c1", "c3", "c3_affine", "c4", "c4_spans", "host", "cli", "cli_all")
-PMC_FILES = ("pmc_traffic.json", "pmc_legs.json")  # under profiles/
+PMC_FILES = ("pmc_traffic.json", "pmc_legs.json", "pmc_c2full.json")  # under profiles/
 
 
 # SALN_* environment variables the bench runs with (recorded in the JSON
@@ -566,7 +566,7 @@ def leg_c2_full(torch, saln, n=N_PAIRS, steps=10, warmup=2):
                                  step_frac=round(cells / dt / 1e9 / HBM_PEAK_GBS, 4),
                                  traceback_avg_ms=round(tb_ms / max(1, tb_n), 4),
                                  note="algorithmic bytes = 1 B/cell, here also the bytes the "
-                                      "fill stores; traffic from profiles/pmc_legs.json",
+                                      "fill stores; traffic from profiles/pmc_c2full.json",
                                  valu=valu_roof(kern, fill_s)),
             "verified": verified, "dense_mask_equal_oracle": bool(mask_ok),
             "cpu_baseline": "the headline's (the oracle's fill computes every parent set)"}

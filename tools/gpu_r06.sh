@@ -90,6 +90,10 @@ for st in ${STAGES:-smoke tests bench}; do
           python3 tools/trace_overlap.py $O/profseq --out $O/profseq_overlap.json ;;
     proflegs) step proflegs 900 rocprofv3 --kernel-trace --stats -d $O/proflegs -o run --output-format csv -- python3 tools/prof_legs.py
               find $O/proflegs -name '*kernel_stats.csv' -exec head -20 {} \; | cut -c1-220 ;;
+    pmctab) PMC_SETS="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU;SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU" step pmctab 600 bash tools/pmc.sh --opt-sets "${OPT_SETS:-nw.pk_tab=1;nw.pk_tab=2}"
+           python3 tools/pmc_summary.py gpurun_out/pmc > $O/pmctab_summary.txt 2>&1; cp -r gpurun_out/pmc $O/pmctab_raw; head -60 $O/pmctab_summary.txt ;;
+    pmcc2full) PMC_SCRIPT=tools/prof_legs.py PMC_SETS="FETCH_SIZE;WRITE_SIZE;SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU" step pmc_c2full 600 bash tools/pmc.sh --legs c2_full
+           python3 tools/pmc_traffic.py gpurun_out/pmc $O/pmc_c2full.json r06 legs > /dev/null || exit 1 ;;
     pmc)   PMC_SETS=${PMC_SETS:-"FETCH_SIZE;WRITE_SIZE;SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU;SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU"} step pmc 900 bash tools/pmc.sh
            python3 tools/pmc_traffic.py gpurun_out/pmc $O/pmc_traffic.json r06 nw > /dev/null || exit 1 ;;
     pmclegs) PMC_SCRIPT=tools/prof_legs.py PMC_SETS=${PMC_SETS:-"FETCH_SIZE;WRITE_SIZE;SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU"} step pmc_legs 1100 bash tools/pmc.sh --legs ${PROF_LEGS:-c2_full,c1,c3,c3_affine,c4,c5}
