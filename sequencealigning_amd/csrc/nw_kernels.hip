@@ -1619,6 +1619,12 @@ __device__ __forceinline__ uint32_t hmax3(uint32_t a, uint32_t b, uint32_t c) {
                                                     __builtin_bit_cast(f16x2, c))));
 }
 
+// A step's row inputs: w = the packed db word (kRowProf: the two chars as
+// A | B << 8), lo / hi = kRowProf's profiles of the row's A and B chars.
+struct RowIn {
+    uint32_t w, lo, hi;
+};
+
 // Returns (per lane; wave-uniform over the lanes that hold pairs): 0 filled
 // (or no pair), 1 the table body left the wave's pairs to the fallback launch
 // (a byte other than A, C, G, T), 2 the fallback body found nothing to do.
@@ -1630,7 +1636,13 @@ __device__ __forceinline__ int fill_pk_body(Src src, uint32_t count, const uint8
                                             uint32_t ld_max, bool sc_steady) {
     // table body (kTabMode 1; 4: the same at scale 4, below); kTabMode 2: the
     // generic body of its bail-outs
-    constexpr bool kTab = kTabMode == 1 || kTabMode == 4;
+    constexpr bool kTab = kTabMode == 1 || kTabMode == 4 || kTabMode == 5;
+    // kTabMode 5 (round 6): the table body with row profiles - the staging
+    // holds per row the bonus of each query code against the row's db char of
+    // pair A (dword lo) and of pair B (dword hi), so a column's bonus is one
+    // v_perm with a per-column selector of its query codes (no xor per column);
+    // the rows' db chars sit beside them as 16-bit (A | B << 8) words
+    constexpr bool kRowProf = kTabMode == 5;
     // the extension-free frame (alpha = beta = -2*gap_extend, M~ = H~ + bonus):
     // the table body, and kTabMode 3 = query profiles holding bonuses
     constexpr bool kFree = kTab || kTabMode == 3;
@@ -1713,7 +1725,10 @@ __device__ __forceinline__ int fill_pk_body(Src src, uint32_t count, const uint8
             const uint32_t ca = j <= lqA ? (uint32_t)qA[j - 1] : 'A';
             const uint32_t cb = j <= lqB ? (uint32_t)qB[j - 1] : 'A';
             bad |= !acgt(ca) || !acgt(cb);
-            qc[k] = ((ca >> 1) & 3u) | ((cb >> 1) & 3u) << 16;
+            // kRowProf: the v_perm selector of the row profiles (A: bytes 0-3
+            // of the lo dword, B: bytes 4-7 = the hi dword; 0x0C = zero byte)
+            qc[k] = kRowProf ? (((ca >> 1) & 3u) | 0x0C00u | (((cb >> 1) & 3u) + 4u) << 16 | 0x0C000000u)
+                             : (((ca >> 1) & 3u) | ((cb >> 1) & 3u) << 16);
         } else {
             const uint32_t ca = j <= lqA ? (uint32_t)qA[j - 1] << 5 : 0xE000u;
             const uint32_t cb = j <= lqB ? (uint32_t)qB[j - 1] << 5 : 0xE000u;
@@ -1739,12 +1754,24 @@ __device__ __forceinline__ int fill_pk_body(Src src, uint32_t count, const uint8
     uint32_t *__restrict__ myrow = drow + (threadIdx.x / G) * (ld_max + 2 * G) + G;
     uint16_t *__restrict__ myrow16 = reinterpret_cast<uint16_t *>(drow) +
                                      (threadIdx.x / G) * (ld_max + 2 * G) + G;
+    // kRowProf: [GPB][ld_max + 2G] uint2 profiles, then [GPB][ld_max + 2G] chars
+    uint2 *__restrict__ myprof = reinterpret_cast<uint2 *>(drow) +
+                                 (threadIdx.x / G) * (ld_max + 2 * G) + G;
+    uint16_t *__restrict__ mych = reinterpret_cast<uint16_t *>(reinterpret_cast<uint2 *>(drow) +
+                                                               GPB * (ld_max + 2 * G)) +
+                                  (threadIdx.x / G) * (ld_max + 2 * G) + G;
     for (int i = lane; i < ldM; i += G) {
         const uint32_t ca = i < ldA ? (uint32_t)dA[i] : 0u;
         const uint32_t cb = i < ldB ? (uint32_t)dB[i] : 0u;
         if constexpr (kRebase) {
             if constexpr (kTabMode == 2) bad |= (i < ldA && !acgt(ca)) || (i < ldB && !acgt(cb));
             myrow16[i] = (uint16_t)(ca | (cb << 8));
+        } else if constexpr (kRowProf) {
+            bad |= (i < ldA && !acgt(ca)) || (i < ldB && !acgt(cb));
+            // bonus of query code c against this char: cm at byte code(char), cmm elsewhere
+            auto prof = [&](uint32_t c) { return cmm * 0x01010101u + ((cm - cmm) << (8 * ((c >> 1) & 3u))); };
+            myprof[i] = make_uint2(prof(ca), prof(cb));
+            mych[i] = (uint16_t)(ca | (cb << 8));
         } else if constexpr (kTab) {
             bad |= (i < ldA && !acgt(ca)) || (i < ldB && !acgt(cb));
             myrow[i] = ((ca >> 1) & 3u) | ((cb >> 1) & 3u) << 16 | 0x0C000C00u;
@@ -1776,6 +1803,8 @@ __device__ __forceinline__ int fill_pk_body(Src src, uint32_t count, const uint8
                                (int64_t)lane * (int64_t)pb.mask_rs;
     const uint32_t *__restrict__ rowp = myrow - lane;  // word of row r-1 at step 0
     const uint16_t *__restrict__ rowp16 = myrow16 - lane;
+    const uint2 *__restrict__ rowpp = myprof - lane;
+    const uint16_t *__restrict__ rowpc = mych - lane;
     const int T = (int)geo.steps((uint32_t)ldM);
     // Walk codes: a lane whose columns all lie past a pair's query stores
     // nothing for it (no walker reads past column len_q; 16 x 10 groups on
@@ -1798,14 +1827,19 @@ __device__ __forceinline__ int fill_pk_body(Src src, uint32_t count, const uint8
     // rows: sentinel-free), advanced by one row's drift per step.
     uint32_t sF = 0, sH = 0;
     const uint32_t kRowAdd = cst2(drift);
-    auto step = [&](int t, uint32_t(&Hin)[K], uint32_t(&Hout)[K], auto steady_c, uint32_t dch_in)
+    auto step = [&](int t, uint32_t(&Hin)[K], uint32_t(&Hout)[K], auto steady_c, RowIn row_in)
                     __attribute__((always_inline)) {
         constexpr bool kSteady = decltype(steady_c)::value;
         constexpr bool kRun = kSteady && !kRebase;  // running inputs, prefetched db word
         const int r = t - lane + 1;
         uint32_t dch;
+        RowIn rw{};  // kRowProf: the row's profiles (dch holds its chars)
         if constexpr (kRun)
-            dch = dch_in;
+            rw = row_in;
+        else if constexpr (kRowProf)
+            rw = RowIn{(uint32_t)rowpc[t], rowpp[t].x, rowpp[t].y};
+        if constexpr (kRun || kRowProf)
+            dch = rw.w;
         else if constexpr (kRebase)  // [A, 0, B, 0] << 5
             dch = __builtin_amdgcn_perm(0u, (uint32_t)rowp16[t], 0x0C010C00u) << 5;
         else
@@ -1864,9 +1898,10 @@ __device__ __forceinline__ int fill_pk_body(Src src, uint32_t count, const uint8
             for (int k = 0; k < K; ++k) {
                 const uint32_t hdk = diag;
                 diag = Hin[k];
-                const uint32_t pen = kProf ? __builtin_amdgcn_perm(0u, qc[k], psel)
-                                     : kTab  ? __builtin_amdgcn_perm(0u, kBonus, qc[k] ^ dch)
-                                             : umin2(qc[k] ^ dch, kPen);
+                const uint32_t pen = kProf     ? __builtin_amdgcn_perm(0u, qc[k], psel)
+                                     : kRowProf ? __builtin_amdgcn_perm(rw.hi, rw.lo, qc[k])
+                                     : kTab     ? __builtin_amdgcn_perm(0u, kBonus, qc[k] ^ dch)
+                                                : umin2(qc[k] ^ dch, kPen);
                 const uint32_t M = kFree ? hdk + pen : hdk - pen;
                 const uint32_t I = F, D = Dn[k];
                 const uint32_t H = kFree ? hmax3(M, I, D) : umax2(M, umax2(I, D));
@@ -1988,8 +2023,9 @@ __device__ __forceinline__ int fill_pk_body(Src src, uint32_t count, const uint8
                 // -> per-pair halves, two groups per dword; the db chars
                 // (dch = A << 5 | B << 21) rotated to bytes 0 / 2
                 constexpr int NG = (K + 3) / 4, ND = NG / 2 + 1;
-                const uint32_t rot = kTab ? __builtin_amdgcn_perm(0u, kAcgt, dch)
-                                          : __builtin_amdgcn_alignbit(dch, dch, 5);
+                const uint32_t rot = kRowProf ? __builtin_amdgcn_perm(0u, dch, 0x0C010C00u)
+                                     : kTab   ? __builtin_amdgcn_perm(0u, kAcgt, dch)
+                                              : __builtin_amdgcn_alignbit(dch, dch, 5);
                 NibSeg<K> na, nb;
 #pragma unroll
                 for (int d = 0; d < NG / 2; ++d) {
@@ -2055,9 +2091,16 @@ __device__ __forceinline__ int fill_pk_body(Src src, uint32_t count, const uint8
     const int tS0 = min((G + 1) & ~1, T & ~1);
     const int tS1 = sc_steady ? max(tS0, tS0 + ((ldm - 1 - tS0) & ~1) * (ldm - 1 > tS0 ? 1 : 0)) : tS0;
     int t = 0;
+    const RowIn z{};
+    // the steady loop's row inputs, read a step ahead
+    auto rowin = [&](int tt) __attribute__((always_inline)) {
+        if constexpr (kRebase) return z;
+        else if constexpr (kRowProf) return RowIn{(uint32_t)rowpc[tt], rowpp[tt].x, rowpp[tt].y};
+        else return RowIn{rowp[tt], 0u, 0u};
+    };
     for (; t < tS0; t += 2) {
-        step(t, Hp, HpB, G0, 0u);
-        step(t + 1, HpB, Hp, G0, 0u);
+        step(t, Hp, HpB, G0, z);
+        step(t + 1, HpB, Hp, G0, z);
     }
     if (tS1 > tS0) {
         if constexpr (!kRebase) {
@@ -2067,19 +2110,19 @@ __device__ __forceinline__ int fill_pk_body(Src src, uint32_t count, const uint8
             sF = pkx(bF, bF);
             sH = pkx(bH, bH);
         }
-        uint32_t d0 = kRebase ? 0u : rowp[t];
+        RowIn d0 = rowin(t);
         for (; t < tS1; t += 2) {
-            const uint32_t d1 = kRebase ? 0u : rowp[t + 1];
+            const RowIn d1 = rowin(t + 1);
             step(t, Hp, HpB, S1, d0);
-            d0 = kRebase ? 0u : rowp[t + 2];
+            d0 = rowin(t + 2);
             step(t + 1, HpB, Hp, S1, d1);
         }
     }
     for (; t + 1 < T; t += 2) {
-        step(t, Hp, HpB, G0, 0u);
-        step(t + 1, HpB, Hp, G0, 0u);
+        step(t, Hp, HpB, G0, z);
+        step(t + 1, HpB, Hp, G0, z);
     }
-    if (t < T) step(t, Hp, HpB, G0, 0u);
+    if (t < T) step(t, Hp, HpB, G0, z);
     return 0;
 }
 
@@ -2102,8 +2145,10 @@ __global__ __launch_bounds__(256, (pk_min_waves<G, K, kCodesNib>())) void nw_fil
     Src src, uint32_t count, const uint8_t *__restrict__ qs, const uint8_t *__restrict__ ds,
     uint8_t *__restrict__ mask, Scoring sc, uint32_t ld_max, uint32_t *__restrict__ bail,
     uint32_t epoch) {
-    const int st = fill_pk_body<G, K, kCodesNib, Src, K, false, false, kScale == 4 ? 4 : 1>(
-        src, count, qs, ds, mask, sc, ld_max, true);
+    // kScale: 2 or 4 (the value scale); 3: scale 2 with row profiles (kTabMode 5)
+    const int st = fill_pk_body<G, K, kCodesNib, Src, K, false, false,
+                                kScale == 4 ? 4 : kScale == 3 ? 5 : 1>(src, count, qs, ds, mask,
+                                                                       sc, ld_max, true);
     if (__builtin_amdgcn_ballot_w64(st == 1) && (threadIdx.x & 63u) == 0) *bail = epoch;
 }
 // (kRebaseGeneric: the fallback of a launch whose dbs need the rebasing frame;
@@ -3250,19 +3295,28 @@ static hipError_t fill_pk(dim3 grid, hipStream_t s, const NwPairDesc *pairs, uin
             if (o[Opt::PkTab] && fx.bail && pk_free_ok(sc, G * K, ld_max) &&
                 lds_tab <= std::max(lds, kLdsPerCu / 4)) {
                 constexpr bool kRb = decltype(rebase_c)::value;
-                // nw.pk_tab 1: the scale-4 body where its window holds the
-                // launch (C2: 150 rows), else the scale-2 one; 2: scale 2 only
-                const bool s4 = o[Opt::PkTab] == 1 && pk_free_ok(sc, G * K, ld_max, 4);
-                const void *tk = s4 ? (const void *)nw_fill_pk_tab_kernel<G, K, PlanSrc, 4>
-                                    : (const void *)nw_fill_pk_tab_kernel<G, K, PlanSrc, 2>;
-                const hipError_t e = big_lds({tk, (const void *)nw_fill_pk_tabfb_kernel<G, K, PlanSrc, kRb>},
-                                             lds_tab);
+                // nw.pk_tab 1: scale 2; 2: the scale-4 body where its window
+                // holds the launch, else scale 2; 3: row profiles (scale 2)
+                // where their 10-byte rows keep three workgroups per CU
+                const size_t lds_prof = (size_t)(256 / G) * (ld_max + 2 * G) * 10;
+                const int sel = o[Opt::PkTab] == 2 && pk_free_ok(sc, G * K, ld_max, 4) ? 4
+                                : o[Opt::PkTab] == 3 && lds_prof <= kLdsPerCu / 3 ? 3 : 2;
+                const void *tk = sel == 4 ? (const void *)nw_fill_pk_tab_kernel<G, K, PlanSrc, 4>
+                                 : sel == 3 ? (const void *)nw_fill_pk_tab_kernel<G, K, PlanSrc, 3>
+                                            : (const void *)nw_fill_pk_tab_kernel<G, K, PlanSrc, 2>;
+                const size_t lds_k = sel == 3 ? lds_prof : lds_tab;
+                hipError_t e = big_lds({tk}, lds_k);
+                if (e == hipSuccess)
+                    e = big_lds({(const void *)nw_fill_pk_tabfb_kernel<G, K, PlanSrc, kRb>}, lds_tab);
                 if (e != hipSuccess) return e;
-                if (s4)
-                    nw_fill_pk_tab_kernel<G, K, PlanSrc, 4><<<grid, dim3(256), lds_tab, s>>>(
+                if (sel == 4)
+                    nw_fill_pk_tab_kernel<G, K, PlanSrc, 4><<<grid, dim3(256), lds_k, s>>>(
+                        src, count, qs, ds, mask, sc, ld_max, fx.bail, fx.epoch);
+                else if (sel == 3)
+                    nw_fill_pk_tab_kernel<G, K, PlanSrc, 3><<<grid, dim3(256), lds_k, s>>>(
                         src, count, qs, ds, mask, sc, ld_max, fx.bail, fx.epoch);
                 else
-                    nw_fill_pk_tab_kernel<G, K, PlanSrc, 2><<<grid, dim3(256), lds_tab, s>>>(
+                    nw_fill_pk_tab_kernel<G, K, PlanSrc, 2><<<grid, dim3(256), lds_k, s>>>(
                         src, count, qs, ds, mask, sc, ld_max, fx.bail, fx.epoch);
                 auto fb = [=, bail = fx.bail, epoch = fx.epoch](hipStream_t fs) {
                     nw_fill_pk_tabfb_kernel<G, K, PlanSrc, kRb><<<grid, dim3(256), lds_tab, fs>>>(

@@ -161,7 +161,7 @@ def test_c2_scale_properties(saln, oracle):
     plan.close()
 
 
-@pytest.mark.parametrize("tab", [1, 2, 0])
+@pytest.mark.parametrize("tab", [1, 2, 3, 0])
 def test_walk_code_formats_match_oracle(saln, oracle, saln_opt, tab):
     """The 4-bit walk codes of the short-query packed fills (8 x 19 groups for
     queries of <= 152 columns, 16 x 10 up to 160) give the oracle's results
@@ -229,7 +229,7 @@ def _run_plan(saln, qs, qo, ds, do, scoring=None):
     return res, cig, off
 
 
-@pytest.mark.parametrize("tab", [1, 2])
+@pytest.mark.parametrize("tab", [1, 2, 3])
 @pytest.mark.parametrize("case", ["acgt", "with_n", "scheme", "long_db", "long_db_n"])
 def test_table_fill_equals_generic(saln, oracle, saln_opt, case, tab):
     """nw.pk_tab = 1 (the 4-bit-code fill with table penalties in the
@@ -243,8 +243,9 @@ def test_table_fill_equals_generic(saln, oracle, saln_opt, case, tab):
     pairs (8 x 19 groups) and 155 x 500 pairs (16 x 10
     groups), whose dbs need the rebasing frame in the original frame but not
     in the extension-free one (the fallback launch then rebases).  tab = 1:
-    the scale-4 table body (round 6; values 4x + p, full-rate subtracts for
-    the walk tests), 2: the scale-2 one."""
+    the scale-2 table body (the default), 2: scale 4 (round 6; values 4x + p,
+    full-rate subtracts for the walk tests), 3: scale 2 with row profiles
+    (round 6; one v_perm per column bonus, no xor)."""
     from sequencealigning_amd import synth
     n, L = 20_000, 150
     LD = L

@@ -4,7 +4,7 @@
 #            REPS alternations of tools/bench_long.py (walk codes and score-only)
 #   abwalk   C2 step with this tree's walker vs sequencealigning_amd/libsaln_prev.so
 #            (an earlier commit's build), sequential and pipelined, REPS alternations
-#   abtab    C2 step, scale-4 table fill (nw.pk_tab=1) vs scale 2 (nw.pk_tab=2), REPS alternations
+#   abtab    C2 step, table fill variants TABS (nw.pk_tab: 1 scale 2, 2 scale 4, 3 row profiles), REPS alternations
 #   c2full   the c2_full leg alone (full 1 B/cell parent sets)
 #   smoke    __graft_entry__.smoke()
 #   tests    pytest -m gpu (TESTS= narrows it to files, KEXPR= to a -k expression)
@@ -58,9 +58,9 @@ for st in ${STAGES:-smoke tests bench}; do
           done
         done
       done ;;
-    abtab)  # C2 table fill at scale 4 (nw.pk_tab=1) vs scale 2 (nw.pk_tab=2), sequential and pipelined
+    abtab)  # C2 table fill variants (nw.pk_tab values TABS), sequential and pipelined
       for i in ${REPS:-1 2}; do
-        for t in 2 1; do
+        for t in ${TABS:-1 3}; do
           for pl in "" "--pipeline"; do
             tag=tab${t}${pl:+_pipe}_$i
             step $tag 180 python tools/ab_c2.py --tag $tag $pl --opt nw.pk_tab=$t
