@@ -1619,10 +1619,9 @@ __device__ __forceinline__ uint32_t hmax3(uint32_t a, uint32_t b, uint32_t c) {
                                                     __builtin_bit_cast(f16x2, c))));
 }
 
-// A step's row inputs: w = the packed db word (kRowProf: the two chars as
-// A | B << 8), lo / hi = kRowProf's profiles of the row's A and B chars.
+// A step's row input: the packed db word of its row.
 struct RowIn {
-    uint32_t w, lo, hi;
+    uint32_t w;
 };
 
 // Returns (per lane; wave-uniform over the lanes that hold pairs): 0 filled
@@ -1637,11 +1636,17 @@ __device__ __forceinline__ int fill_pk_body(Src src, uint32_t count, const uint8
     // table body (kTabMode 1; 4: the same at scale 4, below); kTabMode 2: the
     // generic body of its bail-outs
     constexpr bool kTab = kTabMode == 1 || kTabMode == 4 || kTabMode == 5;
-    // kTabMode 5 (round 6): the table body with row profiles - the staging
-    // holds per row the bonus of each query code against the row's db char of
-    // pair A (dword lo) and of pair B (dword hi), so a column's bonus is one
-    // v_perm with a per-column selector of its query codes (no xor per column);
-    // the rows' db chars sit beside them as 16-bit (A | B << 8) words
+    // kTabMode 5 (round 6): the table body with row profiles.  A step builds
+    // its row's two profiles - the bonus of every query code against the
+    // row's db char of pair A (lo) and of pair B (hi): cmm in each byte, cm in
+    // byte code(char) - with one v_lshl_add each from the staged word
+    // [8 code(A), 0x60, 8 code(B), 0x60], so a column's bonus is one v_perm
+    // with a per-column selector of its query codes instead of an xor and a
+    // v_perm (~19 fewer VALU per step for K = 19).  The staged word >> 3 is
+    // the table body's [code(A), 0x0C, code(B), 0x0C] (the segment's chars).
+    // (A first version staged both profiles in LDS, 10 B per row: fill -4.5 %
+    // alone, but three fill workgroups then took the CU's LDS and the
+    // pipelined walk lost its room: C2 step 0.86 -> 0.99 ms.)
     constexpr bool kRowProf = kTabMode == 5;
     // the extension-free frame (alpha = beta = -2*gap_extend, M~ = H~ + bonus):
     // the table body, and kTabMode 3 = query profiles holding bonuses
@@ -1698,6 +1703,7 @@ __device__ __forceinline__ int fill_pk_body(Src src, uint32_t count, const uint8
     const uint32_t cm = (uint32_t)(kSc * sc.match + alpha + beta) & 0xFFu;
     const uint32_t cmm = (uint32_t)(kSc * sc.mismatch + alpha + beta) & 0xFFu;
     const uint32_t kBonus = cm | cmm * 0x01010100u;
+    const uint32_t kProfBase = cmm * 0x01010101u, kProfStep = cm - cmm;  // kRowProf
     constexpr uint32_t kAcgt = 'A' | 'C' << 8 | 'T' << 16 | 'G' << 24;
     auto acgt = [](uint32_t c) { return c == 'A' || c == 'C' || c == 'G' || c == 'T'; };
     bool bad = false;  // kTabMode: a byte other than A, C, G, T in this lane's share
@@ -1754,12 +1760,6 @@ __device__ __forceinline__ int fill_pk_body(Src src, uint32_t count, const uint8
     uint32_t *__restrict__ myrow = drow + (threadIdx.x / G) * (ld_max + 2 * G) + G;
     uint16_t *__restrict__ myrow16 = reinterpret_cast<uint16_t *>(drow) +
                                      (threadIdx.x / G) * (ld_max + 2 * G) + G;
-    // kRowProf: [GPB][ld_max + 2G] uint2 profiles, then [GPB][ld_max + 2G] chars
-    uint2 *__restrict__ myprof = reinterpret_cast<uint2 *>(drow) +
-                                 (threadIdx.x / G) * (ld_max + 2 * G) + G;
-    uint16_t *__restrict__ mych = reinterpret_cast<uint16_t *>(reinterpret_cast<uint2 *>(drow) +
-                                                               GPB * (ld_max + 2 * G)) +
-                                  (threadIdx.x / G) * (ld_max + 2 * G) + G;
     for (int i = lane; i < ldM; i += G) {
         const uint32_t ca = i < ldA ? (uint32_t)dA[i] : 0u;
         const uint32_t cb = i < ldB ? (uint32_t)dB[i] : 0u;
@@ -1768,10 +1768,7 @@ __device__ __forceinline__ int fill_pk_body(Src src, uint32_t count, const uint8
             myrow16[i] = (uint16_t)(ca | (cb << 8));
         } else if constexpr (kRowProf) {
             bad |= (i < ldA && !acgt(ca)) || (i < ldB && !acgt(cb));
-            // bonus of query code c against this char: cm at byte code(char), cmm elsewhere
-            auto prof = [&](uint32_t c) { return cmm * 0x01010101u + ((cm - cmm) << (8 * ((c >> 1) & 3u))); };
-            myprof[i] = make_uint2(prof(ca), prof(cb));
-            mych[i] = (uint16_t)(ca | (cb << 8));
+            myrow[i] = ((ca >> 1) & 3u) << 3 | ((cb >> 1) & 3u) << 19 | 0x60006000u;
         } else if constexpr (kTab) {
             bad |= (i < ldA && !acgt(ca)) || (i < ldB && !acgt(cb));
             myrow[i] = ((ca >> 1) & 3u) | ((cb >> 1) & 3u) << 16 | 0x0C000C00u;
@@ -1803,8 +1800,6 @@ __device__ __forceinline__ int fill_pk_body(Src src, uint32_t count, const uint8
                                (int64_t)lane * (int64_t)pb.mask_rs;
     const uint32_t *__restrict__ rowp = myrow - lane;  // word of row r-1 at step 0
     const uint16_t *__restrict__ rowp16 = myrow16 - lane;
-    const uint2 *__restrict__ rowpp = myprof - lane;
-    const uint16_t *__restrict__ rowpc = mych - lane;
     const int T = (int)geo.steps((uint32_t)ldM);
     // Walk codes: a lane whose columns all lie past a pair's query stores
     // nothing for it (no walker reads past column len_q; 16 x 10 groups on
@@ -1833,17 +1828,18 @@ __device__ __forceinline__ int fill_pk_body(Src src, uint32_t count, const uint8
         constexpr bool kRun = kSteady && !kRebase;  // running inputs, prefetched db word
         const int r = t - lane + 1;
         uint32_t dch;
-        RowIn rw{};  // kRowProf: the row's profiles (dch holds its chars)
         if constexpr (kRun)
-            rw = row_in;
-        else if constexpr (kRowProf)
-            rw = RowIn{(uint32_t)rowpc[t], rowpp[t].x, rowpp[t].y};
-        if constexpr (kRun || kRowProf)
-            dch = rw.w;
+            dch = row_in.w;
         else if constexpr (kRebase)  // [A, 0, B, 0] << 5
             dch = __builtin_amdgcn_perm(0u, (uint32_t)rowp16[t], 0x0C010C00u) << 5;
         else
             dch = rowp[t];
+        // kRowProf: the row's profiles (v_lshl_add: the shift takes bits 4:0)
+        uint32_t prof_lo = 0, prof_hi = 0;
+        if constexpr (kRowProf) {
+            prof_lo = (kProfStep << (dch & 31u)) + kProfBase;
+            prof_hi = (kProfStep << ((dch >> 16) & 31u)) + kProfBase;
+        }
         int32_t base = 0;  // frame of step t (kRebase)
         if constexpr (kRebase) {
             base = drift * (t & -kRebaseSteps) + ctr;
@@ -1899,7 +1895,7 @@ __device__ __forceinline__ int fill_pk_body(Src src, uint32_t count, const uint8
                 const uint32_t hdk = diag;
                 diag = Hin[k];
                 const uint32_t pen = kProf     ? __builtin_amdgcn_perm(0u, qc[k], psel)
-                                     : kRowProf ? __builtin_amdgcn_perm(rw.hi, rw.lo, qc[k])
+                                     : kRowProf ? __builtin_amdgcn_perm(prof_hi, prof_lo, qc[k])
                                      : kTab     ? __builtin_amdgcn_perm(0u, kBonus, qc[k] ^ dch)
                                                 : umin2(qc[k] ^ dch, kPen);
                 const uint32_t M = kFree ? hdk + pen : hdk - pen;
@@ -2023,7 +2019,7 @@ __device__ __forceinline__ int fill_pk_body(Src src, uint32_t count, const uint8
                 // -> per-pair halves, two groups per dword; the db chars
                 // (dch = A << 5 | B << 21) rotated to bytes 0 / 2
                 constexpr int NG = (K + 3) / 4, ND = NG / 2 + 1;
-                const uint32_t rot = kRowProf ? __builtin_amdgcn_perm(0u, dch, 0x0C010C00u)
+                const uint32_t rot = kRowProf ? __builtin_amdgcn_perm(0u, kAcgt, dch >> 3)
                                      : kTab   ? __builtin_amdgcn_perm(0u, kAcgt, dch)
                                               : __builtin_amdgcn_alignbit(dch, dch, 5);
                 NibSeg<K> na, nb;
@@ -2095,8 +2091,7 @@ __device__ __forceinline__ int fill_pk_body(Src src, uint32_t count, const uint8
     // the steady loop's row inputs, read a step ahead
     auto rowin = [&](int tt) __attribute__((always_inline)) {
         if constexpr (kRebase) return z;
-        else if constexpr (kRowProf) return RowIn{(uint32_t)rowpc[tt], rowpp[tt].x, rowpp[tt].y};
-        else return RowIn{rowp[tt], 0u, 0u};
+        else return RowIn{rowp[tt]};
     };
     for (; t < tS0; t += 2) {
         step(t, Hp, HpB, G0, z);
@@ -3297,10 +3292,9 @@ static hipError_t fill_pk(dim3 grid, hipStream_t s, const NwPairDesc *pairs, uin
                 constexpr bool kRb = decltype(rebase_c)::value;
                 // nw.pk_tab 1: scale 2; 2: the scale-4 body where its window
                 // holds the launch, else scale 2; 3: row profiles (scale 2)
-                // where their 10-byte rows keep three workgroups per CU
-                const size_t lds_prof = (size_t)(256 / G) * (ld_max + 2 * G) * 10;
+                const size_t lds_prof = lds_tab;
                 const int sel = o[Opt::PkTab] == 2 && pk_free_ok(sc, G * K, ld_max, 4) ? 4
-                                : o[Opt::PkTab] == 3 && lds_prof <= kLdsPerCu / 3 ? 3 : 2;
+                                : o[Opt::PkTab] == 3 ? 3 : 2;
                 const void *tk = sel == 4 ? (const void *)nw_fill_pk_tab_kernel<G, K, PlanSrc, 4>
                                  : sel == 3 ? (const void *)nw_fill_pk_tab_kernel<G, K, PlanSrc, 3>
                                             : (const void *)nw_fill_pk_tab_kernel<G, K, PlanSrc, 2>;
