@@ -23,7 +23,7 @@ const OptDesc kDesc[kNumOpts] = {
     {"nw.rows_lone", 1, 0, 1},
     {"nw.rows_xcd", 1, 0, 1},
     {"nw.avsa_profile", 1, 0, 1},
-    {"nw.pk_tab", 1, 0, 3},
+    {"nw.pk_tab", 3, 0, 3},
     {"nw.walk_waves", -1, -1, 1 << 20},
     {"wfa2.seq_lds", 24 * 1024, 0, 64 * 1024},
     {"wfa2.w1", 0, 0, 4096},

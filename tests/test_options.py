@@ -29,7 +29,7 @@ def test_option_set_get_reset(saln):
     assert _lib.non_default_options() == {"nw.spec_passes": 5}
     with _lib.options(**{"nw.spec_passes": 7, "nw.pk_tab": 0}):
         assert _lib.get_option("nw.spec_passes")[0] == 7 and _lib.get_option("nw.pk_tab")[0] == 0
-    assert _lib.get_option("nw.spec_passes")[0] == 5 and _lib.get_option("nw.pk_tab")[0] == 1
+    assert _lib.get_option("nw.spec_passes")[0] == 5 and _lib.get_option("nw.pk_tab")[0] == 3
     assert _lib.lib().saln_options_reset() == 0
     assert _lib.non_default_options() == {}
 
