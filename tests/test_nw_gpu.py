@@ -785,11 +785,12 @@ def test_context_options_two_threads(saln, oracle):
     want = [oracle.nw(qs[k], ds[k], literal_dfs=False) for k in range(0, n, 10)]
     ctxs = [_lib.new_context(0), _lib.new_context(0)]
     try:
+        default = _lib.get_option("nw.pk_tab")[1]
         _lib.set_context_option(ctxs[0], "nw.pk_tab", 1)
         _lib.set_context_option(ctxs[1], "nw.pk_tab", 0)
         assert _lib.get_context_option(ctxs[1], "nw.pk_tab") == 0
-        assert _lib.get_option("nw.pk_tab")[0] == 1
-        assert _lib.get_context_option(_lib.context(0), "nw.pk_tab") == 1
+        assert _lib.get_option("nw.pk_tab")[0] == default
+        assert _lib.get_context_option(_lib.context(0), "nw.pk_tab") == default
         out = [None, None]
         errs = []
 
@@ -818,7 +819,7 @@ def test_context_options_two_threads(saln, oracle):
                     assert (saln.cigar_ops_string(cg[k]) if res["printed"][k] else None) == \
                         o.first_ops, (i, k)
         _lib.clear_context_option(ctxs[1])
-        assert _lib.get_context_option(ctxs[1], "nw.pk_tab") == 1
+        assert _lib.get_context_option(ctxs[1], "nw.pk_tab") == default
     finally:
         for c in ctxs:
             L.saln_context_destroy(c)
