@@ -713,6 +713,9 @@ int saln_nw_execute(saln_nw_plan *p, const uint8_t *d_q, const uint8_t *d_db,
     HIP_TRY(hipEventRecord(filled, s));
     if (t != s) HIP_TRY(hipStreamWaitEvent(t, filled, 0));
     for (auto &fb : fallbacks) HIP_TRY(fb(t));
+    // (async plans: the deferred fallback launches sit between ev[1] and
+    // ev[2], so neither "nw_fill" nor "nw_traceback" counts them; they run
+    // only for waves whose pairs hold a byte other than A, C, G, T)
     if (ev) HIP_TRY(hipEventRecord(ev[2], t));
     for (int v = 0; v < kNumVariants; ++v) {
         const uint32_t a = p->var_first[v], b = a + p->var_count[v];
