@@ -139,15 +139,22 @@ __device__ __forceinline__ int32_t wfa_pair(const S &q, int32_t lq, const S &d, 
     const int32_t tx = prm.x / prm.g, toe = (prm.o + prm.e) / prm.g, te = prm.e / prm.g;
     const int32_t kend = ld - lq;
     __builtin_amdgcn_wave_barrier();
+    // wnd: per slot, the diagonals its step wrote (kNeg outside the slot's
+    // own range within them): [mLo, mLo + 256 groups - 1]
+    int32_t *wnd = rng + 6 * kRingMax;
     if (lane < 3 * kRingMax) {  // every slot empty
         rng[2 * lane] = kEmptyLo;
         rng[2 * lane + 1] = -kEmptyLo;
+        wnd[2 * lane] = kEmptyLo;
+        wnd[2 * lane + 1] = -kEmptyLo;
     }
     // s = 0: M[0][0] = 0, extended
     if (lane == 0) {
         Mr[0] = (OffT)extend(q, lq, d, ld, 0, 0);
         rng[0] = 0;
         rng[1] = 0;
+        wnd[0] = 0;
+        wnd[1] = 0;
     }
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
     __builtin_amdgcn_wave_barrier();
@@ -161,17 +168,22 @@ __device__ __forceinline__ int32_t wfa_pair(const S &q, int32_t lq, const S &d, 
         sM = sM + 1 == prm.RM ? 0 : sM + 1;
         sI = sI + 1 == prm.RI ? 0 : sI + 1;
         // sources (slot, range); a negative step or an empty slot has lo > hi
+        // the sources' written windows: wl = the highest start, wh = the lowest end
+        int32_t wl = -kEmptyLo, wh = kEmptyLo;
         auto src = [&](int comp, int32_t ts, int32_t slot_now, int32_t back, int32_t ring,
                        int32_t &slot, int32_t &lo, int32_t &hi) __attribute__((always_inline)) {
             if (ts < 0) {
                 slot = 0;
                 lo = kEmptyLo;
                 hi = -kEmptyLo;
+                wl = kEmptyLo;
                 return;
             }
             slot = wrap(slot_now - back, ring);  // back < ring
             lo = rng[2 * (comp * kRingMax + slot)];
             hi = rng[2 * (comp * kRingMax + slot) + 1];
+            wl = max(wl, wnd[2 * (comp * kRingMax + slot)]);
+            wh = min(wh, wnd[2 * (comp * kRingMax + slot) + 1]);
         };
         int32_t soe, loMo, hiMo, sx, loMx, hiMx, sie, loI, hiI, sde, loD, hiD;
         src(0, t - toe, sM, toe, prm.RM, soe, loMo, hiMo);
@@ -192,6 +204,9 @@ __device__ __forceinline__ int32_t wfa_pair(const S &q, int32_t lq, const S &d, 
                 rng[2 * sM] = kEmptyLo, rng[2 * sM + 1] = -kEmptyLo;
                 rng[2 * (kRingMax + sI)] = kEmptyLo, rng[2 * (kRingMax + sI) + 1] = -kEmptyLo;
                 rng[2 * (2 * kRingMax + sI)] = kEmptyLo, rng[2 * (2 * kRingMax + sI) + 1] = -kEmptyLo;
+                wnd[2 * sM] = kEmptyLo, wnd[2 * sM + 1] = -kEmptyLo;
+                wnd[2 * (kRingMax + sI)] = kEmptyLo, wnd[2 * (kRingMax + sI) + 1] = -kEmptyLo;
+                wnd[2 * (2 * kRingMax + sI)] = kEmptyLo, wnd[2 * (2 * kRingMax + sI) + 1] = -kEmptyLo;
             }
             __builtin_amdgcn_s_waitcnt(0xC07F);
             __builtin_amdgcn_wave_barrier();
@@ -226,6 +241,13 @@ __device__ __forceinline__ int32_t wfa_pair(const S &q, int32_t lq, const S &d, 
         // a group never spans more than W diagonals, so nothing valid is hit.
         // (I and D outside their own ranges read -inf from both sources.)
         const int32_t span = mHi - mLo;
+        // Round 6: a chunk whose reads (its diagonals - 1 .. + 1) lie inside
+        // every source's written window, and whose diagonals all lie in the
+        // step's range, reads without the range selects (an entry of a written
+        // window outside its slot's range is kNeg) and writes M unmasked.
+        // Near the range's ends, and in steps with an empty source, the
+        // checked reads stay.  (wfa_pair's sources are all this pair's steps.)
+        const int32_t fast_lo = wl + 1 - mLo, fast_hi = min(wh - 64, mHi - 63) - mLo;
 #pragma unroll
         for (int g = 0; g < CM / 4; ++g) {
             if (256 * g > span) break;  // uniform
@@ -234,6 +256,22 @@ __device__ __forceinline__ int32_t wfa_pair(const S &q, int32_t lq, const S &d, 
 #pragma unroll
             for (int c = 0; c < 4; ++c) {
                 const int32_t k = mLo + 64 * (4 * g + c) + lane;
+                const int32_t kc = 64 * (4 * g + c);  // the chunk's first diagonal - mLo
+                if (kc >= fast_lo && kc <= fast_hi) {  // uniform
+                    auto rdf = [&](const OffT *ring, int32_t slot, int32_t kk) __attribute__((always_inline)) {
+                        return (int32_t)ring[slot * W + (kk & wm)];
+                    };
+                    int32_t I = max(rdf(Mr, soe, k - 1), rdf(Ir, sie, k - 1)) + 1;
+                    I = cell(I, k) ? I : kNeg;
+                    int32_t D = max(rdf(Mr, soe, k + 1), rdf(Dr, sde, k + 1));
+                    D = cell(D, k) ? D : kNeg;
+                    int32_t X = rdf(Mr, sx, k) + 1;
+                    X = cell(X, k) ? X : kNeg;
+                    Iv[c] = I;
+                    Dv[c] = D;
+                    Mv[c] = max(X, max(I, D));
+                    continue;
+                }
                 int32_t I = max(rd(Mr, soe, k - 1, loMo, spMo), rd(Ir, sie, k - 1, loI, spI)) + 1;
                 I = cell(I, k) ? I : kNeg;
                 int32_t D = max(rd(Mr, soe, k + 1, loMo, spMo), rd(Dr, sde, k + 1, loD, spD));
@@ -274,6 +312,10 @@ __device__ __forceinline__ int32_t wfa_pair(const S &q, int32_t lq, const S &d, 
             rng[2 * sM] = mLo, rng[2 * sM + 1] = mHi;
             rng[2 * (kRingMax + sI)] = iLo, rng[2 * (kRingMax + sI) + 1] = iHi;
             rng[2 * (2 * kRingMax + sI)] = dLo, rng[2 * (2 * kRingMax + sI) + 1] = dHi;
+            const int32_t wtop = mLo + 256 * (span / 256 + 1) - 1;  // the groups written
+            wnd[2 * sM] = mLo, wnd[2 * sM + 1] = wtop;
+            wnd[2 * (kRingMax + sI)] = mLo, wnd[2 * (kRingMax + sI) + 1] = wtop;
+            wnd[2 * (2 * kRingMax + sI)] = mLo, wnd[2 * (2 * kRingMax + sI) + 1] = wtop;
         }
         __builtin_amdgcn_s_waitcnt(0xC07F);
         __builtin_amdgcn_wave_barrier();
@@ -340,8 +382,8 @@ __global__ __launch_bounds__(64) void wfa_affine_kernel(const WfaAffPair *__rest
     if (n_dev) n_pairs = *n_dev;
     extern __shared__ __attribute__((aligned(16))) uint8_t lds_raw[];
     // ranges: [component][slot] = (lo, hi); component 0 M, 1 I, 2 D
-    int32_t *rng = (int32_t *)lds_raw;
-    OffT *Mr = (OffT *)(lds_raw + 3 * kRingMax * 2 * sizeof(int32_t));
+    int32_t *rng = (int32_t *)lds_raw;  // then the written windows (wfa_pair's wnd)
+    OffT *Mr = (OffT *)(lds_raw + 2 * 3 * kRingMax * 2 * sizeof(int32_t));
     OffT *Ir = Mr + prm.RM * prm.W;
     OffT *Dr = Ir + prm.RI * prm.W;
     // staged sequences (prm.seqcap bytes, 16-aligned after the rings)
@@ -409,7 +451,7 @@ __global__ __launch_bounds__(64) void wfa_affine_kernel(const WfaAffPair *__rest
 }  // namespace
 
 size_t wfa_affine_lds_bytes(const WfaAffParams &prm, bool wide) {
-    const size_t rings = 3 * kRingMax * 2 * sizeof(int32_t) +
+    const size_t rings = 2 * 3 * kRingMax * 2 * sizeof(int32_t) +
                          (size_t)(prm.RM + 2 * prm.RI) * prm.W *
                              (wide ? sizeof(int32_t) : sizeof(int16_t));
     return ((rings + 15) & ~(size_t)15) + (size_t)prm.seqcap;
