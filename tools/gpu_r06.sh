@@ -68,6 +68,13 @@ for st in ${STAGES:-smoke tests bench}; do
           done
         done
       done ;;
+    abwfa2)  # corrected WFA: this tree vs sequencealigning_amd/libsaln_prev.so, REPS alternations
+      for i in ${REPS:-1 2}; do
+        SALN_LIB=sequencealigning_amd/libsaln_prev.so step wfa2_prev_$i 300 python tools/bench_wfa_affine.py --pairs 200000
+        tail -1 $O/wfa2_prev_$i.log
+        step wfa2_cur_$i 300 python tools/bench_wfa_affine.py --pairs 200000
+        tail -1 $O/wfa2_cur_$i.log
+      done ;;
     c2full) step c2full 400 python bench.py --steps 5 --warmup 2 --legs c2_full --no-cpu-baseline
             tail -1 $O/c2full.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(json.dumps(d['configs']['c2_full'])[:1500])" ;;
     chains) step chains 300 tools/micro/row_chains
