@@ -241,10 +241,10 @@ __device__ __forceinline__ int32_t wfa_pair(const S &q, int32_t lq, const S &d, 
         // a group never spans more than W diagonals, so nothing valid is hit.
         // (I and D outside their own ranges read -inf from both sources.)
         const int32_t span = mHi - mLo;
-        // Round 6: a group of chunks whose reads (its diagonals - 1 .. + 1) lie
-        // inside every source's written window, and whose diagonals all lie in
-        // the step's range, reads without the range selects (an entry of a
-        // written window outside its slot's range is kNeg) and writes M unmasked.
+        // Round 6: a chunk whose reads (its diagonals - 1 .. + 1) lie inside
+        // every source's written window, and whose diagonals all lie in the
+        // step's range, reads without the range selects (an entry of a written
+        // window outside its slot's range is kNeg) and writes M unmasked.
         // Near the range's ends, and in steps with an empty source, the
         // checked reads stay.  (wfa_pair's sources are all this pair's steps.)
         const int32_t fast_lo = wl + 1 - mLo, fast_hi = min(wh - 64, mHi - 63) - mLo;
@@ -253,15 +253,14 @@ __device__ __forceinline__ int32_t wfa_pair(const S &q, int32_t lq, const S &d, 
             if (256 * g > span) break;  // uniform
             int32_t Mv[4], Iv[4], Dv[4];
             bool slow[4];
-            // the group's four chunks inner (uniform): a branch-free group
-            // either way, so the four chunks' LDS reads still overlap
-            if (256 * g >= fast_lo && 256 * g + 192 <= fast_hi) {
-                auto rdf = [&](const OffT *ring, int32_t slot, int32_t kk) __attribute__((always_inline)) {
-                    return (int32_t)ring[slot * W + (kk & wm)];
-                };
 #pragma unroll
-                for (int c = 0; c < 4; ++c) {
-                    const int32_t k = mLo + 64 * (4 * g + c) + lane;
+            for (int c = 0; c < 4; ++c) {
+                const int32_t k = mLo + 64 * (4 * g + c) + lane;
+                const int32_t kc = 64 * (4 * g + c);  // the chunk's first diagonal - mLo
+                if (kc >= fast_lo && kc <= fast_hi) {  // uniform
+                    auto rdf = [&](const OffT *ring, int32_t slot, int32_t kk) __attribute__((always_inline)) {
+                        return (int32_t)ring[slot * W + (kk & wm)];
+                    };
                     int32_t I = max(rdf(Mr, soe, k - 1), rdf(Ir, sie, k - 1)) + 1;
                     I = cell(I, k) ? I : kNeg;
                     int32_t D = max(rdf(Mr, soe, k + 1), rdf(Dr, sde, k + 1));
@@ -271,22 +270,18 @@ __device__ __forceinline__ int32_t wfa_pair(const S &q, int32_t lq, const S &d, 
                     Iv[c] = I;
                     Dv[c] = D;
                     Mv[c] = max(X, max(I, D));
+                    continue;
                 }
-            } else {
-#pragma unroll
-                for (int c = 0; c < 4; ++c) {
-                    const int32_t k = mLo + 64 * (4 * g + c) + lane;
-                    int32_t I = max(rd(Mr, soe, k - 1, loMo, spMo), rd(Ir, sie, k - 1, loI, spI)) + 1;
-                    I = cell(I, k) ? I : kNeg;
-                    int32_t D = max(rd(Mr, soe, k + 1, loMo, spMo), rd(Dr, sde, k + 1, loD, spD));
-                    D = cell(D, k) ? D : kNeg;
-                    int32_t X = rd(Mr, sx, k, loMx, spMx) + 1;
-                    X = cell(X, k) ? X : kNeg;
-                    const int32_t M = max(X, max(I, D));
-                    Iv[c] = I;
-                    Dv[c] = D;
-                    Mv[c] = (uint32_t)(k - mLo) <= (uint32_t)span ? M : kNeg;
-                }
+                int32_t I = max(rd(Mr, soe, k - 1, loMo, spMo), rd(Ir, sie, k - 1, loI, spI)) + 1;
+                I = cell(I, k) ? I : kNeg;
+                int32_t D = max(rd(Mr, soe, k + 1, loMo, spMo), rd(Dr, sde, k + 1, loD, spD));
+                D = cell(D, k) ? D : kNeg;
+                int32_t X = rd(Mr, sx, k, loMx, spMx) + 1;
+                X = cell(X, k) ? X : kNeg;
+                const int32_t M = max(X, max(I, D));
+                Iv[c] = I;
+                Dv[c] = D;
+                Mv[c] = (uint32_t)(k - mLo) <= (uint32_t)span ? M : kNeg;
             }
             uint32_t more = 0;  // bit c: chunk c's lane matched 4 bases, keep extending
 #pragma unroll
