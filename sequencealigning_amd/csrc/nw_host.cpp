@@ -1015,88 +1015,90 @@ char col_d(int st, const uint8_t *d, uint32_t i) { return st == ST_I ? '-' : (ch
 DfsOutcome render_blocks(const HostMask &hm, const uint8_t *q, const uint8_t *d,
                          uint64_t max_blocks, std::string *out) {
     DfsOutcome res;
-    struct Item {
-        Node n;
-        uint32_t depth;
-    };
-    // Every mask layout is row-separable: cell(i, j) = (i-1) RS + co[j] (the
-    // packed stripes' skew included, RS = 256), so a node's code byte is one
-    // multiply-add and a table load instead of Geom::cell's divisions.
     const uint32_t lq = hm.lq, ld = hm.ld;
+    // Every mask layout is row-separable: cell(i, j) = (i-1) RS + co[j] (the
+    // packed stripes' skew included, RS = 256), so a node's code byte is a
+    // row pointer and a column offset from two tables instead of
+    // Geom::cell's divisions.
     std::vector<uint64_t> co(lq + 1, 0);
     for (uint32_t j = 1; j <= lq && ld; ++j) co[j] = hm.g.cell(1, j, hm.rs, hm.bs, hm.cs);
     const uint64_t RS = hm.bs == 0 ? 256 : hm.rs;
-    auto byte = [&](uint32_t i, uint32_t j) -> uint8_t {
-        return hm.m[(uint64_t)(i - 1) * RS + co[j]] ^ 0x7F;
-    };
-    auto argmax = [&](uint32_t i, uint32_t j) -> uint8_t {
-        if (i == 0 || j == 0) return hm.argmax(i, j);
-        return byte(i, j) & 7;
-    };
-    auto kids = [&](int st, uint32_t i, uint32_t j, int *ps, uint32_t *pi, uint32_t *pj) -> int {
-        if (i == 0 || j == 0 || (st == ST_I && j == 1) || (st == ST_D && i == 1))
-            return parents(hm, st, i, j, ps, pi, pj);
-        int n = 0;
-        if (st == ST_M) {
-            const uint8_t a = argmax(i - 1, j - 1);
-            if (a & kArgM) { ps[n] = ST_M; pi[n] = i - 1; pj[n] = j - 1; ++n; }
-            if (a & kArgI) { ps[n] = ST_I; pi[n] = i - 1; pj[n] = j - 1; ++n; }
-            if (a & kArgD) { ps[n] = ST_D; pi[n] = i - 1; pj[n] = j - 1; ++n; }
-        } else if (st == ST_I) {
-            const uint8_t b = (byte(i, j - 1) >> 3) & 3;
-            if (b & 1) { ps[n] = ST_I; pi[n] = i; pj[n] = j - 1; ++n; }
-            if (b & 2) { ps[n] = ST_M; pi[n] = i; pj[n] = j - 1; ++n; }
-        } else {
-            const uint8_t b = (byte(i - 1, j) >> 5) & 3;
-            if (b & 1) { ps[n] = ST_D; pi[n] = i - 1; pj[n] = j; ++n; }
-            if (b & 2) { ps[n] = ST_M; pi[n] = i - 1; pj[n] = j; ++n; }
-        }
-        return n;
+    std::vector<const uint8_t *> rowp(ld + 1, nullptr);
+    for (uint32_t i = 1; i <= ld && lq; ++i) rowp[i] = hm.m + (uint64_t)(i - 1) * RS;
+    auto byte = [&](uint32_t i, uint32_t j) -> uint32_t { return rowp[i][co[j]] ^ 0x7Fu; };
+    struct Item {
+        uint32_t i, j, st, depth;
     };
     std::vector<Item> stack;
+    stack.reserve(4 * ((size_t)lq + ld) + 8);
     // the path's columns stored back to front (depth k at cap - 1 - k), so a
     // block's three lines are three contiguous copies
     const uint32_t cap = lq + ld + 1;
     std::vector<char> p1(cap), p2(cap), pb(cap);
-    Node ends[3];
-    const int ne = end_nodes(hm, ends);
-    for (int k = ne - 1; k >= 0; --k) stack.push_back({ends[k], 0});  // pop order D, M, I
+    {   // end states pushed I, M, D (:251-280): popped D, M, I
+        const uint8_t a = hm.argmax(ld, lq);
+        if (a & kArgI) stack.push_back({ld, lq, ST_I, 0});
+        if (a & kArgM) stack.push_back({ld, lq, ST_M, 0});
+        if (a & kArgD) stack.push_back({ld, lq, ST_D, 0});
+    }
     while (!stack.empty()) {
-        const Item it = stack.back();
+        Item it = stack.back();
         stack.pop_back();
-        const Node n = it.n;
-        if (n.i == 0 && n.j == 0) {  // :283-286
-            if (max_blocks && res.blocks >= max_blocks) {
-                res.status = SALN_ENUM_CAP;
+        // a node's last pushed parent is the next popped: it is followed at
+        // once, without the stack, down the chain until a leaf
+        for (;;) {
+            const uint32_t i = it.i, j = it.j, st = it.st, dep = it.depth;
+            if (i == 0 && j == 0) {  // :283-286
+                if (max_blocks && res.blocks >= max_blocks) {
+                    res.status = SALN_ENUM_CAP;
+                    return res;
+                }
+                if (out) {
+                    const uint32_t a = cap - dep;
+                    out->append("alignment found\n\nseq1: ");
+                    out->append(p1.data() + a, dep);
+                    out->append("\n      ");
+                    out->append(pb.data() + a, dep);
+                    out->append("\nseq2: ");
+                    out->append(p2.data() + a, dep);
+                    out->push_back('\n');
+                }
+                ++res.blocks;
+                break;
+            }
+            // parents in the reference's push order (parents() above)
+            uint32_t ps[3], pi[3], pj[3];
+            int np = 0;
+            if (i == 0 || j == 0) {  // boundary nodes, :172-216
+                if (st == ST_D && i == 0) { ps[0] = ST_D; pi[0] = 0; pj[0] = j - 1; np = 1; }
+                else if (st == ST_I && j == 0) { ps[0] = ST_I; pi[0] = i - 1; pj[0] = 0; np = 1; }
+            } else if (st == ST_M) {
+                const uint32_t a = (i == 1 || j == 1) ? hm.argmax(i - 1, j - 1) : (byte(i - 1, j - 1) & 7u);
+                if (a & kArgM) { ps[np] = ST_M; pi[np] = i - 1; pj[np] = j - 1; ++np; }
+                if (a & kArgI) { ps[np] = ST_I; pi[np] = i - 1; pj[np] = j - 1; ++np; }
+                if (a & kArgD) { ps[np] = ST_D; pi[np] = i - 1; pj[np] = j - 1; ++np; }
+            } else if (st == ST_I) {
+                const uint32_t b = j == 1 ? ibits_col1(hm.sc, i) : (byte(i, j - 1) >> 3) & 3u;
+                if (b & 1) { ps[np] = ST_I; pi[np] = i; pj[np] = j - 1; ++np; }
+                if (b & 2) { ps[np] = ST_M; pi[np] = i; pj[np] = j - 1; ++np; }
+            } else {
+                const uint32_t b = i == 1 ? dbits_row1(hm.sc, j) : (byte(i - 1, j) >> 5) & 3u;
+                if (b & 1) { ps[np] = ST_D; pi[np] = i - 1; pj[np] = j; ++np; }
+                if (b & 2) { ps[np] = ST_M; pi[np] = i - 1; pj[np] = j; ++np; }
+            }
+            if (np == 0) break;  // a sentinel-rooted dead end: dropped silently
+            if (panics((int)st, i, j, np)) {
+                res.status = SALN_REF_PANIC_BOUNDARY;
                 return res;
             }
-            if (out) {
-                const uint32_t D = it.depth, a = cap - D;
-                out->append("alignment found\n\nseq1: ");
-                out->append(p1.data() + a, D);
-                out->append("\n      ");
-                out->append(pb.data() + a, D);
-                out->append("\nseq2: ");
-                out->append(p2.data() + a, D);
-                out->push_back('\n');
-            }
-            ++res.blocks;
-        }
-        int ps[3];
-        uint32_t pi[3], pj[3];
-        const int np = kids(n.st, n.i, n.j, ps, pi, pj);
-        if (panics(n.st, n.i, n.j, np)) {
-            res.status = SALN_REF_PANIC_BOUNDARY;
-            return res;
-        }
-        if (np) {
-            const uint32_t x = cap - 1 - it.depth;
-            const char c1 = col_q(n.st, q, n.j), c2 = col_d(n.st, d, n.i);
+            const uint32_t x = cap - 1 - dep;
+            const char c1 = col_q((int)st, q, j), c2 = col_d((int)st, d, i);
             p1[x] = c1;
             p2[x] = c2;
             pb[x] = c1 == c2 ? '|' : ' ';
+            for (int k = 0; k < np - 1; ++k) stack.push_back({pi[k], pj[k], ps[k], dep + 1});
+            it = {pi[np - 1], pj[np - 1], ps[np - 1], dep + 1};
         }
-        for (int k = 0; k < np; ++k) stack.push_back({{ps[k], pi[k], pj[k]}, it.depth + 1});
     }
     return res;
 }
