@@ -248,6 +248,14 @@ int saln_nw_plan_create_full(saln_context *ctx, const uint64_t *q_off, uint64_t 
  * (waits for it), as saln_nw_dense_mask lays them out: (len_db+1) x (len_q+1)
  * bytes. */
 int saln_nw_plan_dense_mask(saln_nw_plan *plan, uint64_t pair, uint8_t *out);
+/* The 4-bit walk codes a (non-full) plan's short-query fills store for pair
+ * `pair` (parity tests): len_db x len_q bytes, cell (i, j) at (i-1) len_q +
+ * j-1, bits set when the parent is ABSENT - 0 argI, 1 argD (M's predecessor:
+ * I / D in max(M, I, D) at (i, j), :120-153), 2 I-open (M(i, j) + open
+ * among the maxima of I(i, j+1), :108-119), 3 D-open (the same for D(i+1,
+ * j), :96-107); in the last row bit 3 of the end cell is argM.  Last
+ * synchronous execute; SALN_E_INVALID for a pair stored otherwise. */
+int saln_nw_plan_walk_codes(saln_nw_plan *plan, uint64_t pair, uint8_t *out);
 /* mask_bytes: HBM parent-mask workspace (owned by the plan);
  * cigar_words: required length of the device cigar buffer. */
 int saln_nw_plan_info(const saln_nw_plan *plan, uint64_t *mask_bytes, uint64_t *cigar_words,

@@ -84,6 +84,7 @@ EXPORTS = [
     "saln_context_create", "saln_context_destroy", "saln_last_error", "saln_abi_version",
     "saln_nw_align", "saln_nw_render", "saln_nw_dense_mask", "saln_nw_align_batch",
     "saln_nw_plan_create", "saln_nw_plan_create_full", "saln_nw_plan_dense_mask",
+    "saln_nw_plan_walk_codes",
     "saln_nw_plan_info", "saln_nw_cigar_offsets", "saln_nw_execute",
     "saln_nw_plan_set_timing", "saln_nw_plan_kernel_time", "saln_nw_plan_set_async",
     "saln_nw_plan_set_score_only", "saln_nw_plan_sync", "saln_nw_plan_destroy",
@@ -167,6 +168,7 @@ def lib() -> C.CDLL:
                                           C.POINTER(vp)]
         L.saln_nw_plan_create_full.argtypes = L.saln_nw_plan_create.argtypes
         L.saln_nw_plan_dense_mask.argtypes = [vp, C.c_uint64, vp]
+        L.saln_nw_plan_walk_codes.argtypes = [vp, C.c_uint64, vp]
         L.saln_nw_plan_info.argtypes = [vp, u64p, u64p, u64p]
         L.saln_nw_cigar_offsets.argtypes = [vp, vp]
         L.saln_nw_execute.argtypes = [vp, vp, vp, vp, vp, vp]

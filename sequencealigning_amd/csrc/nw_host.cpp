@@ -221,6 +221,41 @@ int saln_nw_plan_dense_mask(saln_nw_plan *p, uint64_t pair, uint8_t *out) {
     return SALN_OK;
 }
 
+int saln_nw_plan_walk_codes(saln_nw_plan *p, uint64_t pair, uint8_t *out) {
+    if (!p || !out || pair >= p->n_pairs) return SALN_E_INVALID;
+    if (p->async_tb) {
+        set_error("saln_nw_plan_walk_codes: synchronous plans only");
+        return SALN_E_INVALID;
+    }
+    const NwPairDesc &d = p->h_pairs[p->plan_index[pair]];
+    if (d.variant >= (uint32_t)kNumVariants || !p->nib[d.variant] || !d.len_q || !d.len_db) {
+        set_error("saln_nw_plan_walk_codes: the pair's fill stores no 4-bit walk codes");
+        return SALN_E_INVALID;
+    }
+    HIP_TRY(hipSetDevice(p->ctx->device));
+    for (int b = 0; b < 2; ++b)
+        if (p->tb_pending[b]) HIP_TRY(hipEventSynchronize(p->tb_done(b)));
+    // segments of block b at row i: mask_off + (i-1) rs + b bs (Geom::LBn
+    // bytes; column c's nibble at bit nib_bit(c) of dword c / 8)
+    const Geom g = variant_geom((int)d.variant);
+    // every block of each row (rs / bs of them: the pack's width) as one
+    // bs-pitched 2-D region of LBn-byte rows
+    const uint64_t per_row = d.mask_rs / d.mask_bs;
+    std::vector<uint8_t> all((uint64_t)d.len_db * per_row * g.LBn());
+    HIP_TRY(hipMemcpy2D(all.data(), g.LBn(), p->d_mask + d.mask_off, d.mask_bs, g.LBn(),
+                        (uint64_t)d.len_db * per_row, hipMemcpyDeviceToHost));
+    for (uint32_t i = 1; i <= d.len_db; ++i)
+        for (uint32_t j = 1; j <= d.len_q; ++j) {
+            const uint32_t b = (j - 1) / g.K, c = (j - 1) % g.K;
+            const uint8_t *sp = all.data() + ((uint64_t)(i - 1) * per_row + b) * g.LBn();
+            uint32_t w;
+            std::memcpy(&w, sp + 4 * (c >> 3), 4);
+            const uint32_t bit = ((c & 4u) << 2) | ((c & 1u) << 3) | ((c & 2u) << 1);
+            out[(uint64_t)(i - 1) * d.len_q + (j - 1)] = (uint8_t)((w >> bit) & 15u);
+        }
+    return SALN_OK;
+}
+
 }  // extern "C"
 
 // Plan creation.  full_codes: the fills store every parent set (host DFS,

@@ -323,6 +323,16 @@ class NwPlan:
                    "saln_nw_plan_dense_mask")
         return out
 
+    def walk_codes(self, pair: int) -> np.ndarray:
+        """Pair `pair`'s 4-bit walk codes from the last execute of a synchronous
+        plan: (len_db, len_q) uint8, bits set = parent absent (0 argI, 1 argD,
+        2 I-open, 3 D-open; argM at the end cell), saln_nw_plan_walk_codes."""
+        lq, ld = int(self._lens[0][pair]), int(self._lens[1][pair])
+        out = np.zeros((ld, lq), np.uint8)
+        _lib.check(self._L.saln_nw_plan_walk_codes(self._h, pair, out.ctypes.data_as(C.c_void_p)),
+                   "saln_nw_plan_walk_codes")
+        return out
+
     def status(self) -> int:
         """Wait for every execute since the last call; return and clear the
         device error flags they raised (include/saln.h saln_nw_plan_status)."""

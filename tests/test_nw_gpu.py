@@ -1035,3 +1035,53 @@ def test_full_code_plan_c2(saln, oracle, async_):
         assert int(rr["score"][k]) == o.score, shapes[k]
         assert np.array_equal(plan.dense_mask(k), o.dense_mask), shapes[k]
     plan.close()
+
+
+@pytest.mark.parametrize("tab", [0, 1, 2, 3])
+def test_walk_codes_bit_by_bit(saln, oracle, saln_opt, tab):
+    """the 4-bit walk codes of the short-query fills
+    (8 x 19 for <= 152 query columns, 16 x 10 up to 160), read back from the
+    plan (saln_nw_plan_walk_codes), equal bit by bit what the reference's
+    parent sets say for every cell the walker can read: argI / argD (I or D
+    among the maxima at (i, j)), I-open (M + open among the maxima of I(i,
+    j+1)), D-open (of D(i+1, j)), and argM at the end cell - through the
+    generic fill (nw.pk_tab 0), the constant-table fill (1), scale 4 (2) and
+    row profiles (3), with N bytes in some pairs (their waves take the
+    fallback launch) and a db longer than the query's frame."""
+    import torch
+    saln_opt("nw.pk_tab", tab)
+    rng = np.random.default_rng(707 + tab)
+    shapes = [(150, 150)] * 6 + [(156, 156)] * 4 + [(152, 40), (140, 420), (160, 90), (37, 151)]
+    qsl = [bytearray(rand_seq(rng, a)) for a, _ in shapes]
+    dsl = [bytearray(rand_seq(rng, b)) for _, b in shapes]
+    for k in (1, 7):  # N bytes: those waves go to the fallback launch
+        qsl[k][int(rng.integers(len(qsl[k])))] = ord("N")
+        dsl[k][int(rng.integers(len(dsl[k])))] = ord("N")
+    base = rand_seq(rng, 150)  # tie-heavy: near-identical pair
+    qsl.append(bytearray(base))
+    dsl.append(bytearray(base[:70] + base[71:]))
+    qsl, dsl = [bytes(x) for x in qsl], [bytes(x) for x in dsl]
+    m = len(qsl)
+    qcat, qo = saln.pack_csr(qsl)
+    dcat, do = saln.pack_csr(dsl)
+    plan = saln.NwPlan(qo, do, pairs=np.stack([np.arange(m)] * 2, 1))
+    r = torch.zeros(m * 4, dtype=torch.int32, device="cuda")
+    c = torch.zeros(max(1, plan.cigar_words), dtype=torch.int32, device="cuda")
+    plan.execute(torch.from_numpy(qcat).cuda(), torch.from_numpy(dcat).cuda(), r, c)
+    plan.check()
+    torch.cuda.synchronize()
+    for k in range(m):
+        lq, ld = len(qsl[k]), len(dsl[k])
+        got = plan.walk_codes(k)
+        dm = oracle.nw(qsl[k], dsl[k], literal_dfs=False).dense_mask  # present bits
+        inner = dm[1:, 1:]
+        want_i = (inner & 2) == 0
+        want_d = (inner & 4) == 0
+        assert np.array_equal((got & 1) != 0, want_i), (k, "argI")
+        assert np.array_equal((got & 2) != 0, want_d), (k, "argD")
+        # I-open of I(i, j+1) at (i, j): columns 1 .. lq-1
+        assert np.array_equal((got[:, :-1] & 4) != 0, (dm[1:, 2:] & 0x10) == 0), (k, "I-open")
+        # D-open of D(i+1, j) at (i, j): rows 1 .. ld-1
+        assert np.array_equal((got[:-1, :] & 8) != 0, (dm[2:, 1:] & 0x40) == 0), (k, "D-open")
+        assert bool(got[ld - 1, lq - 1] & 8) == ((dm[ld, lq] & 1) == 0), (k, "argM")
+    plan.close()
