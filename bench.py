@@ -768,7 +768,7 @@ def leg_c4_sharded(world, rank, local, dist, torch, reps=3, band_rows=1024, engi
                         f"per rank (ShardedLongPair: {band_rows}-row bands over "
                         f"{'RCCL' if sp.nccl else 'the host relay'}, right-to-left walk, CIGAR "
                         f"on rank 0)",
-            "value": round(cells / (med / 1e3) / 1e9, 2), "unit": "GCUPS",
+            "value": round(cells / (med / 1e3) / 1e9, 5), "unit": "GCUPS",
             "ms": round(med, 3), "ms_max": round(float(wall_max.item()) * 1e3, 3),
             "n_ranks": world, "reps": reps, "per_rank": per,
             "result": {"score": int(res.score), "status": int(res.status),

@@ -24,6 +24,7 @@
 #include <thread>
 #include <vector>
 
+#include <sys/stat.h>
 #include <sys/uio.h>
 #include <unistd.h>
 
@@ -303,6 +304,18 @@ int main(int argc, char **argv) {
                      "saln: -a a-star (the reference's A* aligner) is not part of this engine; "
                      "use -a needleman-wunsch or -a wfa\n");
         return 2;
+    }
+    // The reference's default NW output (every block) runs the host DFS over
+    // parent codes downloaded per chunk: the context faults their host buffer
+    // in while the HIP runtime starts (host.prefault_mb), sized from the files
+    // (~1.3 B of codes per cell, a chunk of at most 2^31 cells; 512 MB at most)
+    if (a.algo == 1 && a.max_blocks != 1) {
+        struct stat sq{}, sd{};
+        if (::stat(a.query.c_str(), &sq) == 0 && ::stat(a.db.c_str(), &sd) == 0) {
+            const double cells = std::min((double)sq.st_size * (double)sd.st_size, double(1u << 31));
+            const int64_t mb = std::min<int64_t>(512, (int64_t)(cells * 1.3 / (1 << 20)) + 1);
+            if (mb >= 16) saln_option_set("host.prefault_mb", mb);
+        }
     }
     // the HIP runtime starts (~0.2 s) while the FASTA files are read
     saln_context *ctx = nullptr;

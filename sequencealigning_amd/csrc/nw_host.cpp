@@ -14,8 +14,11 @@
 #include <map>
 #include <numeric>
 #include <string>
+#include <thread>
 #include <unordered_set>
 #include <vector>
+
+#include <sys/mman.h>
 
 #include "nw_host.hpp"
 
@@ -133,6 +136,28 @@ int saln_abi_version(void) { return SALN_ABI_VERSION; }
 int saln_context_create(int device, saln_context **out) {
     if (!out) return SALN_E_INVALID;
     *out = nullptr;
+    // host.prefault_mb: the host buffer of render batches' parent codes,
+    // allocated and faulted in on a helper thread while the HIP runtime
+    // starts (~0.2 s; the CLI's first full chunk otherwise faults ~0.4 GB in
+    // during its mask download: 56 ms, round 6)
+    saln_context::HostBuf pre;
+    std::thread pre_th;
+    if (const int64_t mb = opt(Opt::HostPrefaultMb); mb > 0) {
+        pre_th = std::thread([&pre, mb] {
+            constexpr size_t kHuge = size_t(2) << 20;
+            const size_t want = (((size_t)mb << 20) + kHuge - 1) / kHuge * kHuge;
+            void *hp = nullptr;
+            if (posix_memalign(&hp, kHuge, want) != 0 || !hp) return;
+            (void)madvise(hp, want, MADV_HUGEPAGE);
+            std::memset(hp, 0, want);
+            pre.p = (uint8_t *)hp;
+            pre.n = want;
+        });
+    }
+    struct Join {
+        std::thread &t;
+        ~Join() { if (t.joinable()) t.join(); }
+    } join_pre{pre_th};
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess || n <= device || device < 0) {
         set_error("no HIP device " + std::to_string(device) + " (saln has no CPU path)");
@@ -152,6 +177,11 @@ int saln_context_create(int device, saln_context **out) {
         delete c;
         set_error("hipStreamCreate failed");
         return SALN_E_HIP;
+    }
+    if (pre_th.joinable()) {
+        pre_th.join();
+        std::swap(c->host_mask.p, pre.p);
+        std::swap(c->host_mask.n, pre.n);
     }
     *out = c;
     return SALN_OK;

@@ -34,6 +34,7 @@ enum class Opt : int {
     Wfa2W1,             // "wfa2.w1": first-pass ring width (0 auto)
     Wfa2W2,             // "wfa2.w2": second-pass ring width (0 auto)
     HostTiming,         // "host.timing": stage times of the host paths on stderr
+    HostPrefaultMb,     // "host.prefault_mb": host buffer a new context faults in while HIP starts
     Count
 };
 constexpr int kNumOpts = (int)Opt::Count;
