@@ -46,6 +46,7 @@ struct Args {
     uint64_t chunk_pairs = 1u << 14;  // pairs per render batch (the first one: a quarter)
     bool stage_times = false;
     bool teardown = false;
+    std::vector<std::pair<std::string, int64_t>> options;  // --option NAME=VALUE, in order
 };
 
 const char *kUsage =
@@ -68,6 +69,7 @@ const char *kUsage =
     "      --chunk-pairs <N>          pairs per GPU batch [default: 16384]\n"
     "      --stage-times              stage times of this run on stderr\n"
     "      --teardown                 the HIP runtime's full tear-down at exit (for profilers)\n"
+    "      --option <NAME=VALUE>      set an engine option (saln_option_set; repeatable)\n"
     "  -h, --help                     Print help\n";
 
 [[noreturn]] void usage_error(const std::string &msg) {
@@ -129,6 +131,14 @@ Args parse_args(int argc, char **argv) {
             a.teardown = true;
         } else if (is("--max-blocks", "--max-blocks")) {
             a.max_blocks = std::strtoull(need("--max-blocks <N>").c_str(), nullptr, 10);
+        } else if (is("--option", "--option")) {
+            val = need("--option <NAME=VALUE>");
+            const size_t eq = val.find('=');
+            char *end = nullptr;
+            const long long v = eq == std::string::npos ? 0 : std::strtoll(val.c_str() + eq + 1, &end, 10);
+            if (eq == std::string::npos || eq == 0 || end == val.c_str() + eq + 1 || *end != '\0')
+                usage_error("invalid value '" + val + "' for '--option <NAME=VALUE>'");
+            a.options.emplace_back(val.substr(0, eq), (int64_t)v);
         } else if (is("--chunk-pairs", "--chunk-pairs")) {
             a.chunk_pairs = std::max<uint64_t>(1, std::strtoull(need("--chunk-pairs <N>").c_str(), nullptr, 10));
         } else {
@@ -315,6 +325,15 @@ int main(int argc, char **argv) {
             const double cells = std::min((double)sq.st_size * (double)sd.st_size, double(1u << 31));
             const int64_t mb = std::min<int64_t>(512, (int64_t)(cells * 1.3 / (1 << 20)) + 1);
             if (mb >= 16) saln_option_set("host.prefault_mb", mb);
+        }
+    }
+    // the first copy and launch's set-up beside the context's stream creation
+    saln_option_set("host.warmup", 1);
+    for (const auto &o : a.options) {
+        if (saln_option_set(o.first.c_str(), o.second) != SALN_OK) {
+            std::fprintf(stderr, "saln: --option %s=%lld: %s\n", o.first.c_str(), (long long)o.second,
+                         saln_last_error());
+            return 2;
         }
     }
     // the HIP runtime starts (~0.2 s) while the FASTA files are read

@@ -34,6 +34,24 @@ def test_unknown_and_missing_arguments_exit_2():
     assert r.returncode == 2 and "invalid value 'sideways'" in r.stderr
 
 
+def test_option_flag_is_checked_before_any_work(tmp_path):
+    """--option NAME=VALUE goes to saln_option_set before the context exists:
+    a malformed pair is a usage error, an unknown name or an out-of-range
+    value stops the run with exit 2 (no GPU needed for either)."""
+    fa = tmp_path / "a.fa"
+    fa.write_text(">a\nACGT\n")
+    base = ("-q", str(fa), "-d", str(fa), "-a", "needleman-wunsch")
+    r = _run(*base, "--option", "host.warmup")
+    assert r.returncode == 2 and "invalid value 'host.warmup'" in r.stderr
+    r = _run(*base, "--option=host.warmup=x")
+    assert r.returncode == 2 and "invalid value" in r.stderr
+    r = _run(*base, "--option", "nw.no_such_knob=1")
+    assert r.returncode == 2 and "--option nw.no_such_knob=1" in r.stderr
+    r = _run(*base, "--option", "nw.pk_tab=9")
+    assert r.returncode == 2 and "--option nw.pk_tab=9" in r.stderr
+    assert "--option <NAME=VALUE>" in _run("--help").stdout
+
+
 def test_unreadable_fasta_is_reported_and_returns(tmp_path):
     good = tmp_path / "d.fa"
     good.write_text(">d\nACGT\n")
