@@ -119,7 +119,7 @@ int saln_abi_version(void);
  * "nw.wide_min_pairs", "nw.rows_k", "nw.stripe_pk", "nw.spec",
  * "nw.spec_passes", "nw.spec_strict", "nw.avsa_narrow", "nw.rows_lone",
  * "nw.rows_xcd", "nw.avsa_profile", "nw.pk_tab", "nw.walk_waves",
- * "wfa2.seq_lds", "wfa2.w1", "wfa2.w2", "host.timing", "host.prefault_mb", "host.warmup".
+ * "wfa2.seq_lds", "wfa2.w1", "wfa2.w2", "host.timing", "host.prefault_mb".
  * Two levels, no other shared state:
  *  - saln_option_*: the process registry, the default of every context;
  *  - saln_context_option_*: overrides of one context (its own thread's

@@ -327,8 +327,6 @@ int main(int argc, char **argv) {
             if (mb >= 16) saln_option_set("host.prefault_mb", mb);
         }
     }
-    // the first copy and launch's set-up beside the context's stream creation
-    saln_option_set("host.warmup", 1);
     for (const auto &o : a.options) {
         if (saln_option_set(o.first.c_str(), o.second) != SALN_OK) {
             std::fprintf(stderr, "saln: --option %s=%lld: %s\n", o.first.c_str(), (long long)o.second,

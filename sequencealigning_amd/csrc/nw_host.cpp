@@ -172,43 +172,12 @@ int saln_context_create(int device, saln_context **out) {
     HIP_TRY(hipSetDevice(device));
     auto *c = new saln_context;
     c->device = device;
-    // host.warmup: a process's first pinned allocation, first copy and first
-    // launch of the NW code object cost ~30 ms together (the staging buffer
-    // pinned, the copy path set up, the code object loaded); a helper thread
-    // takes them while the streams are created. Its buffers stay in the
-    // context (the pinned staging, the device block cache).
-    std::thread warm_th;
-    if (opt(Opt::HostWarmup)) {
-        warm_th = std::thread([c, device] {
-            if (hipSetDevice(device) != hipSuccess) return;
-            void *st = nullptr, *d = nullptr;
-            {
-                std::lock_guard<std::mutex> lk(c->staging_mu);
-                if (pinned_staging(c, size_t(4) << 20, &st) != hipSuccess) return;
-                std::memset(st, 'A', 4096);
-            }
-            if (dev_alloc(c, &d, 4096) != hipSuccess) return;
-            // the null stream: the plans' synchronous descriptor copies use it
-            if (hipMemcpy(d, st, 4096, hipMemcpyHostToDevice) == hipSuccess &&
-                launch_acgt_check((const uint8_t *)d, 64, (uint32_t *)((uint8_t *)d + 2048),
-                                  nullptr) == hipSuccess)
-                (void)hipStreamSynchronize(nullptr);
-            (void)hipGetLastError();
-            dev_free(c, d);
-        });
-    }
-    struct JoinW {
-        std::thread &t;
-        ~JoinW() { if (t.joinable()) t.join(); }
-    } join_warm{warm_th};
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&c->tb_stream, hipStreamNonBlocking) != hipSuccess) {
-        if (warm_th.joinable()) warm_th.join();
         delete c;
         set_error("hipStreamCreate failed");
         return SALN_E_HIP;
     }
-    if (warm_th.joinable()) warm_th.join();
     if (pre_th.joinable()) {
         pre_th.join();
         std::swap(c->host_mask.p, pre.p);

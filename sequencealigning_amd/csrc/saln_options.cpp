@@ -30,7 +30,6 @@ const OptDesc kDesc[kNumOpts] = {
     {"wfa2.w2", 0, 0, 4096},
     {"host.timing", 0, 0, 1},
     {"host.prefault_mb", 0, 0, 1 << 16},
-    {"host.warmup", 0, 0, 1},
 };
 struct Values {
     std::atomic<int64_t> v[kNumOpts];

@@ -35,7 +35,6 @@ enum class Opt : int {
     Wfa2W2,             // "wfa2.w2": second-pass ring width (0 auto)
     HostTiming,         // "host.timing": stage times of the host paths on stderr
     HostPrefaultMb,     // "host.prefault_mb": host buffer a new context faults in while HIP starts
-    HostWarmup,         // "host.warmup": a new context takes the first copy / launch costs while its streams are made
     Count
 };
 constexpr int kNumOpts = (int)Opt::Count;

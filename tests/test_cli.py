@@ -41,9 +41,9 @@ def test_option_flag_is_checked_before_any_work(tmp_path):
     fa = tmp_path / "a.fa"
     fa.write_text(">a\nACGT\n")
     base = ("-q", str(fa), "-d", str(fa), "-a", "needleman-wunsch")
-    r = _run(*base, "--option", "host.warmup")
-    assert r.returncode == 2 and "invalid value 'host.warmup'" in r.stderr
-    r = _run(*base, "--option=host.warmup=x")
+    r = _run(*base, "--option", "host.prefault_mb")
+    assert r.returncode == 2 and "invalid value 'host.prefault_mb'" in r.stderr
+    r = _run(*base, "--option=host.prefault_mb=x")
     assert r.returncode == 2 and "invalid value" in r.stderr
     r = _run(*base, "--option", "nw.no_such_knob=1")
     assert r.returncode == 2 and "--option nw.no_such_knob=1" in r.stderr
