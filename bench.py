@@ -1388,7 +1388,14 @@ def main() -> None:
             out["cpu_baseline"] = cpu_baseline()
         print(json.dumps(out), flush=True)
     if world > 1:
+        # the line is out: a teardown stuck behind a peer that left a leg
+        # early (c4_sharded's error path) must not hold the job
+        import threading
+        t = threading.Timer(60.0, lambda: (sys.stderr.flush(), os._exit(0)))
+        t.daemon = True
+        t.start()
         dist.destroy_process_group()
+        t.cancel()
 
 
 if __name__ == "__main__":
