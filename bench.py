@@ -511,25 +511,25 @@ def leg_c2_full(torch, saln, n=N_PAIRS, steps=10, warmup=2):
     """configs[1] as SURVEY 8(d) defines it: 10^5 G-iid 150x150 pairs, fill +
     the reference's full parent sets stored (1 B/cell, the 7 parent bits of
     needleman_wunsch_affine.rs:96-153 that the all-blocks DFS :281-329 reads;
-    saln_nw_plan_create_full) + the first printed traceback / CIGAR, pipelined
-    like the headline (the headline stores 4-bit walk codes instead)."""
+    saln_nw_plan_create_full) + the first printed traceback / CIGAR (the
+    headline stores 4-bit walk codes instead).  Sequential steps, fill then
+    walk: beside the next fill the full-code walk (a lane per pair) costs the
+    fill more than it overlaps (round 6, profiles/r06_full_tab_ab.jsonl:
+    1.353-1.356 ms per step sequential, 1.367-1.376 pipelined)."""
     from sequencealigning_amd import synth
     qs, qo, ds, do = synth.iid_pairs(n, LQ, LD, seed=SEED)
     plan = saln.NwPlan(qo, do, pairs=np.stack([np.arange(n), np.arange(n)], 1), full_codes=True)
     dq, dd = torch.from_numpy(qs).cuda(), torch.from_numpy(ds).cuda()
-    plan.set_async(True)
     res = [torch.zeros(n * 4, dtype=torch.int32, device="cuda") for _ in range(2)]
     cig = [torch.zeros(max(1, plan.cigar_words), dtype=torch.int32, device="cuda")
            for _ in range(2)]
     for k in range(warmup):
         plan.execute(dq, dd, res[k % 2], cig[k % 2])
-    plan.sync()
     torch.cuda.synchronize()
     plan.set_timing(True)
     t0 = time.perf_counter()
     for k in range(steps):
         plan.execute(dq, dd, res[k % 2], cig[k % 2])
-    plan.sync()
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / steps
     plan.check()
@@ -539,13 +539,7 @@ def leg_c2_full(torch, saln, n=N_PAIRS, steps=10, warmup=2):
     hr = res[last].cpu().numpy()
     verified = verify_c2(hr, cig[last].cpu().numpy().view(np.uint32), plan.cigar_off, qs, qo, ds,
                          do)
-    plan.set_async(False)
-    plan.set_timing(True)
-    for _ in range(5):
-        plan.execute(dq, dd, res[0], cig[0])
-    torch.cuda.synchronize()
-    plan.check()
-    fa_ms, fa_n = plan.kernel_time("nw_fill")
+    fa_ms, fa_n = fill_ms, fill_n  # every fill of a sequential plan runs alone
     # the dense parent sets of one pair of the timed plan, against the oracle (untimed)
     from oracle import refcpu  # checker only
     mask_ok = all(np.array_equal(plan.dense_mask(k), refcpu.nw(
@@ -554,12 +548,14 @@ def leg_c2_full(torch, saln, n=N_PAIRS, steps=10, warmup=2):
     cells = plan.cells
     plan.close()
     fill_s, alone_s = fill_ms / max(1, fill_n) / 1e3, fa_ms / max(1, fa_n) / 1e3
-    kern = "nw_fill_pk_kernel<16, 10, 1, PlanSrc, 10, false>"
+    # the table fill with row profiles (round 6; nw.pk_tab), else the generic one
+    kern = pmc_name("nw_fill_pk_tab_kernel<16, 10, saln::PlanSrc, 3, 1>",
+                    "nw_fill_pk_kernel<16, 10, 1, saln::PlanSrc, 10, false>")
     return {"workload": "configs[1] as SURVEY 8(d) defines it: 10^5 independent 150x150 G-iid "
                         "pairs, fill + full 1 B/cell parent sets (7 bits: argmax {M,I,D}, I and "
-                        "D extend/open) + first-printed traceback/CIGAR, pipelined",
+                        "D extend/open) + first-printed traceback/CIGAR, sequential steps",
             "value": round(cells / dt / 1e9, 2), "unit": "GCUPS", "ms_per_step": round(dt * 1e3, 4),
-            "steps": steps, "cells": cells, "executes": warmup + steps + 5,
+            "steps": steps, "cells": cells, "executes": warmup + steps, "pipelined": False,
             "roofline": roof_hbm(cells, fill_s, kern, pmc(kern),
                                  kernel_avg_ms_alone=round(alone_s * 1e3, 4),
                                  frac_alone=round(cells / alone_s / 1e9 / HBM_PEAK_GBS, 4),

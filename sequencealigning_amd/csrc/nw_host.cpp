@@ -51,8 +51,8 @@ bool scores_fit_i32(const Scoring &s, uint64_t lq, uint64_t ld) {
 
 using namespace saln;
 
-
-
+// a plan's table-fill bail words per mask workspace: one per fill variant
+constexpr size_t kBailBytes = kNumVariants * sizeof(uint32_t);
 
 struct saln_nw_plan {
     saln_context *ctx = nullptr;
@@ -603,10 +603,12 @@ int saln::plan_create(saln_context *ctx, const uint64_t *q_off, uint64_t n_q,
     p->ops_words = ooff;
     if (ooff && (e = dev_alloc(p->ctx, (void **)&p->d_ops, ooff * sizeof(uint32_t))) != hipSuccess)
         return fail(e, "hipMalloc(op stream)");
-    if ((p->var_count[kNarrowVariant] && p->nib[kNarrowVariant]) || (p->var_count[7] && p->nib[7])) {
-        if ((e = dev_alloc(p->ctx, (void **)&p->d_bail[0], 16)) != hipSuccess ||
-            (e = hipMemset(p->d_bail[0], 0, 16)) != hipSuccess)
-            return fail(e, "table fill bail word");
+    // table fills (4-bit codes; full codes in 16-lane groups): a bail word per variant
+    if ((p->var_count[kNarrowVariant] && p->nib[kNarrowVariant]) || (p->var_count[7] && p->nib[7]) ||
+        (p->full_codes && (p->var_count[5] || p->var_count[7]))) {
+        if ((e = dev_alloc(p->ctx, (void **)&p->d_bail[0], kBailBytes)) != hipSuccess ||
+            (e = hipMemset(p->d_bail[0], 0, kBailBytes)) != hipSuccess)
+            return fail(e, "table fill bail words");
     }
     {
         // Speculative stripe walks: a few long column-stripe pairs walk all
@@ -765,9 +767,9 @@ int saln_nw_execute(saln_nw_plan *p, const uint8_t *d_q, const uint8_t *d_db,
             continue;
         }
         fx.epoch = ++p->epoch;
-        // one bail word per 4-bit-code variant: two table fills queued before
-        // either deferred fallback runs must not overwrite each other's epoch
-        fx.bail = p->d_bail[cur] ? p->d_bail[cur] + (v == 7 ? 1 : 0) : nullptr;
+        // one bail word per variant: two table fills queued before either
+        // deferred fallback runs must not overwrite each other's epoch
+        fx.bail = p->d_bail[cur] ? p->d_bail[cur] + v : nullptr;
         HIP_TRY(launch_fill(v, p->d_pairs, a, b - a, d_q, d_db, mask, p->d_scratch, endh,
                             d_results, d_cigar, p->sc,
                             p->score_only ? 2 : p->full_codes ? 1 : p->nib[v] ? 3 : 0,
@@ -839,8 +841,8 @@ int saln_nw_plan_set_async(saln_nw_plan *p, int enable) {
         if (p->ops_words)
             HIP_TRY(dev_alloc(p->ctx, (void **)&p->d_ops2, p->ops_words * sizeof(uint32_t)));
         if (p->d_bail[0]) {
-            HIP_TRY(dev_alloc(p->ctx, (void **)&p->d_bail[1], 16));
-            HIP_TRY(hipMemset(p->d_bail[1], 0, 16));
+            HIP_TRY(dev_alloc(p->ctx, (void **)&p->d_bail[1], kBailBytes));
+            HIP_TRY(hipMemset(p->d_bail[1], 0, kBailBytes));
         }
     }
     p->async_tb = enable != 0;

@@ -49,8 +49,9 @@ __device__ __forceinline__ int32_t shr1(int32_t old, int32_t v) {
 // i % 8).  The bpp workgroups that fill one pack (64 consecutive pairs whose
 // mask rows are interleaved) are remapped onto one XCD, so the partial lines
 // they write meet in one L2.  The grid is a multiple of 8*bpp.
-__device__ __forceinline__ uint32_t pack_block(uint32_t bpp) {
-    const uint32_t i = blockIdx.x, sup = 8u * bpp;
+// (i: the block index, blockIdx.x unless a grid-stride loop runs virtual blocks)
+__device__ __forceinline__ uint32_t pack_block(uint32_t bpp, uint32_t i = blockIdx.x) {
+    const uint32_t sup = 8u * bpp;
     const uint32_t r = i % sup;
     return i - r + (r % 8u) * bpp + r / 8u;
 }
@@ -1632,7 +1633,8 @@ template <int G, int K, int kCodes, typename Src, int KS, bool kRebase = false, 
 __device__ __forceinline__ int fill_pk_body(Src src, uint32_t count, const uint8_t *__restrict__ qs,
                                             const uint8_t *__restrict__ ds,
                                             uint8_t *__restrict__ mask, Scoring sc,
-                                            uint32_t ld_max, bool sc_steady) {
+                                            uint32_t ld_max, bool sc_steady,
+                                            uint32_t vblock = ~0u) {
     // table body (kTabMode 1; 4: the same at scale 4, below); kTabMode 2: the
     // generic body of its bail-outs
     constexpr bool kTab = kTabMode == 1 || kTabMode == 4 || kTabMode == 5;
@@ -1673,13 +1675,16 @@ __device__ __forceinline__ int fill_pk_body(Src src, uint32_t count, const uint8
         return ((uint32_t)(lo + kBias) & 0xFFFFu) | ((uint32_t)(hi + kBias) << 16);
     };
     static_assert(!kProf || (kCodes == kCodesNone && !kRebase), "profiles: score-only, one frame");
-    static_assert(!kTab || ((kCodes == kCodesNib || kCodes == kCodesNone) && !kRebase && !kProf),
-                  "tables: 4-bit codes or score-only, one frame");
+    static_assert(!kTab || ((kCodes == kCodesNib || kCodes == kCodesNone || kCodes == kCodesFull) &&
+                            !kRebase && !kProf && !(kS4 && kCodes == kCodesFull)),
+                  "tables: 4-bit codes, full codes (scale 2) or score-only, one frame");
     constexpr int GPB = 256 / G;
     constexpr Geom geo{G, K};
     extern __shared__ uint32_t drow[];  // [GPB][G + ld_max + G] packed db chars (dch) per row
     const int lane = threadIdx.x % G;
-    const uint32_t gi = pack_block(blocks_per_pack(2 * GPB)) * GPB + threadIdx.x / G;
+    // (vblock: the block of a grid-stride launch, nw_fill_pk_tabfb_kernel)
+    const uint32_t gi = pack_block(blocks_per_pack(2 * GPB), vblock == ~0u ? blockIdx.x : vblock) * GPB +
+                        threadIdx.x / G;
     const uint32_t ia = 2 * gi, ib = 2 * gi + 1;
     if (ia >= count) return 0;  // whole group
     const bool hasB = ib < count;
@@ -1704,6 +1709,7 @@ __device__ __forceinline__ int fill_pk_body(Src src, uint32_t count, const uint8
     const uint32_t cmm = (uint32_t)(kSc * sc.mismatch + alpha + beta) & 0xFFu;
     const uint32_t kBonus = cm | cmm * 0x01010100u;
     const uint32_t kProfBase = cmm * 0x01010101u, kProfStep = cm - cmm;  // kRowProf
+    const uint32_t kCmm2 = cmm * 0x00010001u;  // full codes' eq sign in the free frame
     constexpr uint32_t kAcgt = 'A' | 'C' << 8 | 'T' << 16 | 'G' << 24;
     auto acgt = [](uint32_t c) { return c == 'A' || c == 'C' || c == 'G' || c == 'T'; };
     bool bad = false;  // kTabMode: a byte other than A, C, G, T in this lane's share
@@ -1976,7 +1982,9 @@ __device__ __forceinline__ int fill_pk_body(Src src, uint32_t count, const uint8
                 // sign <=> q == d (bit 7): pen is 0 or pen_max >= 2 in both
                 // halves (the low half's borrow moves the high half from
                 // pen_max - 1 to pen_max - 2 or from -1 to -2)
-                sg[7] = pen - 0x00010001u;
+                // (the extension-free frame's bonus: cm on a match, cmm < cm
+                // otherwise, so cmm - bonus is negative exactly on a match)
+                sg[7] = kFree ? psub(kCmm2, pen) : pen - 0x00010001u;
                 if constexpr (kCodes == kCodesFull) {
                     const uint32_t tOc = tO & 0xFFFEFFFEu;
                     sg[3] = psub(I, tOc);
@@ -2135,27 +2143,35 @@ __global__ __launch_bounds__(256, (pk_min_waves<G, K, kCodes>())) void nw_fill_p
 // launches of one workspace run in stream order); the fallback launch runs
 // only when that word holds its epoch.  Two kernels, not one with both
 // bodies: together they spill.
-template <int G, int K, typename Src, int kScale = 2>
-__global__ __launch_bounds__(256, (pk_min_waves<G, K, kCodesNib>())) void nw_fill_pk_tab_kernel(
+// kCodes: kCodesNib, or kCodesFull (round 6: every parent set, row profiles only)
+template <int G, int K, typename Src, int kScale = 2, int kCodes = kCodesNib>
+__global__ __launch_bounds__(256, (pk_min_waves<G, K, kCodes>())) void nw_fill_pk_tab_kernel(
     Src src, uint32_t count, const uint8_t *__restrict__ qs, const uint8_t *__restrict__ ds,
     uint8_t *__restrict__ mask, Scoring sc, uint32_t ld_max, uint32_t *__restrict__ bail,
     uint32_t epoch) {
     // kScale: 2 or 4 (the value scale); 3: scale 2 with row profiles (kTabMode 5)
-    const int st = fill_pk_body<G, K, kCodesNib, Src, K, false, false,
+    const int st = fill_pk_body<G, K, kCodes, Src, K, false, false,
                                 kScale == 4 ? 4 : kScale == 3 ? 5 : 1>(src, count, qs, ds, mask,
                                                                        sc, ld_max, true);
     if (__builtin_amdgcn_ballot_w64(st == 1) && (threadIdx.x & 63u) == 0) *bail = epoch;
 }
 // (kRebaseGeneric: the fallback of a launch whose dbs need the rebasing frame;
 // the extension-free table body has no drift and needs none)
-template <int G, int K, typename Src, bool kRebaseGeneric>
-__global__ __launch_bounds__(256, (pk_min_waves<G, K, kCodesNib>())) void nw_fill_pk_tabfb_kernel(
+// A grid-stride launch over the table launch's `vblocks` blocks (64
+// workgroups instead of one per block: the launch behind every table fill
+// mostly finds its word unset, and its workgroups' dispatch was its time - a
+// full grid of waves that only read the word took 42 us per C2 step, 512
+// workgroups 27 us; round 6).
+constexpr uint32_t kTabFbBlocks = 64;
+template <int G, int K, typename Src, bool kRebaseGeneric, int kCodes = kCodesNib>
+__global__ __launch_bounds__(256, (pk_min_waves<G, K, kCodes>())) void nw_fill_pk_tabfb_kernel(
     Src src, uint32_t count, const uint8_t *__restrict__ qs, const uint8_t *__restrict__ ds,
     uint8_t *__restrict__ mask, Scoring sc, uint32_t ld_max, const uint32_t *__restrict__ bail,
-    uint32_t epoch) {
+    uint32_t epoch, uint32_t vblocks) {
     if (__builtin_amdgcn_readfirstlane(*bail) != epoch) return;
-    fill_pk_body<G, K, kCodesNib, Src, K, kRebaseGeneric, false, 2>(src, count, qs, ds, mask, sc,
-                                                                     ld_max, true);
+    for (uint32_t vb = blockIdx.x; vb < vblocks; vb += gridDim.x)
+        fill_pk_body<G, K, kCodes, Src, K, kRebaseGeneric, false, 2>(src, count, qs, ds, mask, sc,
+                                                                      ld_max, true, vb);
 }
 
 // Score-only all-vs-all of the other query classes with table penalties in
@@ -3313,8 +3329,33 @@ static hipError_t fill_pk(dim3 grid, hipStream_t s, const NwPairDesc *pairs, uin
                     nw_fill_pk_tab_kernel<G, K, PlanSrc, 2><<<grid, dim3(256), lds_k, s>>>(
                         src, count, qs, ds, mask, sc, ld_max, fx.bail, fx.epoch);
                 auto fb = [=, bail = fx.bail, epoch = fx.epoch](hipStream_t fs) {
-                    nw_fill_pk_tabfb_kernel<G, K, PlanSrc, kRb><<<grid, dim3(256), lds_tab, fs>>>(
-                        src, count, qs, ds, mask, sc, ld_max, bail, epoch);
+                    nw_fill_pk_tabfb_kernel<G, K, PlanSrc, kRb>
+                        <<<dim3(std::min(grid.x, kTabFbBlocks)), dim3(256), lds_tab, fs>>>(
+                            src, count, qs, ds, mask, sc, ld_max, bail, epoch, grid.x);
+                    return hipGetLastError();
+                };
+                if (fx.deferred) fx.deferred->push_back(fb);
+                else return fb(s);
+                return hipSuccess;
+            }
+        }
+        // full parent sets (round 6): the table body with row profiles for the
+        // 16-lane geometries (queries of up to 256 columns), nw.pk_tab != 0
+        if constexpr (decltype(codes_c)::value == kCodesFull && KS == K && G == 16) {
+            const size_t lds_tab = (size_t)(256 / G) * (ld_max + 2 * G) * 4;
+            if (o[Opt::PkTab] && fx.bail && pk_free_ok(sc, G * K, ld_max) &&
+                lds_tab <= std::max(lds, kLdsPerCu / 4)) {
+                constexpr bool kRb = decltype(rebase_c)::value;
+                const void *tk = (const void *)nw_fill_pk_tab_kernel<G, K, PlanSrc, 3, kCodesFull>;
+                const void *fk = (const void *)nw_fill_pk_tabfb_kernel<G, K, PlanSrc, kRb, kCodesFull>;
+                hipError_t e = big_lds({tk, fk}, lds_tab);
+                if (e != hipSuccess) return e;
+                nw_fill_pk_tab_kernel<G, K, PlanSrc, 3, kCodesFull><<<grid, dim3(256), lds_tab, s>>>(
+                    src, count, qs, ds, mask, sc, ld_max, fx.bail, fx.epoch);
+                auto fb = [=, bail = fx.bail, epoch = fx.epoch](hipStream_t fs) {
+                    nw_fill_pk_tabfb_kernel<G, K, PlanSrc, kRb, kCodesFull>
+                        <<<dim3(std::min(grid.x, kTabFbBlocks)), dim3(256), lds_tab, fs>>>(
+                            src, count, qs, ds, mask, sc, ld_max, bail, epoch, grid.x);
                     return hipGetLastError();
                 };
                 if (fx.deferred) fx.deferred->push_back(fb);
@@ -3611,6 +3652,10 @@ hipError_t launch_traceback(int variant, const NwPairDesc *pairs, uint32_t first
         case 5: tb_lds<16, 16>(stream, pairs, first, n, mask, end_h, ops, results, cigar, sc, qs); break;
         case 6: tb_lds<32, 16>(stream, pairs, first, n, mask, end_h, ops, results, cigar, sc, qs); break;
         case 7:
+            // (a lane per pair: two per lane made both 16 x 10 walks slower
+            // beside the next fill - the 4-bit one in round 5, the full-code
+            // one 1.367-1.384 -> 1.429-1.433 ms per step in round 6,
+            // profiles/r06_full_walk_ab.jsonl)
             if (nib) tb_lds<16, 10, true>(stream, pairs, first, n, mask, end_h, ops, results, cigar, sc, qs);
             else tb_lds<16, 10>(stream, pairs, first, n, mask, end_h, ops, results, cigar, sc, qs);
             break;

@@ -1037,6 +1037,75 @@ def test_full_code_plan_c2(saln, oracle, async_):
     plan.close()
 
 
+def test_full_code_table_fill_equals_generic(saln, oracle):
+    """Round 6: full-code plans fill their 16-lane geometries (16 x 10 for
+    queries of <= 160 columns, 16 x 16 for <= 256) with the table body and row
+    profiles (nw.pk_tab != 0).  One async plan holds both variants; every
+    other step puts N bytes into pairs of both, so both table launches bail
+    and both fallbacks run behind them (a bail word per variant).  Every
+    parent set of every pair equals the generic fill's (nw.pk_tab = 0) and, on
+    a sample, the oracle's; results and CIGARs equal the synchronous generic
+    plan's at every step."""
+    import torch
+    from sequencealigning_amd import synth
+    n = 601
+    lq = np.array([[150, 230, 157, 256, 1, 160][k % 6] for k in range(n)], np.int64)
+    ld = np.array([[150, 300, 97, 150, 12, 1][k % 6] for k in range(n)], np.int64)
+    qo = np.concatenate([[0], np.cumsum(lq)]).astype(np.uint64)
+    do = np.concatenate([[0], np.cumsum(ld)]).astype(np.uint64)
+    qs0 = synth.random_bases(0x5EED0061, int(qo[-1]))
+    ds0 = synth.random_bases(0x5EED0062, int(do[-1]))
+    pairs = np.stack([np.arange(n)] * 2, 1)
+    with saln.options(**{"nw.pk_tab": 0}):
+        gen = saln.NwPlan(qo, do, pairs=pairs, full_codes=True)
+    tab = saln.NwPlan(qo, do, pairs=pairs, full_codes=True)
+    tab.set_async(True)
+    rng = np.random.default_rng(61)
+    steps = 4
+    ins, want, got = [], [], []
+    for s_ in range(steps):
+        qs, ds = qs0.copy(), ds0.copy()
+        if s_ % 2 == 0:
+            qs[rng.random(qs.size) < 0.003] = ord("N")
+            ds[rng.random(ds.size) < 0.003] = ord("N")
+        else:
+            ds = np.roll(ds, s_)
+        dq, dd = torch.from_numpy(qs).cuda(), torch.from_numpy(ds).cuda()
+        r = torch.zeros(n * 4, dtype=torch.int32, device="cuda")
+        c = torch.zeros(max(1, gen.cigar_words), dtype=torch.int32, device="cuda")
+        gen.execute(dq, dd, r, c)
+        ins.append((dq, dd, qs, ds))
+        want.append((r, c))
+    for s_ in range(steps):
+        r = torch.full((n * 4,), -1, dtype=torch.int32, device="cuda")
+        c = torch.zeros(max(1, tab.cigar_words), dtype=torch.int32, device="cuda")
+        tab.execute(ins[s_][0], ins[s_][1], r, c)
+        got.append((r, c))
+    tab.sync()
+    tab.check()
+    gen.check()
+    torch.cuda.synchronize()
+    for s_ in range(steps):
+        assert torch.equal(got[s_][0], want[s_][0]), s_
+        assert torch.equal(got[s_][1], want[s_][1]), s_
+    # the last step's workspace: every parent set, table vs generic, and the
+    # oracle's on a sample (N bytes included: step 2 bailed in both variants)
+    last = steps - 2
+    gen.execute(ins[last][0], ins[last][1], *want[last])
+    tab.set_async(False)
+    tab.execute(ins[last][0], ins[last][1], *got[last])
+    torch.cuda.synchronize()
+    qs, ds = ins[last][2], ins[last][3]
+    for k in range(n):
+        m = tab.dense_mask(k)
+        assert np.array_equal(m, gen.dense_mask(k)), k
+        if k % 37 == 0:
+            q, d = qs[qo[k]:qo[k + 1]].tobytes(), ds[do[k]:do[k + 1]].tobytes()
+            assert np.array_equal(m, oracle.nw(q, d, literal_dfs=False).dense_mask), k
+    gen.close()
+    tab.close()
+
+
 @pytest.mark.parametrize("tab", [0, 1, 2, 3])
 def test_walk_codes_bit_by_bit(saln, oracle, saln_opt, tab):
     """the 4-bit walk codes of the short-query fills

@@ -27,6 +27,8 @@ def main():
                     help="the bench's default loop: step k's walk beside step k+1's fill")
     ap.add_argument("--no-timing", action="store_true",
                     help="no per-execute hipEvents (wall time only)")
+    ap.add_argument("--full", action="store_true",
+                    help="full parent sets (saln_nw_plan_create_full, the c2_full leg's plan)")
     ap.add_argument("--opt", action="append", default=[],
                     help="engine option name=value (saln_option_set), repeatable")
     a = ap.parse_args()
@@ -38,7 +40,7 @@ def main():
         _lib.set_option(k, int(v))
     n, L = a.pairs, a.len
     qs, qo, ds, do = synth.iid_pairs(n, L, L, seed=0x5EED0002)
-    plan = saln.NwPlan(qo, do, pairs=np.stack([np.arange(n)] * 2, 1))
+    plan = saln.NwPlan(qo, do, pairs=np.stack([np.arange(n)] * 2, 1), full_codes=a.full)
     dq, dd = torch.from_numpy(qs).cuda(), torch.from_numpy(ds).cuda()
     nb = 2 if a.pipeline else 1
     plan.set_async(a.pipeline)
@@ -62,7 +64,7 @@ def main():
     tb, tn = plan.kernel_time("nw_traceback") if not a.no_timing else (0.0, 1)
     print(json.dumps({"tag": a.tag, "lib": os.path.basename(_lib.LIB_PATH), "opts": a.opt,
                       "timing": not a.no_timing,
-                      "pipeline": a.pipeline,
+                      "pipeline": a.pipeline, "full": a.full,
                       "gcups": round(plan.cells / dt / 1e9, 1), "ms_per_step": round(dt * 1e3, 4),
                       "fill_ms": round(f / fn, 4), "traceback_ms": round(tb / tn, 4)}))
 

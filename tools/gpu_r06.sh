@@ -4,6 +4,7 @@
 #            REPS alternations of tools/bench_long.py (walk codes and score-only)
 #   abwalk   C2 step with this tree's walker vs sequencealigning_amd/libsaln_prev.so
 #            (an earlier commit's build), sequential and pipelined, REPS alternations
+#   abfull   c2_full step (full parent sets): table fill vs generic fill, REPS alternations
 #   abtab    C2 step, table fill variants TABS (nw.pk_tab: 1 scale 2, 2 scale 4, 3 row profiles), REPS alternations
 #   c2full   the c2_full leg alone (full 1 B/cell parent sets)
 #   smoke    __graft_entry__.smoke()
@@ -64,6 +65,16 @@ for st in ${STAGES:-smoke tests bench}; do
           for pl in "" "--pipeline"; do
             tag=tab${t}${pl:+_pipe}_$i
             step $tag 180 python tools/ab_c2.py --tag $tag $pl --opt nw.pk_tab=$t
+            tail -1 $O/$tag.log
+          done
+        done
+      done ;;
+    abfull)  # full-code plans: table fill (nw.pk_tab=3) vs the generic fill (0), REPS alternations
+      for i in ${REPS:-1 2}; do
+        for t in 0 3; do
+          for pl in "" "--pipeline"; do
+            tag=full${t}${pl:+_pipe}_$i
+            step $tag 180 python tools/ab_c2.py --full --tag $tag $pl --opt nw.pk_tab=$t
             tail -1 $O/$tag.log
           done
         done
