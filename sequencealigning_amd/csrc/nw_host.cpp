@@ -677,6 +677,15 @@ int saln_nw_plan_set_timing(saln_nw_plan *p, int enable) {
     }
     p->timing = enable != 0;
     p->ktime.clear();
+    // the event sets of the next executes, created now rather than inside
+    // them (a timed C2 step that created its four events ran 0.5 % slower,
+    // round 6, profiles/r06_timing_events_ab.jsonl); more are made on demand
+    constexpr size_t kEventSets = 64;
+    while (p->timing && p->ev_pool.size() < kEventSets) {
+        std::array<hipEvent_t, 4> e4{};
+        for (auto &e : e4) HIP_TRY(hipEventCreate(&e));
+        p->ev_pool.push_back(e4);
+    }
     return SALN_OK;
 }
 
