@@ -28,7 +28,7 @@ enum class Opt : int {
     RowsLone,           // "nw.rows_lone": a row fill that fits the SIMDs gets one stripe per SIMD
     RowsXcd,            // "nw.rows_xcd": XCD-local neighbours for row fills whose stripes fit the SIMDs
     AvsaProfile,        // "nw.avsa_profile": query-profile penalties in the 8 x 19 all-vs-all fill
-    PkTab,              // "nw.pk_tab": table penalties + extension-free frame in the 4-bit-code fills (1: scale 2, 2: scale 4 where it fits, 3: scale 2 with row profiles, the default)
+    PkTab,              // "nw.pk_tab": table penalties + extension-free frame in the 4-bit-code fills (1: scale 2, 2: scale 4 where it fits, 3: scale 2 with row profiles, the default); != 0: the full-code 16-lane fills' row-profile body
     WalkWaves,          // "nw.walk_waves": waves of an LDS walk launch (-1 auto, 0 a lane per pair)
     Wfa2SeqLds,         // "wfa2.seq_lds": LDS bytes for staged sequences (corrected WFA)
     Wfa2W1,             // "wfa2.w1": first-pass ring width (0 auto)
