@@ -718,15 +718,23 @@ __global__ __launch_bounds__(256) void nw_traceback_lds_kernel(
     constexpr uint32_t kWave = WalkGeo<K, kNib, G * K>::kWaveLds;
     __shared__ __attribute__((aligned(16))) uint8_t win_all[tb_lds_threads<G, K, kNib>() / 64u * kWave];
     // The walk is a latency-bound chain that shares SIMDs with the VALU-bound
-    // fill of the next batch in pipelined plans: it issues at the highest
-    // priority (round 4: 3 / 1 / 0 gave 0.94 / 0.94 / 0.96 ms per step).
+    // fill of the next batch in pipelined plans.  Issue priority against the
+    // table fills (priority 2): above them for a lane's first pair, below
+    // them for the next ones (a grid that walks two pairs per lane beside the
+    // next fill).  Above throughout, the walk took 0.63 ms and the co-run fill
+    // 0.84; below throughout, the walk outlasted the fill (0.83 against 0.74);
+    // first above, then below: fill 0.82, walk 0.79, C2 step 0.861-0.865 ->
+    // 0.844-0.852 ms (round 6, profiles/r06_prio_ab.jsonl, five calls).
     __builtin_amdgcn_s_setprio(3);
     lds_u8 *win = (lds_u8 *)(win_all + (threadIdx.x / 64u) * kWave);
     // a lane per pair; a grid smaller than the pairs walks them in turns (the
     // wave's lanes start their next pairs together, after the last of the
     // previous ones has finished)
     const uint32_t stride = gridDim.x * blockDim.x;
+    bool later = false;
     for (uint32_t rel = blockIdx.x * blockDim.x + threadIdx.x; rel < n; rel += stride) {
+        if (later) __builtin_amdgcn_s_setprio(1);
+        later = true;
         const uint32_t idx = first + rel;
         const NwPairDesc p = pairs[idx];
         walk_pack_lds<G, K, kNib>(p, end_h[idx], mask, ops, results, cigar, sc, win, qs);
@@ -2150,6 +2158,9 @@ __global__ __launch_bounds__(256, (pk_min_waves<G, K, kCodes>())) void nw_fill_p
     uint8_t *__restrict__ mask, Scoring sc, uint32_t ld_max, uint32_t *__restrict__ bail,
     uint32_t epoch) {
     // kScale: 2 or 4 (the value scale); 3: scale 2 with row profiles (kTabMode 5)
+    // (issue priority 2: between a pipelined walk's first pairs and its
+    // later ones, nw_traceback_lds_kernel)
+    __builtin_amdgcn_s_setprio(2);
     const int st = fill_pk_body<G, K, kCodes, Src, K, false, false,
                                 kScale == 4 ? 4 : kScale == 3 ? 5 : 1>(src, count, qs, ds, mask,
                                                                        sc, ld_max, true);
